@@ -1,0 +1,168 @@
+#!/usr/bin/env python3
+"""Headline benchmark: ResNet-50 DDP training throughput (images/sec, whole node) on MI355X.
+
+BASELINE.json metric: "images/sec (whole node) ResNet-50 DDP at 1/2/4/8 MI355X". The reference
+publishes no number, so ``vs_baseline`` is null.
+
+  python bench.py --gpus N --steps K --warmup W            # N=1: plain process
+  torchrun --nproc-per-node N ... bench.py --gpus N ...    # N>1: one rank per GPU (RCCL)
+
+Each step is a full training step on synthetic 224x224 ImageNet-shaped batches with
+random-init ResNet-50 weights: forward, loss, backward, bucketed RCCL all-reduce
+overlapped with backward, fused SGD update. W warm-up steps are untimed; exactly K steps
+are timed between barrier + device synchronize on both sides; the reported time is the MAX
+over ranks; ``value`` is total images/sec over all N GPUs (weak scaling: per-GPU batch fixed).
+
+--impl ours       : this framework (DDP reducer, HIP BN/CE/SGD kernels, bf16 + fp32 master, hipGraph)
+--impl torch_ddp  : stock torch.nn.parallel.DistributedDataParallel + autocast bf16 + torch SGD (B0)
+--impl reference  : the reference algorithm — per-parameter all-reduce after backward (B1)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from pytorch_distributed_training_example_amd.parallel import launcher  # noqa: E402
+
+METRIC = "images/sec (whole node) ResNet-50 DDP"
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--model", default="resnet50")
+    ap.add_argument("--batch-size", type=int, default=256, help="per-GPU batch")
+    ap.add_argument("--image-size", type=int, default=224)
+    ap.add_argument("--impl", default="ours", choices=["ours", "torch_ddp", "reference"])
+    ap.add_argument("--graph", type=int, default=1, help="hipGraph-capture the step (ours)")
+    ap.add_argument("--bucket-cap-mb", type=float, default=25.0)
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "amp_bf16", "fp32"])
+    ap.add_argument("--lr", type=float, default=0.1)
+    ap.add_argument("--json-out", default=None)
+    return ap.parse_args(argv)
+
+
+def build(args, ctx):
+    from pytorch_distributed_training_example_amd.models import get_model
+    from pytorch_distributed_training_example_amd.models.precision import apply_precision
+    dev = ctx.device
+    torch.manual_seed(1234)
+    model = get_model(args.model).to(dev).to(memory_format=torch.channels_last)
+    precision = args.precision
+    if args.impl != "ours" and precision == "bf16":
+        precision = "amp_bf16"  # stock path: fp32 params + autocast (what torch users run)
+    model = apply_precision(model, precision)
+    world = ctx.world_size
+    if args.impl == "ours":
+        from pytorch_distributed_training_example_amd.optim import FusedSGD
+        from pytorch_distributed_training_example_amd.parallel import DistributedDataParallel
+        ddp = DistributedDataParallel(model, bucket_cap_mb=args.bucket_cap_mb, broadcast_buffers=False,
+                                      gradient_as_bucket_view=True)
+        opt = FusedSGD(model.parameters(), lr=args.lr, momentum=0.9, weight_decay=5e-5, nesterov=False)
+    elif args.impl == "torch_ddp":
+        ddp = torch.nn.parallel.DistributedDataParallel(model, device_ids=[dev.index], bucket_cap_mb=args.bucket_cap_mb,
+                                                        broadcast_buffers=False, gradient_as_bucket_view=True) \
+            if world > 1 else model
+        opt = torch.optim.SGD(model.parameters(), lr=args.lr, momentum=0.9, weight_decay=5e-5)
+    else:
+        ddp = model
+        opt = torch.optim.SGD(model.parameters(), lr=args.lr, momentum=0.9, weight_decay=5e-5)
+    return model, ddp, opt, precision
+
+
+def main(argv=None):
+    args = parse(argv)
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    ctx = launcher.init_distributed(backend="nccl" if torch.cuda.is_available() else "gloo")
+    dev = ctx.device
+    world = ctx.world_size
+    torch.backends.cudnn.benchmark = True
+    model, ddp, opt, precision = build(args, ctx)
+    from pytorch_distributed_training_example_amd.ops.cross_entropy import cross_entropy
+    from pytorch_distributed_training_example_amd.parallel.reference import average_gradients
+
+    B, S = args.batch_size, args.image_size
+    in_dtype = torch.bfloat16 if precision == "bf16" else torch.float32
+    g = torch.Generator(device=dev).manual_seed(100 + ctx.rank)
+    pool = [torch.randn(B, 3, S, S, device=dev, generator=g).to(in_dtype).contiguous(memory_format=torch.channels_last)
+            for _ in range(2)]
+    tpool = [torch.randint(0, 1000, (B,), device=dev, generator=g) for _ in range(2)]
+    autocast = precision == "amp_bf16"
+
+    def step(x, y):
+        if args.impl == "ours":
+            for buf in ddp.grad_buffers():
+                buf.zero_()
+        else:
+            opt.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=autocast):
+            out = ddp(x)
+        if args.impl == "ours":
+            loss = cross_entropy(out, y, label_smoothing=0.1)
+        else:
+            loss = torch.nn.functional.cross_entropy(out.float(), y, label_smoothing=0.1)
+        loss.backward()
+        if args.impl == "reference" and world > 1:
+            average_gradients(model)
+        opt.step()
+        return loss.detach()
+
+    runner = None
+    if args.impl == "ours" and args.graph:
+        from pytorch_distributed_training_example_amd.engine.graph import StaticStep
+        runner = StaticStep(step, [pool[0], tpool[0]], warmup=max(3, min(args.warmup, 5)))
+
+    def run(i):
+        x, y = pool[i % 2], tpool[i % 2]
+        return runner(x, y) if runner is not None else step(x, y)
+
+    for i in range(args.warmup):
+        loss = run(i)
+    torch.cuda.synchronize()
+    launcher.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        loss = run(i)
+    torch.cuda.synchronize()
+    launcher.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms = elapsed / args.steps * 1e3
+    value = B * world * args.steps / elapsed
+    result = {
+        "metric": METRIC, "value": round(value, 2), "unit": "images/sec", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "bf16" if precision != "fp32" else "fp32",
+        "data": "synthetic (random 224x224 images, random labels, random-init weights)",
+        "config": {"model": args.model, "global_batch": B * world, "per_gpu_batch": B, "seq_len": None,
+                   "image_size": S, "parallelism": f"dp{world}", "impl": args.impl,
+                   "graph": bool(runner is not None), "precision": precision,
+                   "bucket_cap_mb": args.bucket_cap_mb, "final_loss": round(float(loss.float().item()), 4)},
+    }
+    if ctx.rank == 0:
+        print(json.dumps(result), flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                json.dump(result, f)
+    launcher.destroy()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,433 @@
+// Python binding for the gfx950 kernels (pybind11 over at::Tensor).
+//
+// Thin by design: validates devices / dtypes / layouts, collects raw pointers, and calls the
+// C-ABI launchers in kernels/*.hip on the current HIP stream (so the calls are ordered with
+// PyTorch's own kernels and can be captured into a hipGraph). Every kernel lives in its own
+// .hip translation unit; this file is the only one that includes the PyTorch headers.
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+
+#include <vector>
+
+extern "C" {
+int pdt_sgd(int n, void* const* p, void* const* g, void* const* buf, void* const* copy, const int64_t* numel,
+            int p_dtype, int g_dtype, float lr, const float* lr_ptr, float momentum, float dampening, float wd,
+            int nesterov, int first, int maximize, const float* inv_scale, const float* found_inf, hipStream_t s);
+int pdt_adam(int n, void* const* p, void* const* g, void* const* m, void* const* v, void* const* copy,
+             const int64_t* numel, int p_dtype, int g_dtype, float lr, const float* lr_ptr, float beta1, float beta2,
+             float eps, float wd, int decoupled, const float* step_ptr, float step_host, int maximize,
+             const float* inv_scale, const float* found_inf, hipStream_t s);
+int pdt_adadelta(int n, void* const* p, void* const* g, void* const* sa, void* const* ad, void* const* copy,
+                 const int64_t* numel, int p_dtype, int g_dtype, float lr, const float* lr_ptr, float rho, float eps,
+                 float wd, int maximize, const float* inv_scale, const float* found_inf, hipStream_t s);
+int pdt_amp_unscale(int n, void* const* g, const int64_t* numel, int dtype, const float* inv_scale, float* found_inf,
+                    hipStream_t s);
+int pdt_amp_update(float* scale, int* growth_tracker, const float* found_inf, float growth, float backoff,
+                   int interval, hipStream_t s);
+int pdt_mt_scale(int n, void* const* x, const int64_t* numel, int dtype, const float* scale_ptr, float scale,
+                 hipStream_t s);
+int pdt_mt_copy(int n, void* const* src, void* const* dst, const int64_t* numel, int sdt, int ddt,
+                const float* scale_ptr, float scale, hipStream_t s);
+int pdt_l2norm_sq(int n, void* const* x, const int64_t* numel, int dtype, float* out, hipStream_t s);
+int pdt_clip_coef(const float* sumsq, float max_norm, float* coef, float* norm, hipStream_t s);
+int64_t pdt_bn_workspace_floats(int64_t M, int C);
+int pdt_bn_fwd_train(const uint16_t* x, const uint16_t* res, const float* gamma, const float* beta,
+                     float* running_mean, float* running_var, float momentum, float eps, int64_t M, int C, int relu,
+                     uint16_t* y, float* mean, float* invstd, float* ws, hipStream_t s);
+int pdt_bn_fwd_eval(const uint16_t* x, const uint16_t* res, const float* gamma, const float* beta,
+                    const float* running_mean, const float* running_var, float eps, int64_t M, int C, int relu,
+                    uint16_t* y, float* ws, hipStream_t s);
+int pdt_bn_bwd_train(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* gamma, const float* mean,
+                     const float* invstd, int64_t M, int C, int relu, int has_res, uint16_t* dx, uint16_t* dres,
+                     float* dgamma, float* dbeta, float* ws, hipStream_t s);
+int pdt_ce_fwd(const void* logits, int dtype, const int64_t* target, int64_t N, int64_t V, float smoothing,
+               int64_t ignore_index, float* loss, float* lse, hipStream_t s);
+int pdt_ce_bwd(const void* logits, int dtype, const int64_t* target, const float* lse, const float* dloss,
+               float dloss_scale, int64_t N, int64_t V, float smoothing, int64_t ignore_index, void* dlogits,
+               hipStream_t s);
+int64_t pdt_ln_workspace_floats(int64_t N, int D);
+int pdt_ln_fwd(const void* x, int dtype, const float* w, const float* b, void* y, float* mean, float* rstd, int64_t N,
+               int D, float eps, hipStream_t s);
+int pdt_ln_bwd(const void* dy, const void* x, int dtype, const float* w, const float* mean, const float* rstd,
+               void* dx, float* dw, float* db, int64_t N, int D, float* ws, hipStream_t s);
+int64_t pdt_gelu_workspace_floats(int64_t N, int D);
+int pdt_bias_gelu_fwd(const void* x, int dtype, const float* bias, void* y, int64_t N, int D, int tanh_form,
+                      hipStream_t s);
+int pdt_bias_gelu_bwd(const void* dy, const void* x, int dtype, const float* bias, void* dx, float* dbias,
+                      int64_t N, int D, int tanh_form, float* ws, hipStream_t s);
+}
+
+namespace {
+
+using at::Tensor;
+
+hipStream_t stream() { return at::hip::getCurrentHIPStream().stream(); }
+
+int dcode(const Tensor& t) {
+  if (t.scalar_type() == at::kFloat) return 0;
+  if (t.scalar_type() == at::kBFloat16) return 1;
+  TORCH_CHECK(false, "pdt: unsupported dtype ", t.scalar_type(), " (fp32 / bf16 only)");
+}
+
+void check_cuda(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), "pdt: ", name, " must be a GPU tensor");
+}
+
+bool dense(const Tensor& t) { return t.is_contiguous() || t.is_non_overlapping_and_dense(); }
+
+const float* opt_fptr(const c10::optional<Tensor>& t) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  TORCH_CHECK(t->scalar_type() == at::kFloat, "pdt: scalar tensors must be fp32");
+  return t->data_ptr<float>();
+}
+
+struct Lists {
+  std::vector<void*> ptrs;
+  static Lists from(const std::vector<Tensor>& ts, const char* name, int expect_dtype, size_t n) {
+    Lists l;
+    if (ts.empty()) {
+      l.ptrs.assign(n, nullptr);
+      return l;
+    }
+    TORCH_CHECK(ts.size() == n, "pdt: list ", name, " has ", ts.size(), " tensors, expected ", n);
+    for (const auto& t : ts) {
+      check_cuda(t, name);
+      TORCH_CHECK(dense(t), "pdt: ", name, " tensors must be dense");
+      if (expect_dtype >= 0) TORCH_CHECK(dcode(t) == expect_dtype, "pdt: ", name, " dtype mismatch");
+      l.ptrs.push_back(t.data_ptr());
+    }
+    return l;
+  }
+};
+
+std::vector<int64_t> numels(const std::vector<Tensor>& ts) {
+  std::vector<int64_t> n;
+  n.reserve(ts.size());
+  for (const auto& t : ts) n.push_back(t.numel());
+  return n;
+}
+
+void check_same_numel(const std::vector<Tensor>& a, const std::vector<Tensor>& b, const char* name) {
+  if (b.empty()) return;
+  for (size_t i = 0; i < a.size(); ++i)
+    TORCH_CHECK(a[i].numel() == b[i].numel() && (a[i].strides() == b[i].strides() || a[i].is_contiguous() ==
+                b[i].is_contiguous()), "pdt: ", name, "[", i, "] shape/layout mismatch");
+}
+
+int uniform_dtype(const std::vector<Tensor>& ts) {
+  TORCH_CHECK(!ts.empty(), "pdt: empty tensor list");
+  const int d = dcode(ts[0]);
+  for (const auto& t : ts) TORCH_CHECK(dcode(t) == d, "pdt: mixed dtypes in one tensor list");
+  return d;
+}
+
+// ----------------------------------------------------------------------------- optimizers
+void sgd(std::vector<Tensor> params, std::vector<Tensor> grads, std::vector<Tensor> bufs,
+         std::vector<Tensor> copies, double lr, c10::optional<Tensor> lr_t, double momentum, double dampening,
+         double wd, bool nesterov, bool first, bool maximize, c10::optional<Tensor> inv_scale,
+         c10::optional<Tensor> found_inf) {
+  if (params.empty()) return;
+  const size_t n = params.size();
+  const int pd = uniform_dtype(params), gd = uniform_dtype(grads);
+  check_same_numel(params, grads, "grads");
+  check_same_numel(params, bufs, "momentum_buffer");
+  check_same_numel(params, copies, "model_copy");
+  auto P = Lists::from(params, "params", pd, n), G = Lists::from(grads, "grads", gd, n),
+       B = Lists::from(bufs, "momentum_buffer", 0, n), C = Lists::from(copies, "model_copy", 1, n);
+  auto ne = numels(params);
+  int rc = pdt_sgd((int)n, P.ptrs.data(), G.ptrs.data(), B.ptrs.data(), C.ptrs.data(), ne.data(), pd, gd, (float)lr,
+                   opt_fptr(lr_t), (float)momentum, (float)dampening, (float)wd, nesterov, first, maximize,
+                   opt_fptr(inv_scale), opt_fptr(found_inf), stream());
+  TORCH_CHECK(rc == 0, "pdt_sgd failed");
+}
+
+void adam(std::vector<Tensor> params, std::vector<Tensor> grads, std::vector<Tensor> exp_avg,
+          std::vector<Tensor> exp_avg_sq, std::vector<Tensor> copies, double lr, c10::optional<Tensor> lr_t,
+          double beta1, double beta2, double eps, double wd, bool decoupled, c10::optional<Tensor> step_t,
+          double step, bool maximize, c10::optional<Tensor> inv_scale, c10::optional<Tensor> found_inf) {
+  if (params.empty()) return;
+  const size_t n = params.size();
+  const int pd = uniform_dtype(params), gd = uniform_dtype(grads);
+  check_same_numel(params, grads, "grads");
+  check_same_numel(params, exp_avg, "exp_avg");
+  check_same_numel(params, exp_avg_sq, "exp_avg_sq");
+  check_same_numel(params, copies, "model_copy");
+  TORCH_CHECK(!exp_avg.empty() && !exp_avg_sq.empty(), "pdt_adam: states required");
+  auto P = Lists::from(params, "params", pd, n), G = Lists::from(grads, "grads", gd, n),
+       M = Lists::from(exp_avg, "exp_avg", 0, n), V = Lists::from(exp_avg_sq, "exp_avg_sq", 0, n),
+       C = Lists::from(copies, "model_copy", 1, n);
+  auto ne = numels(params);
+  int rc = pdt_adam((int)n, P.ptrs.data(), G.ptrs.data(), M.ptrs.data(), V.ptrs.data(), C.ptrs.data(), ne.data(), pd,
+                    gd, (float)lr, opt_fptr(lr_t), (float)beta1, (float)beta2, (float)eps, (float)wd, decoupled,
+                    opt_fptr(step_t), (float)step, maximize, opt_fptr(inv_scale), opt_fptr(found_inf), stream());
+  TORCH_CHECK(rc == 0, "pdt_adam failed");
+}
+
+void adadelta(std::vector<Tensor> params, std::vector<Tensor> grads, std::vector<Tensor> square_avg,
+              std::vector<Tensor> acc_delta, std::vector<Tensor> copies, double lr, c10::optional<Tensor> lr_t,
+              double rho, double eps, double wd, bool maximize, c10::optional<Tensor> inv_scale,
+              c10::optional<Tensor> found_inf) {
+  if (params.empty()) return;
+  const size_t n = params.size();
+  const int pd = uniform_dtype(params), gd = uniform_dtype(grads);
+  check_same_numel(params, grads, "grads");
+  check_same_numel(params, square_avg, "square_avg");
+  check_same_numel(params, acc_delta, "acc_delta");
+  check_same_numel(params, copies, "model_copy");
+  auto P = Lists::from(params, "params", pd, n), G = Lists::from(grads, "grads", gd, n),
+       S = Lists::from(square_avg, "square_avg", 0, n), A = Lists::from(acc_delta, "acc_delta", 0, n),
+       C = Lists::from(copies, "model_copy", 1, n);
+  auto ne = numels(params);
+  int rc = pdt_adadelta((int)n, P.ptrs.data(), G.ptrs.data(), S.ptrs.data(), A.ptrs.data(), C.ptrs.data(), ne.data(),
+                        pd, gd, (float)lr, opt_fptr(lr_t), (float)rho, (float)eps, (float)wd, maximize,
+                        opt_fptr(inv_scale), opt_fptr(found_inf), stream());
+  TORCH_CHECK(rc == 0, "pdt_adadelta failed");
+}
+
+// ----------------------------------------------------------------------------- amp / buffers
+void amp_unscale(std::vector<Tensor> grads, Tensor inv_scale, Tensor found_inf) {
+  if (grads.empty()) return;
+  const int d = uniform_dtype(grads);
+  auto G = Lists::from(grads, "grads", d, grads.size());
+  auto ne = numels(grads);
+  TORCH_CHECK(pdt_amp_unscale((int)grads.size(), G.ptrs.data(), ne.data(), d, inv_scale.data_ptr<float>(),
+                              found_inf.data_ptr<float>(), stream()) == 0, "pdt_amp_unscale failed");
+}
+
+void amp_update(Tensor scale, Tensor growth_tracker, Tensor found_inf, double growth, double backoff, int64_t interval) {
+  TORCH_CHECK(growth_tracker.scalar_type() == at::kInt, "growth_tracker must be int32");
+  pdt_amp_update(scale.data_ptr<float>(), growth_tracker.data_ptr<int>(), found_inf.data_ptr<float>(), (float)growth,
+                 (float)backoff, (int)interval, stream());
+}
+
+void mt_scale(std::vector<Tensor> xs, c10::optional<Tensor> scale_t, double scale) {
+  if (xs.empty()) return;
+  const int d = uniform_dtype(xs);
+  auto X = Lists::from(xs, "x", d, xs.size());
+  auto ne = numels(xs);
+  TORCH_CHECK(pdt_mt_scale((int)xs.size(), X.ptrs.data(), ne.data(), d, opt_fptr(scale_t), (float)scale, stream()) == 0,
+              "pdt_mt_scale failed");
+}
+
+void mt_copy(std::vector<Tensor> src, std::vector<Tensor> dst, c10::optional<Tensor> scale_t, double scale) {
+  if (src.empty()) return;
+  TORCH_CHECK(src.size() == dst.size(), "mt_copy: list size mismatch");
+  check_same_numel(src, dst, "dst");
+  const int sd = uniform_dtype(src), dd = uniform_dtype(dst);
+  auto S = Lists::from(src, "src", sd, src.size()), D = Lists::from(dst, "dst", dd, dst.size());
+  auto ne = numels(src);
+  TORCH_CHECK(pdt_mt_copy((int)src.size(), S.ptrs.data(), D.ptrs.data(), ne.data(), sd, dd, opt_fptr(scale_t),
+                          (float)scale, stream()) == 0, "pdt_mt_copy failed");
+}
+
+void l2norm_sq(std::vector<Tensor> xs, Tensor out) {
+  TORCH_CHECK(out.scalar_type() == at::kFloat && out.numel() >= 1, "l2norm_sq: out must be fp32");
+  if (xs.empty()) {
+    out.zero_();
+    return;
+  }
+  const int d = uniform_dtype(xs);
+  auto X = Lists::from(xs, "x", d, xs.size());
+  auto ne = numels(xs);
+  pdt_l2norm_sq((int)xs.size(), X.ptrs.data(), ne.data(), d, out.data_ptr<float>(), stream());
+}
+
+void clip_coef(Tensor sumsq, double max_norm, Tensor coef, c10::optional<Tensor> norm) {
+  pdt_clip_coef(sumsq.data_ptr<float>(), (float)max_norm, coef.data_ptr<float>(),
+                norm.has_value() ? norm->data_ptr<float>() : nullptr, stream());
+}
+
+// ----------------------------------------------------------------------------- batchnorm (NHWC bf16)
+void check_nhwc_bf16(const Tensor& t, const char* name) {
+  check_cuda(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, "pdt bn: ", name, " must be bf16");
+  if (t.dim() == 4) {
+    TORCH_CHECK(t.is_contiguous(at::MemoryFormat::ChannelsLast), "pdt bn: ", name, " must be channels_last");
+  } else {
+    TORCH_CHECK(t.dim() == 2 && t.is_contiguous(), "pdt bn: ", name, " must be [M, C] contiguous or NHWC");
+  }
+}
+
+int64_t bn_ws_floats(int64_t M, int64_t C) { return pdt_bn_workspace_floats(M, (int)C) + 4 * C; }
+
+std::vector<Tensor> bn_fwd_train(Tensor x, c10::optional<Tensor> res, c10::optional<Tensor> weight,
+                                 c10::optional<Tensor> bias, c10::optional<Tensor> running_mean,
+                                 c10::optional<Tensor> running_var, double momentum, double eps, bool relu) {
+  check_nhwc_bf16(x, "x");
+  const int64_t C = x.size(1);
+  const int64_t M = x.numel() / C;
+  TORCH_CHECK(C % 8 == 0, "pdt bn: C must be a multiple of 8");
+  auto y = at::empty_like(x);
+  auto fopt = x.options().dtype(at::kFloat);
+  auto mean = at::empty({C}, fopt), invstd = at::empty({C}, fopt);
+  auto ws = at::empty({bn_ws_floats(M, C)}, fopt);
+  const uint16_t* rp = nullptr;
+  if (res.has_value() && res->defined()) {
+    check_nhwc_bf16(*res, "residual");
+    TORCH_CHECK(res->sizes() == x.sizes() && res->strides() == x.strides(), "pdt bn: residual layout mismatch");
+    rp = reinterpret_cast<const uint16_t*>(res->data_ptr());
+  }
+  float* rm = running_mean.has_value() && running_mean->defined() ? running_mean->data_ptr<float>() : nullptr;
+  float* rv = running_var.has_value() && running_var->defined() ? running_var->data_ptr<float>() : nullptr;
+  int rc = pdt_bn_fwd_train(reinterpret_cast<const uint16_t*>(x.data_ptr()), rp, opt_fptr(weight), opt_fptr(bias), rm, rv,
+                            (float)momentum, (float)eps, M, (int)C, relu, reinterpret_cast<uint16_t*>(y.data_ptr()),
+                            mean.data_ptr<float>(), invstd.data_ptr<float>(), ws.data_ptr<float>(), stream());
+  TORCH_CHECK(rc == 0, "pdt_bn_fwd_train failed");
+  return {y, mean, invstd};
+}
+
+Tensor bn_fwd_eval(Tensor x, c10::optional<Tensor> res, c10::optional<Tensor> weight, c10::optional<Tensor> bias,
+                   Tensor running_mean, Tensor running_var, double eps, bool relu) {
+  check_nhwc_bf16(x, "x");
+  const int64_t C = x.size(1);
+  const int64_t M = x.numel() / C;
+  auto y = at::empty_like(x);
+  auto ws = at::empty({2 * C}, x.options().dtype(at::kFloat));
+  const uint16_t* rp = (res.has_value() && res->defined()) ? reinterpret_cast<const uint16_t*>(res->data_ptr()) : nullptr;
+  int rc = pdt_bn_fwd_eval(reinterpret_cast<const uint16_t*>(x.data_ptr()), rp, opt_fptr(weight), opt_fptr(bias),
+                           running_mean.data_ptr<float>(), running_var.data_ptr<float>(), (float)eps, M, (int)C, relu,
+                           reinterpret_cast<uint16_t*>(y.data_ptr()), ws.data_ptr<float>(), stream());
+  TORCH_CHECK(rc == 0, "pdt_bn_fwd_eval failed");
+  return y;
+}
+
+std::vector<Tensor> bn_bwd_train(Tensor dy, Tensor x, c10::optional<Tensor> y, c10::optional<Tensor> weight, Tensor mean,
+                                 Tensor invstd, bool relu, bool has_res, bool need_dgamma) {
+  check_nhwc_bf16(x, "x");
+  TORCH_CHECK(dy.sizes() == x.sizes() && dy.strides() == x.strides(), "pdt bn bwd: dy layout mismatch");
+  const int64_t C = x.size(1);
+  const int64_t M = x.numel() / C;
+  auto dx = at::empty_like(x);
+  Tensor dres;
+  if (has_res) dres = at::empty_like(x);
+  auto fopt = x.options().dtype(at::kFloat);
+  Tensor dg, db;
+  if (need_dgamma) {
+    dg = at::empty({C}, fopt);
+    db = at::empty({C}, fopt);
+  }
+  auto ws = at::empty({bn_ws_floats(M, C)}, fopt);
+  const uint16_t* yp = nullptr;
+  if (relu) {
+    TORCH_CHECK(y.has_value() && y->defined(), "pdt bn bwd: relu needs the forward output");
+    yp = reinterpret_cast<const uint16_t*>(y->data_ptr());
+  }
+  int rc = pdt_bn_bwd_train(reinterpret_cast<const uint16_t*>(dy.data_ptr()), reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                            yp, opt_fptr(weight), mean.data_ptr<float>(), invstd.data_ptr<float>(), M, (int)C, relu,
+                            has_res, reinterpret_cast<uint16_t*>(dx.data_ptr()),
+                            has_res ? reinterpret_cast<uint16_t*>(dres.data_ptr()) : nullptr,
+                            need_dgamma ? dg.data_ptr<float>() : nullptr, need_dgamma ? db.data_ptr<float>() : nullptr,
+                            ws.data_ptr<float>(), stream());
+  TORCH_CHECK(rc == 0, "pdt_bn_bwd_train failed");
+  return {dx, dres, dg, db};
+}
+
+// ----------------------------------------------------------------------------- cross entropy
+std::vector<Tensor> ce_fwd(Tensor logits, Tensor target, double smoothing, int64_t ignore_index) {
+  check_cuda(logits, "logits");
+  TORCH_CHECK(logits.dim() == 2 && logits.is_contiguous(), "ce: logits must be contiguous [N, V]");
+  TORCH_CHECK(target.scalar_type() == at::kLong && target.is_contiguous(), "ce: target must be int64");
+  const int64_t N = logits.size(0), V = logits.size(1);
+  auto fopt = logits.options().dtype(at::kFloat);
+  auto loss = at::empty({N}, fopt), lse = at::empty({N}, fopt);
+  pdt_ce_fwd(logits.data_ptr(), dcode(logits), target.data_ptr<int64_t>(), N, V, (float)smoothing, ignore_index,
+             loss.data_ptr<float>(), lse.data_ptr<float>(), stream());
+  return {loss, lse};
+}
+
+Tensor ce_bwd(Tensor logits, Tensor target, Tensor lse, c10::optional<Tensor> dloss, double dloss_scale,
+              double smoothing, int64_t ignore_index) {
+  const int64_t N = logits.size(0), V = logits.size(1);
+  auto dl = at::empty_like(logits);
+  const float* dp = nullptr;
+  Tensor dloss_c;
+  if (dloss.has_value() && dloss->defined()) {
+    dloss_c = dloss->to(at::kFloat).contiguous();
+    if (dloss_c.numel() == 1) dloss_c = dloss_c.expand({N}).contiguous();
+    dp = dloss_c.data_ptr<float>();
+  }
+  pdt_ce_bwd(logits.data_ptr(), dcode(logits), target.data_ptr<int64_t>(), lse.data_ptr<float>(), dp,
+             (float)dloss_scale, N, V, (float)smoothing, ignore_index, dl.data_ptr(), stream());
+  return dl;
+}
+
+// ----------------------------------------------------------------------------- layernorm
+std::vector<Tensor> ln_fwd(Tensor x, Tensor w, Tensor b, double eps) {
+  check_cuda(x, "x");
+  TORCH_CHECK(x.is_contiguous(), "ln: x must be contiguous");
+  const int64_t D = x.size(-1), N = x.numel() / D;
+  TORCH_CHECK(w.scalar_type() == at::kFloat && b.scalar_type() == at::kFloat, "ln: weight/bias must be fp32");
+  auto y = at::empty_like(x);
+  auto fopt = x.options().dtype(at::kFloat);
+  auto mean = at::empty({N}, fopt), rstd = at::empty({N}, fopt);
+  int rc = pdt_ln_fwd(x.data_ptr(), dcode(x), w.data_ptr<float>(), b.data_ptr<float>(), y.data_ptr(),
+                      mean.data_ptr<float>(), rstd.data_ptr<float>(), N, (int)D, (float)eps, stream());
+  TORCH_CHECK(rc == 0, "pdt_ln_fwd: unsupported D=", D);
+  return {y, mean, rstd};
+}
+
+std::vector<Tensor> ln_bwd(Tensor dy, Tensor x, Tensor w, Tensor mean, Tensor rstd) {
+  TORCH_CHECK(dy.is_contiguous() && x.is_contiguous(), "ln bwd: contiguous inputs required");
+  const int64_t D = x.size(-1), N = x.numel() / D;
+  auto dx = at::empty_like(x);
+  auto fopt = x.options().dtype(at::kFloat);
+  auto dw = at::empty({D}, fopt), db = at::empty({D}, fopt);
+  auto ws = at::empty({std::max<int64_t>(pdt_ln_workspace_floats(N, (int)D), 1)}, fopt);
+  int rc = pdt_ln_bwd(dy.data_ptr(), x.data_ptr(), dcode(x), w.data_ptr<float>(), mean.data_ptr<float>(),
+                      rstd.data_ptr<float>(), dx.data_ptr(), dw.data_ptr<float>(), db.data_ptr<float>(), N, (int)D,
+                      ws.data_ptr<float>(), stream());
+  TORCH_CHECK(rc == 0, "pdt_ln_bwd: unsupported D=", D);
+  return {dx, dw, db};
+}
+
+// ----------------------------------------------------------------------------- bias + gelu
+Tensor bias_gelu_fwd(Tensor x, c10::optional<Tensor> bias, bool tanh_form) {
+  TORCH_CHECK(x.is_contiguous(), "gelu: x must be contiguous");
+  const int64_t D = x.size(-1), N = x.numel() / D;
+  auto y = at::empty_like(x);
+  int rc = pdt_bias_gelu_fwd(x.data_ptr(), dcode(x), opt_fptr(bias), y.data_ptr(), N, (int)D, tanh_form, stream());
+  TORCH_CHECK(rc == 0, "pdt_bias_gelu_fwd failed");
+  return y;
+}
+
+std::vector<Tensor> bias_gelu_bwd(Tensor dy, Tensor x, c10::optional<Tensor> bias, bool tanh_form) {
+  TORCH_CHECK(dy.is_contiguous() && x.is_contiguous(), "gelu bwd: contiguous inputs required");
+  const int64_t D = x.size(-1), N = x.numel() / D;
+  auto dx = at::empty_like(x);
+  auto fopt = x.options().dtype(at::kFloat);
+  const bool hb = bias.has_value() && bias->defined();
+  Tensor db, ws;
+  if (hb) {
+    db = at::empty({D}, fopt);
+    ws = at::empty({pdt_gelu_workspace_floats(N, (int)D)}, fopt);
+  }
+  int rc = pdt_bias_gelu_bwd(dy.data_ptr(), x.data_ptr(), dcode(x), opt_fptr(bias), dx.data_ptr(),
+                             hb ? db.data_ptr<float>() : nullptr, N, (int)D, tanh_form,
+                             hb ? ws.data_ptr<float>() : nullptr, stream());
+  TORCH_CHECK(rc == 0, "pdt_bias_gelu_bwd failed");
+  return {dx, db};
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "gfx950 HIP kernels for pytorch_distributed_training_example_amd";
+  m.def("sgd", &sgd);
+  m.def("adam", &adam);
+  m.def("adadelta", &adadelta);
+  m.def("amp_unscale", &amp_unscale);
+  m.def("amp_update", &amp_update);
+  m.def("mt_scale", &mt_scale);
+  m.def("mt_copy", &mt_copy);
+  m.def("l2norm_sq", &l2norm_sq);
+  m.def("clip_coef", &clip_coef);
+  m.def("bn_fwd_train", &bn_fwd_train);
+  m.def("bn_fwd_eval", &bn_fwd_eval);
+  m.def("bn_bwd_train", &bn_bwd_train);
+  m.def("ce_fwd", &ce_fwd);
+  m.def("ce_bwd", &ce_bwd);
+  m.def("ln_fwd", &ln_fwd);
+  m.def("ln_bwd", &ln_bwd);
+  m.def("bias_gelu_fwd", &bias_gelu_fwd);
+  m.def("bias_gelu_bwd", &bias_gelu_bwd);
+}

@@ -1,0 +1,68 @@
+"""hipGraph capture of a whole training step (forward, backward, RCCL bucket all-reduces,
+optimizer) — the MI355X replacement for a tracing compiler.
+
+The reference has no step capture (its loop is plain eager PyTorch, /root/reference/train.py:44-57).
+ResNet-50 at small per-GPU batches and LeNet at any batch are launch-bound: one eager step
+is hundreds of kernel launches plus Python. A captured step replays them with one
+``hipGraphLaunch`` (≈10-16 µs host cost, MI355X_MICROARCH.md graph-replay-floor).
+
+Requirements (checked or arranged here):
+  * static shapes and static input/target buffers (``StaticStep.copy_inputs``);
+  * warm-up iterations on a side stream before capture (allocator pools, RCCL
+    communicator, MIOpen algorithm selection, DDP bucket rebuild, optimizer state);
+  * no host synchronisation inside the step: the DDP reducer waits on RCCL work with
+    stream-ordered waits, the fused optimizers read lr/step/scale from device tensors.
+"""
+from __future__ import annotations
+
+from typing import Callable, Optional, Sequence
+
+import torch
+
+
+class StaticStep:
+    """Capture ``fn(*static_inputs) -> loss`` into a hipGraph and replay it.
+
+    ``fn`` must perform the full step (zero grads, forward, backward, optimizer.step). The
+    returned loss tensor is a static output refreshed by every replay.
+    """
+
+    def __init__(self, fn: Callable[..., torch.Tensor], example_inputs: Sequence[torch.Tensor],
+                 warmup: int = 3, pool=None, enabled: bool = True):
+        self.fn = fn
+        self.enabled = enabled and torch.cuda.is_available()
+        self.static_inputs = [t.clone() for t in example_inputs]
+        self.graph: Optional[torch.cuda.CUDAGraph] = None
+        self.static_loss: Optional[torch.Tensor] = None
+        self._warmup = warmup
+        self._pool = pool
+
+    def capture(self) -> None:
+        if not self.enabled:
+            return
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(self._warmup):
+                self.static_loss = self.fn(*self.static_inputs)
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph, pool=self._pool):
+            self.static_loss = self.fn(*self.static_inputs)
+        torch.cuda.synchronize()
+
+    def copy_inputs(self, *inputs: torch.Tensor) -> None:
+        for dst, src in zip(self.static_inputs, inputs):
+            if src is not None and src.data_ptr() != dst.data_ptr():
+                dst.copy_(src, non_blocking=True)
+
+    def __call__(self, *inputs: torch.Tensor) -> torch.Tensor:
+        if not self.enabled:
+            return self.fn(*(inputs or self.static_inputs))
+        if self.graph is None:
+            self.capture()
+        if inputs:
+            self.copy_inputs(*inputs)
+        self.graph.replay()
+        return self.static_loss

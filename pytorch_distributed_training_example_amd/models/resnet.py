@@ -1,0 +1,138 @@
+"""ResNet (v1.5, torchvision-compatible) for the ResNet-50 north-star config.
+
+Not in the reference (its only model is LeNet, /root/reference/cnn.py); BASELINE.json's headline
+metric is ResNet-50 DDP images/sec. Parameter and buffer names match
+``torchvision.models.resnet50`` exactly (``conv1``, ``bn1``, ``layer{1-4}.{i}.conv{1,2,3}``,
+``bn{1,2,3}``, ``downsample.{0,1}``, ``fc``) so checkpoints interchange; torchvision itself is
+not needed at run time.
+
+MI355X-first layout: the model runs channels_last (NHWC) so every convolution is an
+implicit GEMM with C contiguous (MIOpen / hipBLASLt MFMA kernels) and every BatchNorm is the
+fused NHWC bf16 HIP kernel (ops/batchnorm.py). ReLU is fused into bn1/bn2, and the bottleneck
+tail ``relu(bn3(conv3) + identity)`` is ONE kernel.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Type
+
+import torch
+from torch import nn
+
+from ..ops.batchnorm import BatchNorm2d
+
+
+def conv3x3(inp: int, out: int, stride: int = 1, groups: int = 1, dilation: int = 1) -> nn.Conv2d:
+    return nn.Conv2d(inp, out, 3, stride=stride, padding=dilation, groups=groups, bias=False, dilation=dilation)
+
+
+def conv1x1(inp: int, out: int, stride: int = 1) -> nn.Conv2d:
+    return nn.Conv2d(inp, out, 1, stride=stride, bias=False)
+
+
+class _Downsample(nn.Sequential):
+    """conv1x1 + BN (no ReLU); indices 0/1 as in torchvision."""
+
+
+class BasicBlock(nn.Module):
+    expansion = 1
+
+    def __init__(self, inplanes, planes, stride=1, downsample=None, groups=1, base_width=64, dilation=1):
+        super().__init__()
+        self.conv1 = conv3x3(inplanes, planes, stride)
+        self.bn1 = BatchNorm2d(planes, fused_relu=True)
+        self.relu = nn.ReLU(inplace=True)
+        self.conv2 = conv3x3(planes, planes)
+        self.bn2 = BatchNorm2d(planes)
+        self.downsample = downsample
+        self.stride = stride
+
+    def forward(self, x):
+        identity = x if self.downsample is None else self.downsample(x)
+        out = self.bn1(self.conv1(x))
+        return self.bn2(self.conv2(out), residual=identity, relu=True)
+
+
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, inplanes, planes, stride=1, downsample=None, groups=1, base_width=64, dilation=1):
+        super().__init__()
+        width = int(planes * (base_width / 64.0)) * groups
+        self.conv1 = conv1x1(inplanes, width)
+        self.bn1 = BatchNorm2d(width, fused_relu=True)
+        self.conv2 = conv3x3(width, width, stride, groups, dilation)
+        self.bn2 = BatchNorm2d(width, fused_relu=True)
+        self.conv3 = conv1x1(width, planes * self.expansion)
+        self.bn3 = BatchNorm2d(planes * self.expansion)
+        self.relu = nn.ReLU(inplace=True)
+        self.downsample = downsample
+        self.stride = stride
+
+    def forward(self, x):
+        identity = x if self.downsample is None else self.downsample(x)
+        out = self.bn1(self.conv1(x))
+        out = self.bn2(self.conv2(out))
+        return self.bn3(self.conv3(out), residual=identity, relu=True)
+
+
+class ResNet(nn.Module):
+    def __init__(self, block: Type[nn.Module], layers: List[int], num_classes: int = 1000,
+                 zero_init_residual: bool = False, groups: int = 1, width_per_group: int = 64):
+        super().__init__()
+        self.inplanes = 64
+        self.dilation = 1
+        self.groups = groups
+        self.base_width = width_per_group
+        self.conv1 = nn.Conv2d(3, self.inplanes, kernel_size=7, stride=2, padding=3, bias=False)
+        self.bn1 = BatchNorm2d(self.inplanes, fused_relu=True)
+        self.relu = nn.ReLU(inplace=True)
+        self.maxpool = nn.MaxPool2d(kernel_size=3, stride=2, padding=1)
+        self.layer1 = self._make_layer(block, 64, layers[0])
+        self.layer2 = self._make_layer(block, 128, layers[1], stride=2)
+        self.layer3 = self._make_layer(block, 256, layers[2], stride=2)
+        self.layer4 = self._make_layer(block, 512, layers[3], stride=2)
+        self.avgpool = nn.AdaptiveAvgPool2d((1, 1))
+        self.fc = nn.Linear(512 * block.expansion, num_classes)
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+            elif isinstance(m, nn.BatchNorm2d):
+                nn.init.constant_(m.weight, 1)
+                nn.init.constant_(m.bias, 0)
+        if zero_init_residual:
+            for m in self.modules():
+                if isinstance(m, Bottleneck):
+                    nn.init.constant_(m.bn3.weight, 0)
+                elif isinstance(m, BasicBlock):
+                    nn.init.constant_(m.bn2.weight, 0)
+
+    def _make_layer(self, block, planes, blocks, stride=1):
+        downsample = None
+        if stride != 1 or self.inplanes != planes * block.expansion:
+            downsample = _Downsample(conv1x1(self.inplanes, planes * block.expansion, stride),
+                                     BatchNorm2d(planes * block.expansion))
+        layers = [block(self.inplanes, planes, stride, downsample, self.groups, self.base_width)]
+        self.inplanes = planes * block.expansion
+        for _ in range(1, blocks):
+            layers.append(block(self.inplanes, planes, groups=self.groups, base_width=self.base_width))
+        return nn.Sequential(*layers)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        x = self.bn1(self.conv1(x))
+        x = self.maxpool(x)
+        x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+        x = self.avgpool(x)
+        x = torch.flatten(x, 1)
+        return self.fc(x)
+
+
+def resnet18(**kw) -> ResNet:
+    return ResNet(BasicBlock, [2, 2, 2, 2], **kw)
+
+
+def resnet50(**kw) -> ResNet:
+    return ResNet(Bottleneck, [3, 4, 6, 3], **kw)
+
+
+def resnet101(**kw) -> ResNet:
+    return ResNet(Bottleneck, [3, 4, 23, 3], **kw)

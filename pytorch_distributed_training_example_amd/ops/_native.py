@@ -1,0 +1,55 @@
+"""Loader for the in-tree gfx950 extension (``_C``).
+
+GPU tensors always go through the HIP kernels: if the extension is missing or fails to load,
+GPU calls raise immediately (no silent eager/PyTorch fallback). CPU tensors use the pure
+PyTorch reference implementations in each op module (tests on the CPU-only container).
+Set ``PDT_DISABLE_NATIVE=1`` to force the reference path (A/B benchmarking only).
+"""
+from __future__ import annotations
+
+import importlib
+import os
+
+_mod = None
+_err: Exception | None = None
+
+
+def _load():
+    global _mod, _err
+    if _mod is not None or _err is not None:
+        return _mod
+    try:
+        import torch  # noqa: F401  (libc10 / libtorch must be loaded first)
+        _mod = importlib.import_module("pytorch_distributed_training_example_amd._C")
+    except Exception as e:  # pragma: no cover - depends on build state
+        _err = e
+    return _mod
+
+
+def available() -> bool:
+    return _load() is not None
+
+
+def disabled() -> bool:
+    return os.environ.get("PDT_DISABLE_NATIVE", "0") == "1"
+
+
+def native():
+    """The extension module, or a RuntimeError explaining how to build it."""
+    m = _load()
+    if m is None:
+        raise RuntimeError(
+            "pytorch_distributed_training_example_amd._C (gfx950 HIP kernels) is not built or failed to "
+            f"load: {_err!r}. Build it with `python -m pytorch_distributed_training_example_amd._build`.")
+    return m
+
+
+def use_native(*tensors) -> bool:
+    """True when these tensors must take the HIP path (any on GPU and native not disabled)."""
+    on_gpu = any(t is not None and getattr(t, "is_cuda", False) for t in tensors)
+    if not on_gpu:
+        return False
+    if disabled():
+        return False
+    native()  # raise loudly if missing
+    return True

@@ -1,0 +1,129 @@
+"""BatchNorm2d with fused ReLU and fused residual add, backed by NHWC bf16 HIP kernels.
+
+``BatchNorm2d`` subclasses ``torch.nn.BatchNorm2d`` (same parameters, buffers and state_dict
+keys, so torchvision-style ResNet checkpoints load unchanged) and adds
+``forward(x, residual=None, relu=None)``:
+
+    y = relu?( batchnorm(x) + residual? )
+
+On a channels_last bf16 GPU tensor this is 3 kernels forward (reduce, finalize, apply) and 3
+backward, instead of BN + add + ReLU as separate passes (csrc/kernels/batchnorm.hip). Other
+inputs (CPU, fp32, NCHW) take the PyTorch reference path — identical math, used by the
+CPU tests and as the numerics oracle.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from ._native import native, use_native
+
+
+def bn_reference(x, residual, weight, bias, running_mean, running_var, training, momentum, eps, relu):
+    y = F.batch_norm(x, running_mean, running_var, weight, bias, training, momentum, eps)
+    if residual is not None:
+        y = y + residual
+    if relu:
+        y = F.relu(y)
+    return y
+
+
+class _BNTrainFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, residual, weight, bias, running_mean, running_var, momentum, eps, relu):
+        C = native()
+        y, mean, invstd = C.bn_fwd_train(x, residual, weight, bias, running_mean, running_var,
+                                         momentum, eps, relu)
+        ctx.relu = relu
+        ctx.has_res = residual is not None
+        ctx.has_weight = weight is not None
+        ctx.save_for_backward(x, y if relu else None, weight, mean, invstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, weight, mean, invstd = ctx.saved_tensors
+        fmt = torch.channels_last if x.dim() == 4 else torch.contiguous_format
+        dy = dy.contiguous(memory_format=fmt)
+        need_w = ctx.has_weight and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3])
+        dx, dres, dg, db = native().bn_bwd_train(dy, x, y, weight, mean, invstd, ctx.relu,
+                                                 ctx.has_res, need_w)
+        return (dx, dres if ctx.has_res else None, dg if need_w else None, db if need_w else None,
+                None, None, None, None, None)
+
+
+class _BNEvalFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, residual, weight, bias, running_mean, running_var, eps, relu):
+        y = native().bn_fwd_eval(x, residual, weight, bias, running_mean, running_var, eps, relu)
+        ctx.relu, ctx.has_res, ctx.eps = relu, residual is not None, eps
+        ctx.save_for_backward(y if relu else None, weight, running_var)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        y, weight, rv = ctx.saved_tensors
+        dz = dy * (y > 0) if ctx.relu else dy
+        a = torch.rsqrt(rv + ctx.eps)
+        if weight is not None:
+            a = a * weight
+        dx = (dz.float() * a.view(1, -1, 1, 1) if dz.dim() == 4 else dz.float() * a).to(dz.dtype)
+        return dx, (dz if ctx.has_res else None), None, None, None, None, None, None
+
+
+def batch_norm_act(x, residual, weight, bias, running_mean, running_var, training, momentum, eps, relu):
+    """Functional fused BN(+add)(+ReLU). Native when x is a channels_last bf16 GPU tensor."""
+    nhwc = x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last) or \
+        (x.dim() == 2 and x.is_contiguous())
+    if (use_native(x) and x.dtype == torch.bfloat16 and nhwc and x.shape[1] % 8 == 0
+            and (residual is None or (residual.shape == x.shape and residual.dtype == x.dtype))):
+        if residual is not None:
+            residual = residual.contiguous(memory_format=torch.channels_last if x.dim() == 4
+                                           else torch.contiguous_format)
+        if training:
+            return _BNTrainFn.apply(x, residual, weight, bias, running_mean, running_var,
+                                    float(momentum), float(eps), bool(relu))
+        return _BNEvalFn.apply(x, residual, weight, bias, running_mean, running_var, float(eps), bool(relu))
+    return bn_reference(x, residual, weight, bias, running_mean, running_var, training, momentum, eps, relu)
+
+
+class BatchNorm2d(nn.BatchNorm2d):
+    """``nn.BatchNorm2d`` + fused ReLU / residual (state_dict-compatible)."""
+
+    def __init__(self, num_features, eps=1e-5, momentum=0.1, affine=True, track_running_stats=True,
+                 fused_relu: bool = False, device=None, dtype=None):
+        super().__init__(num_features, eps, momentum, affine, track_running_stats, device, dtype)
+        self.fused_relu = fused_relu
+        self._nbt = 0  # host-side num_batches_tracked (synced into the buffer on save)
+
+    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
+                relu: Optional[bool] = None) -> torch.Tensor:
+        relu = self.fused_relu if relu is None else relu
+        training = self.training or not self.track_running_stats
+        momentum = self.momentum
+        if self.training and self.track_running_stats:
+            self._nbt += 1
+            if momentum is None:  # cumulative moving average
+                momentum = 1.0 / float(self._nbt + int(self.num_batches_tracked.item()))
+        rm = self.running_mean if (not self.training or self.track_running_stats) else None
+        rv = self.running_var if (not self.training or self.track_running_stats) else None
+        w = self.weight if self.affine else None
+        b = self.bias if self.affine else None
+        return batch_norm_act(x, residual, w, b, rm, rv, training, momentum if momentum is not None else 0.0,
+                              self.eps, relu)
+
+    def sync_num_batches_tracked(self) -> None:
+        if self.track_running_stats and self._nbt:
+            self.num_batches_tracked.add_(self._nbt)
+            self._nbt = 0
+
+    def _save_to_state_dict(self, destination, prefix, keep_vars):
+        self.sync_num_batches_tracked()
+        super()._save_to_state_dict(destination, prefix, keep_vars)
+
+    def _load_from_state_dict(self, *args, **kwargs):
+        self._nbt = 0
+        super()._load_from_state_dict(*args, **kwargs)

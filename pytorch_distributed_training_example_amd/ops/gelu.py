@@ -1,0 +1,34 @@
+"""Bias + GELU (csrc/kernels/gelu.hip): ``gelu(x + bias)`` with the bias gradient fused."""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+from ._native import native, use_native
+
+
+class _BiasGeluFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, bias, tanh_form):
+        y = native().bias_gelu_fwd(x, bias, tanh_form)
+        ctx.save_for_backward(x, bias)
+        ctx.tanh_form = tanh_form
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, bias = ctx.saved_tensors
+        dx, db = native().bias_gelu_bwd(dy.contiguous(), x, bias, ctx.tanh_form)
+        return dx, (db if bias is not None else None), None
+
+
+def bias_gelu(x: torch.Tensor, bias: Optional[torch.Tensor] = None, approximate: str = "none") -> torch.Tensor:
+    tanh_form = approximate == "tanh"
+    if (use_native(x) and x.dtype in (torch.float32, torch.bfloat16) and x.shape[-1] % 4 == 0
+            and (bias is None or bias.dtype == torch.float32)):
+        return _BiasGeluFn.apply(x.contiguous(), bias, tanh_form)
+    if bias is not None:
+        x = x + bias.to(x.dtype)
+    return F.gelu(x, approximate=approximate)

@@ -1,0 +1,414 @@
+"""Bucketed, backward-overlapped data parallelism (``DistributedDataParallel``).
+
+Reference: /root/reference/train.py:34-39 (``average_gradients``) averages gradients with one
+blocking ``dist.all_reduce`` per parameter after ``loss.backward()`` returns, i.e. no
+bucketing and no overlap (the comment at train.py:24 names DDP but it is never used).
+
+This module is a from-scratch reducer with the ``torch.nn.parallel.DistributedDataParallel``
+API surface (ctor kwargs, ``no_sync``, ``register_comm_hook``, ``module.``-prefixed
+state_dict, rank-0 parameter/buffer broadcast) built for MI355X:
+
+  * gradients live in flat per-bucket buffers (``gradient_as_bucket_view``) so a bucket is
+    reduced with ONE RCCL call and the fused optimizers read it in place;
+  * a post-accumulate-grad hook marks parameters ready; a bucket launches as soon as its
+    last gradient exists, in bucket order on every rank (collective order must match
+    across ranks), as an async RCCL all-reduce. c10d runs it on its own RCCL HIP stream,
+    ordered after the producing kernels by an event, so it overlaps the rest of backward;
+  * the 1/world averaging is done inside the collective (``ReduceOp.AVG``) on RCCL — no
+    per-parameter ``div_`` kernels (the reference launches 10 per step, train.py:39);
+  * at the end of backward (autograd engine callback) the compute stream waits on the
+    outstanding collectives — the host never blocks, so the whole step can be captured in
+    a hipGraph (engine/graph.py);
+  * after the first iteration buckets are rebuilt in the order gradients actually
+    became ready (rank 0's order is broadcast so all ranks agree);
+  * optional ``reduce_dtype`` (e.g. reduce bf16 gradients in fp32) and comm hooks
+    (bf16/fp16 compression, per-rank debugging).
+"""
+from __future__ import annotations
+
+import contextlib
+import logging
+import warnings
+from typing import Any, Callable, Dict, List, Optional, Sequence
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from .buckets import (DEFAULT_BUCKET_CAP_MB, DEFAULT_FIRST_BUCKET_BYTES, BucketSpec,
+                      compute_bucket_assignment)
+
+log = logging.getLogger(__name__)
+
+
+class GradBucket:
+    """What a comm hook sees (mirrors ``torch.distributed.GradBucket``)."""
+
+    def __init__(self, index: int, buffer: torch.Tensor, params: List[nn.Parameter],
+                 views: List[torch.Tensor], is_last: bool):
+        self._index = index
+        self._buffer = buffer
+        self._params = params
+        self._views = views
+        self._is_last = is_last
+
+    def index(self) -> int:
+        return self._index
+
+    def buffer(self) -> torch.Tensor:
+        return self._buffer
+
+    def set_buffer(self, t: torch.Tensor) -> None:
+        self._buffer.copy_(t)
+
+    def gradients(self) -> List[torch.Tensor]:
+        return self._views
+
+    def parameters(self) -> List[nn.Parameter]:
+        return self._params
+
+    def is_last(self) -> bool:
+        return self._is_last
+
+
+def is_dense(t: torch.Tensor) -> bool:
+    """True if ``t`` covers exactly ``numel`` consecutive elements (any dim order)."""
+    dims = sorted((st, sz) for st, sz in zip(t.stride(), t.shape) if sz != 1)
+    expect = 1
+    for st, sz in dims:
+        if st != expect:
+            return False
+        expect *= sz
+    return True
+
+
+def _strided_view(buffer: torch.Tensor, p: torch.Tensor, offset: int) -> torch.Tensor:
+    if p.is_contiguous() or not is_dense(p):
+        return buffer[offset:offset + p.numel()].view(p.shape)
+    return torch.as_strided(buffer, p.shape, p.stride(), offset)
+
+
+class _Bucket:
+    def __init__(self, index: int, spec: BucketSpec, params: List[nn.Parameter],
+                 reduce_dtype: Optional[torch.dtype]):
+        self.index = index
+        self.spec = spec
+        self.params = params
+        self.buffer = torch.zeros(spec.total, dtype=spec.dtype, device=spec.device)
+        # Views keep the parameter's strides (e.g. channels_last conv weights), so autograd
+        # accumulates into them without a layout-changing copy.
+        self.views = [_strided_view(self.buffer, p, o) for p, o in zip(params, spec.offsets)]
+        self.comm_buffer = self.buffer
+        if reduce_dtype is not None and reduce_dtype != spec.dtype:
+            self.comm_buffer = torch.zeros(spec.total, dtype=reduce_dtype, device=spec.device)
+        self.pending = len(params)
+        self.arrived = [False] * len(params)
+        self.launched = False
+        self.work: Any = None
+        self.future: Any = None
+
+    def reset(self) -> None:
+        self.pending = len(self.params)
+        self.arrived = [False] * len(self.params)
+        self.launched = False
+        self.work = None
+        self.future = None
+
+
+def _default_avg_op(pg) -> tuple[Any, bool]:
+    """(op, needs_divide). RCCL averages in-collective; gloo has no AVG."""
+    backend = dist.get_backend(pg)
+    if backend == "nccl":
+        return dist.ReduceOp.AVG, False
+    return dist.ReduceOp.SUM, True
+
+
+class DistributedDataParallel(nn.Module):
+    """Drop-in for ``torch.nn.parallel.DistributedDataParallel`` (single device per rank)."""
+
+    def __init__(
+        self,
+        module: nn.Module,
+        device_ids: Optional[Sequence[int]] = None,
+        output_device: Optional[int] = None,
+        dim: int = 0,
+        broadcast_buffers: bool = True,
+        init_sync: bool = True,
+        process_group=None,
+        bucket_cap_mb: Optional[float] = None,
+        find_unused_parameters: bool = False,
+        check_reduction: bool = False,
+        gradient_as_bucket_view: bool = True,
+        static_graph: bool = False,
+        first_bucket_mb: Optional[float] = None,
+        reduce_dtype: Optional[torch.dtype] = None,
+        rebuild_buckets: bool = True,
+    ):
+        super().__init__()
+        self.module = module
+        self.device_ids = list(device_ids) if device_ids is not None else None
+        self.output_device = output_device
+        self.dim = dim
+        self.process_group = process_group if process_group is not None else (
+            dist.group.WORLD if dist.is_initialized() else None)
+        self.world_size = dist.get_world_size(self.process_group) if dist.is_initialized() else 1
+        self.broadcast_buffers = broadcast_buffers
+        self.find_unused_parameters = find_unused_parameters
+        self.gradient_as_bucket_view = gradient_as_bucket_view
+        self.static_graph = static_graph
+        self.reduce_dtype = reduce_dtype
+        self.bucket_bytes_cap = int((bucket_cap_mb if bucket_cap_mb is not None
+                                     else DEFAULT_BUCKET_CAP_MB) * 1024 * 1024)
+        self.first_bucket_bytes = int(first_bucket_mb * 1024 * 1024) if first_bucket_mb is not None \
+            else min(DEFAULT_FIRST_BUCKET_BYTES, self.bucket_bytes_cap)
+        self.require_backward_grad_sync = True
+        self._comm_hook: Optional[Callable] = None
+        self._comm_hook_state: Any = None
+        self._rebuild_enabled = rebuild_buckets and not static_graph
+        self._ready_order: List[int] = []
+        self._rebuilt = False
+        self._rebuild_pending = False
+        self._callback_queued = False
+        self._next_bucket = 0
+        self._num_iterations = 0
+
+        ignore = getattr(module, "_ddp_params_and_buffers_to_ignore", set())
+        seen = set()
+        self._params: List[nn.Parameter] = []
+        self._param_names: List[str] = []
+        for name, p in module.named_parameters():
+            if not p.requires_grad or name in ignore or id(p) in seen:
+                continue
+            seen.add(id(p))
+            self._params.append(p)
+            self._param_names.append(name)
+        self._buffers_to_sync = [b for n, b in module.named_buffers() if n not in ignore]
+        if self.process_group is not None and self.world_size > 1:
+            self._avg_op, self._needs_div = _default_avg_op(self.process_group)
+        else:
+            self._avg_op, self._needs_div = None, False
+
+        if init_sync and self.world_size > 1:
+            self._sync_module_states()
+        self._build_buckets(order=None)
+        self._hook_handles = [p.register_post_accumulate_grad_hook(self._make_hook(i))
+                              for i, p in enumerate(self._params)]
+
+    # ------------------------------------------------------------------ setup
+    def _sync_module_states(self) -> None:
+        """Broadcast rank 0's parameters and buffers (coalesced by dtype).
+
+        The reference relies on every rank using the same seed (train.py:80-81) and never
+        broadcasts; a broadcast makes replicas identical regardless of init RNG.
+        """
+        tensors = [p.data for p in self.module.parameters()] + list(self._buffers_to_sync)
+        self._broadcast_coalesced(tensors)
+
+    def _broadcast_coalesced(self, tensors: List[torch.Tensor], bucket_bytes: int = 256 << 20) -> None:
+        by_key: Dict[Any, List[torch.Tensor]] = {}
+        for t in tensors:
+            if t.numel() == 0:
+                continue
+            by_key.setdefault((t.dtype, t.device), []).append(t)
+        for _, ts in by_key.items():
+            chunk: List[torch.Tensor] = []
+            size = 0
+            for t in ts + [None]:  # type: ignore[list-item]
+                if t is not None:
+                    chunk.append(t)
+                    size += t.numel() * t.element_size()
+                if chunk and (t is None or size >= bucket_bytes):
+                    flat = torch.cat([c.reshape(-1) for c in chunk])
+                    dist.broadcast(flat, src=dist.get_global_rank(self.process_group, 0)
+                                   if self.process_group not in (None, dist.group.WORLD) else 0,
+                                   group=self.process_group)
+                    off = 0
+                    for c in chunk:
+                        c.copy_(flat[off:off + c.numel()].view_as(c))
+                        off += c.numel()
+                    chunk, size = [], 0
+
+    def _build_buckets(self, order: Optional[List[int]]) -> None:
+        specs = compute_bucket_assignment(self._params, self.bucket_bytes_cap,
+                                          self.first_bucket_bytes, order=order)
+        old_grads = {i: p.grad for i, p in enumerate(self._params)}
+        self._buckets: List[_Bucket] = []
+        self._param_loc: Dict[int, tuple[int, int]] = {}
+        for b, spec in enumerate(specs):
+            params = [self._params[i] for i in spec.indices]
+            bucket = _Bucket(b, spec, params, self.reduce_dtype)
+            for j, i in enumerate(spec.indices):
+                self._param_loc[i] = (b, j)
+            self._buckets.append(bucket)
+        if self.gradient_as_bucket_view:
+            for i, p in enumerate(self._params):
+                b, j = self._param_loc[i]
+                view = self._buckets[b].views[j]
+                g = old_grads[i]
+                if g is not None:
+                    view.copy_(g)
+                    p.grad = view
+
+    def bucket_specs(self) -> List[BucketSpec]:
+        return [b.spec for b in self._buckets]
+
+    # ------------------------------------------------------------------ hooks
+    def _make_hook(self, index: int) -> Callable:
+        def hook(param: torch.Tensor) -> None:
+            self._on_grad_ready(index, param)
+        return hook
+
+    def _on_grad_ready(self, index: int, param: torch.Tensor) -> None:
+        if not self.require_backward_grad_sync:
+            return
+        if not self._callback_queued:
+            self._callback_queued = True
+            torch.autograd.Variable._execution_engine.queue_callback(self._finalize_backward)
+        if self._rebuild_enabled and not self._rebuilt:
+            self._ready_order.append(index)
+        b, j = self._param_loc[index]
+        bucket = self._buckets[b]
+        if bucket.arrived[j]:
+            return
+        view = bucket.views[j]
+        g = param.grad
+        if g is None:
+            view.zero_()
+        elif g.data_ptr() != view.data_ptr():
+            view.copy_(g)
+        if self.gradient_as_bucket_view:
+            param.grad = view
+        bucket.arrived[j] = True
+        bucket.pending -= 1
+        self._launch_ready_buckets()
+
+    def _launch_ready_buckets(self) -> None:
+        while self._next_bucket < len(self._buckets) and self._buckets[self._next_bucket].pending == 0:
+            self._launch(self._buckets[self._next_bucket])
+            self._next_bucket += 1
+
+    def _launch(self, bucket: _Bucket) -> None:
+        bucket.launched = True
+        if self.world_size <= 1 and self._comm_hook is None:
+            return
+        if bucket.comm_buffer is not bucket.buffer:
+            bucket.comm_buffer.copy_(bucket.buffer)
+        if self._comm_hook is not None:
+            gb = GradBucket(bucket.index, bucket.comm_buffer, bucket.params, bucket.views,
+                            bucket.index == len(self._buckets) - 1)
+            bucket.future = self._comm_hook(self._comm_hook_state, gb)
+            return
+        bucket.work = dist.all_reduce(bucket.comm_buffer, op=self._avg_op,
+                                      group=self.process_group, async_op=True)
+
+    def _finalize_backward(self) -> None:
+        # Parameters that did not take part in this backward (unused / frozen branch)
+        # contribute zeros so every rank launches the same collectives in the same order.
+        for bucket in self._buckets:
+            if bucket.pending > 0:
+                for j, arrived in enumerate(bucket.arrived):
+                    if not arrived:
+                        bucket.views[j].zero_()
+                        p = bucket.params[j]
+                        if self.gradient_as_bucket_view:
+                            p.grad = bucket.views[j]
+                        bucket.arrived[j] = True
+                bucket.pending = 0
+        self._launch_ready_buckets()
+        for bucket in self._buckets:
+            if bucket.future is not None:
+                out = bucket.future.wait()
+                if isinstance(out, (list, tuple)):
+                    out = out[0]
+                if out is not None and out.data_ptr() != bucket.buffer.data_ptr():
+                    bucket.buffer.copy_(out.view(-1)[: bucket.buffer.numel()])
+            elif bucket.work is not None:
+                bucket.work.wait()  # stream-ordered: compute stream waits on the RCCL stream
+                if self._needs_div:
+                    bucket.comm_buffer.div_(self.world_size)
+                if bucket.comm_buffer is not bucket.buffer:
+                    bucket.buffer.copy_(bucket.comm_buffer)
+            if not self.gradient_as_bucket_view:
+                for p, v in zip(bucket.params, bucket.views):
+                    if p.grad is None:
+                        p.grad = v.clone()
+                    elif p.grad.data_ptr() != v.data_ptr():
+                        p.grad.copy_(v)
+            bucket.reset()
+        self._next_bucket = 0
+        self._callback_queued = False
+        self._num_iterations += 1
+        if self._rebuild_enabled and not self._rebuilt:
+            self._rebuild_pending = True
+
+    def _maybe_rebuild(self) -> None:
+        if not self._rebuild_pending:
+            return
+        self._rebuild_pending = False
+        self._rebuilt = True
+        order = list(dict.fromkeys(self._ready_order))
+        order += [i for i in range(len(self._params)) if i not in set(order)]
+        if self.world_size > 1:
+            obj = [order]
+            dist.broadcast_object_list(obj, src=0, group=self.process_group)
+            order = obj[0]
+        self._build_buckets(order=order)
+
+    # ------------------------------------------------------------------ API
+    def forward(self, *inputs, **kwargs):
+        if torch.is_grad_enabled() and self.require_backward_grad_sync:
+            self._maybe_rebuild()
+        if self.broadcast_buffers and self.world_size > 1 and self._buffers_to_sync:
+            self._broadcast_coalesced(list(self._buffers_to_sync))
+        return self.module(*inputs, **kwargs)
+
+    @contextlib.contextmanager
+    def no_sync(self):
+        """Accumulate gradients locally (into the bucket buffers) without communicating."""
+        old = self.require_backward_grad_sync
+        self.require_backward_grad_sync = False
+        try:
+            yield
+        finally:
+            self.require_backward_grad_sync = old
+
+    def register_comm_hook(self, state: Any, hook: Callable) -> None:
+        if self._comm_hook is not None:
+            raise RuntimeError("register_comm_hook can only be called once")
+        self._comm_hook_state = state
+        self._comm_hook = hook
+
+    def zero_grad_buckets(self) -> None:
+        """Zero all flat gradient buckets with one memset each (keeps grads as views)."""
+        for b in self._buckets:
+            b.buffer.zero_()
+        if self.gradient_as_bucket_view:
+            for b in self._buckets:
+                for p, v in zip(b.params, b.views):
+                    p.grad = v
+
+    def grad_buffers(self) -> List[torch.Tensor]:
+        return [b.buffer for b in self._buckets]
+
+    def parameters_and_views(self):
+        for b in self._buckets:
+            yield from zip(b.params, b.views)
+
+    def __getattr__(self, name: str):
+        try:
+            return super().__getattr__(name)
+        except AttributeError:
+            return getattr(self.module, name)
+
+    def __del__(self):
+        for h in getattr(self, "_hook_handles", []):
+            try:
+                h.remove()
+            except Exception:
+                pass
+
+
+def unwrap(model: nn.Module) -> nn.Module:
+    """Strip a DDP wrapper (ours or torch's)."""
+    return model.module if hasattr(model, "module") and isinstance(
+        model, (DistributedDataParallel, torch.nn.parallel.DistributedDataParallel)) else model

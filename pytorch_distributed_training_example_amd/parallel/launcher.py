@@ -1,0 +1,204 @@
+"""Process launch and process-group initialisation.
+
+Reference parity:
+  * ``init_process`` (/root/reference/train.py:26-31) hard-codes ``MASTER_ADDR=127.0.0.1``,
+    ``MASTER_PORT=29500`` and calls ``dist.init_process_group`` with no ``set_device``,
+    no barrier and no teardown.
+  * The launcher (/root/reference/train.py:134-147) spawns one process per visible GPU
+    with ``torch.multiprocessing.spawn``.
+
+MI355X-first design:
+  * One process per GPU. ``LOCAL_RANK`` selects the HIP device *before* the first
+    collective so RCCL builds its communicator over the right xGMI endpoint.
+  * Works both under ``torchrun`` (env:// variables already present) and as a
+    self-spawning script (``spawn``), and on CPU with ``gloo`` (tests).
+  * Rendezvous defaults to 127.0.0.1 (the container hostname may not resolve),
+    overridable through the usual ``MASTER_ADDR`` / ``MASTER_PORT`` env vars
+    (multi-node ready: the reference is localhost-only, train.py:28).
+  * ``init_distributed`` sets a bounded timeout and ``destroy`` tears the group down
+    cleanly (the reference never calls ``destroy_process_group``).
+"""
+from __future__ import annotations
+
+import datetime
+import os
+import socket
+from dataclasses import dataclass
+from typing import Any, Callable, Optional, Sequence
+
+import torch
+import torch.distributed as dist
+
+DEFAULT_MASTER_ADDR = "127.0.0.1"
+DEFAULT_MASTER_PORT = 29500
+
+
+@dataclass
+class DistContext:
+    rank: int = 0
+    world_size: int = 1
+    local_rank: int = 0
+    local_world_size: int = 1
+    backend: str = "gloo"
+    device: torch.device = torch.device("cpu")
+
+    @property
+    def is_main(self) -> bool:
+        return self.rank == 0
+
+    @property
+    def distributed(self) -> bool:
+        return dist.is_available() and dist.is_initialized()
+
+
+_CTX: Optional[DistContext] = None
+
+
+def find_free_port(addr: str = DEFAULT_MASTER_ADDR) -> int:
+    """Return an unused TCP port on ``addr`` (used by tests and ``spawn``)."""
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind((addr, 0))
+        return s.getsockname()[1]
+
+
+def env_rank_info() -> tuple[int, int, int, int]:
+    """(rank, world_size, local_rank, local_world_size) from torchrun-style env vars."""
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    return rank, world, local_rank, local_world
+
+
+def default_backend(use_gpu: Optional[bool] = None) -> str:
+    """RCCL (torch backend name ``nccl``) when GPUs are usable, else gloo."""
+    if use_gpu is None:
+        use_gpu = torch.cuda.is_available()
+    return "nccl" if use_gpu else "gloo"
+
+
+def init_distributed(
+    backend: Optional[str] = None,
+    rank: Optional[int] = None,
+    world_size: Optional[int] = None,
+    local_rank: Optional[int] = None,
+    timeout_s: float = 600.0,
+    use_gpu: Optional[bool] = None,
+    set_device: bool = True,
+) -> DistContext:
+    """Initialise the default process group (env:// rendezvous over a TCPStore).
+
+    Unlike the reference (train.py:26-31) this binds the rank to its GPU first and
+    allows world_size == 1 (the reference's SplitDataset asserts >= 2 ranks,
+    splitdataset.py:38-39).
+    """
+    global _CTX
+    e_rank, e_world, e_local, e_lws = env_rank_info()
+    rank = e_rank if rank is None else rank
+    world_size = e_world if world_size is None else world_size
+    local_rank = e_local if local_rank is None else local_rank
+    if use_gpu is None:
+        use_gpu = torch.cuda.is_available() and (backend in (None, "nccl"))
+    backend = backend or default_backend(use_gpu)
+    os.environ.setdefault("MASTER_ADDR", DEFAULT_MASTER_ADDR)
+    os.environ.setdefault("MASTER_PORT", str(DEFAULT_MASTER_PORT))
+    # dmabuf IPC is the only IPC mode the MI355X host driver supports; keep it for RCCL.
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
+    device = torch.device("cpu")
+    if use_gpu:
+        n = torch.cuda.device_count()
+        dev_idx = local_rank % max(n, 1)
+        if set_device:
+            torch.cuda.set_device(dev_idx)
+        device = torch.device("cuda", dev_idx)
+
+    if world_size > 1 or backend == "nccl" or os.environ.get("PDT_FORCE_PG"):
+        if not dist.is_initialized():
+            kwargs: dict[str, Any] = dict(
+                backend=backend,
+                rank=rank,
+                world_size=world_size,
+                timeout=datetime.timedelta(seconds=timeout_s),
+            )
+            if backend == "nccl" and device.type == "cuda":
+                # Eager communicator creation binds the RCCL comm to this device.
+                kwargs["device_id"] = device
+            dist.init_process_group(**kwargs)
+    _CTX = DistContext(rank, world_size, local_rank, e_lws, backend, device)
+    return _CTX
+
+
+def context() -> DistContext:
+    global _CTX
+    if _CTX is None:
+        if dist.is_available() and dist.is_initialized():
+            _CTX = DistContext(
+                dist.get_rank(), dist.get_world_size(), env_rank_info()[2], env_rank_info()[3],
+                dist.get_backend(),
+                torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available()
+                else torch.device("cpu"),
+            )
+        else:
+            _CTX = DistContext()
+    return _CTX
+
+
+def get_rank() -> int:
+    return dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+
+
+def get_world_size() -> int:
+    return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+
+
+def barrier() -> None:
+    if dist.is_available() and dist.is_initialized():
+        if dist.get_backend() == "nccl" and torch.cuda.is_available():
+            dist.barrier(device_ids=[torch.cuda.current_device()])
+        else:
+            dist.barrier()
+
+
+def destroy() -> None:
+    """Tear down the default group (the reference never does, train.py:26-31)."""
+    global _CTX
+    if dist.is_available() and dist.is_initialized():
+        dist.destroy_process_group()
+    _CTX = None
+
+
+def _spawn_entry(local_rank: int, world_size: int, fn: Callable, args: Sequence,
+                 backend: str, addr: str, port: int, use_gpu: bool,
+                 timeout_s: float) -> None:
+    os.environ["MASTER_ADDR"] = addr
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ["RANK"] = str(local_rank)
+    os.environ["LOCAL_RANK"] = str(local_rank)
+    os.environ["WORLD_SIZE"] = str(world_size)
+    os.environ["LOCAL_WORLD_SIZE"] = str(world_size)
+    init_distributed(backend=backend, use_gpu=use_gpu, timeout_s=timeout_s)
+    try:
+        fn(local_rank, world_size, *args)
+    finally:
+        destroy()
+
+
+def spawn(fn: Callable, nprocs: int, args: Sequence = (), backend: Optional[str] = None,
+          master_addr: str = DEFAULT_MASTER_ADDR, master_port: Optional[int] = None,
+          use_gpu: Optional[bool] = None, timeout_s: float = 600.0, join: bool = True):
+    """Spawn ``nprocs`` ranks, each running ``fn(rank, world_size, *args)`` after init.
+
+    Equivalent of ``spawn(init_process, ...)`` in /root/reference/train.py:147, but with a
+    free port by default (no collisions between concurrent jobs / tests), a selectable
+    backend, and a torchrun-compatible environment inside each child.
+    """
+    import torch.multiprocessing as mp
+
+    if use_gpu is None:
+        use_gpu = torch.cuda.is_available() and backend in (None, "nccl")
+    backend = backend or default_backend(use_gpu)
+    port = master_port or find_free_port(master_addr)
+    return mp.spawn(_spawn_entry,
+                    args=(nprocs, fn, tuple(args), backend, master_addr, port, use_gpu, timeout_s),
+                    nprocs=nprocs, join=join)

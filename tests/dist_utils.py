@@ -1,0 +1,26 @@
+"""Run a function on N gloo ranks (CPU) and collect per-rank results."""
+import os
+import tempfile
+
+import torch
+import torch.multiprocessing as mp
+
+
+def _entry(rank, world, fn, port, outdir, args):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world))
+    from pytorch_distributed_training_example_amd.parallel import launcher
+    launcher.init_distributed(backend="gloo", use_gpu=False, timeout_s=120)
+    try:
+        out = fn(rank, world, *args)
+        torch.save(out, os.path.join(outdir, f"r{rank}.pt"))
+    finally:
+        launcher.destroy()
+
+
+def run_ranks(fn, world=2, args=()):
+    from pytorch_distributed_training_example_amd.parallel.launcher import find_free_port
+    torch.set_num_threads(1)
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_entry, args=(world, fn, find_free_port(), d, tuple(args)), nprocs=world, join=True)
+        return [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=False) for r in range(world)]

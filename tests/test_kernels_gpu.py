@@ -1,0 +1,246 @@
+"""Numerics of every gfx950 HIP kernel vs a plain PyTorch fp32 reference of the same op."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _native():
+    from pytorch_distributed_training_example_amd.ops._native import native
+    return native()
+
+
+# ----------------------------------------------------------------------------- BatchNorm NHWC
+@pytest.mark.parametrize("C", [64, 256, 2048, 4096, 24])
+@pytest.mark.parametrize("relu,res", [(False, False), (True, False), (True, True), (False, True)])
+def test_batchnorm_train_fwd_bwd(C, relu, res):
+    from pytorch_distributed_training_example_amd.ops.batchnorm import batch_norm_act
+    torch.manual_seed(0)
+    N, H, W = (4, 7, 9) if C >= 1024 else (8, 14, 13)
+    x = (torch.randn(N, C, H, W, device=DEV) * 2 + 0.5).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    r = torch.randn_like(x) if res else None
+    w = torch.rand(C, device=DEV) + 0.5
+    b = torch.randn(C, device=DEV)
+    rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    rm2, rv2 = rm.clone(), rv.clone()
+    xs = x.detach().requires_grad_(True)
+    ws, bs = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    rs = r.detach().requires_grad_(True) if res else None
+    y = batch_norm_act(xs, rs, ws, bs, rm, rv, True, 0.1, 1e-5, relu)
+    # fp32 reference
+    xf = x.float().detach().requires_grad_(True)
+    wf, bf = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    rf = r.float().detach().requires_grad_(True) if res else None
+    yf = F.batch_norm(xf, rm2, rv2, wf, bf, True, 0.1, 1e-5)
+    if res:
+        yf = yf + rf
+    if relu:
+        yf = F.relu(yf)
+    assert y.dtype == torch.bfloat16 and y.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(y.float(), yf, rtol=2e-2, atol=3e-2)
+    torch.testing.assert_close(rm, rm2, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(rv, rv2, rtol=1e-3, atol=1e-3)
+    g = torch.randn_like(y)
+    y.backward(g)
+    yf.backward(g.float())
+    torch.testing.assert_close(xs.grad.float(), xf.grad, rtol=3e-2, atol=3e-2)
+    torch.testing.assert_close(ws.grad, wf.grad, rtol=2e-2, atol=2e-1)
+    torch.testing.assert_close(bs.grad, bf.grad, rtol=2e-2, atol=2e-1)
+    if res:
+        torch.testing.assert_close(rs.grad.float(), rf.grad, rtol=2e-2, atol=2e-2)
+
+
+def test_batchnorm_large_mean_stability():
+    """Shifted sums must not lose the variance when |mean| >> std."""
+    from pytorch_distributed_training_example_amd.ops.batchnorm import batch_norm_act
+    C = 64
+    x = (torch.randn(32, C, 16, 16, device=DEV) * 0.5 + 40.0).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    y = batch_norm_act(x, None, None, None, rm, rv, True, 1.0, 1e-5, False)
+    yf = F.batch_norm(x.float(), None, None, None, None, True, 0.0, 1e-5)
+    torch.testing.assert_close(y.float(), yf, rtol=3e-2, atol=6e-2)
+
+
+def test_batchnorm_eval():
+    from pytorch_distributed_training_example_amd.ops.batchnorm import BatchNorm2d
+    C = 128
+    bn = BatchNorm2d(C, fused_relu=True).to(DEV).eval()
+    bn.running_mean.uniform_(-1, 1)
+    bn.running_var.uniform_(0.5, 2)
+    x = torch.randn(4, C, 8, 8, device=DEV).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    y = bn(x)
+    yf = F.relu(F.batch_norm(x.float(), bn.running_mean, bn.running_var, bn.weight, bn.bias, False, 0.1, bn.eps))
+    torch.testing.assert_close(y.float(), yf, rtol=2e-2, atol=2e-2)
+
+
+# ----------------------------------------------------------------------------- LayerNorm
+@pytest.mark.parametrize("D", [256, 768, 1024])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_layernorm(D, dtype):
+    from pytorch_distributed_training_example_amd.ops.layernorm import layer_norm
+    torch.manual_seed(0)
+    x = (torch.randn(37, 5, D, device=DEV) * 3 + 1).to(dtype).requires_grad_(True)
+    w = (torch.rand(D, device=DEV) + 0.5).requires_grad_(True)
+    b = torch.randn(D, device=DEV).requires_grad_(True)
+    y = layer_norm(x, (D,), w, b, 1e-5)
+    xf = x.detach().float().requires_grad_(True)
+    wf, bf = w.detach().clone().requires_grad_(True), b.detach().clone().requires_grad_(True)
+    yf = F.layer_norm(xf, (D,), wf, bf, 1e-5)
+    tol = dict(rtol=1e-4, atol=1e-4) if dtype == torch.float32 else dict(rtol=2e-2, atol=3e-2)
+    torch.testing.assert_close(y.float(), yf, **tol)
+    g = torch.randn_like(yf)
+    y.backward(g.to(dtype))
+    yf.backward(g.to(dtype).float())
+    torch.testing.assert_close(x.grad.float(), xf.grad, **(tol if dtype == torch.float32 else dict(rtol=3e-2, atol=5e-2)))
+    torch.testing.assert_close(w.grad, wf.grad, rtol=1e-3 if dtype == torch.float32 else 2e-2, atol=1e-2 if dtype == torch.float32 else 3e-1)
+    torch.testing.assert_close(b.grad, bf.grad, rtol=1e-3, atol=1e-2 if dtype == torch.float32 else 3e-1)
+
+
+# ----------------------------------------------------------------------------- cross entropy
+@pytest.mark.parametrize("V", [10, 1000, 50304, 50257])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("smoothing", [0.0, 0.1])
+def test_cross_entropy(V, dtype, smoothing):
+    from pytorch_distributed_training_example_amd.ops.cross_entropy import cross_entropy
+    torch.manual_seed(0)
+    N = 33
+    logits = (torch.randn(N, V, device=DEV) * 3).to(dtype).requires_grad_(True)
+    t = torch.randint(0, V, (N,), device=DEV)
+    t[3] = -100
+    loss = cross_entropy(logits, t, label_smoothing=smoothing)
+    lf = logits.detach().float().requires_grad_(True)
+    ref = F.cross_entropy(lf, t, label_smoothing=smoothing)
+    torch.testing.assert_close(loss, ref, rtol=1e-4, atol=1e-4)
+    loss.backward()
+    ref.backward()
+    tol = dict(rtol=1e-4, atol=1e-6) if dtype == torch.float32 else dict(rtol=2e-2, atol=1e-4)
+    torch.testing.assert_close(logits.grad.float(), lf.grad, **tol)
+
+
+# ----------------------------------------------------------------------------- bias + gelu
+@pytest.mark.parametrize("approx", ["none", "tanh"])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_bias_gelu(approx, dtype):
+    from pytorch_distributed_training_example_amd.ops.gelu import bias_gelu
+    torch.manual_seed(0)
+    x = torch.randn(67, 3072, device=DEV).to(dtype).requires_grad_(True)
+    b = torch.randn(3072, device=DEV).requires_grad_(True)
+    y = bias_gelu(x, b, approx)
+    xf = x.detach().float().requires_grad_(True)
+    bf = b.detach().clone().requires_grad_(True)
+    yf = F.gelu(xf + bf, approximate=approx)
+    tol = dict(rtol=1e-4, atol=1e-5) if dtype == torch.float32 else dict(rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(y.float(), yf, **tol)
+    g = torch.randn_like(yf)
+    y.backward(g.to(dtype))
+    yf.backward(g.to(dtype).float())
+    torch.testing.assert_close(x.grad.float(), xf.grad, **tol)
+    torch.testing.assert_close(b.grad, bf.grad, rtol=1e-3 if dtype == torch.float32 else 3e-2, atol=1e-3 if dtype == torch.float32 else 3e-1)
+
+
+# ----------------------------------------------------------------------------- optimizers
+def _params(dtype=torch.float32, channels_last=False):
+    torch.manual_seed(0)
+    shapes = [(64, 3, 7, 7), (64,), (1000, 2048), (3,), (70001,), (5, 5)]
+    ps = []
+    for s in shapes:
+        p = torch.randn(s, device=DEV)
+        if channels_last and len(s) == 4:
+            p = p.to(memory_format=torch.channels_last)
+        ps.append(torch.nn.Parameter(p.to(dtype)))
+    return ps
+
+
+def _run_opt(make, ps, steps=3, seed=1):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    opt = make(ps)
+    for _ in range(steps):
+        for p in ps:
+            p.grad = torch.randn(p.shape, device=DEV, generator=g).to(p.dtype)
+            if p.dim() == 4:
+                p.grad = p.grad.contiguous(memory_format=torch.channels_last) if p.is_contiguous(memory_format=torch.channels_last) else p.grad
+        opt.step()
+    return ps, opt
+
+
+@pytest.mark.parametrize("nesterov,wd,mom", [(False, 0.0, 0.0), (False, 1e-4, 0.9), (True, 5e-5, 0.9)])
+def test_fused_sgd_matches_torch(nesterov, wd, mom):
+    from pytorch_distributed_training_example_amd.optim import FusedSGD
+    a, _ = _run_opt(lambda ps: FusedSGD(ps, lr=0.1, momentum=mom, weight_decay=wd, nesterov=nesterov), _params(channels_last=True))
+    b, _ = _run_opt(lambda ps: torch.optim.SGD(ps, lr=0.1, momentum=mom, weight_decay=wd, nesterov=nesterov), _params(channels_last=True))
+    for x, y in zip(a, b):
+        torch.testing.assert_close(x, y, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("wd,adamw", [(0.0, False), (1e-2, True), (1e-2, False)])
+def test_fused_adam_matches_torch(wd, adamw):
+    from pytorch_distributed_training_example_amd.optim import FusedAdam
+    a, _ = _run_opt(lambda ps: FusedAdam(ps, lr=1e-3, weight_decay=wd, adam_w_mode=adamw), _params())
+    cls = torch.optim.AdamW if adamw else torch.optim.Adam
+    b, _ = _run_opt(lambda ps: cls(ps, lr=1e-3, weight_decay=wd), _params())
+    for x, y in zip(a, b):
+        torch.testing.assert_close(x, y, rtol=1e-5, atol=1e-6)
+
+
+def test_fused_adadelta_matches_torch():
+    from pytorch_distributed_training_example_amd.optim import FusedAdadelta
+    a, oa = _run_opt(lambda ps: FusedAdadelta(ps, lr=0.1), _params())
+    b, ob = _run_opt(lambda ps: torch.optim.Adadelta(ps, lr=0.1), _params())
+    for x, y in zip(a, b):
+        torch.testing.assert_close(x, y, rtol=1e-5, atol=1e-6)
+    # state layout identical to torch (checkpoint compatible)
+    sa, sb = oa.state_dict()["state"][0], ob.state_dict()["state"][0]
+    assert set(sa) == set(sb)
+
+
+def test_master_weights_bf16():
+    from pytorch_distributed_training_example_amd.optim import FusedSGD
+    ps = _params(torch.bfloat16)
+    ref = [torch.nn.Parameter(p.detach().float()) for p in ps]
+    a, oa = _run_opt(lambda q: FusedSGD(q, lr=0.1, momentum=0.9), ps)
+    b, _ = _run_opt(lambda q: torch.optim.SGD(q, lr=0.1, momentum=0.9), ref)
+    for p, r in zip(a, b):
+        m = oa.state[p]["master_param"]
+        torch.testing.assert_close(m, r, rtol=2e-2, atol=2e-2)
+        assert torch.equal(p.detach(), m.to(torch.bfloat16))
+
+
+def test_amp_skip_on_inf_and_unscale():
+    from pytorch_distributed_training_example_amd.optim import FusedSGD
+    from pytorch_distributed_training_example_amd.ops import multi_tensor as mt
+    ps = _params()
+    before = [p.detach().clone() for p in ps]
+    opt = FusedSGD(ps, lr=0.1)
+    for p in ps:
+        p.grad = torch.ones_like(p) * 4
+    ps[2].grad[3, 3] = float("inf")
+    inv = torch.full((1,), 0.25, device=DEV)
+    found = torch.zeros(1, device=DEV)
+    mt.unscale_([p.grad for p in ps], inv, found)
+    assert found.item() == 1.0
+    assert ps[0].grad[0, 0, 0, 0].item() == 1.0
+    opt.step(found_inf=found)
+    for p, q in zip(ps, before):
+        assert torch.equal(p.detach(), q)
+
+
+def test_l2norm_and_clip():
+    from pytorch_distributed_training_example_amd.ops import multi_tensor as mt
+    gs = [torch.randn(s, device=DEV) for s in [(100003,), (7, 9), (64, 64, 3, 3)]] + [torch.randn(1000, device=DEV).bfloat16()]
+    ref = torch.sqrt(sum((g.float() ** 2).sum() for g in gs))
+    norm = mt.clip_grad_norm_(gs, 1.0)
+    torch.testing.assert_close(norm.reshape(()), ref, rtol=1e-4, atol=1e-4)
+    after = torch.sqrt(sum((g.float() ** 2).sum() for g in gs))
+    assert abs(after.item() - 1.0) < 1e-2
+
+
+def test_mt_copy_with_scale():
+    from pytorch_distributed_training_example_amd.ops import multi_tensor as mt
+    src = [torch.randn(s, device=DEV) for s in [(5,), (33333,), (4, 4)]]
+    dst = [torch.empty(s.shape, device=DEV, dtype=torch.bfloat16) for s in src]
+    mt.copy_(src, dst, factor=0.5)
+    for s, d in zip(src, dst):
+        torch.testing.assert_close(d.float(), (s * 0.5).bfloat16().float())
