@@ -7,6 +7,7 @@
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 
+#include <map>
 #include <vector>
 
 extern "C" {
@@ -33,13 +34,14 @@ int pdt_clip_coef(const float* sumsq, float max_norm, float* coef, float* norm, 
 int64_t pdt_bn_workspace_floats(int64_t M, int C);
 int pdt_bn_fwd_train(const uint16_t* x, const uint16_t* res, const float* gamma, const float* beta,
                      float* running_mean, float* running_var, float momentum, float eps, int64_t M, int C, int relu,
-                     uint16_t* y, float* mean, float* invstd, float* ws, hipStream_t s);
+                     uint16_t* y, uint8_t* mask, float* mean, float* invstd, float* ws, unsigned* counters,
+                     hipStream_t s);
 int pdt_bn_fwd_eval(const uint16_t* x, const uint16_t* res, const float* gamma, const float* beta,
                     const float* running_mean, const float* running_var, float eps, int64_t M, int C, int relu,
                     uint16_t* y, float* ws, hipStream_t s);
-int pdt_bn_bwd_train(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* gamma, const float* mean,
-                     const float* invstd, int64_t M, int C, int relu, int has_res, uint16_t* dx, uint16_t* dres,
-                     float* dgamma, float* dbeta, float* ws, hipStream_t s);
+int pdt_bn_bwd_train(const uint16_t* dy, const uint16_t* x, const uint8_t* mask, const float* gamma,
+                     const float* mean, const float* invstd, int64_t M, int C, int relu, int has_res, uint16_t* dx,
+                     uint16_t* dres, float* dgamma, float* dbeta, float* ws, unsigned* counters, hipStream_t s);
 int pdt_ce_fwd(const void* logits, int dtype, const int64_t* target, int64_t N, int64_t V, float smoothing,
                int64_t ignore_index, float* loss, float* lse, hipStream_t s);
 int pdt_ce_bwd(const void* logits, int dtype, const int64_t* target, const float* lse, const float* dloss,
@@ -248,7 +250,19 @@ void check_nhwc_bf16(const Tensor& t, const char* name) {
   }
 }
 
-int64_t bn_ws_floats(int64_t M, int64_t C) { return pdt_bn_workspace_floats(M, (int)C) + 4 * C; }
+int64_t bn_ws_floats(int64_t M, int64_t C) { return pdt_bn_workspace_floats(M, (int)C); }
+
+// Self-resetting arrival counters of the BN reduce kernels (one per 64-channel chunk), one
+// buffer per device, zeroed once at creation (first call happens before any graph capture).
+unsigned* bn_counters(const Tensor& like) {
+  static std::map<int, Tensor> bufs;
+  const int dev = like.get_device();
+  auto it = bufs.find(dev);
+  if (it == bufs.end()) {
+    it = bufs.emplace(dev, at::zeros({4096}, like.options().dtype(at::kInt))).first;
+  }
+  return reinterpret_cast<unsigned*>(it->second.data_ptr<int>());
+}
 
 std::vector<Tensor> bn_fwd_train(Tensor x, c10::optional<Tensor> res, c10::optional<Tensor> weight,
                                  c10::optional<Tensor> bias, c10::optional<Tensor> running_mean,
@@ -256,8 +270,10 @@ std::vector<Tensor> bn_fwd_train(Tensor x, c10::optional<Tensor> res, c10::optio
   check_nhwc_bf16(x, "x");
   const int64_t C = x.size(1);
   const int64_t M = x.numel() / C;
-  TORCH_CHECK(C % 8 == 0, "pdt bn: C must be a multiple of 8");
+  TORCH_CHECK(C % 64 == 0 && C <= 64 * 4096, "pdt bn: C must be a multiple of 64");
   auto y = at::empty_like(x);
+  Tensor mask;
+  if (relu) mask = at::empty({M * C / 8}, x.options().dtype(at::kByte));
   auto fopt = x.options().dtype(at::kFloat);
   auto mean = at::empty({C}, fopt), invstd = at::empty({C}, fopt);
   auto ws = at::empty({bn_ws_floats(M, C)}, fopt);
@@ -271,9 +287,10 @@ std::vector<Tensor> bn_fwd_train(Tensor x, c10::optional<Tensor> res, c10::optio
   float* rv = running_var.has_value() && running_var->defined() ? running_var->data_ptr<float>() : nullptr;
   int rc = pdt_bn_fwd_train(reinterpret_cast<const uint16_t*>(x.data_ptr()), rp, opt_fptr(weight), opt_fptr(bias), rm, rv,
                             (float)momentum, (float)eps, M, (int)C, relu, reinterpret_cast<uint16_t*>(y.data_ptr()),
-                            mean.data_ptr<float>(), invstd.data_ptr<float>(), ws.data_ptr<float>(), stream());
+                            relu ? mask.data_ptr<uint8_t>() : nullptr, mean.data_ptr<float>(),
+                            invstd.data_ptr<float>(), ws.data_ptr<float>(), bn_counters(x), stream());
   TORCH_CHECK(rc == 0, "pdt_bn_fwd_train failed");
-  return {y, mean, invstd};
+  return {y, mask, mean, invstd};
 }
 
 Tensor bn_fwd_eval(Tensor x, c10::optional<Tensor> res, c10::optional<Tensor> weight, c10::optional<Tensor> bias,
@@ -291,12 +308,13 @@ Tensor bn_fwd_eval(Tensor x, c10::optional<Tensor> res, c10::optional<Tensor> we
   return y;
 }
 
-std::vector<Tensor> bn_bwd_train(Tensor dy, Tensor x, c10::optional<Tensor> y, c10::optional<Tensor> weight, Tensor mean,
-                                 Tensor invstd, bool relu, bool has_res, bool need_dgamma) {
+std::vector<Tensor> bn_bwd_train(Tensor dy, Tensor x, c10::optional<Tensor> mask, c10::optional<Tensor> weight,
+                                 Tensor mean, Tensor invstd, bool relu, bool has_res, bool need_dgamma) {
   check_nhwc_bf16(x, "x");
   TORCH_CHECK(dy.sizes() == x.sizes() && dy.strides() == x.strides(), "pdt bn bwd: dy layout mismatch");
   const int64_t C = x.size(1);
   const int64_t M = x.numel() / C;
+  TORCH_CHECK(C % 64 == 0, "pdt bn bwd: C must be a multiple of 64");
   auto dx = at::empty_like(x);
   Tensor dres;
   if (has_res) dres = at::empty_like(x);
@@ -307,17 +325,17 @@ std::vector<Tensor> bn_bwd_train(Tensor dy, Tensor x, c10::optional<Tensor> y, c
     db = at::empty({C}, fopt);
   }
   auto ws = at::empty({bn_ws_floats(M, C)}, fopt);
-  const uint16_t* yp = nullptr;
+  const uint8_t* mp = nullptr;
   if (relu) {
-    TORCH_CHECK(y.has_value() && y->defined(), "pdt bn bwd: relu needs the forward output");
-    yp = reinterpret_cast<const uint16_t*>(y->data_ptr());
+    TORCH_CHECK(mask.has_value() && mask->defined() && mask->numel() == M * C / 8, "pdt bn bwd: relu needs the mask");
+    mp = mask->data_ptr<uint8_t>();
   }
   int rc = pdt_bn_bwd_train(reinterpret_cast<const uint16_t*>(dy.data_ptr()), reinterpret_cast<const uint16_t*>(x.data_ptr()),
-                            yp, opt_fptr(weight), mean.data_ptr<float>(), invstd.data_ptr<float>(), M, (int)C, relu,
+                            mp, opt_fptr(weight), mean.data_ptr<float>(), invstd.data_ptr<float>(), M, (int)C, relu,
                             has_res, reinterpret_cast<uint16_t*>(dx.data_ptr()),
                             has_res ? reinterpret_cast<uint16_t*>(dres.data_ptr()) : nullptr,
                             need_dgamma ? dg.data_ptr<float>() : nullptr, need_dgamma ? db.data_ptr<float>() : nullptr,
-                            ws.data_ptr<float>(), stream());
+                            ws.data_ptr<float>(), bn_counters(x), stream());
   TORCH_CHECK(rc == 0, "pdt_bn_bwd_train failed");
   return {dx, dres, dg, db};
 }

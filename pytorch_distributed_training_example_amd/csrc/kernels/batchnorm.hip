@@ -3,16 +3,21 @@
 //
 // Not in the reference (LeNet has no BN, /root/reference/cnn.py:9-23); required by the
 // ResNet-50 north-star config (BASELINE.json). Activations are [M = N*H*W, C] bf16 with C
-// contiguous, so every lane moves 8 channels (16 B) per access and a wave reads whole rows.
+// contiguous.
 //
-// Forward (train):   reduce  -> per-block (Σ(x-k), Σ(x-k)²) partials, k = x[0, c] shift
-//                    finalize-> mean, invstd, running stats, per-channel (a, b)
-//                    apply   -> y = x*a + b (+ residual) (relu), bf16 out
-// Backward (train):  reduce  -> per-block (Σdz, Σdz(x-mean)), dz = dy * (y > 0)
-//                    finalize-> dgamma, dbeta and per-channel dx coefficients
-//                    apply   -> dx = A dz + B (x-mean) + D, (dres = dz)
-// Partials are summed in a fixed order (deterministic, no float atomics). The apply passes
-// use a grid-stride of a multiple of C so each lane's 8-channel coefficients are loaded once.
+// Forward (train): 2 kernels
+//   reduce+finalize : grid (row blocks, C/64 chunks); a lane owns 8 channels (one 16-B load)
+//                     of a 64-channel chunk, 32 rows per pass; per-block shifted sums
+//                     (Σ(x-k), Σ(x-k)², k = x[0,c]) go to a partial slab, and the LAST block to
+//                     arrive for a chunk (agent-scope release → relaxed ticket → agent-scope
+//                     acquire, cdna_hip_programming.md §6 G16) reduces the slab in a fixed
+//                     order (deterministic) and writes mean / invstd / running stats and the
+//                     per-channel affine (a, b) — no separate finalize launch.
+//   apply           : y = relu?(x*a + b + residual?) in bf16, plus a 1-bit ReLU mask
+//                     (1/16 of y's bytes) so backward never re-reads y.
+// Backward (train): 2 kernels, same structure
+//   reduce+finalize : Σdz, Σdz(x-mean) with dz = dy·mask → dgamma, dbeta, dx coefficients
+//   apply           : dx = A·dz + B·(x-mean) + D (and dres = dz for the residual branch)
 #include "../common.h"
 
 using namespace pdt;
@@ -20,172 +25,165 @@ using namespace pdt;
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kChunkC = 2048;  // channels per workgroup in the reduce pass (256 lanes x 8)
+constexpr int kCC = 64;   // channels per reduce workgroup
+constexpr int kL = 8;     // lanes per row (8 channels each)
+constexpr int kR = 32;    // rows per pass
 
-struct Geo {
-  int CC, L, R;  // channels in this chunk, lanes per row, rows per pass
+struct FinArgs {
+  // forward
+  const uint16_t* x;          // shift source (row 0)
+  const float* gamma;
+  const float* beta;
+  float* mean_out;
+  float* invstd_out;
+  float* a_out;
+  float* b_out;
+  float* running_mean;
+  float* running_var;
+  float momentum, eps;
+  // backward
+  const float* invstd;
+  float* dgamma;
+  float* dbeta;
+  float* A;
+  float* B;
+  float* D;
+  int64_t M;
 };
-__device__ __forceinline__ Geo geo(int C, int chunk) {
-  Geo g;
-  const int c0 = chunk * kChunkC;
-  g.CC = min(kChunkC, C - c0);
-  g.L = g.CC / 8;
-  g.R = kThreads / g.L;
-  return g;
+
+__device__ __forceinline__ void ld8_f32(const float* p, float (&v)[8]) {
+  const float4 a = *reinterpret_cast<const float4*>(p);
+  const float4 b = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
 }
 
-// MODE 0: forward stats. MODE 1: backward reduce (no relu). MODE 2: backward reduce w/ relu mask.
+// MODE 0: forward stats. MODE 1: backward, no relu. MODE 2: backward with relu mask.
+template <int MODE>
+__device__ __forceinline__ void accum_row(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
+                                          const uint8_t* __restrict__ mask, int64_t m, int C, int c,
+                                          const float (&k)[8], float (&s1)[8], float (&s2)[8]) {
+  float xv[8];
+  ld8_bf16(x + m * C + c, xv);
+  if (MODE == 0) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { const float d = xv[j] - k[j]; s1[j] += d; s2[j] += d * d; }
+  } else {
+    float g[8];
+    ld8_bf16(dy + m * C + c, g);
+    if (MODE == 2) {
+      const unsigned mb = mask[(m * C + c) >> 3];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = (mb >> j) & 1u ? g[j] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { s1[j] += g[j]; s2[j] += g[j] * (xv[j] - k[j]); }
+  }
+}
+
 template <int MODE>
 __global__ __launch_bounds__(kThreads) void bn_reduce_kernel(
-    const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy, const uint16_t* __restrict__ y,
-    const float* __restrict__ mean, int64_t M, int C, int64_t rows_per_block,
-    float* __restrict__ part) {
-  __shared__ __attribute__((aligned(16))) float sm[2][kChunkC];
-  const Geo g = geo(C, blockIdx.y);
+    const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy, const uint8_t* __restrict__ mask,
+    const float* __restrict__ mean, int64_t M, int C, int64_t rows_per_block, int nrow,
+    float* __restrict__ part, unsigned* __restrict__ counters, FinArgs fa) {
+  // ONE shared array (LDS reduction, last-arriver flag, finalize reduction)
+  __shared__ __attribute__((aligned(16))) float sm[2 * kR * kCC + 4];
   const int tid = threadIdx.x;
-  const int r = tid / g.L, l = tid % g.L;
-  const int c = blockIdx.y * kChunkC + l * 8;
-  const bool active = r < g.R;
+  const int chunk = blockIdx.y;
+  const int l = tid & (kL - 1), r = tid >> 3;
+  const int c = chunk * kCC + l * 8;
   const int64_t m0 = (int64_t)blockIdx.x * rows_per_block;
   const int64_t m1 = min(M, m0 + rows_per_block);
   float k[8], s1[8], s2[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) { s1[j] = 0.f; s2[j] = 0.f; }
-  if (active) {
-    if (MODE == 0) ld8_bf16(x + c, k);  // shift: first row of the tensor (same for all blocks)
-    else {
-      const float4 a = *reinterpret_cast<const float4*>(mean + c);
-      const float4 b = *reinterpret_cast<const float4*>(mean + c + 4);
-      k[0] = a.x; k[1] = a.y; k[2] = a.z; k[3] = a.w; k[4] = b.x; k[5] = b.y; k[6] = b.z; k[7] = b.w;
-    }
-    int64_t m = m0 + r;
-    // 2-deep unroll: two independent rows in flight per lane
-    for (; m + g.R < m1; m += 2 * g.R) {
-      float xa[8], xb[8];
-      ld8_bf16(x + m * C + c, xa);
-      ld8_bf16(x + (m + g.R) * C + c, xb);
-      if (MODE == 0) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float da = xa[j] - k[j], db = xb[j] - k[j];
-          s1[j] += da + db;
-          s2[j] += da * da + db * db;
-        }
-      } else {
-        float ga[8], gb[8];
-        ld8_bf16(dy + m * C + c, ga);
-        ld8_bf16(dy + (m + g.R) * C + c, gb);
-        if (MODE == 2) {
-          float ya[8], yb[8];
-          ld8_bf16(y + m * C + c, ya);
-          ld8_bf16(y + (m + g.R) * C + c, yb);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            ga[j] = ya[j] > 0.f ? ga[j] : 0.f;
-            gb[j] = yb[j] > 0.f ? gb[j] : 0.f;
-          }
-        }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          s1[j] += ga[j] + gb[j];
-          s2[j] += ga[j] * (xa[j] - k[j]) + gb[j] * (xb[j] - k[j]);
-        }
-      }
-    }
-    for (; m < m1; m += g.R) {
-      float xa[8];
-      ld8_bf16(x + m * C + c, xa);
-      if (MODE == 0) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) { const float d = xa[j] - k[j]; s1[j] += d; s2[j] += d * d; }
-      } else {
-        float ga[8];
-        ld8_bf16(dy + m * C + c, ga);
-        if (MODE == 2) {
-          float ya[8];
-          ld8_bf16(y + m * C + c, ya);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) ga[j] = ya[j] > 0.f ? ga[j] : 0.f;
-        }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) { s1[j] += ga[j]; s2[j] += ga[j] * (xa[j] - k[j]); }
-      }
-    }
+  if (MODE == 0) ld8_bf16(x + c, k);  // shift: first row (same for every block)
+  else ld8_f32(mean + c, k);
+  int64_t m = m0 + r;
+  for (; m + kR < m1; m += 2 * kR) {
+    accum_row<MODE>(x, dy, mask, m, C, c, k, s1, s2);
+    accum_row<MODE>(x, dy, mask, m + kR, C, c, k, s1, s2);
   }
-  // reduce the R row-groups of the block through LDS (rows of width CC)
-  const int CC = g.CC;
-  if (g.R == 1) {
-    if (active) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        part[((int64_t)blockIdx.x * 2 + 0) * C + c + j] = s1[j];
-        part[((int64_t)blockIdx.x * 2 + 1) * C + c + j] = s2[j];
-      }
-    }
-    return;
+  if (m < m1) accum_row<MODE>(x, dy, mask, m, C, c, k, s1, s2);
+
+  // reduce the 32 row-groups through LDS: sm[0][r][64] = s1, sm[1][r][64] = s2
+  float* d0 = &sm[r * kCC + l * 8];
+  float* d1 = &sm[kR * kCC + r * kCC + l * 8];
+  *reinterpret_cast<float4*>(d0) = make_float4(s1[0], s1[1], s1[2], s1[3]);
+  *reinterpret_cast<float4*>(d0 + 4) = make_float4(s1[4], s1[5], s1[6], s1[7]);
+  *reinterpret_cast<float4*>(d1) = make_float4(s2[0], s2[1], s2[2], s2[3]);
+  *reinterpret_cast<float4*>(d1 + 4) = make_float4(s2[4], s2[5], s2[6], s2[7]);
+  __syncthreads();
+  float* slab = part + ((int64_t)chunk * nrow + blockIdx.x) * (2 * kCC);
+  if (tid < 2 * kCC) {
+    const int which = tid / kCC, cl = tid % kCC;
+    const float* src = &sm[which * kR * kCC + cl];
+    float a = 0.f;
+#pragma unroll 8
+    for (int rr = 0; rr < kR; ++rr) a += src[rr * kCC];
+    slab[tid] = a;  // [0..63] = S1, [64..127] = S2
   }
-  // tree over r: sm holds R x CC partials only when R*CC <= kChunkC (always: R*L*8 <= 2048)
-  if (active) {
-    float* d0 = &sm[0][r * CC + l * 8];
-    float* d1 = &sm[1][r * CC + l * 8];
-    *reinterpret_cast<float4*>(d0) = make_float4(s1[0], s1[1], s1[2], s1[3]);
-    *reinterpret_cast<float4*>(d0 + 4) = make_float4(s1[4], s1[5], s1[6], s1[7]);
-    *reinterpret_cast<float4*>(d1) = make_float4(s2[0], s2[1], s2[2], s2[3]);
-    *reinterpret_cast<float4*>(d1 + 4) = make_float4(s2[4], s2[5], s2[6], s2[7]);
+  // publish the slab, take a ticket (G16 counter form)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned t = __hip_atomic_fetch_add(&counters[chunk], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sm[2 * kR * kCC] = (t == (unsigned)(nrow - 1)) ? 1.f : 0.f;
   }
   __syncthreads();
-  for (int cc = tid; cc < CC; cc += kThreads) {
-    float a = 0.f, b = 0.f;
-    for (int rr = 0; rr < g.R; ++rr) { a += sm[0][rr * CC + cc]; b += sm[1][rr * CC + cc]; }
-    part[((int64_t)blockIdx.x * 2 + 0) * C + blockIdx.y * kChunkC + cc] = a;
-    part[((int64_t)blockIdx.x * 2 + 1) * C + blockIdx.y * kChunkC + cc] = b;
+  if (sm[2 * kR * kCC] == 0.f) return;
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
-}
-
-// Sum nblk partials for 64 channels per workgroup (4 groups of 64 lanes, fixed order).
-__device__ __forceinline__ void sum_partials(const float* __restrict__ part, int nblk, int C, int c,
-                                             float& S1, float& S2) {
-  __shared__ float red[2][4][64];
-  const int grp = threadIdx.x / 64, ln = threadIdx.x % 64;
+  __syncthreads();
+  // last arriver: fixed-order reduction of the chunk's nrow slabs (4 groups x 64 channels)
+  const int g = tid >> 6, cl = tid & 63;
+  const float* base = part + (int64_t)chunk * nrow * (2 * kCC);
   float a = 0.f, b = 0.f;
-  if (c < C) {
-    for (int blk = grp; blk < nblk; blk += 4) {
-      a += part[((int64_t)blk * 2 + 0) * C + c];
-      b += part[((int64_t)blk * 2 + 1) * C + c];
-    }
+  for (int blk = g; blk < nrow; blk += 4) {
+    a += base[(int64_t)blk * (2 * kCC) + cl];
+    b += base[(int64_t)blk * (2 * kCC) + kCC + cl];
   }
-  red[0][grp][ln] = a;
-  red[1][grp][ln] = b;
   __syncthreads();
-  S1 = red[0][0][ln] + red[0][1][ln] + red[0][2][ln] + red[0][3][ln];
-  S2 = red[1][0][ln] + red[1][1][ln] + red[1][2][ln] + red[1][3][ln];
-}
-
-__global__ __launch_bounds__(256) void bn_fwd_finalize_kernel(
-    const float* __restrict__ part, int nblk, int C, int64_t M, const uint16_t* __restrict__ x,
-    const float* __restrict__ gamma, const float* __restrict__ beta, float* __restrict__ mean_out,
-    float* __restrict__ invstd_out, float* __restrict__ a_out, float* __restrict__ b_out,
-    float* __restrict__ running_mean, float* __restrict__ running_var, float momentum, float eps) {
-  const int c = blockIdx.x * 64 + (threadIdx.x % 64);
-  float S1, S2;
-  sum_partials(part, nblk, C, c, S1, S2);
-  if (threadIdx.x >= 64 || c >= C) return;
-  const float k = bf2f(x[c]);
-  const double inv_m = 1.0 / (double)M;
-  const double d1 = (double)S1 * inv_m;
-  double var = (double)S2 * inv_m - d1 * d1;
-  var = var < 0.0 ? 0.0 : var;
-  const float mean = (float)(k + d1);
-  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
-  mean_out[c] = mean;
-  invstd_out[c] = invstd;
-  const float gm = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
-  a_out[c] = gm * invstd;
-  b_out[c] = bt - mean * gm * invstd;
-  if (running_mean) running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mean;
-  if (running_var) {
-    const double unbiased = M > 1 ? var * (double)M / (double)(M - 1) : var;
-    running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unbiased;
+  sm[g * kCC + cl] = a;
+  sm[4 * kCC + g * kCC + cl] = b;
+  __syncthreads();
+  if (tid == 0) counters[chunk] = 0u;  // self-reset for the next launch (stream-ordered)
+  if (tid >= kCC) return;
+  const int ch = chunk * kCC + tid;
+  const float S1 = sm[tid] + sm[kCC + tid] + sm[2 * kCC + tid] + sm[3 * kCC + tid];
+  const float S2 = sm[4 * kCC + tid] + sm[5 * kCC + tid] + sm[6 * kCC + tid] + sm[7 * kCC + tid];
+  const int64_t Mt = fa.M;
+  if (MODE == 0) {
+    const float kk = bf2f(fa.x[ch]);
+    const double inv_m = 1.0 / (double)Mt;
+    const double d1 = (double)S1 * inv_m;
+    double var = (double)S2 * inv_m - d1 * d1;
+    var = var < 0.0 ? 0.0 : var;
+    const float mu = (float)(kk + d1);
+    const float is = (float)(1.0 / sqrt(var + (double)fa.eps));
+    fa.mean_out[ch] = mu;
+    fa.invstd_out[ch] = is;
+    const float gm = fa.gamma ? fa.gamma[ch] : 1.f, bt = fa.beta ? fa.beta[ch] : 0.f;
+    fa.a_out[ch] = gm * is;
+    fa.b_out[ch] = bt - mu * gm * is;
+    if (fa.running_mean) fa.running_mean[ch] = (1.f - fa.momentum) * fa.running_mean[ch] + fa.momentum * mu;
+    if (fa.running_var) {
+      const double unb = Mt > 1 ? var * (double)Mt / (double)(Mt - 1) : var;
+      fa.running_var[ch] = (1.f - fa.momentum) * fa.running_var[ch] + fa.momentum * (float)unb;
+    }
+  } else {
+    const float is = fa.invstd[ch];
+    const float gm = fa.gamma ? fa.gamma[ch] : 1.f;
+    const float db = S1, dg = S2 * is;
+    if (fa.dgamma) fa.dgamma[ch] = dg;
+    if (fa.dbeta) fa.dbeta[ch] = db;
+    const float inv_m = 1.f / (float)Mt;
+    fa.A[ch] = gm * is;
+    fa.B[ch] = -gm * is * is * dg * inv_m;
+    fa.D[ch] = -gm * is * db * inv_m;
   }
 }
 
@@ -200,35 +198,11 @@ __global__ void bn_eval_coef_kernel(int C, const float* __restrict__ gamma, cons
   b_out[c] = bt - rm[c] * gm * invstd;
 }
 
-__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(
-    const float* __restrict__ part, int nblk, int C, int64_t M, const float* __restrict__ gamma,
-    const float* __restrict__ invstd, float* __restrict__ dgamma, float* __restrict__ dbeta,
-    float* __restrict__ A, float* __restrict__ B, float* __restrict__ D) {
-  const int c = blockIdx.x * 64 + (threadIdx.x % 64);
-  float S1, S2;
-  sum_partials(part, nblk, C, c, S1, S2);
-  if (threadIdx.x >= 64 || c >= C) return;
-  const float is = invstd[c];
-  const float gm = gamma ? gamma[c] : 1.f;
-  const float db = S1, dg = S2 * is;
-  if (dgamma) dgamma[c] = dg;
-  if (dbeta) dbeta[c] = db;
-  const float inv_m = 1.f / (float)M;
-  A[c] = gm * is;
-  B[c] = -gm * is * is * dg * inv_m;
-  D[c] = -gm * is * db * inv_m;
-}
-
-__device__ __forceinline__ void ld8_f32(const float* p, float (&v)[8]) {
-  const float4 a = *reinterpret_cast<const float4*>(p);
-  const float4 b = *reinterpret_cast<const float4*>(p + 4);
-  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-}
-
-template <bool RELU, bool RES>
+template <bool RELU, bool RES, bool MASK>
 __global__ __launch_bounds__(256) void bn_apply_kernel(
     const uint16_t* __restrict__ x, const uint16_t* __restrict__ res, const float* __restrict__ a,
-    const float* __restrict__ b, uint16_t* __restrict__ y, int64_t nvec, int C, int fixed) {
+    const float* __restrict__ b, uint16_t* __restrict__ y, uint8_t* __restrict__ mask, int64_t nvec, int C,
+    int fixed) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   float av[8], bv[8];
@@ -247,23 +221,28 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(
     ld8_bf16(x + i * 8, v);
     float rv[8];
     if (RES) ld8_bf16(res + i * 8, rv);
+    unsigned mb = 0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float t = v[j] * av[j] + bv[j];
       if (RES) t += rv[j];
-      if (RELU) t = t > 0.f ? t : 0.f;
+      if (RELU) {
+        mb |= (t > 0.f ? 1u : 0u) << j;
+        t = t > 0.f ? t : 0.f;
+      }
       v[j] = t;
     }
     st8_bf16(y + i * 8, v);
+    if (MASK) mask[i] = (uint8_t)mb;
   }
 }
 
 template <bool RELU, bool RES>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
-    const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x, const uint16_t* __restrict__ y,
+    const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x, const uint8_t* __restrict__ mask,
     const float* __restrict__ mean, const float* __restrict__ A, const float* __restrict__ B,
-    const float* __restrict__ D, uint16_t* __restrict__ dx, uint16_t* __restrict__ dres, int64_t nvec,
-    int C, int fixed) {
+    const float* __restrict__ D, uint16_t* __restrict__ dx, uint16_t* __restrict__ dres, int64_t nvec, int C,
+    int fixed) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   float mv[8], av[8], bv[8], dv[8];
@@ -281,10 +260,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     ld8_bf16(dy + i * 8, g);
     ld8_bf16(x + i * 8, xv);
     if (RELU) {
-      float yv[8];
-      ld8_bf16(y + i * 8, yv);
+      const unsigned mb = mask[i];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) g[j] = yv[j] > 0.f ? g[j] : 0.f;
+      for (int j = 0; j < 8; ++j) g[j] = (mb >> j) & 1u ? g[j] : 0.f;
     }
     if (RES) st8_bf16(dres + i * 8, g);
     float o[8];
@@ -294,17 +272,23 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
   }
 }
 
-inline int num_reduce_blocks(int64_t M, int C, int64_t& rows_per_block) {
-  const int CC = C < kChunkC ? C : kChunkC;
-  const int R = kThreads / (CC / 8);
-  const int nchunks = (C + kChunkC - 1) / kChunkC;
-  int64_t nblk = (M + (int64_t)R * 8 - 1) / ((int64_t)R * 8);  // >= 8 row-passes per lane
-  const int64_t cap = 512 / nchunks > 0 ? 512 / nchunks : 1;
-  if (nblk > cap) nblk = cap;
-  if (nblk < 1) nblk = 1;
-  rows_per_block = (M + nblk - 1) / nblk;
-  nblk = (M + rows_per_block - 1) / rows_per_block;
-  return (int)nblk;
+struct ReduceGeo {
+  int nrow, nchunks;
+  int64_t rows_per_block;
+};
+
+inline ReduceGeo reduce_geo(int64_t M, int C) {
+  ReduceGeo g;
+  g.nchunks = C / kCC;
+  int64_t nrow = 1024 / g.nchunks;
+  if (nrow > 512) nrow = 512;
+  if (nrow < 4) nrow = 4;
+  const int64_t max_rows = (M + 2 * kR - 1) / (2 * kR);  // >= 2 passes per block
+  if (nrow > max_rows) nrow = max_rows;
+  if (nrow < 1) nrow = 1;
+  g.rows_per_block = (M + nrow - 1) / nrow;
+  g.nrow = (int)((M + g.rows_per_block - 1) / g.rows_per_block);
+  return g;
 }
 
 inline int apply_grid(int64_t nvec) {
@@ -317,90 +301,92 @@ inline int apply_grid(int64_t nvec) {
 
 extern "C" {
 
-// Workspace size (floats) for the partial sums of a reduce pass.
+// Workspace floats needed by a train fwd/bwd call (partial slabs + per-channel coefficients).
 int64_t pdt_bn_workspace_floats(int64_t M, int C) {
-  int64_t rpb;
-  const int nblk = num_reduce_blocks(M, C, rpb);
-  return (int64_t)nblk * 2 * C;
+  const ReduceGeo g = reduce_geo(M, C);
+  return (int64_t)g.nchunks * g.nrow * 2 * kCC + 4 * (int64_t)C;
 }
 
-// Training forward. Outputs: y (bf16), mean/invstd (f32 [C]); updates running stats.
-// ws: >= pdt_bn_workspace_floats(M,C) + 2*C floats.
+// Training forward. Outputs: y (bf16), mask (uint8, M*C/8, when relu), mean/invstd (f32 [C]);
+// updates running stats. counters: >= C/64 zeroed uint32 (self-resetting).
 int pdt_bn_fwd_train(const uint16_t* x, const uint16_t* res, const float* gamma, const float* beta,
-                     float* running_mean, float* running_var, float momentum, float eps, int64_t M,
-                     int C, int relu, uint16_t* y, float* mean, float* invstd, float* ws,
-                     hipStream_t s) {
-  if (C % 8 != 0) return -1;
-  int64_t rpb;
-  const int nblk = num_reduce_blocks(M, C, rpb);
-  const int nchunks = (C + kChunkC - 1) / kChunkC;
+                     float* running_mean, float* running_var, float momentum, float eps, int64_t M, int C,
+                     int relu, uint16_t* y, uint8_t* mask, float* mean, float* invstd, float* ws,
+                     unsigned* counters, hipStream_t s) {
+  if (C % kCC != 0 || M < 1) return -1;
+  const ReduceGeo g = reduce_geo(M, C);
   float* part = ws;
-  float* a = ws + (int64_t)nblk * 2 * C;
+  float* a = ws + (int64_t)g.nchunks * g.nrow * 2 * kCC;
   float* b = a + C;
-  hipLaunchKernelGGL(bn_reduce_kernel<0>, dim3(nblk, nchunks), dim3(kThreads), 0, s, x, nullptr, nullptr,
-                     nullptr, M, C, rpb, part);
-  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, s, part, nblk, C, M, x,
-                     gamma, beta, mean, invstd, a, b, running_mean, running_var, momentum, eps);
+  FinArgs fa{};
+  fa.x = x; fa.gamma = gamma; fa.beta = beta; fa.mean_out = mean; fa.invstd_out = invstd; fa.a_out = a;
+  fa.b_out = b; fa.running_mean = running_mean; fa.running_var = running_var; fa.momentum = momentum;
+  fa.eps = eps; fa.M = M;
+  hipLaunchKernelGGL(bn_reduce_kernel<0>, dim3(g.nrow, g.nchunks), dim3(kThreads), 0, s, x, nullptr, nullptr,
+                     nullptr, M, C, g.rows_per_block, g.nrow, part, counters, fa);
   const int64_t nvec = M * C / 8;
   const int fixed = (2048 % C) == 0;
   const int grid = apply_grid(nvec);
-#define PDT_APPLY(RL, RS) \
-  hipLaunchKernelGGL((bn_apply_kernel<RL, RS>), dim3(grid), dim3(256), 0, s, x, res, a, b, y, nvec, C, fixed)
-  if (relu && res) PDT_APPLY(true, true);
-  else if (relu) PDT_APPLY(true, false);
-  else if (res) PDT_APPLY(false, true);
-  else PDT_APPLY(false, false);
+#define PDT_APPLY(RL, RS, MK)                                                                                 \
+  hipLaunchKernelGGL((bn_apply_kernel<RL, RS, MK>), dim3(grid), dim3(256), 0, s, x, res, a, b, y, mask, nvec, \
+                     C, fixed)
+  const bool mk = mask != nullptr;
+  if (relu && res) { if (mk) PDT_APPLY(true, true, true); else PDT_APPLY(true, true, false); }
+  else if (relu) { if (mk) PDT_APPLY(true, false, true); else PDT_APPLY(true, false, false); }
+  else if (res) PDT_APPLY(false, true, false);
+  else PDT_APPLY(false, false, false);
   return 0;
 }
 
 // Eval forward with running statistics. ws: >= 2*C floats.
 int pdt_bn_fwd_eval(const uint16_t* x, const uint16_t* res, const float* gamma, const float* beta,
-                    const float* running_mean, const float* running_var, float eps, int64_t M, int C,
-                    int relu, uint16_t* y, float* ws, hipStream_t s) {
+                    const float* running_mean, const float* running_var, float eps, int64_t M, int C, int relu,
+                    uint16_t* y, float* ws, hipStream_t s) {
   if (C % 8 != 0) return -1;
   float* a = ws;
   float* b = ws + C;
-  hipLaunchKernelGGL(bn_eval_coef_kernel, dim3((C + 255) / 256), dim3(256), 0, s, C, gamma, beta,
-                     running_mean, running_var, eps, a, b);
+  uint8_t* mask = nullptr;
+  hipLaunchKernelGGL(bn_eval_coef_kernel, dim3((C + 255) / 256), dim3(256), 0, s, C, gamma, beta, running_mean,
+                     running_var, eps, a, b);
   const int64_t nvec = M * C / 8;
   const int fixed = (2048 % C) == 0;
   const int grid = apply_grid(nvec);
-  if (relu && res) PDT_APPLY(true, true);
-  else if (relu) PDT_APPLY(true, false);
-  else if (res) PDT_APPLY(false, true);
-  else PDT_APPLY(false, false);
+  if (relu && res) PDT_APPLY(true, true, false);
+  else if (relu) PDT_APPLY(true, false, false);
+  else if (res) PDT_APPLY(false, true, false);
+  else PDT_APPLY(false, false, false);
 #undef PDT_APPLY
   return 0;
 }
 
-// Training backward. y is the forward OUTPUT (used for the relu mask when relu != 0).
+// Training backward. mask: the forward's relu bit-mask (required when relu != 0).
 // Outputs dx (bf16), dres (bf16, when has_res), dgamma/dbeta (f32 [C]).
-// ws: >= pdt_bn_workspace_floats(M,C) + 3*C floats.
-int pdt_bn_bwd_train(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* gamma,
+int pdt_bn_bwd_train(const uint16_t* dy, const uint16_t* x, const uint8_t* mask, const float* gamma,
                      const float* mean, const float* invstd, int64_t M, int C, int relu, int has_res,
-                     uint16_t* dx, uint16_t* dres, float* dgamma, float* dbeta, float* ws, hipStream_t s) {
-  if (C % 8 != 0) return -1;
-  int64_t rpb;
-  const int nblk = num_reduce_blocks(M, C, rpb);
-  const int nchunks = (C + kChunkC - 1) / kChunkC;
+                     uint16_t* dx, uint16_t* dres, float* dgamma, float* dbeta, float* ws, unsigned* counters,
+                     hipStream_t s) {
+  if (C % kCC != 0 || M < 1) return -1;
+  if (relu && !mask) return -2;
+  const ReduceGeo g = reduce_geo(M, C);
   float* part = ws;
-  float* A = ws + (int64_t)nblk * 2 * C;
+  float* A = ws + (int64_t)g.nchunks * g.nrow * 2 * kCC;
   float* B = A + C;
   float* D = B + C;
+  FinArgs fa{};
+  fa.gamma = gamma; fa.invstd = invstd; fa.dgamma = dgamma; fa.dbeta = dbeta; fa.A = A; fa.B = B; fa.D = D;
+  fa.M = M;
   if (relu)
-    hipLaunchKernelGGL(bn_reduce_kernel<2>, dim3(nblk, nchunks), dim3(kThreads), 0, s, x, dy, y, mean, M, C,
-                       rpb, part);
+    hipLaunchKernelGGL(bn_reduce_kernel<2>, dim3(g.nrow, g.nchunks), dim3(kThreads), 0, s, x, dy, mask, mean, M, C,
+                       g.rows_per_block, g.nrow, part, counters, fa);
   else
-    hipLaunchKernelGGL(bn_reduce_kernel<1>, dim3(nblk, nchunks), dim3(kThreads), 0, s, x, dy, y, mean, M, C,
-                       rpb, part);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, s, part, nblk, C, M, gamma,
-                     invstd, dgamma, dbeta, A, B, D);
+    hipLaunchKernelGGL(bn_reduce_kernel<1>, dim3(g.nrow, g.nchunks), dim3(kThreads), 0, s, x, dy, mask, mean, M, C,
+                       g.rows_per_block, g.nrow, part, counters, fa);
   const int64_t nvec = M * C / 8;
   const int fixed = (2048 % C) == 0;
   const int grid = apply_grid(nvec);
-#define PDT_BAPPLY(RL, RS)                                                                             \
-  hipLaunchKernelGGL((bn_bwd_apply_kernel<RL, RS>), dim3(grid), dim3(256), 0, s, dy, x, y, mean, A, B, D, \
-                     dx, dres, nvec, C, fixed)
+#define PDT_BAPPLY(RL, RS)                                                                                      \
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<RL, RS>), dim3(grid), dim3(256), 0, s, dy, x, mask, mean, A, B, D, dx, \
+                     dres, nvec, C, fixed)
   if (relu && has_res) PDT_BAPPLY(true, true);
   else if (relu) PDT_BAPPLY(true, false);
   else if (has_res) PDT_BAPPLY(false, true);

@@ -33,23 +33,43 @@ class _Downsample(nn.Sequential):
     """conv1x1 + BN (no ReLU); indices 0/1 as in torchvision."""
 
 
+_NORM = {"pdt": BatchNorm2d, "torch": nn.BatchNorm2d}
+_norm_kind = ["pdt"]
+
+
+def _bn(c: int, fused_relu: bool = False) -> nn.Module:
+    if _norm_kind[0] == "pdt":
+        return BatchNorm2d(c, fused_relu=fused_relu)
+    return nn.BatchNorm2d(c)
+
+
+def bn_act(bn: nn.Module, x, residual=None, relu: bool = False):
+    """relu?(bn(x) + residual?) — one fused kernel for our BN, three ops for torch's."""
+    if isinstance(bn, BatchNorm2d):
+        return bn(x, residual=residual, relu=relu)
+    y = bn(x)
+    if residual is not None:
+        y = y + residual
+    return torch.relu(y) if relu else y
+
+
 class BasicBlock(nn.Module):
     expansion = 1
 
     def __init__(self, inplanes, planes, stride=1, downsample=None, groups=1, base_width=64, dilation=1):
         super().__init__()
         self.conv1 = conv3x3(inplanes, planes, stride)
-        self.bn1 = BatchNorm2d(planes, fused_relu=True)
+        self.bn1 = _bn(planes, fused_relu=True)
         self.relu = nn.ReLU(inplace=True)
         self.conv2 = conv3x3(planes, planes)
-        self.bn2 = BatchNorm2d(planes)
+        self.bn2 = _bn(planes)
         self.downsample = downsample
         self.stride = stride
 
     def forward(self, x):
         identity = x if self.downsample is None else self.downsample(x)
-        out = self.bn1(self.conv1(x))
-        return self.bn2(self.conv2(out), residual=identity, relu=True)
+        out = bn_act(self.bn1, self.conv1(x), relu=True)
+        return bn_act(self.bn2, self.conv2(out), residual=identity, relu=True)
 
 
 class Bottleneck(nn.Module):
@@ -59,32 +79,34 @@ class Bottleneck(nn.Module):
         super().__init__()
         width = int(planes * (base_width / 64.0)) * groups
         self.conv1 = conv1x1(inplanes, width)
-        self.bn1 = BatchNorm2d(width, fused_relu=True)
+        self.bn1 = _bn(width, fused_relu=True)
         self.conv2 = conv3x3(width, width, stride, groups, dilation)
-        self.bn2 = BatchNorm2d(width, fused_relu=True)
+        self.bn2 = _bn(width, fused_relu=True)
         self.conv3 = conv1x1(width, planes * self.expansion)
-        self.bn3 = BatchNorm2d(planes * self.expansion)
+        self.bn3 = _bn(planes * self.expansion)
         self.relu = nn.ReLU(inplace=True)
         self.downsample = downsample
         self.stride = stride
 
     def forward(self, x):
         identity = x if self.downsample is None else self.downsample(x)
-        out = self.bn1(self.conv1(x))
-        out = self.bn2(self.conv2(out))
-        return self.bn3(self.conv3(out), residual=identity, relu=True)
+        out = bn_act(self.bn1, self.conv1(x), relu=True)
+        out = bn_act(self.bn2, self.conv2(out), relu=True)
+        return bn_act(self.bn3, self.conv3(out), residual=identity, relu=True)
 
 
 class ResNet(nn.Module):
     def __init__(self, block: Type[nn.Module], layers: List[int], num_classes: int = 1000,
-                 zero_init_residual: bool = False, groups: int = 1, width_per_group: int = 64):
+                 zero_init_residual: bool = False, groups: int = 1, width_per_group: int = 64,
+                 norm: str = "pdt"):
         super().__init__()
+        _norm_kind[0] = norm
         self.inplanes = 64
         self.dilation = 1
         self.groups = groups
         self.base_width = width_per_group
         self.conv1 = nn.Conv2d(3, self.inplanes, kernel_size=7, stride=2, padding=3, bias=False)
-        self.bn1 = BatchNorm2d(self.inplanes, fused_relu=True)
+        self.bn1 = _bn(self.inplanes, fused_relu=True)
         self.relu = nn.ReLU(inplace=True)
         self.maxpool = nn.MaxPool2d(kernel_size=3, stride=2, padding=1)
         self.layer1 = self._make_layer(block, 64, layers[0])
@@ -99,6 +121,7 @@ class ResNet(nn.Module):
             elif isinstance(m, nn.BatchNorm2d):
                 nn.init.constant_(m.weight, 1)
                 nn.init.constant_(m.bias, 0)
+        _norm_kind[0] = "pdt"
         if zero_init_residual:
             for m in self.modules():
                 if isinstance(m, Bottleneck):
@@ -110,7 +133,7 @@ class ResNet(nn.Module):
         downsample = None
         if stride != 1 or self.inplanes != planes * block.expansion:
             downsample = _Downsample(conv1x1(self.inplanes, planes * block.expansion, stride),
-                                     BatchNorm2d(planes * block.expansion))
+                                     _bn(planes * block.expansion))
         layers = [block(self.inplanes, planes, stride, downsample, self.groups, self.base_width)]
         self.inplanes = planes * block.expansion
         for _ in range(1, blocks):
@@ -118,7 +141,7 @@ class ResNet(nn.Module):
         return nn.Sequential(*layers)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        x = self.bn1(self.conv1(x))
+        x = bn_act(self.bn1, self.conv1(x), relu=True)
         x = self.maxpool(x)
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         x = self.avgpool(x)

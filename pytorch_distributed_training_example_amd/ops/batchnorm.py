@@ -35,21 +35,22 @@ class _BNTrainFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, residual, weight, bias, running_mean, running_var, momentum, eps, relu):
         C = native()
-        y, mean, invstd = C.bn_fwd_train(x, residual, weight, bias, running_mean, running_var,
-                                         momentum, eps, relu)
+        y, mask, mean, invstd = C.bn_fwd_train(x, residual, weight, bias, running_mean, running_var,
+                                               momentum, eps, relu)
         ctx.relu = relu
         ctx.has_res = residual is not None
         ctx.has_weight = weight is not None
-        ctx.save_for_backward(x, y if relu else None, weight, mean, invstd)
+        # backward needs the BN input and a 1-bit ReLU mask, never the output y
+        ctx.save_for_backward(x, mask if relu else None, weight, mean, invstd)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, y, weight, mean, invstd = ctx.saved_tensors
+        x, mask, weight, mean, invstd = ctx.saved_tensors
         fmt = torch.channels_last if x.dim() == 4 else torch.contiguous_format
         dy = dy.contiguous(memory_format=fmt)
         need_w = ctx.has_weight and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3])
-        dx, dres, dg, db = native().bn_bwd_train(dy, x, y, weight, mean, invstd, ctx.relu,
+        dx, dres, dg, db = native().bn_bwd_train(dy, x, mask, weight, mean, invstd, ctx.relu,
                                                  ctx.has_res, need_w)
         return (dx, dres if ctx.has_res else None, dg if need_w else None, db if need_w else None,
                 None, None, None, None, None)
@@ -78,7 +79,7 @@ def batch_norm_act(x, residual, weight, bias, running_mean, running_var, trainin
     """Functional fused BN(+add)(+ReLU). Native when x is a channels_last bf16 GPU tensor."""
     nhwc = x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last) or \
         (x.dim() == 2 and x.is_contiguous())
-    if (use_native(x) and x.dtype == torch.bfloat16 and nhwc and x.shape[1] % 8 == 0
+    if (use_native(x) and x.dtype == torch.bfloat16 and nhwc and x.shape[1] % 64 == 0
             and (residual is None or (residual.shape == x.shape and residual.dtype == x.dtype))):
         if residual is not None:
             residual = residual.contiguous(memory_format=torch.channels_last if x.dim() == 4

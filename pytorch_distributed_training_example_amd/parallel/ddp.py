@@ -35,6 +35,7 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
+from ..ops import multi_tensor
 from .buckets import (DEFAULT_BUCKET_CAP_MB, DEFAULT_FIRST_BUCKET_BYTES, BucketSpec,
                       compute_bucket_assignment)
 
@@ -106,6 +107,10 @@ class _Bucket:
         self.launched = False
         self.work: Any = None
         self.future: Any = None
+        self.zero_slots: List[int] = []
+        self.copy_src: List[torch.Tensor] = []
+        self.copy_dst: List[torch.Tensor] = []
+        self.copy_params: List[nn.Parameter] = []
 
     def reset(self) -> None:
         self.pending = len(self.params)
@@ -258,8 +263,12 @@ class DistributedDataParallel(nn.Module):
             self._on_grad_ready(index, param)
         return hook
 
+    def _active(self) -> bool:
+        """Buckets/collectives are only needed with >1 rank or a comm hook."""
+        return self.world_size > 1 or self._comm_hook is not None
+
     def _on_grad_ready(self, index: int, param: torch.Tensor) -> None:
-        if not self.require_backward_grad_sync:
+        if not self.require_backward_grad_sync or not self._active():
             return
         if not self._callback_queued:
             self._callback_queued = True
@@ -270,14 +279,16 @@ class DistributedDataParallel(nn.Module):
         bucket = self._buckets[b]
         if bucket.arrived[j]:
             return
-        view = bucket.views[j]
         g = param.grad
+        view = bucket.views[j]
         if g is None:
-            view.zero_()
+            bucket.zero_slots.append(j)
         elif g.data_ptr() != view.data_ptr():
-            view.copy_(g)
-        if self.gradient_as_bucket_view:
-            param.grad = view
+            # autograd stole a fresh gradient tensor: pack it into the bucket together with the
+            # bucket's other stolen grads in ONE multi-tensor copy at launch time
+            bucket.copy_src.append(g)
+            bucket.copy_dst.append(view)
+            bucket.copy_params.append(param)
         bucket.arrived[j] = True
         bucket.pending -= 1
         self._launch_ready_buckets()
@@ -287,12 +298,23 @@ class DistributedDataParallel(nn.Module):
             self._launch(self._buckets[self._next_bucket])
             self._next_bucket += 1
 
+    def _pack(self, bucket: _Bucket) -> None:
+        for j in bucket.zero_slots:
+            bucket.views[j].zero_()
+            if self.gradient_as_bucket_view:
+                bucket.params[j].grad = bucket.views[j]
+        if bucket.copy_src:
+            multi_tensor.copy_(bucket.copy_src, bucket.copy_dst)
+            if self.gradient_as_bucket_view:
+                for p, v in zip(bucket.copy_params, bucket.copy_dst):
+                    p.grad = v
+        bucket.zero_slots, bucket.copy_src, bucket.copy_dst, bucket.copy_params = [], [], [], []
+
     def _launch(self, bucket: _Bucket) -> None:
         bucket.launched = True
-        if self.world_size <= 1 and self._comm_hook is None:
-            return
+        self._pack(bucket)
         if bucket.comm_buffer is not bucket.buffer:
-            bucket.comm_buffer.copy_(bucket.buffer)
+            multi_tensor.copy_([bucket.buffer], [bucket.comm_buffer])
         if self._comm_hook is not None:
             gb = GradBucket(bucket.index, bucket.comm_buffer, bucket.params, bucket.views,
                             bucket.index == len(self._buckets) - 1)
@@ -308,10 +330,7 @@ class DistributedDataParallel(nn.Module):
             if bucket.pending > 0:
                 for j, arrived in enumerate(bucket.arrived):
                     if not arrived:
-                        bucket.views[j].zero_()
-                        p = bucket.params[j]
-                        if self.gradient_as_bucket_view:
-                            p.grad = bucket.views[j]
+                        bucket.zero_slots.append(j)
                         bucket.arrived[j] = True
                 bucket.pending = 0
         self._launch_ready_buckets()
@@ -327,7 +346,7 @@ class DistributedDataParallel(nn.Module):
                 if self._needs_div:
                     bucket.comm_buffer.div_(self.world_size)
                 if bucket.comm_buffer is not bucket.buffer:
-                    bucket.buffer.copy_(bucket.comm_buffer)
+                    multi_tensor.copy_([bucket.comm_buffer], [bucket.buffer])
             if not self.gradient_as_bucket_view:
                 for p, v in zip(bucket.params, bucket.views):
                     if p.grad is None:
@@ -377,6 +396,15 @@ class DistributedDataParallel(nn.Module):
             raise RuntimeError("register_comm_hook can only be called once")
         self._comm_hook_state = state
         self._comm_hook = hook
+
+    def zero_grad(self, set_to_none: bool = True) -> None:
+        """set_to_none (default): autograd then steals fresh gradients and the reducer packs
+        them with one multi-tensor copy per bucket — cheaper than zeroing + accumulating."""
+        if set_to_none:
+            for p in self._params:
+                p.grad = None
+        else:
+            self.zero_grad_buckets()
 
     def zero_grad_buckets(self) -> None:
         """Zero all flat gradient buckets with one memset each (keeps grads as views)."""

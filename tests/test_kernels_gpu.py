@@ -14,7 +14,7 @@ def _native():
 
 
 # ----------------------------------------------------------------------------- BatchNorm NHWC
-@pytest.mark.parametrize("C", [64, 256, 2048, 4096, 24])
+@pytest.mark.parametrize("C", [64, 256, 2048, 4096, 192])
 @pytest.mark.parametrize("relu,res", [(False, False), (True, False), (True, True), (False, True)])
 def test_batchnorm_train_fwd_bwd(C, relu, res):
     from pytorch_distributed_training_example_amd.ops.batchnorm import batch_norm_act

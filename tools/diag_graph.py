@@ -1,0 +1,66 @@
+"""Diagnose eager-vs-hipGraph gradient mismatches (lr=0): per-parameter relative error."""
+import copy
+import sys
+
+import torch
+
+sys.path.insert(0, ".")
+from pytorch_distributed_training_example_amd.engine.graph import StaticStep  # noqa: E402
+from pytorch_distributed_training_example_amd.models import get_model  # noqa: E402
+from pytorch_distributed_training_example_amd.models.precision import to_bf16_mixed  # noqa: E402
+from pytorch_distributed_training_example_amd.ops.cross_entropy import cross_entropy  # noqa: E402
+from pytorch_distributed_training_example_amd.optim import FusedSGD  # noqa: E402
+from pytorch_distributed_training_example_amd.parallel import DistributedDataParallel  # noqa: E402
+
+
+def run(base, mode, xs, ys):
+    m = copy.deepcopy(base)
+    ddp = DistributedDataParallel(m)
+    opt = FusedSGD(m.parameters(), lr=0.0, momentum=0.9)
+
+    def step(x, y):
+        opt.zero_grad(set_to_none=True)
+        loss = cross_entropy(ddp(x), y)
+        loss.backward()
+        opt.step()
+        return loss.detach()
+    if mode == "eager":
+        for _ in range(3):
+            step(xs[0], ys[0])
+        for x, y in zip(xs[1:], ys[1:]):
+            step(x, y)
+    else:
+        r = StaticStep(step, [xs[0], ys[0]], warmup=3)
+        r.capture()
+        for x, y in zip(xs[1:], ys[1:]):
+            r(x, y)
+    torch.cuda.synchronize()
+    return {n: p.grad.detach().float().clone() for n, p in m.named_parameters()}
+
+
+def main():
+    for det in (False, True):
+        for bench in (False, True):
+            for norm in ("pdt", "torch"):
+                torch.backends.cudnn.deterministic = det
+                torch.backends.cudnn.benchmark = bench
+                torch.manual_seed(0)
+                base = to_bf16_mixed(get_model("resnet18", num_classes=16, norm=norm).cuda()
+                                     .to(memory_format=torch.channels_last))
+                g = torch.Generator(device="cuda").manual_seed(3)
+                xs = [torch.randn(8, 3, 64, 64, device="cuda", generator=g).bfloat16()
+                      .contiguous(memory_format=torch.channels_last) for _ in range(4)]
+                ys = [torch.randint(0, 16, (8,), device="cuda", generator=g) for _ in range(4)]
+                ge = run(base, "eager", xs, ys)
+                gg = run(base, "graph", xs, ys)
+                bad = []
+                for n in ge:
+                    err = ((gg[n] - ge[n]).norm() / (ge[n].norm() + 1e-12)).item()
+                    if err > 1e-2:
+                        bad.append(f"{n}:{err:.2f}")
+                print(f"deterministic={det} benchmark={bench} norm={norm}: {len(bad)}/{len(ge)} bad  {bad[:12]}",
+                      flush=True)
+
+
+if __name__ == "__main__":
+    main()
