@@ -7,19 +7,23 @@ publishes no number, so ``vs_baseline`` is null.
   python bench.py --gpus N --steps K --warmup W            # N=1: plain process
   torchrun --nproc-per-node N ... bench.py --gpus N ...    # N>1: one rank per GPU (RCCL)
 
-Each step is a full training step on synthetic 224x224 ImageNet-shaped batches with
-random-init ResNet-50 weights: forward, loss, backward, bucketed RCCL all-reduce
-overlapped with backward, fused SGD update. W warm-up steps are untimed; exactly K steps
-are timed between barrier + device synchronize on both sides; the reported time is the MAX
-over ranks; ``value`` is total images/sec over all N GPUs (weak scaling: per-GPU batch fixed).
+Each step is a full training step on synthetic data with random-init weights: forward, loss,
+backward, bucketed RCCL all-reduce overlapped with backward, fused optimizer update. W
+warm-up steps are untimed; exactly K steps are timed between barrier + device synchronize on
+both sides; the reported time is the MAX over ranks; ``value`` is the total over all N GPUs
+(weak scaling: per-GPU batch fixed).
 
---impl ours       : this framework (DDP reducer, HIP BN/CE/SGD kernels, bf16 + fp32 master, hipGraph)
---impl torch_ddp  : stock torch.nn.parallel.DistributedDataParallel + autocast bf16 + torch SGD (B0)
---impl reference  : the reference algorithm — per-parameter all-reduce after backward (B1)
+--model resnet50 (default, headline) | vit_b16 | gpt2_medium (other north-star configs)
+--impl ours       : this framework (DDP reducer, HIP BN/LN/GELU/CE/optimizer kernels, bf16 params +
+                    fp32 master weights)
+--impl torch_ddp  : stock torch.nn.parallel.DistributedDataParallel + autocast bf16 + stock
+                    nn modules + torch optimizer (baseline B0)
+--impl reference  : the reference's algorithm — per-parameter all-reduce after backward (B1)
 """
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import os
 import sys
@@ -33,7 +37,12 @@ sys.path.insert(0, ROOT)
 
 from pytorch_distributed_training_example_amd.parallel import launcher  # noqa: E402
 
-METRIC = "images/sec (whole node) ResNet-50 DDP"
+WORKLOADS = {
+    # name: (metric, unit, default per-GPU batch, optimizer)
+    "resnet50": ("images/sec (whole node) ResNet-50 DDP", "images/sec", 256, "sgd"),
+    "vit_b16": ("images/sec (whole node) ViT-B/16 DDP", "images/sec", 128, "adamw"),
+    "gpt2_medium": ("tokens/sec (whole node) GPT-2-medium DDP", "tokens/sec", 8, "adamw"),
+}
 
 
 def parse(argv=None):
@@ -41,18 +50,29 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--model", default="resnet50")
-    ap.add_argument("--batch-size", type=int, default=256, help="per-GPU batch")
+    ap.add_argument("--model", default="resnet50", choices=sorted(WORKLOADS))
+    ap.add_argument("--batch-size", type=int, default=None, help="per-GPU batch (default per model)")
+    ap.add_argument("--grad-accum", type=int, default=1, help="micro-batches per step (no_sync)")
     ap.add_argument("--image-size", type=int, default=224)
+    ap.add_argument("--seq-len", type=int, default=1024)
     ap.add_argument("--impl", default="ours", choices=["ours", "torch_ddp", "reference"])
-    ap.add_argument("--graph", type=int, default=1, help="hipGraph-capture the step (ours)")
+    ap.add_argument("--graph", type=int, default=0,
+                    help="hipGraph-capture the step (ours; needs deterministic MIOpen solvers)")
     ap.add_argument("--bucket-cap-mb", type=float, default=25.0)
     ap.add_argument("--precision", default="bf16", choices=["bf16", "amp_bf16", "fp32"])
-    ap.add_argument("--lr", type=float, default=0.1)
+    ap.add_argument("--lr", type=float, default=None)
     ap.add_argument("--cudnn-benchmark", type=int, default=1, help="MIOpen find mode for conv algorithms")
     ap.add_argument("--deterministic", type=int, default=-1, help="-1: on iff hipGraph capture")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args(argv)
+
+
+def _to_stock_modules(model):
+    """Baseline: our LayerNorm subclasses run torch's own LayerNorm kernels."""
+    from pytorch_distributed_training_example_amd.ops import layernorm as ln
+    for m in model.modules():
+        if isinstance(m, ln.LayerNorm):
+            m.forward = torch.nn.LayerNorm.forward.__get__(m)
 
 
 def build(args, ctx):
@@ -60,27 +80,37 @@ def build(args, ctx):
     from pytorch_distributed_training_example_amd.models.precision import apply_precision
     dev = ctx.device
     torch.manual_seed(1234)
-    norm = "pdt" if args.impl == "ours" else "torch"  # stock baseline uses nn.BatchNorm2d
-    model = get_model(args.model, norm=norm).to(dev).to(memory_format=torch.channels_last)
+    kw = {}
+    if args.model.startswith("resnet"):
+        kw["norm"] = "pdt" if args.impl == "ours" else "torch"  # stock baseline uses nn.BatchNorm2d
+    model = get_model(args.model, **kw).to(dev)
+    if args.model.startswith("resnet"):
+        model = model.to(memory_format=torch.channels_last)
+    if args.impl != "ours":
+        _to_stock_modules(model)
     precision = args.precision
     if args.impl != "ours" and precision == "bf16":
         precision = "amp_bf16"  # stock path: fp32 params + autocast (what torch users run)
     model = apply_precision(model, precision)
     world = ctx.world_size
+    opt_name = WORKLOADS[args.model][3]
+    lr = args.lr if args.lr is not None else (0.1 if opt_name == "sgd" else 1e-4)
     if args.impl == "ours":
-        from pytorch_distributed_training_example_amd.optim import FusedSGD
+        from pytorch_distributed_training_example_amd.optim import FusedAdamW, FusedSGD
         from pytorch_distributed_training_example_amd.parallel import DistributedDataParallel
         ddp = DistributedDataParallel(model, bucket_cap_mb=args.bucket_cap_mb, broadcast_buffers=False,
                                       gradient_as_bucket_view=True)
-        opt = FusedSGD(model.parameters(), lr=args.lr, momentum=0.9, weight_decay=5e-5, nesterov=False)
-    elif args.impl == "torch_ddp":
-        ddp = torch.nn.parallel.DistributedDataParallel(model, device_ids=[dev.index], bucket_cap_mb=args.bucket_cap_mb,
-                                                        broadcast_buffers=False, gradient_as_bucket_view=True) \
-            if world > 1 else model
-        opt = torch.optim.SGD(model.parameters(), lr=args.lr, momentum=0.9, weight_decay=5e-5)
+        opt = FusedSGD(model.parameters(), lr=lr, momentum=0.9, weight_decay=5e-5) if opt_name == "sgd" \
+            else FusedAdamW(model.parameters(), lr=lr, weight_decay=0.1)
     else:
-        ddp = model
-        opt = torch.optim.SGD(model.parameters(), lr=args.lr, momentum=0.9, weight_decay=5e-5)
+        if args.impl == "torch_ddp" and world > 1:
+            ddp = torch.nn.parallel.DistributedDataParallel(model, device_ids=[dev.index],
+                                                            bucket_cap_mb=args.bucket_cap_mb,
+                                                            broadcast_buffers=False, gradient_as_bucket_view=True)
+        else:
+            ddp = model
+        opt = torch.optim.SGD(model.parameters(), lr=lr, momentum=0.9, weight_decay=5e-5) if opt_name == "sgd" \
+            else torch.optim.AdamW(model.parameters(), lr=lr, weight_decay=0.1, fused=True)
     return model, ddp, opt, precision
 
 
@@ -90,6 +120,8 @@ def main(argv=None):
     ctx = launcher.init_distributed(backend="nccl" if torch.cuda.is_available() else "gloo")
     dev = ctx.device
     world = ctx.world_size
+    metric, unit, default_b, _ = WORKLOADS[args.model]
+    B = args.batch_size or default_b
     torch.backends.cudnn.benchmark = bool(args.cudnn_benchmark)
     # MIOpen's non-deterministic conv solvers are not hipGraph-capture safe (replays give wrong
     # gradients, tools/diag_graph.py); capture therefore requires the deterministic solvers.
@@ -99,35 +131,57 @@ def main(argv=None):
     from pytorch_distributed_training_example_amd.ops.cross_entropy import cross_entropy
     from pytorch_distributed_training_example_amd.parallel.reference import average_gradients
 
-    B, S = args.batch_size, args.image_size
-    in_dtype = torch.bfloat16 if precision == "bf16" else torch.float32
     g = torch.Generator(device=dev).manual_seed(100 + ctx.rank)
-    pool = [torch.randn(B, 3, S, S, device=dev, generator=g).to(in_dtype).contiguous(memory_format=torch.channels_last)
-            for _ in range(2)]
-    tpool = [torch.randint(0, 1000, (B,), device=dev, generator=g) for _ in range(2)]
+    is_lm = args.model.startswith("gpt")
+    S, T = args.image_size, args.seq_len
+    assert B % args.grad_accum == 0, "batch must be divisible by grad-accum"
+    in_dtype = torch.bfloat16 if precision == "bf16" else torch.float32
+    pool = []
+    for _ in range(2):
+        if is_lm:
+            x = torch.randint(0, 50257, (B, T), device=dev, generator=g)
+            y = torch.randint(0, 50257, (B, T), device=dev, generator=g)
+        else:
+            x = torch.randn(B, 3, S, S, device=dev, generator=g).to(in_dtype)
+            if args.model.startswith("resnet"):
+                x = x.contiguous(memory_format=torch.channels_last)
+            y = torch.randint(0, 1000, (B,), device=dev, generator=g)
+        pool.append((x, y))
     autocast = precision == "amp_bf16"
+    ls = 0.1 if args.model.startswith("resnet") else 0.0
+
+    def loss_of(out, y):
+        if is_lm:
+            out, y = out.reshape(-1, out.shape[-1]), y.reshape(-1)
+        if args.impl == "ours":
+            return cross_entropy(out, y, label_smoothing=ls)
+        return torch.nn.functional.cross_entropy(out.float(), y, label_smoothing=ls)
 
     def step(x, y):
         opt.zero_grad(set_to_none=True)
-        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=autocast):
-            out = ddp(x)
-        if args.impl == "ours":
-            loss = cross_entropy(out, y, label_smoothing=0.1)
-        else:
-            loss = torch.nn.functional.cross_entropy(out.float(), y, label_smoothing=0.1)
-        loss.backward()
+        xs, ys = x.chunk(args.grad_accum), y.chunk(args.grad_accum)
+        total = None
+        for i, (xm, ym) in enumerate(zip(xs, ys)):
+            last = i == len(xs) - 1
+            sync = ddp.no_sync() if (not last and hasattr(ddp, "no_sync")) else contextlib.nullcontext()
+            with sync:
+                with torch.autocast("cuda", dtype=torch.bfloat16, enabled=autocast):
+                    out = ddp(xm)
+                loss = loss_of(out, ym) / len(xs)
+                loss.backward()
+            total = loss.detach() if total is None else total + loss.detach()
         if args.impl == "reference" and world > 1:
             average_gradients(model)
         opt.step()
-        return loss.detach()
+        return total
 
     runner = None
     if args.impl == "ours" and args.graph:
         from pytorch_distributed_training_example_amd.engine.graph import StaticStep
-        runner = StaticStep(step, [pool[0], tpool[0]], warmup=max(3, min(args.warmup, 5)))
+        runner = StaticStep(step, list(pool[0]), warmup=max(3, min(args.warmup, 5)))
 
     def run(i):
-        x, y = pool[i % 2], tpool[i % 2]
+        x, y = pool[i % 2]
         return runner(x, y) if runner is not None else step(x, y)
 
     for i in range(args.warmup):
@@ -149,16 +203,18 @@ def main(argv=None):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms = elapsed / args.steps * 1e3
-    value = B * world * args.steps / elapsed
+    per_step = B * (T if is_lm else 1)
+    value = per_step * world * args.steps / elapsed
     result = {
-        "metric": METRIC, "value": round(value, 2), "unit": "images/sec", "n_gpus": world,
+        "metric": metric, "value": round(value, 2), "unit": unit, "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "bf16" if precision != "fp32" else "fp32",
-        "data": "synthetic (random 224x224 images, random labels, random-init weights)",
-        "config": {"model": args.model, "global_batch": B * world, "per_gpu_batch": B, "seq_len": None,
-                   "image_size": S, "parallelism": f"dp{world}", "impl": args.impl,
-                   "graph": bool(runner is not None), "precision": precision,
-                   "bucket_cap_mb": args.bucket_cap_mb, "deterministic": bool(det), "final_loss": round(float(loss.float().item()), 4)},
+        "data": "synthetic (random inputs and labels, random-init weights)",
+        "config": {"model": args.model, "global_batch": B * world, "per_gpu_batch": B,
+                   "seq_len": T if is_lm else None, "image_size": None if is_lm else S,
+                   "parallelism": f"dp{world}", "grad_accum": args.grad_accum, "impl": args.impl,
+                   "graph": bool(runner is not None), "precision": precision, "bucket_cap_mb": args.bucket_cap_mb,
+                   "deterministic": bool(det), "final_loss": round(float(loss.float().item()), 4)},
     }
     if ctx.rank == 0:
         print(json.dumps(result), flush=True)

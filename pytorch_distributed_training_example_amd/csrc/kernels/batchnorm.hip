@@ -99,11 +99,14 @@ __global__ __launch_bounds__(kThreads) void bn_reduce_kernel(
   if (MODE == 0) ld8_bf16(x + c, k);  // shift: first row (same for every block)
   else ld8_f32(mean + c, k);
   int64_t m = m0 + r;
-  for (; m + kR < m1; m += 2 * kR) {
+  // 4 independent rows in flight per lane (≈16-48 KB per workgroup outstanding)
+  for (; m + 3 * kR < m1; m += 4 * kR) {
     accum_row<MODE>(x, dy, mask, m, C, c, k, s1, s2);
     accum_row<MODE>(x, dy, mask, m + kR, C, c, k, s1, s2);
+    accum_row<MODE>(x, dy, mask, m + 2 * kR, C, c, k, s1, s2);
+    accum_row<MODE>(x, dy, mask, m + 3 * kR, C, c, k, s1, s2);
   }
-  if (m < m1) accum_row<MODE>(x, dy, mask, m, C, c, k, s1, s2);
+  for (; m < m1; m += kR) accum_row<MODE>(x, dy, mask, m, C, c, k, s1, s2);
 
   // reduce the 32 row-groups through LDS: sm[0][r][64] = s1, sm[1][r][64] = s2
   float* d0 = &sm[r * kCC + l * 8];
@@ -138,23 +141,31 @@ __global__ __launch_bounds__(kThreads) void bn_reduce_kernel(
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
-  // last arriver: fixed-order reduction of the chunk's nrow slabs (4 groups x 64 channels)
-  const int g = tid >> 6, cl = tid & 63;
-  const float* base = part + (int64_t)chunk * nrow * (2 * kCC);
-  float a = 0.f, b = 0.f;
-  for (int blk = g; blk < nrow; blk += 4) {
-    a += base[(int64_t)blk * (2 * kCC) + cl];
-    b += base[(int64_t)blk * (2 * kCC) + kCC + cl];
+  // last arriver: fixed-order reduction of the chunk's nrow slabs. The slabs were written by
+  // other CUs/XCDs, so every load is a cross-XCD round trip: issue them 16 at a time as
+  // independent float4 loads (thread t owns float4 column t&31 of every 8th slab).
+  const int col = tid & 31, bg = tid >> 5;
+  const float4* base4 = reinterpret_cast<const float4*>(part + (int64_t)chunk * nrow * (2 * kCC));
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int b0 = bg; b0 < nrow; b0 += 8 * 16) {
+    float4 v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int blk = b0 + 8 * u;
+      v[u] = blk < nrow ? base4[(int64_t)blk * 32 + col] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) { acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w; }
   }
   __syncthreads();
-  sm[g * kCC + cl] = a;
-  sm[4 * kCC + g * kCC + cl] = b;
+  reinterpret_cast<float4*>(sm)[bg * 32 + col] = acc;
   __syncthreads();
   if (tid == 0) counters[chunk] = 0u;  // self-reset for the next launch (stream-ordered)
   if (tid >= kCC) return;
   const int ch = chunk * kCC + tid;
-  const float S1 = sm[tid] + sm[kCC + tid] + sm[2 * kCC + tid] + sm[3 * kCC + tid];
-  const float S2 = sm[4 * kCC + tid] + sm[5 * kCC + tid] + sm[6 * kCC + tid] + sm[7 * kCC + tid];
+  float S1 = 0.f, S2 = 0.f;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) { S1 += sm[q * 128 + tid]; S2 += sm[q * 128 + kCC + tid]; }
   const int64_t Mt = fa.M;
   if (MODE == 0) {
     const float kk = bf2f(fa.x[ch]);

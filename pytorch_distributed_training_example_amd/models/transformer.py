@@ -1,0 +1,85 @@
+"""Transformer building blocks shared by ViT-B/16 and GPT-2 (north-star configs 3 and 4).
+
+Not in the reference (LeNet only). MI355X-first choices:
+  * every GEMM is a plain bf16 ``F.linear`` (hipBLASLt, MFMA) with NO fused bias where an
+    epilogue kernel follows: the MLP's first bias is applied inside the fused bias+GELU HIP
+    kernel (ops/gelu.py), so the [tokens, 4·D] activation is read/written once;
+  * LayerNorm is the wave-per-row HIP kernel (ops/layernorm.py) with fp32 parameters;
+  * attention goes through ``ops.attention.attention`` ([B, H, T, Dh] bf16);
+  * the LM / classifier loss is the fused softmax-cross-entropy kernel.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from ..ops.attention import attention
+from ..ops.gelu import bias_gelu
+from ..ops.layernorm import LayerNorm
+
+
+class SelfAttention(nn.Module):
+    def __init__(self, dim: int, heads: int, causal: bool, bias: bool = True, dropout: float = 0.0):
+        super().__init__()
+        assert dim % heads == 0
+        self.heads = heads
+        self.causal = causal
+        self.c_attn = nn.Linear(dim, 3 * dim, bias=bias)
+        self.c_proj = nn.Linear(dim, dim, bias=bias)
+        self.dropout = dropout
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        B, T, D = x.shape
+        qkv = self.c_attn(x).view(B, T, 3, self.heads, D // self.heads)
+        q, k, v = qkv.permute(2, 0, 3, 1, 4).unbind(0)  # [B, H, T, Dh]
+        y = attention(q, k, v, causal=self.causal, dropout_p=self.dropout if self.training else 0.0)
+        y = y.transpose(1, 2).reshape(B, T, D)
+        return self.c_proj(y)
+
+
+class MLP(nn.Module):
+    def __init__(self, dim: int, hidden: int, approximate: str = "none", bias: bool = True):
+        super().__init__()
+        self.c_fc = nn.Linear(dim, hidden, bias=bias)
+        self.c_proj = nn.Linear(hidden, dim, bias=bias)
+        self.approximate = approximate
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        h = F.linear(x, self.c_fc.weight)  # bias is fused into the GELU kernel
+        b = self.c_fc.bias
+        h = bias_gelu(h, b.float() if b is not None and b.dtype != torch.float32 else b, self.approximate)
+        return self.c_proj(h)
+
+
+class Block(nn.Module):
+    """Pre-norm transformer block: x + attn(ln_1(x)), then x + mlp(ln_2(x))."""
+
+    def __init__(self, dim: int, heads: int, mlp_ratio: float = 4.0, causal: bool = False,
+                 approximate: str = "none", eps: float = 1e-5):
+        super().__init__()
+        self.ln_1 = LayerNorm(dim, eps=eps)
+        self.attn = SelfAttention(dim, heads, causal)
+        self.ln_2 = LayerNorm(dim, eps=eps)
+        self.mlp = MLP(dim, int(dim * mlp_ratio), approximate)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        x = x + self.attn(self.ln_1(x))
+        x = x + self.mlp(self.ln_2(x))
+        return x
+
+
+def init_weights(module: nn.Module, std: float = 0.02, n_layer: Optional[int] = None) -> None:
+    for name, m in module.named_modules():
+        if isinstance(m, nn.Linear):
+            s = std
+            if n_layer is not None and name.endswith("c_proj"):
+                s = std / math.sqrt(2 * n_layer)  # GPT-2 residual-projection scaling
+            nn.init.normal_(m.weight, 0.0, s)
+            if m.bias is not None:
+                nn.init.zeros_(m.bias)
+        elif isinstance(m, nn.Embedding):
+            nn.init.normal_(m.weight, 0.0, std)
