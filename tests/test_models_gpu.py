@@ -18,30 +18,32 @@ def _grads(model, x, y, loss_fn):
     return float(loss), {n: p.grad.float().clone() for n, p in model.named_parameters() if p.grad is not None}
 
 
-def _compare(name, make_input, loss_fn, tol=0.08, **kw):
+def _compare(name, make_input, loss_fn, slack=1.3, **kw):
+    """Native bf16 path must be as accurate as the stock bf16 path, both measured against an fp32
+    oracle. (A direct native-vs-stock comparison is meaningless for deep random-init nets: two
+    bf16 runs differing by 1e-3 in the input already disagree by >100% in early-layer grads,
+    see tools/diag_e2e.py.)"""
     from pytorch_distributed_training_example_amd.models import get_model
     from pytorch_distributed_training_example_amd.models.precision import to_bf16_mixed
-    from pytorch_distributed_training_example_amd.ops import _native
     torch.manual_seed(0)
-    m = get_model(name, **kw).cuda()
+    base = get_model(name, **kw).cuda()
     if name.startswith("resnet"):
-        m = m.to(memory_format=torch.channels_last)
-    m = to_bf16_mixed(m)
+        base = base.to(memory_format=torch.channels_last)
     x, y = make_input()
-    ref = copy.deepcopy(m)
-    l_nat, g_nat = _grads(m, x, y, loss_fn)
+    xb = x.bfloat16() if x.is_floating_point() else x
     os.environ["PDT_DISABLE_NATIVE"] = "1"
     try:
-        l_ref, g_ref = _grads(ref, x, y, loss_fn)
+        l32, g32 = _grads(copy.deepcopy(base), x, y, loss_fn)
+        l_ref, g_ref = _grads(to_bf16_mixed(copy.deepcopy(base)), xb, y, loss_fn)
     finally:
         os.environ.pop("PDT_DISABLE_NATIVE")
-    assert abs(l_nat - l_ref) < 0.02 * max(1.0, abs(l_ref)), (l_nat, l_ref)
-    bad = []
-    for n in g_ref:
-        err = ((g_nat[n] - g_ref[n]).norm() / (g_ref[n].norm() + 1e-6)).item()
-        if err > tol:
-            bad.append((n, err))
-    assert not bad, bad[:5]
+    l_nat, g_nat = _grads(to_bf16_mixed(copy.deepcopy(base)), xb, y, loss_fn)
+    assert abs(l_nat - l32) <= slack * abs(l_ref - l32) + 0.02 * max(1.0, abs(l32)), (l_nat, l_ref, l32)
+    e = lambda a, b: ((a - b).norm() / (b.norm() + 1e-9)).item()
+    e_nat = torch.tensor([e(g_nat[n], g32[n]) for n in g32])
+    e_ref = torch.tensor([e(g_ref[n], g32[n]) for n in g32])
+    assert e_nat.median() <= slack * e_ref.median() + 0.02, (e_nat.median(), e_ref.median())
+    assert e_nat.max() <= slack * e_ref.max() + 0.05, (e_nat.max(), e_ref.max())
 
 
 def _ce(out, y):
@@ -51,14 +53,14 @@ def _ce(out, y):
 
 def test_resnet50_native_matches_reference():
     def inp():
-        x = torch.randn(16, 3, 64, 64, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+        x = torch.randn(16, 3, 64, 64, device="cuda").contiguous(memory_format=torch.channels_last)
         return x, torch.randint(0, 1000, (16,), device="cuda")
     _compare("resnet50", inp, _ce)
 
 
 def test_vit_native_matches_reference():
     def inp():
-        return torch.randn(8, 3, 32, 32, device="cuda").bfloat16(), torch.randint(0, 1000, (8,), device="cuda")
+        return torch.randn(8, 3, 32, 32, device="cuda"), torch.randint(0, 1000, (8,), device="cuda")
     _compare("vit_tiny", inp, _ce)
 
 
