@@ -63,6 +63,7 @@ def parse(argv=None):
     ap.add_argument("--lr", type=float, default=None)
     ap.add_argument("--cudnn-benchmark", type=int, default=1, help="MIOpen find mode for conv algorithms")
     ap.add_argument("--deterministic", type=int, default=-1, help="-1: on iff hipGraph capture")
+    ap.add_argument("--backend", default=None, help="process-group backend (default: nccl = RCCL on GPU)")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args(argv)
 
@@ -117,7 +118,8 @@ def build(args, ctx):
 def main(argv=None):
     args = parse(argv)
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    ctx = launcher.init_distributed(backend="nccl" if torch.cuda.is_available() else "gloo")
+    ctx = launcher.init_distributed(backend=args.backend or ("nccl" if torch.cuda.is_available() else "gloo"),
+                                    use_gpu=torch.cuda.is_available())
     dev = ctx.device
     world = ctx.world_size
     metric, unit, default_b, _ = WORKLOADS[args.model]

@@ -195,6 +195,14 @@ def run(rank: int, world: int, args) -> dict:
         if rank == 0:
             print(f"resumed from {args.checkpoint} at epoch {start_epoch}", flush=True)
     metrics = MetricsWriter(args.metrics, rank)
+    from .parallel.fault import FaultInjector
+    injector = FaultInjector(rank=rank)
+    gstep = [0]
+
+    def on_step(epoch, batch_idx):
+        gstep[0] += 1
+        injector.maybe_fail(gstep[0])
+
     result = {}
     for epoch in range(start_epoch, args.epochs + 1):
         if train_sampler is not None:
@@ -202,7 +210,8 @@ def run(rank: int, world: int, args) -> dict:
         if hasattr(train_loader, "set_epoch"):
             train_loader.set_epoch(epoch)
         stats = train_epoch(step, train_loader, device, epoch, args.log_interval, args.dry_run, rank, metrics,
-                            max_steps=args.steps_per_epoch, input_dtype=in_dtype, channels_last=args.channels_last)
+                            max_steps=args.steps_per_epoch, input_dtype=in_dtype, channels_last=args.channels_last,
+                            on_step=on_step)
         result["train"] = stats
         metrics.log({"event": "epoch", "epoch": epoch, **stats})
         if test_loader is not None and not args.no_eval:

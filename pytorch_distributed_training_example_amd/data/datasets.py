@@ -45,7 +45,7 @@ def _find(root: str, stem: str) -> Optional[str]:
 
 class _NormalizedImages(Dataset):
     def __init__(self, images: np.ndarray, labels: np.ndarray):
-        self.images = torch.from_numpy(np.ascontiguousarray(images))  # uint8 [N, 28, 28]
+        self.images = torch.from_numpy(np.array(images, dtype=np.uint8, copy=True))  # uint8 [N, 28, 28]
         self.targets = torch.from_numpy(labels.astype(np.int64))
 
     def __len__(self) -> int:

@@ -101,8 +101,11 @@ class TrainStep:
 
 def train_epoch(step: TrainStep, loader, device, epoch: int, log_interval: int = 15, dry_run: bool = False,
                 rank: Optional[int] = None, metrics=None, max_steps: Optional[int] = None,
-                input_dtype: Optional[torch.dtype] = None, channels_last: bool = False) -> dict:
-    """Reference-compatible train loop (log line format of train.py:52-55)."""
+                input_dtype: Optional[torch.dtype] = None, channels_last: bool = False,
+                on_step: Optional[Callable[[int, int], None]] = None) -> dict:
+    """Reference-compatible train loop (log line format of train.py:52-55).
+
+    ``on_step(epoch, batch_idx)`` runs after every optimizer step (fault injection, profiling)."""
     rank = launcher.get_rank() if rank is None else rank
     step.model.train()
     nb = len(loader)
@@ -121,6 +124,8 @@ def train_epoch(step: TrainStep, loader, device, epoch: int, log_interval: int =
             xs, ys = data, target
         loss = step(xs, ys)
         seen += data.shape[0]
+        if on_step is not None:
+            on_step(epoch, batch_idx)
         if batch_idx % log_interval == 0 and rank == 0:
             print("Train Epoch: {} [{}/{} ({:.0f}%)]\tLoss: {:.6f}".format(
                 epoch, batch_idx * len(data), len(loader.dataset), 100.0 * batch_idx / nb, loss.item()),

@@ -223,9 +223,12 @@ class FusedAdam(_FusedOptimizer):
 
     def _ref_step(self, group, ps, kparams, grads):
         b1, b2 = group["betas"]
+        bumped = set()
         for p, kp, g in zip(ps, kparams, grads):
             st = self.state[p]
-            st["step"] += 1
+            if id(st["step"]) not in bumped:  # step tensors may be shared across the group
+                st["step"] += 1
+                bumped.add(id(st["step"]))
             t = float(st["step"])
             g = g.float()
             if group["maximize"]:

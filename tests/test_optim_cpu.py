@@ -1,0 +1,108 @@
+"""Fused optimizers (CPU reference path) == torch.optim; state_dict interchange; AMP scaler."""
+import pytest
+import torch
+
+from pytorch_distributed_training_example_amd.engine.amp import GradScaler
+from pytorch_distributed_training_example_amd.ops import multi_tensor as mt
+from pytorch_distributed_training_example_amd.optim import (FusedAdadelta, FusedAdam, FusedAdamW, FusedSGD,
+                                                            build_scheduler)
+
+
+def _params():
+    torch.manual_seed(0)
+    return [torch.nn.Parameter(torch.randn(s)) for s in [(6, 1, 5, 5), (6,), (84, 120), (10,)]]
+
+
+def _run(make, steps=4):
+    ps = _params()
+    opt = make(ps)
+    g = torch.Generator().manual_seed(1)
+    for _ in range(steps):
+        for p in ps:
+            p.grad = torch.randn(p.shape, generator=g)
+        opt.step()
+    return ps, opt
+
+
+CASES = [
+    (lambda ps: FusedSGD(ps, lr=0.1), lambda ps: torch.optim.SGD(ps, lr=0.1)),
+    (lambda ps: FusedSGD(ps, lr=0.1, momentum=0.9, weight_decay=1e-4, nesterov=True),
+     lambda ps: torch.optim.SGD(ps, lr=0.1, momentum=0.9, weight_decay=1e-4, nesterov=True)),
+    (lambda ps: FusedSGD(ps, lr=0.1, momentum=0.9, dampening=0.1),
+     lambda ps: torch.optim.SGD(ps, lr=0.1, momentum=0.9, dampening=0.1)),
+    (lambda ps: FusedAdam(ps, lr=1e-2, weight_decay=1e-2), lambda ps: torch.optim.Adam(ps, lr=1e-2, weight_decay=1e-2)),
+    (lambda ps: FusedAdamW(ps, lr=1e-2), lambda ps: torch.optim.AdamW(ps, lr=1e-2)),
+    (lambda ps: FusedAdadelta(ps, lr=0.1), lambda ps: torch.optim.Adadelta(ps, lr=0.1)),
+    (lambda ps: FusedAdadelta(ps, lr=1.0, weight_decay=1e-3, maximize=True),
+     lambda ps: torch.optim.Adadelta(ps, lr=1.0, weight_decay=1e-3, maximize=True)),
+]
+
+
+@pytest.mark.parametrize("case", range(len(CASES)))
+def test_fused_matches_torch(case):
+    ours, ref = CASES[case]
+    a, _ = _run(ours)
+    b, _ = _run(ref)
+    for x, y in zip(a, b):
+        torch.testing.assert_close(x, y, rtol=1e-5, atol=1e-6)
+
+
+def test_adadelta_state_dict_interchange():
+    """A torch Adadelta checkpoint (the reference's optimizer) loads into FusedAdadelta and back."""
+    a, oa = _run(lambda ps: torch.optim.Adadelta(ps, lr=0.1), steps=2)
+    ps = [torch.nn.Parameter(p.detach().clone()) for p in a]
+    fo = FusedAdadelta(ps, lr=0.1)
+    fo.load_state_dict(oa.state_dict())
+    g = torch.Generator().manual_seed(7)
+    grads = [torch.randn(p.shape, generator=g) for p in ps]
+    for p, gg in zip(ps, grads):
+        p.grad = gg.clone()
+    for p, gg in zip(a, grads):
+        p.grad = gg.clone()
+    fo.step()
+    oa.step()
+    for x, y in zip(ps, a):
+        torch.testing.assert_close(x, y)
+    assert set(fo.state_dict()["state"][0]) == {"step", "square_avg", "acc_delta"}
+
+
+def test_steplr_matches_reference_schedule():
+    ps = _params()
+    opt = FusedAdadelta(ps, lr=0.1)
+    sch = build_scheduler("step", opt, gamma=0.9)
+    lrs = []
+    for _ in range(4):
+        lrs.append(opt.param_groups[0]["lr"])
+        sch.step()
+    torch.testing.assert_close(torch.tensor(lrs), torch.tensor([0.1 * 0.9 ** e for e in range(4)]))
+
+
+def test_grad_scaler_cpu_skip_and_backoff():
+    ps = _params()
+    before = [p.detach().clone() for p in ps]
+    opt = FusedSGD(ps, lr=0.1)
+    sc = GradScaler(init_scale=1024.0, growth_interval=2, device="cpu")
+    for p in ps:
+        p.grad = torch.ones_like(p)
+    ps[0].grad[0, 0, 0, 0] = float("inf")
+    sc.step(opt)
+    sc.update()
+    for p, q in zip(ps, before):
+        assert torch.equal(p.detach(), q)  # skipped
+    assert sc.get_scale() == 512.0
+    for _ in range(2):
+        for p in ps:
+            p.grad = torch.ones_like(p) * 512.0
+        sc.step(opt)
+        sc.update()
+    assert sc.get_scale() == 1024.0  # grew after 2 clean steps
+    torch.testing.assert_close(ps[1].detach(), before[1] - 0.2)  # unscaled grads of 1.0, two steps
+
+
+def test_clip_grad_norm_cpu():
+    gs = [torch.full((10,), 3.0), torch.full((6,), 4.0)]
+    n = mt.clip_grad_norm_(gs, 1.0)
+    ref = (90 + 96) ** 0.5
+    assert abs(float(n) - ref) < 1e-4
+    total = torch.sqrt(sum((g ** 2).sum() for g in gs))
+    assert abs(float(total) - 1.0) < 1e-4
