@@ -52,6 +52,13 @@ int pdt_ln_fwd(const void* x, int dtype, const float* w, const float* b, void* y
                int D, float eps, hipStream_t s);
 int pdt_ln_bwd(const void* dy, const void* x, int dtype, const float* w, const float* mean, const float* rstd,
                void* dx, float* dw, float* db, int64_t N, int D, float* ws, hipStream_t s);
+int pdt_attn_fwd(const uint16_t* q, const int64_t* qs, const uint16_t* k, const int64_t* ks, const uint16_t* v,
+                 const int64_t* vs, uint16_t* o, const int64_t* os, float* lse, int B, int H, int T, int Dh,
+                 int causal, float scale, hipStream_t s);
+int pdt_attn_bwd(const uint16_t* dout, const int64_t* dos, const uint16_t* q, const int64_t* qs, const uint16_t* k,
+                 const int64_t* ks, const uint16_t* v, const int64_t* vs, const uint16_t* o, const int64_t* os,
+                 const float* lse, float* delta, uint16_t* dq, uint16_t* dk, uint16_t* dv, const int64_t* gs, int B,
+                 int H, int T, int Dh, int causal, float scale, hipStream_t s);
 int64_t pdt_gelu_workspace_floats(int64_t N, int D);
 int pdt_bias_gelu_fwd(const void* x, int dtype, const float* bias, void* y, int64_t N, int D, int tanh_form,
                       hipStream_t s);
@@ -426,6 +433,51 @@ std::vector<Tensor> bias_gelu_bwd(Tensor dy, Tensor x, c10::optional<Tensor> bia
   return {dx, db};
 }
 
+// ----------------------------------------------------------------------------- flash attention
+// Views are [B, H, T, Dh] bf16 with unit stride on Dh (any b/h/t strides, e.g. slices of a packed qkv).
+struct Strides3 {
+  int64_t v[3];
+};
+Strides3 bht_strides(const Tensor& t, const char* name) {
+  check_cuda(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16 && t.dim() == 4 && t.stride(3) == 1, "attn: ", name,
+              " must be a bf16 [B,H,T,Dh] view with unit Dh stride");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0 && t.stride(2) % 8 == 0 && t.stride(1) % 8 == 0,
+              "attn: ", name, " rows must be 16-byte aligned");
+  return {{t.stride(0), t.stride(1), t.stride(2)}};
+}
+
+void attn_fwd_out(Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, bool causal, double scale) {
+  auto qs = bht_strides(q, "q"), ks = bht_strides(k, "k"), vs = bht_strides(v, "v"), os = bht_strides(o, "o");
+  TORCH_CHECK(q.sizes() == k.sizes() && q.sizes() == v.sizes() && q.sizes() == o.sizes(), "attn: shape mismatch");
+  TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.is_contiguous() && lse.numel() == q.size(0) * q.size(1) * q.size(2),
+              "attn: lse must be fp32 [B,H,T]");
+  const int B = q.size(0), H = q.size(1), T = q.size(2), Dh = q.size(3);
+  int rc = pdt_attn_fwd(reinterpret_cast<const uint16_t*>(q.data_ptr()), qs.v, reinterpret_cast<const uint16_t*>(k.data_ptr()),
+                        ks.v, reinterpret_cast<const uint16_t*>(v.data_ptr()), vs.v,
+                        reinterpret_cast<uint16_t*>(o.data_ptr()), os.v, lse.data_ptr<float>(), B, H, T, Dh, causal,
+                        (float)scale, stream());
+  TORCH_CHECK(rc == 0, "pdt_attn_fwd: unsupported head dim ", Dh);
+}
+
+void attn_bwd_out(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor dq, Tensor dk, Tensor dv,
+                  bool causal, double scale) {
+  auto dos = bht_strides(dout, "dout"), qs = bht_strides(q, "q"), ks = bht_strides(k, "k"), vs = bht_strides(v, "v"),
+       os = bht_strides(o, "o"), gs = bht_strides(dq, "dq"), gk = bht_strides(dk, "dk"), gv = bht_strides(dv, "dv");
+  TORCH_CHECK(gs.v[0] == gk.v[0] && gs.v[1] == gk.v[1] && gs.v[2] == gk.v[2] && gs.v[0] == gv.v[0] &&
+              gs.v[1] == gv.v[1] && gs.v[2] == gv.v[2], "attn bwd: dq/dk/dv must share strides");
+  const int B = q.size(0), H = q.size(1), T = q.size(2), Dh = q.size(3);
+  auto delta = at::empty({(int64_t)B * H * T}, q.options().dtype(at::kFloat));
+  int rc = pdt_attn_bwd(reinterpret_cast<const uint16_t*>(dout.data_ptr()), dos.v,
+                        reinterpret_cast<const uint16_t*>(q.data_ptr()), qs.v, reinterpret_cast<const uint16_t*>(k.data_ptr()),
+                        ks.v, reinterpret_cast<const uint16_t*>(v.data_ptr()), vs.v,
+                        reinterpret_cast<const uint16_t*>(o.data_ptr()), os.v, lse.data_ptr<float>(),
+                        delta.data_ptr<float>(), reinterpret_cast<uint16_t*>(dq.data_ptr()),
+                        reinterpret_cast<uint16_t*>(dk.data_ptr()), reinterpret_cast<uint16_t*>(dv.data_ptr()), gs.v, B,
+                        H, T, Dh, causal, (float)scale, stream());
+  TORCH_CHECK(rc == 0, "pdt_attn_bwd: unsupported head dim ", Dh);
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -448,4 +500,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ln_bwd", &ln_bwd);
   m.def("bias_gelu_fwd", &bias_gelu_fwd);
   m.def("bias_gelu_bwd", &bias_gelu_bwd);
+  m.def("attn_fwd_out", &attn_fwd_out);
+  m.def("attn_bwd_out", &attn_bwd_out);
 }

@@ -17,7 +17,7 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
-from ..ops.attention import attention
+from ..ops.attention import attention_qkv
 from ..ops.gelu import bias_gelu
 from ..ops.layernorm import LayerNorm
 
@@ -33,11 +33,8 @@ class SelfAttention(nn.Module):
         self.dropout = dropout
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        B, T, D = x.shape
-        qkv = self.c_attn(x).view(B, T, 3, self.heads, D // self.heads)
-        q, k, v = qkv.permute(2, 0, 3, 1, 4).unbind(0)  # [B, H, T, Dh]
-        y = attention(q, k, v, causal=self.causal, dropout_p=self.dropout if self.training else 0.0)
-        y = y.transpose(1, 2).reshape(B, T, D)
+        qkv = self.c_attn(x)  # [B, T, 3D]; the attention kernels read Q/K/V in place
+        y = attention_qkv(qkv, self.heads, causal=self.causal, dropout_p=self.dropout if self.training else 0.0)
         return self.c_proj(y)
 
 

@@ -244,3 +244,28 @@ def test_mt_copy_with_scale():
     mt.copy_(src, dst, factor=0.5)
     for s, d in zip(src, dst):
         torch.testing.assert_close(d.float(), (s * 0.5).bfloat16().float())
+
+
+# ----------------------------------------------------------------------------- flash attention
+@pytest.mark.parametrize("B,T,H,causal", [(2, 197, 3, False), (2, 256, 2, True), (1, 100, 4, True),
+                                          (3, 64, 1, False), (1, 1024, 2, True)])
+def test_flash_attention_qkv(B, T, H, causal):
+    from pytorch_distributed_training_example_amd.ops.attention import _views, attention_qkv, attention_reference
+    torch.manual_seed(0)
+    Dh = 64
+    qkv = (torch.randn(B, T, 3 * H * Dh, device=DEV) * 1.5).bfloat16().requires_grad_(True)
+    y = attention_qkv(qkv, H, causal=causal)
+    ref_in = qkv.detach().float().requires_grad_(True)
+    (q, k, v), _ = _views(ref_in, H)
+    yr = attention_reference(q, k, v, causal).transpose(1, 2).reshape(B, T, H * Dh)
+    torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=2e-2)
+    g = torch.randn_like(yr)
+    y.backward(g.bfloat16())
+    yr.backward(g.bfloat16().float())
+    err = (qkv.grad.float() - ref_in.grad).norm() / ref_in.grad.norm()
+    assert err < 2e-2, err
+    # per-slice check (dq / dk / dv)
+    for i in range(3):
+        a = qkv.grad.float().view(B, T, 3, H, Dh)[:, :, i]
+        b = ref_in.grad.view(B, T, 3, H, Dh)[:, :, i]
+        assert (a - b).norm() / (b.norm() + 1e-6) < 3e-2, (i, ((a - b).norm() / b.norm()).item())
