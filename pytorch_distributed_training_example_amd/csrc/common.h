@@ -121,16 +121,16 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 }  // namespace pdt
 
 // Multi-tensor launch metadata, passed BY VALUE as a kernel argument (graph-capture safe,
-// no H2D copy). Each workgroup processes one (tensor, chunk) pair.
+// no H2D copy). Workgroup b processes chunk (b - chunk_start[t]) of tensor t, where t is the
+// last tensor with chunk_start[t] <= b.
 #define PDT_MT_MAX_TENSORS 36
-#define PDT_MT_MAX_BLOCKS 320
-#define PDT_MT_CHUNK 32768
+#define PDT_MT_CHUNK 16384
+#define PDT_MT_MAX_GRID (1 << 30)
 
 template <int NL>
 struct MTMeta {
   void* ptr[NL][PDT_MT_MAX_TENSORS];
   int64_t numel[PDT_MT_MAX_TENSORS];
-  uint8_t block_tensor[PDT_MT_MAX_BLOCKS];
-  uint16_t block_chunk[PDT_MT_MAX_BLOCKS];
-  int nblocks;
+  int chunk_start[PDT_MT_MAX_TENSORS + 1];
+  int ntensors;
 };

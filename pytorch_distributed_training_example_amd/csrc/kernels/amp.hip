@@ -83,8 +83,8 @@ struct CopyOp {
 template <typename T>
 __global__ __launch_bounds__(256) void l2norm_kernel(MTMeta<1> meta, float* out) {
   __shared__ float red[4];
-  const int t = meta.block_tensor[blockIdx.x];
-  const int64_t c = meta.block_chunk[blockIdx.x];
+  const int t = mt_find(meta, blockIdx.x);
+  const int64_t c = blockIdx.x - meta.chunk_start[t];
   const int64_t n = meta.numel[t];
   const int64_t start = c * PDT_MT_CHUNK;
   const int64_t end = start + PDT_MT_CHUNK < n ? start + PDT_MT_CHUNK : n;
@@ -185,35 +185,11 @@ int pdt_mt_copy(int n, void* const* src, void* const* dst, const int64_t* numel,
 
 int pdt_l2norm_sq(int n, void* const* x, const int64_t* numel, int dtype, float* out, hipStream_t s) {
   hipMemsetAsync(out, 0, sizeof(float), s);
-  MTMeta<1> meta;
-  meta.nblocks = 0;
-  int tl = 0;
-  auto flush = [&]() {
-    if (meta.nblocks == 0) return;
-    if (dtype == 0) hipLaunchKernelGGL(l2norm_kernel<float>, dim3(meta.nblocks), dim3(256), 0, s, meta, out);
-    else hipLaunchKernelGGL(l2norm_kernel<uint16_t>, dim3(meta.nblocks), dim3(256), 0, s, meta, out);
-    meta.nblocks = 0;
-  };
-  for (int t = 0; t < n; ++t) {
-    const int64_t ne = numel[t];
-    if (ne == 0) continue;
-    meta.ptr[0][tl] = x[t];
-    meta.numel[tl] = ne;
-    const int64_t nch = (ne + PDT_MT_CHUNK - 1) / PDT_MT_CHUNK;
-    for (int64_t c = 0; c < nch; ++c) {
-      meta.block_tensor[meta.nblocks] = (uint8_t)tl;
-      meta.block_chunk[meta.nblocks] = (uint16_t)c;
-      meta.nblocks++;
-      const bool last = c == nch - 1;
-      if (meta.nblocks == PDT_MT_MAX_BLOCKS || ((tl + 1 == PDT_MT_MAX_TENSORS) && last)) {
-        flush();
-        if (last) tl = -1;
-        else { meta.ptr[0][0] = meta.ptr[0][tl]; meta.numel[0] = ne; tl = 0; }
-      }
-    }
-    tl++;
-  }
-  flush();
+  void* const* lists[1] = {x};
+  mt_batches<1>(n, lists, numel, [&](const MTMeta<1>& meta, int nblocks) {
+    if (dtype == 0) hipLaunchKernelGGL(l2norm_kernel<float>, dim3(nblocks), dim3(256), 0, s, meta, out);
+    else hipLaunchKernelGGL(l2norm_kernel<uint16_t>, dim3(nblocks), dim3(256), 0, s, meta, out);
+  });
   return 0;
 }
 

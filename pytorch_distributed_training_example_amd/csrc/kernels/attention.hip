@@ -168,24 +168,29 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(Tensor4 Q, Tensor4 K, Ten
       }
     }
     // ---- online softmax (per lane = per query), P^T packed as the B operand
+    // masking only on tiles that cross the sequence end or the causal diagonal (wave-uniform)
+    const bool edge = (kv0 + 64 > T) || (CAUSAL && kv0 + 63 > qbase);
     bf16x8 pb[2][2];
 #pragma unroll
     for (int qb = 0; qb < 2; ++qb) {
       const int qi = qbase + 16 * qb + c;
+      if (edge) {
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int key = kv0 + ks * 16 + 4 * g + r;
+            if (key >= T || (CAUSAL && key > qi)) st[qb][ks][r] = -INFINITY;
+          }
+      }
       float mt = -INFINITY;
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int key = kv0 + ks * 16 + 4 * g + r;
-          float sv_ = st[qb][ks][r] * sl2;
-          if (key >= T || (CAUSAL && key > qi)) sv_ = -INFINITY;
-          st[qb][ks][r] = sv_;
-          mt = fmaxf(mt, sv_);
-        }
+        for (int r = 0; r < 4; ++r) mt = fmaxf(mt, st[qb][ks][r]);
       mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
       mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-      const float mn = fmaxf(m[qb], mt);
+      const float mn = fmaxf(m[qb], mt * sl2);  // running max in log2-scaled units
       const float alpha = (mn == -INFINITY) ? 1.f : exp2f(m[qb] - mn);
       const float msub = (mn == -INFINITY) ? 0.f : mn;
       float ls = 0.f;
@@ -193,14 +198,16 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(Tensor4 Q, Tensor4 K, Ten
       for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float p = exp2f(st[qb][ks][r] - msub);
+          const float p = exp2f(fmaf(st[qb][ks][r], sl2, -msub));
           st[qb][ks][r] = p;
           ls += p;
         }
       l[qb] = l[qb] * alpha + ls;
       m[qb] = mn;
+      if (!__all(alpha == 1.f)) {  // exact skip: no query of the wave moved its max
 #pragma unroll
-      for (int n = 0; n < 4; ++n) oacc[qb][n] *= alpha;
+        for (int n = 0; n < 4; ++n) oacc[qb][n] *= alpha;
+      }
       pb[qb][0] = pack8(st[qb][0], st[qb][1]);
       pb[qb][1] = pack8(st[qb][2], st[qb][3]);
     }
@@ -327,12 +334,15 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(Tensor4 Q, Tensor4 K, 
         dp = mfma(va0, bdo[qb][0], dp);
         dp = mfma(va1, bdo[qb][1], dp);
         const int qi = qbase + 16 * qb + c;
+        const bool edge = (kv0 + 64 > T) || (CAUSAL && kv0 + 63 > qbase);
         f4 ds;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int key = kv0 + ks * 16 + 4 * g + r;
-          float p = exp2f(s[r] * sl2 - lse2[qb]);
-          if (key >= T || qi >= T || (CAUSAL && key > qi)) p = 0.f;
+          float p = exp2f(fmaf(s[r], sl2, -lse2[qb]));
+          if (edge) {
+            const int key = kv0 + ks * 16 + 4 * g + r;
+            if (key >= T || qi >= T || (CAUSAL && key > qi)) p = 0.f;
+          }
           ds[r] = p * (dp[r] - dlt[qb]);
         }
         // stash dS^T (fp32) in the S slot; pack after both halves of a 32-key step exist
@@ -451,12 +461,13 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(Tensor4 Q, Tensor4 K
           dp = mfma(da0, bv[kb][0], dp);
           dp = mfma(da1, bv[kb][1], dp);
           const int key = kbase + 16 * kb + c;
+          const bool edge = (q0 + 64 > T) || (kbase + 32 > T) || (CAUSAL && q0 < kbase + 32);
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int ql = qs * 16 + 4 * g + r;
             const int qi = q0 + ql;
-            float p = exp2f(s[r] * sl2 - srow[0][ql]);
-            if (qi >= T || key >= T || (CAUSAL && key > qi)) p = 0.f;
+            float p = exp2f(fmaf(s[r], sl2, -srow[0][ql]));
+            if (edge && (qi >= T || key >= T || (CAUSAL && key > qi))) p = 0.f;
             pp[half][r] = p;
             dd[half][r] = p * (dp[r] - srow[1][ql]);
           }

@@ -73,20 +73,25 @@ __global__ __launch_bounds__(256) void bias_gelu_bwd_kernel(const T* __restrict_
 
 __global__ __launch_bounds__(256) void colsum_finalize_kernel(const float* __restrict__ part, int nblk, int D,
                                                               float* __restrict__ out) {
-  __shared__ float red[4][64];
-  const int grp = threadIdx.x / 64, ln = threadIdx.x % 64;
-  const int c = blockIdx.x * 64 + ln;
+  __shared__ float red[16][17];  // 16 columns x 16 row-groups (fixed order)
+  const int grp = threadIdx.x >> 4, cl = threadIdx.x & 15;
+  const int c = blockIdx.x * 16 + cl;
   float a = 0.f;
   if (c < D)
-    for (int blk = grp; blk < nblk; blk += 4) a += part[(int64_t)blk * D + c];
-  red[grp][ln] = a;
+    for (int blk = grp; blk < nblk; blk += 16) a += part[(int64_t)blk * D + c];
+  red[grp][cl] = a;
   __syncthreads();
-  if (grp == 0 && c < D) out[c] = red[0][ln] + red[1][ln] + red[2][ln] + red[3][ln];
+  if (grp == 0 && c < D) {
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) s += red[q][cl];
+    out[c] = s;
+  }
 }
 
 inline int gelu_bwd_blocks(int64_t N, int& rpb) {
-  int64_t nblk = (N + 7) / 8;
-  if (nblk > 1024) nblk = 1024;
+  int64_t nblk = (N + 31) / 32;
+  if (nblk > 256) nblk = 256;
   if (nblk < 1) nblk = 1;
   rpb = (int)((N + nblk - 1) / nblk);
   return (int)((N + rpb - 1) / rpb);
@@ -131,7 +136,7 @@ int pdt_bias_gelu_bwd(const void* dy, const void* x, int dtype, const float* bia
     hipLaunchKernelGGL(bias_gelu_bwd_kernel<uint16_t>, dim3(nblk), dim3(256), 0, s, (const uint16_t*)dy,
                        (const uint16_t*)x, bias, (uint16_t*)dx, part, N, D, rpb, tanh_form);
   if (dbias)
-    hipLaunchKernelGGL(colsum_finalize_kernel, dim3((D + 63) / 64), dim3(256), 0, s, ws, nblk, D, dbias);
+    hipLaunchKernelGGL(colsum_finalize_kernel, dim3((D + 15) / 16), dim3(256), 0, s, ws, nblk, D, dbias);
   return 0;
 }
 

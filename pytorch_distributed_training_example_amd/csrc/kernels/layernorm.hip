@@ -114,29 +114,34 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
   }
 }
 
+// Fixed-order column sums of the per-block partials: 16 columns x 16 row-groups per workgroup,
+// so each thread sums only nblk/16 independent values (latency-bound otherwise).
 __global__ __launch_bounds__(256) void ln_bwd_finalize_kernel(const float* __restrict__ part, int nblk, int D,
                                                               float* __restrict__ dw, float* __restrict__ db) {
-  __shared__ float red[2][4][64];
-  const int grp = threadIdx.x / 64, ln = threadIdx.x % 64;
-  const int c = blockIdx.x * 64 + ln;
+  __shared__ float red[2][16][17];
+  const int grp = threadIdx.x >> 4, cl = threadIdx.x & 15;
+  const int c = blockIdx.x * 16 + cl;
   float a = 0.f, b = 0.f;
   if (c < D)
-    for (int blk = grp; blk < nblk; blk += 4) {
+    for (int blk = grp; blk < nblk; blk += 16) {
       a += part[((int64_t)blk * 2 + 0) * D + c];
       b += part[((int64_t)blk * 2 + 1) * D + c];
     }
-  red[0][grp][ln] = a;
-  red[1][grp][ln] = b;
+  red[0][grp][cl] = a;
+  red[1][grp][cl] = b;
   __syncthreads();
   if (grp == 0 && c < D) {
-    dw[c] = red[0][0][ln] + red[0][1][ln] + red[0][2][ln] + red[0][3][ln];
-    db[c] = red[1][0][ln] + red[1][1][ln] + red[1][2][ln] + red[1][3][ln];
+    float sa = 0.f, sb = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) { sa += red[0][q][cl]; sb += red[1][q][cl]; }
+    dw[c] = sa;
+    db[c] = sb;
   }
 }
 
 inline int ln_bwd_blocks(int64_t N, int& rows_per_block) {
-  int64_t nblk = (N + 15) / 16;  // >= 4 rows per wave
-  if (nblk > 512) nblk = 512;
+  int64_t nblk = (N + 31) / 32;  // >= 8 rows per wave
+  if (nblk > 256) nblk = 256;
   if (nblk < 1) nblk = 1;
   rows_per_block = (int)((N + nblk - 1) / nblk);
   return (int)((N + rows_per_block - 1) / rows_per_block);
@@ -207,7 +212,7 @@ int pdt_ln_bwd(const void* dy, const void* x, int dtype, const float* w, const f
     default: return -1;
   }
 #undef PDT_LNB
-  hipLaunchKernelGGL(ln_bwd_finalize_kernel, dim3((D + 63) / 64), dim3(256), 0, s, ws, nblk, D, dw, db);
+  hipLaunchKernelGGL(ln_bwd_finalize_kernel, dim3((D + 15) / 16), dim3(256), 0, s, ws, nblk, D, dw, db);
   return 0;
 }
 
