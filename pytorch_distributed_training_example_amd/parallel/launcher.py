@@ -102,6 +102,10 @@ def init_distributed(
     backend = backend or default_backend(use_gpu)
     os.environ.setdefault("MASTER_ADDR", DEFAULT_MASTER_ADDR)
     os.environ.setdefault("MASTER_PORT", str(DEFAULT_MASTER_PORT))
+    if backend == "gloo" and os.environ["MASTER_ADDR"] in ("127.0.0.1", "localhost"):
+        # single-host gloo: bind the loopback device (the container hostname may not resolve,
+        # which makes gloo's default interface lookup flaky)
+        os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
     # dmabuf IPC is the only IPC mode the MI355X host driver supports; keep it for RCCL.
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 

@@ -121,9 +121,16 @@ def test_elastic_restart_after_injected_fault(tmp_path):
     """rank 1 dies mid-epoch 2; torchrun restarts the group; training resumes from the epoch-1 checkpoint."""
     from pytorch_distributed_training_example_amd.parallel.launcher import find_free_port
     env = dict(ENV, PDT_FAULT="1:14")  # 600 samples/2 ranks/bs 32 -> 10 steps/epoch; die at step 14
-    r = _train(["--epochs", "3", "--batch-size", "64", "--train-samples", "600", "--log-interval", "100",
-                "--checkpoint", str(tmp_path / "ck.pt"), "--resume"], tmp_path,
-               torchrun=[2, find_free_port(), "--max-restarts", "1"], env=env, timeout=900)
+    for attempt in range(4):
+        ck = tmp_path / f"ck{attempt}.pt"
+        r = _train(["--epochs", "3", "--batch-size", "64", "--train-samples", "600", "--log-interval", "100",
+                    "--checkpoint", str(ck), "--resume"], tmp_path,
+                   torchrun=[2, find_free_port(), "--max-restarts", "1"], env=env, timeout=900)
+        # gloo's TCP mesh setup is occasionally refused in this sandbox before training starts;
+        # that is an environment flake, not the behaviour under test: retry it
+        flake = r.returncode != 0 and "Connection refused" in r.stderr and not os.path.exists(ck)
+        if not flake:
+            break
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
     assert "resumed from" in r.stdout and "at epoch 2" in r.stdout
     assert r.stdout.count("Test set on 0") >= 3  # epoch 1 (first attempt) + epochs 2, 3 (after restart)
