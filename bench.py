@@ -57,12 +57,12 @@ def parse(argv=None):
     ap.add_argument("--seq-len", type=int, default=1024)
     ap.add_argument("--impl", default="ours", choices=["ours", "torch_ddp", "reference"])
     ap.add_argument("--graph", type=int, default=0,
-                    help="hipGraph-capture the step (ours; needs deterministic MIOpen solvers)")
+                    help="hipGraph-capture the step (ours; excludes the capture-unsafe MIOpen solvers)")
     ap.add_argument("--bucket-cap-mb", type=float, default=25.0)
     ap.add_argument("--precision", default="bf16", choices=["bf16", "amp_bf16", "fp32"])
     ap.add_argument("--lr", type=float, default=None)
     ap.add_argument("--cudnn-benchmark", type=int, default=1, help="MIOpen find mode for conv algorithms")
-    ap.add_argument("--deterministic", type=int, default=-1, help="-1: on iff hipGraph capture")
+    ap.add_argument("--deterministic", type=int, default=0, help="MIOpen deterministic solvers (slow)")
     ap.add_argument("--backend", default=None, help="process-group backend (default: nccl = RCCL on GPU)")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args(argv)
@@ -118,9 +118,11 @@ def main(argv=None):
     metric, unit, default_b, _ = WORKLOADS[args.model]
     B = args.batch_size or default_b
     torch.backends.cudnn.benchmark = bool(args.cudnn_benchmark)
-    # MIOpen's non-deterministic conv solvers are not hipGraph-capture safe (replays give wrong
-    # gradients, tools/diag_graph.py); capture therefore requires the deterministic solvers.
-    det = args.deterministic if args.deterministic >= 0 else int(args.impl == "ours" and bool(args.graph))
+    if args.impl == "ours" and args.graph:
+        # two MIOpen CK solvers replay wrong gradients under capture (tools/diag_conv_graph.py)
+        from pytorch_distributed_training_example_amd.engine.graph import make_miopen_capture_safe
+        make_miopen_capture_safe()
+    det = max(args.deterministic, 0)
     torch.backends.cudnn.deterministic = bool(det)
     model, ddp, opt, precision = build(args, ctx)
     from pytorch_distributed_training_example_amd.ops.cross_entropy import cross_entropy

@@ -53,12 +53,15 @@ def _data(n=6):
     return xs, ys
 
 
-@pytest.fixture(autouse=True)
-def _deterministic():
-    old = torch.backends.cudnn.deterministic
-    torch.backends.cudnn.deterministic = True  # MIOpen non-deterministic solvers are not capture-safe
+@pytest.fixture(autouse=True, params=[False, True], ids=["heuristic", "benchmark"])
+def _solver_mode(request):
+    """Default (non-deterministic) MIOpen solvers, heuristic and find-mode selection; conftest has
+    excluded the two capture-unsafe CK solvers (engine/graph.py)."""
+    old = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
+    torch.backends.cudnn.deterministic = False
+    torch.backends.cudnn.benchmark = request.param
     yield
-    torch.backends.cudnn.deterministic = old
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = old
 
 
 def test_graph_step_lr0_matches_eager():

@@ -5,7 +5,7 @@ import sys
 import torch
 
 sys.path.insert(0, ".")
-from pytorch_distributed_training_example_amd.engine.graph import StaticStep  # noqa: E402
+from pytorch_distributed_training_example_amd.engine.graph import StaticStep, make_miopen_capture_safe  # noqa: E402
 from pytorch_distributed_training_example_amd.models import get_model  # noqa: E402
 from pytorch_distributed_training_example_amd.models.precision import to_bf16_mixed  # noqa: E402
 from pytorch_distributed_training_example_amd.ops.cross_entropy import cross_entropy  # noqa: E402
@@ -39,27 +39,38 @@ def run(base, mode, xs, ys):
 
 
 def main():
-    for det in (False, True):
-        for bench in (False, True):
-            for norm in ("pdt", "torch"):
-                torch.backends.cudnn.deterministic = det
-                torch.backends.cudnn.benchmark = bench
-                torch.manual_seed(0)
-                base = to_bf16_mixed(get_model("resnet18", num_classes=16, norm=norm).cuda()
-                                     .to(memory_format=torch.channels_last))
-                g = torch.Generator(device="cuda").manual_seed(3)
-                xs = [torch.randn(8, 3, 64, 64, device="cuda", generator=g).bfloat16()
-                      .contiguous(memory_format=torch.channels_last) for _ in range(4)]
-                ys = [torch.randint(0, 16, (8,), device="cuda", generator=g) for _ in range(4)]
-                ge = run(base, "eager", xs, ys)
-                gg = run(base, "graph", xs, ys)
-                bad = []
-                for n in ge:
-                    err = ((gg[n] - ge[n]).norm() / (ge[n].norm() + 1e-12)).item()
-                    if err > 1e-2:
-                        bad.append(f"{n}:{err:.2f}")
-                print(f"deterministic={det} benchmark={bench} norm={norm}: {len(bad)}/{len(ge)} bad  {bad[:12]}",
-                      flush=True)
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="resnet18")
+    ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--size", type=int, default=64)
+    ap.add_argument("--safe", type=int, default=1, help="exclude capture-unsafe MIOpen solvers")
+    ap.add_argument("--sweep", type=int, default=0, help="also sweep deterministic/benchmark/norm")
+    a = ap.parse_args()
+    if a.safe:
+        make_miopen_capture_safe()
+    combos = [(d, b, n) for d in (False, True) for b in (False, True) for n in ("pdt", "torch")] if a.sweep \
+        else [(False, True, "pdt")]
+    for det, bench, norm in combos:
+        torch.backends.cudnn.deterministic = det
+        torch.backends.cudnn.benchmark = bench
+        torch.manual_seed(0)
+        base = to_bf16_mixed(get_model(a.model, num_classes=16, norm=norm).cuda()
+                             .to(memory_format=torch.channels_last))
+        g = torch.Generator(device="cuda").manual_seed(3)
+        xs = [torch.randn(a.batch, 3, a.size, a.size, device="cuda", generator=g).bfloat16()
+              .contiguous(memory_format=torch.channels_last) for _ in range(4)]
+        ys = [torch.randint(0, 16, (a.batch,), device="cuda", generator=g) for _ in range(4)]
+        ge = run(base, "eager", xs, ys)
+        gg = run(base, "graph", xs, ys)
+        bad, worst = [], 0.0
+        for n in ge:
+            err = ((gg[n] - ge[n]).norm() / (ge[n].norm() + 1e-12)).item()
+            worst = max(worst, err)
+            if err > 1e-2:
+                bad.append(f"{n}:{err:.2f}")
+        print(f"{a.model} b{a.batch} safe={a.safe} deterministic={det} benchmark={bench} norm={norm}: "
+              f"{len(bad)}/{len(ge)} bad worst={worst:.2e} {bad[:12]}", flush=True)
 
 
 if __name__ == "__main__":
