@@ -105,23 +105,28 @@ def build(args, ctx):
     return model, ddp, opt, precision
 
 
-def main(argv=None):
-    args = parse(argv)
+def setup(args):
+    """Environment + process group (once per process)."""
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     if args.impl != "ours":
         # stock baseline: every op (BN, LN, GELU, attention, CE) on PyTorch's own kernels
         os.environ["PDT_DISABLE_NATIVE"] = "1"
-    ctx = launcher.init_distributed(backend=args.backend or ("nccl" if torch.cuda.is_available() else "gloo"),
-                                    use_gpu=torch.cuda.is_available())
+    if args.impl == "ours" and args.graph:
+        # two MIOpen CK solvers replay wrong gradients under capture (tools/diag_conv_graph.py);
+        # MIOpen reads the switch once, so this must precede the first convolution
+        from pytorch_distributed_training_example_amd.engine.graph import make_miopen_capture_safe
+        make_miopen_capture_safe()
+    return launcher.init_distributed(backend=args.backend or ("nccl" if torch.cuda.is_available() else "gloo"),
+                                     use_gpu=torch.cuda.is_available())
+
+
+def run(args, ctx):
+    """Build the workload, warm up, time ``args.steps`` steps; returns the result dict (all ranks)."""
     dev = ctx.device
     world = ctx.world_size
     metric, unit, default_b, _ = WORKLOADS[args.model]
     B = args.batch_size or default_b
     torch.backends.cudnn.benchmark = bool(args.cudnn_benchmark)
-    if args.impl == "ours" and args.graph:
-        # two MIOpen CK solvers replay wrong gradients under capture (tools/diag_conv_graph.py)
-        from pytorch_distributed_training_example_amd.engine.graph import make_miopen_capture_safe
-        make_miopen_capture_safe()
     det = max(args.deterministic, 0)
     torch.backends.cudnn.deterministic = bool(det)
     model, ddp, opt, precision = build(args, ctx)
@@ -213,6 +218,13 @@ def main(argv=None):
                    "graph": bool(runner is not None), "precision": precision, "bucket_cap_mb": args.bucket_cap_mb,
                    "deterministic": bool(det), "final_loss": round(float(loss.float().item()), 4)},
     }
+    return result
+
+
+def main(argv=None):
+    args = parse(argv)
+    ctx = setup(args)
+    result = run(args, ctx)
     if ctx.rank == 0:
         print(json.dumps(result), flush=True)
         if args.json_out:

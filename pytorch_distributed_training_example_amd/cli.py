@@ -44,7 +44,7 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--model", default="lenet", help="lenet | mlp | resnet50 | resnet18 | vit_b16 | gpt2_medium | ...")
     p.add_argument("--world-size", type=int, default=None, help="ranks to spawn (default: visible GPUs, 1 on CPU)")
     p.add_argument("--backend", default=None, help="nccl (RCCL) | gloo")
-    p.add_argument("--loss", default=None, help="cross_entropy | nll_on_probs (reference) | mse")
+    p.add_argument("--loss", default=None, help="cross_entropy | nll_on_probs (reference) | prob_nll (reference loss from logits) | mse")
     p.add_argument("--optimizer", default=None, help="adadelta | sgd | adamw | adam")
     p.add_argument("--momentum", type=float, default=0.9)
     p.add_argument("--weight-decay", type=float, default=0.0)
@@ -136,7 +136,11 @@ def run(rank: int, world: int, args) -> dict:
     per_rank = math.ceil(args.batch_size / world)  # reference: ceil(global / world) (train.py:82)
 
     if args.model == "lenet":
-        model = get_model("lenet", output="probs" if loss_kind == "nll_on_probs" else "logits")
+        if loss_kind == "nll_on_probs":
+            # the reference's loss (nll on softmax probabilities, train.py:48), computed from the
+            # logits by one fused kernel: identical values, no separate softmax round trip
+            loss_kind = "prob_nll"
+        model = get_model("lenet", output="logits")
     else:
         model = get_model(args.model)
     model = model.to(device)

@@ -64,6 +64,17 @@ int pdt_bias_gelu_fwd(const void* x, int dtype, const float* bias, void* y, int6
                       hipStream_t s);
 int pdt_bias_gelu_bwd(const void* dy, const void* x, int dtype, const float* bias, void* dx, float* dbias,
                       int64_t N, int D, int tanh_form, float* ws, hipStream_t s);
+int pdt_lenet_stem_fwd(const float* x, const float* w, const float* b, int64_t N, float slope, float* y,
+                       uint8_t* code, hipStream_t s);
+int64_t pdt_lenet_stem_slab_floats(int64_t N, int ipb);
+int pdt_lenet_stem_bwd(const float* dy, const uint8_t* code, const float* x, int64_t N, int ipb, float slope,
+                       float* slab, float* dw, float* db, hipStream_t s);
+int pdt_leaky_pool_fwd(const float* x, int64_t planes, int H, int W, float slope, float* y, uint8_t* code,
+                       hipStream_t s);
+int pdt_leaky_pool_bwd(const float* dy, const uint8_t* code, int64_t planes, int H, int W, float slope, float* dx,
+                       hipStream_t s);
+int pdt_softmax_nll_small(const void* logits, int dtype, const int64_t* target, int64_t N, int V, int mode,
+                          float smoothing, float* loss, void* dlogits, float dscale, double* acc, hipStream_t s);
 }
 
 namespace {
@@ -478,6 +489,82 @@ void attn_bwd_out(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor ls
   TORCH_CHECK(rc == 0, "pdt_attn_bwd: unsupported head dim ", Dh);
 }
 
+// ---- LeNet (reference model) ops: csrc/kernels/lenet.hip ----
+constexpr int kStemIpb = 4;  // images per workgroup in the conv1 weight-gradient reduction
+
+std::vector<Tensor> lenet_stem_fwd(Tensor x, Tensor w, Tensor b, double slope) {
+  check_cuda(x, "x");
+  TORCH_CHECK(x.scalar_type() == at::kFloat && x.is_contiguous() && x.dim() == 4 && x.size(1) == 1 &&
+                  x.size(2) == 28 && x.size(3) == 28, "lenet_stem: x must be contiguous fp32 [N,1,28,28]");
+  TORCH_CHECK(w.scalar_type() == at::kFloat && w.is_contiguous() && w.numel() == 150 && b.numel() == 6 &&
+                  b.is_contiguous(), "lenet_stem: conv1 weight [6,1,5,5] / bias [6] fp32");
+  const int64_t N = x.size(0);
+  auto y = at::empty({N, 6, 14, 14}, x.options());
+  auto code = at::empty({N, 6, 14, 14}, x.options().dtype(at::kByte));
+  pdt_lenet_stem_fwd(x.data_ptr<float>(), w.data_ptr<float>(), b.data_ptr<float>(), N, (float)slope,
+                     y.data_ptr<float>(), code.data_ptr<uint8_t>(), stream());
+  return {y, code};
+}
+
+std::vector<Tensor> lenet_stem_bwd(Tensor dy, Tensor code, Tensor x, double slope) {
+  const int64_t N = x.size(0);
+  dy = dy.contiguous();
+  TORCH_CHECK(dy.scalar_type() == at::kFloat && dy.numel() == N * 1176 && code.numel() == N * 1176 &&
+                  x.numel() == N * 784, "lenet_stem_bwd: shape mismatch");
+  auto slab = at::empty({std::max<int64_t>(pdt_lenet_stem_slab_floats(N, kStemIpb), 1)}, x.options());
+  auto dw = at::empty({6, 1, 5, 5}, x.options());
+  auto db = at::empty({6}, x.options());
+  pdt_lenet_stem_bwd(dy.data_ptr<float>(), code.data_ptr<uint8_t>(), x.data_ptr<float>(), N, kStemIpb,
+                     (float)slope, slab.data_ptr<float>(), dw.data_ptr<float>(), db.data_ptr<float>(), stream());
+  return {dw, db};
+}
+
+std::vector<Tensor> leaky_pool_fwd(Tensor x, double slope) {
+  check_cuda(x, "x");
+  TORCH_CHECK(x.scalar_type() == at::kFloat && x.is_contiguous() && x.dim() == 4, "leaky_pool: contiguous fp32 NCHW");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  auto y = at::empty({N, C, H / 2, W / 2}, x.options());
+  auto code = at::empty({N, C, H / 2, W / 2}, x.options().dtype(at::kByte));
+  pdt_leaky_pool_fwd(x.data_ptr<float>(), N * C, (int)H, (int)W, (float)slope, y.data_ptr<float>(),
+                     code.data_ptr<uint8_t>(), stream());
+  return {y, code};
+}
+
+Tensor leaky_pool_bwd(Tensor dy, Tensor code, int64_t H, int64_t W, double slope) {
+  dy = dy.contiguous();
+  const int64_t N = dy.size(0), C = dy.size(1);
+  TORCH_CHECK(dy.scalar_type() == at::kFloat && dy.size(2) == H / 2 && dy.size(3) == W / 2 &&
+                  code.numel() == dy.numel(), "leaky_pool_bwd: shape mismatch");
+  auto dx = at::empty({N, C, H, W}, dy.options());
+  pdt_leaky_pool_bwd(dy.data_ptr<float>(), code.data_ptr<uint8_t>(), N * C, (int)H, (int)W, (float)slope,
+                     dx.data_ptr<float>(), stream());
+  return dx;
+}
+
+// returns {loss[N] (if want_loss), dlogits (if want_grad)}; acc (fp64 [3]) accumulates eval metrics
+std::vector<Tensor> softmax_nll_small(Tensor logits, Tensor target, int64_t mode, double smoothing, bool want_loss,
+                                      bool want_grad, double dscale, c10::optional<Tensor> acc) {
+  check_cuda(logits, "logits");
+  TORCH_CHECK(logits.dim() == 2 && logits.is_contiguous(), "softmax_nll_small: contiguous [N, V] logits");
+  TORCH_CHECK(logits.size(1) <= 1024, "softmax_nll_small: V <= 1024");
+  TORCH_CHECK(target.scalar_type() == at::kLong && target.is_contiguous(), "softmax_nll_small: int64 target");
+  const int64_t N = logits.size(0);
+  Tensor loss, dl;
+  if (want_loss) loss = at::empty({N}, logits.options().dtype(at::kFloat));
+  if (want_grad) dl = at::empty_like(logits);
+  double* ap = nullptr;
+  if (acc.has_value() && acc->defined()) {
+    TORCH_CHECK(acc->scalar_type() == at::kDouble && acc->numel() >= 3, "softmax_nll_small: acc fp64 [3]");
+    ap = acc->data_ptr<double>();
+  }
+  int rc = pdt_softmax_nll_small(logits.data_ptr(), dcode(logits), target.data_ptr<int64_t>(), N,
+                                 (int)logits.size(1), (int)mode, (float)smoothing,
+                                 want_loss ? loss.data_ptr<float>() : nullptr, want_grad ? dl.data_ptr() : nullptr,
+                                 (float)dscale, ap, stream());
+  TORCH_CHECK(rc == 0, "pdt_softmax_nll_small failed");
+  return {loss, dl};
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -502,4 +589,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bias_gelu_bwd", &bias_gelu_bwd);
   m.def("attn_fwd_out", &attn_fwd_out);
   m.def("attn_bwd_out", &attn_bwd_out);
+  m.def("lenet_stem_fwd", &lenet_stem_fwd);
+  m.def("lenet_stem_bwd", &lenet_stem_bwd);
+  m.def("leaky_pool_fwd", &leaky_pool_fwd);
+  m.def("leaky_pool_bwd", &leaky_pool_bwd);
+  m.def("softmax_nll_small", &softmax_nll_small);
 }

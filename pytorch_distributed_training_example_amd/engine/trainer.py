@@ -27,6 +27,7 @@ import torch.distributed as dist
 from torch import nn
 
 from ..ops.cross_entropy import cross_entropy, nll_on_probs
+from ..ops.lenet import eval_metrics_, softmax_nll
 from ..parallel import launcher
 from ..parallel.reference import average_gradients
 from .amp import autocast_ctx
@@ -35,8 +36,12 @@ from .amp import autocast_ctx
 def make_loss_fn(kind: str) -> Callable[[torch.Tensor, torch.Tensor], torch.Tensor]:
     if kind == "nll_on_probs":  # reference: softmax output + nll_loss (train.py:48)
         return lambda out, y: nll_on_probs(out.float(), y)
+    if kind == "prob_nll":  # the reference's loss computed from logits (ops/lenet.py, one fused kernel)
+        return lambda out, y: softmax_nll(out, y, "prob_nll")
     if kind == "cross_entropy":
-        return lambda out, y: cross_entropy(out, y)
+        # small class counts (LeNet's 10): one wave per row, loss and gradient in one pass
+        return lambda out, y: softmax_nll(out, y, "ce") if out.dim() == 2 and out.shape[-1] <= 64 \
+            else cross_entropy(out, y)
     if kind.startswith("cross_entropy_ls"):
         ls = float(kind.split("=")[1]) if "=" in kind else 0.1
         return lambda out, y: cross_entropy(out, y, label_smoothing=ls)
@@ -158,6 +163,10 @@ def evaluate(model: nn.Module, loader, device, loss_kind: str = "cross_entropy",
             data = data.contiguous(memory_format=torch.channels_last)
         with autocast_ctx(autocast):
             out = model(data)
+        if loss_kind in ("cross_entropy", "prob_nll") and out.dim() == 2 and out.shape[-1] <= 1024:
+            # fused on-device loss-sum / correct / count (one kernel, no per-batch sync)
+            eval_metrics_(acc, out, target, "ce" if loss_kind == "cross_entropy" else "prob_nll")
+            continue
         if loss_kind == "nll_on_probs":
             l = nll_on_probs(out.float(), target, reduction="sum")
         else:

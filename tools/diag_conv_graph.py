@@ -4,14 +4,21 @@ import sys
 
 import torch
 
-torch.backends.cudnn.benchmark = True
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 64
+torch.backends.cudnn.benchmark = bool(int(sys.argv[2])) if len(sys.argv) > 2 else True
+SET = sys.argv[3] if len(sys.argv) > 3 else "r50"
+# (c_in, c_out, kernel, stride, input size); r18s = ResNet-18 at 64x64 input (tests/test_graph_gpu.py)
+R18S = [(3, 64, 7, 2, 64), (64, 64, 3, 1, 16), (64, 128, 3, 2, 16), (64, 128, 1, 2, 16), (128, 128, 3, 1, 8),
+        (128, 256, 3, 2, 8), (128, 256, 1, 2, 8), (256, 256, 3, 1, 4), (256, 512, 3, 2, 4), (256, 512, 1, 2, 4),
+        (512, 512, 3, 1, 2)]
 shapes = [(3, 64, 7, 2, 224), (64, 64, 1, 1, 56), (64, 64, 3, 1, 56), (64, 256, 1, 1, 56), (256, 64, 1, 1, 56),
           (256, 128, 1, 1, 56), (128, 128, 3, 2, 56), (128, 512, 1, 1, 28), (256, 512, 1, 2, 56),
           (512, 128, 1, 1, 28), (128, 128, 3, 1, 28), (512, 256, 1, 1, 28), (256, 256, 3, 2, 28),
           (256, 1024, 1, 1, 14), (512, 1024, 1, 2, 28), (1024, 256, 1, 1, 14), (256, 256, 3, 1, 14),
           (1024, 512, 1, 1, 14), (512, 512, 3, 2, 14), (512, 2048, 1, 1, 7), (1024, 2048, 1, 2, 14),
           (2048, 512, 1, 1, 7), (512, 512, 3, 1, 7)]
+if SET == "r18s":
+    shapes = R18S
 bad = []
 tot = 0.0
 for (ci, co, k, s, h) in shapes:
