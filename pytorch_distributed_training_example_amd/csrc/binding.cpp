@@ -64,6 +64,7 @@ int pdt_bias_gelu_fwd(const void* x, int dtype, const float* bias, void* y, int6
                       hipStream_t s);
 int pdt_bias_gelu_bwd(const void* dy, const void* x, int dtype, const float* bias, void* dx, float* dbias,
                       int64_t N, int D, int tanh_form, float* ws, hipStream_t s);
+int pdt_colsum(const void* x, int dtype, int64_t N, int D, void* out, int odtype, float* ws, hipStream_t s);
 int pdt_lenet_stem_fwd(const float* x, const float* w, const float* b, int64_t N, float slope, float* y,
                        uint8_t* code, hipStream_t s);
 int64_t pdt_lenet_stem_slab_floats(int64_t N, int ipb);
@@ -489,6 +490,19 @@ void attn_bwd_out(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor ls
   TORCH_CHECK(rc == 0, "pdt_attn_bwd: unsupported head dim ", Dh);
 }
 
+// bias gradient of a Linear layer: column sum of dy [*, D] -> [D] in out_dtype (fp32 / bf16)
+Tensor colsum(Tensor dy, at::ScalarType out_dtype) {
+  check_cuda(dy, "dy");
+  TORCH_CHECK(dy.is_contiguous(), "colsum: contiguous input");
+  const int64_t D = dy.size(-1), N = D ? dy.numel() / D : 0;
+  auto out = at::empty({D}, dy.options().dtype(out_dtype));
+  auto ws = at::empty({std::max<int64_t>(pdt_gelu_workspace_floats(N, (int)D), 1)}, dy.options().dtype(at::kFloat));
+  int rc = pdt_colsum(dy.data_ptr(), dcode(dy), N, (int)D, out.data_ptr(), dcode(out), ws.data_ptr<float>(),
+                      stream());
+  TORCH_CHECK(rc == 0, "pdt_colsum failed (D % 8 != 0?)");
+  return out;
+}
+
 // ---- LeNet (reference model) ops: csrc/kernels/lenet.hip ----
 constexpr int kStemIpb = 4;  // images per workgroup in the conv1 weight-gradient reduction
 
@@ -589,6 +603,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bias_gelu_bwd", &bias_gelu_bwd);
   m.def("attn_fwd_out", &attn_fwd_out);
   m.def("attn_bwd_out", &attn_bwd_out);
+  m.def("colsum", &colsum);
   m.def("lenet_stem_fwd", &lenet_stem_fwd);
   m.def("lenet_stem_bwd", &lenet_stem_bwd);
   m.def("leaky_pool_fwd", &leaky_pool_fwd);

@@ -31,9 +31,12 @@ CAPTURE_UNSAFE_MIOPEN_SOLVERS = (
 
 
 def make_miopen_capture_safe() -> None:
-    """Disable the capture-unsafe MIOpen solvers (call before the first convolution)."""
+    """Disable the capture-unsafe MIOpen solvers (call before the first convolution) and select
+    solvers by measurement (find mode): the immediate-mode heuristic pick for the 3-channel stem's
+    weight gradient also replays wrongly (tests/test_graph_gpu.py, ResNet-18 at 64x64)."""
     for k in CAPTURE_UNSAFE_MIOPEN_SOLVERS:
         os.environ.setdefault(k, "0")
+    torch.backends.cudnn.benchmark = True
 
 
 class StaticStep:

@@ -1,9 +1,10 @@
 """Transformer building blocks shared by ViT-B/16 and GPT-2 (north-star configs 3 and 4).
 
 Not in the reference (LeNet only). MI355X-first choices:
-  * every GEMM is a plain bf16 ``F.linear`` (hipBLASLt, MFMA) with NO fused bias where an
-    epilogue kernel follows: the MLP's first bias is applied inside the fused bias+GELU HIP
-    kernel (ops/gelu.py), so the [tokens, 4·D] activation is read/written once;
+  * every GEMM is a plain bf16 hipBLASLt GEMM (ops/linear.py: bias in the GEMM epilogue, bias
+    gradient on the HIP column-strip kernel) with NO fused bias where an epilogue kernel
+    follows: the MLP's first bias is applied inside the fused bias+GELU HIP kernel
+    (ops/gelu.py), so the [tokens, 4·D] activation is read/written once;
   * LayerNorm is the wave-per-row HIP kernel (ops/layernorm.py) with fp32 parameters;
   * attention goes through ``ops.attention.attention`` ([B, H, T, Dh] bf16);
   * the LM / classifier loss is the fused softmax-cross-entropy kernel.
@@ -20,6 +21,7 @@ from torch import nn
 from ..ops.attention import attention_qkv
 from ..ops.gelu import bias_gelu
 from ..ops.layernorm import LayerNorm
+from ..ops.linear import linear
 
 
 class SelfAttention(nn.Module):
@@ -33,9 +35,9 @@ class SelfAttention(nn.Module):
         self.dropout = dropout
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        qkv = self.c_attn(x)  # [B, T, 3D]; the attention kernels read Q/K/V in place
+        qkv = linear(x, self.c_attn.weight, self.c_attn.bias)  # [B, T, 3D]; attention reads Q/K/V in place
         y = attention_qkv(qkv, self.heads, causal=self.causal, dropout_p=self.dropout if self.training else 0.0)
-        return self.c_proj(y)
+        return linear(y, self.c_proj.weight, self.c_proj.bias)
 
 
 class MLP(nn.Module):
@@ -49,7 +51,7 @@ class MLP(nn.Module):
         h = F.linear(x, self.c_fc.weight)  # bias is fused into the GELU kernel
         b = self.c_fc.bias
         h = bias_gelu(h, b.float() if b is not None and b.dtype != torch.float32 else b, self.approximate)
-        return self.c_proj(h)
+        return linear(h, self.c_proj.weight, self.c_proj.bias)
 
 
 class Block(nn.Module):

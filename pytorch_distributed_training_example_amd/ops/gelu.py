@@ -26,7 +26,7 @@ class _BiasGeluFn(torch.autograd.Function):
 
 def bias_gelu(x: torch.Tensor, bias: Optional[torch.Tensor] = None, approximate: str = "none") -> torch.Tensor:
     tanh_form = approximate == "tanh"
-    if (use_native(x) and x.dtype in (torch.float32, torch.bfloat16) and x.shape[-1] % 4 == 0
+    if (use_native(x) and x.dtype in (torch.float32, torch.bfloat16) and x.shape[-1] % 8 == 0
             and (bias is None or bias.dtype == torch.float32)):
         return _BiasGeluFn.apply(x.contiguous(), bias, tanh_form)
     if bias is not None:

