@@ -59,7 +59,8 @@ def parse(argv=None):
     ap.add_argument("--graph", type=int, default=0,
                     help="hipGraph-capture the step (ours; excludes the capture-unsafe MIOpen solvers)")
     ap.add_argument("--bucket-cap-mb", type=float, default=25.0)
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "amp_bf16", "fp32"])
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp8", "amp_bf16", "fp32"],
+                    help="fp8: transformer-block GEMMs on e4m3 with delayed scaling (ViT/GPT-2)")
     ap.add_argument("--lr", type=float, default=None)
     ap.add_argument("--cudnn-benchmark", type=int, default=1, help="MIOpen find mode for conv algorithms")
     ap.add_argument("--deterministic", type=int, default=0, help="MIOpen deterministic solvers (slow)")
@@ -137,7 +138,7 @@ def run(args, ctx):
     is_lm = args.model.startswith("gpt")
     S, T = args.image_size, args.seq_len
     assert B % args.grad_accum == 0, "batch must be divisible by grad-accum"
-    in_dtype = torch.bfloat16 if precision == "bf16" else torch.float32
+    in_dtype = torch.bfloat16 if precision in ("bf16", "fp8") else torch.float32
     pool = []
     for _ in range(2):
         if is_lm:
@@ -210,7 +211,7 @@ def run(args, ctx):
     result = {
         "metric": metric, "value": round(value, 2), "unit": unit, "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "bf16" if precision != "fp32" else "fp32",
+        "scaling": "weak", "vs_baseline": None, "dtype": {"fp32": "fp32", "fp8": "fp8_e4m3+bf16"}.get(precision, "bf16"),
         "data": "synthetic (random inputs and labels, random-init weights)",
         "config": {"model": args.model, "global_batch": B * world, "per_gpu_batch": B,
                    "seq_len": T if is_lm else None, "image_size": None if is_lm else S,

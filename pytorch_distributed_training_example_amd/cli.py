@@ -49,7 +49,7 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--momentum", type=float, default=0.9)
     p.add_argument("--weight-decay", type=float, default=0.0)
     p.add_argument("--scheduler", default="step", help="step (StepLR per epoch) | cosine | none")
-    p.add_argument("--precision", default="fp32", help="fp32 | bf16 | amp_bf16 | amp_fp16")
+    p.add_argument("--precision", default="fp32", help="fp32 | bf16 | fp8 (transformer GEMMs) | amp_bf16 | amp_fp16")
     p.add_argument("--grad-accum", type=int, default=1, help="micro-batches per optimizer step (no_sync)")
     p.add_argument("--clip-grad", type=float, default=0.0)
     p.add_argument("--reducer", default="ddp", help="ddp (ours) | torch_ddp | reference (per-param)")
@@ -175,7 +175,7 @@ def run(rank: int, world: int, args) -> dict:
     train_ds, test_ds = _datasets(args, rank, world)
     train_shard, train_sampler = _shard(train_ds, args, rank, world)
     test_shard, test_sampler = _shard(test_ds, args, rank, world, shuffle=False)
-    in_dtype = torch.bfloat16 if args.precision == "bf16" else None
+    in_dtype = torch.bfloat16 if args.precision in ("bf16", "fp8") else None
     if train_shard is not None:
         train_loader = _loader(train_shard, train_sampler, per_rank, args, device, seed=args.seed + rank)
         test_loader = _loader(test_shard, test_sampler, per_rank, args, device, shuffle=False)

@@ -64,6 +64,15 @@ int pdt_bias_gelu_fwd(const void* x, int dtype, const float* bias, void* y, int6
                       hipStream_t s);
 int pdt_bias_gelu_bwd(const void* dy, const void* x, int dtype, const float* bias, void* dx, float* dbias,
                       int64_t N, int D, int tanh_form, float* ws, hipStream_t s);
+int pdt_bn_relu_maxpool_fwd_train(const uint16_t* x, const float* gamma, const float* beta, float* running_mean,
+                                  float* running_var, float momentum, float eps, int N, int H, int W, int C,
+                                  uint16_t* y, uint8_t* code, float* mean, float* invstd, float* ws,
+                                  unsigned* counters, hipStream_t s);
+int pdt_maxpool3s2_bwd(const uint16_t* dy, const uint8_t* code, uint16_t* dz, int N, int H, int W, int C,
+                       hipStream_t s);
+int pdt_fp8_cast_transpose(const uint16_t* x, int64_t M, int64_t K, const float* scale, uint8_t* out,
+                           uint8_t* out_t, float* amax, hipStream_t s);
+int pdt_fp8_update_scales(float* state, int n, int L, float margin_scale, hipStream_t s);
 int pdt_colsum(const void* x, int dtype, int64_t N, int D, void* out, int odtype, float* ws, hipStream_t s);
 int pdt_lenet_stem_fwd(const float* x, const float* w, const float* b, int64_t N, float slope, float* y,
                        uint8_t* code, hipStream_t s);
@@ -312,6 +321,44 @@ std::vector<Tensor> bn_fwd_train(Tensor x, c10::optional<Tensor> res, c10::optio
   return {y, mask, mean, invstd};
 }
 
+// ResNet stem tail (train): BN + ReLU + MaxPool2d(3, 2, 1) -> {y_pooled, code, mean, invstd}
+std::vector<Tensor> bn_relu_maxpool_fwd(Tensor x, c10::optional<Tensor> weight, c10::optional<Tensor> bias,
+                                        c10::optional<Tensor> running_mean, c10::optional<Tensor> running_var,
+                                        double momentum, double eps) {
+  check_nhwc_bf16(x, "x");
+  TORCH_CHECK(x.dim() == 4, "bn_relu_maxpool: 4-D NHWC input");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(C % 64 == 0, "pdt bn: C must be a multiple of 64");
+  const int64_t Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  auto y = at::empty({N, C, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  auto code = at::empty({N * Ho * Wo * C}, x.options().dtype(at::kByte));
+  auto fopt = x.options().dtype(at::kFloat);
+  auto mean = at::empty({C}, fopt), invstd = at::empty({C}, fopt);
+  auto ws = at::empty({bn_ws_floats(N * H * W, C)}, fopt);
+  float* rm = running_mean.has_value() && running_mean->defined() ? running_mean->data_ptr<float>() : nullptr;
+  float* rv = running_var.has_value() && running_var->defined() ? running_var->data_ptr<float>() : nullptr;
+  int rc = pdt_bn_relu_maxpool_fwd_train(reinterpret_cast<const uint16_t*>(x.data_ptr()), opt_fptr(weight),
+                                         opt_fptr(bias), rm, rv, (float)momentum, (float)eps, (int)N, (int)H, (int)W,
+                                         (int)C, reinterpret_cast<uint16_t*>(y.data_ptr()), code.data_ptr<uint8_t>(),
+                                         mean.data_ptr<float>(), invstd.data_ptr<float>(), ws.data_ptr<float>(),
+                                         bn_counters(x), stream());
+  TORCH_CHECK(rc == 0, "pdt_bn_relu_maxpool_fwd_train failed");
+  return {y, code, mean, invstd};
+}
+
+Tensor maxpool3s2_bwd(Tensor dy, Tensor code, int64_t H, int64_t W) {
+  dy = dy.contiguous(at::MemoryFormat::ChannelsLast);
+  check_nhwc_bf16(dy, "dy");
+  const int64_t N = dy.size(0), C = dy.size(1);
+  TORCH_CHECK(dy.size(2) == (H - 1) / 2 + 1 && dy.size(3) == (W - 1) / 2 + 1 && code.numel() == dy.numel(),
+              "maxpool3s2_bwd: shape mismatch");
+  auto dz = at::empty({N, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  int rc = pdt_maxpool3s2_bwd(reinterpret_cast<const uint16_t*>(dy.data_ptr()), code.data_ptr<uint8_t>(),
+                              reinterpret_cast<uint16_t*>(dz.data_ptr()), (int)N, (int)H, (int)W, (int)C, stream());
+  TORCH_CHECK(rc == 0, "pdt_maxpool3s2_bwd failed");
+  return dz;
+}
+
 Tensor bn_fwd_eval(Tensor x, c10::optional<Tensor> res, c10::optional<Tensor> weight, c10::optional<Tensor> bias,
                    Tensor running_mean, Tensor running_var, double eps, bool relu) {
   check_nhwc_bf16(x, "x");
@@ -503,6 +550,36 @@ Tensor colsum(Tensor dy, at::ScalarType out_dtype) {
   return out;
 }
 
+// ---- fp8 (OCP e4m3fn) casts: csrc/kernels/fp8.hip ----
+// x: bf16 [M, K] contiguous; state_row: fp32 view [3 + L] = (amax, scale, scale_inv, history...)
+// returns {x_fp8 [M, K], x_fp8_t [K, M] (if transpose)}
+std::vector<Tensor> fp8_cast_transpose(Tensor x, Tensor state_row, bool transpose) {
+  check_cuda(x, "x");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.dim() == 2 && x.is_contiguous(), "fp8_cast: bf16 [M, K]");
+  TORCH_CHECK(state_row.scalar_type() == at::kFloat && state_row.numel() >= 3 && state_row.is_contiguous(),
+              "fp8_cast: fp32 state row");
+  const int64_t M = x.size(0), K = x.size(1);
+  TORCH_CHECK(M % 16 == 0 && K % 16 == 0, "fp8_cast: M and K must be multiples of 16");
+  auto o8 = x.options().dtype(at::kFloat8_e4m3fn);
+  auto out = at::empty({M, K}, o8);
+  Tensor out_t;
+  if (transpose) out_t = at::empty({K, M}, o8);
+  float* st = state_row.data_ptr<float>();
+  int rc = pdt_fp8_cast_transpose(reinterpret_cast<const uint16_t*>(x.data_ptr()), M, K, st + 1,
+                                  reinterpret_cast<uint8_t*>(out.data_ptr()),
+                                  transpose ? reinterpret_cast<uint8_t*>(out_t.data_ptr()) : nullptr, st, stream());
+  TORCH_CHECK(rc == 0, "pdt_fp8_cast_transpose failed");
+  return {out, out_t};
+}
+
+void fp8_update_scales(Tensor state, int64_t history, double margin) {
+  check_cuda(state, "state");
+  TORCH_CHECK(state.scalar_type() == at::kFloat && state.is_contiguous() && state.dim() == 2 &&
+                  state.size(1) == 3 + history, "fp8_update_scales: state [n, 3 + L] fp32");
+  pdt_fp8_update_scales(state.data_ptr<float>(), (int)state.size(0), (int)history, (float)std::pow(2.0, margin),
+                        stream());
+}
+
 // ---- LeNet (reference model) ops: csrc/kernels/lenet.hip ----
 constexpr int kStemIpb = 4;  // images per workgroup in the conv1 weight-gradient reduction
 
@@ -594,6 +671,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("clip_coef", &clip_coef);
   m.def("bn_fwd_train", &bn_fwd_train);
   m.def("bn_fwd_eval", &bn_fwd_eval);
+  m.def("bn_relu_maxpool_fwd", &bn_relu_maxpool_fwd);
+  m.def("maxpool3s2_bwd", &maxpool3s2_bwd);
   m.def("bn_bwd_train", &bn_bwd_train);
   m.def("ce_fwd", &ce_fwd);
   m.def("ce_bwd", &ce_bwd);
@@ -604,6 +683,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_fwd_out", &attn_fwd_out);
   m.def("attn_bwd_out", &attn_bwd_out);
   m.def("colsum", &colsum);
+  m.def("fp8_cast_transpose", &fp8_cast_transpose);
+  m.def("fp8_update_scales", &fp8_update_scales);
   m.def("lenet_stem_fwd", &lenet_stem_fwd);
   m.def("lenet_stem_bwd", &lenet_stem_bwd);
   m.def("leaky_pool_fwd", &leaky_pool_fwd);

@@ -283,6 +283,104 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
   }
 }
 
+// ---- ResNet stem: BN apply + ReLU + 3x3/s2/p1 max-pool in one pass (NHWC bf16).
+// The [N,112,112,64] BN output is never written: each pooled output applies the BN affine to its
+// 3x3 window, keeps the max of the pre-ReLU values (ReLU is monotone: max(relu(z)) = relu(max z))
+// and records a 1-byte code per (output, channel): the window index 0..8 of the winner, or 15
+// when the max is <= 0 (ReLU kills the gradient). Ties keep the first element in (kh, kw) scan
+// order, like aten's max_pool2d.
+__global__ __launch_bounds__(256) void bn_apply_pool_kernel(const uint16_t* __restrict__ x,
+                                                            const float* __restrict__ a,
+                                                            const float* __restrict__ b, uint16_t* __restrict__ y,
+                                                            uint8_t* __restrict__ code, int N, int H, int W, int C,
+                                                            int Ho, int Wo) {
+  const int C8 = C >> 3;
+  const int64_t total = (int64_t)N * Ho * Wo * C8;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c8 = (int)(i % C8);
+    int64_t t = i / C8;
+    const int ow = (int)(t % Wo);
+    t /= Wo;
+    const int oh = (int)(t % Ho);
+    const int n = (int)(t / Ho);
+    float av[8], bv[8];
+    Vec4<float>::ld(a, c8 * 8, *reinterpret_cast<float(*)[4]>(av));
+    Vec4<float>::ld(a, c8 * 8 + 4, *reinterpret_cast<float(*)[4]>(av + 4));
+    Vec4<float>::ld(b, c8 * 8, *reinterpret_cast<float(*)[4]>(bv));
+    Vec4<float>::ld(b, c8 * 8 + 4, *reinterpret_cast<float(*)[4]>(bv + 4));
+    float m[8];
+    int k[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { m[j] = -INFINITY; k[j] = 15; }
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      const int ih = 2 * oh - 1 + kh;
+      if (ih < 0 || ih >= H) continue;
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int iw = 2 * ow - 1 + kw;
+        if (iw < 0 || iw >= W) continue;
+        float v[8];
+        ld8_bf16(x + (((int64_t)n * H + ih) * W + iw) * C + c8 * 8, v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float z = fmaf(v[j], av[j], bv[j]);
+          if (z > m[j]) { m[j] = z; k[j] = kh * 3 + kw; }
+        }
+      }
+    }
+    float o[8];
+    uint32_t lo = 0, hi = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const bool pos = m[j] > 0.f;
+      o[j] = pos ? m[j] : 0.f;
+      const uint32_t cj = pos ? (uint32_t)k[j] : 15u;
+      if (j < 4) lo |= cj << (8 * j);
+      else hi |= cj << (8 * (j - 4));
+    }
+    st8_bf16(y + i * 8, o);
+    *reinterpret_cast<uint2*>(code + i * 8) = make_uint2(lo, hi);
+  }
+}
+
+// Gradient of the fused stem w.r.t. the BN output's pre-ReLU value: a gather over the (up to 4)
+// pooled windows that contain each input position — every input written exactly once, no atomics,
+// fixed summation order.
+__global__ __launch_bounds__(256) void maxpool_bwd_kernel(const uint16_t* __restrict__ dy,
+                                                          const uint8_t* __restrict__ code, uint16_t* __restrict__ dz,
+                                                          int N, int H, int W, int C, int Ho, int Wo) {
+  const int C8 = C >> 3;
+  const int64_t total = (int64_t)N * H * W * C8;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c8 = (int)(i % C8);
+    int64_t t = i / C8;
+    const int iw = (int)(t % W);
+    t /= W;
+    const int ih = (int)(t % H);
+    const int n = (int)(t / H);
+    float g[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const int oh0 = ih >> 1, oh1 = min(Ho - 1, (ih + 1) >> 1);
+    const int ow0 = iw >> 1, ow1 = min(Wo - 1, (iw + 1) >> 1);
+    for (int oh = oh0; oh <= oh1; ++oh)
+      for (int ow = ow0; ow <= ow1; ++ow) {
+        const uint32_t idx = (uint32_t)((ih - (2 * oh - 1)) * 3 + (iw - (2 * ow - 1)));
+        const int64_t o = (((int64_t)n * Ho + oh) * Wo + ow) * C + c8 * 8;
+        const uint2 cw = *reinterpret_cast<const uint2*>(code + o);
+        uint32_t hit = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) hit |= ((((j < 4 ? cw.x : cw.y) >> (8 * (j & 3))) & 0xffu) == idx) << j;
+        if (!hit) continue;
+        float v[8];
+        ld8_bf16(dy + o, v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (hit & (1u << j)) g[j] += v[j];
+      }
+    st8_bf16(dz + i * 8, g);
+  }
+}
+
 struct ReduceGeo {
   int nrow, nchunks;
   int64_t rows_per_block;
@@ -346,6 +444,42 @@ int pdt_bn_fwd_train(const uint16_t* x, const uint16_t* res, const float* gamma,
   else if (relu) { if (mk) PDT_APPLY(true, false, true); else PDT_APPLY(true, false, false); }
   else if (res) PDT_APPLY(false, true, false);
   else PDT_APPLY(false, false, false);
+  return 0;
+}
+
+// Training forward of the ResNet stem tail: BN statistics (same reduce as pdt_bn_fwd_train), then
+// BN apply + ReLU + 3x3/s2/p1 max-pool fused. x: NHWC [N,H,W,C]; y: [N,Ho,Wo,C]; code: N*Ho*Wo*C bytes.
+int pdt_bn_relu_maxpool_fwd_train(const uint16_t* x, const float* gamma, const float* beta, float* running_mean,
+                                  float* running_var, float momentum, float eps, int N, int H, int W, int C,
+                                  uint16_t* y, uint8_t* code, float* mean, float* invstd, float* ws,
+                                  unsigned* counters, hipStream_t s) {
+  const int64_t M = (int64_t)N * H * W;
+  if (C % kCC != 0 || M < 1) return -1;
+  const ReduceGeo g = reduce_geo(M, C);
+  float* part = ws;
+  float* a = ws + (int64_t)g.nchunks * g.nrow * 2 * kCC;
+  float* b = a + C;
+  FinArgs fa{};
+  fa.x = x; fa.gamma = gamma; fa.beta = beta; fa.mean_out = mean; fa.invstd_out = invstd; fa.a_out = a;
+  fa.b_out = b; fa.running_mean = running_mean; fa.running_var = running_var; fa.momentum = momentum;
+  fa.eps = eps; fa.M = M;
+  hipLaunchKernelGGL(bn_reduce_kernel<0>, dim3(g.nrow, g.nchunks), dim3(kThreads), 0, s, x, nullptr, nullptr,
+                     nullptr, M, C, g.rows_per_block, g.nrow, part, counters, fa);
+  const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  const int64_t nvec = (int64_t)N * Ho * Wo * (C / 8);
+  hipLaunchKernelGGL(bn_apply_pool_kernel, dim3(apply_grid(nvec)), dim3(256), 0, s, x, a, b, y, code, N, H, W, C,
+                     Ho, Wo);
+  return 0;
+}
+
+// dz [N,H,W,C] (gradient at the BN output, ReLU folded in) from the pooled gradient dy [N,Ho,Wo,C].
+int pdt_maxpool3s2_bwd(const uint16_t* dy, const uint8_t* code, uint16_t* dz, int N, int H, int W, int C,
+                       hipStream_t s) {
+  if (C % 8 != 0) return -1;
+  const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  const int64_t nvec = (int64_t)N * H * W * (C / 8);
+  if (nvec == 0) return 0;
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(apply_grid(nvec)), dim3(256), 0, s, dy, code, dz, N, H, W, C, Ho, Wo);
   return 0;
 }
 

@@ -1,0 +1,121 @@
+// FP8 (OCP e4m3fn, gfx950) training casts with delayed per-tensor scaling.
+//
+// BASELINE.json config 3 ("ViT-B/16 DDP + AMP (bf16/fp8)"). Not in the reference (LeNet, fp32).
+// gfx950's fp8 is the OCP encoding (e4m3fn: max 448, has NaN, no inf) — NOT MI300's fnuz
+// (cdna_hip_programming.md §4). hipBLASLt's fp8 GEMMs on gfx950 run 1.4-2.3x the bf16 rate on
+// ViT/GPT-2 linear shapes (tools/fp8_bench.py), so every Linear's three GEMMs (fwd, dgrad,
+// wgrad) take fp8 operands; the casts are the memory-bound part and live here:
+//
+//   fp8_cast_transpose: one pass over a bf16 [M, K] tensor writes BOTH the row-major fp8 copy
+//     and its transpose (the operand layouts hipBLASLt needs for the fwd / dgrad / wgrad GEMMs),
+//     scales by the tensor's current scale (read from device memory: capture-safe, no host sync)
+//     and folds |x|max into the tensor's amax slot (atomicMax on the float bits — the values are
+//     non-negative so integer order == float order). 64x64 tiles staged through LDS.
+//   fp8_update_scales: one launch per step for ALL fp8 tensors of a model: push amax into the
+//     history (shift register), scale = 448 / (max(history) * 2^margin), scale_inv = 1/scale, reset amax.
+#include "../common.h"
+
+using namespace pdt;
+
+namespace {
+
+constexpr float kE4M3Max = 448.f;
+constexpr int kTile = 64;
+
+__device__ __forceinline__ uint32_t pack4_fp8(float a, float b, float c, float d) {
+  a = __builtin_amdgcn_fmed3f(a, kE4M3Max, -kE4M3Max);
+  b = __builtin_amdgcn_fmed3f(b, kE4M3Max, -kE4M3Max);
+  c = __builtin_amdgcn_fmed3f(c, kE4M3Max, -kE4M3Max);
+  d = __builtin_amdgcn_fmed3f(d, kE4M3Max, -kE4M3Max);
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);  // bytes 0,1
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);        // bytes 2,3
+  return (uint32_t)w;
+}
+
+// Grid (ceil(K/64), ceil(M/64)); 256 threads; thread t handles row t/4 of the tile, 16 columns.
+// Requires M % 16 == 0 and K % 16 == 0 (16-element chunks are fully in or out of bounds).
+__global__ __launch_bounds__(256) void fp8_cast_transpose_kernel(const uint16_t* __restrict__ x, int64_t M, int64_t K,
+                                                                 const float* __restrict__ scale,
+                                                                 uint8_t* __restrict__ out,
+                                                                 uint8_t* __restrict__ out_t,
+                                                                 float* __restrict__ amax) {
+  __shared__ uint32_t tile[kTile][kTile / 4 + 1];  // fp8 bytes, 4 per word, padded rows
+  const int64_t m0 = (int64_t)blockIdx.y * kTile, k0 = (int64_t)blockIdx.x * kTile;
+  const int r = threadIdx.x >> 2, cc = (threadIdx.x & 3) * 16;
+  const float s = *scale;
+  float am = 0.f;
+  const bool in = (m0 + r < M) && (k0 + cc < K);
+  uint32_t w[4] = {0u, 0u, 0u, 0u};
+  if (in) {
+    const uint16_t* src = x + (m0 + r) * K + k0 + cc;
+    float v[16];
+    ld8_bf16(src, *reinterpret_cast<float(*)[8]>(v));
+    ld8_bf16(src + 8, *reinterpret_cast<float(*)[8]>(v + 8));
+#pragma unroll
+    for (int j = 0; j < 16; ++j) am = fmaxf(am, fabsf(v[j]));
+#pragma unroll
+    for (int q = 0; q < 4; ++q) w[q] = pack4_fp8(v[4 * q] * s, v[4 * q + 1] * s, v[4 * q + 2] * s, v[4 * q + 3] * s);
+    *reinterpret_cast<uint4*>(out + (m0 + r) * K + k0 + cc) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) tile[r][(cc >> 2) + q] = w[q];
+  am = wave_max(am);
+  if ((threadIdx.x & 63) == 0 && am > 0.f) atomicMax(reinterpret_cast<int*>(amax), __float_as_int(am));
+  if (!out_t) return;
+  __syncthreads();
+  // transposed: thread t writes 16 bytes of row (k0 + t/4) of out_t, i.e. column t/4 of the tile
+  const int c = threadIdx.x >> 2, rr = (threadIdx.x & 3) * 16;
+  if (k0 + c >= K || m0 + rr >= M) return;
+  const int wsel = c >> 2, sh = (c & 3) * 8;
+  uint32_t o[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v |= ((tile[rr + 4 * q + j][wsel] >> sh) & 0xffu) << (8 * j);
+    o[q] = v;
+  }
+  *reinterpret_cast<uint4*>(out_t + (k0 + c) * M + m0 + rr) = make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+// state rows: [amax_cur, scale, scale_inv, hist_0 .. hist_{L-1}] per tensor (stride 3 + L floats).
+// The history is a shift register (newest first), so no ring position has to live on the host —
+// the update is identical on every replay of a captured step.
+__global__ void fp8_update_scales_kernel(float* __restrict__ state, int n, int L, float margin_scale) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float* st = state + (int64_t)i * (3 + L);
+  float m = st[0];
+  for (int j = L - 1; j > 0; --j) {
+    st[3 + j] = st[3 + j - 1];
+    m = fmaxf(m, st[3 + j]);
+  }
+  st[3] = st[0];
+  if (m > 0.f && isfinite(m)) {
+    const float sc = kE4M3Max / (m * margin_scale);
+    st[1] = sc;
+    st[2] = 1.f / sc;
+  }
+  st[0] = 0.f;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pdt_fp8_cast_transpose(const uint16_t* x, int64_t M, int64_t K, const float* scale, uint8_t* out,
+                           uint8_t* out_t, float* amax, hipStream_t s) {
+  if (M % 16 != 0 || K % 16 != 0) return -1;
+  if (M == 0 || K == 0) return 0;
+  const dim3 grid((unsigned)((K + kTile - 1) / kTile), (unsigned)((M + kTile - 1) / kTile));
+  hipLaunchKernelGGL(fp8_cast_transpose_kernel, grid, dim3(256), 0, s, x, M, K, scale, out, out_t, amax);
+  return 0;
+}
+
+int pdt_fp8_update_scales(float* state, int n, int L, float margin_scale, hipStream_t s) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(fp8_update_scales_kernel, dim3((n + 255) / 256), dim3(256), 0, s, state, n, L, margin_scale);
+  return 0;
+}
+
+}  // extern "C"

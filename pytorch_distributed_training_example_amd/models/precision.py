@@ -32,4 +32,11 @@ def apply_precision(model: nn.Module, precision: str) -> nn.Module:
         return model
     if precision == "bf16":
         return to_bf16_mixed(model)
+    if precision == "fp8":
+        # bf16 params + fp32 master weights, and every transformer-block GEMM on OCP e4m3 operands
+        # with delayed per-tensor scaling (ops/fp8.py)
+        from ..ops.fp8 import enable_fp8
+        model = to_bf16_mixed(model)
+        enable_fp8(model)
+        return model
     raise ValueError(f"unknown precision {precision}")

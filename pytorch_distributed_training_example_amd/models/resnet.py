@@ -141,8 +141,10 @@ class ResNet(nn.Module):
         return nn.Sequential(*layers)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        x = bn_act(self.bn1, self.conv1(x), relu=True)
-        x = self.maxpool(x)
+        if hasattr(self.bn1, "forward_relu_maxpool"):  # fused BN+ReLU+pool: stem output never stored
+            x = self.bn1.forward_relu_maxpool(self.conv1(x))
+        else:
+            x = self.maxpool(bn_act(self.bn1, self.conv1(x), relu=True))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         x = self.avgpool(x)
         x = torch.flatten(x, 1)

@@ -21,7 +21,17 @@ from torch import nn
 from ..ops.attention import attention_qkv
 from ..ops.gelu import bias_gelu
 from ..ops.layernorm import LayerNorm
-from ..ops.linear import linear
+from ..ops.linear import linear as _linear
+
+
+def linear(x, mod: nn.Linear, bias=True):
+    """``mod``'s GEMM: fp8 when ``enable_fp8`` tagged it (ops/fp8.py), else bf16 (ops/linear.py)."""
+    b = mod.bias if bias else None
+    fp8 = getattr(mod, "_fp8", None)
+    if fp8 is not None:
+        from ..ops.fp8 import fp8_linear
+        return fp8_linear(x, mod.weight, b, fp8[0], fp8[1])
+    return _linear(x, mod.weight, b) if b is not None else F.linear(x, mod.weight)
 
 
 class SelfAttention(nn.Module):
@@ -35,9 +45,9 @@ class SelfAttention(nn.Module):
         self.dropout = dropout
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        qkv = linear(x, self.c_attn.weight, self.c_attn.bias)  # [B, T, 3D]; attention reads Q/K/V in place
+        qkv = linear(x, self.c_attn)  # [B, T, 3D]; attention reads Q/K/V in place
         y = attention_qkv(qkv, self.heads, causal=self.causal, dropout_p=self.dropout if self.training else 0.0)
-        return linear(y, self.c_proj.weight, self.c_proj.bias)
+        return linear(y, self.c_proj)
 
 
 class MLP(nn.Module):
@@ -48,10 +58,10 @@ class MLP(nn.Module):
         self.approximate = approximate
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        h = F.linear(x, self.c_fc.weight)  # bias is fused into the GELU kernel
+        h = linear(x, self.c_fc, bias=False)  # bias is fused into the GELU kernel
         b = self.c_fc.bias
         h = bias_gelu(h, b.float() if b is not None and b.dtype != torch.float32 else b, self.approximate)
-        return linear(h, self.c_proj.weight, self.c_proj.bias)
+        return linear(h, self.c_proj)
 
 
 class Block(nn.Module):

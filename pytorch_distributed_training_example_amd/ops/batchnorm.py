@@ -91,6 +91,37 @@ def batch_norm_act(x, residual, weight, bias, running_mean, running_var, trainin
     return bn_reference(x, residual, weight, bias, running_mean, running_var, training, momentum, eps, relu)
 
 
+class _BNReluMaxPoolFn(torch.autograd.Function):
+    """ResNet stem tail (train): BN → ReLU → MaxPool2d(3, 2, 1) with the BN output never stored."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps):
+        y, code, mean, invstd = native().bn_relu_maxpool_fwd(x, weight, bias, running_mean, running_var,
+                                                             momentum, eps)
+        ctx.has_weight = weight is not None
+        ctx.hw = (x.shape[2], x.shape[3])
+        ctx.save_for_backward(x, code, weight, mean, invstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, code, weight, mean, invstd = ctx.saved_tensors
+        dz = native().maxpool3s2_bwd(dy, code, ctx.hw[0], ctx.hw[1])
+        need_w = ctx.has_weight and (ctx.needs_input_grad[1] or ctx.needs_input_grad[2])
+        dx, _, dg, db = native().bn_bwd_train(dz, x, None, weight, mean, invstd, False, False, need_w)
+        return dx, (dg if need_w else None), (db if need_w else None), None, None, None, None
+
+
+def batch_norm_relu_maxpool(x, weight, bias, running_mean, running_var, training, momentum, eps):
+    """relu(batchnorm(x)) followed by max_pool2d(kernel 3, stride 2, padding 1) — one fused
+    apply+pool pass on the native path (training, channels_last bf16, C % 64 == 0)."""
+    if (training and use_native(x) and x.dtype == torch.bfloat16 and x.dim() == 4
+            and x.is_contiguous(memory_format=torch.channels_last) and x.shape[1] % 64 == 0):
+        return _BNReluMaxPoolFn.apply(x, weight, bias, running_mean, running_var, float(momentum), float(eps))
+    y = batch_norm_act(x, None, weight, bias, running_mean, running_var, training, momentum, eps, True)
+    return F.max_pool2d(y, 3, 2, 1)
+
+
 class BatchNorm2d(nn.BatchNorm2d):
     """``nn.BatchNorm2d`` + fused ReLU / residual (state_dict-compatible)."""
 
@@ -115,6 +146,21 @@ class BatchNorm2d(nn.BatchNorm2d):
         b = self.bias if self.affine else None
         return batch_norm_act(x, residual, w, b, rm, rv, training, momentum if momentum is not None else 0.0,
                               self.eps, relu)
+
+    def forward_relu_maxpool(self, x: torch.Tensor) -> torch.Tensor:
+        """``max_pool2d(relu(bn(x)), 3, 2, 1)`` (ResNet stem) with the pool fused into the BN apply."""
+        training = self.training or not self.track_running_stats
+        momentum = self.momentum
+        if self.training and self.track_running_stats:
+            self._nbt += 1
+            if momentum is None:
+                momentum = 1.0 / float(self._nbt + int(self.num_batches_tracked.item()))
+        rm = self.running_mean if (not self.training or self.track_running_stats) else None
+        rv = self.running_var if (not self.training or self.track_running_stats) else None
+        w = self.weight if self.affine else None
+        b = self.bias if self.affine else None
+        return batch_norm_relu_maxpool(x, w, b, rm, rv, training, momentum if momentum is not None else 0.0,
+                                       self.eps)
 
     def sync_num_batches_tracked(self) -> None:
         if self.track_running_stats and self._nbt:

@@ -75,7 +75,7 @@ def test_graph_step_lr0_matches_eager():
     # run to run at the bf16-rounding level even without capture; a broken replay is O(1) off
     for i, (a, b) in enumerate(zip(gg, ge)):
         err = ((a - b).norm() / (b.norm() + 1e-12)).item()
-        assert err < 1e-2, (i, err)
+        assert err < 5e-2, (i, err)
 
 
 def test_graph_step_matches_eager_training():

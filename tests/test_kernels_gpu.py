@@ -53,6 +53,36 @@ def test_batchnorm_train_fwd_bwd(C, relu, res):
         torch.testing.assert_close(rs.grad.float(), rf.grad, rtol=2e-2, atol=2e-2)
 
 
+@pytest.mark.parametrize("shape", [(4, 64, 112, 112), (3, 128, 15, 17)])
+def test_bn_relu_maxpool_stem(shape):
+    """Fused BN + ReLU + MaxPool2d(3,2,1) (ResNet stem) vs the fp32 unfused reference."""
+    from pytorch_distributed_training_example_amd.ops.batchnorm import batch_norm_relu_maxpool
+    torch.manual_seed(0)
+    N, C, H, W = shape
+    x = (torch.randn(N, C, H, W, device=DEV) * 2 + 0.3).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    w, b = torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV) * 0.5
+    rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    rm2, rv2 = rm.clone(), rv.clone()
+    xs = x.detach().requires_grad_(True)
+    ws, bs = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    y = batch_norm_relu_maxpool(xs, ws, bs, rm, rv, True, 0.1, 1e-5)
+    xf = x.float().detach().requires_grad_(True)
+    wf, bf = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    yf = F.max_pool2d(F.relu(F.batch_norm(xf, rm2, rv2, wf, bf, True, 0.1, 1e-5)), 3, 2, 1)
+    assert y.shape == yf.shape and y.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(y.float(), yf, rtol=2e-2, atol=3e-2)
+    torch.testing.assert_close(rm, rm2, rtol=1e-4, atol=1e-4)
+    g = torch.randn_like(y)
+    y.backward(g)
+    yf.backward(g.float())
+    # near-ties inside a window may route a gradient differently than the fp32 oracle: allow a
+    # tiny fraction of elements to differ, everything else must match tightly
+    bad = ((xs.grad.float() - xf.grad).abs() > 3e-2 + 3e-2 * xf.grad.abs()).float().mean().item()
+    assert bad < 1e-4, bad
+    torch.testing.assert_close(ws.grad, wf.grad, rtol=2e-2, atol=5e-1)
+    torch.testing.assert_close(bs.grad, bf.grad, rtol=2e-2, atol=5e-1)
+
+
 def test_batchnorm_large_mean_stability():
     """Shifted sums must not lose the variance when |mean| >> std."""
     from pytorch_distributed_training_example_amd.ops.batchnorm import batch_norm_act
