@@ -14,6 +14,7 @@ both sides; the reported time is the MAX over ranks; ``value`` is the total over
 (weak scaling: per-GPU batch fixed).
 
 --model resnet50 (default, headline) | vit_b16 | gpt2_medium (other north-star configs)
+        | lenet (the reference's own LeNet/MNIST workload, fp32, Adadelta)
 --impl ours       : this framework (DDP reducer, HIP BN/LN/GELU/CE/optimizer kernels, bf16 params +
                     fp32 master weights)
 --impl torch_ddp  : stock torch.nn.parallel.DistributedDataParallel + autocast bf16 + stock
@@ -42,6 +43,9 @@ WORKLOADS = {
     "resnet50": ("images/sec (whole node) ResNet-50 DDP", "images/sec", 256, "sgd"),
     "vit_b16": ("images/sec (whole node) ViT-B/16 DDP", "images/sec", 128, "adamw"),
     "gpt2_medium": ("tokens/sec (whole node) GPT-2-medium DDP", "tokens/sec", 8, "adamw"),
+    # the reference's own workload (train.py:82-105): LeNet on MNIST-shaped data, fp32, Adadelta,
+    # nll_loss on softmax probabilities, global batch 1024 = 128 per GPU at 8 GPUs
+    "lenet": ("images/sec (whole node) LeNet-MNIST DDP (reference workload)", "images/sec", 128, "adadelta"),
 }
 
 
@@ -77,23 +81,31 @@ def build(args, ctx):
     kw = {}
     if args.model.startswith("resnet"):
         kw["norm"] = "pdt" if args.impl == "ours" else "torch"  # stock baseline uses nn.BatchNorm2d
+    if args.model == "lenet":  # ours: fused kernels + reference loss from logits; stock: cnn.py as-is
+        kw = dict(output="logits") if args.impl == "ours" else dict(output="probs", fused=False)
     model = get_model(args.model, **kw).to(dev)
     if args.model.startswith("resnet"):
         model = model.to(memory_format=torch.channels_last)
     precision = args.precision
+    if args.model == "lenet":
+        precision = "fp32"  # the reference trains LeNet in fp32
     if args.impl != "ours" and precision == "bf16":
         precision = "amp_bf16"  # stock path: fp32 params + autocast (what torch users run)
     model = apply_precision(model, precision)
     world = ctx.world_size
     opt_name = WORKLOADS[args.model][3]
-    lr = args.lr if args.lr is not None else (0.1 if opt_name == "sgd" else 1e-4)
+    lr = args.lr if args.lr is not None else (0.1 if opt_name in ("sgd", "adadelta") else 1e-4)
     if args.impl == "ours":
-        from pytorch_distributed_training_example_amd.optim import FusedAdamW, FusedSGD
+        from pytorch_distributed_training_example_amd.optim import FusedAdadelta, FusedAdamW, FusedSGD
         from pytorch_distributed_training_example_amd.parallel import DistributedDataParallel
         ddp = DistributedDataParallel(model, bucket_cap_mb=args.bucket_cap_mb, broadcast_buffers=False,
                                       gradient_as_bucket_view=True)
-        opt = FusedSGD(model.parameters(), lr=lr, momentum=0.9, weight_decay=5e-5) if opt_name == "sgd" \
-            else FusedAdamW(model.parameters(), lr=lr, weight_decay=0.1)
+        if opt_name == "sgd":
+            opt = FusedSGD(model.parameters(), lr=lr, momentum=0.9, weight_decay=5e-5)
+        elif opt_name == "adadelta":
+            opt = FusedAdadelta(model.parameters(), lr=lr)
+        else:
+            opt = FusedAdamW(model.parameters(), lr=lr, weight_decay=0.1)
     else:
         if args.impl == "torch_ddp" and world > 1:
             ddp = torch.nn.parallel.DistributedDataParallel(model, device_ids=[dev.index],
@@ -101,8 +113,12 @@ def build(args, ctx):
                                                             broadcast_buffers=False, gradient_as_bucket_view=True)
         else:
             ddp = model
-        opt = torch.optim.SGD(model.parameters(), lr=lr, momentum=0.9, weight_decay=5e-5) if opt_name == "sgd" \
-            else torch.optim.AdamW(model.parameters(), lr=lr, weight_decay=0.1, fused=True)
+        if opt_name == "sgd":
+            opt = torch.optim.SGD(model.parameters(), lr=lr, momentum=0.9, weight_decay=5e-5)
+        elif opt_name == "adadelta":
+            opt = torch.optim.Adadelta(model.parameters(), lr=lr)
+        else:
+            opt = torch.optim.AdamW(model.parameters(), lr=lr, weight_decay=0.1, fused=True)
     return model, ddp, opt, precision
 
 
@@ -144,6 +160,9 @@ def run(args, ctx):
         if is_lm:
             x = torch.randint(0, 50257, (B, T), device=dev, generator=g)
             y = torch.randint(0, 50257, (B, T), device=dev, generator=g)
+        elif args.model == "lenet":
+            x = torch.randn(B, 1, 28, 28, device=dev, generator=g)
+            y = torch.randint(0, 10, (B,), device=dev, generator=g)
         else:
             x = torch.randn(B, 3, S, S, device=dev, generator=g).to(in_dtype)
             if args.model.startswith("resnet"):
@@ -154,6 +173,11 @@ def run(args, ctx):
     ls = 0.1 if args.model.startswith("resnet") else 0.0
 
     def loss_of(out, y):
+        if args.model == "lenet":  # reference loss: nll_loss on softmax probabilities (train.py:48)
+            if args.impl == "ours":
+                from pytorch_distributed_training_example_amd.ops.lenet import softmax_nll
+                return softmax_nll(out, y, "prob_nll")
+            return torch.nn.functional.nll_loss(out, y)
         if is_lm:
             out, y = out.reshape(-1, out.shape[-1]), y.reshape(-1)
         if args.impl == "ours":

@@ -71,6 +71,12 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--check-sync", action="store_true", help="verify replicas are identical after each epoch")
     p.add_argument("--channels-last", action="store_true")
     p.add_argument("--timeout", type=float, default=600.0, help="process-group timeout (s)")
+    p.add_argument("--amp", default=None, choices=["off", "bf16", "fp8"],
+                   help="alias: off=fp32, bf16=bf16 params+fp32 master, fp8=bf16+e4m3 transformer GEMMs")
+    p.add_argument("--hipgraph", action="store_true",
+                   help="replay each train step as one hipGraph (static shapes; MIOpen capture-safe solvers)")
+    p.add_argument("--profile", default=None, metavar="DIR",
+                   help="torch.profiler trace of a few steps of epoch 1 into DIR (rank 0), roctx ranges on")
     return p
 
 
@@ -171,6 +177,8 @@ def run(rank: int, world: int, args) -> dict:
                      StepConfig(precision=args.precision, grad_accum=args.grad_accum,
                                 reducer=args.reducer if launcher.context().distributed else "none",
                                 clip_grad=args.clip_grad), scaler=scaler, raw_model=model)
+    if args.hipgraph and device.type == "cuda":
+        step.enable_graph()
 
     train_ds, test_ds = _datasets(args, rank, world)
     train_shard, train_sampler = _shard(train_ds, args, rank, world)
@@ -203,9 +211,17 @@ def run(rank: int, world: int, args) -> dict:
     injector = FaultInjector(rank=rank)
     gstep = [0]
 
+    prof = None
+    if args.profile and rank == 0:
+        from .utils.profiling import torch_profiler
+        prof = torch_profiler(args.profile)
+        prof.__enter__()
+
     def on_step(epoch, batch_idx):
         gstep[0] += 1
         injector.maybe_fail(gstep[0])
+        if prof is not None:
+            prof.step()
 
     result = {}
     for epoch in range(start_epoch, args.epochs + 1):
@@ -228,6 +244,9 @@ def run(rank: int, world: int, args) -> dict:
             check_replicas_in_sync(list(model.parameters()))
         if args.checkpoint:
             save_checkpoint(args.checkpoint, model, optimizer, scheduler, scaler, train_sampler, epoch=epoch)
+    if prof is not None:
+        prof.__exit__(None, None, None)
+        print(f"profiler trace written to {args.profile}", flush=True)
     if args.save_model:
         save_model(model, args.save_path, rank)
     metrics.close()
@@ -240,6 +259,15 @@ def _entry(rank: int, world: int, args) -> None:
 
 def main(argv: Optional[list] = None) -> int:
     args = build_parser().parse_args(argv)
+    if args.amp is not None:
+        args.precision = {"off": "fp32", "bf16": "bf16", "fp8": "fp8"}[args.amp]
+    if args.hipgraph:
+        # MIOpen reads its solver switches once per process: set before any convolution
+        from .engine.graph import make_miopen_capture_safe
+        make_miopen_capture_safe()
+    if args.profile:
+        from .utils import profiling
+        profiling.enable_ranges(True)
     use_gpu = not args.no_cuda and torch.cuda.is_available()
     if "RANK" in os.environ and "WORLD_SIZE" in os.environ:  # torchrun
         ctx = launcher.init_distributed(backend=args.backend, use_gpu=use_gpu, timeout_s=args.timeout)

@@ -30,6 +30,7 @@ from ..ops.cross_entropy import cross_entropy, nll_on_probs
 from ..ops.lenet import eval_metrics_, softmax_nll
 from ..parallel import launcher
 from ..parallel.reference import average_gradients
+from ..utils.profiling import range as prof_range
 from .amp import autocast_ctx
 
 
@@ -69,11 +70,36 @@ class TrainStep:
         self.cfg = cfg
         self.scaler = scaler
 
+        self._graphs = None  # {input signature: StaticStep} when hipGraph mode is on
+
     def zero_grad(self):
         self.opt.zero_grad(set_to_none=True)
 
+    def enable_graph(self, warmup: int = 3) -> None:
+        """Replay the whole step (forward, backward, bucket all-reduces, optimizer) as one hipGraph
+        per input shape (engine/graph.py). Host-side lr changes are pushed to the optimizer's
+        device lr tensors before each replay."""
+        self._graphs = {}
+        self._graph_warmup = warmup
+
     def __call__(self, xs, ys) -> torch.Tensor:
         """xs/ys: a tensor (one micro-batch) or a list of micro-batches."""
+        if self._graphs is not None and torch.is_tensor(xs) and xs.is_cuda:
+            return self._replay(xs, ys)
+        return self._eager(xs, ys)
+
+    def _replay(self, x, y) -> torch.Tensor:
+        from .graph import StaticStep
+        key = (tuple(x.shape), x.dtype, tuple(y.shape), y.dtype)
+        runner = self._graphs.get(key)
+        if runner is None:
+            runner = StaticStep(self._eager, [x, y], warmup=self._graph_warmup)
+            self._graphs[key] = runner
+        if hasattr(self.opt, "sync_lr"):
+            self.opt.sync_lr()
+        return runner(x, y)
+
+    def _eager(self, xs, ys) -> torch.Tensor:
         if torch.is_tensor(xs):
             xs, ys = [xs], [ys]
         self.zero_grad()
@@ -83,11 +109,12 @@ class TrainStep:
             last = i == n - 1
             ctx = self.model.no_sync() if (not last and hasattr(self.model, "no_sync")) else contextlib.nullcontext()
             with ctx:
-                with autocast_ctx(self.cfg.precision):
+                with prof_range("forward"), autocast_ctx(self.cfg.precision):
                     out = self.model(x)
-                loss = self.loss_fn(out, y)
+                    loss = self.loss_fn(out, y)
                 l = loss / n if n > 1 else loss
-                (self.scaler.scale(l) if self.scaler is not None else l).backward()
+                with prof_range("backward"):  # includes the overlapped bucket all-reduces
+                    (self.scaler.scale(l) if self.scaler is not None else l).backward()
             total = loss.detach() if total is None else total + loss.detach()
         if self.cfg.reducer == "reference" and launcher.get_world_size() > 1:
             average_gradients(self.raw_model)
@@ -96,11 +123,12 @@ class TrainStep:
             if self.scaler is not None:
                 self.scaler.unscale_(self.opt)
             clip_grad_norm_([p.grad for p in self.raw_model.parameters() if p.grad is not None], self.cfg.clip_grad)
-        if self.scaler is not None:
-            self.scaler.step(self.opt)
-            self.scaler.update()
-        else:
-            self.opt.step()
+        with prof_range("optimizer"):
+            if self.scaler is not None:
+                self.scaler.step(self.opt)
+                self.scaler.update()
+            else:
+                self.opt.step()
         return total / n
 
 

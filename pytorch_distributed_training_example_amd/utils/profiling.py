@@ -16,9 +16,17 @@ from typing import Iterator, Optional
 import torch
 
 
+_RANGES = [os.environ.get("PDT_ROCTX", "0") == "1"]
+
+
+def enable_ranges(on: bool = True) -> None:
+    """Turn the step-phase roctx ranges (forward / backward / optimizer) on or off."""
+    _RANGES[0] = on
+
+
 @contextlib.contextmanager
 def range(name: str) -> Iterator[None]:  # noqa: A001 - mirrors nvtx.range
-    if torch.cuda.is_available():
+    if _RANGES[0] and torch.cuda.is_available():
         torch.cuda.nvtx.range_push(name)
         try:
             yield

@@ -85,3 +85,16 @@ def test_train_cli_lenet_one_gpu(tmp_path):
     acc = [line for line in r.stdout.splitlines() if "Accuracy" in line][-1]
     correct, total = acc.split("Accuracy: ")[1].split(" ")[0].split("/")
     assert int(correct) > 0.3 * int(total), acc  # learned on synthetic MNIST (chance = 10%)
+
+
+@pytest.mark.parametrize("extra", [["--hipgraph"], ["--loss", "nll_on_probs", "--hipgraph"]])
+def test_train_cli_lenet_hipgraph(tmp_path, extra):
+    """--hipgraph: every train step replays one captured graph (fused LeNet kernels, MIOpen fp32
+    convs, fused Adadelta); training must still learn like the eager run."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "train.py"), "--epochs", "2", "--world-size", "1",
+                        "--train-samples", "20000", "--batch-size", "256", "--log-interval", "20", "--lr", "1.0"]
+                       + extra, capture_output=True, text=True, timeout=600, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-3000:]
+    acc = [line for line in r.stdout.splitlines() if "Accuracy" in line][-1]
+    correct, total = acc.split("Accuracy: ")[1].split(" ")[0].split("/")
+    assert int(correct) > 0.3 * int(total), acc
