@@ -63,6 +63,8 @@ def parse(argv=None):
     ap.add_argument("--graph", type=int, default=0,
                     help="hipGraph-capture the step (ours; excludes the capture-unsafe MIOpen solvers)")
     ap.add_argument("--bucket-cap-mb", type=float, default=25.0)
+    ap.add_argument("--comm-hook", default="none", choices=["none", "p2p"],
+                    help="p2p: one-shot xGMI P2P all-reduce for buckets <= 1 MiB, RCCL above (ours, N>1)")
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp8", "amp_bf16", "fp32"],
                     help="fp8: transformer-block GEMMs on e4m3 with delayed scaling (ViT/GPT-2)")
     ap.add_argument("--lr", type=float, default=None)
@@ -100,6 +102,11 @@ def build(args, ctx):
         from pytorch_distributed_training_example_amd.parallel import DistributedDataParallel
         ddp = DistributedDataParallel(model, bucket_cap_mb=args.bucket_cap_mb, broadcast_buffers=False,
                                       gradient_as_bucket_view=True)
+        if args.comm_hook == "p2p" and world > 1:
+            from pytorch_distributed_training_example_amd.parallel.p2p import (P2PAllReduce, P2PHookState,
+                                                                                p2p_allreduce_hook)
+            ddp.register_comm_hook(P2PHookState(P2PAllReduce(capacity_bytes=2 << 20), max_bytes=1 << 20),
+                                   p2p_allreduce_hook)
         if opt_name == "sgd":
             opt = FusedSGD(model.parameters(), lr=lr, momentum=0.9, weight_decay=5e-5)
         elif opt_name == "adadelta":
@@ -241,6 +248,7 @@ def run(args, ctx):
                    "seq_len": T if is_lm else None, "image_size": None if is_lm else S,
                    "parallelism": f"dp{world}", "grad_accum": args.grad_accum, "impl": args.impl,
                    "graph": bool(runner is not None), "precision": precision, "bucket_cap_mb": args.bucket_cap_mb,
+                   "comm_hook": args.comm_hook,
                    "deterministic": bool(det), "final_loss": round(float(loss.float().item()), 4)},
     }
     return result

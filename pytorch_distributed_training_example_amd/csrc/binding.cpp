@@ -7,6 +7,7 @@
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 
+#include <cstring>
 #include <map>
 #include <vector>
 
@@ -73,6 +74,10 @@ int pdt_maxpool3s2_bwd(const uint16_t* dy, const uint8_t* code, uint16_t* dz, in
 int pdt_fp8_cast_transpose(const uint16_t* x, int64_t M, int64_t K, const float* scale, uint8_t* out,
                            uint8_t* out_t, float* amax, hipStream_t s);
 int pdt_fp8_update_scales(float* state, int n, int L, float margin_scale, hipStream_t s);
+int64_t pdt_p2p_flags_bytes();
+int pdt_p2p_allreduce(const void* in, void* out, int64_t n, int dtype, char* const* data_ptrs,
+                      uint32_t* const* flag_ptrs, int rank, int world, int64_t cap, uint32_t epoch,
+                      float post_scale, int* err, int max_blocks, hipStream_t s);
 int pdt_colsum(const void* x, int dtype, int64_t N, int D, void* out, int odtype, float* ws, hipStream_t s);
 int pdt_lenet_stem_fwd(const float* x, const float* w, const float* b, int64_t N, float slope, float* y,
                        uint8_t* code, hipStream_t s);
@@ -580,6 +585,113 @@ void fp8_update_scales(Tensor state, int64_t history, double margin) {
                         stream());
 }
 
+// ---- intra-node P2P all-reduce (csrc/kernels/p2p.hip) ----
+#define PDT_HIP_CHECK(expr)                                                            \
+  do {                                                                                 \
+    hipError_t e_ = (expr);                                                            \
+    TORCH_CHECK(e_ == hipSuccess, "pdt p2p: ", #expr, " failed: ", hipGetErrorString(e_)); \
+  } while (0)
+
+struct DevGuard {  // select `dev` for the scope, restore the caller's device after
+  int prev = 0;
+  explicit DevGuard(int dev) {
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(dev);
+  }
+  ~DevGuard() { (void)hipSetDevice(prev); }
+};
+
+class P2PComm {
+ public:
+  P2PComm(int rank, int world, int64_t capacity_bytes, int max_blocks, int device)
+      : rank_(rank), world_(world), cap_(capacity_bytes), max_blocks_(max_blocks), device_(device) {
+    TORCH_CHECK(world >= 1 && world <= 8 && rank >= 0 && rank < world, "p2p: 1 <= world <= 8");
+    TORCH_CHECK(capacity_bytes % 16 == 0, "p2p: capacity must be a multiple of 16 bytes");
+    DevGuard guard(device_);
+    flags_bytes_ = pdt_p2p_flags_bytes();
+    // uncached: peers poll/read these over xGMI; no stale L2 lines on either side
+    PDT_HIP_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&flags_), flags_bytes_, hipDeviceMallocUncached));
+    PDT_HIP_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&data_), 2 * cap_, hipDeviceMallocUncached));
+    PDT_HIP_CHECK(hipMemset(flags_, 0, flags_bytes_));
+    PDT_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&err_), sizeof(int)));
+    PDT_HIP_CHECK(hipMemset(err_, 0, sizeof(int)));
+    PDT_HIP_CHECK(hipDeviceSynchronize());
+    data_ptrs_.assign(world_, nullptr);
+    flag_ptrs_.assign(world_, nullptr);
+    data_ptrs_[rank_] = data_;
+    flag_ptrs_[rank_] = flags_;
+  }
+  ~P2PComm() {
+    for (int r = 0; r < world_; ++r)
+      if (r != rank_) {
+        if (data_ptrs_[r]) (void)hipIpcCloseMemHandle(data_ptrs_[r]);
+        if (flag_ptrs_[r]) (void)hipIpcCloseMemHandle(flag_ptrs_[r]);
+      }
+    (void)hipFree(flags_);
+    (void)hipFree(data_);
+    (void)hipFree(err_);
+  }
+  // 2 x hipIpcMemHandle_t (data, flags) as bytes, to be exchanged through the c10d store
+  py::bytes handles() const {
+    hipIpcMemHandle_t h[2];
+    PDT_HIP_CHECK(hipIpcGetMemHandle(&h[0], data_));
+    PDT_HIP_CHECK(hipIpcGetMemHandle(&h[1], flags_));
+    return py::bytes(reinterpret_cast<const char*>(h), sizeof(h));
+  }
+  void open(const std::vector<py::bytes>& all) {
+    TORCH_CHECK((int)all.size() == world_, "p2p: need one handle blob per rank");
+    DevGuard guard(device_);
+    for (int r = 0; r < world_; ++r) {
+      if (r == rank_) continue;
+      std::string b = all[r];
+      TORCH_CHECK(b.size() == 2 * sizeof(hipIpcMemHandle_t), "p2p: bad handle blob");
+      hipIpcMemHandle_t h[2];
+      std::memcpy(h, b.data(), sizeof(h));
+      void* d = nullptr;
+      void* f = nullptr;
+      PDT_HIP_CHECK(hipIpcOpenMemHandle(&d, h[0], hipIpcMemLazyEnablePeerAccess));
+      PDT_HIP_CHECK(hipIpcOpenMemHandle(&f, h[1], hipIpcMemLazyEnablePeerAccess));
+      data_ptrs_[r] = static_cast<char*>(d);
+      flag_ptrs_[r] = static_cast<uint32_t*>(f);
+    }
+    opened_ = true;
+  }
+  // out = post_scale * sum over ranks of `in` (out may alias in); enqueued on the current stream
+  void allreduce(Tensor in, Tensor out, double post_scale) {
+    TORCH_CHECK(opened_ || world_ == 1, "p2p: open() the peer handles first");
+    check_cuda(in, "in");
+    TORCH_CHECK(in.is_contiguous() && out.is_contiguous() && in.numel() == out.numel() &&
+                    in.scalar_type() == out.scalar_type(), "p2p: contiguous in/out of equal size and dtype");
+    TORCH_CHECK(in.numel() % 8 == 0, "p2p: numel must be a multiple of 8");
+    TORCH_CHECK(in.numel() * in.element_size() <= cap_, "p2p: tensor larger than the staging capacity");
+    ++epoch_;
+    int rc = pdt_p2p_allreduce(in.data_ptr(), out.data_ptr(), in.numel(), dcode(in), data_ptrs_.data(),
+                               flag_ptrs_.data(), rank_, world_, cap_, epoch_, (float)post_scale, err_,
+                               max_blocks_, stream());
+    TORCH_CHECK(rc == 0, "pdt_p2p_allreduce failed (", rc, ")");
+  }
+  // 1 if any peer failed to arrive within the spin limit since the last reset (host sync)
+  int error() {
+    int h = 0;
+    PDT_HIP_CHECK(hipMemcpy(&h, err_, sizeof(int), hipMemcpyDeviceToHost));
+    return h;
+  }
+  int64_t capacity() const { return cap_; }
+
+ private:
+  int rank_, world_;
+  int64_t cap_;
+  int max_blocks_, device_;
+  int64_t flags_bytes_ = 0;
+  char* data_ = nullptr;
+  uint32_t* flags_ = nullptr;
+  int* err_ = nullptr;
+  uint32_t epoch_ = 0;
+  bool opened_ = false;
+  std::vector<char*> data_ptrs_;
+  std::vector<uint32_t*> flag_ptrs_;
+};
+
 // ---- LeNet (reference model) ops: csrc/kernels/lenet.hip ----
 constexpr int kStemIpb = 4;  // images per workgroup in the conv1 weight-gradient reduction
 
@@ -683,6 +795,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_fwd_out", &attn_fwd_out);
   m.def("attn_bwd_out", &attn_bwd_out);
   m.def("colsum", &colsum);
+  py::class_<P2PComm>(m, "P2PComm")
+      .def(py::init<int, int, int64_t, int, int>(), py::arg("rank"), py::arg("world"), py::arg("capacity_bytes"),
+           py::arg("max_blocks"), py::arg("device"))
+      .def("handles", &P2PComm::handles)
+      .def("open", &P2PComm::open)
+      .def("allreduce", &P2PComm::allreduce)
+      .def("error", &P2PComm::error)
+      .def("capacity", &P2PComm::capacity);
   m.def("fp8_cast_transpose", &fp8_cast_transpose);
   m.def("fp8_update_scales", &fp8_update_scales);
   m.def("lenet_stem_fwd", &lenet_stem_fwd);

@@ -1,4 +1,4 @@
-"""Run a function on N gloo ranks (CPU) and collect per-rank results."""
+"""Run a function on N gloo ranks (CPU, or sharing the GPU) and collect per-rank results."""
 import os
 import tempfile
 
@@ -6,11 +6,11 @@ import torch
 import torch.multiprocessing as mp
 
 
-def _entry(rank, world, fn, port, outdir, args):
+def _entry(rank, world, fn, port, outdir, args, use_gpu=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world))
     from pytorch_distributed_training_example_amd.parallel import launcher
-    launcher.init_distributed(backend="gloo", use_gpu=False, timeout_s=120)
+    launcher.init_distributed(backend="gloo", use_gpu=use_gpu, timeout_s=120)
     try:
         out = fn(rank, world, *args)
         torch.save(out, os.path.join(outdir, f"r{rank}.pt"))
@@ -18,9 +18,10 @@ def _entry(rank, world, fn, port, outdir, args):
         launcher.destroy()
 
 
-def run_ranks(fn, world=2, args=()):
+def run_ranks(fn, world=2, args=(), use_gpu=False):
+    """``use_gpu``: ranks bind cuda:(rank % #GPUs) (several ranks may share one GPU) with a gloo group."""
     from pytorch_distributed_training_example_amd.parallel.launcher import find_free_port
     torch.set_num_threads(1)
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_entry, args=(world, fn, find_free_port(), d, tuple(args)), nprocs=world, join=True)
+        mp.spawn(_entry, args=(world, fn, find_free_port(), d, tuple(args), use_gpu), nprocs=world, join=True)
         return [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=False) for r in range(world)]

@@ -5,7 +5,8 @@ step + RCCL bucket-size sweep").
 Two sweeps, one process per GPU (launch with torchrun, 127.0.0.1 rendezvous):
 
   collectives : all-reduce latency / algorithm bandwidth / bus bandwidth per message size
-                (64 KiB … 256 MiB, bf16) — where the per-link-bound ring regime starts on xGMI
+                (64 KiB … 256 MiB, bf16) — where the per-link-bound ring regime starts on xGMI —
+                for RCCL and for the one-shot P2P kernel (parallel/p2p.py) up to its capacity
   train       : full ResNet-50 DDP steps (bench.py's workload, eager or hipGraph) for each
                 ``bucket_cap_mb`` — the end-to-end effect of bucket granularity on overlap
 
@@ -60,6 +61,22 @@ def time_allreduce(numel: int, dtype, dev, iters: int, warmup: int) -> float:
     return float(m.item())
 
 
+def time_p2p(p2p, numel: int, dtype, dev, iters: int, warmup: int) -> float:
+    t = torch.ones(numel, dtype=dtype, device=dev)
+    for _ in range(warmup):
+        p2p.all_reduce(t)
+    _sync(dev)
+    launcher.barrier()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        p2p.all_reduce(t)
+    _sync(dev)
+    el = (time.perf_counter() - t0) / iters
+    m = torch.tensor([el], dtype=torch.float64, device=dev)
+    dist.all_reduce(m, op=dist.ReduceOp.MAX)
+    return float(m.item())
+
+
 def sweep_collectives(args, ctx, emit):
     dtype = {"bf16": torch.bfloat16, "fp32": torch.float32}[args.dtype]
     esize = torch.finfo(dtype).bits // 8
@@ -69,6 +86,10 @@ def sweep_collectives(args, ctx, emit):
     if args.reference_sizes:
         sizes = [s * 4 for s in REFERENCE_SIZES] + [sum(REFERENCE_SIZES) * 4]
         dtype, esize = torch.float32, 4
+    p2p = None
+    if args.p2p and ctx.device.type == "cuda":
+        from pytorch_distributed_training_example_amd.parallel.p2p import P2PAllReduce
+        p2p = P2PAllReduce(capacity_bytes=args.p2p_capacity_mb << 20)
     for nbytes in sizes:
         numel = max(1, nbytes // esize)
         sec = time_allreduce(numel, dtype, ctx.device, args.iters, args.warmup)
@@ -76,6 +97,12 @@ def sweep_collectives(args, ctx, emit):
         emit({"sweep": "collectives", "op": "all_reduce", "bytes": numel * esize, "dtype": str(dtype),
               "n_ranks": n, "us": round(sec * 1e6, 2), "algbw_GBps": round(algbw, 2),
               "busbw_GBps": round(algbw * 2 * (n - 1) / max(n, 1), 2), "backend": dist.get_backend()})
+        if p2p is not None and numel % 8 == 0 and numel * esize <= p2p.capacity:
+            sec = time_p2p(p2p, numel, dtype, ctx.device, args.iters, args.warmup)
+            emit({"sweep": "collectives", "op": "p2p_oneshot", "bytes": numel * esize, "dtype": str(dtype),
+                  "n_ranks": n, "us": round(sec * 1e6, 2), "algbw_GBps": round(numel * esize / sec / 1e9, 2)})
+    if p2p is not None:
+        p2p.check()
 
 
 def sweep_train(args, ctx, emit):
@@ -102,6 +129,8 @@ def main(argv=None):
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--sizes", default=None, help="comma list of message sizes in bytes")
     ap.add_argument("--reference-sizes", action="store_true", help="the reference's 10 per-param sizes (fp32)")
+    ap.add_argument("--p2p", type=int, default=1, help="also time the one-shot xGMI P2P all-reduce (GPU)")
+    ap.add_argument("--p2p-capacity-mb", type=int, default=16)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--caps", default="1,5,10,25,50,100", help="bucket_cap_mb values for the train sweep")
