@@ -132,6 +132,8 @@ def build(args, ctx):
 def setup(args):
     """Environment + process group (once per process)."""
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    from pytorch_distributed_training_example_amd.engine.miopen_cache import use_repo_miopen_cache
+    use_repo_miopen_cache()
     if args.impl != "ours":
         # stock baseline: every op (BN, LN, GELU, attention, CE) on PyTorch's own kernels
         os.environ["PDT_DISABLE_NATIVE"] = "1"
@@ -218,8 +220,13 @@ def run(args, ctx):
         x, y = pool[i % 2]
         return runner(x, y) if runner is not None else step(x, y)
 
+    tw = time.perf_counter()
     for i in range(args.warmup):
         loss = run(i)
+        if ctx.rank == 0:  # progress (first steps include MIOpen's conv-algorithm search)
+            torch.cuda.synchronize()
+            print(f"[bench] warmup step {i + 1}/{args.warmup} done at {time.perf_counter() - tw:.1f}s",
+                  file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     launcher.barrier()
     torch.cuda.synchronize()

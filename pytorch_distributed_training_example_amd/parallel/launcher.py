@@ -128,6 +128,14 @@ def init_distributed(
             if backend == "nccl" and device.type == "cuda":
                 # Eager communicator creation binds the RCCL comm to this device.
                 kwargs["device_id"] = device
+            attempt = int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0"))
+            if attempt > 0:
+                # torchrun's static rendezvous keeps ONE agent-hosted TCPStore across restarts, so
+                # the restarted group would read the dead attempt's gloo/RCCL bootstrap keys
+                # (connection refused to the old listener): namespace the keys per attempt.
+                store, _, _ = next(dist.rendezvous("env://", rank, world_size,
+                                                   timeout=datetime.timedelta(seconds=timeout_s)))
+                kwargs["store"] = dist.PrefixStore(f"pdt/attempt_{attempt}", store)
             dist.init_process_group(**kwargs)
     _CTX = DistContext(rank, world_size, local_rank, e_lws, backend, device)
     return _CTX

@@ -79,13 +79,23 @@ def test_graph_step_lr0_matches_eager():
 
 
 def test_graph_step_matches_eager_training():
-    """Optimizer/step state across replays: deterministic solvers so eager and graph are
-    bit-comparable over several updates (non-deterministic wgrad atomics make two *eager* runs
-    drift apart by a few % after a few bf16 updates)."""
+    """Optimizer/step state across replays. Even with deterministic MIOpen solvers two *eager*
+    runs are not always bit-identical (find-mode may pick different solvers per run, and a few
+    bf16 SGD updates amplify any rounding difference), so the yardstick is the eager-vs-eager
+    drift: a broken replay (stale optimizer state, wrong input binding) is O(1) off, far above it."""
     torch.backends.cudnn.deterministic = True
     base = _setup()
     xs, ys = _data()
     le, pe, _ = _run(base, "eager", 0.01, xs, ys)
+    le2, _, _ = _run(base, "eager", 0.01, xs, ys)
     lg, pg, _ = _run(base, "graph", 0.01, xs, ys)
     assert torch.isfinite(lg).all()
-    torch.testing.assert_close(lg, le, rtol=2e-2, atol=2e-2)
+    eager_drift = (le2 - le).abs().max().item()
+    graph_drift = (lg - le).abs().max().item()
+    print(f"loss drift eager/eager {eager_drift:.3e} graph/eager {graph_drift:.3e}")
+    assert graph_drift <= max(2e-2, 4 * eager_drift), (graph_drift, eager_drift, lg, le)
+    # the replayed updates must actually train: weights moved like eager's did
+    base_ps = [p.detach().float() for p in base.parameters()]
+    for a, b, p0 in zip(pg, pe, base_ps):
+        da, db = (a - p0).norm().item(), (b - p0).norm().item()
+        assert db < 1e-8 or (0.5 * db < da < 2 * db), (da, db)
