@@ -80,6 +80,42 @@ __device__ __forceinline__ void accum_row(const uint16_t* __restrict__ x, const 
   }
 }
 
+// Per-channel finalize from the full sums (S1, S2): forward -> mean/invstd/affine/running stats,
+// backward -> dgamma/dbeta and the dx coefficients.
+template <int MODE>
+__device__ __forceinline__ void bn_finalize(int ch, float S1, float S2, const FinArgs& fa) {
+  const int64_t Mt = fa.M;
+  if (MODE == 0) {
+    const float kk = bf2f(fa.x[ch]);
+    const double inv_m = 1.0 / (double)Mt;
+    const double d1 = (double)S1 * inv_m;
+    double var = (double)S2 * inv_m - d1 * d1;
+    var = var < 0.0 ? 0.0 : var;
+    const float mu = (float)(kk + d1);
+    const float is = (float)(1.0 / sqrt(var + (double)fa.eps));
+    fa.mean_out[ch] = mu;
+    fa.invstd_out[ch] = is;
+    const float gm = fa.gamma ? fa.gamma[ch] : 1.f, bt = fa.beta ? fa.beta[ch] : 0.f;
+    fa.a_out[ch] = gm * is;
+    fa.b_out[ch] = bt - mu * gm * is;
+    if (fa.running_mean) fa.running_mean[ch] = (1.f - fa.momentum) * fa.running_mean[ch] + fa.momentum * mu;
+    if (fa.running_var) {
+      const double unb = Mt > 1 ? var * (double)Mt / (double)(Mt - 1) : var;
+      fa.running_var[ch] = (1.f - fa.momentum) * fa.running_var[ch] + fa.momentum * (float)unb;
+    }
+  } else {
+    const float is = fa.invstd[ch];
+    const float gm = fa.gamma ? fa.gamma[ch] : 1.f;
+    const float db = S1, dg = S2 * is;
+    if (fa.dgamma) fa.dgamma[ch] = dg;
+    if (fa.dbeta) fa.dbeta[ch] = db;
+    const float inv_m = 1.f / (float)Mt;
+    fa.A[ch] = gm * is;
+    fa.B[ch] = -gm * is * is * dg * inv_m;
+    fa.D[ch] = -gm * is * db * inv_m;
+  }
+}
+
 template <int MODE>
 __global__ __launch_bounds__(kThreads) void bn_reduce_kernel(
     const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy, const uint8_t* __restrict__ mask,
@@ -166,36 +202,119 @@ __global__ __launch_bounds__(kThreads) void bn_reduce_kernel(
   float S1 = 0.f, S2 = 0.f;
 #pragma unroll
   for (int q = 0; q < 8; ++q) { S1 += sm[q * 128 + tid]; S2 += sm[q * 128 + kCC + tid]; }
-  const int64_t Mt = fa.M;
-  if (MODE == 0) {
-    const float kk = bf2f(fa.x[ch]);
-    const double inv_m = 1.0 / (double)Mt;
-    const double d1 = (double)S1 * inv_m;
-    double var = (double)S2 * inv_m - d1 * d1;
-    var = var < 0.0 ? 0.0 : var;
-    const float mu = (float)(kk + d1);
-    const float is = (float)(1.0 / sqrt(var + (double)fa.eps));
-    fa.mean_out[ch] = mu;
-    fa.invstd_out[ch] = is;
-    const float gm = fa.gamma ? fa.gamma[ch] : 1.f, bt = fa.beta ? fa.beta[ch] : 0.f;
-    fa.a_out[ch] = gm * is;
-    fa.b_out[ch] = bt - mu * gm * is;
-    if (fa.running_mean) fa.running_mean[ch] = (1.f - fa.momentum) * fa.running_mean[ch] + fa.momentum * mu;
-    if (fa.running_var) {
-      const double unb = Mt > 1 ? var * (double)Mt / (double)(Mt - 1) : var;
-      fa.running_var[ch] = (1.f - fa.momentum) * fa.running_var[ch] + fa.momentum * (float)unb;
-    }
-  } else {
-    const float is = fa.invstd[ch];
-    const float gm = fa.gamma ? fa.gamma[ch] : 1.f;
-    const float db = S1, dg = S2 * is;
-    if (fa.dgamma) fa.dgamma[ch] = dg;
-    if (fa.dbeta) fa.dbeta[ch] = db;
-    const float inv_m = 1.f / (float)Mt;
-    fa.A[ch] = gm * is;
-    fa.B[ch] = -gm * is * is * dg * inv_m;
-    fa.D[ch] = -gm * is * db * inv_m;
+  bn_finalize<MODE>(ch, S1, S2, fa);
+}
+
+// ---- v2 reduce: U rows in flight per lane, tunable grid, two-level deterministic finalize.
+// Blocks of a chunk are grouped kG at a time: the last block to arrive in a group sums the
+// group's slabs (fixed order) into a group slab, and the last group to arrive sums the group
+// slabs (fixed order) and finalizes. The serial tail is then <= kG + nrow/kG slab reads instead
+// of nrow (512 slabs = 256 KB of cross-XCD reads for C = 64 in v1).
+constexpr int kG = 16;
+
+// Sum `n` slabs of 2*kCC floats (stride 2*kCC) in index order into thread tid's column
+// (tid < 2*kCC); loads are issued 8 at a time so the cross-XCD round trips overlap.
+__device__ __forceinline__ float sum_slabs(const float* __restrict__ base, int n, int tid) {
+  float a = 0.f;
+  int i = 0;
+  for (; i + 8 <= n; i += 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = base[(int64_t)(i + u) * (2 * kCC) + tid];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) a += v[u];
   }
+  for (; i < n; ++i) a += base[(int64_t)i * (2 * kCC) + tid];
+  return a;
+}
+
+template <int MODE, int U>
+__global__ __launch_bounds__(kThreads) void bn_reduce2_kernel(
+    const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy, const uint8_t* __restrict__ mask,
+    const float* __restrict__ mean, int64_t M, int C, int64_t rows_per_block, int nrow,
+    float* __restrict__ part, float* __restrict__ gpart, unsigned* __restrict__ counters, FinArgs fa) {
+  __shared__ __attribute__((aligned(16))) float sm[2 * kR * kCC + 4];
+  const int tid = threadIdx.x;
+  const int chunk = blockIdx.y;
+  const int l = tid & (kL - 1), r = tid >> 3;
+  const int c = chunk * kCC + l * 8;
+  const int64_t m0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t m1 = min(M, m0 + rows_per_block);
+  float k[8], s1[8], s2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { s1[j] = 0.f; s2[j] = 0.f; }
+  if (MODE == 0) ld8_bf16(x + c, k);
+  else ld8_f32(mean + c, k);
+  int64_t m = m0 + r;
+  for (; m + (U - 1) * kR < m1; m += U * kR) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) accum_row<MODE>(x, dy, mask, m + u * kR, C, c, k, s1, s2);
+  }
+  for (; m < m1; m += kR) accum_row<MODE>(x, dy, mask, m, C, c, k, s1, s2);
+
+  float* d0 = &sm[r * kCC + l * 8];
+  float* d1 = &sm[kR * kCC + r * kCC + l * 8];
+  *reinterpret_cast<float4*>(d0) = make_float4(s1[0], s1[1], s1[2], s1[3]);
+  *reinterpret_cast<float4*>(d0 + 4) = make_float4(s1[4], s1[5], s1[6], s1[7]);
+  *reinterpret_cast<float4*>(d1) = make_float4(s2[0], s2[1], s2[2], s2[3]);
+  *reinterpret_cast<float4*>(d1 + 4) = make_float4(s2[4], s2[5], s2[6], s2[7]);
+  __syncthreads();
+  const int ngroups = (nrow + kG - 1) / kG;
+  const int g = blockIdx.x / kG;
+  const int gsize = min(kG, nrow - g * kG);
+  float* slabs = part + (int64_t)chunk * nrow * (2 * kCC);
+  float* gslabs = gpart + (int64_t)chunk * ngroups * (2 * kCC);
+  unsigned* ctr = counters + chunk * (ngroups + 1);
+  float tot = 0.f;  // thread tid < 2*kCC: running column value
+  if (tid < 2 * kCC) {
+    const int which = tid / kCC, cl = tid % kCC;
+    const float* src = &sm[which * kR * kCC + cl];
+#pragma unroll 8
+    for (int rr = 0; rr < kR; ++rr) tot += src[rr * kCC];
+    if (gsize > 1) slabs[(int64_t)blockIdx.x * (2 * kCC) + tid] = tot;
+  }
+  // level 1: last arriver of the group
+  if (gsize > 1) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      const unsigned t = __hip_atomic_fetch_add(&ctr[g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      sm[2 * kR * kCC] = (t == (unsigned)(gsize - 1)) ? 1.f : 0.f;
+    }
+    __syncthreads();
+    if (sm[2 * kR * kCC] == 0.f) return;
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      ctr[g] = 0u;  // self-reset (stream-ordered for the next launch)
+    }
+    __syncthreads();
+    if (tid < 2 * kCC) tot = sum_slabs(slabs + (int64_t)g * kG * (2 * kCC), gsize, tid);
+  }
+  // level 2: last group
+  if (ngroups > 1) {
+    if (tid < 2 * kCC) gslabs[(int64_t)g * (2 * kCC) + tid] = tot;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      const unsigned t = __hip_atomic_fetch_add(&ctr[ngroups], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      sm[2 * kR * kCC + 1] = (t == (unsigned)(ngroups - 1)) ? 1.f : 0.f;
+    }
+    __syncthreads();
+    if (sm[2 * kR * kCC + 1] == 0.f) return;
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      ctr[ngroups] = 0u;
+    }
+    __syncthreads();
+    if (tid < 2 * kCC) tot = sum_slabs(gslabs, ngroups, tid);
+  }
+  __syncthreads();
+  if (tid < 2 * kCC) sm[tid] = tot;
+  __syncthreads();
+  if (tid >= kCC) return;
+  bn_finalize<MODE>(chunk * kCC + tid, sm[tid], sm[kCC + tid], fa);
 }
 
 __global__ void bn_eval_coef_kernel(int C, const float* __restrict__ gamma, const float* __restrict__ beta,
@@ -400,6 +519,60 @@ inline ReduceGeo reduce_geo(int64_t M, int C) {
   return g;
 }
 
+// Reduce-kernel tuning (bn_tune): variant 1 = single-level finalize, 2 = two-level; total
+// workgroups targeted per call; rows in flight per lane for the forward / backward reduce.
+struct BnTune {
+  int variant = 2;
+  int target_blocks = 512;  // tools/bn_reduce_sweep.py: 2 workgroups per CU beat 4-16 (10.5 vs 11.5+ ms/step)
+  int u_fwd = 8;
+  int u_bwd = 4;
+};
+BnTune g_tune;
+
+inline ReduceGeo reduce_geo2(int64_t M, int C, int U) {
+  ReduceGeo g;
+  g.nchunks = C / kCC;
+  int64_t nrow = g_tune.target_blocks / g.nchunks;
+  if (nrow > 1024) nrow = 1024;
+  const int64_t max_rows = (M + (int64_t)U * kR - 1) / ((int64_t)U * kR);  // >= 1 full pass per block
+  if (nrow > max_rows) nrow = max_rows;
+  if (nrow < 1) nrow = 1;
+  g.rows_per_block = (M + nrow - 1) / nrow;
+  g.nrow = (int)((M + g.rows_per_block - 1) / g.rows_per_block);
+  return g;
+}
+
+inline int64_t slab_floats2(const ReduceGeo& g) {
+  const int ngroups = (g.nrow + kG - 1) / kG;
+  return (int64_t)g.nchunks * (g.nrow + ngroups) * 2 * kCC;
+}
+
+// Launch the reduce (+ fused finalize) of MODE; returns the float offset in ws where the
+// per-channel coefficient arrays start.
+template <int MODE>
+int64_t launch_reduce(const uint16_t* x, const uint16_t* dy, const uint8_t* mask, const float* mean, int64_t M,
+                      int C, float* ws, unsigned* counters, const FinArgs& fa, hipStream_t s) {
+  if (g_tune.variant == 1) {
+    const ReduceGeo g = reduce_geo(M, C);
+    hipLaunchKernelGGL(bn_reduce_kernel<MODE>, dim3(g.nrow, g.nchunks), dim3(kThreads), 0, s, x, dy, mask, mean, M,
+                       C, g.rows_per_block, g.nrow, ws, counters, fa);
+    return (int64_t)g.nchunks * g.nrow * 2 * kCC;
+  }
+  const int U = MODE == 0 ? g_tune.u_fwd : g_tune.u_bwd;
+  const ReduceGeo g = reduce_geo2(M, C, U);
+  float* part = ws;
+  float* gpart = ws + (int64_t)g.nchunks * g.nrow * 2 * kCC;
+#define PDT_R2(UU)                                                                                          \
+  hipLaunchKernelGGL((bn_reduce2_kernel<MODE, UU>), dim3(g.nrow, g.nchunks), dim3(kThreads), 0, s, x, dy,   \
+                     mask, mean, M, C, g.rows_per_block, g.nrow, part, gpart, counters, fa)
+  if (U >= 16) PDT_R2(16);
+  else if (U >= 8) PDT_R2(8);
+  else if (U >= 4) PDT_R2(4);
+  else PDT_R2(2);
+#undef PDT_R2
+  return slab_floats2(g);
+}
+
 inline int apply_grid(int64_t nvec) {
   int64_t g = (nvec + 255) / 256;
   const int64_t cap = 256 * 8;  // 8 workgroups per CU, grid-stride the rest
@@ -412,8 +585,18 @@ extern "C" {
 
 // Workspace floats needed by a train fwd/bwd call (partial slabs + per-channel coefficients).
 int64_t pdt_bn_workspace_floats(int64_t M, int C) {
-  const ReduceGeo g = reduce_geo(M, C);
-  return (int64_t)g.nchunks * g.nrow * 2 * kCC + 4 * (int64_t)C;
+  const ReduceGeo g1 = reduce_geo(M, C);
+  const int64_t v1 = (int64_t)g1.nchunks * g1.nrow * 2 * kCC;
+  const int64_t v2 = slab_floats2(reduce_geo2(M, C, 2));  // U = 2 gives the most rows
+  return (v1 > v2 ? v1 : v2) + 4 * (int64_t)C;
+}
+
+// Select the reduce implementation / grid (benchmarking). Values <= 0 keep the current setting.
+void pdt_bn_tune(int variant, int target_blocks, int u_fwd, int u_bwd) {
+  if (variant > 0) g_tune.variant = variant;
+  if (target_blocks > 0) g_tune.target_blocks = target_blocks;
+  if (u_fwd > 0) g_tune.u_fwd = u_fwd;
+  if (u_bwd > 0) g_tune.u_bwd = u_bwd;
 }
 
 // Training forward. Outputs: y (bf16), mask (uint8, M*C/8, when relu), mean/invstd (f32 [C]);
@@ -423,16 +606,14 @@ int pdt_bn_fwd_train(const uint16_t* x, const uint16_t* res, const float* gamma,
                      int relu, uint16_t* y, uint8_t* mask, float* mean, float* invstd, float* ws,
                      unsigned* counters, hipStream_t s) {
   if (C % kCC != 0 || M < 1) return -1;
-  const ReduceGeo g = reduce_geo(M, C);
-  float* part = ws;
-  float* a = ws + (int64_t)g.nchunks * g.nrow * 2 * kCC;
+  // coefficients live at the tail of ws (past the largest slab area)
+  float* a = ws + pdt_bn_workspace_floats(M, C) - 4 * (int64_t)C;
   float* b = a + C;
   FinArgs fa{};
   fa.x = x; fa.gamma = gamma; fa.beta = beta; fa.mean_out = mean; fa.invstd_out = invstd; fa.a_out = a;
   fa.b_out = b; fa.running_mean = running_mean; fa.running_var = running_var; fa.momentum = momentum;
   fa.eps = eps; fa.M = M;
-  hipLaunchKernelGGL(bn_reduce_kernel<0>, dim3(g.nrow, g.nchunks), dim3(kThreads), 0, s, x, nullptr, nullptr,
-                     nullptr, M, C, g.rows_per_block, g.nrow, part, counters, fa);
+  launch_reduce<0>(x, nullptr, nullptr, nullptr, M, C, ws, counters, fa, s);
   const int64_t nvec = M * C / 8;
   const int fixed = (2048 % C) == 0;
   const int grid = apply_grid(nvec);
@@ -455,16 +636,14 @@ int pdt_bn_relu_maxpool_fwd_train(const uint16_t* x, const float* gamma, const f
                                   unsigned* counters, hipStream_t s) {
   const int64_t M = (int64_t)N * H * W;
   if (C % kCC != 0 || M < 1) return -1;
-  const ReduceGeo g = reduce_geo(M, C);
-  float* part = ws;
-  float* a = ws + (int64_t)g.nchunks * g.nrow * 2 * kCC;
+  // coefficients live at the tail of ws (past the largest slab area)
+  float* a = ws + pdt_bn_workspace_floats(M, C) - 4 * (int64_t)C;
   float* b = a + C;
   FinArgs fa{};
   fa.x = x; fa.gamma = gamma; fa.beta = beta; fa.mean_out = mean; fa.invstd_out = invstd; fa.a_out = a;
   fa.b_out = b; fa.running_mean = running_mean; fa.running_var = running_var; fa.momentum = momentum;
   fa.eps = eps; fa.M = M;
-  hipLaunchKernelGGL(bn_reduce_kernel<0>, dim3(g.nrow, g.nchunks), dim3(kThreads), 0, s, x, nullptr, nullptr,
-                     nullptr, M, C, g.rows_per_block, g.nrow, part, counters, fa);
+  launch_reduce<0>(x, nullptr, nullptr, nullptr, M, C, ws, counters, fa, s);
   const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
   const int64_t nvec = (int64_t)N * Ho * Wo * (C / 8);
   hipLaunchKernelGGL(bn_apply_pool_kernel, dim3(apply_grid(nvec)), dim3(256), 0, s, x, a, b, y, code, N, H, W, C,
@@ -512,20 +691,14 @@ int pdt_bn_bwd_train(const uint16_t* dy, const uint16_t* x, const uint8_t* mask,
                      hipStream_t s) {
   if (C % kCC != 0 || M < 1) return -1;
   if (relu && !mask) return -2;
-  const ReduceGeo g = reduce_geo(M, C);
-  float* part = ws;
-  float* A = ws + (int64_t)g.nchunks * g.nrow * 2 * kCC;
+  float* A = ws + pdt_bn_workspace_floats(M, C) - 4 * (int64_t)C;
   float* B = A + C;
   float* D = B + C;
   FinArgs fa{};
   fa.gamma = gamma; fa.invstd = invstd; fa.dgamma = dgamma; fa.dbeta = dbeta; fa.A = A; fa.B = B; fa.D = D;
   fa.M = M;
-  if (relu)
-    hipLaunchKernelGGL(bn_reduce_kernel<2>, dim3(g.nrow, g.nchunks), dim3(kThreads), 0, s, x, dy, mask, mean, M, C,
-                       g.rows_per_block, g.nrow, part, counters, fa);
-  else
-    hipLaunchKernelGGL(bn_reduce_kernel<1>, dim3(g.nrow, g.nchunks), dim3(kThreads), 0, s, x, dy, mask, mean, M, C,
-                       g.rows_per_block, g.nrow, part, counters, fa);
+  if (relu) launch_reduce<2>(x, dy, mask, mean, M, C, ws, counters, fa, s);
+  else launch_reduce<1>(x, dy, mask, mean, M, C, ws, counters, fa, s);
   const int64_t nvec = M * C / 8;
   const int fixed = (2048 % C) == 0;
   const int grid = apply_grid(nvec);
