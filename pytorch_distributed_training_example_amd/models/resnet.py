@@ -19,6 +19,7 @@ import torch
 from torch import nn
 
 from ..ops.batchnorm import BatchNorm2d
+from ..ops.conv import Conv1x1
 
 
 def conv3x3(inp: int, out: int, stride: int = 1, groups: int = 1, dilation: int = 1) -> nn.Conv2d:
@@ -26,6 +27,8 @@ def conv3x3(inp: int, out: int, stride: int = 1, groups: int = 1, dilation: int 
 
 
 def conv1x1(inp: int, out: int, stride: int = 1) -> nn.Conv2d:
+    if _norm_kind[0] == "pdt":  # our path: autotuned MIOpen / hipBLASLt GEMM (ops/conv.py)
+        return Conv1x1(inp, out, stride)
     return nn.Conv2d(inp, out, 1, stride=stride, bias=False)
 
 

@@ -1,0 +1,137 @@
+"""1x1 convolutions as GEMMs, with per-shape algorithm selection (MIOpen vs hipBLASLt).
+
+Not in the reference (LeNet's convs are 5x5, /root/reference/cnn.py:10-16); this serves the
+ResNet-50 north-star config, where 36 of 53 convolutions are 1x1. In channels_last (NHWC) a
+stride-1 1x1 convolution IS a GEMM on views, no copies:
+
+    X [N,H,W,Ci] -> [M, Ci],  W [Co,Ci,1,1] -> [Co, Ci],  Y = X W^T -> [M, Co] = [N,H,W,Co]
+    dX = dY W,  dW = dY^T X
+
+These shapes are HBM-bound (K = Ci is 64..2048 while M = N*H*W is 12K..800K), and which
+library streams them best depends on the shape: MIOpen's implicit-GEMM kernels win for narrow
+K/N (and need a zero-fill + fp32->bf16 cast pass for their atomic split-K outputs), hipBLASLt
+wins for wide ones (tools/conv_bench.py: 1.2 ms/step of ResNet-50 difference). So each
+direction (forward, data-grad, weight-grad) of each shape is timed once with both back ends on
+its first eager call — like ``cudnn.benchmark`` — and the faster one is used from then on
+(``PDT_CONV1X1=miopen|gemm|auto``). Never timed under hipGraph capture (capture falls back to
+MIOpen for an unseen shape), so the warm-up steps before ``StaticStep.capture`` settle it.
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, Tuple
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+_CHOICE: Dict[Tuple, str] = {}
+
+
+def _mode() -> str:
+    return os.environ.get("PDT_CONV1X1", "auto")
+
+
+def _time(fn, reps: int = 3) -> float:
+    fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1)
+
+
+def _pick(key: Tuple, cands: Dict[str, callable]) -> str:
+    mode = _mode()
+    if mode in cands:
+        return mode
+    c = _CHOICE.get(key)
+    if c is not None:
+        return c
+    if torch.cuda.is_current_stream_capturing():
+        return "miopen"
+    times = {name: _time(fn) for name, fn in cands.items()}
+    c = min(times, key=times.get)
+    _CHOICE[key] = c
+    return c
+
+
+def choices() -> Dict[Tuple, str]:
+    """Decisions taken so far: {(direction, M, Ci, Co): 'miopen' | 'gemm'}."""
+    return dict(_CHOICE)
+
+
+def _nhwc2d(t: torch.Tensor) -> torch.Tensor:
+    """[N,C,H,W] channels_last -> [N*H*W, C] view."""
+    return t.permute(0, 2, 3, 1).reshape(-1, t.shape[1])
+
+
+class _Conv1x1Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight):
+        N, Ci, H, W = x.shape
+        Co = weight.shape[0]
+        x2 = _nhwc2d(x)
+        w2 = weight.reshape(Co, Ci)
+        M = x2.shape[0]
+        algo = _pick(("fwd", M, Ci, Co), {
+            "miopen": lambda: F.conv2d(x, weight),
+            "gemm": lambda: torch.mm(x2, w2.t()),
+        })
+        if algo == "gemm":
+            y = torch.mm(x2, w2.t()).view(N, H, W, Co).permute(0, 3, 1, 2)
+        else:
+            y = F.conv2d(x, weight)
+        ctx.save_for_backward(x, weight)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, weight = ctx.saved_tensors
+        N, Ci, H, W = x.shape
+        Co = weight.shape[0]
+        gy = gy.contiguous(memory_format=torch.channels_last)
+        x2, g2, w2 = _nhwc2d(x), _nhwc2d(gy), weight.reshape(Co, Ci)
+        M = x2.shape[0]
+        dx = dw = None
+
+        def conv_bwd(mask):
+            return torch.ops.aten.convolution_backward(gy, x, weight, None, [1, 1], [0, 0], [1, 1], False, [0, 0],
+                                                       1, mask)
+
+        if ctx.needs_input_grad[0]:
+            algo = _pick(("bwd_data", M, Ci, Co), {
+                "miopen": lambda: conv_bwd([True, False, False]),
+                "gemm": lambda: torch.mm(g2, w2),
+            })
+            if algo == "gemm":
+                dx = torch.mm(g2, w2).view(N, H, W, Ci).permute(0, 3, 1, 2)
+            else:
+                dx = conv_bwd([True, False, False])[0]
+        if ctx.needs_input_grad[1]:
+            algo = _pick(("bwd_weight", M, Ci, Co), {
+                "miopen": lambda: conv_bwd([False, True, False]),
+                "gemm": lambda: torch.mm(g2.t(), x2),
+            })
+            if algo == "gemm":
+                # a 1x1 kernel has the same element order in NCHW and NHWC: keep weight's strides
+                dw = torch.mm(g2.t(), x2).as_strided(weight.shape, weight.stride())
+            else:
+                dw = conv_bwd([False, True, False])[1]
+        return dx, dw
+
+
+class Conv1x1(nn.Conv2d):
+    """``nn.Conv2d(Ci, Co, 1, bias=False)`` (same parameters and state_dict) whose stride-1 GPU
+    channels_last path runs as autotuned GEMMs; everything else is plain ``nn.Conv2d``."""
+
+    def __init__(self, inp: int, out: int, stride: int = 1):
+        super().__init__(inp, out, 1, stride=stride, bias=False)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if (self.stride == (1, 1) and x.is_cuda and x.dim() == 4 and x.dtype == self.weight.dtype
+                and x.is_contiguous(memory_format=torch.channels_last) and _mode() != "off"):
+            return _Conv1x1Fn.apply(x, self.weight)
+        return super().forward(x)

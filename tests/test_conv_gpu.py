@@ -1,0 +1,31 @@
+"""1x1 conv as autotuned GEMM (ops/conv.py) vs an fp32 PyTorch conv reference, both back ends."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("mode", ["gemm", "miopen", "auto"])
+@pytest.mark.parametrize("shape", [(4, 64, 256, 14), (2, 256, 64, 7), (3, 128, 512, 5)])
+def test_conv1x1_matches_fp32(monkeypatch, mode, shape):
+    from pytorch_distributed_training_example_amd.ops.conv import Conv1x1
+    monkeypatch.setenv("PDT_CONV1X1", mode)
+    N, Ci, Co, H = shape
+    torch.manual_seed(0)
+    m = Conv1x1(Ci, Co).cuda().bfloat16().to(memory_format=torch.channels_last)
+    x = torch.randn(N, Ci, H, H, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    x.requires_grad_(True)
+    y = m(x)
+    assert y.is_contiguous(memory_format=torch.channels_last)
+    gy = torch.randn_like(y)
+    y.backward(gy)
+    xr = x.detach().float().requires_grad_(True)
+    wr = m.weight.detach().float().requires_grad_(True)
+    yr = F.conv2d(xr, wr)
+    yr.backward(gy.float())
+    torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=2e-2 * yr.abs().max().item() ** 0.5)
+    for a, b in ((x.grad, xr.grad), (m.weight.grad, wr.grad)):
+        err = ((a.float() - b).norm() / b.norm()).item()
+        assert err < 1e-2, err
+    assert m.weight.grad.stride() == m.weight.stride()
