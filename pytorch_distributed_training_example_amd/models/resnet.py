@@ -18,7 +18,7 @@ from typing import List, Optional, Type
 import torch
 from torch import nn
 
-from ..ops.batchnorm import BatchNorm2d
+from ..ops.batchnorm import BatchNorm2d, ResidualGradLink
 from ..ops.conv import Conv1x1
 
 
@@ -37,6 +37,7 @@ class _Downsample(nn.Sequential):
 
 
 _NORM = {"pdt": BatchNorm2d, "torch": nn.BatchNorm2d}
+RESIDUAL_GRAD_LINK = [True]  # identity-block residual gradient accumulated in conv1's dgrad GEMM
 _norm_kind = ["pdt"]
 
 
@@ -92,6 +93,15 @@ class Bottleneck(nn.Module):
         self.stride = stride
 
     def forward(self, x):
+        if (RESIDUAL_GRAD_LINK[0] and self.downsample is None and self.training and x.requires_grad and torch.is_grad_enabled()
+                and isinstance(self.conv1, Conv1x1) and isinstance(self.bn3, BatchNorm2d)
+                and self.conv1.gemm_eligible(x) and x.shape[1] % 64 == 0):
+            # identity block: bn3's backward hands the residual gradient to conv1's backward,
+            # which accumulates its data-gradient GEMM into it (no autograd add kernel)
+            link = ResidualGradLink()
+            out = bn_act(self.bn1, self.conv1(x, res_link=link), relu=True)
+            out = bn_act(self.bn2, self.conv2(out), relu=True)
+            return self.bn3(self.conv3(out), residual=x, relu=True, res_link=link)
         identity = x if self.downsample is None else self.downsample(x)
         out = bn_act(self.bn1, self.conv1(x), relu=True)
         out = bn_act(self.bn2, self.conv2(out), relu=True)

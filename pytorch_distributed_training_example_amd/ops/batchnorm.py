@@ -31,15 +31,33 @@ def bn_reference(x, residual, weight, bias, running_mean, running_var, training,
     return y
 
 
+class ResidualGradLink:
+    """Hands the residual-branch gradient of a fused ``relu(bn(x) + identity)`` to the op that
+    consumes ``identity`` on the main branch (ResNet bottleneck: conv1 of the same block), so
+    that op accumulates into it (GEMM with beta = 1) instead of autograd summing the two
+    branch gradients with a separate add kernel (a full read-read-write pass per block).
+    The BN backward always runs first: the main branch is upstream of the BN."""
+
+    __slots__ = ("grad",)
+
+    def __init__(self):
+        self.grad = None
+
+    def take(self):
+        g, self.grad = self.grad, None
+        return g
+
+
 class _BNTrainFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, residual, weight, bias, running_mean, running_var, momentum, eps, relu):
+    def forward(ctx, x, residual, weight, bias, running_mean, running_var, momentum, eps, relu, link=None):
         C = native()
         y, mask, mean, invstd = C.bn_fwd_train(x, residual, weight, bias, running_mean, running_var,
                                                momentum, eps, relu)
         ctx.relu = relu
         ctx.has_res = residual is not None
         ctx.has_weight = weight is not None
+        ctx.link = link
         # backward needs the BN input and a 1-bit ReLU mask, never the output y
         ctx.save_for_backward(x, mask if relu else None, weight, mean, invstd)
         return y
@@ -52,8 +70,11 @@ class _BNTrainFn(torch.autograd.Function):
         need_w = ctx.has_weight and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3])
         dx, dres, dg, db = native().bn_bwd_train(dy, x, mask, weight, mean, invstd, ctx.relu,
                                                  ctx.has_res, need_w)
+        if ctx.has_res and ctx.link is not None:
+            ctx.link.grad = dres  # the main-branch consumer adds its gradient into this buffer
+            dres = None
         return (dx, dres if ctx.has_res else None, dg if need_w else None, db if need_w else None,
-                None, None, None, None, None)
+                None, None, None, None, None, None)
 
 
 class _BNEvalFn(torch.autograd.Function):
@@ -75,8 +96,12 @@ class _BNEvalFn(torch.autograd.Function):
         return dx, (dz if ctx.has_res else None), None, None, None, None, None, None
 
 
-def batch_norm_act(x, residual, weight, bias, running_mean, running_var, training, momentum, eps, relu):
-    """Functional fused BN(+add)(+ReLU). Native when x is a channels_last bf16 GPU tensor."""
+def batch_norm_act(x, residual, weight, bias, running_mean, running_var, training, momentum, eps, relu,
+                   res_link: Optional[ResidualGradLink] = None):
+    """Functional fused BN(+add)(+ReLU). Native when x is a channels_last bf16 GPU tensor.
+    ``res_link``: route the residual gradient through it instead of returning it (see
+    ``ResidualGradLink``); only honoured on the native training path — callers check
+    ``res_link.grad`` is set before relying on it."""
     nhwc = x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last) or \
         (x.dim() == 2 and x.is_contiguous())
     if (use_native(x) and x.dtype == torch.bfloat16 and nhwc and x.shape[1] % 64 == 0
@@ -86,7 +111,7 @@ def batch_norm_act(x, residual, weight, bias, running_mean, running_var, trainin
                                            else torch.contiguous_format)
         if training:
             return _BNTrainFn.apply(x, residual, weight, bias, running_mean, running_var,
-                                    float(momentum), float(eps), bool(relu))
+                                    float(momentum), float(eps), bool(relu), res_link)
         return _BNEvalFn.apply(x, residual, weight, bias, running_mean, running_var, float(eps), bool(relu))
     return bn_reference(x, residual, weight, bias, running_mean, running_var, training, momentum, eps, relu)
 
@@ -132,7 +157,7 @@ class BatchNorm2d(nn.BatchNorm2d):
         self._nbt = 0  # host-side num_batches_tracked (synced into the buffer on save)
 
     def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
-                relu: Optional[bool] = None) -> torch.Tensor:
+                relu: Optional[bool] = None, res_link: Optional[ResidualGradLink] = None) -> torch.Tensor:
         relu = self.fused_relu if relu is None else relu
         training = self.training or not self.track_running_stats
         momentum = self.momentum
@@ -145,7 +170,7 @@ class BatchNorm2d(nn.BatchNorm2d):
         w = self.weight if self.affine else None
         b = self.bias if self.affine else None
         return batch_norm_act(x, residual, w, b, rm, rv, training, momentum if momentum is not None else 0.0,
-                              self.eps, relu)
+                              self.eps, relu, res_link)
 
     def forward_relu_maxpool(self, x: torch.Tensor) -> torch.Tensor:
         """``max_pool2d(relu(bn(x)), 3, 2, 1)`` (ResNet stem) with the pool fused into the BN apply."""

@@ -25,6 +25,8 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
+from ._native import disabled
+
 _CHOICE: Dict[Tuple, str] = {}
 
 
@@ -70,7 +72,7 @@ def _nhwc2d(t: torch.Tensor) -> torch.Tensor:
 
 class _Conv1x1Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight):
+    def forward(ctx, x, weight, link=None):
         N, Ci, H, W = x.shape
         Co = weight.shape[0]
         x2 = _nhwc2d(x)
@@ -84,6 +86,7 @@ class _Conv1x1Fn(torch.autograd.Function):
             y = torch.mm(x2, w2.t()).view(N, H, W, Co).permute(0, 3, 1, 2)
         else:
             y = F.conv2d(x, weight)
+        ctx.link = link
         ctx.save_for_backward(x, weight)
         return y
 
@@ -101,15 +104,24 @@ class _Conv1x1Fn(torch.autograd.Function):
             return torch.ops.aten.convolution_backward(gy, x, weight, None, [1, 1], [0, 0], [1, 1], False, [0, 0],
                                                        1, mask)
 
+        # residual-branch gradient of x handed over by the block's fused BN (ResidualGradLink)
+        acc = ctx.link.take() if ctx.link is not None else None
         if ctx.needs_input_grad[0]:
             algo = _pick(("bwd_data", M, Ci, Co), {
                 "miopen": lambda: conv_bwd([True, False, False]),
                 "gemm": lambda: torch.mm(g2, w2),
             })
-            if algo == "gemm":
+            if algo == "gemm" and acc is not None and acc.is_contiguous(memory_format=torch.channels_last):
+                _nhwc2d(acc).addmm_(g2, w2)  # dx = dres + dY W in one GEMM (beta = 1)
+                dx, acc = acc, None
+            elif algo == "gemm":
                 dx = torch.mm(g2, w2).view(N, H, W, Ci).permute(0, 3, 1, 2)
             else:
                 dx = conv_bwd([True, False, False])[0]
+            if acc is not None:
+                dx = dx.add_(acc)
+        elif acc is not None:
+            dx = acc
         if ctx.needs_input_grad[1]:
             algo = _pick(("bwd_weight", M, Ci, Co), {
                 "miopen": lambda: conv_bwd([False, True, False]),
@@ -120,7 +132,7 @@ class _Conv1x1Fn(torch.autograd.Function):
                 dw = torch.mm(g2.t(), x2).as_strided(weight.shape, weight.stride())
             else:
                 dw = conv_bwd([False, True, False])[1]
-        return dx, dw
+        return dx, dw, None
 
 
 class Conv1x1(nn.Conv2d):
@@ -130,8 +142,14 @@ class Conv1x1(nn.Conv2d):
     def __init__(self, inp: int, out: int, stride: int = 1):
         super().__init__(inp, out, 1, stride=stride, bias=False)
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
-        if (self.stride == (1, 1) and x.is_cuda and x.dim() == 4 and x.dtype == self.weight.dtype
-                and x.is_contiguous(memory_format=torch.channels_last) and _mode() != "off"):
-            return _Conv1x1Fn.apply(x, self.weight)
+    def gemm_eligible(self, x: torch.Tensor) -> bool:
+        return (self.stride == (1, 1) and x.is_cuda and x.dim() == 4 and x.dtype == self.weight.dtype
+                and x.is_contiguous(memory_format=torch.channels_last) and _mode() != "off" and not disabled())
+
+    def forward(self, x: torch.Tensor, res_link=None) -> torch.Tensor:
+        """``res_link``: a ``ResidualGradLink`` whose gradient (the residual branch's gradient
+        of ``x``) is added into this conv's input gradient; requires ``gemm_eligible(x)``."""
+        if self.gemm_eligible(x):
+            return _Conv1x1Fn.apply(x, self.weight, res_link)
+        assert res_link is None, "res_link needs the GEMM-eligible path"
         return super().forward(x)

@@ -29,3 +29,27 @@ def test_conv1x1_matches_fp32(monkeypatch, mode, shape):
         err = ((a.float() - b).norm() / b.norm()).item()
         assert err < 1e-2, err
     assert m.weight.grad.stride() == m.weight.stride()
+
+
+def test_bottleneck_residual_grad_link_matches_autograd_add():
+    """Identity bottleneck: conv1's dgrad GEMM accumulating bn3's residual gradient (beta = 1)
+    gives the same input/weight gradients as autograd's separate add."""
+    from pytorch_distributed_training_example_amd.models import resnet as R
+    from pytorch_distributed_training_example_amd.models.precision import to_bf16_mixed
+    torch.manual_seed(0)
+    blk = to_bf16_mixed(R.Bottleneck(256, 64).cuda().to(memory_format=torch.channels_last))
+    x0 = torch.randn(8, 256, 14, 14, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    out = {}
+    for linked in (True, False):
+        R.RESIDUAL_GRAD_LINK[0] = linked
+        try:
+            blk.zero_grad(set_to_none=True)
+            x = x0.clone().requires_grad_(True)
+            y = blk(x)
+            y.backward(torch.ones_like(y) * 0.01 + y.detach() * 0.1)
+            out[linked] = [x.grad.float()] + [p.grad.float().clone() for p in blk.parameters()]
+        finally:
+            R.RESIDUAL_GRAD_LINK[0] = True
+    for a, b in zip(out[True], out[False]):
+        err = ((a - b).norm() / (b.norm() + 1e-12)).item()
+        assert err < 2e-2, err
