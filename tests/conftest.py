@@ -10,8 +10,10 @@ os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 # MIOpen reads its solver switches once per process: exclude the capture-unsafe solvers before
 # any test runs a convolution so the hipGraph tests see the same solver set as bench --graph 1
 from pytorch_distributed_training_example_amd.engine.graph import make_miopen_capture_safe  # noqa: E402
+from pytorch_distributed_training_example_amd.engine.miopen_cache import use_repo_miopen_cache  # noqa: E402
 
 make_miopen_capture_safe()
+use_repo_miopen_cache()
 
 
 def pytest_configure(config):
