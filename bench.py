@@ -132,8 +132,6 @@ def build(args, ctx):
 def setup(args):
     """Environment + process group (once per process)."""
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    from pytorch_distributed_training_example_amd.engine.miopen_cache import use_repo_miopen_cache
-    use_repo_miopen_cache()
     if args.impl != "ours":
         # stock baseline: every op (BN, LN, GELU, attention, CE) on PyTorch's own kernels
         os.environ["PDT_DISABLE_NATIVE"] = "1"
@@ -142,6 +140,8 @@ def setup(args):
         # MIOpen reads the switch once, so this must precede the first convolution
         from pytorch_distributed_training_example_amd.engine.graph import make_miopen_capture_safe
         make_miopen_capture_safe()
+    from pytorch_distributed_training_example_amd.engine.miopen_cache import use_repo_miopen_cache
+    use_repo_miopen_cache()  # persisted conv-algorithm find-db + kernel cache (after the solver switches)
     return launcher.init_distributed(backend=args.backend or ("nccl" if torch.cuda.is_available() else "gloo"),
                                      use_gpu=torch.cuda.is_available())
 

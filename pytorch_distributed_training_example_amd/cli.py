@@ -261,12 +261,12 @@ def main(argv: Optional[list] = None) -> int:
     args = build_parser().parse_args(argv)
     if args.amp is not None:
         args.precision = {"off": "fp32", "bf16": "bf16", "fp8": "fp8"}[args.amp]
-    from .engine.miopen_cache import use_repo_miopen_cache
-    use_repo_miopen_cache()  # persisted conv-algorithm find-db (engine/miopen_cache.py)
     if args.hipgraph:
         # MIOpen reads its solver switches once per process: set before any convolution
         from .engine.graph import make_miopen_capture_safe
         make_miopen_capture_safe()
+    from .engine.miopen_cache import use_repo_miopen_cache
+    use_repo_miopen_cache()  # persisted conv-algorithm find-db (engine/miopen_cache.py)
     if args.profile:
         from .utils import profiling
         profiling.enable_ranges(True)

@@ -12,7 +12,10 @@ Multi-process jobs: only local rank 0 uses (and may update) the in-tree director
 rank works on a private copy under the temp dir, so N ranks never write one sqlite / text db
 concurrently.
 
-Must run before the first convolution (MIOpen reads these variables once per process).
+Processes that restricted MIOpen's solver set for hipGraph capture (engine/graph.py) use a
+separate ``capture_safe`` sub-directory.
+
+Must run after ``make_miopen_capture_safe`` (when used) and before the first convolution (MIOpen reads these variables once per process).
 Explicit ``MIOPEN_*`` settings in the environment always win.
 """
 from __future__ import annotations
@@ -31,6 +34,11 @@ def use_repo_miopen_cache(path: str | None = None) -> str | None:
     path = path or os.environ.get("PDT_MIOPEN_CACHE") or DEFAULT_DIR
     if path in ("0", "off", "none"):
         return None
+    from .graph import CAPTURE_UNSAFE_MIOPEN_SOLVERS
+    if any(os.environ.get(k) == "0" for k in CAPTURE_UNSAFE_MIOPEN_SOLVERS):
+        # a solver set restricted for hipGraph capture gets its own find-db, so a db entry
+        # found without the restriction is never replayed under capture
+        path = os.path.join(path, "capture_safe")
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if local_rank > 0:
         private = os.path.join(tempfile.gettempdir(), f"pdt_miopen_{os.getpid()}_r{local_rank}")
