@@ -29,6 +29,9 @@ constexpr int D = 64;
 constexpr int ROW_BYTES = D * 2;  // 128 B per LDS row
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float LN2 = 0.6931471805599453f;
+#ifndef DKDV_MINW
+#define DKDV_MINW 2
+#endif
 
 struct Tensor4 {  // bf16 [B, H, T, D] view with arbitrary (b, h, t) strides, d stride 1
   const uint16_t* p;
@@ -68,6 +71,11 @@ __device__ __forceinline__ bf16x8 pack8(f4 a, f4 b) {
   return r;
 }
 
+// Raw v_exp_f32 (2^x): exp2f() adds a denormal range-reduction (cmp, 2 cndmask, add, ldexp)
+// around every exponential — 4 extra VALU ops per score for results that underflow to 0 in
+// bf16 anyway. exp2(-inf) = 0 holds for the masked scores.
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 __device__ __forceinline__ f4 mfma(bf16x8 a, bf16x8 b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
@@ -102,8 +110,10 @@ struct Stage {
 
 // ============================================================================ forward
 // grid (ceil(T/128), H, B), 256 threads; wave w owns queries [blk*128 + 32w, +32) as 2 x 16.
-template <bool CAUSAL>
-__global__ __launch_bounds__(256) void attn_fwd_kernel(Tensor4 Q, Tensor4 K, Tensor4 V, uint16_t* __restrict__ O,
+// MINW: waves per SIMD the register allocation must allow (occupancy); DEEP: K/V tiles are
+// prefetched two tiles ahead (two register stage sets, loop unrolled by 2) instead of one.
+template <bool CAUSAL, int MINW, bool DEEP>
+__global__ __launch_bounds__(256, MINW) void attn_fwd_kernel(Tensor4 Q, Tensor4 K, Tensor4 V, uint16_t* __restrict__ O,
                                                        int64_t o_sb, int64_t o_sh, int64_t o_st,
                                                        float* __restrict__ LSE, int H, int T, float sl2) {
   __shared__ __attribute__((aligned(16))) char lds[2 * 64 * ROW_BYTES];
@@ -139,20 +149,18 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(Tensor4 Q, Tensor4 K, Ten
 
   const int kv_end = CAUSAL ? min(T, qblk + 128) : T;
   const int ntiles = (kv_end + 63) / 64;
-  Stage sk, sv;
-  sk.load(K, koff, 0, T, tid);
-  sv.load(V, voff, 0, T, tid);
-  for (int t = 0; t < ntiles; ++t) {
+  // one K/V tile: wait for its staged registers, publish to LDS, prefetch tile `tn`, compute
+  auto tile = [&](int t, Stage& sk, Stage& sv, int tn) {
     const int kv0 = t * 64;
     __syncthreads();
     sk.store(Ks, tid);
     sv.store(Vs, tid);
     __syncthreads();
-    if (t + 1 < ntiles) {  // prefetch the next tile into registers while this one computes
-      sk.load(K, koff, kv0 + 64, T, tid);
-      sv.load(V, voff, kv0 + 64, T, tid);
+    if (tn < ntiles) {  // prefetch into the registers just drained, while this tile computes
+      sk.load(K, koff, tn * 64, T, tid);
+      sv.load(V, voff, tn * 64, T, tid);
     }
-    if (CAUSAL && kv0 > qbase + 31) continue;
+    if (CAUSAL && kv0 > qbase + 31) return;
     // ---- S^T = K Q^T for 4 key subtiles x 2 query blocks
     f4 st[2][4];
 #pragma unroll
@@ -191,14 +199,14 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(Tensor4 Q, Tensor4 K, Ten
       mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
       mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
       const float mn = fmaxf(m[qb], mt * sl2);  // running max in log2-scaled units
-      const float alpha = (mn == -INFINITY) ? 1.f : exp2f(m[qb] - mn);
+      const float alpha = (mn == -INFINITY) ? 1.f : fast_exp2(m[qb] - mn);
       const float msub = (mn == -INFINITY) ? 0.f : mn;
       float ls = 0.f;
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float p = exp2f(fmaf(st[qb][ks][r], sl2, -msub));
+          const float p = fast_exp2(fmaf(st[qb][ks][r], sl2, -msub));
           st[qb][ks][r] = p;
           ls += p;
         }
@@ -220,6 +228,24 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(Tensor4 Q, Tensor4 K, Ten
 #pragma unroll
         for (int qb = 0; qb < 2; ++qb) oacc[qb][n] = mfma(va, pb[qb][kst], oacc[qb][n]);
       }
+    };
+  if (DEEP) {
+    Stage sk0, sv0, sk1, sv1;
+    sk0.load(K, koff, 0, T, tid);
+    sv0.load(V, voff, 0, T, tid);
+    if (ntiles > 1) {
+      sk1.load(K, koff, 64, T, tid);
+      sv1.load(V, voff, 64, T, tid);
+    }
+    for (int t = 0; t < ntiles; t += 2) {
+      tile(t, sk0, sv0, t + 2);
+      if (t + 1 < ntiles) tile(t + 1, sk1, sv1, t + 3);
+    }
+  } else {
+    Stage sk, sv;
+    sk.load(K, koff, 0, T, tid);
+    sv.load(V, voff, 0, T, tid);
+    for (int t = 0; t < ntiles; ++t) tile(t, sk, sv, t + 1);
   }
   // ---- epilogue: normalise, store O (8 B per lane per d-tile) and LSE
 #pragma unroll
@@ -338,7 +364,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(Tensor4 Q, Tensor4 K, 
         f4 ds;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          float p = exp2f(fmaf(s[r], sl2, -lse2[qb]));
+          float p = fast_exp2(fmaf(s[r], sl2, -lse2[qb]));
           if (edge) {
             const int key = kv0 + ks * 16 + 4 * g + r;
             if (key >= T || qi >= T || (CAUSAL && key > qi)) p = 0.f;
@@ -382,7 +408,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(Tensor4 Q, Tensor4 K, 
 // Per 64-query tile (Q, dO staged in LDS): S = Q K^T and dP = dO V^T with lane = key,
 // dV^T += dO^T P and dK^T += Q^T dS (dO^T, Q^T via transposed LDS reads).
 template <bool CAUSAL>
-__global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(Tensor4 Q, Tensor4 K, Tensor4 V, Tensor4 DO,
+__global__ __launch_bounds__(256, DKDV_MINW) void attn_bwd_dkdv_kernel(Tensor4 Q, Tensor4 K, Tensor4 V, Tensor4 DO,
                                                             const float* __restrict__ LSE,
                                                             const float* __restrict__ DELTA, uint16_t* __restrict__ DK,
                                                             uint16_t* __restrict__ DV, int64_t g_sb, int64_t g_sh,
@@ -466,7 +492,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(Tensor4 Q, Tensor4 K
           for (int r = 0; r < 4; ++r) {
             const int ql = qs * 16 + 4 * g + r;
             const int qi = q0 + ql;
-            float p = exp2f(fmaf(s[r], sl2, -srow[0][ql]));
+            float p = fast_exp2(fmaf(s[r], sl2, -srow[0][ql]));
             if (edge && (qi >= T || key >= T || (CAUSAL && key > qi))) p = 0.f;
             pp[half][r] = p;
             dd[half][r] = p * (dp[r] - srow[1][ql]);
@@ -506,6 +532,11 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(Tensor4 Q, Tensor4 K
 
 extern "C" {
 
+// Forward kernel variant (benchmarking): 0 = 2 waves/SIMD, 1-deep prefetch; 1 = 3 waves/SIMD;
+// 2 = 4 waves/SIMD; 3 = 2 waves/SIMD, 2-deep prefetch; 4 = 3 waves/SIMD, 2-deep.
+static int g_attn_fwd_variant = 0;
+void pdt_attn_set_variant(int fwd) { g_attn_fwd_variant = fwd; }
+
 // q/k/v/o/do/dq/dk/dv: bf16 [B, H, T, 64] views given by (b, h, t) strides (d stride 1, 16-B aligned rows).
 int pdt_attn_fwd(const uint16_t* q, const int64_t* qs, const uint16_t* k, const int64_t* ks, const uint16_t* v,
                  const int64_t* vs, uint16_t* o, const int64_t* os, float* lse, int B, int H, int T, int Dh,
@@ -514,10 +545,17 @@ int pdt_attn_fwd(const uint16_t* q, const int64_t* qs, const uint16_t* k, const 
   const Tensor4 Q{q, qs[0], qs[1], qs[2]}, K{k, ks[0], ks[1], ks[2]}, V{v, vs[0], vs[1], vs[2]};
   const dim3 grid((T + 127) / 128, H, B);
   const float sl2 = scale * LOG2E;
-  if (causal)
-    hipLaunchKernelGGL(attn_fwd_kernel<true>, grid, dim3(256), 0, s, Q, K, V, o, os[0], os[1], os[2], lse, H, T, sl2);
-  else
-    hipLaunchKernelGGL(attn_fwd_kernel<false>, grid, dim3(256), 0, s, Q, K, V, o, os[0], os[1], os[2], lse, H, T, sl2);
+#define PDT_FWD(C, MW, DP)                                                                                  \
+  hipLaunchKernelGGL((attn_fwd_kernel<C, MW, DP>), grid, dim3(256), 0, s, Q, K, V, o, os[0], os[1], os[2], lse, \
+                     H, T, sl2)
+  switch (g_attn_fwd_variant) {
+    case 1: if (causal) PDT_FWD(true, 3, false); else PDT_FWD(false, 3, false); break;
+    case 2: if (causal) PDT_FWD(true, 4, false); else PDT_FWD(false, 4, false); break;
+    case 3: if (causal) PDT_FWD(true, 2, true); else PDT_FWD(false, 2, true); break;
+    case 4: if (causal) PDT_FWD(true, 3, true); else PDT_FWD(false, 3, true); break;
+    default: if (causal) PDT_FWD(true, 2, false); else PDT_FWD(false, 2, false); break;
+  }
+#undef PDT_FWD
   return 0;
 }
 
