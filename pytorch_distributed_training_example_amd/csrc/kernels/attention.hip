@@ -88,15 +88,23 @@ __device__ __forceinline__ bf16x8 gload8(const uint16_t* p, bool ok) {
   return z;
 }
 
+// Buffer resource over one (batch, head) slice of a [B, H, T, 64] view: rows 0..T-1 at stride
+// `st` elements. Loads past row T-1 fall outside num_records and return 0 in hardware, so tile
+// staging needs no per-row bounds branch (raw buffer, stride 0; dword3 = gfx9 raw-buffer format).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t slice_rsrc(const uint16_t* base, int T, int64_t st) {
+  const uint32_t bytes = (uint32_t)(((int64_t)(T - 1) * st + D) * 2);
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(base), (short)0, bytes, 0x00020000);
+}
+
 // Stage a 64-row tile (rows r0.. of a [T, 64] head slice) into LDS: 512 16-B chunks, 2 per thread.
 struct Stage {
   bf16x8 v[2];
-  __device__ __forceinline__ void load(const Tensor4& t, int64_t base, int r0, int T, int tid) {
+  __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t rs, int64_t st, int r0, int tid) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int id = tid + 256 * u, row = id >> 3, ch = id & 7;
-      const int gr = r0 + row;
-      v[u] = gload8(t.p + base + (int64_t)gr * t.st + ch * 8, gr < T);
+      const uint32_t off = (uint32_t)(((int64_t)(r0 + row) * st + ch * 8) * 2);
+      v[u] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
     }
   }
   __device__ __forceinline__ void store(char* tile, int tid) const {
@@ -127,6 +135,7 @@ __global__ __launch_bounds__(256, MINW) void attn_fwd_kernel(Tensor4 Q, Tensor4 
   const int64_t qoff = (int64_t)b * Q.sb + (int64_t)h * Q.sh;
   const int64_t koff = (int64_t)b * K.sb + (int64_t)h * K.sh;
   const int64_t voff = (int64_t)b * V.sb + (int64_t)h * V.sh;
+  const __amdgpu_buffer_rsrc_t krs = slice_rsrc(K.p + koff, T, K.st), vrs = slice_rsrc(V.p + voff, T, V.st);
 
   // Q^T as B operand, held in registers: [qb][k-step]
   bf16x8 bq[2][2];
@@ -157,10 +166,10 @@ __global__ __launch_bounds__(256, MINW) void attn_fwd_kernel(Tensor4 Q, Tensor4 
     sv.store(Vs, tid);
     __syncthreads();
     if (tn < ntiles) {  // prefetch into the registers just drained, while this tile computes
-      sk.load(K, koff, tn * 64, T, tid);
-      sv.load(V, voff, tn * 64, T, tid);
+      sk.load(krs, K.st, tn * 64, tid);
+      sv.load(vrs, V.st, tn * 64, tid);
     }
-    if (CAUSAL && kv0 > qbase + 31) return;
+    if (qbase >= T || (CAUSAL && kv0 > qbase + 31)) return;  // wave has no query here
     // ---- S^T = K Q^T for 4 key subtiles x 2 query blocks
     f4 st[2][4];
 #pragma unroll
@@ -231,11 +240,11 @@ __global__ __launch_bounds__(256, MINW) void attn_fwd_kernel(Tensor4 Q, Tensor4 
     };
   if (DEEP) {
     Stage sk0, sv0, sk1, sv1;
-    sk0.load(K, koff, 0, T, tid);
-    sv0.load(V, voff, 0, T, tid);
+    sk0.load(krs, K.st, 0, tid);
+    sv0.load(vrs, V.st, 0, tid);
     if (ntiles > 1) {
-      sk1.load(K, koff, 64, T, tid);
-      sv1.load(V, voff, 64, T, tid);
+      sk1.load(krs, K.st, 64, tid);
+      sv1.load(vrs, V.st, 64, tid);
     }
     for (int t = 0; t < ntiles; t += 2) {
       tile(t, sk0, sv0, t + 2);
@@ -243,8 +252,8 @@ __global__ __launch_bounds__(256, MINW) void attn_fwd_kernel(Tensor4 Q, Tensor4 
     }
   } else {
     Stage sk, sv;
-    sk.load(K, koff, 0, T, tid);
-    sv.load(V, voff, 0, T, tid);
+    sk.load(krs, K.st, 0, tid);
+    sv.load(vrs, V.st, 0, tid);
     for (int t = 0; t < ntiles; ++t) tile(t, sk, sv, t + 1);
   }
   // ---- epilogue: normalise, store O (8 B per lane per d-tile) and LSE
@@ -293,7 +302,7 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(Tensor4 DO, Tensor4 O
 // Forward structure: S^T = K Q^T, dP^T = V dO^T (lane = query), dS^T = P^T (dP^T - delta),
 // dQ^T += K^T dS^T (K^T by transposed LDS reads).
 template <bool CAUSAL>
-__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(Tensor4 Q, Tensor4 K, Tensor4 V, Tensor4 DO,
+__global__ __launch_bounds__(256, CAUSAL ? 2 : 3) void attn_bwd_dq_kernel(Tensor4 Q, Tensor4 K, Tensor4 V, Tensor4 DO,
                                                           const float* __restrict__ LSE, const float* __restrict__ DELTA,
                                                           uint16_t* __restrict__ DQ, int64_t dq_sb, int64_t dq_sh,
                                                           int64_t dq_st, int H, int T, float sl2, float scale) {
@@ -333,9 +342,10 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(Tensor4 Q, Tensor4 K, 
 
   const int kv_end = CAUSAL ? min(T, qblk + 128) : T;
   const int ntiles = (kv_end + 63) / 64;
+  const __amdgpu_buffer_rsrc_t krs = slice_rsrc(K.p + koff, T, K.st), vrs = slice_rsrc(V.p + voff, T, V.st);
   Stage sk, sv;
-  sk.load(K, koff, 0, T, tid);
-  sv.load(V, voff, 0, T, tid);
+  sk.load(krs, K.st, 0, tid);
+  sv.load(vrs, V.st, 0, tid);
   for (int t = 0; t < ntiles; ++t) {
     const int kv0 = t * 64;
     __syncthreads();
@@ -343,10 +353,10 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(Tensor4 Q, Tensor4 K, 
     sv.store(Vs, tid);
     __syncthreads();
     if (t + 1 < ntiles) {
-      sk.load(K, koff, kv0 + 64, T, tid);
-      sv.load(V, voff, kv0 + 64, T, tid);
+      sk.load(krs, K.st, kv0 + 64, tid);
+      sv.load(vrs, V.st, kv0 + 64, tid);
     }
-    if (CAUSAL && kv0 > qbase + 31) continue;
+    if (qbase >= T || (CAUSAL && kv0 > qbase + 31)) continue;
     bf16x8 dsb[2][2];
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
@@ -451,9 +461,10 @@ __global__ __launch_bounds__(256, DKDV_MINW) void attn_bwd_dkdv_kernel(Tensor4 Q
 
   const int q_start = CAUSAL ? (kblk / 64) * 64 : 0;
   const int ntiles = (T - q_start + 63) / 64;
+  const __amdgpu_buffer_rsrc_t qrs = slice_rsrc(Q.p + qoff, T, Q.st), drs = slice_rsrc(DO.p + dooff, T, DO.st);
   Stage sq, sd;
-  sq.load(Q, qoff, q_start, T, tid);
-  sd.load(DO, dooff, q_start, T, tid);
+  sq.load(qrs, Q.st, q_start, tid);
+  sd.load(drs, DO.st, q_start, tid);
   for (int t = 0; t < ntiles; ++t) {
     const int q0 = q_start + t * 64;
     __syncthreads();
@@ -466,10 +477,11 @@ __global__ __launch_bounds__(256, DKDV_MINW) void attn_bwd_dkdv_kernel(Tensor4 Q
     }
     __syncthreads();
     if (t + 1 < ntiles) {
-      sq.load(Q, qoff, q0 + 64, T, tid);
-      sd.load(DO, dooff, q0 + 64, T, tid);
+      sq.load(qrs, Q.st, q0 + 64, tid);
+      sd.load(drs, DO.st, q0 + 64, tid);
     }
-    if (CAUSAL && q0 + 63 < kbase) continue;  // every query of the tile precedes this wave's keys
+    // no key of this wave exists, or every query of the tile precedes this wave's keys
+    if (kbase >= T || (CAUSAL && q0 + 63 < kbase)) continue;
 #pragma unroll
     for (int kq = 0; kq < 2; ++kq) {  // 32-query k-step for the dV/dK products
       bf16x8 pb[2], dsb[2];
