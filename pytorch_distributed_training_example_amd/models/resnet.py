@@ -19,7 +19,7 @@ import torch
 from torch import nn
 
 from ..ops.batchnorm import BatchNorm2d, ResidualGradLink
-from ..ops.conv import Conv1x1
+from ..ops.conv import Conv1x1, linked_conv
 
 
 def conv3x3(inp: int, out: int, stride: int = 1, groups: int = 1, dilation: int = 1) -> nn.Conv2d:
@@ -93,15 +93,22 @@ class Bottleneck(nn.Module):
         self.stride = stride
 
     def forward(self, x):
-        if (RESIDUAL_GRAD_LINK[0] and self.downsample is None and self.training and x.requires_grad and torch.is_grad_enabled()
+        if (RESIDUAL_GRAD_LINK[0] and self.training and x.requires_grad and torch.is_grad_enabled()
                 and isinstance(self.conv1, Conv1x1) and isinstance(self.bn3, BatchNorm2d)
                 and self.conv1.gemm_eligible(x) and x.shape[1] % 64 == 0):
-            # identity block: bn3's backward hands the residual gradient to conv1's backward,
-            # which accumulates its data-gradient GEMM into it (no autograd add kernel)
+            # the two gradients of x (conv1 branch, shortcut) meet in conv1's data-gradient GEMM
+            # (beta = 1) instead of an autograd add kernel (ops/batchnorm.py ResidualGradLink)
             link = ResidualGradLink()
             out = bn_act(self.bn1, self.conv1(x, res_link=link), relu=True)
             out = bn_act(self.bn2, self.conv2(out), relu=True)
-            return self.bn3(self.conv3(out), residual=x, relu=True, res_link=link)
+            out = self.conv3(out)
+            if self.downsample is None:  # identity: bn3's backward deposits the shortcut gradient
+                return self.bn3(out, residual=x, relu=True, res_link=link)
+            # shortcut built AFTER the main branch so its backward nodes run first (higher
+            # autograd sequence numbers): the shortcut conv deposits, conv1 accumulates. Either
+            # order is correct (whichever branch finishes second adds), this one saves a pass.
+            identity = bn_act(self.downsample[1], linked_conv(self.downsample[0], x, link))
+            return bn_act(self.bn3, out, residual=identity, relu=True)
         identity = x if self.downsample is None else self.downsample(x)
         out = bn_act(self.bn1, self.conv1(x), relu=True)
         out = bn_act(self.bn2, self.conv2(out), relu=True)

@@ -32,11 +32,13 @@ def bn_reference(x, residual, weight, bias, running_mean, running_var, training,
 
 
 class ResidualGradLink:
-    """Hands the residual-branch gradient of a fused ``relu(bn(x) + identity)`` to the op that
-    consumes ``identity`` on the main branch (ResNet bottleneck: conv1 of the same block), so
-    that op accumulates into it (GEMM with beta = 1) instead of autograd summing the two
-    branch gradients with a separate add kernel (a full read-read-write pass per block).
-    The BN backward always runs first: the main branch is upstream of the BN."""
+    """Meeting point of the two branch gradients of one tensor (a ResNet block input feeds the
+    main branch's conv1 and the shortcut): the first branch to finish backward deposits its
+    gradient here and returns None to autograd; the second accumulates into it — conv1's
+    data-gradient GEMM with beta = 1 — and returns the sum, so autograd never runs a separate
+    add kernel (a full read-read-write pass per block). Identity blocks: the fused
+    ``relu(bn3(x) + identity)`` backward deposits (it always runs first: the main branch is
+    upstream of it); downsample blocks: the shortcut conv deposits (ops/conv.py linked_conv)."""
 
     __slots__ = ("grad",)
 

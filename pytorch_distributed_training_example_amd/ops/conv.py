@@ -105,7 +105,9 @@ class _Conv1x1Fn(torch.autograd.Function):
                                                        1, mask)
 
         # residual-branch gradient of x handed over by the block's fused BN (ResidualGradLink)
+        # the other branch's gradient of x, if it already arrived (ResidualGradLink)
         acc = ctx.link.take() if ctx.link is not None else None
+        first = ctx.link is not None and acc is None
         if ctx.needs_input_grad[0]:
             algo = _pick(("bwd_data", M, Ci, Co), {
                 "miopen": lambda: conv_bwd([True, False, False]),
@@ -122,6 +124,8 @@ class _Conv1x1Fn(torch.autograd.Function):
                 dx = dx.add_(acc)
         elif acc is not None:
             dx = acc
+        if first and dx is not None:  # first of the two branches: leave dx for the partner to add to
+            ctx.link.grad, dx = dx, None
         if ctx.needs_input_grad[1]:
             algo = _pick(("bwd_weight", M, Ci, Co), {
                 "miopen": lambda: conv_bwd([False, True, False]),
@@ -133,6 +137,41 @@ class _Conv1x1Fn(torch.autograd.Function):
             else:
                 dw = conv_bwd([False, True, False])[1]
         return dx, dw, None
+
+
+class _LinkedConvFn(torch.autograd.Function):
+    """Plain (MIOpen) convolution whose input gradient meets the other branch's gradient of the
+    same input through a ``ResidualGradLink``: the first branch to finish backward stashes its
+    gradient and returns None, the second adds into it and returns the sum — correct in either
+    execution order, no autograd add node."""
+
+    @staticmethod
+    def forward(ctx, x, weight, stride, padding, link):
+        ctx.save_for_backward(x, weight)
+        ctx.stride, ctx.padding, ctx.link = stride, padding, link
+        return F.conv2d(x, weight, None, stride, padding)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, weight = ctx.saved_tensors
+        gy = gy.contiguous(memory_format=torch.channels_last)
+        dx, dw, _ = torch.ops.aten.convolution_backward(
+            gy, x, weight, None, list(ctx.stride), list(ctx.padding), [1, 1], False, [0, 0], 1,
+            [ctx.needs_input_grad[0], ctx.needs_input_grad[1], False])
+        if dx is not None:
+            acc = ctx.link.take()
+            if acc is None:
+                ctx.link.grad, dx = dx, None
+            else:
+                dx = acc.add_(dx)
+        return dx, dw, None, None, None
+
+
+def linked_conv(conv: nn.Conv2d, x: torch.Tensor, link) -> torch.Tensor:
+    """``conv(x)`` whose input gradient is summed with the partner branch's through ``link``."""
+    if isinstance(conv, Conv1x1) and conv.gemm_eligible(x):
+        return conv(x, res_link=link)
+    return _LinkedConvFn.apply(x, conv.weight, conv.stride, conv.padding, link)
 
 
 class Conv1x1(nn.Conv2d):

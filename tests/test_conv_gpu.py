@@ -31,14 +31,18 @@ def test_conv1x1_matches_fp32(monkeypatch, mode, shape):
     assert m.weight.grad.stride() == m.weight.stride()
 
 
-def test_bottleneck_residual_grad_link_matches_autograd_add():
-    """Identity bottleneck: conv1's dgrad GEMM accumulating bn3's residual gradient (beta = 1)
-    gives the same input/weight gradients as autograd's separate add."""
+@pytest.mark.parametrize("kind", ["identity", "downsample_s1", "downsample_s2"])
+def test_bottleneck_residual_grad_link_matches_autograd_add(kind):
+    """Bottleneck blocks: conv1's dgrad GEMM accumulating the shortcut's gradient of x (beta = 1;
+    identity: deposited by bn3's backward, downsample: by the shortcut conv) gives the same input
+    and weight gradients as autograd's separate add."""
     from pytorch_distributed_training_example_amd.models import resnet as R
     from pytorch_distributed_training_example_amd.models.precision import to_bf16_mixed
     torch.manual_seed(0)
-    blk = to_bf16_mixed(R.Bottleneck(256, 64).cuda().to(memory_format=torch.channels_last))
-    x0 = torch.randn(8, 256, 14, 14, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    cin, stride = {"identity": (256, 1), "downsample_s1": (64, 1), "downsample_s2": (256, 2)}[kind]
+    ds = None if kind == "identity" else R._Downsample(R.conv1x1(cin, 256, stride), R._bn(256))
+    blk = to_bf16_mixed(R.Bottleneck(cin, 64, stride, ds).cuda().to(memory_format=torch.channels_last))
+    x0 = torch.randn(8, cin, 14, 14, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
     out = {}
     for linked in (True, False):
         R.RESIDUAL_GRAD_LINK[0] = linked
