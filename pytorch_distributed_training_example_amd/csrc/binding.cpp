@@ -51,10 +51,10 @@ int pdt_ce_bwd(const void* logits, int dtype, const int64_t* target, const float
                float dloss_scale, int64_t N, int64_t V, float smoothing, int64_t ignore_index, void* dlogits,
                hipStream_t s);
 int64_t pdt_ln_workspace_floats(int64_t N, int D);
-int pdt_ln_fwd(const void* x, int dtype, const float* w, const float* b, void* y, float* mean, float* rstd, int64_t N,
-               int D, float eps, hipStream_t s);
-int pdt_ln_bwd(const void* dy, const void* x, int dtype, const float* w, const float* mean, const float* rstd,
-               void* dx, float* dw, float* db, int64_t N, int D, float* ws, hipStream_t s);
+int pdt_ln_fwd(const void* x, const void* res, int dtype, const float* w, const float* b, void* y, void* sum_out,
+               float* mean, float* rstd, int64_t N, int D, float eps, hipStream_t s);
+int pdt_ln_bwd(const void* dy, const void* x, const void* dres, int dtype, const float* w, const float* mean,
+               const float* rstd, void* dx, float* dw, float* db, int64_t N, int D, float* ws, hipStream_t s);
 int pdt_attn_fwd(const uint16_t* q, const int64_t* qs, const uint16_t* k, const int64_t* ks, const uint16_t* v,
                  const int64_t* vs, uint16_t* o, const int64_t* os, float* lse, int B, int H, int T, int Dh,
                  int causal, float scale, hipStream_t s);
@@ -443,30 +443,43 @@ Tensor ce_bwd(Tensor logits, Tensor target, Tensor lse, c10::optional<Tensor> dl
 }
 
 // ----------------------------------------------------------------------------- layernorm
-std::vector<Tensor> ln_fwd(Tensor x, Tensor w, Tensor b, double eps) {
+// res: optional residual branch; then the sum s = x + res is returned as a 4th output and normalised.
+std::vector<Tensor> ln_fwd(Tensor x, Tensor w, Tensor b, double eps, c10::optional<Tensor> res) {
   check_cuda(x, "x");
   TORCH_CHECK(x.is_contiguous(), "ln: x must be contiguous");
   const int64_t D = x.size(-1), N = x.numel() / D;
   TORCH_CHECK(w.scalar_type() == at::kFloat && b.scalar_type() == at::kFloat, "ln: weight/bias must be fp32");
+  const bool hr = res.has_value() && res->defined();
+  if (hr)
+    TORCH_CHECK(res->is_contiguous() && res->sizes() == x.sizes() && res->scalar_type() == x.scalar_type(),
+                "ln: residual must match x (contiguous, same shape/dtype)");
   auto y = at::empty_like(x);
+  Tensor sum;
+  if (hr) sum = at::empty_like(x);
   auto fopt = x.options().dtype(at::kFloat);
   auto mean = at::empty({N}, fopt), rstd = at::empty({N}, fopt);
-  int rc = pdt_ln_fwd(x.data_ptr(), dcode(x), w.data_ptr<float>(), b.data_ptr<float>(), y.data_ptr(),
-                      mean.data_ptr<float>(), rstd.data_ptr<float>(), N, (int)D, (float)eps, stream());
+  int rc = pdt_ln_fwd(x.data_ptr(), hr ? res->data_ptr() : nullptr, dcode(x), w.data_ptr<float>(),
+                      b.data_ptr<float>(), y.data_ptr(), hr ? sum.data_ptr() : nullptr, mean.data_ptr<float>(),
+                      rstd.data_ptr<float>(), N, (int)D, (float)eps, stream());
   TORCH_CHECK(rc == 0, "pdt_ln_fwd: unsupported D=", D);
-  return {y, mean, rstd};
+  return {y, mean, rstd, sum};
 }
 
-std::vector<Tensor> ln_bwd(Tensor dy, Tensor x, Tensor w, Tensor mean, Tensor rstd) {
+// dres: optional gradient added into dx (the residual stream's own gradient).
+std::vector<Tensor> ln_bwd(Tensor dy, Tensor x, Tensor w, Tensor mean, Tensor rstd, c10::optional<Tensor> dres) {
   TORCH_CHECK(dy.is_contiguous() && x.is_contiguous(), "ln bwd: contiguous inputs required");
   const int64_t D = x.size(-1), N = x.numel() / D;
+  const bool hr = dres.has_value() && dres->defined();
+  if (hr)
+    TORCH_CHECK(dres->is_contiguous() && dres->sizes() == x.sizes() && dres->scalar_type() == x.scalar_type(),
+                "ln bwd: dres must match x (contiguous, same shape/dtype)");
   auto dx = at::empty_like(x);
   auto fopt = x.options().dtype(at::kFloat);
   auto dw = at::empty({D}, fopt), db = at::empty({D}, fopt);
   auto ws = at::empty({std::max<int64_t>(pdt_ln_workspace_floats(N, (int)D), 1)}, fopt);
-  int rc = pdt_ln_bwd(dy.data_ptr(), x.data_ptr(), dcode(x), w.data_ptr<float>(), mean.data_ptr<float>(),
-                      rstd.data_ptr<float>(), dx.data_ptr(), dw.data_ptr<float>(), db.data_ptr<float>(), N, (int)D,
-                      ws.data_ptr<float>(), stream());
+  int rc = pdt_ln_bwd(dy.data_ptr(), x.data_ptr(), hr ? dres->data_ptr() : nullptr, dcode(x), w.data_ptr<float>(),
+                      mean.data_ptr<float>(), rstd.data_ptr<float>(), dx.data_ptr(), dw.data_ptr<float>(),
+                      db.data_ptr<float>(), N, (int)D, ws.data_ptr<float>(), stream());
   TORCH_CHECK(rc == 0, "pdt_ln_bwd: unsupported D=", D);
   return {dx, dw, db};
 }
@@ -794,8 +807,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_bwd_train", &bn_bwd_train);
   m.def("ce_fwd", &ce_fwd);
   m.def("ce_bwd", &ce_bwd);
-  m.def("ln_fwd", &ln_fwd);
-  m.def("ln_bwd", &ln_bwd);
+  m.def("ln_fwd", &ln_fwd, py::arg("x"), py::arg("w"), py::arg("b"), py::arg("eps"), py::arg("res") = py::none());
+  m.def("ln_bwd", &ln_bwd, py::arg("dy"), py::arg("x"), py::arg("w"), py::arg("mean"), py::arg("rstd"),
+        py::arg("dres") = py::none());
   m.def("bias_gelu_fwd", &bias_gelu_fwd);
   m.def("bias_gelu_bwd", &bias_gelu_bwd);
   m.def("attn_fwd_out", &attn_fwd_out);

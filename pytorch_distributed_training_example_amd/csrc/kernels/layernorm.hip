@@ -5,6 +5,12 @@
 // vectors), so the forward is an exact two-pass mean/variance with a single HBM read and
 // write. The backward computes dx per row in registers and per-workgroup partial
 // dgamma/dbeta (fixed-order second pass: deterministic, no atomics).
+//
+// Residual fusion (pre-norm transformer blocks): the forward optionally adds a residual branch
+// first, s = x + h (rounded to the storage dtype, exactly as a separate add would store it),
+// writes s (the new residual stream) and normalises it; the backward optionally adds the
+// residual stream's own gradient, dx = LN'(dy) + ds. That removes the separate add kernels
+// (2 per block forward, 2 per block backward) and one full read of s.
 #include "../common.h"
 
 using namespace pdt;
@@ -13,10 +19,14 @@ namespace {
 
 constexpr int kRowsPerBlock = 4;  // 4 waves, one row each
 
+template <typename T> __device__ __forceinline__ float round_to(float v) { return v; }
+template <> __device__ __forceinline__ float round_to<uint16_t>(float v) { return bf2f(f2bf(v)); }
+
 // K = D / 256: 4-element groups per lane (D = 256*K)
 template <typename T, int K>
-__global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, const float* __restrict__ w,
-                                                     const float* __restrict__ b, T* __restrict__ y,
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, const T* __restrict__ res,
+                                                     const float* __restrict__ w, const float* __restrict__ b,
+                                                     T* __restrict__ y, T* __restrict__ sum_out,
                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out,
                                                      int64_t N, float eps) {
   constexpr int D = 256 * K;
@@ -29,6 +39,13 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, co
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     Vec4<T>::ld(xr, (int64_t)(k * 256 + lane * 4), v[k]);
+    if (res != nullptr) {  // s = x + h, stored and normalised at storage precision
+      float hv[4];
+      Vec4<T>::ld(res + row * D, (int64_t)(k * 256 + lane * 4), hv);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[k][j] = round_to<T>(v[k][j] + hv[j]);
+      Vec4<T>::st(sum_out + row * D, (int64_t)(k * 256 + lane * 4), v[k]);
+    }
     s += v[k][0] + v[k][1] + v[k][2] + v[k][3];
   }
   const float mean = wave_sum(s) * (1.f / D);
@@ -55,6 +72,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, co
 // Backward: dx per row; per-block partial dgamma/dbeta written to part[blk][2][D].
 template <typename T, int K>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                     const T* __restrict__ dres,
                                                      const float* __restrict__ w, const float* __restrict__ mean,
                                                      const float* __restrict__ rstd, T* __restrict__ dx,
                                                      float* __restrict__ part, int64_t N, int rows_per_block) {
@@ -71,33 +89,56 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
   }
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
   const int64_t r1 = min(N, r0 + rows_per_block);
-  for (int64_t row = r0 + wv_id; row < r1; row += 4) {
-    const float mu = mean[row], rs = rstd[row];
-    float g[K][4], xh[K][4];
-    float s1 = 0.f, s2 = 0.f;
+  // RF rows per wave in flight (rows r, r + 4, ...): all loads of them are issued before any
+  // row's math, so a wave exposes the memory latency once per RF rows (single-row: 2.5 TB/s)
+  constexpr int RF = K <= 4 ? 4 : 2;
+  for (int64_t row0 = r0 + wv_id; row0 < r1; row0 += 4 * RF) {
+    float g[RF][K][4], xh[RF][K][4], rr[RF][K][4];
+    float mu[RF], rs[RF];
+    bool ok[RF];
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const int64_t c = row * D + k * 256 + lane * 4;
-      Vec4<T>::ld(dy, c, g[k]);
-      Vec4<T>::ld(x, c, xh[k]);
+    for (int q = 0; q < RF; ++q) {
+      const int64_t row = row0 + 4 * q;
+      ok[q] = row < r1;
+      const int64_t rw = ok[q] ? row : row0;  // duplicate load for a missing second row, result unused
+      mu[q] = mean[rw];
+      rs[q] = rstd[rw];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        xh[k][j] = (xh[k][j] - mu) * rs;
-        db[k][j] += g[k][j];
-        dw[k][j] += g[k][j] * xh[k][j];
-        const float gw = g[k][j] * wr[k][j];
-        s1 += gw;
-        s2 += gw * xh[k][j];
+      for (int k = 0; k < K; ++k) {
+        const int64_t c = rw * D + k * 256 + lane * 4;
+        Vec4<T>::ld(dy, c, g[q][k]);
+        Vec4<T>::ld(x, c, xh[q][k]);
+        if (dres != nullptr) Vec4<T>::ld(dres, c, rr[q][k]);
       }
     }
-    s1 = wave_sum(s1) * (1.f / D);
-    s2 = wave_sum(s2) * (1.f / D);
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-      float o[4];
+    for (int q = 0; q < RF; ++q) {
+      if (!ok[q]) continue;
+      const int64_t row = row0 + 4 * q;
+      float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) o[j] = rs * (g[k][j] * wr[k][j] - s1 - xh[k][j] * s2);
-      Vec4<T>::st(dx, row * D + k * 256 + lane * 4, o);
+      for (int k = 0; k < K; ++k)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          xh[q][k][j] = (xh[q][k][j] - mu[q]) * rs[q];
+          db[k][j] += g[q][k][j];
+          dw[k][j] += g[q][k][j] * xh[q][k][j];
+          const float gw = g[q][k][j] * wr[k][j];
+          s1 += gw;
+          s2 += gw * xh[q][k][j];
+        }
+      s1 = wave_sum(s1) * (1.f / D);
+      s2 = wave_sum(s2) * (1.f / D);
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        float o[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          o[j] = rs[q] * (g[q][k][j] * wr[k][j] - s1 - xh[q][k][j] * s2);
+          if (dres != nullptr) o[j] += rr[q][k][j];  // + the residual stream's own gradient
+        }
+        Vec4<T>::st(dx, row * D + k * 256 + lane * 4, o);
+      }
     }
   }
 #pragma unroll
@@ -141,7 +182,7 @@ __global__ __launch_bounds__(256) void ln_bwd_finalize_kernel(const float* __res
 
 inline int ln_bwd_blocks(int64_t N, int& rows_per_block) {
   int64_t nblk = (N + 31) / 32;  // >= 8 rows per wave
-  if (nblk > 256) nblk = 256;
+  if (nblk > 512) nblk = 512;     // 2 workgroups per CU; the dgamma/dbeta slab is nblk x 2 x D floats
   if (nblk < 1) nblk = 1;
   rows_per_block = (int)((N + nblk - 1) / nblk);
   return (int)((N + rows_per_block - 1) / rows_per_block);
@@ -171,25 +212,28 @@ int64_t pdt_ln_workspace_floats(int64_t N, int D) {
     default: return -1;      \
   }
 
-int pdt_ln_fwd(const void* x, int dtype, const float* w, const float* b, void* y, float* mean, float* rstd,
-               int64_t N, int D, float eps, hipStream_t s) {
+// res / sum_out: optional residual branch h and the stored sum s = x + h (both or neither).
+int pdt_ln_fwd(const void* x, const void* res, int dtype, const float* w, const float* b, void* y, void* sum_out,
+               float* mean, float* rstd, int64_t N, int D, float eps, hipStream_t s) {
+  if ((res == nullptr) != (sum_out == nullptr)) return -2;
   if (D % 256 != 0) return -1;
   if (N == 0) return 0;
   const dim3 grid((unsigned)((N + kRowsPerBlock - 1) / kRowsPerBlock));
 #define PDT_LNF(K)                                                                                           \
   if (dtype == 0)                                                                                            \
-    hipLaunchKernelGGL((ln_fwd_kernel<float, K>), grid, dim3(256), 0, s, (const float*)x, w, b, (float*)y, mean, \
-                       rstd, N, eps);                                                                        \
+    hipLaunchKernelGGL((ln_fwd_kernel<float, K>), grid, dim3(256), 0, s, (const float*)x, (const float*)res, w, \
+                       b, (float*)y, (float*)sum_out, mean, rstd, N, eps);                                    \
   else                                                                                                       \
-    hipLaunchKernelGGL((ln_fwd_kernel<uint16_t, K>), grid, dim3(256), 0, s, (const uint16_t*)x, w, b,         \
-                       (uint16_t*)y, mean, rstd, N, eps);
+    hipLaunchKernelGGL((ln_fwd_kernel<uint16_t, K>), grid, dim3(256), 0, s, (const uint16_t*)x,               \
+                       (const uint16_t*)res, w, b, (uint16_t*)y, (uint16_t*)sum_out, mean, rstd, N, eps);
   PDT_LN_SWITCH(PDT_LNF)
 #undef PDT_LNF
   return 0;
 }
 
-int pdt_ln_bwd(const void* dy, const void* x, int dtype, const float* w, const float* mean, const float* rstd,
-               void* dx, float* dw, float* db, int64_t N, int D, float* ws, hipStream_t s) {
+// dres: optional gradient added into dx (residual stream), same dtype/layout as dx.
+int pdt_ln_bwd(const void* dy, const void* x, const void* dres, int dtype, const float* w, const float* mean,
+               const float* rstd, void* dx, float* dw, float* db, int64_t N, int D, float* ws, hipStream_t s) {
   if (D % 256 != 0 || D > 2048) return -1;  // LDS: 2 x 4 x D floats
   if (N == 0) return 0;
   int rpb;
@@ -197,10 +241,10 @@ int pdt_ln_bwd(const void* dy, const void* x, int dtype, const float* w, const f
 #define PDT_LNB(K)                                                                                            \
   if (dtype == 0)                                                                                             \
     hipLaunchKernelGGL((ln_bwd_kernel<float, K>), dim3(nblk), dim3(256), 0, s, (const float*)dy, (const float*)x, \
-                       w, mean, rstd, (float*)dx, ws, N, rpb);                                                \
+                       (const float*)dres, w, mean, rstd, (float*)dx, ws, N, rpb);                            \
   else                                                                                                        \
     hipLaunchKernelGGL((ln_bwd_kernel<uint16_t, K>), dim3(nblk), dim3(256), 0, s, (const uint16_t*)dy,         \
-                       (const uint16_t*)x, w, mean, rstd, (uint16_t*)dx, ws, N, rpb);
+                       (const uint16_t*)x, (const uint16_t*)dres, w, mean, rstd, (uint16_t*)dx, ws, N, rpb);
   switch (D / 256) {
     case 1: PDT_LNB(1); break;
     case 2: PDT_LNB(2); break;

@@ -15,7 +15,7 @@ from torch import nn
 
 from ..ops.cross_entropy import cross_entropy
 from ..ops.layernorm import LayerNorm
-from .transformer import Block, init_weights
+from .transformer import Block, init_weights, run_blocks
 
 
 @dataclass
@@ -46,9 +46,7 @@ class GPT(nn.Module):
         B, T = idx.shape
         pos = torch.arange(T, device=idx.device)
         x = self.transformer.wte(idx) + self.transformer.wpe(pos)
-        for blk in self.transformer.h:
-            x = blk(x)
-        x = self.transformer.ln_f(x)
+        x = run_blocks(self.transformer.h, x, self.transformer.ln_f)  # == ln_f(h[-1](...h[0](x)))
         logits = self.lm_head(x)
         if targets is None:
             return logits

@@ -12,6 +12,7 @@ Not in the reference (LeNet only). MI355X-first choices:
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional
 
 import torch
@@ -20,7 +21,7 @@ from torch import nn
 
 from ..ops.attention import attention_qkv
 from ..ops.gelu import bias_gelu
-from ..ops.layernorm import LayerNorm
+from ..ops.layernorm import LayerNorm, add_layer_norm
 from ..ops.linear import linear as _linear
 
 
@@ -79,6 +80,24 @@ class Block(nn.Module):
         x = x + self.attn(self.ln_1(x))
         x = x + self.mlp(self.ln_2(x))
         return x
+
+
+def run_blocks(blocks, x: torch.Tensor, final_ln: nn.Module) -> torch.Tensor:
+    """``final_ln(blocks(x))`` for pre-norm blocks, with every residual add fused into the
+    LayerNorm that follows it (the block's ln_2, the next block's ln_1, finally ``final_ln``):
+    one add+LN kernel per residual step forward and one LN-backward-with-accumulate backward,
+    instead of separate add kernels each way (ops/layernorm.py add_layer_norm)."""
+    blocks = list(blocks)
+    if not blocks or os.environ.get("PDT_FUSED_ADDLN", "1") == "0":
+        for blk in blocks:
+            x = blk(x)
+        return final_ln(x)
+    y = blocks[0].ln_1(x)
+    for i, blk in enumerate(blocks):
+        x, y = add_layer_norm(x, blk.attn(y), blk.ln_2)
+        nxt = blocks[i + 1].ln_1 if i + 1 < len(blocks) else final_ln
+        x, y = add_layer_norm(x, blk.mlp(y), nxt)
+    return y
 
 
 def init_weights(module: nn.Module, std: float = 0.02, n_layer: Optional[int] = None) -> None:

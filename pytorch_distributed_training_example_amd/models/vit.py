@@ -12,7 +12,7 @@ import torch
 from torch import nn
 
 from ..ops.layernorm import LayerNorm
-from .transformer import Block, init_weights
+from .transformer import Block, init_weights, run_blocks
 
 
 class _Encoder(nn.Module):
@@ -25,9 +25,7 @@ class _Encoder(nn.Module):
 
     def forward(self, x):
         x = x + self.pos_embedding.to(x.dtype)
-        for blk in self.layers:
-            x = blk(x)
-        return self.ln(x)
+        return run_blocks(self.layers, x, self.ln)  # == ln(layers[-1](...layers[0](x)))
 
 
 class _Heads(nn.Module):

@@ -129,6 +129,37 @@ def test_layernorm(D, dtype):
     torch.testing.assert_close(b.grad, bf.grad, rtol=1e-3, atol=1e-2 if dtype == torch.float32 else 3e-1)
 
 
+@pytest.mark.parametrize("D", [768, 1024])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_add_layernorm_fused(D, dtype):
+    """(s, y) = (x + h, LN(x + h)) with both outputs consumed downstream: values and the
+    gradients of x, h (ds + LN'(dy), one kernel) against an fp32 PyTorch reference."""
+    from pytorch_distributed_training_example_amd.ops.layernorm import LayerNorm, add_layer_norm
+    torch.manual_seed(0)
+    ln = LayerNorm(D).to(DEV)
+    with torch.no_grad():
+        ln.weight.uniform_(0.5, 1.5)
+        ln.bias.normal_()
+    x = (torch.randn(6, 33, D, device=DEV) * 2 + 0.5).to(dtype).requires_grad_(True)
+    h = torch.randn(6, 33, D, device=DEV).to(dtype).requires_grad_(True)
+    s, y = add_layer_norm(x, h, ln)
+    xf, hf = x.detach().float().requires_grad_(True), h.detach().float().requires_grad_(True)
+    wf, bf = ln.weight.detach().clone().requires_grad_(True), ln.bias.detach().clone().requires_grad_(True)
+    sf = xf + hf
+    yf = F.layer_norm(sf, (D,), wf, bf, ln.eps)
+    tol = dict(rtol=1e-4, atol=1e-4) if dtype == torch.float32 else dict(rtol=2e-2, atol=3e-2)
+    torch.testing.assert_close(s.float(), sf, **tol)
+    torch.testing.assert_close(y.float(), yf, **tol)
+    gs, gy = torch.randn_like(sf), torch.randn_like(yf)
+    (s.float() * gs.to(dtype).float()).sum().add((y.float() * gy.to(dtype).float()).sum()).backward()
+    ((sf * gs.to(dtype).float()).sum() + (yf * gy.to(dtype).float()).sum()).backward()
+    gtol = tol if dtype == torch.float32 else dict(rtol=3e-2, atol=5e-2)
+    torch.testing.assert_close(x.grad.float(), xf.grad, **gtol)
+    torch.testing.assert_close(h.grad.float(), hf.grad, **gtol)
+    torch.testing.assert_close(ln.weight.grad, wf.grad, rtol=2e-2, atol=3e-1)
+    torch.testing.assert_close(ln.bias.grad, bf.grad, rtol=2e-2, atol=3e-1)
+
+
 # ----------------------------------------------------------------------------- cross entropy
 @pytest.mark.parametrize("V", [10, 1000, 50304, 50257])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
