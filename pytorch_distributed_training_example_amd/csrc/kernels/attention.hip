@@ -17,6 +17,8 @@
 // so dQ needs no atomics and no cross-workgroup reduction (deterministic).
 #include "../common.h"
 
+#include <type_traits>
+
 using namespace pdt;
 
 namespace {
@@ -302,7 +304,7 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(Tensor4 DO, Tensor4 O
 // Forward structure: S^T = K Q^T, dP^T = V dO^T (lane = query), dS^T = P^T (dP^T - delta),
 // dQ^T += K^T dS^T (K^T by transposed LDS reads).
 template <bool CAUSAL>
-__global__ __launch_bounds__(256, CAUSAL ? 2 : 3) void attn_bwd_dq_kernel(Tensor4 Q, Tensor4 K, Tensor4 V, Tensor4 DO,
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(Tensor4 Q, Tensor4 K, Tensor4 V, Tensor4 DO,
                                                           const float* __restrict__ LSE, const float* __restrict__ DELTA,
                                                           uint16_t* __restrict__ DQ, int64_t dq_sb, int64_t dq_sh,
                                                           int64_t dq_st, int H, int T, float sl2, float scale) {
@@ -357,48 +359,55 @@ __global__ __launch_bounds__(256, CAUSAL ? 2 : 3) void attn_bwd_dq_kernel(Tensor
       sv.load(vrs, V.st, kv0 + 64, tid);
     }
     if (qbase >= T || (CAUSAL && kv0 > qbase + 31)) continue;
-    bf16x8 dsb[2][2];
+    // masking only on tiles that cross the sequence end or the causal diagonal (mask-free
+    // instantiation for interior tiles)
+    const bool edge = (kv0 + 64 > T) || (CAUSAL && kv0 + 63 > qbase);
+    auto tile_body = [&](auto edge_c) {
+      constexpr bool EDGE = decltype(edge_c)::value;
+      bf16x8 dsb[2][2];
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      const bf16x8 ka0 = lds_row8(Ks, ks * 16 + c, g), ka1 = lds_row8(Ks, ks * 16 + c, 4 + g);
-      const bf16x8 va0 = lds_row8(Vs, ks * 16 + c, g), va1 = lds_row8(Vs, ks * 16 + c, 4 + g);
+      for (int ks = 0; ks < 4; ++ks) {
+        const bf16x8 ka0 = lds_row8(Ks, ks * 16 + c, g), ka1 = lds_row8(Ks, ks * 16 + c, 4 + g);
+        const bf16x8 va0 = lds_row8(Vs, ks * 16 + c, g), va1 = lds_row8(Vs, ks * 16 + c, 4 + g);
 #pragma unroll
-      for (int qb = 0; qb < 2; ++qb) {
-        f4 s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
-        s = mfma(ka0, bq[qb][0], s);
-        s = mfma(ka1, bq[qb][1], s);
-        dp = mfma(va0, bdo[qb][0], dp);
-        dp = mfma(va1, bdo[qb][1], dp);
-        const int qi = qbase + 16 * qb + c;
-        const bool edge = (kv0 + 64 > T) || (CAUSAL && kv0 + 63 > qbase);
-        f4 ds;
+        for (int qb = 0; qb < 2; ++qb) {
+          f4 s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+          s = mfma(ka0, bq[qb][0], s);
+          s = mfma(ka1, bq[qb][1], s);
+          dp = mfma(va0, bdo[qb][0], dp);
+          dp = mfma(va1, bdo[qb][1], dp);
+          const int qi = qbase + 16 * qb + c;
+          f4 ds;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float p = fast_exp2(fmaf(s[r], sl2, -lse2[qb]));
-          if (edge) {
-            const int key = kv0 + ks * 16 + 4 * g + r;
-            if (key >= T || qi >= T || (CAUSAL && key > qi)) p = 0.f;
+          for (int r = 0; r < 4; ++r) {
+            float p = fast_exp2(fmaf(s[r], sl2, -lse2[qb]));
+            if (EDGE) {
+              const int key = kv0 + ks * 16 + 4 * g + r;
+              if (key >= T || qi >= T || (CAUSAL && key > qi)) p = 0.f;
+            }
+            ds[r] = p * (dp[r] - dlt[qb]);
           }
-          ds[r] = p * (dp[r] - dlt[qb]);
-        }
-        // stash dS^T (fp32) in the S slot; pack after both halves of a 32-key step exist
-        if ((ks & 1) == 0) dsb[qb][ks >> 1] = pack8(ds, f4{0.f, 0.f, 0.f, 0.f});
-        else {
-          bf16x8 t8 = dsb[qb][ks >> 1];
-          t8[4] = (__bf16)ds[0]; t8[5] = (__bf16)ds[1]; t8[6] = (__bf16)ds[2]; t8[7] = (__bf16)ds[3];
-          dsb[qb][ks >> 1] = t8;
+          // stash dS^T (fp32) in the S slot; pack after both halves of a 32-key step exist
+          if ((ks & 1) == 0) dsb[qb][ks >> 1] = pack8(ds, f4{0.f, 0.f, 0.f, 0.f});
+          else {
+            bf16x8 t8 = dsb[qb][ks >> 1];
+            t8[4] = (__bf16)ds[0]; t8[5] = (__bf16)ds[1]; t8[6] = (__bf16)ds[2]; t8[7] = (__bf16)ds[3];
+            dsb[qb][ks >> 1] = t8;
+          }
         }
       }
-    }
-    // dQ^T += K^T dS^T
+      // dQ^T += K^T dS^T
 #pragma unroll
-    for (int n = 0; n < 4; ++n)
+      for (int n = 0; n < 4; ++n)
 #pragma unroll
-      for (int kst = 0; kst < 2; ++kst) {
-        const bf16x8 ka = cat8(lds_tr4(Ks, 32 * kst + 4 * g, 16 * n, lane), lds_tr4(Ks, 32 * kst + 16 + 4 * g, 16 * n, lane));
+        for (int kst = 0; kst < 2; ++kst) {
+          const bf16x8 ka = cat8(lds_tr4(Ks, 32 * kst + 4 * g, 16 * n, lane), lds_tr4(Ks, 32 * kst + 16 + 4 * g, 16 * n, lane));
 #pragma unroll
-        for (int qb = 0; qb < 2; ++qb) dq[qb][n] = mfma(ka, dsb[qb][kst], dq[qb][n]);
-      }
+          for (int qb = 0; qb < 2; ++qb) dq[qb][n] = mfma(ka, dsb[qb][kst], dq[qb][n]);
+        }
+    };
+    if (edge) tile_body(std::true_type{});
+    else tile_body(std::false_type{});
   }
 #pragma unroll
   for (int qb = 0; qb < 2; ++qb) {
@@ -482,48 +491,55 @@ __global__ __launch_bounds__(256, DKDV_MINW) void attn_bwd_dkdv_kernel(Tensor4 Q
     }
     // no key of this wave exists, or every query of the tile precedes this wave's keys
     if (kbase >= T || (CAUSAL && q0 + 63 < kbase)) continue;
+    // masking only on tiles that cross the sequence end or the causal diagonal; interior tiles
+    // run a mask-free instantiation (no per-score compare/select: ~80 VALU ops per tile)
+    const bool edge = (q0 + 64 > T) || (kbase + 32 > T) || (CAUSAL && q0 < kbase + 32);
+    auto tile_body = [&](auto edge_c) {
+      constexpr bool EDGE = decltype(edge_c)::value;
 #pragma unroll
-    for (int kq = 0; kq < 2; ++kq) {  // 32-query k-step for the dV/dK products
-      bf16x8 pb[2], dsb[2];
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb) {
-        f4 pp[2], dd[2];
-#pragma unroll
-        for (int half = 0; half < 2; ++half) {
-          const int qs = 2 * kq + half;  // 16-query subtile
-          const bf16x8 qa0 = lds_row8(Qs, qs * 16 + c, g), qa1 = lds_row8(Qs, qs * 16 + c, 4 + g);
-          const bf16x8 da0 = lds_row8(Ds, qs * 16 + c, g), da1 = lds_row8(Ds, qs * 16 + c, 4 + g);
-          f4 s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
-          s = mfma(qa0, bk[kb][0], s);
-          s = mfma(qa1, bk[kb][1], s);
-          dp = mfma(da0, bv[kb][0], dp);
-          dp = mfma(da1, bv[kb][1], dp);
-          const int key = kbase + 16 * kb + c;
-          const bool edge = (q0 + 64 > T) || (kbase + 32 > T) || (CAUSAL && q0 < kbase + 32);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int ql = qs * 16 + 4 * g + r;
-            const int qi = q0 + ql;
-            float p = fast_exp2(fmaf(s[r], sl2, -srow[0][ql]));
-            if (edge && (qi >= T || key >= T || (CAUSAL && key > qi))) p = 0.f;
-            pp[half][r] = p;
-            dd[half][r] = p * (dp[r] - srow[1][ql]);
-          }
-        }
-        pb[kb] = pack8(pp[0], pp[1]);
-        dsb[kb] = pack8(dd[0], dd[1]);
-      }
-#pragma unroll
-      for (int n = 0; n < 4; ++n) {
-        const bf16x8 doT = cat8(lds_tr4(Ds, 32 * kq + 4 * g, 16 * n, lane), lds_tr4(Ds, 32 * kq + 16 + 4 * g, 16 * n, lane));
-        const bf16x8 qT = cat8(lds_tr4(Qs, 32 * kq + 4 * g, 16 * n, lane), lds_tr4(Qs, 32 * kq + 16 + 4 * g, 16 * n, lane));
+      for (int kq = 0; kq < 2; ++kq) {  // 32-query k-step for the dV/dK products
+        bf16x8 pb[2], dsb[2];
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb) {
-          dv[kb][n] = mfma(doT, pb[kb], dv[kb][n]);
-          dk[kb][n] = mfma(qT, dsb[kb], dk[kb][n]);
+          f4 pp[2], dd[2];
+#pragma unroll
+          for (int half = 0; half < 2; ++half) {
+            const int qs = 2 * kq + half;  // 16-query subtile
+            const bf16x8 qa0 = lds_row8(Qs, qs * 16 + c, g), qa1 = lds_row8(Qs, qs * 16 + c, 4 + g);
+            const bf16x8 da0 = lds_row8(Ds, qs * 16 + c, g), da1 = lds_row8(Ds, qs * 16 + c, 4 + g);
+            f4 s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+            s = mfma(qa0, bk[kb][0], s);
+            s = mfma(qa1, bk[kb][1], s);
+            dp = mfma(da0, bv[kb][0], dp);
+            dp = mfma(da1, bv[kb][1], dp);
+            const int key = kbase + 16 * kb + c;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int ql = qs * 16 + 4 * g + r;
+              const int qi = q0 + ql;
+              float p = fast_exp2(fmaf(s[r], sl2, -srow[0][ql]));
+              if (EDGE && (qi >= T || key >= T || (CAUSAL && key > qi))) p = 0.f;
+              pp[half][r] = p;
+              dd[half][r] = p * (dp[r] - srow[1][ql]);
+            }
+          }
+          pb[kb] = pack8(pp[0], pp[1]);
+          dsb[kb] = pack8(dd[0], dd[1]);
+        }
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+          const bf16x8 doT = cat8(lds_tr4(Ds, 32 * kq + 4 * g, 16 * n, lane), lds_tr4(Ds, 32 * kq + 16 + 4 * g, 16 * n, lane));
+          const bf16x8 qT = cat8(lds_tr4(Qs, 32 * kq + 4 * g, 16 * n, lane), lds_tr4(Qs, 32 * kq + 16 + 4 * g, 16 * n, lane));
+#pragma unroll
+          for (int kb = 0; kb < 2; ++kb) {
+            dv[kb][n] = mfma(doT, pb[kb], dv[kb][n]);
+            dk[kb][n] = mfma(qT, dsb[kb], dk[kb][n]);
+          }
         }
       }
-    }
+    };
+    if (edge) tile_body(std::true_type{});
+    else tile_body(std::false_type{});
   }
 #pragma unroll
   for (int kb = 0; kb < 2; ++kb) {
