@@ -1,0 +1,79 @@
+"""Profiling gate (last row): a training step's kernel trace shows OUR HIP kernels
+for the hot ops, and not the PyTorch/MIOpen kernels they replace.
+
+Runs one step of a small ResNet and a small GPT under ``torch.profiler`` (kineto, ROCm device
+activity) and checks kernel names — the in-test equivalent of the committed rocprofv3 summaries
+in profiles/.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _kernels(fn):
+    from torch.profiler import ProfilerActivity, profile
+    fn()  # warm-up: autotuning / MIOpen find happen outside the trace
+    torch.cuda.synchronize()
+    with profile(activities=[ProfilerActivity.CUDA]) as prof:
+        fn()
+        torch.cuda.synchronize()
+    return [e.name for e in prof.events() if e.device_type == torch.autograd.DeviceType.CUDA]
+
+
+def _has(names, needle):
+    return any(needle in n for n in names)
+
+
+def test_resnet_step_runs_our_kernels():
+    from pytorch_distributed_training_example_amd.models import get_model
+    from pytorch_distributed_training_example_amd.models.precision import to_bf16_mixed
+    from pytorch_distributed_training_example_amd.ops.cross_entropy import cross_entropy
+    from pytorch_distributed_training_example_amd.optim import FusedSGD
+    torch.manual_seed(0)
+    m = to_bf16_mixed(get_model("resnet50", num_classes=64).cuda().to(memory_format=torch.channels_last))
+    opt = FusedSGD(m.parameters(), lr=0.01, momentum=0.9)
+    x = torch.randn(8, 3, 64, 64, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 64, (8,), device="cuda")
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        cross_entropy(m(x), y).backward()
+        opt.step()
+
+    names = _kernels(step)
+    assert names, "no device kernels recorded"
+    for ours in ("bn_reduce2_kernel", "bn_apply_kernel", "bn_bwd_apply_kernel", "bn_apply_pool_kernel",
+                 "maxpool_bwd_kernel", "ce_fwd_kernel", "ce_bwd_kernel", "mt_kernel"):
+        assert _has(names, ours), (ours, sorted(set(names))[:40])
+    for stock in ("MIOpenBatchNorm", "batch_norm", "max_pool", "nll_loss", "log_softmax"):
+        assert not _has(names, stock), (stock, [n for n in names if stock in n][:5])
+    # residual gradients meet in conv1's dgrad GEMM: no per-block autograd add kernels (16 before;
+    # one scalar-sized add per step remains)
+    assert sum("CUDAFunctor_add" in n for n in names) <= 2, [n for n in names if "CUDAFunctor_add" in n]
+
+
+def test_gpt_step_runs_our_kernels():
+    from pytorch_distributed_training_example_amd.models import get_model
+    from pytorch_distributed_training_example_amd.models.precision import to_bf16_mixed
+    from pytorch_distributed_training_example_amd.optim import FusedAdamW
+    torch.manual_seed(0)
+    m = to_bf16_mixed(get_model("gpt2_tiny").cuda())
+    opt = FusedAdamW(m.parameters(), lr=1e-4)
+    idx = torch.randint(0, 512, (4, 64), device="cuda")
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        m(idx, idx).backward()
+        opt.step()
+
+    names = _kernels(step)
+    for ours in ("attn_fwd_kernel", "attn_bwd_dq_kernel", "attn_bwd_dkdv_kernel", "ln_fwd_kernel",
+                 "ln_bwd_kernel", "strip_kernel", "ce_fwd_kernel", "ce_bwd_kernel", "mt_kernel"):
+        assert _has(names, ours), (ours, sorted(set(names))[:40])
+    # aten LayerNorm / GELU / softmax kernels, SDPA's flash / fmha kernels
+    for stock in ("layer_norm", "LayerNorm", "GeluCUDAKernel", "fmha", "flash", "log_softmax", "softmax_warp"):
+        assert not _has(names, stock), (stock, [n for n in names if stock in n][:5])
+    # residual adds are fused into the LayerNorm kernels (4 per block before); what remains is the
+    # token + position embedding add, its gradient fan-in and the tied-embedding weight gradient
+    assert sum("CUDAFunctor_add" in n for n in names) <= 4, [n for n in names if "CUDAFunctor_add" in n]
