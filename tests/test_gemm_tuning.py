@@ -1,0 +1,53 @@
+"""GEMM tuning table plumbing (engine/gemm_tuning.py): merge semantics and the read-only
+TunableOp environment each rank gets. CPU-only (no GEMM runs)."""
+import os
+
+from pytorch_distributed_training_example_amd.engine import gemm_tuning
+
+
+def _write(path, lines):
+    with open(path, "w") as f:
+        f.write("\n".join(lines) + "\n")
+
+
+def test_merge_tables_union_later_wins(tmp_path):
+    a, b, out = tmp_path / "a.csv", tmp_path / "b.csv", tmp_path / "o" / "m.csv"
+    _write(a, ["Validator,PT_VERSION,2.10.0", "GemmTunableOp_BFloat16_TN,tn_1_2_3,Gemm_Hipblaslt_1,0.5",
+               "GemmTunableOp_BFloat16_NN,nn_4_5_6,Gemm_Rocblas_2,0.7"])
+    _write(b, ["Validator,PT_VERSION,9.9.9", "GemmTunableOp_BFloat16_TN,tn_1_2_3,Gemm_Hipblaslt_9,0.4"])
+    assert gemm_tuning.merge_tables([str(a), str(b)], str(out)) == 2
+    text = out.read_text().splitlines()
+    assert text[0] == "Validator,PT_VERSION,2.10.0" and len([t for t in text if t.startswith("Validator")]) == 1
+    assert "GemmTunableOp_BFloat16_TN,tn_1_2_3,Gemm_Hipblaslt_9,0.4" in text
+    assert "GemmTunableOp_BFloat16_NN,nn_4_5_6,Gemm_Rocblas_2,0.7" in text
+
+
+def test_read_only_env_and_per_device_copy(tmp_path, monkeypatch):
+    for k in list(os.environ):
+        if k.startswith("PYTORCH_TUNABLEOP_") or k.startswith("PDT_TUNE") or k == "PDT_GEMM_TUNING":
+            monkeypatch.delenv(k, raising=False)
+    table = tmp_path / "t.csv"
+    _write(table, ["Validator,PT_VERSION,2.10.0", "GemmTunableOp_BFloat16_TN,tn_1_2_3,Gemm_Hipblaslt_1,0.5"])
+    monkeypatch.setattr(gemm_tuning.tempfile, "gettempdir", lambda: str(tmp_path))
+    pattern = gemm_tuning.use_repo_gemm_tuning(device_index=3, table=str(table))
+    assert pattern is not None and pattern.endswith("tunableop%d.csv")
+    assert os.environ["PYTORCH_TUNABLEOP_ENABLED"] == "1"
+    assert os.environ["PYTORCH_TUNABLEOP_TUNING"] == "0"  # never searches inside a timed run
+    copy = pattern.replace("%d", "3")
+    assert open(copy).read() == table.read_text()
+
+
+def test_disabled_and_explicit_env_win(tmp_path, monkeypatch):
+    table = tmp_path / "t.csv"
+    _write(table, ["Validator,PT_VERSION,2.10.0"])
+    monkeypatch.setenv("PDT_GEMM_TUNING", "0")
+    assert gemm_tuning.use_repo_gemm_tuning(table=str(table)) is None
+    monkeypatch.delenv("PDT_GEMM_TUNING")
+    monkeypatch.setenv("PYTORCH_TUNABLEOP_ENABLED", "0")
+    assert gemm_tuning.use_repo_gemm_tuning(table=str(table)) is None
+
+
+def test_committed_table_has_validators_and_entries():
+    lines = open(gemm_tuning.TABLE).read().splitlines()
+    assert any(l.startswith("Validator,GCN_ARCH_NAME,gfx950") for l in lines)
+    assert sum(not l.startswith("Validator") for l in lines if l) >= 10
