@@ -19,11 +19,12 @@ import torch
 from torch import nn
 
 from ..ops.batchnorm import BatchNorm2d, ResidualGradLink
-from ..ops.conv import Conv1x1, linked_conv
+from ..ops.conv import Conv1x1, SplitConv2d, linked_conv
 
 
 def conv3x3(inp: int, out: int, stride: int = 1, groups: int = 1, dilation: int = 1) -> nn.Conv2d:
-    return nn.Conv2d(inp, out, 3, stride=stride, padding=dilation, groups=groups, bias=False, dilation=dilation)
+    cls = SplitConv2d if _norm_kind[0] == "pdt" else nn.Conv2d  # ours: weight grad on a side stream
+    return cls(inp, out, 3, stride=stride, padding=dilation, groups=groups, bias=False, dilation=dilation)
 
 
 def conv1x1(inp: int, out: int, stride: int = 1) -> nn.Conv2d:
@@ -125,7 +126,8 @@ class ResNet(nn.Module):
         self.dilation = 1
         self.groups = groups
         self.base_width = width_per_group
-        self.conv1 = nn.Conv2d(3, self.inplanes, kernel_size=7, stride=2, padding=3, bias=False)
+        stem = SplitConv2d if norm == "pdt" else nn.Conv2d
+        self.conv1 = stem(3, self.inplanes, kernel_size=7, stride=2, padding=3, bias=False)
         self.bn1 = _bn(self.inplanes, fused_relu=True)
         self.relu = nn.ReLU(inplace=True)
         self.maxpool = nn.MaxPool2d(kernel_size=3, stride=2, padding=1)

@@ -29,6 +29,71 @@ from ._native import disabled
 
 _CHOICE: Dict[Tuple, str] = {}
 
+# ---------------------------------------------------------------- weight gradients off the critical path
+# A convolution's weight gradient is needed only by the optimizer / all-reduce, while its data
+# gradient feeds the rest of backward. Issuing the weight-gradient kernel on a side HIP stream
+# lets it run concurrently with the next layers' data-gradient and (bandwidth-bound) BatchNorm
+# backward kernels. The current stream re-joins the side stream (one event wait) before any
+# gradient is read: at every DDP bucket launch and at the end of backward (an autograd-engine
+# callback queued with the first deferred weight gradient of a backward pass).
+# Opt-in (PDT_WGRAD_STREAM=1): measured on one MI355X the concurrency makes ResNet-50 SLOWER
+# (10,212 vs 10,617-10,631 img/s at 512/GPU, tools/gpu_wgrad.sh) — both streams' kernels already
+# fill the chip, and running them together costs cache locality — so the default is in-stream.
+_SIDE: Dict[int, "torch.cuda.Stream"] = {}
+_PENDING: Dict[int, "torch.cuda.Event"] = {}
+_CALLBACK_QUEUED = [False]
+
+
+def _wgrad_stream_enabled() -> bool:
+    return os.environ.get("PDT_WGRAD_STREAM", "0") == "1"
+
+
+def join_wgrad_streams() -> None:
+    """Make the current stream wait for every weight gradient issued on the side stream."""
+    if not _PENDING:
+        return
+    cur = torch.cuda.current_stream()
+    for ev in _PENDING.values():
+        cur.wait_event(ev)
+    _PENDING.clear()
+
+
+def _end_of_backward() -> None:
+    _CALLBACK_QUEUED[0] = False
+    join_wgrad_streams()
+
+
+def _on_side_stream(fn, weight, *used):
+    """Run ``fn()`` (returns ``weight``'s gradient) on the side stream, ordered after the current
+    stream's work; tensors in ``used`` are protected from reuse until the side stream is done.
+
+    The deferral is only safe when autograd will merely *steal* the returned tensor into
+    ``weight.grad`` (no grad yet, strides obeying the parameter's layout); when it would instead
+    accumulate or re-layout on the current stream (gradient accumulation, ``zero_grad(False)``),
+    the current stream joins the side stream immediately — still overlapped with nothing, but
+    correct."""
+    cur = torch.cuda.current_stream()
+    dev = cur.device.index
+    side = _SIDE.get(dev)
+    if side is None:
+        side = _SIDE[dev] = torch.cuda.Stream(device=cur.device)
+    side.wait_stream(cur)
+    with torch.cuda.stream(side):
+        dw = fn()
+    for t in used:
+        t.record_stream(side)
+    dw.record_stream(cur)
+    if weight.grad is not None or dw.stride() != weight.stride():
+        cur.wait_stream(side)
+        return dw
+    ev = torch.cuda.Event()
+    ev.record(side)
+    _PENDING[dev] = ev  # events of one stream complete in order: the latest suffices
+    if not _CALLBACK_QUEUED[0]:
+        _CALLBACK_QUEUED[0] = True
+        torch.autograd.Variable._execution_engine.queue_callback(_end_of_backward)
+    return dw
+
 
 def _mode() -> str:
     return os.environ.get("PDT_CONV1X1", "auto")
@@ -104,7 +169,6 @@ class _Conv1x1Fn(torch.autograd.Function):
             return torch.ops.aten.convolution_backward(gy, x, weight, None, [1, 1], [0, 0], [1, 1], False, [0, 0],
                                                        1, mask)
 
-        # residual-branch gradient of x handed over by the block's fused BN (ResidualGradLink)
         # the other branch's gradient of x, if it already arrived (ResidualGradLink)
         acc = ctx.link.take() if ctx.link is not None else None
         first = ctx.link is not None and acc is None
@@ -133,9 +197,10 @@ class _Conv1x1Fn(torch.autograd.Function):
             })
             if algo == "gemm":
                 # a 1x1 kernel has the same element order in NCHW and NHWC: keep weight's strides
-                dw = torch.mm(g2.t(), x2).as_strided(weight.shape, weight.stride())
+                wfn = lambda: torch.mm(g2.t(), x2).as_strided(weight.shape, weight.stride())  # noqa: E731
             else:
-                dw = conv_bwd([False, True, False])[1]
+                wfn = lambda: conv_bwd([False, True, False])[1]  # noqa: E731
+            dw = _on_side_stream(wfn, weight, gy, x) if _wgrad_stream_enabled() else wfn()
         return dx, dw, None
 
 
@@ -155,9 +220,13 @@ class _LinkedConvFn(torch.autograd.Function):
     def backward(ctx, gy):
         x, weight = ctx.saved_tensors
         gy = gy.contiguous(memory_format=torch.channels_last)
-        dx, dw, _ = torch.ops.aten.convolution_backward(
-            gy, x, weight, None, list(ctx.stride), list(ctx.padding), [1, 1], False, [0, 0], 1,
-            [ctx.needs_input_grad[0], ctx.needs_input_grad[1], False])
+        args = (gy, x, weight, None, list(ctx.stride), list(ctx.padding), [1, 1], False, [0, 0], 1)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.ops.aten.convolution_backward(*args, [True, False, False])[0]
+        if ctx.needs_input_grad[1]:
+            wfn = lambda: torch.ops.aten.convolution_backward(*args, [False, True, False])[1]  # noqa: E731
+            dw = _on_side_stream(wfn, weight, gy, x) if _wgrad_stream_enabled() else wfn()
         if dx is not None:
             acc = ctx.link.take()
             if acc is None:
@@ -165,6 +234,42 @@ class _LinkedConvFn(torch.autograd.Function):
             else:
                 dx = acc.add_(dx)
         return dx, dw, None, None, None
+
+
+class _SplitConvFn(torch.autograd.Function):
+    """Bias-free convolution whose weight gradient runs on the side stream (see above)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, stride, padding, dilation, groups):
+        ctx.save_for_backward(x, weight)
+        ctx.cfg = (list(stride), list(padding), list(dilation), groups)
+        return F.conv2d(x, weight, None, stride, padding, dilation, groups)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, weight = ctx.saved_tensors
+        stride, padding, dilation, groups = ctx.cfg
+        gy = gy.contiguous(memory_format=torch.channels_last) if x.is_contiguous(
+            memory_format=torch.channels_last) else gy.contiguous()
+        args = (gy, x, weight, None, stride, padding, dilation, False, [0, 0], groups)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.ops.aten.convolution_backward(*args, [True, False, False])[0]
+        if ctx.needs_input_grad[1]:
+            wfn = lambda: torch.ops.aten.convolution_backward(*args, [False, True, False])[1]  # noqa: E731
+            dw = _on_side_stream(wfn, weight, gy, x)
+        return dx, dw, None, None, None, None
+
+
+class SplitConv2d(nn.Conv2d):
+    """``nn.Conv2d`` (same parameters / state_dict) whose GPU training backward can issue the
+    weight gradient on a side stream to overlap the rest of backward (``PDT_WGRAD_STREAM=1``)."""
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if (self.bias is None and x.is_cuda and self.padding_mode == "zeros" and torch.is_grad_enabled()
+                and self.weight.requires_grad and _wgrad_stream_enabled() and not disabled()):
+            return _SplitConvFn.apply(x, self.weight, self.stride, self.padding, self.dilation, self.groups)
+        return super().forward(x)
 
 
 def linked_conv(conv: nn.Conv2d, x: torch.Tensor, link) -> torch.Tensor:

@@ -36,6 +36,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from ..ops import multi_tensor
+from ..ops.conv import join_wgrad_streams
 from .buckets import (DEFAULT_BUCKET_CAP_MB, DEFAULT_FIRST_BUCKET_BYTES, BucketSpec,
                       compute_bucket_assignment)
 
@@ -312,6 +313,7 @@ class DistributedDataParallel(nn.Module):
 
     def _launch(self, bucket: _Bucket) -> None:
         bucket.launched = True
+        join_wgrad_streams()  # weight gradients issued on the side stream (ops/conv.py)
         self._pack(bucket)
         if bucket.comm_buffer is not bucket.buffer:
             multi_tensor.copy_([bucket.buffer], [bucket.comm_buffer])

@@ -69,13 +69,15 @@ def test_graph_step_lr0_matches_eager():
     base = _setup()
     xs, ys = _data()
     le, _, ge = _run(base, "eager", 0.0, xs, ys)
+    _, _, ge2 = _run(base, "eager", 0.0, xs, ys)
     lg, _, gg = _run(base, "graph", 0.0, xs, ys)
     torch.testing.assert_close(lg, le, rtol=1e-3, atol=1e-3)
-    # per-tensor relative error: MIOpen's non-deterministic (atomic split-K) solvers differ
-    # run to run at the bf16-rounding level even without capture; a broken replay is O(1) off
-    for i, (a, b) in enumerate(zip(gg, ge)):
-        err = ((a - b).norm() / (b.norm() + 1e-12)).item()
-        assert err < 5e-2, (i, err)
+    # per-tensor relative error against the eager-vs-eager noise: MIOpen's non-deterministic
+    # (atomic split-K) solvers differ run to run at the bf16-rounding level even without capture,
+    # and the side-stream weight gradients change their interleaving; a broken replay is O(1) off
+    rel = lambda a, b: ((a - b).norm() / (b.norm() + 1e-12)).item()  # noqa: E731
+    for i, (a, b, b2) in enumerate(zip(gg, ge, ge2)):
+        assert rel(a, b) < max(5e-2, 3 * rel(b2, b)), (i, rel(a, b), rel(b2, b))
 
 
 def test_graph_step_matches_eager_training():
