@@ -87,6 +87,8 @@ def main():
 # measured on MI355X (round 1): (2, 512, 8, 4) = 10.50 ms/step of BN vs v1 11.50 ms; more
 # workgroups are slower (2048: 14.45 ms, 4096: 18.1 ms). A v3 with 128/256-channel chunks per
 # workgroup (longer contiguous row segments) measured 10.12-10.23 ms vs 10.14: no gain, not kept.
+# Interleaving the row groups across workgroups (all blocks streaming one contiguous window, like
+# the grid-stride apply kernels) measured 10.68 vs 10.46 ms: not kept either.
 
 
 if __name__ == "__main__":
