@@ -34,7 +34,6 @@ int pdt_l2norm_sq(int n, void* const* x, const int64_t* numel, int dtype, float*
 int pdt_clip_coef(const float* sumsq, float max_norm, float* coef, float* norm, hipStream_t s);
 int64_t pdt_bn_workspace_floats(int64_t M, int C);
 void pdt_bn_tune(int variant, int target_blocks, int u_fwd, int u_bwd);
-void pdt_attn_set_variant(int fwd);
 int pdt_bn_fwd_train(const uint16_t* x, const uint16_t* res, const float* gamma, const float* beta,
                      float* running_mean, float* running_var, float momentum, float eps, int64_t M, int C, int relu,
                      uint16_t* y, uint8_t* mask, float* mean, float* invstd, float* ws, unsigned* counters,
@@ -799,7 +798,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_tune", [](int variant, int target_blocks, int u_fwd, int u_bwd) {
     pdt_bn_tune(variant, target_blocks, u_fwd, u_bwd);
   }, py::arg("variant") = 0, py::arg("target_blocks") = 0, py::arg("u_fwd") = 0, py::arg("u_bwd") = 0);
-  m.def("attn_set_variant", [](int fwd) { pdt_attn_set_variant(fwd); }, py::arg("fwd") = 0);
   m.def("bn_fwd_train", &bn_fwd_train);
   m.def("bn_fwd_eval", &bn_fwd_eval);
   m.def("bn_relu_maxpool_fwd", &bn_relu_maxpool_fwd);

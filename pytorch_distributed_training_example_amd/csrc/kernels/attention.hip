@@ -120,10 +120,10 @@ struct Stage {
 
 // ============================================================================ forward
 // grid (ceil(T/128), H, B), 256 threads; wave w owns queries [blk*128 + 32w, +32) as 2 x 16.
-// MINW: waves per SIMD the register allocation must allow (occupancy); DEEP: K/V tiles are
-// prefetched two tiles ahead (two register stage sets, loop unrolled by 2) instead of one.
-template <bool CAUSAL, int MINW, bool DEEP>
-__global__ __launch_bounds__(256, MINW) void attn_fwd_kernel(Tensor4 Q, Tensor4 K, Tensor4 V, uint16_t* __restrict__ O,
+// ~155 VGPRs: 3 waves per SIMD. Measured alternatives (tools/attn_bench.py, GPT-2 shape): forcing
+// 4 waves/SIMD spills (-14%); prefetching K/V two tiles ahead (+24 VGPR) is -7%.
+template <bool CAUSAL>
+__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(Tensor4 Q, Tensor4 K, Tensor4 V, uint16_t* __restrict__ O,
                                                        int64_t o_sb, int64_t o_sh, int64_t o_st,
                                                        float* __restrict__ LSE, int H, int T, float sl2) {
   __shared__ __attribute__((aligned(16))) char lds[2 * 64 * ROW_BYTES];
@@ -240,24 +240,10 @@ __global__ __launch_bounds__(256, MINW) void attn_fwd_kernel(Tensor4 Q, Tensor4 
         for (int qb = 0; qb < 2; ++qb) oacc[qb][n] = mfma(va, pb[qb][kst], oacc[qb][n]);
       }
     };
-  if (DEEP) {
-    Stage sk0, sv0, sk1, sv1;
-    sk0.load(krs, K.st, 0, tid);
-    sv0.load(vrs, V.st, 0, tid);
-    if (ntiles > 1) {
-      sk1.load(krs, K.st, 64, tid);
-      sv1.load(vrs, V.st, 64, tid);
-    }
-    for (int t = 0; t < ntiles; t += 2) {
-      tile(t, sk0, sv0, t + 2);
-      if (t + 1 < ntiles) tile(t + 1, sk1, sv1, t + 3);
-    }
-  } else {
-    Stage sk, sv;
-    sk.load(krs, K.st, 0, tid);
-    sv.load(vrs, V.st, 0, tid);
-    for (int t = 0; t < ntiles; ++t) tile(t, sk, sv, t + 1);
-  }
+  Stage sk, sv;
+  sk.load(krs, K.st, 0, tid);
+  sv.load(vrs, V.st, 0, tid);
+  for (int t = 0; t < ntiles; ++t) tile(t, sk, sv, t + 1);
   // ---- epilogue: normalise, store O (8 B per lane per d-tile) and LSE
 #pragma unroll
   for (int qb = 0; qb < 2; ++qb) {
@@ -560,11 +546,6 @@ __global__ __launch_bounds__(256, DKDV_MINW) void attn_bwd_dkdv_kernel(Tensor4 Q
 
 extern "C" {
 
-// Forward kernel variant (benchmarking): 0 = 2 waves/SIMD, 1-deep prefetch; 1 = 3 waves/SIMD;
-// 2 = 4 waves/SIMD; 3 = 2 waves/SIMD, 2-deep prefetch; 4 = 3 waves/SIMD, 2-deep.
-static int g_attn_fwd_variant = 0;
-void pdt_attn_set_variant(int fwd) { g_attn_fwd_variant = fwd; }
-
 // q/k/v/o/do/dq/dk/dv: bf16 [B, H, T, 64] views given by (b, h, t) strides (d stride 1, 16-B aligned rows).
 int pdt_attn_fwd(const uint16_t* q, const int64_t* qs, const uint16_t* k, const int64_t* ks, const uint16_t* v,
                  const int64_t* vs, uint16_t* o, const int64_t* os, float* lse, int B, int H, int T, int Dh,
@@ -573,17 +554,10 @@ int pdt_attn_fwd(const uint16_t* q, const int64_t* qs, const uint16_t* k, const 
   const Tensor4 Q{q, qs[0], qs[1], qs[2]}, K{k, ks[0], ks[1], ks[2]}, V{v, vs[0], vs[1], vs[2]};
   const dim3 grid((T + 127) / 128, H, B);
   const float sl2 = scale * LOG2E;
-#define PDT_FWD(C, MW, DP)                                                                                  \
-  hipLaunchKernelGGL((attn_fwd_kernel<C, MW, DP>), grid, dim3(256), 0, s, Q, K, V, o, os[0], os[1], os[2], lse, \
-                     H, T, sl2)
-  switch (g_attn_fwd_variant) {
-    case 1: if (causal) PDT_FWD(true, 3, false); else PDT_FWD(false, 3, false); break;
-    case 2: if (causal) PDT_FWD(true, 4, false); else PDT_FWD(false, 4, false); break;
-    case 3: if (causal) PDT_FWD(true, 2, true); else PDT_FWD(false, 2, true); break;
-    case 4: if (causal) PDT_FWD(true, 3, true); else PDT_FWD(false, 3, true); break;
-    default: if (causal) PDT_FWD(true, 2, false); else PDT_FWD(false, 2, false); break;
-  }
-#undef PDT_FWD
+  if (causal)
+    hipLaunchKernelGGL(attn_fwd_kernel<true>, grid, dim3(256), 0, s, Q, K, V, o, os[0], os[1], os[2], lse, H, T, sl2);
+  else
+    hipLaunchKernelGGL(attn_fwd_kernel<false>, grid, dim3(256), 0, s, Q, K, V, o, os[0], os[1], os[2], lse, H, T, sl2);
   return 0;
 }
 

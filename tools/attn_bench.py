@@ -34,30 +34,8 @@ def timed(fn, it=10):
     return e0.elapsed_time(e1) / it * 1e3
 
 
-def variants(C, D=64):
-    """Forward kernel variants (pdt_attn_set_variant) on every shape, checked against variant 0."""
-    for name, B, H, T, causal in SHAPES:
-        q, k, v = (torch.randn(B, H, T, D, device="cuda", dtype=torch.bfloat16) for _ in range(3))
-        out = torch.empty(B, H, T, D, device="cuda", dtype=torch.bfloat16)
-        lse = torch.empty(B, H, T, device="cuda", dtype=torch.float32)
-        fl = 4 * B * H * T * T * D * (0.5 if causal else 1.0)
-        ref, cols = None, []
-        for var in (0, 2, 3, 4):
-            C.attn_set_variant(var)
-            t = timed(lambda: C.attn_fwd_out(q, k, v, out, lse, causal, 0.125))
-            if ref is None:
-                ref = out.clone()
-            else:
-                torch.testing.assert_close(out, ref, rtol=0, atol=0)
-            cols.append(f"v{var} {t:6.1f}us {fl / t / 1e6:4.0f}TF")
-        print(f"{name:12s} fwd variants: " + " | ".join(cols), flush=True)
-    C.attn_set_variant(0)
-
-
 def main():
     C = native()
-    if hasattr(C, "attn_set_variant"):
-        variants(C)
     D = 64
     print(f"{'shape':12s} | {'ours fwd us':>11} {'TF/s':>5} | {'ours bwd us':>11} {'TF/s':>5} | "
           f"{'sdpa fwd us':>11} {'TF/s':>5} | {'sdpa bwd us':>11} {'TF/s':>5}")
