@@ -267,7 +267,9 @@ def main(argv: Optional[list] = None) -> int:
         make_miopen_capture_safe()
     from .engine.miopen_cache import use_repo_miopen_cache
     use_repo_miopen_cache()  # persisted conv-algorithm find-db (engine/miopen_cache.py)
-    if args.model not in ("lenet", "mlp"):  # tiny launch-bound GEMMs: TunableOp's host lookup costs more
+    # measured GEMM solutions pay off for big GEMMs only: TunableOp's per-call host lookup costs
+    # more than it saves on launch-bound models (LeNet, MLP) and micro-batched steps
+    if args.model not in ("lenet", "mlp") and args.grad_accum == 1:
         from .engine.gemm_tuning import use_repo_gemm_tuning
         use_repo_gemm_tuning()  # measured GEMM solutions (engine/gemm_tuning.py), read-only
     if args.profile:
