@@ -172,6 +172,9 @@ class _Conv1x1Fn(torch.autograd.Function):
         # the other branch's gradient of x, if it already arrived (ResidualGradLink)
         acc = ctx.link.take() if ctx.link is not None else None
         first = ctx.link is not None and acc is None
+        strided = None
+        if isinstance(acc, StridedGrad):  # a stride-2 shortcut's compact gradient: added below
+            strided, acc = acc, None
         if ctx.needs_input_grad[0]:
             algo = _pick(("bwd_data", M, Ci, Co), {
                 "miopen": lambda: conv_bwd([True, False, False]),
@@ -188,6 +191,8 @@ class _Conv1x1Fn(torch.autograd.Function):
                 dx = dx.add_(acc)
         elif acc is not None:
             dx = acc
+        if strided is not None and dx is not None:
+            strided.add_into(dx)
         if first and dx is not None:  # first of the two branches: leave dx for the partner to add to
             ctx.link.grad, dx = dx, None
         if ctx.needs_input_grad[1]:
@@ -202,6 +207,65 @@ class _Conv1x1Fn(torch.autograd.Function):
                 wfn = lambda: conv_bwd([False, True, False])[1]  # noqa: E731
             dw = _on_side_stream(wfn, weight, gy, x) if _wgrad_stream_enabled() else wfn()
         return dx, dw, None
+
+
+class StridedGrad:
+    """Gradient of a strided subsampling ``x[:, :, ::s, ::s]`` kept compact (only the sampled
+    positions are non-zero) until it is added into a full-size gradient of ``x``."""
+
+    __slots__ = ("t", "s")
+
+    def __init__(self, t: torch.Tensor, s: int):
+        self.t, self.s = t, s
+
+    def add_into(self, full: torch.Tensor) -> torch.Tensor:
+        full[:, :, ::self.s, ::self.s].add_(self.t)
+        return full
+
+    def dense(self, shape) -> torch.Tensor:
+        full = torch.zeros(shape, dtype=self.t.dtype, device=self.t.device).contiguous(
+            memory_format=torch.channels_last)
+        return self.add_into(full)
+
+
+class _Conv1x1StridedFn(torch.autograd.Function):
+    """Stride-s 1x1 convolution (the ResNet downsample shortcut) as a gather of the sampled pixels
+    + GEMMs, instead of MIOpen's strided implicit-GEMM kernels (which need zero-fill passes). The
+    data gradient is non-zero only at the sampled positions: with a ``ResidualGradLink`` it is
+    handed over compact (``StridedGrad``) and added into conv1's full-size gradient at those
+    positions, so no full-size zero tensor is ever written."""
+
+    @staticmethod
+    def forward(ctx, x, weight, s, link):
+        N, Ci, H, W = x.shape
+        Co = weight.shape[0]
+        xs = x[:, :, ::s, ::s].contiguous(memory_format=torch.channels_last)
+        Hs, Ws = xs.shape[2], xs.shape[3]
+        y = torch.mm(_nhwc2d(xs), weight.reshape(Co, Ci).t()).view(N, Hs, Ws, Co).permute(0, 3, 1, 2)
+        ctx.save_for_backward(xs, weight)
+        ctx.s, ctx.link, ctx.xshape = s, link, x.shape
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        xs, weight = ctx.saved_tensors
+        N, Ci, Hs, Ws = xs.shape
+        Co = weight.shape[0]
+        gy = gy.contiguous(memory_format=torch.channels_last)
+        g2, w2 = _nhwc2d(gy), weight.reshape(Co, Ci)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            compact = StridedGrad(torch.mm(g2, w2).view(N, Hs, Ws, Ci).permute(0, 3, 1, 2), ctx.s)
+            acc = ctx.link.take() if ctx.link is not None else None
+            if ctx.link is not None and acc is None:
+                ctx.link.grad = compact  # first: conv1's backward adds it into its full gradient
+            elif acc is not None:
+                dx = compact.add_into(acc)
+            else:
+                dx = compact.dense(ctx.xshape)
+        if ctx.needs_input_grad[1]:
+            dw = torch.mm(g2.t(), _nhwc2d(xs)).as_strided(weight.shape, weight.stride())
+        return dx, dw, None, None
 
 
 class _LinkedConvFn(torch.autograd.Function):
@@ -274,7 +338,7 @@ class SplitConv2d(nn.Conv2d):
 
 def linked_conv(conv: nn.Conv2d, x: torch.Tensor, link) -> torch.Tensor:
     """``conv(x)`` whose input gradient is summed with the partner branch's through ``link``."""
-    if isinstance(conv, Conv1x1) and conv.gemm_eligible(x):
+    if isinstance(conv, Conv1x1) and (conv.gemm_eligible(x) or conv.strided_gemm_eligible(x)):
         return conv(x, res_link=link)
     return _LinkedConvFn.apply(x, conv.weight, conv.stride, conv.padding, link)
 
@@ -286,14 +350,25 @@ class Conv1x1(nn.Conv2d):
     def __init__(self, inp: int, out: int, stride: int = 1):
         super().__init__(inp, out, 1, stride=stride, bias=False)
 
-    def gemm_eligible(self, x: torch.Tensor) -> bool:
-        return (self.stride == (1, 1) and x.is_cuda and x.dim() == 4 and x.dtype == self.weight.dtype
+    def _gemm_ok(self, x: torch.Tensor) -> bool:
+        return (x.is_cuda and x.dim() == 4 and x.dtype == self.weight.dtype and self.padding == (0, 0)
                 and x.is_contiguous(memory_format=torch.channels_last) and _mode() != "off" and not disabled())
 
+    def gemm_eligible(self, x: torch.Tensor) -> bool:
+        return self.stride == (1, 1) and self._gemm_ok(x)
+
+    def strided_gemm_eligible(self, x: torch.Tensor) -> bool:
+        s = self.stride[0]
+        # opt-in: measured 1.2% slower end to end on ResNet-50 than MIOpen's strided kernels
+        # (10,352-10,394 vs 10,496-10,509 img/s; tools/gpu_s2.sh)
+        return s > 1 and self.stride == (s, s) and self._gemm_ok(x) and os.environ.get("PDT_CONV1X1_S2", "0") == "1"
+
     def forward(self, x: torch.Tensor, res_link=None) -> torch.Tensor:
-        """``res_link``: a ``ResidualGradLink`` whose gradient (the residual branch's gradient
-        of ``x``) is added into this conv's input gradient; requires ``gemm_eligible(x)``."""
+        """``res_link``: a ``ResidualGradLink`` whose gradient (the other branch's gradient of
+        ``x``) meets this conv's input gradient; requires one of the GEMM paths."""
         if self.gemm_eligible(x):
             return _Conv1x1Fn.apply(x, self.weight, res_link)
-        assert res_link is None, "res_link needs the GEMM-eligible path"
+        if self.strided_gemm_eligible(x):
+            return _Conv1x1StridedFn.apply(x, self.weight, self.stride[0], res_link)
+        assert res_link is None, "res_link needs a GEMM path"
         return super().forward(x)
