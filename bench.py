@@ -158,6 +158,8 @@ def run(args, ctx):
     """Build the workload, warm up, time ``args.steps`` steps; returns the result dict (all ranks)."""
     dev = ctx.device
     world = ctx.world_size
+    # device sync (a no-op for CPU/gloo rehearsals of the multi-rank path)
+    dsync = torch.cuda.synchronize if dev.type == "cuda" else (lambda: None)
     metric, unit, default_b, _ = WORKLOADS[args.model]
     B = args.batch_size or default_b
     torch.backends.cudnn.benchmark = bool(args.cudnn_benchmark)
@@ -232,21 +234,23 @@ def run(args, ctx):
     for i in range(args.warmup):
         loss = run(i)
         if ctx.rank == 0:  # progress (first steps include MIOpen's conv-algorithm search)
-            torch.cuda.synchronize()
+            dsync()
             print(f"[bench] warmup step {i + 1}/{args.warmup} done at {time.perf_counter() - tw:.1f}s",
                   file=sys.stderr, flush=True)
-    torch.cuda.synchronize()
+    dsync()
     launcher.barrier()
-    torch.cuda.synchronize()
-    torch.cuda.nvtx.range_push("timed")
+    dsync()
+    if dev.type == "cuda":
+        torch.cuda.nvtx.range_push("timed")
     t0 = time.perf_counter()
     for i in range(args.steps):
         loss = run(i)
-    torch.cuda.synchronize()
+    dsync()
     launcher.barrier()
-    torch.cuda.synchronize()
+    dsync()
     elapsed = time.perf_counter() - t0
-    torch.cuda.nvtx.range_pop()
+    if dev.type == "cuda":
+        torch.cuda.nvtx.range_pop()
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

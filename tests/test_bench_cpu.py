@@ -1,0 +1,42 @@
+"""bench.py driver contract, rehearsed on CPU/gloo: the launch line the driver uses
+(torch.distributed.run, 127.0.0.1, one rank per device), one JSON line from rank 0 with the
+whole-job aggregate, the BASELINE.json metric and the dp<N> parallelism tag."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+        "scaling", "vs_baseline", "dtype", "data", "config"}
+
+
+def _run(nproc, port, extra=()):
+    env = dict(os.environ, OMP_NUM_THREADS="2", MASTER_ADDR="127.0.0.1")
+    args = ["--steps", "2", "--warmup", "1", "--batch-size", "2", "--image-size", "32", *extra]
+    if nproc == 1:
+        cmd = [sys.executable, "bench.py", *args]
+    else:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+               "--master-addr", "127.0.0.1", f"--master-port={port}", "bench.py", "--gpus", str(nproc), *args]
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=400)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout  # rank 0 only
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("nproc,port", [(1, 0), (4, 29671)])
+def test_bench_json_contract(nproc, port):
+    r = _run(nproc, port)
+    assert KEYS <= set(r)
+    baseline = json.load(open(os.path.join(ROOT, "BASELINE.json")))
+    assert baseline["metric"].startswith(r["metric"])
+    assert r["n_gpus"] == nproc and r["steps"] == 2 and r["warmup"] == 1
+    assert r["config"]["model"] == "resnet50" and r["config"]["parallelism"] == f"dp{nproc}"
+    assert r["config"]["global_batch"] == 2 * nproc
+    assert r["scaling"] == "weak" and r["higher_is_better"] is True and r["dtype"] == "bf16"
+    # value is the whole-job aggregate derived from the (max over ranks) step time
+    assert r["value"] == pytest.approx(2 * nproc / (r["ms_per_step"] / 1e3), rel=1e-2)
