@@ -275,6 +275,9 @@ def run(args, ctx):
 
 def main(argv=None):
     args = parse(argv)
+    if os.environ.get("PDT_STACK_DUMP"):  # periodic Python stacks: where a slow warm-up spends time
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ["PDT_STACK_DUMP"]), repeat=True)
     ctx = setup(args)
     result = run(args, ctx)
     if ctx.rank == 0:

@@ -15,9 +15,17 @@ direction (forward, data-grad, weight-grad) of each shape is timed once with bot
 its first eager call — like ``cudnn.benchmark`` — and the faster one is used from then on
 (``PDT_CONV1X1=miopen|gemm|auto``). Never timed under hipGraph capture (capture falls back to
 MIOpen for an unseen shape), so the warm-up steps before ``StaticStep.capture`` settle it.
+
+Decisions measured on an MI355X are committed in ``tuning/conv1x1_gfx950.json`` and used without
+timing: a shape decided for GEMM then never calls MIOpen at all, which matters on a fresh box,
+where timing the MIOpen candidate costs its full algorithm search (ResNet-50 at 1024/GPU: most
+of a 237 s first step). ``PDT_CONV1X1_TABLE=0`` ignores the table; ``PDT_CONV1X1_DUMP=<path>``
+writes table + new decisions at exit (to extend the table).
 """
 from __future__ import annotations
 
+import atexit
+import json
 import os
 from typing import Dict, Tuple
 
@@ -28,6 +36,44 @@ from torch import nn
 from ._native import disabled
 
 _CHOICE: Dict[Tuple, str] = {}
+_TABLE_LOADED = [False]
+TABLE = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
+                     "tuning", "conv1x1_gfx950.json")
+
+
+def _key_str(key: Tuple) -> str:
+    return ",".join(str(k) for k in key)
+
+
+def load_table(path: str | None = None) -> int:
+    """Seed the decisions from a measured table; returns the number of entries loaded."""
+    path = path or TABLE
+    if not os.path.exists(path):
+        return 0
+    with open(path) as f:
+        tab = json.load(f)
+    for k, v in tab.items():
+        d, *dims = k.split(",")
+        if v in ("miopen", "gemm"):
+            _CHOICE.setdefault((d, *map(int, dims)), v)
+    return len(tab)
+
+
+def dump_table(path: str) -> None:
+    """Write every decision (table + measured this run) as a table file."""
+    with open(path, "w") as f:
+        json.dump({_key_str(k): v for k, v in sorted(_CHOICE.items())}, f, indent=0, sort_keys=True)
+
+
+def _ensure_table() -> None:
+    if _TABLE_LOADED[0]:
+        return
+    _TABLE_LOADED[0] = True
+    if os.environ.get("PDT_CONV1X1_TABLE", "1") != "0":
+        load_table()
+    out = os.environ.get("PDT_CONV1X1_DUMP")
+    if out:
+        atexit.register(dump_table, out)
 
 # ---------------------------------------------------------------- weight gradients off the critical path
 # A convolution's weight gradient is needed only by the optimizer / all-reduce, while its data
@@ -114,6 +160,7 @@ def _pick(key: Tuple, cands: Dict[str, callable]) -> str:
     mode = _mode()
     if mode in cands:
         return mode
+    _ensure_table()
     c = _CHOICE.get(key)
     if c is not None:
         return c

@@ -51,3 +51,22 @@ def test_committed_table_has_validators_and_entries():
     lines = open(gemm_tuning.TABLE).read().splitlines()
     assert any(l.startswith("Validator,GCN_ARCH_NAME,gfx950") for l in lines)
     assert sum(not l.startswith("Validator") for l in lines if l) >= 10
+
+
+def test_conv1x1_decision_table_roundtrip(tmp_path, monkeypatch):
+    """Measured 1x1-conv decisions (ops/conv.py) load from / dump to a JSON table; a key in the
+    table is used without timing (no GPU needed to pick)."""
+    from pytorch_distributed_training_example_amd.ops import conv as C
+    monkeypatch.setattr(C, "_CHOICE", {})
+    monkeypatch.setattr(C, "_TABLE_LOADED", [True])
+    C._CHOICE[("fwd", 802816, 64, 256)] = "gemm"
+    C._CHOICE[("bwd_weight", 802816, 64, 256)] = "miopen"
+    p = tmp_path / "t.json"
+    C.dump_table(str(p))
+    C._CHOICE.clear()
+    assert C.load_table(str(p)) == 2
+    assert C._pick(("fwd", 802816, 64, 256), {"miopen": None, "gemm": None}) == "gemm"
+    assert C._pick(("bwd_weight", 802816, 64, 256), {"miopen": None, "gemm": None}) == "miopen"
+    import json
+    tab = json.load(open(C.TABLE))  # the committed table parses and holds only valid choices
+    assert set(tab.values()) <= {"miopen", "gemm"}
