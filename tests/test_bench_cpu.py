@@ -33,7 +33,7 @@ def test_bench_json_contract(nproc, port):
     r = _run(nproc, port)
     assert KEYS <= set(r)
     baseline = json.load(open(os.path.join(ROOT, "BASELINE.json")))
-    assert baseline["metric"].startswith(r["metric"])
+    assert r["metric"] == baseline["metric"]
     assert r["n_gpus"] == nproc and r["steps"] == 2 and r["warmup"] == 1
     assert r["config"]["model"] == "resnet50" and r["config"]["parallelism"] == f"dp{nproc}"
     assert r["config"]["global_batch"] == 2 * nproc
