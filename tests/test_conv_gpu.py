@@ -71,13 +71,19 @@ def test_side_stream_weight_grads_match(monkeypatch, accumulate):
     from pytorch_distributed_training_example_amd.models import get_model
     from pytorch_distributed_training_example_amd.models.precision import to_bf16_mixed
     from pytorch_distributed_training_example_amd.ops.cross_entropy import cross_entropy
+    # deterministic MIOpen solvers: atomic split-K weight-gradient solvers are not bit-reproducible
+    # and a deep random-init net (BN over 2x2 maps at this size) amplifies that into run-to-run
+    # gradient differences of 2-11% (measured), which would hide a real race; without them the
+    # in-stream runs agree (near) exactly and the side-stream run must too
+    monkeypatch.setattr(torch.backends.cudnn, "deterministic", True)
+    monkeypatch.setattr(torch.backends.cudnn, "benchmark", False)
     torch.manual_seed(0)
     base = to_bf16_mixed(get_model("resnet50", num_classes=32).cuda().to(memory_format=torch.channels_last))
     xs = [torch.randn(8, 3, 64, 64, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
           for _ in range(2)]
     ys = [torch.randint(0, 32, (8,), device="cuda") for _ in range(2)]
     out = []
-    for on in ("0", "0", "1"):  # two in-stream runs measure MIOpen's own run-to-run noise
+    for on in ("0", "0", "0", "1"):  # three in-stream runs measure the run-to-run noise
         monkeypatch.setenv("PDT_WGRAD_STREAM", on)
         base.zero_grad(set_to_none=True)
         for x, y in zip(xs, ys) if accumulate else zip(xs[:1], ys[:1]):
@@ -89,8 +95,12 @@ def test_side_stream_weight_grads_match(monkeypatch, accumulate):
     # that in early layers; a race (reading an unfinished gradient) is O(1) off everywhere
     # (a single small-norm BN gradient measured 0.104 against a 0.012 noise draw, so the
     # per-parameter bound only catches O(1) errors; the whole-model bound is the tight one)
-    for i, (off1, off2, on) in enumerate(zip(*out)):
-        noise = rel(off2, off1)
+    for i, (off1, off2, off3, on) in enumerate(zip(*out)):
+        noise = max(rel(off2, off1), rel(off3, off1))
         assert rel(on, off1) <= 4 * noise + 0.25, (i, rel(on, off1), noise)
     flat = [torch.cat([g.flatten() for g in run]) for run in out]
-    assert rel(flat[2], flat[0]) <= 4 * rel(flat[1], flat[0]) + 2e-2
+    # measured with deterministic solvers: on 0.025 / noise 0.026 (some GEMM and reduction
+    # order noise remains); the unbounded-draw failure seen before this used a single noise draw
+    noise = max(rel(flat[1], flat[0]), rel(flat[2], flat[0]))
+    print("side-stream rel", rel(flat[3], flat[0]), "noise", noise)
+    assert rel(flat[3], flat[0]) <= 4 * noise + 2e-3

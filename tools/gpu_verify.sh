@@ -1,15 +1,14 @@
 #!/bin/bash
-# Fresh-box verification: full GPU test tier, smoke, headline bench; MIOpen db harvested into gpurun_out.
+# Fresh-box verification exactly as the round-end driver runs it: headline bench (committed
+# in-tree MIOpen find-db / GEMM tables, no PDT_MIOPEN_CACHE override), full GPU test tier, smoke.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-export PDT_MIOPEN_CACHE=$PWD/gpurun_out/miopen_cache
 mkdir -p gpurun_out
-timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > gpurun_out/bench_default.log 2>&1
+PDT_STACK_DUMP=60 timeout -k 10 ${TB:-300} python -u bench.py --steps 20 --warmup 5 > gpurun_out/bench_default.log 2>&1
 rc=$?; echo "bench rc=$rc"; grep -E "warmup|metric" gpurun_out/bench_default.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
+timeout -k 10 ${TP:-600} python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -15 gpurun_out/pytest_gpu.log
 [ $rc -le 1 ] || exit $rc
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
 rc=$?; echo "smoke rc=$rc"; tail -1 gpurun_out/smoke.log
-du -sh gpurun_out/miopen_cache
 exit $rc
