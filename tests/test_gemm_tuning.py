@@ -70,3 +70,35 @@ def test_conv1x1_decision_table_roundtrip(tmp_path, monkeypatch):
     import json
     tab = json.load(open(C.TABLE))  # the committed table parses and holds only valid choices
     assert set(tab.values()) <= {"miopen", "gemm"}
+
+
+def test_conv1x1_table_covers_bench_default_resnet50():
+    """Every stride-1 1x1 convolution of the headline bench (ResNet-50, 224x224, bench.py's default
+    per-GPU batch) has all three directions in the committed table, so a fresh box never times
+    MIOpen against GEMM (or runs MIOpen's search for a GEMM-decided shape) inside warm-up."""
+    import json
+
+    import torch
+
+    import bench
+    from pytorch_distributed_training_example_amd.models import get_model
+    from pytorch_distributed_training_example_amd.ops import conv as C
+    batch = bench.WORKLOADS["resnet50"][2]
+    model = get_model("resnet50").eval()
+    shapes = set()
+
+    def hook(mod, inp, out):
+        if isinstance(mod, C.Conv1x1) and mod.stride == (1, 1):
+            n, ci, h, w = inp[0].shape
+            shapes.add((batch * h * w, ci, mod.out_channels))
+
+    hs = [m.register_forward_hook(hook) for m in model.modules()]
+    with torch.no_grad():
+        model(torch.zeros(1, 3, 224, 224))
+    for h in hs:
+        h.remove()
+    assert len(shapes) >= 10
+    tab = json.load(open(C.TABLE))
+    missing = [f"{d},{m},{ci},{co}" for (m, ci, co) in sorted(shapes)
+               for d in ("fwd", "bwd_data", "bwd_weight") if f"{d},{m},{ci},{co}" not in tab]
+    assert not missing, missing
