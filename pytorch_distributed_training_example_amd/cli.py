@@ -81,7 +81,9 @@ def build_parser() -> argparse.ArgumentParser:
 
 
 MODEL_DEFAULTS = {
-    "lenet": dict(optimizer="adadelta", loss="cross_entropy"),
+    # the reference's loss: nll_loss on softmax probabilities (train.py:48), values in [-1, 0];
+    # computed from the logits by one fused kernel (--loss cross_entropy for the usual loss)
+    "lenet": dict(optimizer="adadelta", loss="nll_on_probs"),
     "mlp": dict(optimizer="sgd", loss="mse"),
 }
 
@@ -253,7 +255,22 @@ def run(rank: int, world: int, args) -> dict:
     return result
 
 
+def configure_process(args) -> None:
+    """Per-rank library settings, applied once LOCAL_RANK is known and before the first conv or
+    GEMM: MIOpen's in-tree find-db (local rank 0 only; other ranks get private copies) and the
+    measured GEMM table copied for THIS rank's device. Called in each rank, never in a
+    spawning parent, whose environment every child would inherit."""
+    from .engine.miopen_cache import use_repo_miopen_cache
+    use_repo_miopen_cache()  # persisted conv-algorithm find-db (engine/miopen_cache.py)
+    # measured GEMM solutions pay off for big GEMMs only: TunableOp's per-call host lookup costs
+    # more than it saves on launch-bound models (LeNet, MLP) and micro-batched steps
+    if args.model not in ("lenet", "mlp") and args.grad_accum == 1:
+        from .engine.gemm_tuning import use_repo_gemm_tuning
+        use_repo_gemm_tuning()  # measured GEMM solutions (engine/gemm_tuning.py), read-only
+
+
 def _entry(rank: int, world: int, args) -> None:
+    configure_process(args)
     run(rank, world, args)
 
 
@@ -265,18 +282,12 @@ def main(argv: Optional[list] = None) -> int:
         # MIOpen reads its solver switches once per process: set before any convolution
         from .engine.graph import make_miopen_capture_safe
         make_miopen_capture_safe()
-    from .engine.miopen_cache import use_repo_miopen_cache
-    use_repo_miopen_cache()  # persisted conv-algorithm find-db (engine/miopen_cache.py)
-    # measured GEMM solutions pay off for big GEMMs only: TunableOp's per-call host lookup costs
-    # more than it saves on launch-bound models (LeNet, MLP) and micro-batched steps
-    if args.model not in ("lenet", "mlp") and args.grad_accum == 1:
-        from .engine.gemm_tuning import use_repo_gemm_tuning
-        use_repo_gemm_tuning()  # measured GEMM solutions (engine/gemm_tuning.py), read-only
     if args.profile:
         from .utils import profiling
         profiling.enable_ranges(True)
     use_gpu = not args.no_cuda and torch.cuda.is_available()
     if "RANK" in os.environ and "WORLD_SIZE" in os.environ:  # torchrun
+        configure_process(args)
         ctx = launcher.init_distributed(backend=args.backend, use_gpu=use_gpu, timeout_s=args.timeout)
         try:
             run(ctx.rank, ctx.world_size, args)

@@ -16,7 +16,8 @@ its first eager call — like ``cudnn.benchmark`` — and the faster one is used
 (``PDT_CONV1X1=miopen|gemm|auto``). Never timed under hipGraph capture (capture falls back to
 MIOpen for an unseen shape), so the warm-up steps before ``StaticStep.capture`` settle it.
 
-Decisions measured on an MI355X are committed in ``tuning/conv1x1_gfx950.json`` and used without
+Decisions measured on an MI355X are committed in ``tuning/conv1x1_gfx950.json`` (keyed by direction,
+dtype and GEMM shape; loaded only on a gfx950 device, measured for bf16) and used without
 timing: a shape decided for GEMM then never calls MIOpen at all, which matters on a fresh box,
 where timing the MIOpen candidate costs its full algorithm search (ResNet-50 at 1024/GPU: most
 of a 237 s first step). ``PDT_CONV1X1_TABLE=0`` ignores the table; ``PDT_CONV1X1_DUMP=<path>``
@@ -53,10 +54,21 @@ def load_table(path: str | None = None) -> int:
     with open(path) as f:
         tab = json.load(f)
     for k, v in tab.items():
-        d, *dims = k.split(",")
-        if v in ("miopen", "gemm"):
-            _CHOICE.setdefault((d, *map(int, dims)), v)
+        d, dt, *dims = k.split(",")
+        if v in ("miopen", "gemm") and len(dims) == 3:
+            _CHOICE.setdefault((d, dt, *map(int, dims)), v)
     return len(tab)
+
+
+def _dtype_name(t: torch.Tensor) -> str:
+    return {torch.bfloat16: "bf16", torch.float16: "fp16", torch.float32: "fp32"}.get(t.dtype, str(t.dtype))
+
+
+def _table_arch_ok() -> bool:
+    """The committed decisions were measured on gfx950: any other device times its own."""
+    if not torch.cuda.is_available():
+        return False
+    return torch.cuda.get_device_properties(torch.cuda.current_device()).gcnArchName.startswith("gfx950")
 
 
 def dump_table(path: str) -> None:
@@ -69,7 +81,7 @@ def _ensure_table() -> None:
     if _TABLE_LOADED[0]:
         return
     _TABLE_LOADED[0] = True
-    if os.environ.get("PDT_CONV1X1_TABLE", "1") != "0":
+    if os.environ.get("PDT_CONV1X1_TABLE", "1") != "0" and _table_arch_ok():
         load_table()
     out = os.environ.get("PDT_CONV1X1_DUMP")
     if out:
@@ -173,7 +185,7 @@ def _pick(key: Tuple, cands: Dict[str, callable]) -> str:
 
 
 def choices() -> Dict[Tuple, str]:
-    """Decisions taken so far: {(direction, M, Ci, Co): 'miopen' | 'gemm'}."""
+    """Decisions taken so far: {(direction, dtype, M, Ci, Co): 'miopen' | 'gemm'}."""
     return dict(_CHOICE)
 
 
@@ -190,7 +202,7 @@ class _Conv1x1Fn(torch.autograd.Function):
         x2 = _nhwc2d(x)
         w2 = weight.reshape(Co, Ci)
         M = x2.shape[0]
-        algo = _pick(("fwd", M, Ci, Co), {
+        algo = _pick(("fwd", _dtype_name(x), M, Ci, Co), {
             "miopen": lambda: F.conv2d(x, weight),
             "gemm": lambda: torch.mm(x2, w2.t()),
         })
@@ -223,7 +235,7 @@ class _Conv1x1Fn(torch.autograd.Function):
         if isinstance(acc, StridedGrad):  # a stride-2 shortcut's compact gradient: added below
             strided, acc = acc, None
         if ctx.needs_input_grad[0]:
-            algo = _pick(("bwd_data", M, Ci, Co), {
+            algo = _pick(("bwd_data", _dtype_name(x), M, Ci, Co), {
                 "miopen": lambda: conv_bwd([True, False, False]),
                 "gemm": lambda: torch.mm(g2, w2),
             })
@@ -243,7 +255,7 @@ class _Conv1x1Fn(torch.autograd.Function):
         if first and dx is not None:  # first of the two branches: leave dx for the partner to add to
             ctx.link.grad, dx = dx, None
         if ctx.needs_input_grad[1]:
-            algo = _pick(("bwd_weight", M, Ci, Co), {
+            algo = _pick(("bwd_weight", _dtype_name(x), M, Ci, Co), {
                 "miopen": lambda: conv_bwd([False, True, False]),
                 "gemm": lambda: torch.mm(g2.t(), x2),
             })

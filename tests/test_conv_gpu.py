@@ -64,6 +64,40 @@ def test_bottleneck_residual_grad_link_matches_autograd_add(monkeypatch, kind):
         assert err < 2e-2, err
 
 
+@pytest.mark.parametrize("layer", ["conv1x1_gemm", "conv3x3"])
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_side_stream_weight_grad_bitwise(monkeypatch, layer, accumulate):
+    """One convolution's weight gradient issued on the side stream (ops/conv.py:_on_side_stream)
+    is BITWISE the in-stream one, read on the current stream right after backward (no host
+    sync in between, so a missing join would read a partly written gradient). Deterministic
+    kernels only: the 1x1 conv as a hipBLASLt GEMM (no atomic split-K), the 3x3 conv on
+    MIOpen's deterministic solvers; the in-stream run is repeated to prove that."""
+    from pytorch_distributed_training_example_amd.ops.conv import Conv1x1, SplitConv2d
+    monkeypatch.setenv("PDT_CONV1X1", "gemm")
+    monkeypatch.setattr(torch.backends.cudnn, "deterministic", True)
+    monkeypatch.setattr(torch.backends.cudnn, "benchmark", False)
+    torch.manual_seed(0)
+    if layer == "conv1x1_gemm":
+        m, ci = Conv1x1(256, 512), 256
+    else:
+        m, ci = SplitConv2d(128, 128, 3, padding=1, bias=False), 128
+    m = m.cuda().bfloat16().to(memory_format=torch.channels_last)
+    xs = [torch.randn(32, ci, 28, 28, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+          for _ in range(2)]
+    res = []
+    for on in ("0", "0", "1"):
+        monkeypatch.setenv("PDT_WGRAD_STREAM", on)
+        m.zero_grad(set_to_none=True)
+        for x in xs if accumulate else xs[:1]:
+            y = m(x.requires_grad_(False))
+            y.backward(y.detach() * 0.5)
+        read = m.weight.grad.float().clone()  # current-stream read, before any host sync
+        torch.cuda.synchronize()
+        res.append(read)
+    assert torch.equal(res[0], res[1]), "in-stream weight gradient not reproducible"
+    assert torch.equal(res[2], res[0]), (res[2] - res[0]).abs().max().item()
+
+
 @pytest.mark.parametrize("accumulate", [False, True])
 def test_side_stream_weight_grads_match(monkeypatch, accumulate):
     """Weight gradients issued on the side stream (ops/conv.py) equal the in-stream ones, also

@@ -59,14 +59,14 @@ def test_conv1x1_decision_table_roundtrip(tmp_path, monkeypatch):
     from pytorch_distributed_training_example_amd.ops import conv as C
     monkeypatch.setattr(C, "_CHOICE", {})
     monkeypatch.setattr(C, "_TABLE_LOADED", [True])
-    C._CHOICE[("fwd", 802816, 64, 256)] = "gemm"
-    C._CHOICE[("bwd_weight", 802816, 64, 256)] = "miopen"
+    C._CHOICE[("fwd", "bf16", 802816, 64, 256)] = "gemm"
+    C._CHOICE[("bwd_weight", "bf16", 802816, 64, 256)] = "miopen"
     p = tmp_path / "t.json"
     C.dump_table(str(p))
     C._CHOICE.clear()
     assert C.load_table(str(p)) == 2
-    assert C._pick(("fwd", 802816, 64, 256), {"miopen": None, "gemm": None}) == "gemm"
-    assert C._pick(("bwd_weight", 802816, 64, 256), {"miopen": None, "gemm": None}) == "miopen"
+    assert C._pick(("fwd", "bf16", 802816, 64, 256), {"miopen": None, "gemm": None}) == "gemm"
+    assert C._pick(("bwd_weight", "bf16", 802816, 64, 256), {"miopen": None, "gemm": None}) == "miopen"
     import json
     tab = json.load(open(C.TABLE))  # the committed table parses and holds only valid choices
     assert set(tab.values()) <= {"miopen", "gemm"}
@@ -99,6 +99,20 @@ def test_conv1x1_table_covers_bench_default_resnet50():
         h.remove()
     assert len(shapes) >= 10
     tab = json.load(open(C.TABLE))
-    missing = [f"{d},{m},{ci},{co}" for (m, ci, co) in sorted(shapes)
-               for d in ("fwd", "bwd_data", "bwd_weight") if f"{d},{m},{ci},{co}" not in tab]
+    missing = [f"{d},bf16,{m},{ci},{co}" for (m, ci, co) in sorted(shapes)
+               for d in ("fwd", "bwd_data", "bwd_weight") if f"{d},bf16,{m},{ci},{co}" not in tab]
     assert not missing, missing
+
+
+def test_conv1x1_table_keyed_by_dtype_and_arch(tmp_path, monkeypatch):
+    """A bf16 decision never decides an fp32 conv of the same shape, and the committed (gfx950)
+    table is not loaded on any other device (here: no GPU at all)."""
+    from pytorch_distributed_training_example_amd.ops import conv as C
+    monkeypatch.setattr(C, "_CHOICE", {})
+    monkeypatch.setattr(C, "_TABLE_LOADED", [False])
+    C._ensure_table()
+    assert C._CHOICE == {}  # no gfx950 device here: nothing loaded
+    C.load_table()
+    assert C._CHOICE and all(k[1] == "bf16" for k in C._CHOICE)
+    k = next(iter(C._CHOICE))
+    assert ("fwd", "fp32", *k[2:]) not in C._CHOICE

@@ -81,11 +81,12 @@ def test_graph_step_lr0_matches_eager():
 
 
 def test_graph_step_matches_eager_training():
-    """Optimizer/step state across replays. Even with deterministic MIOpen solvers two *eager*
-    runs are not always bit-identical (find-mode may pick different solvers per run, and a few
-    bf16 SGD updates amplify any rounding difference), so the yardstick is the eager-vs-eager
-    drift: a broken replay (stale optimizer state, wrong input binding) is O(1) off, far above it."""
-    torch.backends.cudnn.deterministic = True
+    """Optimizer/step state across replays. Two *eager* runs are not bit-identical (MIOpen's
+    atomic split-K solvers, and a few bf16 SGD updates amplify any rounding difference), so the
+    yardstick is the eager-vs-eager drift: a broken replay (stale optimizer state, wrong input
+    binding) is O(1) off, far above it. Runs on the default solver set: MIOpen's deterministic
+    mode combined with the capture-safe solver exclusions has no solver for one of these
+    backward shapes on a fresh find-db (miopenStatusBadParm, seen on the round-end box)."""
     base = _setup()
     xs, ys = _data()
     le, pe, _ = _run(base, "eager", 0.01, xs, ys)
