@@ -317,6 +317,264 @@ __global__ __launch_bounds__(kThreads) void bn_reduce2_kernel(
   bn_finalize<MODE>(chunk * kCC + tid, sm[tid], sm[kCC + tid], fa);
 }
 
+// ---- v3 reduce: wide channel chunks + software-pipelined loads.
+// v2 measured 3.0-3.8 TB/s on the ResNet-50 shapes (tools/r50_roofline.py): every lane issued its
+// U loads, waited for all of them, accumulated, and only then issued the next U, so the bytes in
+// flight per CU fell to zero once per iteration; for C >= 256 each wave also read 8 separate
+// 128-B row pieces. v3:
+//   * a chunk is CC = min(C, 512) channels, LPR = CC/8 lanes per row, so one wave load instruction
+//     always reads 1 KB of contiguous memory (8 rows of C=64, ..., 1 row of C>=512);
+//   * the loads of iteration i+1 are issued before iteration i is accumulated (two register
+//     sets; the last iteration re-loads valid rows instead of branching around its loads, so
+//     hipcc's counted vmcnt waits stay intact — cdna_hip_programming.md §5 item 4(c));
+//   * the same deterministic two-level last-arriver finalize as v2, generalised to 2*CC columns.
+template <int MODE, int U>
+struct RowSet {
+  uint4 x[U];
+  uint4 g[U];
+  uint8_t mk[U];
+};
+
+template <int MODE, int U>
+__device__ __forceinline__ void load_set(RowSet<MODE, U>& s, const uint16_t* __restrict__ x,
+                                         const uint16_t* __restrict__ dy, const uint8_t* __restrict__ mask,
+                                         int64_t m, int64_t step, int C, int c) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t o = (m + u * step) * C + c;
+    s.x[u] = *reinterpret_cast<const uint4*>(x + o);
+    if (MODE != 0) s.g[u] = *reinterpret_cast<const uint4*>(dy + o);
+    if (MODE == 2) s.mk[u] = mask[o >> 3];
+  }
+}
+
+__device__ __forceinline__ void unpack8(const uint4& t, float (&v)[8]) {
+  const uint32_t w[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    v[2 * k] = __uint_as_float(w[k] << 16);
+    v[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+  }
+}
+
+template <int MODE, int U>
+__device__ __forceinline__ void accum_set(const RowSet<MODE, U>& s, const float (&k)[8], float (&s1)[8],
+                                          float (&s2)[8]) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    float xv[8];
+    unpack8(s.x[u], xv);
+    if (MODE == 0) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { const float d = xv[j] - k[j]; s1[j] += d; s2[j] = fmaf(d, d, s2[j]); }
+    } else {
+      float g[8];
+      unpack8(s.g[u], g);
+      if (MODE == 2) {
+        const unsigned mb = s.mk[u];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) g[j] = (mb >> j) & 1u ? g[j] : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { s1[j] += g[j]; s2[j] = fmaf(g[j], xv[j] - k[j], s2[j]); }
+    }
+  }
+}
+
+template <int LPR>
+__device__ __forceinline__ void sum_slabs3(const float* __restrict__ base, int n, int tid, float (&tot)[4]) {
+  constexpr int W = 2 * 8 * LPR;  // floats per slab
+  constexpr int NV = (W + kThreads - 1) / kThreads;
+#pragma unroll
+  for (int q = 0; q < NV; ++q) tot[q] = 0.f;
+  int i = 0;
+  for (; i + 8 <= n; i += 8) {
+#pragma unroll
+    for (int q = 0; q < NV; ++q) {
+      const int v = tid + q * kThreads;
+      if (v < W) {
+        float t[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) t[u] = base[(int64_t)(i + u) * W + v];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) tot[q] += t[u];
+      }
+    }
+  }
+  for (; i < n; ++i) {
+#pragma unroll
+    for (int q = 0; q < NV; ++q) {
+      const int v = tid + q * kThreads;
+      if (v < W) tot[q] += base[(int64_t)i * W + v];
+    }
+  }
+}
+
+template <int MODE, int LPR, int U>
+__global__ __launch_bounds__(kThreads) void bn_reduce3_kernel(
+    const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy, const uint8_t* __restrict__ mask,
+    const float* __restrict__ mean, int64_t M, int C, int64_t rows_per_block, int nrow,
+    float* __restrict__ part, float* __restrict__ gpart, unsigned* __restrict__ counters, FinArgs fa,
+    int split_fin) {
+  constexpr int CC = 8 * LPR;            // channels per chunk
+  constexpr int R = kThreads / LPR;      // rows per pass
+  constexpr int W = 2 * CC;              // floats per slab
+  constexpr int NV = (W + kThreads - 1) / kThreads;
+  __shared__ __attribute__((aligned(16))) float sm[2 * R * CC + 4];
+  const int tid = threadIdx.x;
+  const int chunk = blockIdx.y;
+  const int l = tid % LPR, r = tid / LPR;
+  const int c = chunk * CC + l * 8;
+  const int64_t m0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t m1 = min(M, m0 + rows_per_block);
+  float k[8], s1[8], s2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { s1[j] = 0.f; s2[j] = 0.f; }
+  if (MODE == 0) ld8_bf16(x + c, k);  // shift: row 0 (same for every block)
+  else ld8_f32(mean + c, k);
+  const int64_t per_it = (int64_t)U * R;
+  const int64_t nfull = (m1 - m0) / per_it;
+  if (nfull > 0) {
+    RowSet<MODE, U> a, b;
+    load_set<MODE, U>(a, x, dy, mask, m0 + r, R, C, c);
+    for (int64_t it = 0; it < nfull; it += 2) {
+      // prefetch it+1 (clamped: the tail re-loads valid rows, never branches around loads)
+      const int64_t n1 = it + 1 < nfull ? it + 1 : nfull - 1;
+      load_set<MODE, U>(b, x, dy, mask, m0 + n1 * per_it + r, R, C, c);
+      accum_set<MODE, U>(a, k, s1, s2);
+      if (it + 1 >= nfull) break;
+      const int64_t n2 = it + 2 < nfull ? it + 2 : nfull - 1;
+      load_set<MODE, U>(a, x, dy, mask, m0 + n2 * per_it + r, R, C, c);
+      accum_set<MODE, U>(b, k, s1, s2);
+    }
+  }
+  for (int64_t m = m0 + nfull * per_it + r; m < m1; m += R) {
+    RowSet<MODE, 1> t;
+    load_set<MODE, 1>(t, x, dy, mask, m, R, C, c);
+    accum_set<MODE, 1>(t, k, s1, s2);
+  }
+
+  float* d0 = &sm[r * CC + l * 8];
+  float* d1 = &sm[R * CC + r * CC + l * 8];
+  *reinterpret_cast<float4*>(d0) = make_float4(s1[0], s1[1], s1[2], s1[3]);
+  *reinterpret_cast<float4*>(d0 + 4) = make_float4(s1[4], s1[5], s1[6], s1[7]);
+  *reinterpret_cast<float4*>(d1) = make_float4(s2[0], s2[1], s2[2], s2[3]);
+  *reinterpret_cast<float4*>(d1 + 4) = make_float4(s2[4], s2[5], s2[6], s2[7]);
+  __syncthreads();
+  const int ngroups = (nrow + kG - 1) / kG;
+  const int g = blockIdx.x / kG;
+  const int gsize = min(kG, nrow - g * kG);
+  float* slabs = part + (int64_t)chunk * nrow * W;
+  float* gslabs = gpart + (int64_t)chunk * ngroups * W;
+  unsigned* ctr = counters + chunk * (ngroups + 1);
+  float tot[4];
+#pragma unroll
+  for (int q = 0; q < NV; ++q) {
+    tot[q] = 0.f;
+    const int v = tid + q * kThreads;
+    if (v < W) {
+      const int which = v / CC, cl = v % CC;
+      const float* src = &sm[which * R * CC + cl];
+#pragma unroll 4
+      for (int rr = 0; rr < R; ++rr) tot[q] += src[rr * CC];
+      if (gsize > 1 || split_fin) slabs[(int64_t)blockIdx.x * W + v] = tot[q];
+    }
+  }
+  if (split_fin) return;  // bn_fin_kernel reduces the slabs (next launch on the stream)
+  if (gsize > 1) {  // level 1: last arriver of the group of kG blocks
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned t = __hip_atomic_fetch_add(&ctr[g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      sm[2 * R * CC] = (t == (unsigned)(gsize - 1)) ? 1.f : 0.f;
+    }
+    __syncthreads();
+    if (sm[2 * R * CC] == 0.f) return;
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      ctr[g] = 0u;  // self-reset (stream-ordered for the next launch)
+    }
+    __syncthreads();
+    sum_slabs3<LPR>(slabs + (int64_t)g * kG * W, gsize, tid, tot);
+  }
+  if (ngroups > 1) {  // level 2: last group
+#pragma unroll
+    for (int q = 0; q < NV; ++q) {
+      const int v = tid + q * kThreads;
+      if (v < W) gslabs[(int64_t)g * W + v] = tot[q];
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned t = __hip_atomic_fetch_add(&ctr[ngroups], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      sm[2 * R * CC + 1] = (t == (unsigned)(ngroups - 1)) ? 1.f : 0.f;
+    }
+    __syncthreads();
+    if (sm[2 * R * CC + 1] == 0.f) return;
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      ctr[ngroups] = 0u;
+    }
+    __syncthreads();
+    sum_slabs3<LPR>(gslabs, ngroups, tid, tot);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < NV; ++q) {
+    const int v = tid + q * kThreads;
+    if (v < W) sm[v] = tot[q];
+  }
+  __syncthreads();
+  for (int ch = tid; ch < CC; ch += kThreads) bn_finalize<MODE>(chunk * CC + ch, sm[ch], sm[CC + ch], fa);
+}
+
+// Split finalize (bn_tune variant 5, default): the reduce kernel only writes one slab per block and
+// this kernel, next on the stream, sums them. Measured on the ResNet-50 shapes (tools/bn_trace.py):
+// the in-kernel last-arriver finalize (agent release fence, ticket, acquire fence, cross-XCD slab
+// reads, twice) cost 10-20 us per call on top of 12-160 us of streaming; a kernel boundary plus
+// this launch costs a few us. One block per 64 channels, summed in a fixed order (deterministic).
+template <int MODE>
+__global__ __launch_bounds__(1024) void bn_fin_kernel(const float* __restrict__ part, int nrow, int CC, FinArgs fa) {
+  // 1024 threads = 128 columns (S1, S2 of 64 channels) x 8 slab subsets; every thread issues its
+  // loads 16 at a time (clamped indices, no branches around loads) so one block's serial part is
+  // a few cross-XCD round trips, not nrow/2 of them
+  __shared__ float sm[8 * 128];
+  const int tid = threadIdx.x;
+  const int ch0 = blockIdx.x * 64;
+  const int chunk = ch0 / CC, off = ch0 % CC;
+  const int W = 2 * CC;
+  const int col = tid & 127, j = tid >> 7;
+  const int v = (col >> 6) * CC + off + (col & 63);
+  const float* base = part + (int64_t)chunk * nrow * W + v;
+  float a = 0.f;
+  for (int b0 = j; b0 < nrow; b0 += 8 * 16) {
+    float t[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int b = b0 + 8 * u;
+      t[u] = base[(int64_t)(b < nrow ? b : j) * W];
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) a += (b0 + 8 * u < nrow) ? t[u] : 0.f;
+  }
+  sm[j * 128 + col] = a;
+  __syncthreads();
+  if (tid < 128) {
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) s += sm[q * 128 + tid];
+    sm[tid] = s;
+  }
+  __syncthreads();
+  if (tid < 64) bn_finalize<MODE>(ch0 + tid, sm[tid], sm[64 + tid], fa);
+}
+
 __global__ void bn_eval_coef_kernel(int C, const float* __restrict__ gamma, const float* __restrict__ beta,
                                     const float* __restrict__ rm, const float* __restrict__ rv, float eps,
                                     float* __restrict__ a_out, float* __restrict__ b_out) {
@@ -525,7 +783,7 @@ inline ReduceGeo reduce_geo(int64_t M, int C) {
 // Reduce-kernel tuning (bn_tune): variant 1 = single-level finalize, 2 = two-level; total
 // workgroups targeted per call; rows in flight per lane for the forward / backward reduce.
 struct BnTune {
-  int variant = 2;
+  int variant = 5;
   int target_blocks = 512;  // tools/bn_reduce_sweep.py: 2 workgroups per CU beat 4-16 (10.5 vs 11.5+ ms/step)
   int u_fwd = 8;
   int u_bwd = 4;
@@ -550,6 +808,33 @@ inline int64_t slab_floats2(const ReduceGeo& g) {
   return (int64_t)g.nchunks * (g.nrow + ngroups) * 2 * kCC;
 }
 
+// v3: chunk = min(C, 512) channels (C is a multiple of 64; chunks must tile C exactly)
+inline int chunk3(int C) {
+  for (int cc = 512; cc > 64; cc >>= 1)
+    if (C % cc == 0) return cc;
+  return 64;
+}
+
+inline ReduceGeo reduce_geo3(int64_t M, int C, int U) {
+  ReduceGeo g;
+  const int cc = chunk3(C);
+  g.nchunks = C / cc;
+  const int R = kThreads / (cc / 8);
+  int64_t nrow = g_tune.target_blocks / g.nchunks;
+  if (nrow > 1024) nrow = 1024;
+  const int64_t max_rows = (M + 2 * (int64_t)U * R - 1) / (2 * (int64_t)U * R);  // >= 2 pipelined iterations
+  if (nrow > max_rows) nrow = max_rows;
+  if (nrow < 1) nrow = 1;
+  g.rows_per_block = (M + nrow - 1) / nrow;
+  g.nrow = (int)((M + g.rows_per_block - 1) / g.rows_per_block);
+  return g;
+}
+
+inline int64_t slab_floats3(const ReduceGeo& g, int C) {
+  const int ngroups = (g.nrow + kG - 1) / kG;
+  return (int64_t)(g.nrow + ngroups) * 2 * C;  // nchunks * (nrow + ngroups) * 2 * cc
+}
+
 // Launch the reduce (+ fused finalize) of MODE; returns the float offset in ws where the
 // per-channel coefficient arrays start.
 template <int MODE>
@@ -562,6 +847,28 @@ int64_t launch_reduce(const uint16_t* x, const uint16_t* dy, const uint8_t* mask
     return (int64_t)g.nchunks * g.nrow * 2 * kCC;
   }
   const int U = MODE == 0 ? g_tune.u_fwd : g_tune.u_bwd;
+  if (g_tune.variant >= 3) {
+    const ReduceGeo g = reduce_geo3(M, C, U);
+    float* part = ws;
+    float* gpart = ws + (int64_t)g.nrow * 2 * C;
+    const int cc = chunk3(C);
+#define PDT_R3(LPR, UU)                                                                                      \
+  hipLaunchKernelGGL((bn_reduce3_kernel<MODE, LPR, UU>), dim3(g.nrow, g.nchunks), dim3(kThreads), 0, s, x, dy, \
+                     mask, mean, M, C, g.rows_per_block, g.nrow, part, gpart, counters, fa, g_tune.variant >= 4)
+#define PDT_R3U(LPR)              \
+  if (U >= 8) PDT_R3(LPR, 8);     \
+  else if (U >= 4) PDT_R3(LPR, 4); \
+  else PDT_R3(LPR, 2)
+    if (cc == 512) { PDT_R3U(64); }
+    else if (cc == 256) { PDT_R3U(32); }
+    else if (cc == 128) { PDT_R3U(16); }
+    else { PDT_R3U(8); }
+#undef PDT_R3U
+#undef PDT_R3
+    if (g_tune.variant == 5)
+      hipLaunchKernelGGL(bn_fin_kernel<MODE>, dim3(C / 64), dim3(1024), 0, s, part, g.nrow, cc, fa);
+    return slab_floats3(g, C);
+  }
   const ReduceGeo g = reduce_geo2(M, C, U);
   float* part = ws;
   float* gpart = ws + (int64_t)g.nchunks * g.nrow * 2 * kCC;
@@ -596,7 +903,10 @@ int64_t pdt_bn_workspace_floats(int64_t M, int C) {
   const ReduceGeo g1 = reduce_geo(M, C);
   const int64_t v1 = (int64_t)g1.nchunks * g1.nrow * 2 * kCC;
   const int64_t v2 = slab_floats2(reduce_geo2(M, C, 2));  // U = 2 gives the most rows
-  return (v1 > v2 ? v1 : v2) + 4 * (int64_t)C;
+  const int64_t v3 = slab_floats3(reduce_geo3(M, C, 2), C);
+  int64_t v = v1 > v2 ? v1 : v2;
+  v = v > v3 ? v : v3;
+  return v + 4 * (int64_t)C;
 }
 
 // Select the reduce implementation / grid (benchmarking). Values <= 0 keep the current setting.

@@ -83,6 +83,37 @@ def test_bn_relu_maxpool_stem(shape):
     torch.testing.assert_close(bs.grad, bf.grad, rtol=2e-2, atol=5e-1)
 
 
+@pytest.mark.parametrize("C,N,H", [(64, 32, 37), (128, 16, 29), (1024, 12, 15), (2048, 9, 7)])
+@pytest.mark.parametrize("variant", [2, 5])
+def test_batchnorm_reduce_variants_large_m(C, N, H, variant):
+    """The BN reduce implementations (v2: in-kernel two-level finalize; v5 = default: pipelined
+    wide-chunk reduce + separate finalize kernel) at row counts that exercise several pipelined
+    iterations per workgroup and ragged tails, against the fp32 reference."""
+    C_ = _native()
+    torch.manual_seed(1)
+    try:
+        C_.bn_tune(variant, 512, 8, 4)
+        x = (torch.randn(N, C, H, H, device=DEV) * 1.5 + 0.7).to(torch.bfloat16).to(memory_format=torch.channels_last)
+        w, b = torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV)
+        rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+        y, mask, mean, invstd = C_.bn_fwd_train(x, None, w, b, rm, rv, 0.1, 1e-5, True)
+        xf = x.float()
+        mu = xf.mean(dim=(0, 2, 3))
+        var = xf.var(dim=(0, 2, 3), unbiased=False)
+        torch.testing.assert_close(mean, mu, rtol=1e-4, atol=1e-4)
+        torch.testing.assert_close(invstd, torch.rsqrt(var + 1e-5), rtol=1e-3, atol=1e-3)
+        yf = F.relu((xf - mu.view(1, -1, 1, 1)) * (w * torch.rsqrt(var + 1e-5)).view(1, -1, 1, 1) + b.view(1, -1, 1, 1))
+        torch.testing.assert_close(y.float(), yf, rtol=2e-2, atol=3e-2)
+        dy = torch.randn_like(x)
+        dx, _, dg, db = C_.bn_bwd_train(dy, x, mask, w, mean, invstd, True, False, True)
+        dz = dy.float() * (yf > 0)
+        xhat = (xf - mu.view(1, -1, 1, 1)) * torch.rsqrt(var + 1e-5).view(1, -1, 1, 1)
+        torch.testing.assert_close(db, dz.sum(dim=(0, 2, 3)), rtol=1e-3, atol=1e-1)
+        torch.testing.assert_close(dg, (dz * xhat).sum(dim=(0, 2, 3)), rtol=1e-3, atol=1e-1)
+    finally:
+        C_.bn_tune(5, 512, 8, 4)
+
+
 def test_batchnorm_large_mean_stability():
     """Shifted sums must not lose the variance when |mean| >> std."""
     from pytorch_distributed_training_example_amd.ops.batchnorm import batch_norm_act

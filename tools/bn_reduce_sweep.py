@@ -23,8 +23,8 @@ SHAPES = [
     (512, 14, 1, True, False), (512, 7, 5, True, False), (2048, 7, 3, True, True), (2048, 7, 1, False, False),
 ]
 TUNINGS = [  # (variant, target_blocks, u_fwd, u_bwd)
-    (1, 0, 0, 0), (2, 1024, 8, 4), (2, 768, 8, 4), (2, 512, 8, 4), (2, 512, 4, 4), (2, 512, 8, 8),
-    (2, 384, 8, 4), (2, 256, 8, 4), (2, 256, 16, 8),
+    (2, 512, 8, 4), (3, 512, 8, 4), (3, 512, 4, 4), (3, 512, 8, 8), (3, 512, 4, 2), (3, 1024, 8, 4),
+    (3, 1024, 4, 2), (3, 256, 8, 4), (3, 768, 4, 4), (2, 512, 8, 4),
 ]
 
 
@@ -43,7 +43,7 @@ def timed(fn, it=10):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--batch", type=int, default=512)
     a = ap.parse_args()
     C_ = native()
     data = []
