@@ -70,6 +70,9 @@ int pdt_bn_relu_maxpool_fwd_train(const uint16_t* x, const float* gamma, const f
                                   float* running_var, float momentum, float eps, int N, int H, int W, int C,
                                   uint16_t* y, uint8_t* code, float* mean, float* invstd, float* ws,
                                   unsigned* counters, hipStream_t s);
+int pdt_conv3x3s1_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int N, int H, int W, int Ci, int Co,
+                      hipStream_t s);
+int pdt_conv3x3_flip_weights(const uint16_t* w, uint16_t* wf, int Co, int Ci, hipStream_t s);
 int pdt_maxpool3s2_bwd(const uint16_t* dy, const uint8_t* code, uint16_t* dz, int N, int H, int W, int C,
                        hipStream_t s);
 int pdt_fp8_cast_transpose(const uint16_t* x, int64_t M, int64_t K, const float* scale, uint8_t* out,
@@ -410,6 +413,39 @@ std::vector<Tensor> bn_bwd_train(Tensor dy, Tensor x, c10::optional<Tensor> mask
                             ws.data_ptr<float>(), bn_counters(x), stream());
   TORCH_CHECK(rc == 0, "pdt_bn_bwd_train failed");
   return {dx, dres, dg, db};
+}
+
+// ----------------------------------------------------------------------------- 3x3 conv (stride 1, pad 1)
+// y = conv2d(x, w, stride=1, padding=1) for channels_last bf16 x [N,Ci,H,W] and w [Co,Ci,3,3]
+// (w's channels_last storage is [Co][3][3][Ci], the kernel's layout).
+Tensor conv3x3s1_fwd(Tensor x, Tensor w) {
+  check_nhwc_bf16(x, "x");
+  TORCH_CHECK(w.dim() == 4 && w.size(2) == 3 && w.size(3) == 3 && w.size(1) == x.size(1) &&
+              w.scalar_type() == at::kBFloat16, "conv3x3: weight [Co, Ci, 3, 3] bf16");
+  w = w.contiguous(at::MemoryFormat::ChannelsLast);
+  const int64_t N = x.size(0), Ci = x.size(1), H = x.size(2), W = x.size(3), Co = w.size(0);
+  auto y = at::empty({N, Co, H, W}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const int rc = pdt_conv3x3s1_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                                   reinterpret_cast<const uint16_t*>(w.data_ptr()),
+                                   reinterpret_cast<uint16_t*>(y.data_ptr()), (int)N, (int)H, (int)W, (int)Ci, (int)Co,
+                                   stream());
+  TORCH_CHECK(rc == 0, "pdt_conv3x3s1_fwd failed: ", rc);
+  return y;
+}
+
+// Data-gradient weights: wf [Ci, Co, 3, 3] (channels_last storage [Ci][3][3][Co]) with
+// wf[ci, co, kh, kw] = w[co, ci, 2 - kh, 2 - kw], so dx = conv3x3s1_fwd(dy, wf).
+Tensor conv3x3_flip(Tensor w) {
+  check_cuda(w, "w");
+  TORCH_CHECK(w.dim() == 4 && w.size(2) == 3 && w.size(3) == 3 && w.scalar_type() == at::kBFloat16,
+              "conv3x3_flip: weight [Co, Ci, 3, 3] bf16");
+  w = w.contiguous(at::MemoryFormat::ChannelsLast);
+  const int64_t Co = w.size(0), Ci = w.size(1);
+  auto wf = at::empty({Ci, Co, 3, 3}, w.options().memory_format(at::MemoryFormat::ChannelsLast));
+  TORCH_CHECK(pdt_conv3x3_flip_weights(reinterpret_cast<const uint16_t*>(w.data_ptr()),
+                                       reinterpret_cast<uint16_t*>(wf.data_ptr()), (int)Co, (int)Ci, stream()) == 0,
+              "pdt_conv3x3_flip_weights failed");
+  return wf;
 }
 
 // ----------------------------------------------------------------------------- cross entropy
@@ -802,6 +838,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_fwd_eval", &bn_fwd_eval);
   m.def("bn_relu_maxpool_fwd", &bn_relu_maxpool_fwd);
   m.def("maxpool3s2_bwd", &maxpool3s2_bwd);
+  m.def("conv3x3s1_fwd", &conv3x3s1_fwd);
+  m.def("conv3x3_flip", &conv3x3_flip);
   m.def("bn_bwd_train", &bn_bwd_train);
   m.def("ce_fwd", &ce_fwd);
   m.def("ce_bwd", &ce_bwd);

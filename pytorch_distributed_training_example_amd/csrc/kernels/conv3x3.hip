@@ -1,0 +1,857 @@
+// 3x3 / stride 1 / pad 1 convolution as an implicit GEMM on MFMA (gfx950), NHWC bf16, fp32 accumulate.
+//
+// Not in the reference (LeNet's convs are 5x5 on 1-16 channels, /root/reference/cnn.py:10-16).
+// Serves the ResNet-50 north-star config: 13 of its 16 3x3 convs are stride 1, and every one does
+// 118 GFLOP per direction at batch 512. MIOpen's kernels ran them at 0.35-0.9 PF
+// (tools/r50_roofline.py: fwd 135-255 us, data-gradient 210-296 us vs a 74 us MFMA floor).
+//
+//   Y[m, co] = sum_{tap, ci} X[pixel(m) + shift(tap), ci] * Wt[co, tap, ci]      (m = (n, oh, ow))
+//
+// GEMM view: M = N*H*W pixels, N = Co, K = 9 taps x Ci. A k-step is one tap and 64 input
+// channels, so every A row is 128 contiguous bytes of one (shifted) input pixel, or zeros when
+// the shifted pixel is in the padding. The data gradient of the same conv is this kernel on dY
+// with the weights flipped and transposed (conv3x3_flip_weights): Wt'[ci, 8 - tap, co].
+//
+// Structure (cdna_hip_programming.md §5):
+//   * tile 256 pixels x BN (64 | 128) output channels, 512 threads = 8 waves as 4 (M) x 2 (N),
+//     each wave 64 x BN/2 as 4 x BN/32 blocks of v_mfma_f32_16x16x32_bf16;
+//   * operands staged global -> LDS by LDS-DMA (global_load_lds_dwordx4: 1 KB = 8 rows of 128 B
+//     per wave instruction) into a 3-slot ring: the slot for k-step s+2 is issued right after the
+//     barrier of step s, while steps s (being read) and s+1 (landing) are resident; ONE raw
+//     s_barrier per k-step and a counted vmcnt, so the DMA stays in flight across barriers;
+//   * padding rows are DMA'd from a 256-B zero page (per-lane source address), no branches;
+//   * rows XOR-swizzled ((row >> 1) & 7 on the 16-B chunk: conflict-free ds_read_b128 for the
+//     16x16x32 lane map) by permuting each lane's SOURCE chunk — the DMA writes LDS linearly;
+//   * MFMA operands swapped (A = weights, B = pixels) so a lane's accumulator holds 4
+//     consecutive channels of one pixel; the epilogue stages the bf16 tile through LDS and
+//     writes whole 16-B row pieces;
+//   * block -> tile map XCD-aware (xcd_remap): the output-channel tiles of one pixel tile, and
+//     neighbouring pixel tiles (which share input rows), run on one XCD's L2.
+#include "../common.h"
+
+using namespace pdt;
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+#define PDT_LDS __attribute__((address_space(3)))
+
+__device__ __attribute__((aligned(256))) uint4 g_conv_zero[16];  // zero page for padding rows (never written)
+
+constexpr int kSlots = 3;
+
+// Tile BM pixels x BN channels, WM x WN waves (each (BM/WM) x (BN/WN)), BK input channels per
+// k-step (LDS rows of 2*BK bytes), 3-slot LDS ring.
+template <int BM_, int BN_, int WM_, int WN_, int BK_>
+struct Cfg {
+  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, BK = BK_;
+  static constexpr int kThreads = WM * WN * 64;
+  static constexpr int kRow = BK * 2;
+  static constexpr int kRPI = 1024 / kRow;  // rows per 1-KB DMA instruction
+  static constexpr int kABytes = BM * kRow;
+  static constexpr int kBBytes = BN * kRow;
+  static constexpr int kSlot = kABytes + kBBytes;
+  static constexpr int kEpiStride = BN * 2 + 16;
+  static constexpr int kLds = (kSlots * kSlot > BM * kEpiStride) ? kSlots * kSlot : BM * kEpiStride;
+  static constexpr int kMB = BM / WM / 16;  // 16-row pixel blocks per wave
+  static constexpr int kNB = BN / WN / 16;  // 16-wide channel blocks per wave
+  static constexpr int kALd = BM / kRPI / (WM * WN);  // DMA instructions per wave per slot
+  static constexpr int kBLd = BN / kRPI / (WM * WN);
+  static constexpr int kG = kALd + kBLd;
+  static_assert(kALd * kRPI * WM * WN == BM && kBLd * kRPI * WM * WN == BN, "DMA split");
+};
+
+// 16-B chunk swizzle: conflict-free ds_read_b128 of 16 consecutive rows for the 16x16x32 lane
+// map (lanes 16q..16q+15 read chunk q of rows 0..15; ds_read_b128 serves lane groups
+// {0-3,12-15,20-27}, {4-11,16-19,28-31}, ... one LDS cycle each). 128-B rows: chunk ^ ((row>>1)&7).
+// 64-B rows (4 rows per 256-B bank row): chunk ^ (((row>>2)&1)<<1) — conflict-free for 16
+// consecutive rows starting at ANY row (the halo kernel's tap-shifted reads), not just aligned ones:
+// in every lane group the 4 rows of one residue mod 4 have consecutive row>>2 and chunks c, c^1,
+// c^1, c, which this XOR maps to 4 distinct 16-B slots (checked by hand for all four groups).
+template <int ROW>
+__device__ __forceinline__ int swz(int row, int chunk) {
+  if constexpr (ROW == 128) return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4);
+  else return row * 64 + ((chunk ^ (((row >> 2) & 1) << 1)) << 4);
+}
+
+__device__ __forceinline__ f4 mfma(bf16x8 a, bf16x8 b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ void dma16(const void* src, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds(src, (PDT_LDS void*)lds_wave_base, 16, 0, 0);
+}
+
+template <int G>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(G >= 0 && G <= 8, "vmcnt");
+  if constexpr (G == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (G == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if constexpr (G == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+  else if constexpr (G == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (G == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+  else if constexpr (G == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if constexpr (G == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+#ifndef PDT_CONV_PROBE
+#define PDT_CONV_PROBE 0  // diagnostics only: 1 = DMA without MFMA, 2 = MFMA without DMA
+#endif
+template <class Cf>
+__global__ __launch_bounds__(Cf::kThreads, Cf::kThreads / 128) void conv3x3s1_kernel(
+    const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wt, uint16_t* __restrict__ Y, int N, int H, int W,
+    int Ci, int Co) {
+  constexpr int BM = Cf::BM, BN = Cf::BN, BK = Cf::BK, ROW = Cf::kRow, RPI = Cf::kRPI, CPR = BK / 8;
+  constexpr int WROWS = BM / Cf::WM, WCOLS = BN / Cf::WN;
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid % Cf::WM, wn = wid / Cf::WM;
+  const int HW = H * W;
+  const int M = N * HW;
+  const int ntiles = Co / BN;
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (tile / ntiles) * BM, n0 = (tile % ntiles) * BN;
+
+  // ---- rows this lane DMAs: A rows (wid*kALd + i)*RPI + lane/CPR, chunk lane%CPR (pre-swizzled)
+  const int sub = lane / CPR, p = lane % CPR;
+  int aoff[Cf::kALd];
+  unsigned amask[Cf::kALd];
+#pragma unroll
+  for (int i = 0; i < Cf::kALd; ++i) {
+    const int r = (wid * Cf::kALd + i) * RPI + sub;
+    const int m = m0 + r;
+    const int chk = (swz<ROW>(r, p) - r * ROW) >> 4;  // logical chunk stored at physical p
+    unsigned mk = 0;
+    aoff[i] = chk * 8;
+    if (m < M) {
+      const int rem = m % HW, oh = rem / W, ow = rem % W;
+      aoff[i] += m * Ci;
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+          const int ih = oh + kh - 1, iw = ow + kw - 1;
+          if (ih >= 0 && ih < H && iw >= 0 && iw < W) mk |= 1u << (kh * 3 + kw);
+        }
+    }
+    amask[i] = mk;
+  }
+  int boff[Cf::kBLd];
+#pragma unroll
+  for (int j = 0; j < Cf::kBLd; ++j) {
+    const int r = (wid * Cf::kBLd + j) * RPI + sub;
+    boff[j] = (n0 + r) * 9 * Ci + ((swz<ROW>(r, p) - r * ROW) >> 4) * 8;
+  }
+  const int kcc = Ci / BK;
+  const int S = 9 * kcc;
+
+  auto issue = [&](int s) {
+    const int tap = s % 9, cc = s / 9;
+    const int kh = tap / 3, kw = tap - kh * 3;
+    const int toff = ((kh - 1) * W + (kw - 1)) * Ci + cc * BK;
+    char* slot = lds + (s % kSlots) * Cf::kSlot;
+#pragma unroll
+    for (int i = 0; i < Cf::kALd; ++i) {
+      const uint16_t* src =
+          ((amask[i] >> tap) & 1u) ? X + (aoff[i] + toff) : reinterpret_cast<const uint16_t*>(g_conv_zero);
+      dma16(src, slot + (wid * Cf::kALd + i) * 1024);
+    }
+    const int wo = tap * Ci + cc * BK;
+#pragma unroll
+    for (int j = 0; j < Cf::kBLd; ++j)
+      dma16(Wt + (boff[j] + wo), slot + Cf::kABytes + (wid * Cf::kBLd + j) * 1024);
+  };
+
+  f4 acc[Cf::kMB][Cf::kNB];
+#pragma unroll
+  for (int i = 0; i < Cf::kMB; ++i)
+#pragma unroll
+    for (int j = 0; j < Cf::kNB; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+
+  issue(0);
+  if (S > 1) issue(1);
+  const int lrow = lane & 15, lchk = lane >> 4;
+  for (int s = 0; s < S; ++s) {
+    if (s + 1 < S) wait_vm<Cf::kG>();
+    else wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (PDT_CONV_PROBE != 2 && s + 2 < S) issue(s + 2);
+    if (PDT_CONV_PROBE == 1) continue;
+    const char* As = lds + (s % kSlots) * Cf::kSlot;
+    const char* Bs = As + Cf::kABytes;
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      bf16x8 a[Cf::kMB], b[Cf::kNB];
+#pragma unroll
+      for (int i = 0; i < Cf::kMB; ++i)
+        a[i] = *reinterpret_cast<const bf16x8*>(As + swz<ROW>(wm * WROWS + i * 16 + lrow, kk * 4 + lchk));
+#pragma unroll
+      for (int j = 0; j < Cf::kNB; ++j)
+        b[j] = *reinterpret_cast<const bf16x8*>(Bs + swz<ROW>(wn * WCOLS + j * 16 + lrow, kk * 4 + lchk));
+#pragma unroll
+      for (int i = 0; i < Cf::kMB; ++i)
+#pragma unroll
+        for (int j = 0; j < Cf::kNB; ++j) acc[i][j] = mfma(b[j], a[i], acc[i][j]);  // D[co][m]
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+
+  // ---- epilogue: bf16 tile [BM pixels][BN] through LDS, then 16-B row pieces to Y
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < Cf::kMB; ++i)
+#pragma unroll
+    for (int j = 0; j < Cf::kNB; ++j) {
+      const int ml = wm * WROWS + i * 16 + lrow;
+      const int cl = wn * WCOLS + j * 16 + 4 * lchk;
+      const f4 v = acc[i][j];
+      uint2 pk;
+      pk.x = (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)v[0]) |
+             ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)v[1]) << 16);
+      pk.y = (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)v[2]) |
+             ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)v[3]) << 16);
+      *reinterpret_cast<uint2*>(lds + ml * Cf::kEpiStride + cl * 2) = pk;
+    }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  constexpr int kChunks = BN / 8;
+  for (int idx = tid; idx < BM * kChunks; idx += Cf::kThreads) {
+    const int r = idx / kChunks, c = idx % kChunks;
+    const int m = m0 + r;
+    if (m < M)
+      *reinterpret_cast<uint4*>(Y + (int64_t)m * Co + n0 + c * 8) =
+          *reinterpret_cast<const uint4*>(lds + r * Cf::kEpiStride + c * 16);
+  }
+}
+
+// ---------------------------------------------------------------- halo variant (default)
+// The per-tap kernel above DMAs its A tile once per TAP: every input pixel crosses L2 -> LDS nine
+// times, and at 48 KB per k-step the L2 -> LDS path (~60-70 GB/s per CU) bounds it near 0.8 PF
+// (SQ_VALU_MFMA_BUSY 37 %). Here the A operand of one 32-channel chunk is staged ONCE as the
+// tile's padded input halo — the input rows its 256 output pixels touch, each row W+2 pixels wide
+// (pad columns and rows DMA'd from the zero page) — and the nine taps read shifted fragment rows
+// out of it: LDS row of (pixel m, tap kh,kw) = base(m) + kh*(W+2) + kw. Only the weights stream
+// per tap. LDS: 2 halo buffers (chunk c computes while c+1 lands) + 2 weight slots = 80 KB ->
+// two workgroups per CU.
+template <int BN_, int WM_, int WN_>
+struct HCfg {
+  static constexpr int BM = 256, BN = BN_, WM = WM_, WN = WN_, BK = 32;
+  static constexpr int kThreads = WM * WN * 64;
+  static constexpr int kWaves = WM * WN;
+  static constexpr int kRow = 64;
+  static constexpr int kHaloRows = 512;  // >= padded-halo rows of any 256-pixel tile (host-checked)
+  static constexpr int kHaloBytes = kHaloRows * kRow;
+  static constexpr int kBBytes = BN * kRow;
+  static constexpr int kHLd = kHaloRows / 16 / kWaves;  // halo DMA instructions per wave
+  static constexpr int kBLd = BN / 16 / kWaves;         // weight DMA instructions per wave per tap
+  static constexpr int kMB = BM / WM / 16, kNB = BN / WN / 16;
+  static constexpr int kEpiStride = BN * 2 + 16;
+  static constexpr int kMain = 2 * kHaloBytes + 2 * kBBytes;
+  static constexpr int kLds = kMain > BM * kEpiStride ? kMain : BM * kEpiStride;
+  static_assert(kHLd * 16 * kWaves == kHaloRows && kBLd * 16 * kWaves == BN, "DMA split");
+};
+
+__device__ __forceinline__ int chk64(int row, int p) { return p ^ (((row >> 2) & 1) << 1); }  // = swz<64>, involution
+
+template <class Cf>
+__global__ __launch_bounds__(Cf::kThreads, Cf::kThreads / 128) void conv3x3h_kernel(
+    const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wt, uint16_t* __restrict__ Y, int N, int H, int W,
+    int Ci, int Co) {
+  constexpr int BM = Cf::BM, BN = Cf::BN, BK = Cf::BK;
+  constexpr int WROWS = BM / Cf::WM, WCOLS = BN / Cf::WN;
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid % Cf::WM, wn = wid / Cf::WM;
+  const int HW = H * W, M = N * HW, W2 = W + 2, H2 = H + 2;
+  const int ntiles = Co / BN;
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (tile / ntiles) * BM, n0 = (tile % ntiles) * BN;
+  const int mlast = min(m0 + BM, M) - 1;
+  const int pr0 = (m0 / HW) * H2 + (m0 % HW) / W;  // padded row of (n_first, oh_first - 1)
+  const int Q = ((mlast / HW) * H2 + (mlast % HW) / W + 2 - pr0 + 1) * W2;
+
+  const int sub = lane >> 2, p = lane & 3;
+  int hoff[Cf::kHLd];  // element offset of this lane's halo piece, -1 = zero page
+#pragma unroll
+  for (int i = 0; i < Cf::kHLd; ++i) {
+    const int q = (wid * Cf::kHLd + i) * 16 + sub;
+    int off = -1;
+    if (q < Q) {
+      const int PR = pr0 + q / W2, col = q % W2;
+      const int n = PR / H2, ih = PR % H2 - 1, iw = col - 1;
+      if (ih >= 0 && ih < H && iw >= 0 && iw < W && n < N) off = ((n * H + ih) * W + iw) * Ci + chk64(q, p) * 8;
+    }
+    hoff[i] = off;
+  }
+  int boff[Cf::kBLd];
+#pragma unroll
+  for (int j = 0; j < Cf::kBLd; ++j) {
+    const int r = (wid * Cf::kBLd + j) * 16 + sub;
+    boff[j] = (n0 + r) * 9 * Ci + chk64(r, p) * 8;
+  }
+  const int lrow = lane & 15, lchk = lane >> 4;
+  int abase[Cf::kMB];
+#pragma unroll
+  for (int i = 0; i < Cf::kMB; ++i) {
+    const int m = min(m0 + wm * WROWS + i * 16 + lrow, mlast);  // rows past M: computed, never stored
+    const int n = m / HW, rem = m % HW, oh = rem / W, ow = rem % W;
+    abase[i] = (n * H2 + oh - pr0) * W2 + ow;
+  }
+  const int nch = Ci / BK;
+  const int S = 9 * nch;
+  char* const halo0 = lds;
+  char* const bslot0 = lds + 2 * Cf::kHaloBytes;
+
+  auto issue_halo = [&](int c) {
+    char* hb = halo0 + (c & 1) * Cf::kHaloBytes;
+#pragma unroll
+    for (int i = 0; i < Cf::kHLd; ++i) {
+      const uint16_t* src = hoff[i] >= 0 ? X + (hoff[i] + c * BK) : reinterpret_cast<const uint16_t*>(g_conv_zero);
+      dma16(src, hb + (wid * Cf::kHLd + i) * 1024);
+    }
+  };
+  auto issue_b = [&](int s) {
+    const int c = s / 9, t = s - 9 * c;
+    char* bs = bslot0 + (s & 1) * Cf::kBBytes;
+#pragma unroll
+    for (int j = 0; j < Cf::kBLd; ++j) dma16(Wt + (boff[j] + t * Ci + c * BK), bs + (wid * Cf::kBLd + j) * 1024);
+  };
+
+  f4 acc[Cf::kMB][Cf::kNB];
+#pragma unroll
+  for (int i = 0; i < Cf::kMB; ++i)
+#pragma unroll
+    for (int j = 0; j < Cf::kNB; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+
+  issue_halo(0);
+  issue_b(0);
+  bool pend = false;  // a halo DMA was issued after the last weight DMA (wave-uniform)
+  for (int s = 0; s < S; ++s) {
+    // weights of step s (issued last step) and, at a chunk start, its halo (issued 8 steps ago
+    // and retired two steps after issue by the in-order vmcnt) are resident once every wave has
+    // waited for its own DMA and passed the barrier
+    if (pend) wait_vm<Cf::kHLd>();
+    else wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    pend = false;
+    const int c = s / 9, t = s - 9 * c;
+    if (s + 1 < S) issue_b(s + 1);
+    if (t == 1 && c + 1 < nch) {  // buffer (c+1)&1 was last read in chunk c-1: every wave is past it
+      issue_halo(c + 1);
+      pend = true;
+    }
+    const char* hb = halo0 + (c & 1) * Cf::kHaloBytes;
+    const char* bs = bslot0 + (s & 1) * Cf::kBBytes;
+    const int toff = (t / 3) * W2 + (t % 3);
+    bf16x8 a[Cf::kMB], b[Cf::kNB];
+#pragma unroll
+    for (int i = 0; i < Cf::kMB; ++i) {
+      const int q = abase[i] + toff;
+      a[i] = *reinterpret_cast<const bf16x8*>(hb + q * 64 + (chk64(q, lchk) << 4));
+    }
+#pragma unroll
+    for (int j = 0; j < Cf::kNB; ++j) {
+      const int r = wn * WCOLS + j * 16 + lrow;
+      b[j] = *reinterpret_cast<const bf16x8*>(bs + r * 64 + (chk64(r, lchk) << 4));
+    }
+#pragma unroll
+    for (int i = 0; i < Cf::kMB; ++i)
+#pragma unroll
+      for (int j = 0; j < Cf::kNB; ++j) acc[i][j] = mfma(b[j], a[i], acc[i][j]);  // D[co][m]
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < Cf::kMB; ++i)
+#pragma unroll
+    for (int j = 0; j < Cf::kNB; ++j) {
+      const int ml = wm * WROWS + i * 16 + lrow;
+      const int cl = wn * WCOLS + j * 16 + 4 * lchk;
+      const f4 v = acc[i][j];
+      uint2 pk;
+      pk.x = (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)v[0]) |
+             ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)v[1]) << 16);
+      pk.y = (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)v[2]) |
+             ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)v[3]) << 16);
+      *reinterpret_cast<uint2*>(lds + ml * Cf::kEpiStride + cl * 2) = pk;
+    }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  constexpr int kChunks = BN / 8;
+  for (int idx = tid; idx < BM * kChunks; idx += Cf::kThreads) {
+    const int r = idx / kChunks, cc = idx % kChunks;
+    const int m = m0 + r;
+    if (m < M)
+      *reinterpret_cast<uint4*>(Y + (int64_t)m * Co + n0 + cc * 8) =
+          *reinterpret_cast<const uint4*>(lds + r * Cf::kEpiStride + cc * 16);
+  }
+}
+
+// ---------------------------------------------------------------- warp-specialised halo variant
+// Counters on the two kernels above (SQ_VALU_MFMA_BUSY 37-40 %, SQ_WAIT_ANY 33 %) point at their
+// barrier-per-k-step structure: every 16 MFMAs per wave all waves meet, issue DMA, and wait for
+// fresh LDS reads before the matrix pipe restarts. Here one workgroup = 4 consumer waves (one per
+// SIMD, 64 pixels x 64 channels each) + NL loader waves, and the unit of synchronisation is a whole
+// 32-channel chunk: its padded input halo AND the weights of all nine taps (68 KB) sit in one of two
+// LDS buffers, so a consumer runs 9 x 16 MFMAs with its fragment reads for tap t+1 issued under the
+// MFMAs of tap t and meets the others once per chunk. Loader waves DMA chunk c+1 into the other
+// buffer meanwhile (their DMA issue never blocks a consumer's MFMA issue).
+template <int NL_>
+struct WCfg {
+  static constexpr int BM = 256, BN = 64, BK = 32, NL = NL_;
+  static constexpr int kThreads = (4 + NL) * 64;
+  static constexpr int kHaloRows = 512;
+  static constexpr int kHaloBytes = kHaloRows * 64;  // 32 KB
+  static constexpr int kBRows = 9 * BN;              // [tap][co]
+  static constexpr int kBBytes = kBRows * 64;        // 36 KB
+  static constexpr int kBuf = kHaloBytes + kBBytes;
+  static constexpr int kHIns = kHaloRows / 16 / NL, kBIns = kBRows / 16 / NL;  // DMA instrs per loader
+  static constexpr int kEpiStride = BN * 2 + 16;
+  static constexpr int kLds = 2 * kBuf;
+  static_assert(kHIns * 16 * NL == kHaloRows && kBIns * 16 * NL == kBRows, "DMA split");
+  static_assert(BM * kEpiStride <= kLds, "epilogue");
+};
+
+template <class Cf>
+__global__ __launch_bounds__(Cf::kThreads, 1) void conv3x3ws_kernel(const uint16_t* __restrict__ X,
+                                                                  const uint16_t* __restrict__ Wt,
+                                                                  uint16_t* __restrict__ Y, int N, int H, int W,
+                                                                  int Ci, int Co) {
+  constexpr int BM = Cf::BM, BN = Cf::BN, BK = Cf::BK;
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const bool loader = wid >= 4;
+  const int HW = H * W, M = N * HW, W2 = W + 2, H2 = H + 2;
+  const int ntiles = Co / BN;
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (tile / ntiles) * BM, n0 = (tile % ntiles) * BN;
+  const int mlast = min(m0 + BM, M) - 1;
+  const int pr0 = (m0 / HW) * H2 + (m0 % HW) / W;
+  const int Q = ((mlast / HW) * H2 + (mlast % HW) / W + 2 - pr0 + 1) * W2;
+  const int nch = Ci / BK;
+
+  // loader state: element offsets of this lane's halo and weight pieces (-1 = zero page)
+  int hoff[Cf::kHIns], boff[Cf::kBIns];
+  const int sub = lane >> 2, p = lane & 3;
+  if (loader) {
+    const int l = wid - 4;
+#pragma unroll
+    for (int i = 0; i < Cf::kHIns; ++i) {
+      const int q = (l * Cf::kHIns + i) * 16 + sub;
+      int off = -1;
+      if (q < Q) {
+        const int PR = pr0 + q / W2, col = q % W2;
+        const int n = PR / H2, ih = PR % H2 - 1, iw = col - 1;
+        if (ih >= 0 && ih < H && iw >= 0 && iw < W && n < N) off = ((n * H + ih) * W + iw) * Ci + chk64(q, p) * 8;
+      }
+      hoff[i] = off;
+    }
+#pragma unroll
+    for (int j = 0; j < Cf::kBIns; ++j) {
+      const int r = (l * Cf::kBIns + j) * 16 + sub;  // [tap][co] row
+      const int t = r / BN, co = r % BN;
+      boff[j] = (n0 + co) * 9 * Ci + t * Ci + chk64(r, p) * 8;
+    }
+  }
+  auto dma_chunk = [&](int c) {
+    const int l = wid - 4;
+    char* buf = lds + (c & 1) * Cf::kBuf;
+#pragma unroll
+    for (int i = 0; i < Cf::kHIns; ++i) {
+      const uint16_t* src = hoff[i] >= 0 ? X + (hoff[i] + c * BK) : reinterpret_cast<const uint16_t*>(g_conv_zero);
+      dma16(src, buf + (l * Cf::kHIns + i) * 1024);
+    }
+#pragma unroll
+    for (int j = 0; j < Cf::kBIns; ++j) dma16(Wt + (boff[j] + c * BK), buf + Cf::kHaloBytes + (l * Cf::kBIns + j) * 1024);
+  };
+
+  // consumer state
+  const int lrow = lane & 15, lchk = lane >> 4;
+  int abase[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = min(m0 + wid * 64 + i * 16 + lrow, mlast);
+    const int n = m / HW, rem = m % HW, oh = rem / W, ow = rem % W;
+    abase[i] = (n * H2 + oh - pr0) * W2 + ow;
+  }
+  f4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+
+  if (loader) {
+    dma_chunk(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  for (int c = 0; c < nch; ++c) {
+    if (loader) {
+      if (c + 1 < nch) {
+        dma_chunk(c + 1);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    } else {
+      const char* hb = lds + (c & 1) * Cf::kBuf;
+      const char* bb = hb + Cf::kHaloBytes;
+      bf16x8 a[2][4], b[2][4];
+      auto rd = [&](int t, int set) {
+        const int toff = (t / 3) * W2 + (t % 3);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int q = abase[i] + toff;
+          a[set][i] = *reinterpret_cast<const bf16x8*>(hb + q * 64 + (chk64(q, lchk) << 4));
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int r = t * BN + j * 16 + lrow;
+          b[set][j] = *reinterpret_cast<const bf16x8*>(bb + r * 64 + (chk64(r, lchk) << 4));
+        }
+      };
+      rd(0, 0);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        if (t < 8) rd(t + 1, (t + 1) & 1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = mfma(b[t & 1][j], a[t & 1][i], acc[i][j]);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
+
+  if (!loader) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int ml = wid * 64 + i * 16 + lrow;
+        const int cl = j * 16 + 4 * lchk;
+        const f4 v = acc[i][j];
+        uint2 pk;
+        pk.x = (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)v[0]) |
+               ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)v[1]) << 16);
+        pk.y = (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)v[2]) |
+               ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)v[3]) << 16);
+        *reinterpret_cast<uint2*>(lds + ml * Cf::kEpiStride + cl * 2) = pk;
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  constexpr int kChunks = BN / 8;
+  for (int idx = tid; idx < BM * kChunks; idx += Cf::kThreads) {
+    const int r = idx / kChunks, cc = idx % kChunks;
+    const int m = m0 + r;
+    if (m < M)
+      *reinterpret_cast<uint4*>(Y + (int64_t)m * Co + n0 + cc * 8) =
+          *reinterpret_cast<const uint4*>(lds + r * Cf::kEpiStride + cc * 16);
+  }
+}
+
+// ---------------------------------------------------------------- weight-stationary persistent variant
+// For small filters (ResNet-50 layer 1: 64 -> 64 channels, 74 KB of bf16 weights) every variant
+// above spends as long on per-tile overhead as on MFMA work: a 256 x 64 tile is only 19 MFLOP, so
+// the first DMA's latency, the barriers and the epilogue of every tile sit on the critical path
+// (all of them ran layer 1 at 0.45 PF). Here the weights are loaded into LDS ONCE per workgroup,
+// one workgroup per CU walks a contiguous range of pixel tiles, and the 32-channel halo chunks of
+// consecutive tiles stream through two LDS buffers without a break: loader waves DMA pair k+1
+// (tile, chunk) while the consumers compute pair k, and a tile's results go straight from the
+// accumulators to HBM (8-B stores, no LDS round trip) while the next tile's halo is landing.
+template <int CI_, int CO_>
+struct SCfg {
+  static constexpr int BM = 256, BK = 32, CI = CI_, CO = CO_, NL = 4;
+  static constexpr int kThreads = (4 + NL) * 64;
+  static constexpr int kHaloRows = 640, kHaloBytes = kHaloRows * 64;  // W=56 tiles crossing an image: 580
+  static constexpr int kNch = CI / BK;
+  static constexpr int kWRows = kNch * 9 * CO;  // [chunk][tap][co] rows of 64 B
+  static constexpr int kWBytes = kWRows * 64;
+  static constexpr int kLds = kWBytes + 2 * kHaloBytes;
+  static constexpr int kHIns = kHaloRows / 16 / NL;
+  static_assert(CO == 64, "4 consumer waves x 64 pixels x 64 channels");
+  static_assert(kWRows % (16 * (4 + NL)) == 0, "weight DMA split");
+  static_assert(kLds <= 160 * 1024, "LDS");
+};
+
+template <class Cf>
+__global__ __launch_bounds__(Cf::kThreads, 1) void conv3x3wst_kernel(const uint16_t* __restrict__ X,
+                                                                   const uint16_t* __restrict__ Wt,
+                                                                   uint16_t* __restrict__ Y, int N, int H, int W) {
+  constexpr int BM = Cf::BM, BK = Cf::BK, CI = Cf::CI, CO = Cf::CO, NCH = Cf::kNch;
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  char* const wlds = lds;
+  char* const halo0 = lds + Cf::kWBytes;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const bool loader = wid >= 4;
+  const int HW = H * W, M = N * HW, W2 = W + 2, H2 = H + 2;
+  const int ntile = (M + BM - 1) / BM;
+  // contiguous tile range per workgroup: neighbouring tiles share halo rows (L2 hits)
+  const int g = gridDim.x, b = blockIdx.x;
+  const int t_begin = (int)((int64_t)ntile * b / g), t_end = (int)((int64_t)ntile * (b + 1) / g);
+  const int K = (t_end - t_begin) * NCH;  // (tile, chunk) pairs of this workgroup
+  const int sub = lane >> 2, p = lane & 3;
+
+  // weights: every wave DMAs its share once
+  {
+    constexpr int kIns = Cf::kWRows / 16 / (4 + Cf::NL);
+#pragma unroll
+    for (int i = 0; i < kIns; ++i) {
+      const int r = (wid * kIns + i) * 16 + sub;  // [c][t][co]
+      const int c = r / (9 * CO), t = (r / CO) % 9, co = r % CO;
+      dma16(Wt + (co * 9 + t) * CI + c * BK + chk64(r, p) * 8, wlds + (wid * kIns + i) * 1024);
+    }
+  }
+  auto tile_geo = [&](int tl, int& m0, int& mlast, int& pr0, int& Q) {
+    m0 = tl * BM;
+    mlast = min(m0 + BM, M) - 1;
+    pr0 = (m0 / HW) * H2 + (m0 % HW) / W;
+    Q = ((mlast / HW) * H2 + (mlast % HW) / W + 2 - pr0 + 1) * W2;
+  };
+  auto dma_halo = [&](int k) {
+    const int tl = t_begin + k / NCH, c = k % NCH;
+    int m0, mlast, pr0, Q;
+    tile_geo(tl, m0, mlast, pr0, Q);
+    const int l = wid - 4;
+    char* hb = halo0 + (k & 1) * Cf::kHaloBytes;
+#pragma unroll
+    for (int i = 0; i < Cf::kHIns; ++i) {
+      const int q = (l * Cf::kHIns + i) * 16 + sub;
+      const uint16_t* src = reinterpret_cast<const uint16_t*>(g_conv_zero);
+      if (q < Q) {
+        const int PR = pr0 + q / W2, col = q % W2;
+        const int n = PR / H2, ih = PR % H2 - 1, iw = col - 1;
+        if (ih >= 0 && ih < H && iw >= 0 && iw < W && n < N)
+          src = X + (((n * H + ih) * W + iw) * CI + c * BK + chk64(q, p) * 8);
+      }
+      dma16(src, hb + (l * Cf::kHIns + i) * 1024);
+    }
+  };
+
+  const int lrow = lane & 15, lchk = lane >> 4;
+  f4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  int abase[4];
+  int cur_m0 = 0, cur_mlast = -1;
+
+  if (loader && K > 0) dma_halo(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  for (int k = 0; k < K; ++k) {
+    if (loader) {
+      if (k + 1 < K) {
+        dma_halo(k + 1);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    } else {
+      const int tl = t_begin + k / NCH, c = k % NCH;
+      if (c == 0) {  // new tile: fragment row bases
+        int pr0, Q;
+        tile_geo(tl, cur_m0, cur_mlast, pr0, Q);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int m = min(cur_m0 + wid * 64 + i * 16 + lrow, cur_mlast);
+          const int n = m / HW, rem = m % HW, oh = rem / W, ow = rem % W;
+          abase[i] = (n * H2 + oh - pr0) * W2 + ow;
+        }
+      }
+      const char* hb = halo0 + (k & 1) * Cf::kHaloBytes;
+      const char* wb = wlds + c * 9 * CO * 64;
+      bf16x8 a[2][4], bq[2][4];
+      auto rd = [&](int t, int set) {
+        const int toff = (t / 3) * W2 + (t % 3);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int q = abase[i] + toff;
+          a[set][i] = *reinterpret_cast<const bf16x8*>(hb + q * 64 + (chk64(q, lchk) << 4));
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int r = c * 9 * CO + t * CO + j * 16 + lrow;
+          bq[set][j] = *reinterpret_cast<const bf16x8*>(wlds + r * 64 + (chk64(r, lchk) << 4));
+        }
+      };
+      (void)wb;
+      rd(0, 0);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        if (t < 8) rd(t + 1, (t + 1) & 1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = mfma(bq[t & 1][j], a[t & 1][i], acc[i][j]);
+      }
+      if (c == NCH - 1) {  // tile done: accumulators straight to HBM (4 channels = 8 B per lane)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int m = cur_m0 + wid * 64 + i * 16 + lrow;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const f4 v = acc[i][j];
+            if (m <= cur_mlast) {
+              uint2 pk;
+              pk.x = (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)v[0]) |
+                     ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)v[1]) << 16);
+              pk.y = (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)v[2]) |
+                     ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)v[3]) << 16);
+              *reinterpret_cast<uint2*>(Y + (int64_t)m * CO + j * 16 + 4 * lchk) = pk;
+            }
+            acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+          }
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
+}
+
+// Upper bound of the padded-halo rows of a 256-pixel tile (kernel's Q).
+inline int64_t halo_rows_bound(int H, int W, int BM) {
+  const int64_t rows = (BM - 1) / W + 2;                    // output rows a tile can touch
+  const int64_t imgs = rows <= H ? 2 : (rows - 1) / H + 2;  // images those rows can span
+  return (rows + 2 * imgs) * (W + 2);
+}
+
+template <class Cf>
+int launch_h(const uint16_t* x, const uint16_t* w, uint16_t* y, int N, int H, int W, int Ci, int Co, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3h_kernel<Cf>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, Cf::kLds) != hipSuccess)
+      return -3;
+    attr = true;
+  }
+  if (Ci % Cf::BK != 0 || Co % Cf::BN != 0) return -1;
+  if (halo_rows_bound(H, W, Cf::BM) > Cf::kHaloRows) return -4;
+  const int64_t M = (int64_t)N * H * W;
+  const int64_t grid = (M + Cf::BM - 1) / Cf::BM * (Co / Cf::BN);
+  hipLaunchKernelGGL(conv3x3h_kernel<Cf>, dim3((unsigned)grid), dim3(Cf::kThreads), Cf::kLds, s, x, w, y, N, H, W,
+                     Ci, Co);
+  return 0;
+}
+
+template <class Cf>
+int launch_ws(const uint16_t* x, const uint16_t* w, uint16_t* y, int N, int H, int W, int Ci, int Co, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3ws_kernel<Cf>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, Cf::kLds) != hipSuccess)
+      return -3;
+    attr = true;
+  }
+  if (Ci % Cf::BK != 0 || Co % Cf::BN != 0) return -1;
+  if (halo_rows_bound(H, W, Cf::BM) > Cf::kHaloRows) return -4;
+  const int64_t M = (int64_t)N * H * W;
+  const int64_t grid = (M + Cf::BM - 1) / Cf::BM * (Co / Cf::BN);
+  hipLaunchKernelGGL(conv3x3ws_kernel<Cf>, dim3((unsigned)grid), dim3(Cf::kThreads), Cf::kLds, s, x, w, y, N, H, W,
+                     Ci, Co);
+  return 0;
+}
+
+template <class Cf>
+int launch_wst(const uint16_t* x, const uint16_t* w, uint16_t* y, int N, int H, int W, int Ci, int Co, hipStream_t s) {
+  static bool attr = false;
+  static int ncu = 0;
+  if (!attr) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3wst_kernel<Cf>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, Cf::kLds) != hipSuccess)
+      return -3;
+    int dev = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    attr = true;
+  }
+  if (Ci != Cf::CI || Co != Cf::CO) return -1;
+  if (halo_rows_bound(H, W, Cf::BM) > Cf::kHaloRows) return -4;
+  const int64_t M = (int64_t)N * H * W;
+  const int64_t ntile = (M + Cf::BM - 1) / Cf::BM;
+  const int grid = (int)(ntile < ncu ? ntile : ncu);
+  hipLaunchKernelGGL(conv3x3wst_kernel<Cf>, dim3(grid), dim3(Cf::kThreads), Cf::kLds, s, x, w, y, N, H, W);
+  return 0;
+}
+
+using HWide = HCfg<128, 4, 2>;   // 8 waves of 64x64
+using HNarrow = HCfg<64, 4, 1>;  // 4 waves of 64x64
+
+// Wt'[ci][t][co] = Wt[co][8 - t][ci]: the data gradient of a stride-1 pad-1 3x3 conv is a
+// stride-1 pad-1 3x3 conv of dY with these weights.
+__global__ void conv3x3_flip_kernel(const uint16_t* __restrict__ w, uint16_t* __restrict__ wf, int Co, int Ci) {
+  const int64_t n = (int64_t)Co * 9 * Ci;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int ci = (int)(i / (9 * Co));
+    const int rem = (int)(i % (9 * Co));
+    const int t = rem / Co, co = rem % Co;
+    wf[i] = w[((int64_t)co * 9 + (8 - t)) * Ci + ci];
+  }
+}
+
+template <class Cf>
+int launch(const uint16_t* x, const uint16_t* w, uint16_t* y, int N, int H, int W, int Ci, int Co, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3s1_kernel<Cf>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, Cf::kLds) != hipSuccess)
+      return -3;
+    attr = true;
+  }
+  if (Ci % Cf::BK != 0 || Co % Cf::BN != 0) return -1;
+  const int64_t M = (int64_t)N * H * W;
+  const int64_t grid = (M + Cf::BM - 1) / Cf::BM * (Co / Cf::BN);
+  hipLaunchKernelGGL(conv3x3s1_kernel<Cf>, dim3((unsigned)grid), dim3(Cf::kThreads), Cf::kLds, s, x, w, y, N, H, W,
+                     Ci, Co);
+  return 0;
+}
+
+using CfWide = Cfg<256, 128, 4, 2, 32>;   // Co % 128 == 0: 8 waves of 64x64, 72 KB LDS -> 2 WG/CU
+using CfNarrow = Cfg<256, 64, 4, 1, 32>;  // Co == 64: 4 waves of 64x64, 60 KB LDS
+
+}  // namespace
+
+extern "C" {
+
+// y[N,H,W,Co] = conv3x3(x[N,H,W,Ci], w[Co,3,3,Ci]), stride 1, padding 1 (all NHWC / channels_last
+// bf16). Ci % 64 == 0, Co % 64 == 0, N*H*W*max(Ci,Co) < 2^31. Returns 0 on success.
+int pdt_conv3x3s1_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int N, int H, int W, int Ci, int Co,
+                      hipStream_t s) {
+  if (Ci % 32 != 0 || Co % 64 != 0 || N < 1 || H < 1 || W < 1) return -1;
+  const int64_t M = (int64_t)N * H * W;
+  if (M * (Ci > Co ? Ci : Co) >= (int64_t)1 << 31 || (int64_t)Co * 9 * Ci >= (int64_t)1 << 31) return -2;
+#ifdef PDT_CONV_CFG_OVERRIDE
+  return PDT_CONV_LAUNCH<PDT_CONV_CFG_OVERRIDE>(x, w, y, N, H, W, Ci, Co, s);
+#endif
+  int rc = -1;
+  if (Ci == 64 && Co == 64) rc = launch_wst<SCfg<64, 64>>(x, w, y, N, H, W, Ci, Co, s);
+  if (rc == -1) rc = Co % 128 == 0 ? launch_h<HWide>(x, w, y, N, H, W, Ci, Co, s) : launch_h<HNarrow>(x, w, y, N, H, W, Ci, Co, s);
+  if (rc != -4) return rc;
+  // halo larger than the LDS buffer (tiny W): per-tap staging
+  if (Co % 128 == 0) return launch<CfWide>(x, w, y, N, H, W, Ci, Co, s);
+  return launch<CfNarrow>(x, w, y, N, H, W, Ci, Co, s);
+}
+
+// wf[Ci,3,3,Co] (the data-gradient weights) from w[Co,3,3,Ci].
+int pdt_conv3x3_flip_weights(const uint16_t* w, uint16_t* wf, int Co, int Ci, hipStream_t s) {
+  const int64_t n = (int64_t)Co * 9 * Ci;
+  const int grid = (int)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096);
+  hipLaunchKernelGGL(conv3x3_flip_kernel, dim3(grid), dim3(256), 0, s, w, wf, Co, Ci);
+  return 0;
+}
+
+}  // extern "C"

@@ -384,11 +384,54 @@ class _SplitConvFn(torch.autograd.Function):
         return dx, dw, None, None, None, None
 
 
+def _conv3x3_mode() -> str:
+    return os.environ.get("PDT_CONV3X3", "ours")
+
+
+class _Conv3x3Fn(torch.autograd.Function):
+    """Stride-1 pad-1 3x3 convolution on our MFMA implicit-GEMM kernels (csrc/kernels/conv3x3.hip):
+    forward = conv3x3s1(x, w); data gradient = the SAME kernel on dY with the weights flipped and
+    transposed (conv3x3_flip); weight gradient = MIOpen (optionally on the side stream)."""
+
+    @staticmethod
+    def forward(ctx, x, weight):
+        from ._native import native
+        ctx.save_for_backward(x, weight)
+        return native().conv3x3s1_fwd(x, weight)
+
+    @staticmethod
+    def backward(ctx, gy):
+        from ._native import native
+        x, weight = ctx.saved_tensors
+        gy = gy.contiguous(memory_format=torch.channels_last)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = native().conv3x3s1_fwd(gy, native().conv3x3_flip(weight))
+        if ctx.needs_input_grad[1]:
+            args = (gy, x, weight, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1)
+            wfn = lambda: torch.ops.aten.convolution_backward(*args, [False, True, False])[1]  # noqa: E731
+            dw = _on_side_stream(wfn, weight, gy, x) if _wgrad_stream_enabled() else wfn()
+        return dx, dw
+
+
+def conv3x3_eligible(conv: nn.Conv2d, x: torch.Tensor) -> bool:
+    """Our 3x3 kernel applies: stride 1, padding 1, no bias/groups/dilation, channels_last bf16 GPU
+    input with Ci % 64 == 0 and Co % 64 == 0 (the data gradient swaps them; ResNet-50: 13 of 16 3x3 convs)."""
+    return (conv.kernel_size == (3, 3) and conv.stride == (1, 1) and conv.padding == (1, 1)
+            and conv.dilation == (1, 1) and conv.groups == 1 and conv.bias is None and conv.padding_mode == "zeros"
+            and x.is_cuda and x.dim() == 4 and x.dtype == torch.bfloat16 and conv.weight.dtype == torch.bfloat16
+            and x.is_contiguous(memory_format=torch.channels_last) and x.shape[1] % 64 == 0
+            and conv.out_channels % 64 == 0 and _conv3x3_mode() == "ours" and not disabled())
+
+
 class SplitConv2d(nn.Conv2d):
-    """``nn.Conv2d`` (same parameters / state_dict) whose GPU training backward can issue the
-    weight gradient on a side stream to overlap the rest of backward (``PDT_WGRAD_STREAM=1``)."""
+    """``nn.Conv2d`` (same parameters / state_dict). On the GPU, stride-1 3x3 convolutions run on
+    our MFMA kernels (``_Conv3x3Fn``; ``PDT_CONV3X3=miopen`` switches back); the training backward
+    can issue the weight gradient on a side stream (``PDT_WGRAD_STREAM=1``)."""
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if conv3x3_eligible(self, x):
+            return _Conv3x3Fn.apply(x, self.weight)
         if (self.bias is None and x.is_cuda and self.padding_mode == "zeros" and torch.is_grad_enabled()
                 and self.weight.requires_grad and _wgrad_stream_enabled() and not disabled()):
             return _SplitConvFn.apply(x, self.weight, self.stride, self.padding, self.dilation, self.groups)

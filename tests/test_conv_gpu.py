@@ -138,3 +138,31 @@ def test_side_stream_weight_grads_match(monkeypatch, accumulate):
     noise = max(rel(flat[1], flat[0]), rel(flat[2], flat[0]))
     print("side-stream rel", rel(flat[3], flat[0]), "noise", noise)
     assert rel(flat[3], flat[0]) <= 4 * noise + 2e-3
+
+
+@pytest.mark.parametrize("N,C_in,C_out,H,W", [(2, 64, 64, 13, 11), (3, 64, 64, 56, 56), (2, 128, 128, 28, 28),
+                                              (4, 256, 256, 14, 14), (9, 512, 512, 7, 7), (2, 64, 192, 9, 5),
+                                              (1, 128, 64, 3, 3)])
+def test_conv3x3_ours_matches_fp32(monkeypatch, N, C_in, C_out, H, W):
+    """Our stride-1 3x3 MFMA kernels (weight-stationary for 64->64, halo implicit GEMM otherwise):
+    forward, data gradient (same kernel, flipped weights) and the weight gradient, against an fp32
+    PyTorch conv of the same bf16 inputs."""
+    from pytorch_distributed_training_example_amd.ops.conv import SplitConv2d, conv3x3_eligible
+    monkeypatch.setenv("PDT_CONV3X3", "ours")
+    torch.manual_seed(0)
+    m = SplitConv2d(C_in, C_out, 3, padding=1, bias=False).cuda().bfloat16().to(memory_format=torch.channels_last)
+    x = torch.randn(N, C_in, H, W, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    assert conv3x3_eligible(m, x)
+    x.requires_grad_(True)
+    y = m(x)
+    assert y.is_contiguous(memory_format=torch.channels_last) and y.shape == (N, C_out, H, W)
+    gy = torch.randn_like(y)
+    y.backward(gy)
+    xr = x.detach().float().requires_grad_(True)
+    wr = m.weight.detach().float().requires_grad_(True)
+    yr = F.conv2d(xr, wr, padding=1)
+    yr.backward(gy.float())
+    for a, b in ((y, yr), (x.grad, xr.grad), (m.weight.grad, wr.grad)):
+        err = ((a.float() - b).norm() / b.norm()).item()
+        assert err < 1e-2, err
+    torch.testing.assert_close(y.float(), yr, rtol=3e-2, atol=3e-2 * yr.abs().max().item() ** 0.5)
