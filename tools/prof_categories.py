@@ -1,0 +1,35 @@
+"""Group a prof_window.py *_kernels.csv by kernel family (ms per step)."""
+import csv
+import sys
+
+
+def family(n):
+    if "bn_" in n or "maxpool" in n:
+        return "our BN (+ReLU/residual/pool)"
+    if "conv3x3" in n:
+        return "our 3x3 conv (MFMA)"
+    if "Cijk" in n:
+        return "hipBLASLt GEMM (1x1 convs, fc)"
+    if any(s in n for s in ("igemm", "ck::", "_ZN2ck", "naive_conv", "SubTensor", "fillBuffer", "ranspose")):
+        return "MIOpen conv (+fills)"
+    if any(s in n for s in ("ce_", "mt_kernel", "sgd", "strip", "colsum")):
+        return "our CE / optimizer"
+    return "other"
+
+
+rows = list(csv.DictReader(open(sys.argv[1])))
+steps = float(sys.argv[2]) if len(sys.argv) > 2 else 5.0
+cat = {}
+other = []
+for r in rows:
+    ms = float(r["TotalDurationNs"]) / 1e6 / steps
+    f = family(r["Name"])
+    cat[f] = cat.get(f, 0.0) + ms
+    if f == "other":
+        other.append((ms, r["Name"][:80]))
+print("| family | ms/step |\n|---|---:|")
+for k, v in sorted(cat.items(), key=lambda x: -x[1]):
+    print(f"| {k} | {v:.2f} |")
+print(f"| total busy | {sum(cat.values()):.2f} |")
+for ms, n in sorted(other, reverse=True)[:8]:
+    print(f"  other: {ms:.3f} {n}", file=sys.stderr)
