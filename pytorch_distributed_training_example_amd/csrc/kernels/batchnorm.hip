@@ -586,7 +586,10 @@ __global__ void bn_eval_coef_kernel(int C, const float* __restrict__ gamma, cons
   b_out[c] = bt - rm[c] * gm * invstd;
 }
 
-template <bool RELU, bool RES, bool MASK>
+// Apply passes: grid-stride over 16-B vectors (8 workgroups of 256 per CU), U vectors per thread
+// per iteration with all loads issued first. U = 1 is used: U = 4 (apply) / 2 (backward) measured
+// 5-10 % SLOWER on the ResNet-50 shapes (tools/bn_trace.py, 822 MB: 350 vs 318 us, 520 vs 469 us).
+template <bool RELU, bool RES, bool MASK, int U>
 __global__ __launch_bounds__(256) void bn_apply_kernel(
     const uint16_t* __restrict__ x, const uint16_t* __restrict__ res, const float* __restrict__ a,
     const float* __restrict__ b, uint16_t* __restrict__ y, uint8_t* __restrict__ mask, int64_t nvec, int C,
@@ -594,38 +597,51 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   float av[8], bv[8];
-  if (fixed && i < nvec) {
+  if (fixed && i < nvec) {  // stride % (C/8) == 0: every vector of this thread has the same channels
     const int c = (int)((i * 8) % C);
     ld8_f32(a + c, av);
     ld8_f32(b + c, bv);
   }
-  for (; i < nvec; i += stride) {
-    if (!fixed) {
-      const int c = (int)((i * 8) % C);
-      ld8_f32(a + c, av);
-      ld8_f32(b + c, bv);
-    }
-    float v[8];
-    ld8_bf16(x + i * 8, v);
-    float rv[8];
-    if (RES) ld8_bf16(res + i * 8, rv);
-    unsigned mb = 0;
+  for (; i < nvec; i += U * stride) {
+    uint4 xv[U], rv[U];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float t = v[j] * av[j] + bv[j];
-      if (RES) t += rv[j];
-      if (RELU) {
-        mb |= (t > 0.f ? 1u : 0u) << j;
-        t = t > 0.f ? t : 0.f;
+    for (int u = 0; u < U; ++u) {
+      const int64_t k = i + u * stride;
+      if (k < nvec) {
+        xv[u] = *reinterpret_cast<const uint4*>(x + k * 8);
+        if (RES) rv[u] = *reinterpret_cast<const uint4*>(res + k * 8);
       }
-      v[j] = t;
     }
-    st8_bf16(y + i * 8, v);
-    if (MASK) mask[i] = (uint8_t)mb;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t k = i + u * stride;
+      if (k >= nvec) break;
+      if (!fixed) {
+        const int c = (int)((k * 8) % C);
+        ld8_f32(a + c, av);
+        ld8_f32(b + c, bv);
+      }
+      float v[8], r[8];
+      unpack8(xv[u], v);
+      if (RES) unpack8(rv[u], r);
+      unsigned mb = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float t = v[j] * av[j] + bv[j];
+        if (RES) t += r[j];
+        if (RELU) {
+          mb |= (t > 0.f ? 1u : 0u) << j;
+          t = t > 0.f ? t : 0.f;
+        }
+        v[j] = t;
+      }
+      st8_bf16(y + k * 8, v);
+      if (MASK) mask[k] = (uint8_t)mb;
+    }
   }
 }
 
-template <bool RELU, bool RES>
+template <bool RELU, bool RES, int U>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x, const uint8_t* __restrict__ mask,
     const float* __restrict__ mean, const float* __restrict__ A, const float* __restrict__ B,
@@ -642,21 +658,36 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     ld8_f32(D + c, dv);
   };
   if (fixed && i < nvec) load_coef(i);
-  for (; i < nvec; i += stride) {
-    if (!fixed) load_coef(i);
-    float g[8], xv[8];
-    ld8_bf16(dy + i * 8, g);
-    ld8_bf16(x + i * 8, xv);
-    if (RELU) {
-      const unsigned mb = mask[i];
+  for (; i < nvec; i += U * stride) {
+    uint4 gv[U], xv[U];
+    unsigned mk[U];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) g[j] = (mb >> j) & 1u ? g[j] : 0.f;
+    for (int u = 0; u < U; ++u) {
+      const int64_t k = i + u * stride;
+      if (k < nvec) {
+        gv[u] = *reinterpret_cast<const uint4*>(dy + k * 8);
+        xv[u] = *reinterpret_cast<const uint4*>(x + k * 8);
+        if (RELU) mk[u] = mask[k];
+      }
     }
-    if (RES) st8_bf16(dres + i * 8, g);
-    float o[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = av[j] * g[j] + bv[j] * (xv[j] - mv[j]) + dv[j];
-    st8_bf16(dx + i * 8, o);
+    for (int u = 0; u < U; ++u) {
+      const int64_t k = i + u * stride;
+      if (k >= nvec) break;
+      if (!fixed) load_coef(k);
+      float g[8], xf[8];
+      unpack8(gv[u], g);
+      unpack8(xv[u], xf);
+      if (RELU) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) g[j] = (mk[u] >> j) & 1u ? g[j] : 0.f;
+      }
+      if (RES) st8_bf16(dres + k * 8, g);
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = av[j] * g[j] + bv[j] * (xf[j] - mv[j]) + dv[j];
+      st8_bf16(dx + k * 8, o);
+    }
   }
 }
 
@@ -936,8 +967,8 @@ int pdt_bn_fwd_train(const uint16_t* x, const uint16_t* res, const float* gamma,
   const int fixed = (2048 % C) == 0;
   const int grid = apply_grid(nvec);
 #define PDT_APPLY(RL, RS, MK)                                                                                 \
-  hipLaunchKernelGGL((bn_apply_kernel<RL, RS, MK>), dim3(grid), dim3(256), 0, s, x, res, a, b, y, mask, nvec, \
-                     C, fixed)
+  hipLaunchKernelGGL((bn_apply_kernel<RL, RS, MK, 1>), dim3(grid), dim3(256), 0, s, x, res, a, b, y, mask, \
+                     nvec, C, fixed)
   const bool mk = mask != nullptr;
   if (relu && res) { if (mk) PDT_APPLY(true, true, true); else PDT_APPLY(true, true, false); }
   else if (relu) { if (mk) PDT_APPLY(true, false, true); else PDT_APPLY(true, false, false); }
@@ -1022,8 +1053,8 @@ int pdt_bn_bwd_train(const uint16_t* dy, const uint16_t* x, const uint8_t* mask,
   const int fixed = (2048 % C) == 0;
   const int grid = apply_grid(nvec);
 #define PDT_BAPPLY(RL, RS)                                                                                      \
-  hipLaunchKernelGGL((bn_bwd_apply_kernel<RL, RS>), dim3(grid), dim3(256), 0, s, dy, x, mask, mean, A, B, D, dx, \
-                     dres, nvec, C, fixed)
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<RL, RS, 1>), dim3(grid), dim3(256), 0, s, dy, x, mask, mean, A, B, D, \
+                     dx, dres, nvec, C, fixed)
   if (relu && has_res) PDT_BAPPLY(true, true);
   else if (relu) PDT_BAPPLY(true, false);
   else if (has_res) PDT_BAPPLY(false, true);
