@@ -146,10 +146,11 @@ def setup(args):
         make_miopen_capture_safe()
     from pytorch_distributed_training_example_amd.engine.miopen_cache import use_repo_miopen_cache
     use_repo_miopen_cache()  # persisted conv-algorithm find-db + kernel cache (after the solver switches)
-    # measured hipBLASLt/rocBLAS solution per GEMM shape (read-only table). Not for LeNet or
+    # measured hipBLASLt/rocBLAS solution per GEMM shape (read-only table). Not for LeNet or eager
     # micro-batched steps: TunableOp's per-call host lookup then costs more than the tuned kernels
-    # save (LeNet 177k -> 131k img/s; ViT 4 x 32 micro-batches 3,190 -> 2,999)
-    if args.impl == "ours" and args.model != "lenet" and args.grad_accum == 1:
+    # save (LeNet 177k -> 131k img/s; ViT 4 x 32 micro-batches 3,190 -> 2,999); a hipGraph replay
+    # pays the lookup once, at capture
+    if args.impl == "ours" and args.model != "lenet" and (args.grad_accum == 1 or args.graph):
         from pytorch_distributed_training_example_amd.engine.gemm_tuning import use_repo_gemm_tuning
         use_repo_gemm_tuning()
     return launcher.init_distributed(backend=args.backend or ("nccl" if torch.cuda.is_available() else "gloo"),
