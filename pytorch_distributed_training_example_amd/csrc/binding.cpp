@@ -73,6 +73,9 @@ int pdt_bn_relu_maxpool_fwd_train(const uint16_t* x, const float* gamma, const f
 int pdt_conv3x3s1_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int N, int H, int W, int Ci, int Co,
                       hipStream_t s);
 int pdt_conv3x3_flip_weights(const uint16_t* w, uint16_t* wf, int Co, int Ci, hipStream_t s);
+int64_t pdt_stem_conv_wprep_elems();
+int pdt_stem_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* wp, uint16_t* y, int N, int H, int W,
+                      hipStream_t s);
 int pdt_maxpool3s2_bwd(const uint16_t* dy, const uint8_t* code, uint16_t* dz, int N, int H, int W, int C,
                        hipStream_t s);
 int pdt_fp8_cast_transpose(const uint16_t* x, int64_t M, int64_t K, const float* scale, uint8_t* out,
@@ -446,6 +449,25 @@ Tensor conv3x3_flip(Tensor w) {
                                        reinterpret_cast<uint16_t*>(wf.data_ptr()), (int)Co, (int)Ci, stream()) == 0,
               "pdt_conv3x3_flip_weights failed");
   return wf;
+}
+
+// ----------------------------------------------------------------------------- 7x7/s2 stem conv (3 -> 64)
+// y = conv2d(x, w, stride=2, padding=3) for channels_last bf16 x [N,3,H,W] (W % 32 == 0) and w [64,3,7,7].
+Tensor stem_conv_fwd(Tensor x, Tensor w) {
+  check_nhwc_bf16(x, "x");
+  TORCH_CHECK(x.size(1) == 3 && x.size(3) % 32 == 0, "stem_conv: x [N, 3, H, W] with W % 32 == 0");
+  TORCH_CHECK(w.dim() == 4 && w.size(0) == 64 && w.size(1) == 3 && w.size(2) == 7 && w.size(3) == 7 &&
+              w.scalar_type() == at::kBFloat16, "stem_conv: weight [64, 3, 7, 7] bf16");
+  w = w.contiguous(at::MemoryFormat::ChannelsLast);
+  const int64_t N = x.size(0), H = x.size(2), W = x.size(3), OH = (H - 1) / 2 + 1, OW = W / 2;
+  auto wp = at::empty({pdt_stem_conv_wprep_elems()}, w.options());
+  auto y = at::empty({N, 64, OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const int rc = pdt_stem_conv_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                                   reinterpret_cast<const uint16_t*>(w.data_ptr()),
+                                   reinterpret_cast<uint16_t*>(wp.data_ptr()), reinterpret_cast<uint16_t*>(y.data_ptr()),
+                                   (int)N, (int)H, (int)W, stream());
+  TORCH_CHECK(rc == 0, "pdt_stem_conv_fwd failed: ", rc);
+  return y;
 }
 
 // ----------------------------------------------------------------------------- cross entropy
@@ -840,6 +862,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("maxpool3s2_bwd", &maxpool3s2_bwd);
   m.def("conv3x3s1_fwd", &conv3x3s1_fwd);
   m.def("conv3x3_flip", &conv3x3_flip);
+  m.def("stem_conv_fwd", &stem_conv_fwd);
   m.def("bn_bwd_train", &bn_bwd_train);
   m.def("ce_fwd", &ce_fwd);
   m.def("ce_bwd", &ce_bwd);

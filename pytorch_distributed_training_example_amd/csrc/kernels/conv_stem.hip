@@ -1,0 +1,273 @@
+// ResNet stem convolution: 7x7 / stride 2 / pad 3, 3 -> 64 channels, NHWC bf16 on MFMA (gfx950).
+//
+// Not in the reference (its CNN is LeNet, /root/reference/cnn.py:10-16); it serves the ResNet-50
+// north-star config, where this one layer writes the largest activation of the network
+// (512 x 112 x 112 x 64 bf16 = 822 MB) and MIOpen's igemm_fwd kernel took 716 us for it
+// (profiles/r2/steady_resnet50_ours.md) against a ~165 us HBM floor (154 MB read + 822 MB written).
+//
+// Three input channels make every generic implicit GEMM awkward (K = 147, rows of 6 bytes). Here
+// the input is padded to 4 channels IN LDS and the kernel width to 8 taps in the (prepped)
+// weights, so one k-step of v_mfma_f32_16x16x32_bf16 is one kernel row kh: 8 taps x 4 channels,
+// and a lane's 8 k values (2 taps x 4 channels) are 16 contiguous LDS bytes of 2 neighbouring
+// padded pixels. The 8th tap and 4th channel carry zero weights (and finite zero inputs).
+//
+//   * tile = 4 output rows x 112 output columns of one image, 256 threads: wave w computes
+//     output row w — 7 pixel blocks x 4 channel blocks of 16x16 accumulators (112 VGPRs);
+//   * persistent, 2 workgroups per CU (each a contiguous run of tiles) that drift out of phase,
+//     so one's MFMAs overlap the other's loads, stores and barriers: the prepped weights
+//     (64 x 7 x 32 bf16, 28 KB) are staged to LDS once; each tile's input window (13 rows x 230
+//     columns x 4 channels, 25.6 KB) is loaded into registers after this tile's MFMAs, lands
+//     while its stores drain, and replaces the window after a barrier; 7 k-steps of 28 MFMAs
+//     per wave per tile. (One 8-wave workgroup per CU with two window buffers ran 277 us: its
+//     waves move through the phases in lock step.)
+//   * MFMA operands swapped (A = weights, B = pixels): a lane's accumulator is 4 consecutive
+//     channels of one pixel; each 16-pixel block goes through a wave-private LDS staging block
+//     and out as 16-B pieces, 1 KB contiguous per store instruction. Storing the accumulators
+//     directly (8 B per lane, 16 cache lines per instruction) ran the kernel at 2.6 TB/s — the
+//     no-store probe took 165 us of its 380;
+//   * the kernel is HBM-store bound, not MFMA bound (28 MFMAs per 16 x 64 outputs); a first
+//     non-persistent version (4-row tiles, 3 workgroups per CU, weights re-staged and the window
+//     loaded then waited on per tile) ran 384 us at batch 512 vs MIOpen's 860 us.
+#include "../common.h"
+
+#include <algorithm>
+
+using namespace pdt;
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+constexpr int kCo = 64;
+constexpr int kThreads = 256;                 // 4 waves
+constexpr int kRowsOut = kThreads / 64;       // output rows per workgroup (one per wave)
+constexpr int kTW = 112;                      // output columns per workgroup
+constexpr int kMB = kTW / 16;                 // 16-pixel blocks per wave
+constexpr int kInRows = 2 * kRowsOut + 5;     // 13 input rows
+constexpr int kInCols = 2 * kTW + 6;          // 230 (column 229 only meets the zero 8th tap)
+// LDS pixel column c at byte 8c + 16 (c >> 5): the 16-B pad per 32 pixels spreads the window
+// writes (8 pixels per lane, 64 B apart across lanes: 16-way bank conflicts unpadded, measured
+// as half of all LDS cycles) over all banks, and keeps the fragment reads (pixel pairs) aligned
+// and conflict-free.
+__host__ __device__ constexpr int pix_off(int c) { return 8 * c + 16 * (c >> 5); }
+constexpr int kInPitch = pix_off(kInCols) + 16;  // 1,968 B
+constexpr int kGroups = 30;                   // 8-pixel global load groups per input row
+constexpr int kWRow = 7 * 64;                 // [kh 7][kw 8][ci 4] bf16
+constexpr int kWPitch = kWRow + 16;           // +16 B: conflict-free 16-row fragment reads
+constexpr int kLdsIn = kInRows * kInPitch;    // 25,584 B
+constexpr int kStPitch = kCo * 2 + 16;        // epilogue staging row (one pixel), +16 B vs bank conflicts
+constexpr int kStage = 16 * kStPitch;         // per wave: one 16-pixel block
+constexpr int kLds = kLdsIn + kCo * kWPitch + kRowsOut * kStage;  // 64,496 B: window, weights, staging
+constexpr int kWPrepElems = kCo * 7 * 32;
+
+__device__ __forceinline__ f4 mfma(bf16x8 a, bf16x8 b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ uint32_t pk2(float a, float b) {
+  return (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)a) | ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)b) << 16);
+}
+
+// w: [64][7][7][3] (channels_last storage of [64, 3, 7, 7]) -> wp: [64][7][8][4], zero-padded.
+__global__ __launch_bounds__(256) void stem_wprep_kernel(const uint16_t* __restrict__ w, uint16_t* __restrict__ wp) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= kWPrepElems) return;
+  const int co = i / 224, r = i % 224, kh = r / 32, k = r % 32, kw = k >> 2, ci = k & 3;
+  wp[i] = (kw < 7 && ci < 3) ? w[((co * 7 + kh) * 7 + kw) * 3 + ci] : (uint16_t)0;
+}
+
+// One tile's input window -> registers: 13 rows x 30 groups of 8 pixels (48 B, 16-B aligned since
+// W % 8 == 0), at most 2 groups per thread; out-of-image groups are zeros.
+struct Window {
+  uint4 v[2][3];
+};
+
+__device__ __forceinline__ void load_window(Window& wv, const uint16_t* __restrict__ X, int tid, int n, int ih0,
+                                            int gb, int H, int W) {
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int i = tid + u * kThreads;
+    const int r = i / kGroups, g = i - r * kGroups;
+    const int ih = ih0 + r, iw = gb + 8 * g;
+    wv.v[u][0] = wv.v[u][1] = wv.v[u][2] = make_uint4(0u, 0u, 0u, 0u);
+    if (i < kInRows * kGroups && ih >= 0 && ih < H && iw >= 0 && iw < W) {
+      const uint4* src = reinterpret_cast<const uint4*>(X + ((int64_t)(n * H + ih) * W + iw) * 3);
+      wv.v[u][0] = src[0];
+      wv.v[u][1] = src[1];
+      wv.v[u][2] = src[2];
+    }
+  }
+}
+
+// 24 bf16 = 8 pixels x (c0 c1 c2) -> 8 LDS pixels of (c0 c1 c2 0) at LDS columns 8g - 5 + q.
+__device__ __forceinline__ void store_window(const Window& wv, char* lin, int tid) {
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int i = tid + u * kThreads;
+    if (i >= kInRows * kGroups) continue;
+    const int r = i / kGroups, g = i - r * kGroups;
+    const uint32_t w[12] = {wv.v[u][0].x, wv.v[u][0].y, wv.v[u][0].z, wv.v[u][0].w, wv.v[u][1].x, wv.v[u][1].y,
+                            wv.v[u][1].z, wv.v[u][1].w, wv.v[u][2].x, wv.v[u][2].y, wv.v[u][2].z, wv.v[u][2].w};
+    char* row = lin + r * kInPitch;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int e = 3 * q;  // bf16 index of channel 0
+      const uint32_t c0 = (w[e >> 1] >> ((e & 1) * 16)) & 0xffffu;
+      const uint32_t c1 = (w[(e + 1) >> 1] >> (((e + 1) & 1) * 16)) & 0xffffu;
+      const uint32_t c2 = (w[(e + 2) >> 1] >> (((e + 2) & 1) * 16)) & 0xffffu;
+      const int col = 8 * g - 5 + q;
+      if (col >= 0 && col < kInCols) *reinterpret_cast<uint2*>(row + pix_off(col)) = make_uint2(c0 | (c1 << 16), c2);
+    }
+  }
+}
+
+// Persistent: workgroup b owns a contiguous range of tiles (n, row tile, column tile), column
+// tile fastest; the weights are staged once, and the next tile's input window is loaded into
+// registers while this tile's MFMAs run (two LDS window buffers, one barrier per tile).
+// Requires W % 32 == 0 (OW = W / 2 a multiple of 16; load groups never straddle the image edge).
+#ifndef PDT_STEM_PROBE
+#define PDT_STEM_PROBE 0  // diagnostics only (tools/convbench/stem_bench.cpp): 1 = no Y stores, 2 = no MFMA, 3 = no window loads
+#endif
+template <bool FULL>  // FULL: every column tile is 112 wide (OW % 112 == 0): no per-block predicates
+__global__ __launch_bounds__(kThreads, 2) void stem_conv_kernel(const uint16_t* __restrict__ X,
+                                                          const uint16_t* __restrict__ Wp,
+                                                          uint16_t* __restrict__ Y, int H, int W, int OH, int OW,
+                                                          int nrt, int nct, int ntiles) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  char* const lw = lds + kLdsIn;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int per = ntiles / gridDim.x, rem = ntiles % gridDim.x;
+  const int t0 = blockIdx.x * per + min((int)blockIdx.x, rem);
+  const int cnt = per + ((int)blockIdx.x < rem ? 1 : 0);
+  if (cnt == 0) return;
+
+  auto coords = [&](int t, int& n, int& oh0, int& ow0) {
+    const int ct = t % nct, rt = (t / nct) % nrt;
+    n = t / (nct * nrt);
+    oh0 = rt * kRowsOut;
+    ow0 = ct * kTW;
+  };
+
+  // ---- weights (once): 64 rows x 28 16-B pieces
+  for (int i = tid; i < kCo * 28; i += kThreads) {
+    const int co = i / 28, r = i - co * 28;
+    *reinterpret_cast<uint4*>(lw + co * kWPitch + r * 16) = reinterpret_cast<const uint4*>(Wp)[i];
+  }
+  Window wv;
+  int n, oh0, ow0;
+  coords(t0, n, oh0, ow0);
+  load_window(wv, X, tid, n, 2 * oh0 - 3, 2 * ow0 - 8, H, W);
+  store_window(wv, lds, tid);
+
+  const int pl = lane & 15, g = lane >> 4;
+  const char* wrow = lw + pl * kWPitch + g * 16;
+  char* const stage = lw + kCo * kWPitch + wid * kStage;
+  for (int k = 0; k < cnt; ++k) {
+    const int t = t0 + k;
+    coords(t, n, oh0, ow0);
+    __syncthreads();  // window k visible
+
+    const char* lin = lds;
+    const int nb = min(kMB, (OW - ow0) >> 4);
+    f4 acc[kMB][4];
+#pragma unroll
+    for (int i = 0; i < kMB; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+    // pixel pair p = 16 i + pl + g (columns 2p, 2p + 1) at pix_off(2p) = 16 p + 16 (p >> 4)
+    const char* arow = lin + 2 * wid * kInPitch + 16 * (pl + g) + 16 * ((pl + g) >> 4);
+#pragma unroll
+    for (int kh = 0; kh < 7; ++kh) {
+      bf16x8 bw[4], av[kMB];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bw[j] = *reinterpret_cast<const bf16x8*>(wrow + j * 16 * kWPitch + kh * 64);
+#pragma unroll
+      for (int i = 0; i < kMB; ++i)  // past-the-edge blocks read in-window LDS and are never stored
+        av[i] = *reinterpret_cast<const bf16x8*>(arow + kh * kInPitch + i * 272);
+#pragma unroll
+      for (int i = 0; i < kMB; ++i) {
+        if (FULL || i < nb) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            if constexpr (PDT_STEM_PROBE == 2) acc[i][j] += f4{(float)av[i][j], (float)bw[j][i], 0.f, 0.f};
+            else acc[i][j] = mfma(bw[j], av[i], acc[i][j]);
+          }
+        }
+      }
+    }
+
+    // next window -> registers, issued before this tile's stores: the loads land while the stores
+    // drain (issued earlier, it made the compiler wait for the previous tile's stores — which
+    // share vmcnt and whose data registers the loads reuse — before the MFMAs)
+    if (PDT_STEM_PROBE != 3 && k + 1 < cnt) {
+      int n1, oh1, ow1;
+      coords(t + 1, n1, oh1, ow1);
+      load_window(wv, X, tid, n1, 2 * oh1 - 3, 2 * ow1 - 8, H, W);
+    }
+
+    // ---- epilogue: lane = pixel pl of each block, channels 16j + 4g .. +3 -> the wave's LDS
+    // staging block [16 px][64 ch] -> 16-B pieces, each store instruction 1 KB contiguous of Y
+    const int oh = oh0 + wid;
+    if (oh < OH) {
+      uint16_t* yrow = Y + ((int64_t)(n * OH + oh) * OW + ow0) * kCo;
+#pragma unroll
+      for (int i = 0; i < kMB; ++i) {
+        if (FULL || i < nb) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const f4 v = acc[i][j];
+            *reinterpret_cast<uint2*>(stage + pl * kStPitch + j * 32 + g * 8) =
+                make_uint2(pk2(v[0], v[1]), pk2(v[2], v[3]));
+          }
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {  // the wave's own LDS writes above complete in order first
+            const int idx = lane + 64 * h, px = idx >> 3, c = idx & 7;
+            const uint4 pv = *reinterpret_cast<const uint4*>(stage + px * kStPitch + c * 16);
+            if (PDT_STEM_PROBE == 1 && pv.x != 12345u) continue;
+            *reinterpret_cast<uint4*>(yrow + (int64_t)(i * 16 + px) * kCo + c * 8) = pv;
+          }
+        }
+      }
+    }
+    if (PDT_STEM_PROBE != 3 && k + 1 < cnt) {
+      __syncthreads();  // every wave is done reading window k
+      store_window(wv, lds, tid);
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int64_t pdt_stem_conv_wprep_elems() { return kWPrepElems; }
+
+// y[N, 64, OH, OW] (channels_last) = conv2d(x[N, 3, H, W] (channels_last), w[64, 3, 7, 7]
+// (channels_last storage [64][7][7][3]), stride 2, padding 3); wp: kWPrepElems bf16 scratch.
+extern "C" int pdt_stem_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* wp, uint16_t* y, int N, int H,
+                                 int W, hipStream_t s) {
+  if (N < 1 || H < 1 || W < 32 || W % 32 != 0) return -1;
+  const int OH = (H - 1) / 2 + 1, OW = W / 2;
+  static const bool attr_ok =
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_conv_kernel<true>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, kLds) == hipSuccess &&
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_conv_kernel<false>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, kLds) == hipSuccess;
+  if (!attr_ok) return -2;
+  static const int ncu = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 256;
+    return hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0 ? v : 256;
+  }();
+  const int nrt = (OH + kRowsOut - 1) / kRowsOut, nct = (OW + kTW - 1) / kTW;
+  const int64_t ntiles = (int64_t)N * nrt * nct;
+  if (ntiles > 0x7fffffff || (int64_t)N * H > 0x7fffffff / 4) return -3;
+  const int grid = (int)std::min<int64_t>(ntiles, 2 * ncu);  // 2 workgroups (61.4 KB LDS each) per CU: out of phase
+  hipLaunchKernelGGL(stem_wprep_kernel, dim3((kWPrepElems + 255) / 256), dim3(256), 0, s, w, wp);
+  if (OW % kTW == 0)
+    hipLaunchKernelGGL(stem_conv_kernel<true>, dim3(grid), dim3(kThreads), kLds, s, x, wp, y, H, W, OH, OW, nrt, nct,
+                       (int)ntiles);
+  else
+    hipLaunchKernelGGL(stem_conv_kernel<false>, dim3(grid), dim3(kThreads), kLds, s, x, wp, y, H, W, OH, OW, nrt, nct,
+                       (int)ntiles);
+  return hipGetLastError() == hipSuccess ? 0 : -4;
+}

@@ -424,14 +424,52 @@ def conv3x3_eligible(conv: nn.Conv2d, x: torch.Tensor) -> bool:
             and conv.out_channels % 64 == 0 and _conv3x3_mode() == "ours" and not disabled())
 
 
+class _StemConvFn(torch.autograd.Function):
+    """ResNet stem (7x7 / stride 2 / pad 3, 3 -> 64) forward on our MFMA kernel
+    (csrc/kernels/conv_stem.hip); gradients on MIOpen (the image needs none in training)."""
+
+    @staticmethod
+    def forward(ctx, x, weight):
+        from ._native import native
+        ctx.save_for_backward(x, weight)
+        return native().stem_conv_fwd(x, weight)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, weight = ctx.saved_tensors
+        gy = gy.contiguous(memory_format=torch.channels_last)
+        args = (gy, x, weight, None, [2, 2], [3, 3], [1, 1], False, [0, 0], 1)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.ops.aten.convolution_backward(*args, [True, False, False])[0]
+        if ctx.needs_input_grad[1]:
+            wfn = lambda: torch.ops.aten.convolution_backward(*args, [False, True, False])[1]  # noqa: E731
+            dw = _on_side_stream(wfn, weight, gy, x) if _wgrad_stream_enabled() else wfn()
+        return dx, dw
+
+
+def stem_eligible(conv: nn.Conv2d, x: torch.Tensor) -> bool:
+    """Our stem kernel applies: 7x7 / stride 2 / pad 3, 3 -> 64 channels, no bias, channels_last
+    bf16 GPU input with W % 32 == 0 (``PDT_CONV_STEM=miopen`` switches back)."""
+    return (conv.kernel_size == (7, 7) and conv.stride == (2, 2) and conv.padding == (3, 3)
+            and conv.dilation == (1, 1) and conv.groups == 1 and conv.bias is None and conv.padding_mode == "zeros"
+            and conv.in_channels == 3 and conv.out_channels == 64 and x.is_cuda and x.dim() == 4
+            and x.dtype == torch.bfloat16 and conv.weight.dtype == torch.bfloat16
+            and x.is_contiguous(memory_format=torch.channels_last) and x.shape[3] % 32 == 0
+            and os.environ.get("PDT_CONV_STEM", "ours") == "ours" and not disabled())
+
+
 class SplitConv2d(nn.Conv2d):
-    """``nn.Conv2d`` (same parameters / state_dict). On the GPU, stride-1 3x3 convolutions run on
-    our MFMA kernels (``_Conv3x3Fn``; ``PDT_CONV3X3=miopen`` switches back); the training backward
-    can issue the weight gradient on a side stream (``PDT_WGRAD_STREAM=1``)."""
+    """``nn.Conv2d`` (same parameters / state_dict). On the GPU, stride-1 3x3 convolutions and
+    the ResNet stem run on our MFMA kernels (``_Conv3x3Fn`` / ``_StemConvFn``;
+    ``PDT_CONV3X3=miopen`` / ``PDT_CONV_STEM=miopen`` switch back); the training backward can
+    issue the weight gradient on a side stream (``PDT_WGRAD_STREAM=1``)."""
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if conv3x3_eligible(self, x):
             return _Conv3x3Fn.apply(x, self.weight)
+        if stem_eligible(self, x):
+            return _StemConvFn.apply(x, self.weight)
         if (self.bias is None and x.is_cuda and self.padding_mode == "zeros" and torch.is_grad_enabled()
                 and self.weight.requires_grad and _wgrad_stream_enabled() and not disabled()):
             return _SplitConvFn.apply(x, self.weight, self.stride, self.padding, self.dilation, self.groups)

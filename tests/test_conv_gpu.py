@@ -166,3 +166,31 @@ def test_conv3x3_ours_matches_fp32(monkeypatch, N, C_in, C_out, H, W):
         err = ((a.float() - b).norm() / b.norm()).item()
         assert err < 1e-2, err
     torch.testing.assert_close(y.float(), yr, rtol=3e-2, atol=3e-2 * yr.abs().max().item() ** 0.5)
+
+
+@pytest.mark.parametrize("N,H,W", [(2, 224, 224), (3, 32, 64), (1, 17, 256), (2, 9, 32)])
+def test_stem_conv_ours_matches_fp32(monkeypatch, N, H, W):
+    """Our 7x7/s2 stem kernel (csrc/kernels/conv_stem.hip) against an fp32 PyTorch conv of the same
+    bf16 inputs: forward (odd H, several 112-column tiles and partial row tiles included) and the
+    MIOpen gradients behind it."""
+    from pytorch_distributed_training_example_amd.ops.conv import SplitConv2d, stem_eligible
+    monkeypatch.setenv("PDT_CONV_STEM", "ours")
+    torch.manual_seed(0)
+    m = SplitConv2d(3, 64, 7, stride=2, padding=3, bias=False).cuda().bfloat16().to(
+        memory_format=torch.channels_last)
+    x = (torch.randn(N, 3, H, W, device="cuda") + 0.5).bfloat16().contiguous(memory_format=torch.channels_last)
+    assert stem_eligible(m, x)
+    x.requires_grad_(True)
+    y = m(x)
+    assert y.is_contiguous(memory_format=torch.channels_last)
+    xr = x.detach().float().requires_grad_(True)
+    wr = m.weight.detach().float().requires_grad_(True)
+    yr = F.conv2d(xr, wr, stride=2, padding=3)
+    assert y.shape == yr.shape
+    gy = torch.randn_like(y)
+    y.backward(gy)
+    yr.backward(gy.float())
+    for a, b in ((y, yr), (x.grad, xr.grad), (m.weight.grad, wr.grad)):
+        err = ((a.float() - b).norm() / b.norm()).item()
+        assert err < 1e-2, err
+    torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=2e-2 * yr.abs().max().item() ** 0.5)
