@@ -750,6 +750,11 @@ __global__ __launch_bounds__(Cf::kThreads, 1) void conv3x3wst_kernel(const uint1
 // VALU-bound at 0.27-0.44 PF). Staging goes through registers: the next tile's global loads are
 // in flight while the current tile is computed. Per-split fp32 partials go to a workspace that
 // conv3x3_wgrad_reduce sums in a fixed order (deterministic).
+// Measured (tools/gpu_wgrad.sh, batch 512): 384/268/223/217 us at L1-L4, slower than MIOpen's
+// 284/~200 us; the MFMA-only probe (no staging) takes 230/141/123/117 us. A wave map with all 4
+// co blocks per wave (8 + 18 transposed reads per 36 MFMAs instead of 4 + 18 per 18) measured
+// the same in both, so LDS read bandwidth is not the limit; the register staging + 2 barriers
+// per 128-pixel tile are.
 struct GCfg {
   static constexpr int BM = 128, kThreads = 512;
   static constexpr int kPitch = 144;

@@ -1,12 +1,7 @@
 #!/bin/bash
-cd "${GRAFT_REPO_ROOT:-/root/repo}"
-export HSA_ENABLE_IPC_MODE_LEGACY=0
+# 3x3 weight-gradient kernel: correctness + timing (new wave map, old map, MFMA-only probe).
+set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 500 python -u -m pytest tests/test_conv_gpu.py tests/test_graph_gpu.py tests/test_models_gpu.py tests/test_profile_gate_gpu.py -q -x --timeout 200 --timeout-method thread > gpurun_out/wg_tests.log 2>&1; rc=$?
-tail -3 gpurun_out/wg_tests.log; [ $rc -eq 0 ] || exit $rc
-run() { n=$1; shift; timeout -k 10 500 python -u bench.py "$@" > gpurun_out/wg_$n.log 2>&1; rc=$?
-  echo "$n rc=$rc $(grep -o '"value": [0-9.]*' gpurun_out/wg_$n.log)"; [ $rc -ne 0 ] && tail -5 gpurun_out/wg_$n.log; return $rc; }
-run on --steps 20 --warmup 5 || exit 1
-PDT_WGRAD_STREAM=0 run off --steps 20 --warmup 5 || exit 1
-run on2 --steps 20 --warmup 5 || exit 1
-PDT_WGRAD_STREAM=0 run off2 --steps 20 --warmup 5 || exit 1
+WGRAD=1 timeout -k 10 120 tools/convbench/conv3x3_bench 20 2>&1 | tee gpurun_out/wgrad_new.log || exit 1
+WGRAD=1 timeout -k 10 120 tools/convbench/conv3x3_bench_c1 20 2>&1 | tee gpurun_out/wgrad_old.log || exit 1
+WGRAD=1 PROBE=1 timeout -k 10 120 tools/convbench/conv3x3_bench_p2 20 2>&1 | tee gpurun_out/wgrad_probe2.log
