@@ -76,6 +76,9 @@ int pdt_conv3x3_flip_weights(const uint16_t* w, uint16_t* wf, int Co, int Ci, hi
 int64_t pdt_stem_conv_wprep_elems();
 int pdt_stem_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* wp, uint16_t* y, int N, int H, int W,
                       hipStream_t s);
+int64_t pdt_stem_wgrad_ws_floats();
+int pdt_stem_conv_wgrad(const uint16_t* x, const uint16_t* dy, uint16_t* dw, float* ws, int N, int H, int W,
+                        hipStream_t s);
 int pdt_maxpool3s2_bwd(const uint16_t* dy, const uint8_t* code, uint16_t* dz, int N, int H, int W, int C,
                        hipStream_t s);
 int pdt_fp8_cast_transpose(const uint16_t* x, int64_t M, int64_t K, const float* scale, uint8_t* out,
@@ -468,6 +471,25 @@ Tensor stem_conv_fwd(Tensor x, Tensor w) {
                                    (int)N, (int)H, (int)W, stream());
   TORCH_CHECK(rc == 0, "pdt_stem_conv_fwd failed: ", rc);
   return y;
+}
+
+// Weight gradient of stem_conv_fwd: dw [64, 3, 7, 7] (channels_last) from x and dy [N, 64, OH, OW]
+// (channels_last); W % 32 == 0 and W <= 224.
+Tensor stem_conv_wgrad(Tensor x, Tensor dy) {
+  check_nhwc_bf16(x, "x");
+  check_nhwc_bf16(dy, "dy");
+  const int64_t N = x.size(0), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(x.size(1) == 3 && W % 32 == 0 && W <= 224, "stem_conv_wgrad: x [N, 3, H, W], W % 32 == 0, W <= 224");
+  TORCH_CHECK(dy.size(0) == N && dy.size(1) == 64 && dy.size(2) == (H - 1) / 2 + 1 && dy.size(3) == W / 2,
+              "stem_conv_wgrad: dy [N, 64, OH, OW]");
+  auto ws = at::empty({pdt_stem_wgrad_ws_floats()}, x.options().dtype(at::kFloat));
+  auto dw = at::empty({64, 3, 7, 7}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const int rc = pdt_stem_conv_wgrad(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                                     reinterpret_cast<const uint16_t*>(dy.data_ptr()),
+                                     reinterpret_cast<uint16_t*>(dw.data_ptr()), ws.data_ptr<float>(), (int)N, (int)H,
+                                     (int)W, stream());
+  TORCH_CHECK(rc == 0, "pdt_stem_conv_wgrad failed: ", rc);
+  return dw;
 }
 
 // ----------------------------------------------------------------------------- cross entropy
@@ -863,6 +885,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv3x3s1_fwd", &conv3x3s1_fwd);
   m.def("conv3x3_flip", &conv3x3_flip);
   m.def("stem_conv_fwd", &stem_conv_fwd);
+  m.def("stem_conv_wgrad", &stem_conv_wgrad);
   m.def("bn_bwd_train", &bn_bwd_train);
   m.def("ce_fwd", &ce_fwd);
   m.def("ce_bwd", &ce_bwd);

@@ -237,7 +237,244 @@ __global__ __launch_bounds__(kThreads, 2) void stem_conv_kernel(const uint16_t* 
   }
 }
 
+
+// ---------------------------------------------------------------- weight gradient
+//   dW[co, kh, kw, ci] = sum_px dY[px, co] * X[2 oh + kh - 3, 2 ow + kw - 3, ci]
+// MIOpen's kernel took 690 us for it at batch 512 (profiles/r2/steady_resnet50_ours.md); the work
+// is a GEMM [64 co] x [224 patch k] over K = 6.4M pixels, HBM-bound on reading dY (822 MB).
+// Both operands are pixel-major in memory and need pixels along the MFMA k dimension: fragments
+// come from transposed LDS reads (ds_read_b64_tr_b16: each lane names one pixel row, the 16 lanes
+// of a group receive one column of 4 pixels), as in conv3x3.hip's weight gradient.
+//   * tile = 2 output rows of one image (2 x OW <= 224 pixels = up to 7 k-steps of 32), 512
+//     threads: wave = k half (patch blocks 0-6 | 7-13) x pixel group (k-steps j with
+//     (j + tile) % 4 == group), 4 co blocks x 7 patch blocks = 28 accumulators;
+//   * dY tile (contiguous in NHWC: 2 full rows) arrives by LDS-DMA into a double buffer, rows
+//     XOR-swizzled on 16-B chunks by ((row >> 1) & 3) << 1 through the SOURCE address so the
+//     transposed reads of 8 consecutive rows hit distinct banks; the X window (9 rows, 3 -> 4
+//     channels) goes through registers like the forward's; one barrier per tile;
+//   * persistent, 1 workgroup per CU; the 4 pixel groups are summed through LDS at the end and
+//     each workgroup writes one fp32 partial, summed in a fixed order by stem_wgrad_reduce_kernel.
+constexpr int kGThreads = 512;
+constexpr int kGRowsOut = 2;
+constexpr int kGInRows = 2 * kGRowsOut + 5;  // 9
+// window column c <-> input column c - 4 (232 columns): input pixel PAIRS (12 B, 4-B aligned at an
+// even input column) go to 16-B aligned LDS pairs, so consecutive lanes write consecutive 16 B
+// (8 pixels per lane, 64 B apart across lanes, cost 16-way bank conflicts: 47% of LDS cycles)
+constexpr int kGCols = 232;
+constexpr int kGInPitch = kGCols * 8;  // unpadded: a patch half (4 pixels) is 32 contiguous B
+constexpr int kGMaxPx = kGRowsOut * kTW;     // 224
+constexpr int kGDy = kGMaxPx * 128;          // dY tile [224 px][64 co] bf16
+constexpr int kGBuf = kGDy + kGInRows * kGInPitch;
+constexpr int kGLds = 2 * kGBuf;             // 90,768 B
+constexpr int kGK = 7 * 32;                  // padded patch length (kh x kw 8 x ci 4)
+constexpr int kGPairs = kGCols / 2;
+constexpr int kGItems = kGInRows * kGPairs;  // 1,044 pixel pairs per window
+constexpr int kGRounds = (kGItems + kGThreads - 1) / kGThreads;
+
+__device__ __attribute__((aligned(256))) uint4 g_stem_zero[8];  // zero page for DMA of rows past OH
+
+// LDS-DMA (global_load_lds_dwordx4: lane i's 16 B land at M0 + 16 i) issued from inline asm: the
+// builtin form makes the compiler assume the DMA may alias every later LDS read and put a
+// vmcnt(0) in front of the next tile's fragment reads — i.e. wait for the prefetch it was meant
+// to overlap. Ordering is by the kernel's own counted vmcnt waits and barriers instead.
+__device__ __forceinline__ void dma16_opaque(const void* src, const char* lds_dst) {
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)lds_dst);
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(m0) : "memory");
+}
+
+typedef short s4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ bf16x8 tr8(const char* p0, const char* p1) {
+  const s4v a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4v*)p0);
+  const s4v b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4v*)p1);
+  typedef short s8 __attribute__((ext_vector_type(8)));
+  const s8 r = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  return __builtin_bit_cast(bf16x8, r);
+}
+
+#ifndef PDT_STEM_WG_PROBE
+#define PDT_STEM_WG_PROBE 0  // diagnostics only: 1 = staging without compute, 2 = compute without staging
+#endif
+__global__ __launch_bounds__(kGThreads, 1) void stem_wgrad_kernel(const uint16_t* __restrict__ X,
+                                                                  const uint16_t* __restrict__ dY,
+                                                                  float* __restrict__ ws, int H, int W, int OH,
+                                                                  int OW, int nrt, int ntiles) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int per = ntiles / gridDim.x, rem = ntiles % gridDim.x;
+  const int t0 = blockIdx.x * per + min((int)blockIdx.x, rem);
+  const int cnt = per + ((int)blockIdx.x < rem ? 1 : 0);
+  const int P = kGRowsOut * OW;  // pixels per tile (multiple of 32)
+  const int nks = P >> 5;
+
+  // ---- staging: dY tile by DMA (P/8 instructions of 8 rows; instruction q by wave q % 8)
+  auto dma_dy = [&](int t, char* buf) {
+    const int n = t / nrt, oh0 = (t - n * nrt) * kGRowsOut;
+    const uint16_t* src0 = dY + (int64_t)(n * OH + oh0) * OW * 64;
+    const int vrows = min(kGRowsOut, OH - oh0) * OW;  // valid pixel rows of the tile
+    for (int q = wid; q < (P >> 3); q += 8) {
+      const int r = q * 8 + (lane >> 3), pos = lane & 7;
+      const int chunk = pos ^ (((r >> 1) & 3) << 1);
+      const void* src = r < vrows ? (const void*)(src0 + (int64_t)r * 64 + chunk * 8) : (const void*)g_stem_zero;
+      dma16_opaque(src, buf + q * 1024);
+    }
+  };
+  uint3 xv[kGRounds];
+  bool xok[kGRounds];
+  auto load_x = [&](int t) {
+    const int n = t / nrt, oh0 = (t - n * nrt) * kGRowsOut;
+#pragma unroll
+    for (int u = 0; u < kGRounds; ++u) {
+      const int i = tid + u * kGThreads;
+      const int r = i / kGPairs, pp = i - r * kGPairs;
+      const int ih = 2 * oh0 - 3 + r, iw = 2 * pp - 4;  // even: a pair is all in or all out of the image
+      // clamped address, zeroed in store_x (the select here would wait for the load at once)
+      const bool ok = i < kGItems && ih >= 0 && ih < H && iw >= 0 && iw < W;
+      xv[u] = *reinterpret_cast<const uint3*>(X + (ok ? ((int64_t)(n * H + ih) * W + iw) * 3 : 0));
+      xok[u] = ok;
+    }
+  };
+  auto store_x = [&](char* win) {
+#pragma unroll
+    for (int u = 0; u < kGRounds; ++u) {
+      const int i = tid + u * kGThreads;
+      if (i >= kGItems) continue;
+      const int r = i / kGPairs, pp = i - r * kGPairs;
+      // (c0 c1 c2)(c0 c1 c2) -> (c0 c1 c2 0)(c0 c1 c2 0)
+      const uint3 w = xok[u] ? xv[u] : make_uint3(0u, 0u, 0u);
+      *reinterpret_cast<uint4*>(win + r * kGInPitch + pp * 16) =
+          make_uint4(w.x, w.y & 0xffffu, (w.y >> 16) | (w.z << 16), w.z >> 16);
+    }
+  };
+
+  // ---- per-lane fragment geometry: lane group g, row-in-group rsub, 8-B column piece csub
+  const int g = lane >> 4, li = lane & 15, rsub = li >> 2, csub = li & 3;
+  const int khalf = wid & 1, pgrp = wid >> 1;
+  const int sw = (((4 * g + rsub) >> 1) & 3) << 1;  // the dY swizzle of rows 4g + rsub (+16, +32k)
+  int dyo[4];
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb) dyo[cb] = (((2 * cb) ^ sw) | (csub >> 1)) * 16 + (csub & 1) * 8;
+
+  f4 acc[4][7];
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+    for (int b = 0; b < 7; ++b) acc[cb][b] = f4{0.f, 0.f, 0.f, 0.f};
+
+  // 2 buffers. Iteration k: load tile k+1's window into registers and DMA its dY (opaque: see
+  // dma16_opaque), compute tile k, write the window registers (the compiler's wait for them also
+  // retires the DMA issued after them), barrier.
+  if (cnt > 0) {
+    load_x(t0);
+    dma_dy(t0, lds);
+    store_x(lds + kGDy);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int k = 0; k < cnt; ++k) {
+    char* const buf = lds + (k & 1) * kGBuf;
+    char* const nbuf = lds + ((k + 1) & 1) * kGBuf;
+    if (PDT_STEM_WG_PROBE != 2 && k + 1 < cnt) {
+      load_x(t0 + k + 1);
+      dma_dy(t0 + k + 1, nbuf);
+    }
+    const char* win = buf + kGDy;
+    // this wave's k-steps of the tile: j0 and j0 + 4 (7 k-steps over 4 pixel groups); both
+    // steps' fragments are read before the first MFMA so the second batch of reads overlaps it
+    const int j0 = (pgrp - (t0 + k)) & 3;
+    const int nj = PDT_STEM_WG_PROBE == 1 ? 0 : (j0 < nks) + (j0 + 4 < nks);
+    bf16x8 a[2][4], bx[2][7];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (u < nj) {
+        const int r0 = (j0 + 4 * u) * 32 + 4 * g + rsub, r1 = r0 + 16;
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) a[u][cb] = tr8(buf + r0 * 128 + dyo[cb], buf + r1 * 128 + dyo[cb]);
+        // window address of pixel r: row 2 (r >= OW), column 2 (r mod OW) + 1, plus this lane's piece
+        const int h0 = r0 >= OW, h1 = r1 >= OW;
+        const char* x0 = win + 2 * h0 * kGInPitch + (2 * (r0 - h0 * OW) + csub + 1) * 8;
+        const char* x1 = win + 2 * h1 * kGInPitch + (2 * (r1 - h1 * OW) + csub + 1) * 8;
+#pragma unroll
+        for (int b = 0; b < 7; ++b) {
+          const int kb = 7 * khalf + b;
+          const int off = (kb >> 1) * kGInPitch + (kb & 1) * 32;
+          bx[u][b] = tr8(x0 + off, x1 + off);
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (u < nj) {
+#pragma unroll
+        for (int b = 0; b < 7; ++b)
+#pragma unroll
+          for (int cb = 0; cb < 4; ++cb) acc[cb][b] = mfma(a[u][cb], bx[u][b], acc[cb][b]);  // D[co][patch k]
+      }
+    }
+    if (PDT_STEM_WG_PROBE != 2 && k + 1 < cnt) store_x(nbuf + kGDy);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // tile k + 1 landed everywhere; everyone is done with tile k's buffer
+  }
+
+  // ---- pixel groups 1..3 -> LDS -> group 0 adds (one patch block column per round)
+  f4* red = reinterpret_cast<f4*>(lds);
+#pragma unroll
+  for (int b = 0; b < 7; ++b) {
+    if (pgrp != 0) {
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) red[(((pgrp - 1) * 2 + khalf) * 4 + cb) * 64 + lane] = acc[cb][b];
+    }
+    __syncthreads();
+    if (pgrp == 0) {
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) acc[cb][b] += red[((q * 2 + khalf) * 4 + cb) * 64 + lane];
+    }
+    __syncthreads();
+  }
+  if (pgrp != 0) return;
+  // partial [64 co][224 k]: lane holds D[co = 16 cb + 4 g + t][k = 16 kb + li]
+  float* wp = ws + (int64_t)blockIdx.x * 64 * kGK;
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+    for (int b = 0; b < 7; ++b)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) wp[(cb * 16 + 4 * g + t) * kGK + (7 * khalf + b) * 16 + li] = acc[cb][b][t];
+}
+
+// dw[co][kh][kw][ci] (bf16, the channels_last storage of [64, 3, 7, 7]) = sum of the partials in
+// workgroup order (deterministic), dropping the padded tap kw = 7 and channel ci = 3. Block b
+// sums columns [256 b, 256 b + 256) of the [64 x 224] partials: 4 partial subsets x 256 columns,
+// loads issued 16 at a time (a thread-per-column loop over 256 partials took 62 us in the step).
+__global__ __launch_bounds__(1024) void stem_wgrad_reduce_kernel(const float* __restrict__ ws, int nparts,
+                                                                 uint16_t* __restrict__ dw) {
+  __shared__ float sm[4][256];
+  const int tid = threadIdx.x, c = tid & 255, q = tid >> 8;
+  const int col = blockIdx.x * 256 + c;  // < 64 * 224 (grid = 56)
+  float a = 0.f;
+  for (int p0 = q; p0 < nparts; p0 += 4 * 16) {
+    float t[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int p = p0 + 4 * u;
+      t[u] = ws[(int64_t)(p < nparts ? p : q) * 64 * kGK + col];
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) a += (p0 + 4 * u < nparts) ? t[u] : 0.f;
+  }
+  sm[q][c] = a;
+  __syncthreads();
+  if (q != 0) return;
+  const float s = sm[0][c] + sm[1][c] + sm[2][c] + sm[3][c];
+  const int co = col / kGK, k = col - co * kGK, kh = k >> 5, kw = (k >> 2) & 7, ci = k & 3;
+  if (kw < 7 && ci < 3) dw[co * 147 + kh * 21 + kw * 3 + ci] = __builtin_bit_cast(uint16_t, (__bf16)s);
+}
+
 }  // namespace
+
+static int stem_ncu();
 
 extern "C" int64_t pdt_stem_conv_wprep_elems() { return kWPrepElems; }
 
@@ -253,11 +490,7 @@ extern "C" int pdt_stem_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t*
       hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_conv_kernel<false>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, kLds) == hipSuccess;
   if (!attr_ok) return -2;
-  static const int ncu = [] {
-    int dev = 0, v = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return 256;
-    return hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0 ? v : 256;
-  }();
+  const int ncu = stem_ncu();
   const int nrt = (OH + kRowsOut - 1) / kRowsOut, nct = (OW + kTW - 1) / kTW;
   const int64_t ntiles = (int64_t)N * nrt * nct;
   if (ntiles > 0x7fffffff || (int64_t)N * H > 0x7fffffff / 4) return -3;
@@ -269,5 +502,36 @@ extern "C" int pdt_stem_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t*
   else
     hipLaunchKernelGGL(stem_conv_kernel<false>, dim3(grid), dim3(kThreads), kLds, s, x, wp, y, H, W, OH, OW, nrt, nct,
                        (int)ntiles);
+  return hipGetLastError() == hipSuccess ? 0 : -4;
+}
+
+static int stem_ncu() {
+  static const int ncu = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 256;
+    return hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0 ? v : 256;
+  }();
+  return ncu;
+}
+
+// fp32 workspace floats for pdt_stem_conv_wgrad (one [64][224] partial per workgroup).
+extern "C" int64_t pdt_stem_wgrad_ws_floats() { return (int64_t)stem_ncu() * 64 * kGK; }
+
+// dw [64, 3, 7, 7] (channels_last storage [64][7][7][3], bf16) of the stem conv from x [N, 3, H, W]
+// and dy [N, 64, OH, OW] (both channels_last). Requires W % 32 == 0 and W <= 224 (OW <= 112).
+extern "C" int pdt_stem_conv_wgrad(const uint16_t* x, const uint16_t* dy, uint16_t* dw, float* ws, int N, int H,
+                                   int W, hipStream_t s) {
+  if (N < 1 || H < 1 || W < 32 || W % 32 != 0 || W > 2 * kTW) return -1;
+  const int OH = (H - 1) / 2 + 1, OW = W / 2;
+  static const bool attr_ok = hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_wgrad_kernel),
+                                                  hipFuncAttributeMaxDynamicSharedMemorySize, kGLds) == hipSuccess;
+  if (!attr_ok) return -2;
+  const int nrt = (OH + kGRowsOut - 1) / kGRowsOut;
+  const int64_t ntiles = (int64_t)N * nrt;
+  if (ntiles > 0x7fffffff || (int64_t)N * OH * OW * 64 > 0x7fffffffLL * 4) return -3;
+  const int grid = (int)std::min<int64_t>(ntiles, stem_ncu());
+  hipLaunchKernelGGL(stem_wgrad_kernel, dim3(grid), dim3(kGThreads), kGLds, s, x, dy, ws, H, W, OH, OW, nrt,
+                     (int)ntiles);
+  hipLaunchKernelGGL(stem_wgrad_reduce_kernel, dim3(64 * kGK / 256), dim3(1024), 0, s, ws, grid, dw);
   return hipGetLastError() == hipSuccess ? 0 : -4;
 }

@@ -425,8 +425,9 @@ def conv3x3_eligible(conv: nn.Conv2d, x: torch.Tensor) -> bool:
 
 
 class _StemConvFn(torch.autograd.Function):
-    """ResNet stem (7x7 / stride 2 / pad 3, 3 -> 64) forward on our MFMA kernel
-    (csrc/kernels/conv_stem.hip); gradients on MIOpen (the image needs none in training)."""
+    """ResNet stem (7x7 / stride 2 / pad 3, 3 -> 64) on our MFMA kernels (csrc/kernels/conv_stem.hip):
+    forward and weight gradient (W <= 224; MIOpen beyond); the input gradient — which training
+    never asks for (the images need none) — on MIOpen."""
 
     @staticmethod
     def forward(ctx, x, weight):
@@ -443,7 +444,11 @@ class _StemConvFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = torch.ops.aten.convolution_backward(*args, [True, False, False])[0]
         if ctx.needs_input_grad[1]:
-            wfn = lambda: torch.ops.aten.convolution_backward(*args, [False, True, False])[1]  # noqa: E731
+            if x.shape[3] <= 224:
+                from ._native import native
+                wfn = lambda: native().stem_conv_wgrad(x, gy)  # noqa: E731
+            else:
+                wfn = lambda: torch.ops.aten.convolution_backward(*args, [False, True, False])[1]  # noqa: E731
             dw = _on_side_stream(wfn, weight, gy, x) if _wgrad_stream_enabled() else wfn()
         return dx, dw
 

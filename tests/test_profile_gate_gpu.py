@@ -48,7 +48,8 @@ def test_resnet_step_runs_our_kernels(monkeypatch):
     assert names, "no device kernels recorded"
     for ours in ("bn_reduce3_kernel", "bn_fin_kernel", "bn_apply_kernel", "bn_bwd_apply_kernel",
                  "bn_apply_pool_kernel", "maxpool_bwd_kernel", "ce_fwd_kernel", "ce_bwd_kernel", "mt_kernel",
-                 "conv3x3wst_kernel", "conv3x3h_kernel", "conv3x3_flip_kernel"):
+                 "conv3x3wst_kernel", "conv3x3h_kernel", "conv3x3_flip_kernel", "stem_conv_kernel",
+                 "stem_wgrad_kernel"):
         assert _has(names, ours), (ours, sorted(set(names))[:40])
     for stock in ("MIOpenBatchNorm", "batch_norm", "max_pool", "nll_loss", "log_softmax"):
         assert not _has(names, stock), (stock, [n for n in names if stock in n][:5])

@@ -20,6 +20,10 @@ __global__ void fill_kernel(uint16_t* p, int64_t n, uint32_t seed, float scale) 
   }
 }
 
+__global__ void fill_one(uint16_t* p, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = 0x3f80;
+}
+
 __global__ void ref_kernel(const uint16_t* x, const uint16_t* w, float* y, int N, int H, int W, int OH, int OW) {
   const int64_t total = (int64_t)N * OH * OW * 64;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
@@ -38,9 +42,80 @@ __global__ void ref_kernel(const uint16_t* x, const uint16_t* w, float* y, int N
   }
 }
 
+__global__ void ref_wgrad_kernel(const uint16_t* x, const uint16_t* dy, float* dw, int N, int H, int W, int OH, int OW) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 64 * 147) return;
+  const int co = i / 147, r = i % 147, kh = r / 21, kw = (r % 21) / 3, c = r % 3;
+  float acc = 0.f;
+  for (int n = 0; n < N; ++n)
+    for (int oh = 0; oh < OH; ++oh)
+      for (int ow = 0; ow < OW; ++ow) {
+        const int ih = 2 * oh - 3 + kh, iw = 2 * ow - 3 + kw;
+        if (ih < 0 || ih >= H || iw < 0 || iw >= W) continue;
+        acc += bf2f(dy[(((int64_t)n * OH + oh) * OW + ow) * 64 + co]) * bf2f(x[(((int64_t)n * H + ih) * W + iw) * 3 + c]);
+      }
+  dw[i] = acc;
+}
+
 static float bf_host(uint16_t v) { uint32_t u = (uint32_t)v << 16; float f; memcpy(&f, &u, 4); return f; }
 
+static int wgrad_main(int N, int H, int W, bool ref, int iters) {
+  const int OH = (H - 1) / 2 + 1, OW = W / 2;
+  const int64_t nx = (int64_t)N * H * W * 3, ny = (int64_t)N * OH * OW * 64;
+  uint16_t *x, *dy, *dw;
+  float *ws, *dwr;
+  CK(hipMalloc(&x, nx * 2)); CK(hipMalloc(&dy, ny * 2)); CK(hipMalloc(&dw, 64 * 147 * 2));
+  CK(hipMalloc(&ws, pdt_stem_wgrad_ws_floats() * 4)); CK(hipMalloc(&dwr, 64 * 147 * 4));
+  fill_kernel<<<1024, 256>>>(x, nx, 5, 1.f);
+  fill_kernel<<<1024, 256>>>(dy, ny, 6, 1.f);
+  if (getenv("ONESX")) fill_one<<<1024, 256>>>(x, nx);
+  if (getenv("ONESDY")) fill_one<<<1024, 256>>>(dy, ny);
+  int rc = pdt_stem_conv_wgrad(x, dy, dw, ws, N, H, W, 0);
+  CK(hipDeviceSynchronize());
+  if (rc) { printf("wgrad rc %d\n", rc); return 1; }
+  double md = 0, mr = 0;
+  if (ref) {
+    ref_wgrad_kernel<<<(64 * 147 + 255) / 256, 256>>>(x, dy, dwr, N, H, W, OH, OW);
+    CK(hipDeviceSynchronize());
+    std::vector<uint16_t> h(64 * 147);
+    std::vector<float> r(64 * 147);
+    CK(hipMemcpy(h.data(), dw, 64 * 147 * 2, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(r.data(), dwr, 64 * 147 * 4, hipMemcpyDeviceToHost));
+    for (int i = 0; i < 64 * 147; ++i) {
+      md = std::max(md, (double)std::fabs(bf_host(h[i]) - r[i]));
+      mr = std::max(mr, (double)std::fabs(r[i]));
+    }
+    if (getenv("DUMP"))
+      for (int i = 0; i < 147; i += 1) printf("co0 kh%d kw%d ci%d: ours %8.3f ref %8.3f\n", i / 21, (i % 21) / 3, i % 3, bf_host(h[i]), r[i]);
+  }
+  double us = 0;
+  if (iters) {
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+    for (int i = 0; i < 3; ++i) pdt_stem_conv_wgrad(x, dy, dw, ws, N, H, W, 0);
+    CK(hipEventRecord(e0));
+    for (int i = 0; i < iters; ++i) pdt_stem_conv_wgrad(x, dy, dw, ws, N, H, W, 0);
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    us = ms * 1e3 / iters;
+  }
+  printf("stem wgrad N=%d H=%d W=%d: %.1f us  %.2f TB/s  max|err| %.3g (max|ref| %.3g)\n", N, H, W, us,
+         us > 0 ? (nx + ny) * 2 / us / 1e6 : 0.0, md, mr);
+  CK(hipFree(x)); CK(hipFree(dy)); CK(hipFree(dw)); CK(hipFree(ws)); CK(hipFree(dwr));
+  return md > 0.02 * mr + 0.05 ? 2 : 0;
+}
+
 int main(int argc, char** argv) {
+  if (getenv("WGRAD")) {
+    int rc = 0;
+    rc |= wgrad_main(2, 32, 32, true, 0);
+    if (!getenv("DUMP")) rc |= wgrad_main(3, 17, 64, true, 0);
+    if (!getenv("DUMP")) rc |= wgrad_main(2, 224, 224, true, 0);
+    if (!getenv("DUMP")) rc |= wgrad_main(512, 224, 224, false, 20);
+    return rc;
+  }
   const int N = argc > 1 ? atoi(argv[1]) : 512, H = 224, W = 224, OH = 112, OW = 112;
   const int64_t nx = (int64_t)N * H * W * 3, ny = (int64_t)N * OH * OW * 64;
   uint16_t *x, *w, *wp, *y;
