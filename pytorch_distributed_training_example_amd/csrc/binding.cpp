@@ -73,6 +73,8 @@ int pdt_bn_relu_maxpool_fwd_train(const uint16_t* x, const float* gamma, const f
 int pdt_conv3x3s1_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int N, int H, int W, int Ci, int Co,
                       hipStream_t s);
 int pdt_conv3x3_flip_weights(const uint16_t* w, uint16_t* wf, int Co, int Ci, hipStream_t s);
+int pdt_conv3x3s1_fwd_stats(const uint16_t* x, const uint16_t* w, uint16_t* y, float* part, int N, int H, int W,
+                            int Ci, int Co, hipStream_t s);
 int64_t pdt_stem_conv_wprep_elems();
 int pdt_stem_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* wp, uint16_t* y, int N, int H, int W,
                       hipStream_t s);
@@ -81,6 +83,14 @@ int pdt_stem_conv_wgrad(const uint16_t* x, const uint16_t* dy, uint16_t* dw, flo
                         hipStream_t s);
 int pdt_maxpool3s2_bwd(const uint16_t* dy, const uint8_t* code, uint16_t* dz, int N, int H, int W, int C,
                        hipStream_t s);
+int pdt_conv1x1_tile_rows();
+int pdt_conv1x1_gemm(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t* c, float* part, int M, int K,
+                     int N, hipStream_t s);
+int64_t pdt_bn_tiles_ws_floats(int T, int C);
+int pdt_bn_fwd_train_tiles(const float* part, int T, int BMt, const uint16_t* x, const uint16_t* res,
+                           const float* gamma, const float* beta, float* running_mean, float* running_var,
+                           float momentum, float eps, int64_t M, int C, int relu, uint16_t* y, uint8_t* mask,
+                           float* mean, float* invstd, float* ws, hipStream_t s);
 int pdt_fp8_cast_transpose(const uint16_t* x, int64_t M, int64_t K, const float* scale, uint8_t* out,
                            uint8_t* out_t, float* amax, hipStream_t s);
 int pdt_fp8_update_scales(float* state, int n, int L, float margin_scale, hipStream_t s);
@@ -421,6 +431,69 @@ std::vector<Tensor> bn_bwd_train(Tensor dy, Tensor x, c10::optional<Tensor> mask
   return {dx, dres, dg, db};
 }
 
+// ----------------------------------------------------------------------------- 1x1 conv GEMM (+ BN stats)
+// out[M,N] = a[M,K] @ b[N,K]^T (+ out, when acc: in-place accumulate). a, b, out: row-major bf16
+// (a 1x1 conv's channels_last activations viewed as [N*H*W, C]). stats: also return the per-tile
+// partials [2, T, N] fp32 (tile sums, centred tile sums of squares; T = ceil(M / 256)).
+c10::optional<Tensor> conv1x1_gemm(Tensor a, Tensor b, Tensor out, bool acc, bool stats) {
+  for (const Tensor* t : {&a, &b, &out}) {
+    check_cuda(*t, "conv1x1_gemm operand");
+    TORCH_CHECK(t->scalar_type() == at::kBFloat16 && t->dim() == 2 && t->is_contiguous(),
+                "conv1x1_gemm: operands must be 2-D contiguous bf16");
+  }
+  const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
+  TORCH_CHECK(b.size(1) == K && out.size(0) == M && out.size(1) == N, "conv1x1_gemm: shape mismatch");
+  TORCH_CHECK(K % 32 == 0 && N % 64 == 0, "conv1x1_gemm: K % 32 == 0 and N % 64 == 0 required");
+  TORCH_CHECK(!(acc && stats), "conv1x1_gemm: acc and stats are exclusive");
+  c10::optional<Tensor> part;
+  if (stats) {
+    const int64_t T = (M + pdt_conv1x1_tile_rows() - 1) / pdt_conv1x1_tile_rows();
+    part = at::empty({2, T, N}, a.options().dtype(at::kFloat));
+  }
+  const int rc = pdt_conv1x1_gemm(reinterpret_cast<const uint16_t*>(a.data_ptr()),
+                                  reinterpret_cast<const uint16_t*>(b.data_ptr()),
+                                  reinterpret_cast<uint16_t*>(out.data_ptr()),
+                                  acc ? reinterpret_cast<const uint16_t*>(out.data_ptr()) : nullptr,
+                                  stats ? part->data_ptr<float>() : nullptr, (int)M, (int)K, (int)N, stream());
+  TORCH_CHECK(rc == 0, "pdt_conv1x1_gemm failed: ", rc);
+  return part;
+}
+
+// BN training forward with the statistics taken from conv1x1_gemm's per-tile partials.
+std::vector<Tensor> bn_fwd_train_tiles(Tensor x, Tensor part, c10::optional<Tensor> res, c10::optional<Tensor> weight,
+                                       c10::optional<Tensor> bias, c10::optional<Tensor> running_mean,
+                                       c10::optional<Tensor> running_var, double momentum, double eps, bool relu) {
+  check_nhwc_bf16(x, "x");
+  const int64_t C = x.size(1);
+  const int64_t M = x.numel() / C;
+  const int BMt = pdt_conv1x1_tile_rows();
+  const int64_t T = (M + BMt - 1) / BMt;
+  TORCH_CHECK(C % 64 == 0, "pdt bn: C must be a multiple of 64");
+  TORCH_CHECK(part.scalar_type() == at::kFloat && part.is_contiguous() && part.dim() == 3 && part.size(0) == 2 &&
+              part.size(1) == T && part.size(2) == C, "bn_fwd_train_tiles: partials [2, T, C] fp32 expected");
+  auto y = at::empty_like(x);
+  Tensor mask;
+  if (relu) mask = at::empty({M * C / 8}, x.options().dtype(at::kByte));
+  auto fopt = x.options().dtype(at::kFloat);
+  auto mean = at::empty({C}, fopt), invstd = at::empty({C}, fopt);
+  auto ws = at::empty({pdt_bn_tiles_ws_floats((int)T, (int)C)}, fopt);
+  const uint16_t* rp = nullptr;
+  if (res.has_value() && res->defined()) {
+    check_nhwc_bf16(*res, "residual");
+    TORCH_CHECK(res->sizes() == x.sizes() && res->strides() == x.strides(), "pdt bn: residual layout mismatch");
+    rp = reinterpret_cast<const uint16_t*>(res->data_ptr());
+  }
+  float* rm = running_mean.has_value() && running_mean->defined() ? running_mean->data_ptr<float>() : nullptr;
+  float* rv = running_var.has_value() && running_var->defined() ? running_var->data_ptr<float>() : nullptr;
+  const int rc = pdt_bn_fwd_train_tiles(part.data_ptr<float>(), (int)T, BMt, reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                                        rp, opt_fptr(weight), opt_fptr(bias), rm, rv, (float)momentum, (float)eps, M,
+                                        (int)C, relu, reinterpret_cast<uint16_t*>(y.data_ptr()),
+                                        relu ? mask.data_ptr<uint8_t>() : nullptr, mean.data_ptr<float>(),
+                                        invstd.data_ptr<float>(), ws.data_ptr<float>(), stream());
+  TORCH_CHECK(rc == 0, "pdt_bn_fwd_train_tiles failed: ", rc);
+  return {y, mask, mean, invstd};
+}
+
 // ----------------------------------------------------------------------------- 3x3 conv (stride 1, pad 1)
 // y = conv2d(x, w, stride=1, padding=1) for channels_last bf16 x [N,Ci,H,W] and w [Co,Ci,3,3]
 // (w's channels_last storage is [Co][3][3][Ci], the kernel's layout).
@@ -437,6 +510,26 @@ Tensor conv3x3s1_fwd(Tensor x, Tensor w) {
                                    stream());
   TORCH_CHECK(rc == 0, "pdt_conv3x3s1_fwd failed: ", rc);
   return y;
+}
+
+// conv3x3s1_fwd + the per-tile BatchNorm statistics of y (tile_stats.h): {y, part [2, T, Co]}, or
+// {y} alone when the shape runs on a kernel without the statistics epilogue.
+std::vector<Tensor> conv3x3s1_fwd_stats(Tensor x, Tensor w) {
+  check_nhwc_bf16(x, "x");
+  TORCH_CHECK(w.dim() == 4 && w.size(2) == 3 && w.size(3) == 3 && w.size(1) == x.size(1) &&
+              w.scalar_type() == at::kBFloat16, "conv3x3: weight [Co, Ci, 3, 3] bf16");
+  w = w.contiguous(at::MemoryFormat::ChannelsLast);
+  const int64_t N = x.size(0), Ci = x.size(1), H = x.size(2), W = x.size(3), Co = w.size(0);
+  auto y = at::empty({N, Co, H, W}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const int64_t T = (N * H * W + pdt_conv1x1_tile_rows() - 1) / pdt_conv1x1_tile_rows();
+  auto part = at::empty({2, T, Co}, x.options().dtype(at::kFloat));
+  const int rc = pdt_conv3x3s1_fwd_stats(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                                         reinterpret_cast<const uint16_t*>(w.data_ptr()),
+                                         reinterpret_cast<uint16_t*>(y.data_ptr()), part.data_ptr<float>(), (int)N,
+                                         (int)H, (int)W, (int)Ci, (int)Co, stream());
+  if (rc == -5) return {conv3x3s1_fwd(x, w)};
+  TORCH_CHECK(rc == 0, "pdt_conv3x3s1_fwd_stats failed: ", rc);
+  return {y, part};
 }
 
 // Data-gradient weights: wf [Ci, Co, 3, 3] (channels_last storage [Ci][3][3][Co]) with
@@ -882,7 +975,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_fwd_eval", &bn_fwd_eval);
   m.def("bn_relu_maxpool_fwd", &bn_relu_maxpool_fwd);
   m.def("maxpool3s2_bwd", &maxpool3s2_bwd);
+  m.def("conv1x1_gemm", &conv1x1_gemm);
+  m.def("bn_fwd_train_tiles", &bn_fwd_train_tiles);
   m.def("conv3x3s1_fwd", &conv3x3s1_fwd);
+  m.def("conv3x3s1_fwd_stats", &conv3x3s1_fwd_stats);
   m.def("conv3x3_flip", &conv3x3_flip);
   m.def("stem_conv_fwd", &stem_conv_fwd);
   m.def("stem_conv_wgrad", &stem_conv_wgrad);

@@ -80,6 +80,25 @@ __device__ __forceinline__ void accum_row(const uint16_t* __restrict__ x, const 
   }
 }
 
+// Forward outputs of one channel from its batch mean and (biased) variance: mean / invstd,
+// the apply coefficients y = a*x + b, and the running statistics (unbiased variance).
+__device__ __forceinline__ void bn_set_fwd(int ch, double mu_d, double var, const FinArgs& fa) {
+  const int64_t Mt = fa.M;
+  var = var < 0.0 ? 0.0 : var;
+  const float mu = (float)mu_d;
+  const float is = (float)(1.0 / sqrt(var + (double)fa.eps));
+  fa.mean_out[ch] = mu;
+  fa.invstd_out[ch] = is;
+  const float gm = fa.gamma ? fa.gamma[ch] : 1.f, bt = fa.beta ? fa.beta[ch] : 0.f;
+  fa.a_out[ch] = gm * is;
+  fa.b_out[ch] = bt - mu * gm * is;
+  if (fa.running_mean) fa.running_mean[ch] = (1.f - fa.momentum) * fa.running_mean[ch] + fa.momentum * mu;
+  if (fa.running_var) {
+    const double unb = Mt > 1 ? var * (double)Mt / (double)(Mt - 1) : var;
+    fa.running_var[ch] = (1.f - fa.momentum) * fa.running_var[ch] + fa.momentum * (float)unb;
+  }
+}
+
 // Per-channel finalize from the full sums (S1, S2): forward -> mean/invstd/affine/running stats,
 // backward -> dgamma/dbeta and the dx coefficients.
 template <int MODE>
@@ -89,20 +108,7 @@ __device__ __forceinline__ void bn_finalize(int ch, float S1, float S2, const Fi
     const float kk = bf2f(fa.x[ch]);
     const double inv_m = 1.0 / (double)Mt;
     const double d1 = (double)S1 * inv_m;
-    double var = (double)S2 * inv_m - d1 * d1;
-    var = var < 0.0 ? 0.0 : var;
-    const float mu = (float)(kk + d1);
-    const float is = (float)(1.0 / sqrt(var + (double)fa.eps));
-    fa.mean_out[ch] = mu;
-    fa.invstd_out[ch] = is;
-    const float gm = fa.gamma ? fa.gamma[ch] : 1.f, bt = fa.beta ? fa.beta[ch] : 0.f;
-    fa.a_out[ch] = gm * is;
-    fa.b_out[ch] = bt - mu * gm * is;
-    if (fa.running_mean) fa.running_mean[ch] = (1.f - fa.momentum) * fa.running_mean[ch] + fa.momentum * mu;
-    if (fa.running_var) {
-      const double unb = Mt > 1 ? var * (double)Mt / (double)(Mt - 1) : var;
-      fa.running_var[ch] = (1.f - fa.momentum) * fa.running_var[ch] + fa.momentum * (float)unb;
-    }
+    bn_set_fwd(ch, (double)kk + d1, (double)S2 * inv_m - d1 * d1, fa);
   } else {
     const float is = fa.invstd[ch];
     const float gm = fa.gamma ? fa.gamma[ch] : 1.f;
@@ -575,6 +581,51 @@ __global__ __launch_bounds__(1024) void bn_fin_kernel(const float* __restrict__ 
   if (tid < 64) bn_finalize<MODE>(ch0 + tid, sm[tid], sm[64 + tid], fa);
 }
 
+// Statistics from the per-tile partials of a producer kernel's epilogue (conv1x1.hip STATS:
+// part = [T][C] tile sums, then [T][C] centred tile sums of squares, tiles of BMt rows). Level 1:
+// block (64 channels, tile range) -> double (S, Q) with Q = sum_t (M2_t + S_t^2 / n_t) — the
+// between-tile term in double, so E[x^2] - mean^2 never cancels in fp32. Level 2 finalizes.
+constexpr int kTilesPerBlock = 128;
+
+__global__ __launch_bounds__(1024) void bn_tiles_l1_kernel(const float* __restrict__ part, int T, int BMt, int64_t M,
+                                                           int C, double* __restrict__ out) {
+  __shared__ double sm[2][16][64];
+  const int tid = threadIdx.x, cl = tid & 63, j = tid >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  const int t0 = blockIdx.y * kTilesPerBlock, t1 = min(T, t0 + kTilesPerBlock);
+  double S = 0.0, Q = 0.0;
+#pragma unroll 4
+  for (int t = t0 + j; t < t1; t += 16) {
+    const float s = part[(int64_t)t * C + c];
+    const float q = part[((int64_t)T + t) * C + c];
+    const int64_t rem = M - (int64_t)t * BMt;
+    const double n = (double)(rem < BMt ? rem : BMt);
+    S += (double)s;
+    Q += (double)q + (double)s * (double)s / n;
+  }
+  sm[0][j][cl] = S;
+  sm[1][j][cl] = Q;
+  __syncthreads();
+  if (j == 0) {
+    double s = 0.0, q = 0.0;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) { s += sm[0][u][cl]; q += sm[1][u][cl]; }
+    out[((int64_t)blockIdx.y * C + c) * 2] = s;
+    out[((int64_t)blockIdx.y * C + c) * 2 + 1] = q;
+  }
+}
+
+__global__ void bn_tiles_l2_kernel(const double* __restrict__ in, int P, int C, FinArgs fa) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0, q = 0.0;
+#pragma unroll 8
+  for (int p = 0; p < P; ++p) { s += in[((int64_t)p * C + c) * 2]; q += in[((int64_t)p * C + c) * 2 + 1]; }
+  const double inv_m = 1.0 / (double)fa.M;
+  const double mu = s * inv_m;
+  bn_set_fwd(c, mu, q * inv_m - mu * mu, fa);
+}
+
 __global__ void bn_eval_coef_kernel(int C, const float* __restrict__ gamma, const float* __restrict__ beta,
                                     const float* __restrict__ rm, const float* __restrict__ rv, float eps,
                                     float* __restrict__ a_out, float* __restrict__ b_out) {
@@ -969,6 +1020,40 @@ int pdt_bn_fwd_train(const uint16_t* x, const uint16_t* res, const float* gamma,
 #define PDT_APPLY(RL, RS, MK)                                                                                 \
   hipLaunchKernelGGL((bn_apply_kernel<RL, RS, MK, 1>), dim3(grid), dim3(256), 0, s, x, res, a, b, y, mask, \
                      nvec, C, fixed)
+  const bool mk = mask != nullptr;
+  if (relu && res) { if (mk) PDT_APPLY(true, true, true); else PDT_APPLY(true, true, false); }
+  else if (relu) { if (mk) PDT_APPLY(true, false, true); else PDT_APPLY(true, false, false); }
+  else if (res) PDT_APPLY(false, true, false);
+  else PDT_APPLY(false, false, false);
+  return 0;
+}
+
+// Workspace floats of pdt_bn_fwd_train_tiles.
+int64_t pdt_bn_tiles_ws_floats(int T, int C) {
+  const int64_t P = (T + kTilesPerBlock - 1) / kTilesPerBlock;
+  return 4 * P * C + 2 * (int64_t)C;
+}
+
+// Training forward whose statistics come from a producer's per-tile partials (see
+// bn_tiles_l1_kernel) instead of a reduce pass over x: finalize (2 small launches) + apply.
+int pdt_bn_fwd_train_tiles(const float* part, int T, int BMt, const uint16_t* x, const uint16_t* res,
+                           const float* gamma, const float* beta, float* running_mean, float* running_var,
+                           float momentum, float eps, int64_t M, int C, int relu, uint16_t* y, uint8_t* mask,
+                           float* mean, float* invstd, float* ws, hipStream_t s) {
+  if (C % kCC != 0 || M < 1 || T != (int)((M + BMt - 1) / BMt)) return -1;
+  const int P = (T + kTilesPerBlock - 1) / kTilesPerBlock;
+  double* lv = reinterpret_cast<double*>(ws);
+  float* a = ws + 4 * (int64_t)P * C;
+  float* b = a + C;
+  FinArgs fa{};
+  fa.gamma = gamma; fa.beta = beta; fa.mean_out = mean; fa.invstd_out = invstd; fa.a_out = a;
+  fa.b_out = b; fa.running_mean = running_mean; fa.running_var = running_var; fa.momentum = momentum;
+  fa.eps = eps; fa.M = M;
+  hipLaunchKernelGGL(bn_tiles_l1_kernel, dim3(C / 64, P), dim3(1024), 0, s, part, T, BMt, M, C, lv);
+  hipLaunchKernelGGL(bn_tiles_l2_kernel, dim3((C + 255) / 256), dim3(256), 0, s, lv, P, C, fa);
+  const int64_t nvec = M * C / 8;
+  const int fixed = (2048 % C) == 0;
+  const int grid = apply_grid(nvec);
   const bool mk = mask != nullptr;
   if (relu && res) { if (mk) PDT_APPLY(true, true, true); else PDT_APPLY(true, true, false); }
   else if (relu) { if (mk) PDT_APPLY(true, false, true); else PDT_APPLY(true, false, false); }

@@ -1,0 +1,266 @@
+// 1x1 convolution (an NHWC GEMM) on MFMA for gfx950, with the epilogues ResNet needs fused in:
+//
+//   Y[m, n] = sum_k A[m, k] * B[n, k]   (+ C[m, n])                     A, B, C, Y bf16, fp32 accumulate
+//
+//   forward     : A = X [M = N*H*W, Ci], B = W [Co, Ci]          -> Y = conv1x1(X)
+//   data grad   : A = dY [M, Co],        B = W^T [Ci, Co]        -> dX (+ C: the other branch's
+//                 gradient of X — the ResNet shortcut — accumulated in place, beta = 1)
+//   STATS       : per 256-pixel tile, per output channel: the tile's sum and its CENTRED sum of
+//                 squares (of the bf16 values written), so the BatchNorm that consumes Y never
+//                 re-reads it for its statistics (ops/batchnorm.py, bn_fwd_train_tiles).
+//
+// Not in the reference (LeNet has no 1x1 convs, /root/reference/cnn.py:10-16). ResNet-50's 1x1
+// convs are HBM-bound (K = 64..2048, M = 25K..1.6M at batch 512; tools/r50_roofline.py); the
+// library kernels (MIOpen / hipBLASLt) cannot fuse the BatchNorm statistics, which cost a full
+// extra read of every conv output (bn_reduce3, ~2 ms of a 44 ms step, profiles/r2).
+//
+// Structure (same machinery as the per-tap 3x3 kernel, conv3x3.hip):
+//   * tile 256 pixels x BN (64 | 128) channels; 4 (M) x BN/64 (N) waves of 64 x 64, each as
+//     4 x 4 blocks of v_mfma_f32_16x16x32_bf16 with the operands swapped (A = B-rows, B = pixels)
+//     so a lane's accumulator holds 4 consecutive channels of one pixel;
+//   * k-steps of 32 channels (64-B LDS rows); A and B staged global -> LDS by LDS-DMA
+//     (global_load_lds_dwordx4, 1 KB = 16 rows per wave instruction) through a 3-slot ring, one
+//     s_barrier per k-step, counted vmcnt so the DMA stays in flight across barriers; ~72 KB of
+//     LDS -> 2 workgroups per CU, so one workgroup's epilogue overlaps the other's loads;
+//   * rows XOR-swizzled (chunk ^ ((row >> 2) & 1) << 1) by permuting each lane's SOURCE chunk,
+//     conflict-free ds_read_b128 for the 16x16x32 lane map; rows past M DMA a zero page;
+//   * epilogue: the bf16 tile is staged through LDS, the statistics are taken from the staged
+//     (rounded) values, and the tile leaves as whole 16-B row pieces (C added there, fp32);
+//   * block -> tile map XCD-aware (xcd_remap): the N-tiles of one pixel tile share an L2.
+#include "../common.h"
+#include "../tile_stats.h"
+
+#include <stdlib.h>
+
+using namespace pdt;
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+#define PDT_LDS __attribute__((address_space(3)))
+
+__device__ __attribute__((aligned(256))) uint4 g_gemm_zero[16];  // zero page for rows past M (never written)
+
+template <int BN_, int WM_, int WN_>
+struct G1 {
+  static constexpr int BM = 256, BN = BN_, WM = WM_, WN = WN_, BK = 32, kSlots = 3;
+  static constexpr int kWaves = WM * WN, kThreads = kWaves * 64;
+  static constexpr int kABytes = BM * 64, kBBytes = BN * 64, kSlot = kABytes + kBBytes;
+  static constexpr int kEpiStride = BN * 2 + 16;
+  static constexpr int kEpi = BM * kEpiStride;
+  static constexpr int kRed = tile_bn_stats_lds<BM, BN, kThreads>();
+  static constexpr int kLds = kSlots * kSlot > kEpi + kRed ? kSlots * kSlot : kEpi + kRed;
+  static constexpr int kMB = BM / WM / 16, kNB = BN / WN / 16;
+  static constexpr int kALd = BM / 16 / kWaves, kBLd = BN / 16 / kWaves, kG = kALd + kBLd;
+  static constexpr int kOcc = (160 * 1024) / kLds;
+  static constexpr int kMinWaves = kOcc * kThreads / 256 > 0 ? kOcc * kThreads / 256 : 1;
+  static_assert(kALd * 16 * kWaves == BM && kBLd * 16 * kWaves == BN, "DMA split");
+};
+
+__device__ __forceinline__ int chk64(int row, int p) { return p ^ (((row >> 2) & 1) << 1); }  // involution
+__device__ __forceinline__ int swz64(int row, int chunk) { return row * 64 + (chk64(row, chunk) << 4); }
+
+__device__ __forceinline__ f4 mfma(bf16x8 a, bf16x8 b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ void dma16(const void* src, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds(src, (PDT_LDS void*)lds_wave_base, 16, 0, 0);
+}
+
+template <int G>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(G >= 0 && G <= 6, "vmcnt");
+  if constexpr (G == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if constexpr (G == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+  else if constexpr (G == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (G == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+  else if constexpr (G == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if constexpr (G == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// part (STATS): [T][N] tile sums, then [T][N] centred tile sums of squares (T = ceil(M / 256)).
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+// NT: streaming (non-temporal) output stores
+template <class Cf, bool ACC, bool STATS, bool NT>
+__global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv1x1_kernel(
+    const uint16_t* __restrict__ A, const uint16_t* __restrict__ B, uint16_t* Y, const uint16_t* Cin,
+    float* __restrict__ part, int M, int K, int N) {
+  constexpr int BM = Cf::BM, BN = Cf::BN;
+  constexpr int WROWS = BM / Cf::WM, WCOLS = BN / Cf::WN;
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid % Cf::WM, wn = wid / Cf::WM;
+  const int ntiles = N / BN;
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = tile / ntiles;
+  const int m0 = mt * BM, n0 = (tile % ntiles) * BN;
+
+  const int sub = lane >> 2, p = lane & 3;
+  int aoff[Cf::kALd];  // element offset of this lane's A piece, -1 = zero page
+#pragma unroll
+  for (int i = 0; i < Cf::kALd; ++i) {
+    const int r = (wid * Cf::kALd + i) * 16 + sub;
+    aoff[i] = m0 + r < M ? (m0 + r) * K + chk64(r, p) * 8 : -1;
+  }
+  int boff[Cf::kBLd];
+#pragma unroll
+  for (int j = 0; j < Cf::kBLd; ++j) {
+    const int r = (wid * Cf::kBLd + j) * 16 + sub;
+    boff[j] = (n0 + r) * K + chk64(r, p) * 8;
+  }
+  const int S = K / Cf::BK;
+
+  auto issue = [&](int s) {
+    char* slot = lds + (s % Cf::kSlots) * Cf::kSlot;
+    const int ko = s * Cf::BK;
+#pragma unroll
+    for (int i = 0; i < Cf::kALd; ++i) {
+      const uint16_t* src = aoff[i] >= 0 ? A + (aoff[i] + ko) : reinterpret_cast<const uint16_t*>(g_gemm_zero);
+      dma16(src, slot + (wid * Cf::kALd + i) * 1024);
+    }
+#pragma unroll
+    for (int j = 0; j < Cf::kBLd; ++j) dma16(B + (boff[j] + ko), slot + Cf::kABytes + (wid * Cf::kBLd + j) * 1024);
+  };
+
+  f4 acc[Cf::kMB][Cf::kNB];
+#pragma unroll
+  for (int i = 0; i < Cf::kMB; ++i)
+#pragma unroll
+    for (int j = 0; j < Cf::kNB; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+
+  issue(0);
+  if (S > 1) issue(1);
+  const int lrow = lane & 15, lchk = lane >> 4;
+  for (int s = 0; s < S; ++s) {
+    if (s + 1 < S) wait_vm<Cf::kG>();
+    else wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (s + 2 < S) issue(s + 2);  // slot (s+2)%3 was last read at step s-1: every wave is past it
+    const char* As = lds + (s % Cf::kSlots) * Cf::kSlot;
+    const char* Bs = As + Cf::kABytes;
+    bf16x8 a[Cf::kMB], b[Cf::kNB];
+#pragma unroll
+    for (int i = 0; i < Cf::kMB; ++i) a[i] = *reinterpret_cast<const bf16x8*>(As + swz64(wm * WROWS + i * 16 + lrow, lchk));
+#pragma unroll
+    for (int j = 0; j < Cf::kNB; ++j) b[j] = *reinterpret_cast<const bf16x8*>(Bs + swz64(wn * WCOLS + j * 16 + lrow, lchk));
+#pragma unroll
+    for (int i = 0; i < Cf::kMB; ++i)
+#pragma unroll
+      for (int j = 0; j < Cf::kNB; ++j) acc[i][j] = mfma(b[j], a[i], acc[i][j]);  // D[n][m]
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+
+  // ---- epilogue: bf16 tile [BM pixels][BN] staged in LDS
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < Cf::kMB; ++i)
+#pragma unroll
+    for (int j = 0; j < Cf::kNB; ++j) {
+      const int ml = wm * WROWS + i * 16 + lrow;
+      const int cl = wn * WCOLS + j * 16 + 4 * lchk;
+      const f4 v = acc[i][j];
+      uint2 pk;
+      pk.x = (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)v[0]) |
+             ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)v[1]) << 16);
+      pk.y = (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)v[2]) |
+             ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)v[3]) << 16);
+      *reinterpret_cast<uint2*>(lds + ml * Cf::kEpiStride + cl * 2) = pk;
+    }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  if constexpr (STATS)
+    tile_bn_stats<BM, BN, Cf::kThreads, Cf::kEpiStride>(lds, reinterpret_cast<float*>(lds + Cf::kEpi),
+                                                         min(BM, M - m0), part, mt, (M + BM - 1) / BM, N, n0);
+
+  constexpr int kChunks = BN / 8;
+  for (int idx = tid; idx < BM * kChunks; idx += Cf::kThreads) {
+    const int r = idx / kChunks, c = idx % kChunks;
+    const int m = m0 + r;
+    if (m >= M) continue;
+    uint4 v = *reinterpret_cast<const uint4*>(lds + r * Cf::kEpiStride + c * 16);
+    const int64_t off = (int64_t)m * N + n0 + c * 8;
+    if constexpr (ACC) {
+      float a[8], cc[8];
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { a[2 * k] = __uint_as_float(w[k] << 16); a[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u); }
+      ld8_bf16(Cin + off, cc);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) a[k] += cc[k];
+      v.x = (uint32_t)f2bf(a[0]) | ((uint32_t)f2bf(a[1]) << 16);
+      v.y = (uint32_t)f2bf(a[2]) | ((uint32_t)f2bf(a[3]) << 16);
+      v.z = (uint32_t)f2bf(a[4]) | ((uint32_t)f2bf(a[5]) << 16);
+      v.w = (uint32_t)f2bf(a[6]) | ((uint32_t)f2bf(a[7]) << 16);
+    }
+    if constexpr (NT) {
+      const u32x4 t = {v.x, v.y, v.z, v.w};
+      __builtin_nontemporal_store(t, reinterpret_cast<u32x4*>(Y + off));
+    } else {
+      *reinterpret_cast<uint4*>(Y + off) = v;
+    }
+  }
+}
+
+int g_nt = 0;  // PDT_GEMM_NT=1: non-temporal output stores (experiment switch)
+
+template <class Cf, bool ACC, bool STATS, bool NT>
+int launch_nt(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t* c, float* part, int M, int K, int N,
+              hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&conv1x1_kernel<Cf, ACC, STATS, NT>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, Cf::kLds) != hipSuccess)
+      return -3;
+    attr = true;
+  }
+  const int64_t grid = (int64_t)(M + Cf::BM - 1) / Cf::BM * (N / Cf::BN);
+  hipLaunchKernelGGL((conv1x1_kernel<Cf, ACC, STATS, NT>), dim3((unsigned)grid), dim3(Cf::kThreads), Cf::kLds, s, a,
+                     b, y, c, part, M, K, N);
+  return 0;
+}
+
+template <class Cf, bool ACC, bool STATS>
+int launch(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t* c, float* part, int M, int K, int N,
+           hipStream_t s) {
+  const char* e = getenv("PDT_GEMM_NT");  // read per launch (A/B inside one process)
+  g_nt = (e && e[0] == '1') ? 1 : 0;
+  if (g_nt) return launch_nt<Cf, ACC, STATS, true>(a, b, y, c, part, M, K, N, s);
+  return launch_nt<Cf, ACC, STATS, false>(a, b, y, c, part, M, K, N, s);
+}
+
+using GWide = G1<128, 4, 2>;   // N % 128 == 0: 8 waves of 64x64
+using GNarrow = G1<64, 4, 1>;  // N == 64 (or odd multiples of 64): 4 waves of 64x64
+
+template <class Cf>
+int dispatch(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t* c, float* part, int M, int K, int N,
+             hipStream_t s) {
+  if (c && part) return -1;  // not instantiated (no caller needs both)
+  if (c) return launch<Cf, true, false>(a, b, y, c, part, M, K, N, s);
+  if (part) return launch<Cf, false, true>(a, b, y, c, part, M, K, N, s);
+  return launch<Cf, false, false>(a, b, y, c, part, M, K, N, s);
+}
+
+}  // namespace
+
+extern "C" {
+
+int pdt_conv1x1_tile_rows() { return 256; }
+
+// y[M,N] = a[M,K] * b[N,K]^T (+ c[M,N]); part: stats of y per 256-row tile (see above), or null.
+// All bf16 row-major, K % 32 == 0, N % 64 == 0, M * max(K, N) < 2^31. c may alias y.
+int pdt_conv1x1_gemm(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t* c, float* part, int M, int K,
+                     int N, hipStream_t s) {
+  if (M < 1 || K < 32 || K % 32 != 0 || N < 64 || N % 64 != 0) return -1;
+  if ((int64_t)M * (K > N ? K : N) >= ((int64_t)1 << 31) || (int64_t)N * K >= ((int64_t)1 << 31)) return -2;
+  if (N % 128 == 0) return dispatch<GWide>(a, b, y, c, part, M, K, N, s);
+  return dispatch<GNarrow>(a, b, y, c, part, M, K, N, s);
+}
+
+}  // extern "C"

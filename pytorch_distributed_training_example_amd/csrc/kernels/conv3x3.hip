@@ -28,6 +28,7 @@
 //   * block -> tile map XCD-aware (xcd_remap): the output-channel tiles of one pixel tile, and
 //     neighbouring pixel tiles (which share input rows), run on one XCD's L2.
 #include "../common.h"
+#include "../tile_stats.h"
 
 using namespace pdt;
 
@@ -252,7 +253,8 @@ struct HCfg {
   static constexpr int kMB = BM / WM / 16, kNB = BN / WN / 16;
   static constexpr int kEpiStride = BN * 2 + 16;
   static constexpr int kMain = 2 * kHaloBytes + 2 * kBBytes;
-  static constexpr int kLds = kMain > BM * kEpiStride ? kMain : BM * kEpiStride;
+  static constexpr int kEpi = BM * kEpiStride + tile_bn_stats_lds<BM, BN, kThreads>();  // staged tile + stats
+  static constexpr int kLds = kMain > kEpi ? kMain : kEpi;
   static constexpr int kOcc = (160 * 1024) / kLds;  // workgroups per CU (LDS-limited)
   static constexpr int kMinWaves = kOcc * kThreads / 256 > 0 ? kOcc * kThreads / 256 : 1;  // per SIMD
   static_assert(kHLd * 16 * kWaves == kHaloRows && kBLd * 16 * kWaves == TPS * BN, "DMA split");
@@ -261,10 +263,10 @@ struct HCfg {
 
 __device__ __forceinline__ int chk64(int row, int p) { return p ^ (((row >> 2) & 1) << 1); }  // = swz<64>, involution
 
-template <class Cf>
+template <class Cf, bool STATS = false>
 __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv3x3h_kernel(
     const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wt, uint16_t* __restrict__ Y, int N, int H, int W,
-    int Ci, int Co) {
+    int Ci, int Co, float* __restrict__ part) {
   constexpr int BM = Cf::BM, BN = Cf::BN, BK = Cf::BK;
   constexpr int WROWS = BM / Cf::WM, WCOLS = BN / Cf::WN;
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -399,6 +401,9 @@ __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv3x3h_kernel(
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
+  if constexpr (STATS)  // BatchNorm statistics of the staged bf16 tile (tile_stats.h)
+    tile_bn_stats<BM, BN, Cf::kThreads, Cf::kEpiStride>(lds, reinterpret_cast<float*>(lds + BM * Cf::kEpiStride),
+                                                         min(BM, M - m0), part, m0 / BM, (M + BM - 1) / BM, Co, n0);
   constexpr int kChunks = BN / 8;
   for (int idx = tid; idx < BM * kChunks; idx += Cf::kThreads) {
     const int r = idx / kChunks, cc = idx % kChunks;
@@ -951,11 +956,12 @@ inline int64_t halo_rows_bound(int H, int W, int BM) {
   return (rows + 2 * imgs) * (W + 2);
 }
 
-template <class Cf>
-int launch_h(const uint16_t* x, const uint16_t* w, uint16_t* y, int N, int H, int W, int Ci, int Co, hipStream_t s) {
+template <class Cf, bool STATS = false>
+int launch_h(const uint16_t* x, const uint16_t* w, uint16_t* y, int N, int H, int W, int Ci, int Co, hipStream_t s,
+             float* part = nullptr) {
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3h_kernel<Cf>),
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3h_kernel<Cf, STATS>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, Cf::kLds) != hipSuccess)
       return -3;
     attr = true;
@@ -964,8 +970,8 @@ int launch_h(const uint16_t* x, const uint16_t* w, uint16_t* y, int N, int H, in
   if (halo_rows_bound(H, W, Cf::BM) > Cf::kHaloRows) return -4;
   const int64_t M = (int64_t)N * H * W;
   const int64_t grid = (M + Cf::BM - 1) / Cf::BM * (Co / Cf::BN);
-  hipLaunchKernelGGL(conv3x3h_kernel<Cf>, dim3((unsigned)grid), dim3(Cf::kThreads), Cf::kLds, s, x, w, y, N, H, W,
-                     Ci, Co);
+  hipLaunchKernelGGL((conv3x3h_kernel<Cf, STATS>), dim3((unsigned)grid), dim3(Cf::kThreads), Cf::kLds, s, x, w, y, N,
+                     H, W, Ci, Co, part);
   return 0;
 }
 
@@ -1065,6 +1071,20 @@ int pdt_conv3x3s1_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int N, 
   // halo larger than the LDS buffer (tiny W): per-tap staging
   if (Co % 128 == 0) return launch<CfWide>(x, w, y, N, H, W, Ci, Co, s);
   return launch<CfNarrow>(x, w, y, N, H, W, Ci, Co, s);
+}
+
+// Forward + per-256-pixel-tile BatchNorm statistics of y into part ([2][T][Co] fp32, tile_stats.h).
+// Only the halo kernel has the statistics epilogue: returns -5 where another kernel would run
+// (64 -> 64 channels: the weight-stationary kernel; tiny W: per-tap staging) — caller falls back.
+int pdt_conv3x3s1_fwd_stats(const uint16_t* x, const uint16_t* w, uint16_t* y, float* part, int N, int H, int W,
+                            int Ci, int Co, hipStream_t s) {
+  if (Ci % 32 != 0 || Co % 64 != 0 || N < 1 || H < 1 || W < 1) return -1;
+  const int64_t M = (int64_t)N * H * W;
+  if (M * (Ci > Co ? Ci : Co) >= (int64_t)1 << 31 || (int64_t)Co * 9 * Ci >= (int64_t)1 << 31) return -2;
+  if (Ci == 64 && Co == 64) return -5;
+  if (halo_rows_bound(H, W, 256) > 512) return -5;
+  return Co % 128 == 0 ? launch_h<HWide, true>(x, w, y, N, H, W, Ci, Co, s, part)
+                       : launch_h<HNarrow, true>(x, w, y, N, H, W, Ci, Co, s, part);
 }
 
 // Weight gradient of the stride-1 pad-1 3x3 conv: dw[Co,3,3,Ci] (bf16) from x[N,H,W,Ci] and

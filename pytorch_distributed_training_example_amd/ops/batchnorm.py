@@ -52,10 +52,15 @@ class ResidualGradLink:
 
 class _BNTrainFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, residual, weight, bias, running_mean, running_var, momentum, eps, relu, link=None):
+    def forward(ctx, x, residual, weight, bias, running_mean, running_var, momentum, eps, relu, link=None,
+                part=None):
         C = native()
-        y, mask, mean, invstd = C.bn_fwd_train(x, residual, weight, bias, running_mean, running_var,
-                                               momentum, eps, relu)
+        if part is not None:  # statistics from the producing conv's epilogue: no reduce pass over x
+            y, mask, mean, invstd = C.bn_fwd_train_tiles(x, part, residual, weight, bias, running_mean,
+                                                         running_var, momentum, eps, relu)
+        else:
+            y, mask, mean, invstd = C.bn_fwd_train(x, residual, weight, bias, running_mean, running_var,
+                                                   momentum, eps, relu)
         ctx.relu = relu
         ctx.has_res = residual is not None
         ctx.has_weight = weight is not None
@@ -76,7 +81,7 @@ class _BNTrainFn(torch.autograd.Function):
             ctx.link.grad = dres  # the main-branch consumer adds its gradient into this buffer
             dres = None
         return (dx, dres if ctx.has_res else None, dg if need_w else None, db if need_w else None,
-                None, None, None, None, None, None)
+                None, None, None, None, None, None, None)
 
 
 class _BNEvalFn(torch.autograd.Function):
@@ -112,8 +117,10 @@ def batch_norm_act(x, residual, weight, bias, running_mean, running_var, trainin
             residual = residual.contiguous(memory_format=torch.channels_last if x.dim() == 4
                                            else torch.contiguous_format)
         if training:
+            from .conv import bn_stats_of
+            part = bn_stats_of(x) if x.dim() == 4 else None
             return _BNTrainFn.apply(x, residual, weight, bias, running_mean, running_var,
-                                    float(momentum), float(eps), bool(relu), res_link)
+                                    float(momentum), float(eps), bool(relu), res_link, part)
         return _BNEvalFn.apply(x, residual, weight, bias, running_mean, running_var, float(eps), bool(relu))
     return bn_reference(x, residual, weight, bias, running_mean, running_var, training, momentum, eps, relu)
 

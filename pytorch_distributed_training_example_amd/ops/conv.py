@@ -55,7 +55,7 @@ def load_table(path: str | None = None) -> int:
         tab = json.load(f)
     for k, v in tab.items():
         d, dt, *dims = k.split(",")
-        if v in ("miopen", "gemm") and len(dims) == 3:
+        if v in ("miopen", "gemm", "ours") and len(dims) == 3:
             _CHOICE.setdefault((d, dt, *map(int, dims)), v)
     return len(tab)
 
@@ -157,6 +157,38 @@ def _mode() -> str:
     return os.environ.get("PDT_CONV1X1", "auto")
 
 
+def _ours_dirs() -> str:
+    """Directions of stride-1 1x1 convs that run on our MFMA GEMM (csrc/kernels/conv1x1.hip):
+    ``PDT_CONV1X1_OURS`` = comma list of ``fwd`` (with the consuming BatchNorm's statistics
+    fused into the epilogue) and ``dgrad`` (with the shortcut gradient accumulated in place),
+    or ``none``."""
+    return os.environ.get("PDT_CONV1X1_OURS", "fwd,dgrad")
+
+
+def _ours_ok(direction: str, M: int, K: int, N: int) -> bool:
+    return (direction in _ours_dirs().split(",") and K % 32 == 0 and N % 64 == 0
+            and M * max(K, N) < 2 ** 31 and _mode() in ("auto", "ours"))
+
+
+class BNStats:
+    """Per-tile BatchNorm statistics of a conv output, computed in the conv's epilogue
+    (conv1x1_gemm ``stats``), attached to the output tensor as ``_pdt_bn_stats``; the BatchNorm
+    that consumes the tensor uses them instead of a reduce pass if the tensor is unmodified
+    (same version counter)."""
+
+    __slots__ = ("part", "version")
+
+    def __init__(self, part: torch.Tensor, version: int):
+        self.part, self.version = part, version
+
+
+def bn_stats_of(x: torch.Tensor):
+    st = getattr(x, "_pdt_bn_stats", None)
+    if st is not None and st.version == x._version:
+        return st.part
+    return None
+
+
 def _time(fn, reps: int = 3) -> float:
     fn()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -174,8 +206,8 @@ def _pick(key: Tuple, cands: Dict[str, callable]) -> str:
         return mode
     _ensure_table()
     c = _CHOICE.get(key)
-    if c is not None:
-        return c
+    if c is not None:  # a decided back end that is switched off here: the GEMM library, untimed
+        return c if c in cands else "gemm"
     if torch.cuda.is_current_stream_capturing():
         return "miopen"
     times = {name: _time(fn) for name, fn in cands.items()}
@@ -196,22 +228,32 @@ def _nhwc2d(t: torch.Tensor) -> torch.Tensor:
 
 class _Conv1x1Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, link=None):
+    def forward(ctx, x, weight, link=None, stats_out=None):
         N, Ci, H, W = x.shape
         Co = weight.shape[0]
         x2 = _nhwc2d(x)
         w2 = weight.reshape(Co, Ci)
         M = x2.shape[0]
-        algo = _pick(("fwd", _dtype_name(x), M, Ci, Co), {
-            "miopen": lambda: F.conv2d(x, weight),
-            "gemm": lambda: torch.mm(x2, w2.t()),
-        })
+        ctx.link = link
+        ctx.save_for_backward(x, weight)
+        cands = {"miopen": lambda: F.conv2d(x, weight), "gemm": lambda: torch.mm(x2, w2.t())}
+        if x.dtype == torch.bfloat16 and _ours_ok("fwd", M, Ci, Co):
+            from ._native import native
+
+            def ours(stats=False):
+                y = torch.empty((N, Co, H, W), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+                return y, native().conv1x1_gemm(x2, w2.contiguous(), _nhwc2d(y), False, stats)
+            cands["ours"] = ours
+        algo = _pick(("fwd", _dtype_name(x), M, Ci, Co), cands)
+        if algo == "ours":  # with the consuming BatchNorm's statistics in the epilogue
+            y, part = cands["ours"](stats_out is not None)
+            if stats_out is not None:
+                stats_out.append(part)
+            return y
         if algo == "gemm":
             y = torch.mm(x2, w2.t()).view(N, H, W, Co).permute(0, 3, 1, 2)
         else:
             y = F.conv2d(x, weight)
-        ctx.link = link
-        ctx.save_for_backward(x, weight)
         return y
 
     @staticmethod
@@ -235,11 +277,23 @@ class _Conv1x1Fn(torch.autograd.Function):
         if isinstance(acc, StridedGrad):  # a stride-2 shortcut's compact gradient: added below
             strided, acc = acc, None
         if ctx.needs_input_grad[0]:
-            algo = _pick(("bwd_data", _dtype_name(x), M, Ci, Co), {
-                "miopen": lambda: conv_bwd([True, False, False]),
-                "gemm": lambda: torch.mm(g2, w2),
-            })
-            if algo == "gemm" and acc is not None and acc.is_contiguous(memory_format=torch.channels_last):
+            cands = {"miopen": lambda: conv_bwd([True, False, False]), "gemm": lambda: torch.mm(g2, w2)}
+            if gy.dtype == torch.bfloat16 and _ours_ok("dgrad", M, Co, Ci):
+                from ._native import native
+                wt = w2.t().contiguous()  # [Ci, Co]: the B operand rows of dX = dY W
+
+                def ours_d():
+                    d = torch.empty_like(x)
+                    native().conv1x1_gemm(g2, wt, _nhwc2d(d), False, False)
+                    return d
+                cands["ours"] = ours_d
+            algo = _pick(("bwd_data", _dtype_name(x), M, Ci, Co), cands)
+            if algo == "ours" and acc is not None and acc.is_contiguous(memory_format=torch.channels_last):
+                native().conv1x1_gemm(g2, wt, _nhwc2d(acc), True, False)  # dx = dres + dY W, in place
+                dx, acc = acc, None
+            elif algo == "ours":
+                dx = ours_d()
+            elif algo == "gemm" and acc is not None and acc.is_contiguous(memory_format=torch.channels_last):
                 _nhwc2d(acc).addmm_(g2, w2)  # dx = dres + dY W in one GEMM (beta = 1)
                 dx, acc = acc, None
             elif algo == "gemm":
@@ -265,7 +319,7 @@ class _Conv1x1Fn(torch.autograd.Function):
             else:
                 wfn = lambda: conv_bwd([False, True, False])[1]  # noqa: E731
             dw = _on_side_stream(wfn, weight, gy, x) if _wgrad_stream_enabled() else wfn()
-        return dx, dw, None
+        return dx, dw, None, None
 
 
 class StridedGrad:
@@ -394,9 +448,14 @@ class _Conv3x3Fn(torch.autograd.Function):
     transposed (conv3x3_flip); weight gradient = MIOpen (optionally on the side stream)."""
 
     @staticmethod
-    def forward(ctx, x, weight):
+    def forward(ctx, x, weight, stats_out=None):
         from ._native import native
         ctx.save_for_backward(x, weight)
+        if stats_out is not None:  # BatchNorm statistics in the epilogue (halo kernel shapes)
+            r = native().conv3x3s1_fwd_stats(x, weight)
+            if len(r) == 2:
+                stats_out.append(r[1])
+            return r[0]
         return native().conv3x3s1_fwd(x, weight)
 
     @staticmethod
@@ -411,7 +470,12 @@ class _Conv3x3Fn(torch.autograd.Function):
             args = (gy, x, weight, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1)
             wfn = lambda: torch.ops.aten.convolution_backward(*args, [False, True, False])[1]  # noqa: E731
             dw = _on_side_stream(wfn, weight, gy, x) if _wgrad_stream_enabled() else wfn()
-        return dx, dw
+        return dx, dw, None
+
+
+def _stats_enabled() -> bool:
+    """``PDT_CONV_BN_STATS=0`` turns off the BatchNorm statistics epilogues of our convs."""
+    return os.environ.get("PDT_CONV_BN_STATS", "1") != "0"
 
 
 def conv3x3_eligible(conv: nn.Conv2d, x: torch.Tensor) -> bool:
@@ -470,9 +534,16 @@ class SplitConv2d(nn.Conv2d):
     ``PDT_CONV3X3=miopen`` / ``PDT_CONV_STEM=miopen`` switch back); the training backward can
     issue the weight gradient on a side stream (``PDT_WGRAD_STREAM=1``)."""
 
+    emit_bn_stats = True  # output feeds a BatchNorm: fuse its statistics where our kernel runs
+
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if conv3x3_eligible(self, x):
-            return _Conv3x3Fn.apply(x, self.weight)
+            holder = [] if (self.emit_bn_stats and self.training and torch.is_grad_enabled()
+                            and _stats_enabled()) else None
+            y = _Conv3x3Fn.apply(x, self.weight, holder)
+            if holder:
+                y._pdt_bn_stats = BNStats(holder[0], y._version)
+            return y
         if stem_eligible(self, x):
             return _StemConvFn.apply(x, self.weight)
         if (self.bias is None and x.is_cuda and self.padding_mode == "zeros" and torch.is_grad_enabled()
@@ -492,8 +563,9 @@ class Conv1x1(nn.Conv2d):
     """``nn.Conv2d(Ci, Co, 1, bias=False)`` (same parameters and state_dict) whose stride-1 GPU
     channels_last path runs as autotuned GEMMs; everything else is plain ``nn.Conv2d``."""
 
-    def __init__(self, inp: int, out: int, stride: int = 1):
+    def __init__(self, inp: int, out: int, stride: int = 1, emit_bn_stats: bool = True):
         super().__init__(inp, out, 1, stride=stride, bias=False)
+        self.emit_bn_stats = emit_bn_stats  # output feeds a BatchNorm: fuse its statistics (our GEMM)
 
     def _gemm_ok(self, x: torch.Tensor) -> bool:
         return (x.is_cuda and x.dim() == 4 and x.dtype == self.weight.dtype and self.padding == (0, 0)
@@ -512,7 +584,12 @@ class Conv1x1(nn.Conv2d):
         """``res_link``: a ``ResidualGradLink`` whose gradient (the other branch's gradient of
         ``x``) meets this conv's input gradient; requires one of the GEMM paths."""
         if self.gemm_eligible(x):
-            return _Conv1x1Fn.apply(x, self.weight, res_link)
+            holder = [] if (self.emit_bn_stats and self.training and torch.is_grad_enabled()
+                            and _stats_enabled()) else None
+            y = _Conv1x1Fn.apply(x, self.weight, res_link, holder)
+            if holder:
+                y._pdt_bn_stats = BNStats(holder[0], y._version)
+            return y
         if self.strided_gemm_eligible(x):
             return _Conv1x1StridedFn.apply(x, self.weight, self.stride[0], res_link)
         assert res_link is None, "res_link needs a GEMM path"

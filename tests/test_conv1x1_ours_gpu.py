@@ -1,0 +1,149 @@
+"""Our MFMA 1x1-conv GEMM (csrc/kernels/conv1x1.hip) against fp32 PyTorch references: plain,
+in-place accumulate (the shortcut-gradient hand-off) and the fused BatchNorm statistics epilogue,
+then the BatchNorm that consumes those statistics against the reduce-pass BatchNorm."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [(1000, 64, 256), (512, 256, 64), (4096, 32, 128), (700, 96, 192), (25088 // 8, 2048, 512),
+          (256, 512, 2048), (300, 64, 64)]
+
+
+def _native():
+    from pytorch_distributed_training_example_amd.ops._native import native
+    return native()
+
+
+def _ab(M, K, N, seed=0):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    b = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).bfloat16()
+    return a, b
+
+
+@pytest.mark.parametrize("M,K,N", SHAPES)
+def test_gemm_matches_fp32(M, K, N):
+    a, b = _ab(M, K, N)
+    y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    assert _native().conv1x1_gemm(a, b, y, False, False) is None
+    ref = a.float() @ b.float().t()
+    torch.testing.assert_close(y.float(), ref, rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("M,K,N", SHAPES[:4])
+def test_gemm_accumulates_in_place(M, K, N):
+    a, b = _ab(M, K, N, 1)
+    c = torch.randn(M, N, device="cuda").bfloat16()
+    ref = c.float() + a.float() @ b.float().t()
+    _native().conv1x1_gemm(a, b, c, True, False)
+    torch.testing.assert_close(c.float(), ref, rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("M,K,N", SHAPES)
+def test_stats_epilogue(M, K, N):
+    a, b = _ab(M, K, N, 2)
+    a = a + 0.5  # non-zero channel means
+    y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    part = _native().conv1x1_gemm(a, b, y, False, True)
+    T = (M + 255) // 256
+    assert part.shape == (2, T, N)
+    yf = torch.cat([y.float(), torch.full((T * 256 - M, N), float("nan"), device="cuda")]).view(T, 256, N)
+    valid = ~torch.isnan(yf)
+    n = valid.sum(1).float()
+    s = torch.where(valid, yf, 0).sum(1)
+    mu = s / n
+    m2 = torch.where(valid, (yf - mu[:, None]) ** 2, 0).sum(1)
+    torch.testing.assert_close(part[0], s, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(part[1], m2, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(y.float(), a.float() @ b.float().t(), rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("relu,res", [(True, False), (False, True), (True, True), (False, False)])
+@pytest.mark.parametrize("shape", [(8, 64, 256, 14, 14), (4, 128, 128, 7, 9)])
+def test_bn_from_tile_stats_matches_reduce_bn(relu, res, shape):
+    N, Ci, Co, H, W = shape
+    M = N * H * W
+    a, b = _ab(M, Ci, Co, 3)
+    y = torch.empty(N, Co, H, W, device="cuda", dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    y2 = y.permute(0, 2, 3, 1).reshape(M, Co)
+    part = _native().conv1x1_gemm(a + 1.0, b, y2, False, True)
+    r = torch.randn_like(y) if res else None
+    w = torch.rand(Co, device="cuda") + 0.5
+    bb = torch.randn(Co, device="cuda")
+    out = {}
+    for kind in ("tiles", "reduce"):
+        rm, rv = torch.zeros(Co, device="cuda"), torch.ones(Co, device="cuda")
+        if kind == "tiles":
+            o = _native().bn_fwd_train_tiles(y, part, r, w, bb, rm, rv, 0.1, 1e-5, relu)
+        else:
+            o = _native().bn_fwd_train(y, r, w, bb, rm, rv, 0.1, 1e-5, relu)
+        out[kind] = (o, rm, rv)
+    (ot, rmt, rvt), (orr, rmr, rvr) = out["tiles"], out["reduce"]
+    torch.testing.assert_close(ot[2], orr[2], rtol=1e-5, atol=1e-5)  # mean
+    torch.testing.assert_close(ot[3], orr[3], rtol=1e-4, atol=1e-5)  # invstd
+    torch.testing.assert_close(rmt, rmr, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(rvt, rvr, rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(ot[0].float(), orr[0].float(), rtol=1e-2, atol=1e-2)
+    if relu:
+        assert (ot[1] != orr[1]).float().mean().item() < 1e-3  # masks (ties at 0 may differ)
+    # and both against the fp32 formula
+    yf = y.float()
+    mu = yf.mean((0, 2, 3))
+    var = yf.var((0, 2, 3), unbiased=False)
+    torch.testing.assert_close(ot[2], mu, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(ot[3], (var + 1e-5).rsqrt(), rtol=1e-3, atol=1e-4)
+
+
+def test_resnet_bottleneck_uses_fused_stats(monkeypatch):
+    """A training Bottleneck on the fused path matches the same block with our GEMM off
+    (library GEMMs + reduce-pass BatchNorm): outputs, input and parameter gradients."""
+    from pytorch_distributed_training_example_amd.models import resnet as R
+    from pytorch_distributed_training_example_amd.models.precision import to_bf16_mixed
+    from pytorch_distributed_training_example_amd.ops import conv as C
+    torch.manual_seed(0)
+    ds = R._Downsample(R.conv1x1(64, 256, 1), R._bn(256))
+    blk = to_bf16_mixed(R.Bottleneck(64, 64, 1, ds).cuda().to(memory_format=torch.channels_last))
+    x0 = torch.randn(16, 64, 28, 28, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    res = {}
+    for ours in ("fwd,dgrad", "none"):
+        monkeypatch.setenv("PDT_CONV1X1_OURS", ours)
+        monkeypatch.setenv("PDT_CONV1X1", "ours" if ours != "none" else "gemm")
+        blk.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_(True)
+        h = blk.conv1(x)
+        assert (C.bn_stats_of(h) is not None) == (ours != "none")
+        y = blk(x)
+        y.backward(torch.ones_like(y) * 0.01 + y.detach() * 0.1)
+        res[ours] = [y.float()] + [x.grad.float()] + [p.grad.float().clone() for p in blk.parameters()]
+    for a, b in zip(res["fwd,dgrad"], res["none"]):
+        err = ((a - b).norm() / (b.norm() + 1e-12)).item()
+        assert err < 3e-2, err
+
+
+@pytest.mark.parametrize("shape", [(4, 128, 128, 28, 28), (8, 256, 256, 14, 14), (2, 64, 128, 9, 11),
+                                   (4, 64, 64, 14, 14)])
+def test_conv3x3_stats_epilogue(shape):
+    """The 3x3 halo kernel's statistics epilogue: same y as the plain launch, per-tile partials
+    match an fp32 recomputation from y (64 -> 64 runs the weight-stationary kernel: no partials)."""
+    N, Ci, Co, H, W = shape
+    torch.manual_seed(0)
+    x = torch.randn(N, Ci, H, W, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(Co, Ci, 3, 3, device="cuda") / (9 * Ci) ** 0.5 + 0.01).bfloat16()
+    r = _native().conv3x3s1_fwd_stats(x, w)
+    y0 = _native().conv3x3s1_fwd(x, w)
+    torch.testing.assert_close(r[0], y0, rtol=0, atol=0)
+    if Ci == 64 and Co == 64:
+        assert len(r) == 1
+        return
+    part = r[1]
+    M = N * H * W
+    T = (M + 255) // 256
+    y2 = r[0].permute(0, 2, 3, 1).reshape(M, Co).float()
+    yf = torch.cat([y2, torch.full((T * 256 - M, Co), float("nan"), device="cuda")]).view(T, 256, Co)
+    valid = ~torch.isnan(yf)
+    s = torch.where(valid, yf, 0).sum(1)
+    mu = s / valid.sum(1).float()
+    m2 = torch.where(valid, (yf - mu[:, None]) ** 2, 0).sum(1)
+    torch.testing.assert_close(part[0], s, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(part[1], m2, rtol=1e-4, atol=1e-3)

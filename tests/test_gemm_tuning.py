@@ -69,7 +69,7 @@ def test_conv1x1_decision_table_roundtrip(tmp_path, monkeypatch):
     assert C._pick(("bwd_weight", "bf16", 802816, 64, 256), {"miopen": None, "gemm": None}) == "miopen"
     import json
     tab = json.load(open(C.TABLE))  # the committed table parses and holds only valid choices
-    assert set(tab.values()) <= {"miopen", "gemm"}
+    assert set(tab.values()) <= {"miopen", "gemm", "ours"}
 
 
 def test_conv1x1_table_covers_bench_default_resnet50():

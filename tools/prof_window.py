@@ -1,6 +1,7 @@
 """Aggregate rocprofv3 kernel-trace rows that fall inside a roctx range (default "timed").
 
-usage: python tools/prof_window.py <rocprof_out_dir> <out_prefix> [range_name] [steps]
+usage: python tools/prof_window.py <rocprof_out_dir> <out_prefix> [range_name] [steps] [occurrence]
+(occurrence: which of several ranges of that name, 0-based; default the last)
 Writes <out_prefix>_kernels.csv (per-kernel totals inside the window) and <out_prefix>.md.
 """
 import csv
@@ -16,11 +17,13 @@ def main():
     steps = int(sys.argv[4]) if len(sys.argv) > 4 else 1
     kt = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)
     mt = glob.glob(os.path.join(d, "**", "*marker_api_trace.csv"), recursive=True)
+    occ = int(sys.argv[5]) if len(sys.argv) > 5 else -1
     lo, hi = 0, float("inf")
     if mt:
-        for r in csv.DictReader(open(mt[0])):
-            if name in (r.get("Function", "") + r.get("Message", "") + r.get("Name", "")):
-                lo, hi = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        ranges = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in csv.DictReader(open(mt[0]))
+                        if name in (r.get("Function", "") + r.get("Message", "") + r.get("Name", "")))
+        if ranges:
+            lo, hi = ranges[occ]
     agg = defaultdict(lambda: [0, 0])
     t_first, t_last = None, None
     for r in csv.DictReader(open(kt[0])):
