@@ -84,8 +84,8 @@ int pdt_stem_conv_wgrad(const uint16_t* x, const uint16_t* dy, uint16_t* dw, flo
 int pdt_maxpool3s2_bwd(const uint16_t* dy, const uint8_t* code, uint16_t* dz, int N, int H, int W, int C,
                        hipStream_t s);
 int pdt_conv1x1_tile_rows();
-int pdt_conv1x1_gemm(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t* c, float* part, int M, int K,
-                     int N, hipStream_t s);
+int pdt_conv1x1_gemm(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t* c, const uint8_t* cm,
+                     float* part, int M, int K, int N, hipStream_t s);
 int64_t pdt_bn_tiles_ws_floats(int T, int C);
 int pdt_bn_fwd_train_tiles(const float* part, int T, int BMt, const uint16_t* x, const uint16_t* res,
                            const float* gamma, const float* beta, float* running_mean, float* running_var,
@@ -435,7 +435,8 @@ std::vector<Tensor> bn_bwd_train(Tensor dy, Tensor x, c10::optional<Tensor> mask
 // out[M,N] = a[M,K] @ b[N,K]^T (+ out, when acc: in-place accumulate). a, b, out: row-major bf16
 // (a 1x1 conv's channels_last activations viewed as [N*H*W, C]). stats: also return the per-tile
 // partials [2, T, N] fp32 (tile sums, centred tile sums of squares; T = ceil(M / 256)).
-c10::optional<Tensor> conv1x1_gemm(Tensor a, Tensor b, Tensor out, bool acc, bool stats) {
+c10::optional<Tensor> conv1x1_gemm(Tensor a, Tensor b, Tensor out, bool acc, bool stats,
+                                   c10::optional<Tensor> c_in, c10::optional<Tensor> c_mask) {
   for (const Tensor* t : {&a, &b, &out}) {
     check_cuda(*t, "conv1x1_gemm operand");
     TORCH_CHECK(t->scalar_type() == at::kBFloat16 && t->dim() == 2 && t->is_contiguous(),
@@ -445,6 +446,22 @@ c10::optional<Tensor> conv1x1_gemm(Tensor a, Tensor b, Tensor out, bool acc, boo
   TORCH_CHECK(b.size(1) == K && out.size(0) == M && out.size(1) == N, "conv1x1_gemm: shape mismatch");
   TORCH_CHECK(K % 32 == 0 && N % 64 == 0, "conv1x1_gemm: K % 32 == 0 and N % 64 == 0 required");
   TORCH_CHECK(!(acc && stats), "conv1x1_gemm: acc and stats are exclusive");
+  // acc source: out itself (in place), or c_in [M, N] (then optionally masked by c_mask, M*N/8 bytes)
+  const uint16_t* cp = acc ? reinterpret_cast<const uint16_t*>(out.data_ptr()) : nullptr;
+  const uint8_t* mp = nullptr;
+  if (c_in.has_value() && c_in->defined()) {
+    TORCH_CHECK(acc, "conv1x1_gemm: c_in needs acc");
+    check_cuda(*c_in, "c_in");
+    TORCH_CHECK(c_in->scalar_type() == at::kBFloat16 && c_in->numel() == M * N && c_in->is_contiguous(
+                    c_in->dim() == 4 ? at::MemoryFormat::ChannelsLast : at::MemoryFormat::Contiguous),
+                "conv1x1_gemm: c_in must be [M, N] bf16 (channels_last when 4-D)");
+    cp = reinterpret_cast<const uint16_t*>(c_in->data_ptr());
+  }
+  if (c_mask.has_value() && c_mask->defined()) {
+    TORCH_CHECK(acc && c_mask->scalar_type() == at::kByte && c_mask->numel() == M * N / 8,
+                "conv1x1_gemm: c_mask must be uint8 [M * N / 8] with acc");
+    mp = c_mask->data_ptr<uint8_t>();
+  }
   c10::optional<Tensor> part;
   if (stats) {
     const int64_t T = (M + pdt_conv1x1_tile_rows() - 1) / pdt_conv1x1_tile_rows();
@@ -452,8 +469,7 @@ c10::optional<Tensor> conv1x1_gemm(Tensor a, Tensor b, Tensor out, bool acc, boo
   }
   const int rc = pdt_conv1x1_gemm(reinterpret_cast<const uint16_t*>(a.data_ptr()),
                                   reinterpret_cast<const uint16_t*>(b.data_ptr()),
-                                  reinterpret_cast<uint16_t*>(out.data_ptr()),
-                                  acc ? reinterpret_cast<const uint16_t*>(out.data_ptr()) : nullptr,
+                                  reinterpret_cast<uint16_t*>(out.data_ptr()), cp, mp,
                                   stats ? part->data_ptr<float>() : nullptr, (int)M, (int)K, (int)N, stream());
   TORCH_CHECK(rc == 0, "pdt_conv1x1_gemm failed: ", rc);
   return part;
@@ -975,7 +991,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_fwd_eval", &bn_fwd_eval);
   m.def("bn_relu_maxpool_fwd", &bn_relu_maxpool_fwd);
   m.def("maxpool3s2_bwd", &maxpool3s2_bwd);
-  m.def("conv1x1_gemm", &conv1x1_gemm);
+  m.def("conv1x1_gemm", &conv1x1_gemm, py::arg("a"), py::arg("b"), py::arg("out"), py::arg("acc"), py::arg("stats"),
+        py::arg("c_in") = py::none(), py::arg("c_mask") = py::none());
   m.def("bn_fwd_train_tiles", &bn_fwd_train_tiles);
   m.def("conv3x3s1_fwd", &conv3x3s1_fwd);
   m.def("conv3x3s1_fwd_stats", &conv3x3s1_fwd_stats);

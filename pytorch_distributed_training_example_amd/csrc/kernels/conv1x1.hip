@@ -88,7 +88,7 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 template <class Cf, bool ACC, bool STATS, bool NT>
 __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv1x1_kernel(
     const uint16_t* __restrict__ A, const uint16_t* __restrict__ B, uint16_t* Y, const uint16_t* Cin,
-    float* __restrict__ part, int M, int K, int N) {
+    const uint8_t* __restrict__ Cmask, float* __restrict__ part, int M, int K, int N) {
   constexpr int BM = Cf::BM, BN = Cf::BN;
   constexpr int WROWS = BM / Cf::WM, WCOLS = BN / Cf::WN;
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -192,8 +192,9 @@ __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv1x1_kernel(
 #pragma unroll
       for (int k = 0; k < 4; ++k) { a[2 * k] = __uint_as_float(w[k] << 16); a[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u); }
       ld8_bf16(Cin + off, cc);
+      const unsigned mb = Cmask ? Cmask[off >> 3] : 0xffu;  // C = Cin * mask: a ReLU's masked gradient
 #pragma unroll
-      for (int k = 0; k < 8; ++k) a[k] += cc[k];
+      for (int k = 0; k < 8; ++k) a[k] += (mb >> k) & 1u ? cc[k] : 0.f;
       v.x = (uint32_t)f2bf(a[0]) | ((uint32_t)f2bf(a[1]) << 16);
       v.y = (uint32_t)f2bf(a[2]) | ((uint32_t)f2bf(a[3]) << 16);
       v.z = (uint32_t)f2bf(a[4]) | ((uint32_t)f2bf(a[5]) << 16);
@@ -211,8 +212,8 @@ __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv1x1_kernel(
 int g_nt = 0;  // PDT_GEMM_NT=1: non-temporal output stores (experiment switch)
 
 template <class Cf, bool ACC, bool STATS, bool NT>
-int launch_nt(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t* c, float* part, int M, int K, int N,
-              hipStream_t s) {
+int launch_nt(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t* c, const uint8_t* cm, float* part,
+              int M, int K, int N, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(&conv1x1_kernel<Cf, ACC, STATS, NT>),
@@ -222,29 +223,29 @@ int launch_nt(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t*
   }
   const int64_t grid = (int64_t)(M + Cf::BM - 1) / Cf::BM * (N / Cf::BN);
   hipLaunchKernelGGL((conv1x1_kernel<Cf, ACC, STATS, NT>), dim3((unsigned)grid), dim3(Cf::kThreads), Cf::kLds, s, a,
-                     b, y, c, part, M, K, N);
+                     b, y, c, cm, part, M, K, N);
   return 0;
 }
 
 template <class Cf, bool ACC, bool STATS>
-int launch(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t* c, float* part, int M, int K, int N,
-           hipStream_t s) {
+int launch(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t* c, const uint8_t* cm, float* part, int M,
+           int K, int N, hipStream_t s) {
   const char* e = getenv("PDT_GEMM_NT");  // read per launch (A/B inside one process)
   g_nt = (e && e[0] == '1') ? 1 : 0;
-  if (g_nt) return launch_nt<Cf, ACC, STATS, true>(a, b, y, c, part, M, K, N, s);
-  return launch_nt<Cf, ACC, STATS, false>(a, b, y, c, part, M, K, N, s);
+  if (g_nt) return launch_nt<Cf, ACC, STATS, true>(a, b, y, c, cm, part, M, K, N, s);
+  return launch_nt<Cf, ACC, STATS, false>(a, b, y, c, cm, part, M, K, N, s);
 }
 
 using GWide = G1<128, 4, 2>;   // N % 128 == 0: 8 waves of 64x64
 using GNarrow = G1<64, 4, 1>;  // N == 64 (or odd multiples of 64): 4 waves of 64x64
 
 template <class Cf>
-int dispatch(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t* c, float* part, int M, int K, int N,
-             hipStream_t s) {
-  if (c && part) return -1;  // not instantiated (no caller needs both)
-  if (c) return launch<Cf, true, false>(a, b, y, c, part, M, K, N, s);
-  if (part) return launch<Cf, false, true>(a, b, y, c, part, M, K, N, s);
-  return launch<Cf, false, false>(a, b, y, c, part, M, K, N, s);
+int dispatch(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t* c, const uint8_t* cm, float* part,
+             int M, int K, int N, hipStream_t s) {
+  if ((c && part) || (cm && !c)) return -1;  // not instantiated (no caller needs both)
+  if (c) return launch<Cf, true, false>(a, b, y, c, cm, part, M, K, N, s);
+  if (part) return launch<Cf, false, true>(a, b, y, c, cm, part, M, K, N, s);
+  return launch<Cf, false, false>(a, b, y, c, cm, part, M, K, N, s);
 }
 
 }  // namespace
@@ -253,14 +254,15 @@ extern "C" {
 
 int pdt_conv1x1_tile_rows() { return 256; }
 
-// y[M,N] = a[M,K] * b[N,K]^T (+ c[M,N]); part: stats of y per 256-row tile (see above), or null.
-// All bf16 row-major, K % 32 == 0, N % 64 == 0, M * max(K, N) < 2^31. c may alias y.
-int pdt_conv1x1_gemm(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t* c, float* part, int M, int K,
-                     int N, hipStream_t s) {
+// y[M,N] = a[M,K] * b[N,K]^T (+ c[M,N], masked by the bit-mask cm when given: bit j of byte
+// (m*N + n) / 8 — the BatchNorm ReLU mask layout); part: stats of y per 256-row tile (see above),
+// or null. All bf16 row-major, K % 32 == 0, N % 64 == 0, M * max(K, N) < 2^31. c may alias y.
+int pdt_conv1x1_gemm(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t* c, const uint8_t* cm,
+                     float* part, int M, int K, int N, hipStream_t s) {
   if (M < 1 || K < 32 || K % 32 != 0 || N < 64 || N % 64 != 0) return -1;
   if ((int64_t)M * (K > N ? K : N) >= ((int64_t)1 << 31) || (int64_t)N * K >= ((int64_t)1 << 31)) return -2;
-  if (N % 128 == 0) return dispatch<GWide>(a, b, y, c, part, M, K, N, s);
-  return dispatch<GNarrow>(a, b, y, c, part, M, K, N, s);
+  if (N % 128 == 0) return dispatch<GWide>(a, b, y, c, cm, part, M, K, N, s);
+  return dispatch<GNarrow>(a, b, y, c, cm, part, M, K, N, s);
 }
 
 }  // extern "C"

@@ -99,7 +99,8 @@ class Bottleneck(nn.Module):
                 and self.conv1.gemm_eligible(x) and x.shape[1] % 64 == 0):
             # the two gradients of x (conv1 branch, shortcut) meet in conv1's data-gradient GEMM
             # (beta = 1) instead of an autograd add kernel (ops/batchnorm.py ResidualGradLink)
-            link = ResidualGradLink()
+            # identity blocks: bn3's backward may hand the shortcut gradient over as (dy, mask)
+            link = ResidualGradLink(lazy=self.downsample is None and self.conv1.masked_residual_ok(x))
             out = bn_act(self.bn1, self.conv1(x, res_link=link), relu=True)
             out = bn_act(self.bn2, self.conv2(out), relu=True)
             out = self.conv3(out)

@@ -40,14 +40,31 @@ class ResidualGradLink:
     ``relu(bn3(x) + identity)`` backward deposits (it always runs first: the main branch is
     upstream of it); downsample blocks: the shortcut conv deposits (ops/conv.py linked_conv)."""
 
-    __slots__ = ("grad",)
+    __slots__ = ("grad", "lazy")
 
-    def __init__(self):
+    def __init__(self, lazy: bool = False):
         self.grad = None
+        # lazy: the depositing BatchNorm hands over (dy, relu mask) instead of writing dres = dy*mask;
+        # the consumer (our 1x1 dgrad GEMM) applies the mask in its accumulate epilogue
+        self.lazy = lazy
 
     def take(self):
         g, self.grad = self.grad, None
         return g
+
+
+class MaskedGrad:
+    """A ReLU'd residual gradient not yet materialised: ``dy * mask`` (mask = the BatchNorm's
+    1-bit ReLU mask, bit j of byte k covers element 8k + j)."""
+
+    __slots__ = ("dy", "mask")
+
+    def __init__(self, dy: torch.Tensor, mask: torch.Tensor):
+        self.dy, self.mask = dy, mask
+
+    def dense(self) -> torch.Tensor:
+        bits = (self.mask.view(-1, 1) >> torch.arange(8, device=self.mask.device, dtype=torch.uint8)) & 1
+        return self.dy * bits.view(self.dy.permute(0, 2, 3, 1).shape).permute(0, 3, 1, 2).to(self.dy.dtype)
 
 
 class _BNTrainFn(torch.autograd.Function):
@@ -75,6 +92,12 @@ class _BNTrainFn(torch.autograd.Function):
         fmt = torch.channels_last if x.dim() == 4 else torch.contiguous_format
         dy = dy.contiguous(memory_format=fmt)
         need_w = ctx.has_weight and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3])
+        if ctx.has_res and ctx.link is not None and ctx.link.lazy and ctx.relu:
+            # the shortcut gradient dy*mask is never written: the consumer's GEMM masks dy itself
+            dx, _, dg, db = native().bn_bwd_train(dy, x, mask, weight, mean, invstd, True, False, need_w)
+            ctx.link.grad = MaskedGrad(dy, mask)
+            return (dx, None, dg if need_w else None, db if need_w else None,
+                    None, None, None, None, None, None, None)
         dx, dres, dg, db = native().bn_bwd_train(dy, x, mask, weight, mean, invstd, ctx.relu,
                                                  ctx.has_res, need_w)
         if ctx.has_res and ctx.link is not None:

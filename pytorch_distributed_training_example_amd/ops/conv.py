@@ -276,7 +276,18 @@ class _Conv1x1Fn(torch.autograd.Function):
         strided = None
         if isinstance(acc, StridedGrad):  # a stride-2 shortcut's compact gradient: added below
             strided, acc = acc, None
-        if ctx.needs_input_grad[0]:
+        from .batchnorm import MaskedGrad
+        if isinstance(acc, MaskedGrad) and ctx.needs_input_grad[0] and _ours_ok("dgrad", M, Co, Ci):
+            # dx = dy*mask + dY W: the shortcut's ReLU-masked gradient applied in the GEMM epilogue
+            from ._native import native
+            dx = torch.empty_like(x)
+            native().conv1x1_gemm(g2, w2.t().contiguous(), _nhwc2d(dx), True, False, acc.dy, acc.mask)
+            acc = None
+        elif isinstance(acc, MaskedGrad):
+            acc = acc.dense()
+        if dx is not None:
+            pass
+        elif ctx.needs_input_grad[0]:
             cands = {"miopen": lambda: conv_bwd([True, False, False]), "gemm": lambda: torch.mm(g2, w2)}
             if gy.dtype == torch.bfloat16 and _ours_ok("dgrad", M, Co, Ci):
                 from ._native import native
@@ -573,6 +584,13 @@ class Conv1x1(nn.Conv2d):
 
     def gemm_eligible(self, x: torch.Tensor) -> bool:
         return self.stride == (1, 1) and self._gemm_ok(x)
+
+    def masked_residual_ok(self, x: torch.Tensor) -> bool:
+        """Our dgrad GEMM can take the shortcut gradient as (dy, ReLU mask) (``MaskedGrad``):
+        ``PDT_RES_MASKED=0`` turns the hand-off off."""
+        N, Ci, H, W = x.shape
+        return (os.environ.get("PDT_RES_MASKED", "1") != "0" and x.dtype == torch.bfloat16
+                and self.gemm_eligible(x) and _ours_ok("dgrad", N * H * W, self.out_channels, Ci))
 
     def strided_gemm_eligible(self, x: torch.Tensor) -> bool:
         s = self.stride[0]

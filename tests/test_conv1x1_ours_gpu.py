@@ -147,3 +147,47 @@ def test_conv3x3_stats_epilogue(shape):
     m2 = torch.where(valid, (yf - mu[:, None]) ** 2, 0).sum(1)
     torch.testing.assert_close(part[0], s, rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(part[1], m2, rtol=1e-4, atol=1e-3)
+
+
+def test_gemm_accumulates_masked_source():
+    """acc from a separate source masked by a BatchNorm ReLU bit-mask (the shortcut hand-off)."""
+    M, K, N = 777, 64, 256
+    a, b = _ab(M, K, N, 5)
+    dy = torch.randn(M, N, device="cuda").bfloat16()
+    bits = torch.rand(M, N, device="cuda") > 0.4
+    mask = (bits.view(-1, 8).to(torch.uint8) << torch.arange(8, device="cuda", dtype=torch.uint8)).sum(1).to(torch.uint8)
+    out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    _native().conv1x1_gemm(a, b, out, True, False, dy, mask)
+    ref = torch.where(bits, dy.float(), 0) + a.float() @ b.float().t()
+    torch.testing.assert_close(out.float(), ref, rtol=2e-2, atol=2e-2)
+    from pytorch_distributed_training_example_amd.ops.batchnorm import MaskedGrad
+    d4 = dy.view(1, 1, M, N).permute(0, 3, 1, 2)  # [1, N, 1, M] channels_last view of [M, N]
+    dense = MaskedGrad(d4, mask).dense()
+    torch.testing.assert_close(dense.permute(0, 2, 3, 1).reshape(M, N).float(), torch.where(bits, dy.float(), 0))
+
+
+@pytest.mark.parametrize("masked", ["1", "0"])
+def test_identity_block_masked_residual_matches_plain(monkeypatch, masked):
+    """Identity Bottleneck: bn3 handing the shortcut gradient over as (dy, mask) gives the same
+    gradients as the materialised dres path and as autograd's own add (link off)."""
+    from pytorch_distributed_training_example_amd.models import resnet as R
+    from pytorch_distributed_training_example_amd.models.precision import to_bf16_mixed
+    torch.manual_seed(0)
+    blk = to_bf16_mixed(R.Bottleneck(256, 64, 1, None).cuda().to(memory_format=torch.channels_last))
+    x0 = torch.randn(8, 256, 14, 14, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    monkeypatch.setenv("PDT_RES_MASKED", masked)
+    monkeypatch.setenv("PDT_CONV1X1", "ours")
+    out = {}
+    for linked in (True, False):
+        R.RESIDUAL_GRAD_LINK[0] = linked
+        try:
+            blk.zero_grad(set_to_none=True)
+            x = x0.clone().requires_grad_(True)
+            y = blk(x)
+            y.backward(torch.ones_like(y) * 0.01 + y.detach() * 0.1)
+            out[linked] = [x.grad.float()] + [p.grad.float().clone() for p in blk.parameters()]
+        finally:
+            R.RESIDUAL_GRAD_LINK[0] = True
+    for a, b in zip(out[True], out[False]):
+        err = ((a - b).norm() / (b.norm() + 1e-12)).item()
+        assert err < 2e-2, err
