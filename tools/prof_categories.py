@@ -8,6 +8,10 @@ def family(n):
         return "our BN (+ReLU/residual/pool)"
     if "conv3x3" in n:
         return "our 3x3 conv (MFMA)"
+    if "conv1x1_kernel" in n:
+        return "our 1x1 conv GEMM (MFMA, fused BN-stats epilogues)"
+    if "stem_" in n:
+        return "our 7x7 stem conv (MFMA)"
     if "Cijk" in n:
         return "hipBLASLt GEMM (1x1 convs, fc)"
     if any(s in n for s in ("igemm", "ck::", "_ZN2ck", "naive_conv", "SubTensor", "fillBuffer", "ranspose")):
