@@ -73,6 +73,9 @@ int pdt_bn_relu_maxpool_fwd_train(const uint16_t* x, const float* gamma, const f
 int pdt_conv3x3s1_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int N, int H, int W, int Ci, int Co,
                       hipStream_t s);
 int pdt_conv3x3_flip_weights(const uint16_t* w, uint16_t* wf, int Co, int Ci, hipStream_t s);
+int pdt_conv3x3s1_fwd_bnbwd(const uint16_t* x, const uint16_t* w, uint16_t* y, const uint16_t* bn_x,
+                            const uint8_t* bn_mask, const float* bn_mean, float* bn_part, int N, int H, int W, int Ci,
+                            int Co, hipStream_t s);
 int pdt_conv3x3s1_fwd_stats(const uint16_t* x, const uint16_t* w, uint16_t* y, float* part, int N, int H, int W,
                             int Ci, int Co, hipStream_t s);
 int64_t pdt_stem_conv_wprep_elems();
@@ -85,7 +88,12 @@ int pdt_maxpool3s2_bwd(const uint16_t* dy, const uint8_t* code, uint16_t* dz, in
                        hipStream_t s);
 int pdt_conv1x1_tile_rows();
 int pdt_conv1x1_gemm(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t* c, const uint8_t* cm,
-                     float* part, int M, int K, int N, hipStream_t s);
+                     float* part, int M, int K, int N, const uint16_t* bn_x, const uint8_t* bn_mask,
+                     const float* bn_mean, float* bn_part, hipStream_t s);
+int pdt_bn_bwd_train_tiles(const float* part, int T, int BMt, const uint16_t* dy, const uint16_t* x,
+                           const uint8_t* mask, const float* gamma, const float* mean, const float* invstd, int64_t M,
+                           int C, int relu, int has_res, uint16_t* dx, uint16_t* dres, float* dgamma, float* dbeta,
+                           float* ws, hipStream_t s);
 int64_t pdt_bn_tiles_ws_floats(int T, int C);
 int pdt_bn_fwd_train_tiles(const float* part, int T, int BMt, const uint16_t* x, const uint16_t* res,
                            const float* gamma, const float* beta, float* running_mean, float* running_var,
@@ -431,12 +439,57 @@ std::vector<Tensor> bn_bwd_train(Tensor dy, Tensor x, c10::optional<Tensor> mask
   return {dx, dres, dg, db};
 }
 
+// BN training backward with the reduction taken from the dy producer's per-tile partials
+// (conv1x1_gemm with bn_x): finalize + apply only.
+std::vector<Tensor> bn_bwd_train_tiles(Tensor dy, Tensor x, Tensor part, c10::optional<Tensor> mask,
+                                       c10::optional<Tensor> weight, Tensor mean, Tensor invstd, bool relu,
+                                       bool has_res, bool need_dgamma) {
+  check_nhwc_bf16(x, "x");
+  TORCH_CHECK(dy.sizes() == x.sizes() && dy.strides() == x.strides(), "pdt bn bwd: dy layout mismatch");
+  const int64_t C = x.size(1);
+  const int64_t M = x.numel() / C;
+  const int BMt = pdt_conv1x1_tile_rows();
+  const int64_t T = (M + BMt - 1) / BMt;
+  TORCH_CHECK(C % 64 == 0, "pdt bn bwd: C must be a multiple of 64");
+  TORCH_CHECK(part.scalar_type() == at::kFloat && part.is_contiguous() && part.dim() == 3 && part.size(0) == 2 &&
+              part.size(1) == T && part.size(2) == C, "bn_bwd_train_tiles: partials [2, T, C] fp32 expected");
+  auto dx = at::empty_like(x);
+  Tensor dres;
+  if (has_res) dres = at::empty_like(x);
+  auto fopt = x.options().dtype(at::kFloat);
+  Tensor dg, db;
+  if (need_dgamma) {
+    dg = at::empty({C}, fopt);
+    db = at::empty({C}, fopt);
+  }
+  auto ws = at::empty({pdt_bn_tiles_ws_floats((int)T, (int)C) + 2 * C}, fopt);
+  const uint8_t* mp = nullptr;
+  if (relu) {
+    TORCH_CHECK(mask.has_value() && mask->defined() && mask->numel() == M * C / 8, "pdt bn bwd: relu needs the mask");
+    mp = mask->data_ptr<uint8_t>();
+  }
+  const int rc = pdt_bn_bwd_train_tiles(part.data_ptr<float>(), (int)T, BMt, reinterpret_cast<const uint16_t*>(dy.data_ptr()),
+                                        reinterpret_cast<const uint16_t*>(x.data_ptr()), mp, opt_fptr(weight),
+                                        mean.data_ptr<float>(), invstd.data_ptr<float>(), M, (int)C, relu, has_res,
+                                        reinterpret_cast<uint16_t*>(dx.data_ptr()),
+                                        has_res ? reinterpret_cast<uint16_t*>(dres.data_ptr()) : nullptr,
+                                        need_dgamma ? dg.data_ptr<float>() : nullptr,
+                                        need_dgamma ? db.data_ptr<float>() : nullptr, ws.data_ptr<float>(), stream());
+  TORCH_CHECK(rc == 0, "pdt_bn_bwd_train_tiles failed: ", rc);
+  return {dx, dres, dg, db};
+}
+
 // ----------------------------------------------------------------------------- 1x1 conv GEMM (+ BN stats)
 // out[M,N] = a[M,K] @ b[N,K]^T (+ out, when acc: in-place accumulate). a, b, out: row-major bf16
 // (a 1x1 conv's channels_last activations viewed as [N*H*W, C]). stats: also return the per-tile
 // partials [2, T, N] fp32 (tile sums, centred tile sums of squares; T = ceil(M / 256)).
+// bn_x / bn_mask / bn_mean: out is the gradient at the output of a BatchNorm with this input
+// (channels_last [M, N] bf16), ReLU bit-mask (or none) and batch mean: return that BatchNorm's
+// backward per-tile partials [2, T, N] fp32 (sum dz, sum dz (x - mean)) instead (not with stats).
 c10::optional<Tensor> conv1x1_gemm(Tensor a, Tensor b, Tensor out, bool acc, bool stats,
-                                   c10::optional<Tensor> c_in, c10::optional<Tensor> c_mask) {
+                                   c10::optional<Tensor> c_in, c10::optional<Tensor> c_mask,
+                                   c10::optional<Tensor> bn_x, c10::optional<Tensor> bn_mask,
+                                   c10::optional<Tensor> bn_mean) {
   for (const Tensor* t : {&a, &b, &out}) {
     check_cuda(*t, "conv1x1_gemm operand");
     TORCH_CHECK(t->scalar_type() == at::kBFloat16 && t->dim() == 2 && t->is_contiguous(),
@@ -463,14 +516,35 @@ c10::optional<Tensor> conv1x1_gemm(Tensor a, Tensor b, Tensor out, bool acc, boo
     mp = c_mask->data_ptr<uint8_t>();
   }
   c10::optional<Tensor> part;
-  if (stats) {
-    const int64_t T = (M + pdt_conv1x1_tile_rows() - 1) / pdt_conv1x1_tile_rows();
+  const int64_t T = (M + pdt_conv1x1_tile_rows() - 1) / pdt_conv1x1_tile_rows();
+  if (stats) part = at::empty({2, T, N}, a.options().dtype(at::kFloat));
+  const bool bstats = bn_x.has_value() && bn_x->defined();
+  const uint16_t* bx = nullptr;
+  const uint8_t* bm = nullptr;
+  const float* bmean = nullptr;
+  if (bstats) {
+    TORCH_CHECK(!stats, "conv1x1_gemm: stats and bn_x are exclusive");
+    check_cuda(*bn_x, "bn_x");
+    TORCH_CHECK(bn_x->scalar_type() == at::kBFloat16 && bn_x->numel() == M * N && bn_x->is_contiguous(
+                    bn_x->dim() == 4 ? at::MemoryFormat::ChannelsLast : at::MemoryFormat::Contiguous),
+                "conv1x1_gemm: bn_x must be [M, N] bf16 (channels_last when 4-D)");
+    TORCH_CHECK(bn_mean.has_value() && bn_mean->defined() && bn_mean->scalar_type() == at::kFloat &&
+                bn_mean->numel() == N && bn_mean->is_contiguous() && bn_mean->is_cuda(),
+                "conv1x1_gemm: bn_mean must be fp32 [N]");
+    if (bn_mask.has_value() && bn_mask->defined()) {
+      TORCH_CHECK(bn_mask->scalar_type() == at::kByte && bn_mask->numel() == M * N / 8 && bn_mask->is_cuda(),
+                  "conv1x1_gemm: bn_mask must be uint8 [M * N / 8]");
+      bm = bn_mask->data_ptr<uint8_t>();
+    }
+    bx = reinterpret_cast<const uint16_t*>(bn_x->data_ptr());
+    bmean = bn_mean->data_ptr<float>();
     part = at::empty({2, T, N}, a.options().dtype(at::kFloat));
   }
   const int rc = pdt_conv1x1_gemm(reinterpret_cast<const uint16_t*>(a.data_ptr()),
                                   reinterpret_cast<const uint16_t*>(b.data_ptr()),
                                   reinterpret_cast<uint16_t*>(out.data_ptr()), cp, mp,
-                                  stats ? part->data_ptr<float>() : nullptr, (int)M, (int)K, (int)N, stream());
+                                  stats ? part->data_ptr<float>() : nullptr, (int)M, (int)K, (int)N, bx, bm, bmean,
+                                  bstats ? part->data_ptr<float>() : nullptr, stream());
   TORCH_CHECK(rc == 0, "pdt_conv1x1_gemm failed: ", rc);
   return part;
 }
@@ -545,6 +619,41 @@ std::vector<Tensor> conv3x3s1_fwd_stats(Tensor x, Tensor w) {
                                          (int)H, (int)W, (int)Ci, (int)Co, stream());
   if (rc == -5) return {conv3x3s1_fwd(x, w)};
   TORCH_CHECK(rc == 0, "pdt_conv3x3s1_fwd_stats failed: ", rc);
+  return {y, part};
+}
+
+// y = conv3x3s1(x, w) where y is the gradient at a BatchNorm's output (bn_x: that BN's input, same
+// shape as y; bn_mask: its ReLU bit-mask or none; bn_mean: its batch mean): returns {y, partials
+// [2, T, Co]} of the BN's backward reduction, or {y} where only a kernel without the epilogue applies.
+std::vector<Tensor> conv3x3s1_fwd_bnbwd(Tensor x, Tensor w, Tensor bn_x, c10::optional<Tensor> bn_mask,
+                                        Tensor bn_mean) {
+  check_nhwc_bf16(x, "x");
+  check_nhwc_bf16(bn_x, "bn_x");
+  TORCH_CHECK(w.dim() == 4 && w.size(2) == 3 && w.size(3) == 3 && w.size(1) == x.size(1) &&
+              w.scalar_type() == at::kBFloat16, "conv3x3: weight [Co, Ci, 3, 3] bf16");
+  w = w.contiguous(at::MemoryFormat::ChannelsLast);
+  const int64_t N = x.size(0), Ci = x.size(1), H = x.size(2), W = x.size(3), Co = w.size(0);
+  TORCH_CHECK(bn_x.size(0) == N && bn_x.size(1) == Co && bn_x.size(2) == H && bn_x.size(3) == W,
+              "conv3x3s1_fwd_bnbwd: bn_x must have the output's shape");
+  TORCH_CHECK(bn_mean.scalar_type() == at::kFloat && bn_mean.numel() == Co && bn_mean.is_contiguous() &&
+              bn_mean.is_cuda(), "conv3x3s1_fwd_bnbwd: bn_mean fp32 [Co]");
+  const uint8_t* mp = nullptr;
+  if (bn_mask.has_value() && bn_mask->defined()) {
+    TORCH_CHECK(bn_mask->scalar_type() == at::kByte && bn_mask->numel() == N * H * W * Co / 8 && bn_mask->is_cuda(),
+                "conv3x3s1_fwd_bnbwd: bn_mask uint8 [M * Co / 8]");
+    mp = bn_mask->data_ptr<uint8_t>();
+  }
+  auto y = at::empty({N, Co, H, W}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const int64_t T = (N * H * W + pdt_conv1x1_tile_rows() - 1) / pdt_conv1x1_tile_rows();
+  auto part = at::empty({2, T, Co}, x.options().dtype(at::kFloat));
+  const int rc = pdt_conv3x3s1_fwd_bnbwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                                         reinterpret_cast<const uint16_t*>(w.data_ptr()),
+                                         reinterpret_cast<uint16_t*>(y.data_ptr()),
+                                         reinterpret_cast<const uint16_t*>(bn_x.data_ptr()), mp,
+                                         bn_mean.data_ptr<float>(), part.data_ptr<float>(), (int)N, (int)H, (int)W,
+                                         (int)Ci, (int)Co, stream());
+  if (rc == -5) return {conv3x3s1_fwd(x, w)};
+  TORCH_CHECK(rc == 0, "pdt_conv3x3s1_fwd_bnbwd failed: ", rc);
   return {y, part};
 }
 
@@ -992,10 +1101,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_relu_maxpool_fwd", &bn_relu_maxpool_fwd);
   m.def("maxpool3s2_bwd", &maxpool3s2_bwd);
   m.def("conv1x1_gemm", &conv1x1_gemm, py::arg("a"), py::arg("b"), py::arg("out"), py::arg("acc"), py::arg("stats"),
-        py::arg("c_in") = py::none(), py::arg("c_mask") = py::none());
+        py::arg("c_in") = py::none(), py::arg("c_mask") = py::none(), py::arg("bn_x") = py::none(),
+        py::arg("bn_mask") = py::none(), py::arg("bn_mean") = py::none());
+  m.def("bn_bwd_train_tiles", &bn_bwd_train_tiles);
   m.def("bn_fwd_train_tiles", &bn_fwd_train_tiles);
   m.def("conv3x3s1_fwd", &conv3x3s1_fwd);
   m.def("conv3x3s1_fwd_stats", &conv3x3s1_fwd_stats);
+  m.def("conv3x3s1_fwd_bnbwd", &conv3x3s1_fwd_bnbwd);
   m.def("conv3x3_flip", &conv3x3_flip);
   m.def("stem_conv_fwd", &stem_conv_fwd);
   m.def("stem_conv_wgrad", &stem_conv_wgrad);

@@ -585,8 +585,10 @@ __global__ __launch_bounds__(1024) void bn_fin_kernel(const float* __restrict__ 
 // part = [T][C] tile sums, then [T][C] centred tile sums of squares, tiles of BMt rows). Level 1:
 // block (64 channels, tile range) -> double (S, Q) with Q = sum_t (M2_t + S_t^2 / n_t) — the
 // between-tile term in double, so E[x^2] - mean^2 never cancels in fp32. Level 2 finalizes.
+// CENTRED = false (backward partials: sum dz, sum dz (x - mean)): plain double sums, Q = sum_t q_t.
 constexpr int kTilesPerBlock = 128;
 
+template <bool CENTRED>
 __global__ __launch_bounds__(1024) void bn_tiles_l1_kernel(const float* __restrict__ part, int T, int BMt, int64_t M,
                                                            int C, double* __restrict__ out) {
   __shared__ double sm[2][16][64];
@@ -601,7 +603,7 @@ __global__ __launch_bounds__(1024) void bn_tiles_l1_kernel(const float* __restri
     const int64_t rem = M - (int64_t)t * BMt;
     const double n = (double)(rem < BMt ? rem : BMt);
     S += (double)s;
-    Q += (double)q + (double)s * (double)s / n;
+    Q += CENTRED ? (double)q + (double)s * (double)s / n : (double)q;
   }
   sm[0][j][cl] = S;
   sm[1][j][cl] = Q;
@@ -624,6 +626,16 @@ __global__ void bn_tiles_l2_kernel(const double* __restrict__ in, int P, int C, 
   const double inv_m = 1.0 / (double)fa.M;
   const double mu = s * inv_m;
   bn_set_fwd(c, mu, q * inv_m - mu * mu, fa);
+}
+
+// Backward finalize from the level-1 sums: S = sum dz, Q = sum dz (x - mean) -> dgamma / dbeta / A, B, D.
+__global__ void bn_tiles_l2b_kernel(const double* __restrict__ in, int P, int C, FinArgs fa) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0, q = 0.0;
+#pragma unroll 8
+  for (int p = 0; p < P; ++p) { s += in[((int64_t)p * C + c) * 2]; q += in[((int64_t)p * C + c) * 2 + 1]; }
+  bn_finalize<1>(c, (float)s, (float)q, fa);
 }
 
 __global__ void bn_eval_coef_kernel(int C, const float* __restrict__ gamma, const float* __restrict__ beta,
@@ -1049,7 +1061,7 @@ int pdt_bn_fwd_train_tiles(const float* part, int T, int BMt, const uint16_t* x,
   fa.gamma = gamma; fa.beta = beta; fa.mean_out = mean; fa.invstd_out = invstd; fa.a_out = a;
   fa.b_out = b; fa.running_mean = running_mean; fa.running_var = running_var; fa.momentum = momentum;
   fa.eps = eps; fa.M = M;
-  hipLaunchKernelGGL(bn_tiles_l1_kernel, dim3(C / 64, P), dim3(1024), 0, s, part, T, BMt, M, C, lv);
+  hipLaunchKernelGGL(bn_tiles_l1_kernel<true>, dim3(C / 64, P), dim3(1024), 0, s, part, T, BMt, M, C, lv);
   hipLaunchKernelGGL(bn_tiles_l2_kernel, dim3((C + 255) / 256), dim3(256), 0, s, lv, P, C, fa);
   const int64_t nvec = M * C / 8;
   const int fixed = (2048 % C) == 0;
@@ -1134,6 +1146,39 @@ int pdt_bn_bwd_train(const uint16_t* dy, const uint16_t* x, const uint8_t* mask,
   fa.M = M;
   if (relu) launch_reduce<2>(x, dy, mask, mean, M, C, ws, counters, fa, s);
   else launch_reduce<1>(x, dy, mask, mean, M, C, ws, counters, fa, s);
+  const int64_t nvec = M * C / 8;
+  const int fixed = (2048 % C) == 0;
+  const int grid = apply_grid(nvec);
+#define PDT_BAPPLY(RL, RS)                                                                                      \
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<RL, RS, 1>), dim3(grid), dim3(256), 0, s, dy, x, mask, mean, A, B, D, \
+                     dx, dres, nvec, C, fixed)
+  if (relu && has_res) PDT_BAPPLY(true, true);
+  else if (relu) PDT_BAPPLY(true, false);
+  else if (has_res) PDT_BAPPLY(false, true);
+  else PDT_BAPPLY(false, false);
+#undef PDT_BAPPLY
+  return 0;
+}
+
+// Training backward whose reduction (sum dz, sum dz (x - mean), dz = dy * mask) comes from the
+// per-tile partials [2][T][C] written by the kernel that produced dy (conv1x1.hip BSTATS): finalize
+// (2 small launches) + apply, no reduce pass over (dy, x). ws: pdt_bn_tiles_ws_floats(T, C) + 2C floats.
+int pdt_bn_bwd_train_tiles(const float* part, int T, int BMt, const uint16_t* dy, const uint16_t* x,
+                           const uint8_t* mask, const float* gamma, const float* mean, const float* invstd, int64_t M,
+                           int C, int relu, int has_res, uint16_t* dx, uint16_t* dres, float* dgamma, float* dbeta,
+                           float* ws, hipStream_t s) {
+  if (C % kCC != 0 || M < 1 || T != (int)((M + BMt - 1) / BMt)) return -1;
+  if (relu && !mask) return -2;
+  const int P = (T + kTilesPerBlock - 1) / kTilesPerBlock;
+  double* lv = reinterpret_cast<double*>(ws);
+  float* A = ws + 4 * (int64_t)P * C;
+  float* B = A + C;
+  float* D = B + C;
+  FinArgs fa{};
+  fa.gamma = gamma; fa.invstd = invstd; fa.dgamma = dgamma; fa.dbeta = dbeta; fa.A = A; fa.B = B; fa.D = D;
+  fa.M = M;
+  hipLaunchKernelGGL(bn_tiles_l1_kernel<false>, dim3(C / 64, P), dim3(1024), 0, s, part, T, BMt, M, C, lv);
+  hipLaunchKernelGGL(bn_tiles_l2b_kernel, dim3((C + 255) / 256), dim3(256), 0, s, lv, P, C, fa);
   const int64_t nvec = M * C / 8;
   const int fixed = (2048 % C) == 0;
   const int grid = apply_grid(nvec);

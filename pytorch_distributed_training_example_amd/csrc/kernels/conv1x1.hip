@@ -27,6 +27,13 @@
 //   * epilogue: the bf16 tile is staged through LDS, the statistics are taken from the staged
 //     (rounded) values, and the tile leaves as whole 16-B row pieces (C added there, fp32);
 //   * block -> tile map XCD-aware (xcd_remap): the N-tiles of one pixel tile share an L2.
+//
+//   BSTATS (data grad only): the output Y is the gradient dy at a BatchNorm's output, and that
+//                 BatchNorm's backward reduction is taken here instead of in a separate pass over
+//                 (dy, x): per 256-pixel tile, per channel, sum(dz) and sum(dz * (xb - mean)) with
+//                 dz = dy * relu mask (xb, mask, mean: the BatchNorm's saved input / mask / mean;
+//                 dz from the bf16 values written). The pass that would re-read dy is gone; xb is
+//                 read once here instead (ops/batchnorm.py GradStatsSource, bn_bwd_train_tiles).
 #include "../common.h"
 #include "../tile_stats.h"
 
@@ -85,10 +92,10 @@ __device__ __forceinline__ void wait_vm() {
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 // NT: streaming (non-temporal) output stores
-template <class Cf, bool ACC, bool STATS, bool NT>
+template <class Cf, bool ACC, bool STATS, bool NT, bool BSTATS>
 __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv1x1_kernel(
     const uint16_t* __restrict__ A, const uint16_t* __restrict__ B, uint16_t* Y, const uint16_t* Cin,
-    const uint8_t* __restrict__ Cmask, float* __restrict__ part, int M, int K, int N) {
+    const uint8_t* __restrict__ Cmask, float* __restrict__ part, int M, int K, int N, BnSrc bs) {
   constexpr int BM = Cf::BM, BN = Cf::BN;
   constexpr int WROWS = BM / Cf::WM, WCOLS = BN / Cf::WN;
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -180,12 +187,27 @@ __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv1x1_kernel(
                                                          min(BM, M - m0), part, mt, (M + BM - 1) / BM, N, n0);
 
   constexpr int kChunks = BN / 8;
+  static_assert(Cf::kThreads % kChunks == 0, "a thread keeps one 8-channel chunk");
+  float bs1[8], bs2[8], bmu[8];
+  if constexpr (BSTATS) {
+    const int c = tid % kChunks;
+    *reinterpret_cast<float4*>(bmu) = *reinterpret_cast<const float4*>(bs.mean + n0 + c * 8);
+    *reinterpret_cast<float4*>(bmu + 4) = *reinterpret_cast<const float4*>(bs.mean + n0 + c * 8 + 4);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { bs1[k] = 0.f; bs2[k] = 0.f; }
+  }
   for (int idx = tid; idx < BM * kChunks; idx += Cf::kThreads) {
     const int r = idx / kChunks, c = idx % kChunks;
     const int m = m0 + r;
     if (m >= M) continue;
     uint4 v = *reinterpret_cast<const uint4*>(lds + r * Cf::kEpiStride + c * 16);
     const int64_t off = (int64_t)m * N + n0 + c * 8;
+    uint4 xb;
+    unsigned bmk = 0xffu;
+    if constexpr (BSTATS) {  // issued before the accumulate's loads: both in flight together
+      xb = *reinterpret_cast<const uint4*>(bs.x + off);
+      if (bs.mask) bmk = bs.mask[off >> 3];
+    }
     if constexpr (ACC) {
       float a[8], cc[8];
       const uint32_t w[4] = {v.x, v.y, v.z, v.w};
@@ -200,6 +222,7 @@ __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv1x1_kernel(
       v.z = (uint32_t)f2bf(a[4]) | ((uint32_t)f2bf(a[5]) << 16);
       v.w = (uint32_t)f2bf(a[6]) | ((uint32_t)f2bf(a[7]) << 16);
     }
+    if constexpr (BSTATS) bn_bwd_accum8(v, xb, bmk, bmu, bs1, bs2);
     if constexpr (NT) {
       const u32x4 t = {v.x, v.y, v.z, v.w};
       __builtin_nontemporal_store(t, reinterpret_cast<u32x4*>(Y + off));
@@ -207,33 +230,36 @@ __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv1x1_kernel(
       *reinterpret_cast<uint4*>(Y + off) = v;
     }
   }
+
+  if constexpr (BSTATS)  // every wave is done reading the staged tile: its LDS holds the block sums
+    bn_bwd_tile_store<BN, Cf::kWaves>(bs1, bs2, reinterpret_cast<float*>(lds), bs.part, (M + BM - 1) / BM, mt, N, n0);
 }
 
 int g_nt = 0;  // PDT_GEMM_NT=1: non-temporal output stores (experiment switch)
 
-template <class Cf, bool ACC, bool STATS, bool NT>
+template <class Cf, bool ACC, bool STATS, bool NT, bool BSTATS>
 int launch_nt(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t* c, const uint8_t* cm, float* part,
-              int M, int K, int N, hipStream_t s) {
+              int M, int K, int N, const BnSrc& bs, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&conv1x1_kernel<Cf, ACC, STATS, NT>),
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&conv1x1_kernel<Cf, ACC, STATS, NT, BSTATS>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, Cf::kLds) != hipSuccess)
       return -3;
     attr = true;
   }
   const int64_t grid = (int64_t)(M + Cf::BM - 1) / Cf::BM * (N / Cf::BN);
-  hipLaunchKernelGGL((conv1x1_kernel<Cf, ACC, STATS, NT>), dim3((unsigned)grid), dim3(Cf::kThreads), Cf::kLds, s, a,
-                     b, y, c, cm, part, M, K, N);
+  hipLaunchKernelGGL((conv1x1_kernel<Cf, ACC, STATS, NT, BSTATS>), dim3((unsigned)grid), dim3(Cf::kThreads), Cf::kLds,
+                     s, a, b, y, c, cm, part, M, K, N, bs);
   return 0;
 }
 
-template <class Cf, bool ACC, bool STATS>
+template <class Cf, bool ACC, bool STATS, bool BSTATS = false>
 int launch(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t* c, const uint8_t* cm, float* part, int M,
-           int K, int N, hipStream_t s) {
+           int K, int N, const BnSrc& bs, hipStream_t s) {
   const char* e = getenv("PDT_GEMM_NT");  // read per launch (A/B inside one process)
   g_nt = (e && e[0] == '1') ? 1 : 0;
-  if (g_nt) return launch_nt<Cf, ACC, STATS, true>(a, b, y, c, cm, part, M, K, N, s);
-  return launch_nt<Cf, ACC, STATS, false>(a, b, y, c, cm, part, M, K, N, s);
+  if (g_nt) return launch_nt<Cf, ACC, STATS, true, BSTATS>(a, b, y, c, cm, part, M, K, N, bs, s);
+  return launch_nt<Cf, ACC, STATS, false, BSTATS>(a, b, y, c, cm, part, M, K, N, bs, s);
 }
 
 using GWide = G1<128, 4, 2>;   // N % 128 == 0: 8 waves of 64x64
@@ -241,11 +267,16 @@ using GNarrow = G1<64, 4, 1>;  // N == 64 (or odd multiples of 64): 4 waves of 6
 
 template <class Cf>
 int dispatch(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t* c, const uint8_t* cm, float* part,
-             int M, int K, int N, hipStream_t s) {
-  if ((c && part) || (cm && !c)) return -1;  // not instantiated (no caller needs both)
-  if (c) return launch<Cf, true, false>(a, b, y, c, cm, part, M, K, N, s);
-  if (part) return launch<Cf, false, true>(a, b, y, c, cm, part, M, K, N, s);
-  return launch<Cf, false, false>(a, b, y, c, cm, part, M, K, N, s);
+             int M, int K, int N, const BnSrc& bs, hipStream_t s) {
+  if ((c && part) || (cm && !c) || (part && bs.part)) return -1;  // not instantiated (no caller needs both)
+  if (bs.part) {
+    if (!bs.x || !bs.mean) return -1;
+    if (c) return launch<Cf, true, false, true>(a, b, y, c, cm, part, M, K, N, bs, s);
+    return launch<Cf, false, false, true>(a, b, y, c, cm, part, M, K, N, bs, s);
+  }
+  if (c) return launch<Cf, true, false>(a, b, y, c, cm, part, M, K, N, bs, s);
+  if (part) return launch<Cf, false, true>(a, b, y, c, cm, part, M, K, N, bs, s);
+  return launch<Cf, false, false>(a, b, y, c, cm, part, M, K, N, bs, s);
 }
 
 }  // namespace
@@ -257,12 +288,17 @@ int pdt_conv1x1_tile_rows() { return 256; }
 // y[M,N] = a[M,K] * b[N,K]^T (+ c[M,N], masked by the bit-mask cm when given: bit j of byte
 // (m*N + n) / 8 — the BatchNorm ReLU mask layout); part: stats of y per 256-row tile (see above),
 // or null. All bf16 row-major, K % 32 == 0, N % 64 == 0, M * max(K, N) < 2^31. c may alias y.
+// bn_x / bn_mask / bn_mean / bn_part (BSTATS, all null = off): y is the gradient at the output of a
+// BatchNorm with input bn_x [M,N], ReLU mask bn_mask (or null) and mean bn_mean [N]; bn_part
+// [2][T][N] receives that BatchNorm's backward per-tile sums (see the header). Not with part.
 int pdt_conv1x1_gemm(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t* c, const uint8_t* cm,
-                     float* part, int M, int K, int N, hipStream_t s) {
+                     float* part, int M, int K, int N, const uint16_t* bn_x, const uint8_t* bn_mask,
+                     const float* bn_mean, float* bn_part, hipStream_t s) {
   if (M < 1 || K < 32 || K % 32 != 0 || N < 64 || N % 64 != 0) return -1;
   if ((int64_t)M * (K > N ? K : N) >= ((int64_t)1 << 31) || (int64_t)N * K >= ((int64_t)1 << 31)) return -2;
-  if (N % 128 == 0) return dispatch<GWide>(a, b, y, c, cm, part, M, K, N, s);
-  return dispatch<GNarrow>(a, b, y, c, cm, part, M, K, N, s);
+  const BnSrc bs{bn_x, bn_mask, bn_mean, bn_part};
+  if (N % 128 == 0) return dispatch<GWide>(a, b, y, c, cm, part, M, K, N, bs, s);
+  return dispatch<GNarrow>(a, b, y, c, cm, part, M, K, N, bs, s);
 }
 
 }  // extern "C"

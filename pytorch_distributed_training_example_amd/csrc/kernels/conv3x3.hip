@@ -263,10 +263,12 @@ struct HCfg {
 
 __device__ __forceinline__ int chk64(int row, int p) { return p ^ (((row >> 2) & 1) << 1); }  // = swz<64>, involution
 
-template <class Cf, bool STATS = false>
+// BSTATS: Y is the gradient at a BatchNorm's output (this launch is a data gradient): its backward
+// reduction is taken in the epilogue (tile_stats.h bn_bwd_accum8 / bn_bwd_tile_store).
+template <class Cf, bool STATS = false, bool BSTATS = false>
 __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv3x3h_kernel(
     const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wt, uint16_t* __restrict__ Y, int N, int H, int W,
-    int Ci, int Co, float* __restrict__ part) {
+    int Ci, int Co, float* __restrict__ part, BnSrc bs) {
   constexpr int BM = Cf::BM, BN = Cf::BN, BK = Cf::BK;
   constexpr int WROWS = BM / Cf::WM, WCOLS = BN / Cf::WN;
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -405,13 +407,32 @@ __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv3x3h_kernel(
     tile_bn_stats<BM, BN, Cf::kThreads, Cf::kEpiStride>(lds, reinterpret_cast<float*>(lds + BM * Cf::kEpiStride),
                                                          min(BM, M - m0), part, m0 / BM, (M + BM - 1) / BM, Co, n0);
   constexpr int kChunks = BN / 8;
+  static_assert(Cf::kThreads % kChunks == 0, "a thread keeps one 8-channel chunk");
+  float bs1[8], bs2[8], bmu[8];
+  if constexpr (BSTATS) {
+    const int c = tid % kChunks;
+    *reinterpret_cast<float4*>(bmu) = *reinterpret_cast<const float4*>(bs.mean + n0 + c * 8);
+    *reinterpret_cast<float4*>(bmu + 4) = *reinterpret_cast<const float4*>(bs.mean + n0 + c * 8 + 4);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { bs1[k] = 0.f; bs2[k] = 0.f; }
+  }
   for (int idx = tid; idx < BM * kChunks; idx += Cf::kThreads) {
     const int r = idx / kChunks, cc = idx % kChunks;
     const int m = m0 + r;
-    if (m < M)
-      *reinterpret_cast<uint4*>(Y + (int64_t)m * Co + n0 + cc * 8) =
-          *reinterpret_cast<const uint4*>(lds + r * Cf::kEpiStride + cc * 16);
+    if (m < M) {
+      const int64_t off = (int64_t)m * Co + n0 + cc * 8;
+      const uint4 v = *reinterpret_cast<const uint4*>(lds + r * Cf::kEpiStride + cc * 16);
+      if constexpr (BSTATS) {
+        const uint4 xb = *reinterpret_cast<const uint4*>(bs.x + off);
+        const unsigned mk = bs.mask ? bs.mask[off >> 3] : 0xffu;
+        bn_bwd_accum8(v, xb, mk, bmu, bs1, bs2);
+      }
+      *reinterpret_cast<uint4*>(Y + off) = v;
+    }
   }
+  if constexpr (BSTATS)  // every wave is done reading the staged tile: its LDS holds the block sums
+    bn_bwd_tile_store<BN, Cf::kWaves>(bs1, bs2, reinterpret_cast<float*>(lds), bs.part, (M + BM - 1) / BM, m0 / BM,
+                                      Co, n0);
 }
 
 // ---------------------------------------------------------------- warp-specialised halo variant
@@ -956,12 +977,12 @@ inline int64_t halo_rows_bound(int H, int W, int BM) {
   return (rows + 2 * imgs) * (W + 2);
 }
 
-template <class Cf, bool STATS = false>
+template <class Cf, bool STATS = false, bool BSTATS = false>
 int launch_h(const uint16_t* x, const uint16_t* w, uint16_t* y, int N, int H, int W, int Ci, int Co, hipStream_t s,
-             float* part = nullptr) {
+             float* part = nullptr, const BnSrc& bs = BnSrc{}) {
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3h_kernel<Cf, STATS>),
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3h_kernel<Cf, STATS, BSTATS>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, Cf::kLds) != hipSuccess)
       return -3;
     attr = true;
@@ -970,8 +991,8 @@ int launch_h(const uint16_t* x, const uint16_t* w, uint16_t* y, int N, int H, in
   if (halo_rows_bound(H, W, Cf::BM) > Cf::kHaloRows) return -4;
   const int64_t M = (int64_t)N * H * W;
   const int64_t grid = (M + Cf::BM - 1) / Cf::BM * (Co / Cf::BN);
-  hipLaunchKernelGGL((conv3x3h_kernel<Cf, STATS>), dim3((unsigned)grid), dim3(Cf::kThreads), Cf::kLds, s, x, w, y, N,
-                     H, W, Ci, Co, part);
+  hipLaunchKernelGGL((conv3x3h_kernel<Cf, STATS, BSTATS>), dim3((unsigned)grid), dim3(Cf::kThreads), Cf::kLds, s, x, w,
+                     y, N, H, W, Ci, Co, part, bs);
   return 0;
 }
 
@@ -1085,6 +1106,23 @@ int pdt_conv3x3s1_fwd_stats(const uint16_t* x, const uint16_t* w, uint16_t* y, f
   if (halo_rows_bound(H, W, 256) > 512) return -5;
   return Co % 128 == 0 ? launch_h<HWide, true>(x, w, y, N, H, W, Ci, Co, s, part)
                        : launch_h<HNarrow, true>(x, w, y, N, H, W, Ci, Co, s, part);
+}
+
+// Data gradient y = conv3x3(dy, flipped w) whose output y is the gradient at a BatchNorm's output
+// (input bn_x [N,H,W,Co] bf16, ReLU bit-mask bn_mask or null, batch mean bn_mean [Co]): also writes
+// that BatchNorm's backward per-tile partials bn_part [2][T][Co] (tile_stats.h). Halo kernel only:
+// returns -5 where another kernel would run (caller falls back to a plain launch + reduce pass).
+int pdt_conv3x3s1_fwd_bnbwd(const uint16_t* x, const uint16_t* w, uint16_t* y, const uint16_t* bn_x,
+                            const uint8_t* bn_mask, const float* bn_mean, float* bn_part, int N, int H, int W, int Ci,
+                            int Co, hipStream_t s) {
+  if (Ci % 32 != 0 || Co % 64 != 0 || N < 1 || H < 1 || W < 1 || !bn_x || !bn_mean || !bn_part) return -1;
+  const int64_t M = (int64_t)N * H * W;
+  if (M * (Ci > Co ? Ci : Co) >= (int64_t)1 << 31 || (int64_t)Co * 9 * Ci >= (int64_t)1 << 31) return -2;
+  if (Ci == 64 && Co == 64) return -5;
+  if (halo_rows_bound(H, W, 256) > 512) return -5;
+  const BnSrc bs{bn_x, bn_mask, bn_mean, bn_part};
+  return Co % 128 == 0 ? launch_h<HWide, false, true>(x, w, y, N, H, W, Ci, Co, s, nullptr, bs)
+                       : launch_h<HNarrow, false, true>(x, w, y, N, H, W, Ci, Co, s, nullptr, bs);
 }
 
 // Weight gradient of the stride-1 pad-1 3x3 conv: dw[Co,3,3,Ci] (bf16) from x[N,H,W,Ci] and

@@ -61,4 +61,65 @@ __device__ __forceinline__ void tile_bn_stats(const char* tile, float* red, int 
 template <int BM, int BN, int THREADS>
 constexpr int tile_bn_stats_lds() { return (THREADS / (BN / 2)) * BN * 4; }
 
+// ---- BatchNorm BACKWARD reduction in the epilogue of the kernel that writes dy (the gradient at a
+// BatchNorm's output): per tile, per channel, sum(dz) and sum(dz * (x - mean)), dz = dy * ReLU mask.
+// part layout as above ([T][N] sums of dz, then [T][N] sums of dz (x - mean)); the finalize is
+// bn_bwd_train_tiles (kernels/batchnorm.hip).
+struct BnSrc {
+  const uint16_t* x;    // the BatchNorm's input [M, N] bf16
+  const uint8_t* mask;  // its ReLU bit-mask (bit j of byte (m*N + n)/8) or null
+  const float* mean;    // its batch mean [N]
+  float* part;          // [2][T][N] output
+};
+
+// One 8-channel piece of the written tile: dy (bf16 x 8, as stored), the BatchNorm input at the same
+// place and its mask byte; mu = the 8 channels' means.
+__device__ __forceinline__ void bn_bwd_accum8(uint4 v, uint4 xb, unsigned mk, const float (&mu)[8], float (&s1)[8],
+                                              float (&s2)[8]) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w}, xw[4] = {xb.x, xb.y, xb.z, xb.w};
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const uint32_t gb = k & 1 ? (w[k >> 1] & 0xffff0000u) : (w[k >> 1] << 16);
+    const uint32_t xv = k & 1 ? (xw[k >> 1] & 0xffff0000u) : (xw[k >> 1] << 16);
+    const float g = (mk >> k) & 1u ? __uint_as_float(gb) : 0.f;
+    s1[k] += g;
+    s2[k] += g * (__uint_as_float(xv) - mu[k]);
+  }
+}
+
+// Block-wide sum of every thread's (s1, s2) for its chunk (tid % CHUNKS; CHUNKS = BN/8 divides 64)
+// and the tile's partials store. `red`: WAVES * 2 * BN floats of LDS no one reads any more
+// (contains __syncthreads: every thread of the block must call it).
+template <int BN, int WAVES>
+__device__ __forceinline__ void bn_bwd_tile_store(float (&s1)[8], float (&s2)[8], float* red, float* __restrict__ part,
+                                                  int T, int mt, int N, int n0) {
+  constexpr int kChunks = BN / 8;
+  static_assert(64 % kChunks == 0, "chunk lanes");
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  // lanes of one wave holding the same chunk differ in the lane bits >= log2(kChunks)
+#pragma unroll
+  for (int sh = kChunks; sh < 64; sh <<= 1)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      s1[k] += __shfl_xor(s1[k], sh, 64);
+      s2[k] += __shfl_xor(s2[k], sh, 64);
+    }
+  __syncthreads();
+  if (lane < kChunks) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      red[(wid * 2) * BN + lane * 8 + k] = s1[k];
+      red[(wid * 2 + 1) * BN + lane * 8 + k] = s2[k];
+    }
+  }
+  __syncthreads();
+  for (int q = tid; q < 2 * BN; q += WAVES * 64) {
+    const int st = q / BN, ch = q % BN;
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < WAVES; ++w) t += red[(w * 2 + st) * BN + ch];
+    part[((int64_t)st * T + mt) * N + n0 + ch] = t;
+  }
+}
+
 }  // namespace pdt

@@ -13,6 +13,7 @@ CPU tests and as the numerics oracle.
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -53,6 +54,48 @@ class ResidualGradLink:
         return g
 
 
+class GradStatsSource:
+    """A BatchNorm output's link to the kernel that will produce its gradient: the consumer (our
+    1x1-conv data-gradient GEMM, ops/conv.py) computes this BatchNorm's backward reduction —
+    sum(dz), sum(dz * (x - mean)), dz = dy * ReLU mask — in its epilogue from the saved input /
+    mask / mean held here, and deposits the per-tile partials together with the identity of the
+    gradient tensor it wrote. The BatchNorm's backward uses them only if the dy it receives IS that
+    tensor, unmodified (same storage, same version counter) — e.g. not when autograd summed
+    another branch's gradient into it — and otherwise falls back to its own reduce pass.
+    ``PDT_BN_BWD_STATS=0`` turns the hand-off off."""
+
+    __slots__ = ("x", "mask", "mean", "out_version", "part", "grad_ptr", "grad_version")
+
+    def __init__(self):
+        self.x = self.mask = self.mean = self.part = None
+        self.out_version = self.grad_ptr = self.grad_version = None
+
+    def ready(self) -> bool:
+        return self.x is not None and self.part is None
+
+    def deposit(self, part: torch.Tensor, grad: torch.Tensor) -> None:
+        self.part, self.grad_ptr, self.grad_version = part, grad.data_ptr(), grad._version
+
+    def take(self, dy: torch.Tensor):
+        part, self.part = self.part, None
+        self.x = self.mask = self.mean = None  # the BatchNorm's backward is the last user
+        if part is not None and dy.data_ptr() == self.grad_ptr and dy._version == self.grad_version:
+            return part
+        return None
+
+
+def bwd_stats_enabled() -> bool:
+    return os.environ.get("PDT_BN_BWD_STATS", "1") != "0"
+
+
+def grad_stats_source_of(x: torch.Tensor):
+    """The ``GradStatsSource`` of a BatchNorm output ``x`` (unmodified since), else None."""
+    g = getattr(x, "_pdt_gsrc", None)
+    if g is not None and g.out_version == x._version and g.ready():
+        return g
+    return None
+
+
 class MaskedGrad:
     """A ReLU'd residual gradient not yet materialised: ``dy * mask`` (mask = the BatchNorm's
     1-bit ReLU mask, bit j of byte k covers element 8k + j)."""
@@ -70,7 +113,7 @@ class MaskedGrad:
 class _BNTrainFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, residual, weight, bias, running_mean, running_var, momentum, eps, relu, link=None,
-                part=None):
+                part=None, gsrc=None):
         C = native()
         if part is not None:  # statistics from the producing conv's epilogue: no reduce pass over x
             y, mask, mean, invstd = C.bn_fwd_train_tiles(x, part, residual, weight, bias, running_mean,
@@ -82,6 +125,9 @@ class _BNTrainFn(torch.autograd.Function):
         ctx.has_res = residual is not None
         ctx.has_weight = weight is not None
         ctx.link = link
+        ctx.gsrc = gsrc
+        if gsrc is not None:  # what the consumer's dgrad GEMM needs for this BN's backward reduction
+            gsrc.x, gsrc.mask, gsrc.mean = x, (mask if relu else None), mean
         # backward needs the BN input and a 1-bit ReLU mask, never the output y
         ctx.save_for_backward(x, mask if relu else None, weight, mean, invstd)
         return y
@@ -92,19 +138,25 @@ class _BNTrainFn(torch.autograd.Function):
         fmt = torch.channels_last if x.dim() == 4 else torch.contiguous_format
         dy = dy.contiguous(memory_format=fmt)
         need_w = ctx.has_weight and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3])
+        # the reduction over (dy, x), if the kernel that wrote dy already took it (GradStatsSource)
+        part = ctx.gsrc.take(dy) if ctx.gsrc is not None else None
+
+        def bwd(relu, has_res):
+            if part is not None:
+                return native().bn_bwd_train_tiles(dy, x, part, mask, weight, mean, invstd, relu, has_res, need_w)
+            return native().bn_bwd_train(dy, x, mask, weight, mean, invstd, relu, has_res, need_w)
+
+        tail = (None,) * 8
         if ctx.has_res and ctx.link is not None and ctx.link.lazy and ctx.relu:
             # the shortcut gradient dy*mask is never written: the consumer's GEMM masks dy itself
-            dx, _, dg, db = native().bn_bwd_train(dy, x, mask, weight, mean, invstd, True, False, need_w)
+            dx, _, dg, db = bwd(True, False)
             ctx.link.grad = MaskedGrad(dy, mask)
-            return (dx, None, dg if need_w else None, db if need_w else None,
-                    None, None, None, None, None, None, None)
-        dx, dres, dg, db = native().bn_bwd_train(dy, x, mask, weight, mean, invstd, ctx.relu,
-                                                 ctx.has_res, need_w)
+            return (dx, None, dg if need_w else None, db if need_w else None) + tail
+        dx, dres, dg, db = bwd(ctx.relu, ctx.has_res)
         if ctx.has_res and ctx.link is not None:
             ctx.link.grad = dres  # the main-branch consumer adds its gradient into this buffer
             dres = None
-        return (dx, dres if ctx.has_res else None, dg if need_w else None, db if need_w else None,
-                None, None, None, None, None, None, None)
+        return (dx, dres if ctx.has_res else None, dg if need_w else None, db if need_w else None) + tail
 
 
 class _BNEvalFn(torch.autograd.Function):
@@ -142,8 +194,14 @@ def batch_norm_act(x, residual, weight, bias, running_mean, running_var, trainin
         if training:
             from .conv import bn_stats_of
             part = bn_stats_of(x) if x.dim() == 4 else None
-            return _BNTrainFn.apply(x, residual, weight, bias, running_mean, running_var,
-                                    float(momentum), float(eps), bool(relu), res_link, part)
+            gsrc = (GradStatsSource() if x.dim() == 4 and torch.is_grad_enabled() and bwd_stats_enabled()
+                    and (x.requires_grad or (weight is not None and weight.requires_grad)) else None)
+            y = _BNTrainFn.apply(x, residual, weight, bias, running_mean, running_var,
+                                 float(momentum), float(eps), bool(relu), res_link, part, gsrc)
+            if gsrc is not None:  # a consumer conv may take this BN's backward reduction (ops/conv.py)
+                gsrc.out_version = y._version
+                y._pdt_gsrc = gsrc
+            return y
         return _BNEvalFn.apply(x, residual, weight, bias, running_mean, running_var, float(eps), bool(relu))
     return bn_reference(x, residual, weight, bias, running_mean, running_var, training, momentum, eps, relu)
 

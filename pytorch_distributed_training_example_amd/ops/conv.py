@@ -228,13 +228,14 @@ def _nhwc2d(t: torch.Tensor) -> torch.Tensor:
 
 class _Conv1x1Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, link=None, stats_out=None):
+    def forward(ctx, x, weight, link=None, stats_out=None, gsrc=None):
         N, Ci, H, W = x.shape
         Co = weight.shape[0]
         x2 = _nhwc2d(x)
         w2 = weight.reshape(Co, Ci)
         M = x2.shape[0]
         ctx.link = link
+        ctx.gsrc = gsrc  # x is a BatchNorm output: our dgrad GEMM can take that BN's backward reduction
         ctx.save_for_backward(x, weight)
         cands = {"miopen": lambda: F.conv2d(x, weight), "gemm": lambda: torch.mm(x2, w2.t())}
         if x.dtype == torch.bfloat16 and _ours_ok("fwd", M, Ci, Co):
@@ -277,11 +278,18 @@ class _Conv1x1Fn(torch.autograd.Function):
         if isinstance(acc, StridedGrad):  # a stride-2 shortcut's compact gradient: added below
             strided, acc = acc, None
         from .batchnorm import MaskedGrad
+        # dx is final (nothing is added to it after the GEMM) unless this is the first of two linked
+        # branches or a strided shortcut's gradient is added below: only then can the GEMM's epilogue
+        # take the producing BatchNorm's backward reduction (GradStatsSource)
+        gs = ctx.gsrc if (ctx.gsrc is not None and ctx.gsrc.ready() and not first and strided is None) else None
+        bn_kw = dict(bn_x=gs.x, bn_mask=gs.mask, bn_mean=gs.mean) if gs is not None else {}
+        gpart = None
         if isinstance(acc, MaskedGrad) and ctx.needs_input_grad[0] and _ours_ok("dgrad", M, Co, Ci):
             # dx = dy*mask + dY W: the shortcut's ReLU-masked gradient applied in the GEMM epilogue
             from ._native import native
             dx = torch.empty_like(x)
-            native().conv1x1_gemm(g2, w2.t().contiguous(), _nhwc2d(dx), True, False, acc.dy, acc.mask)
+            gpart = native().conv1x1_gemm(g2, w2.t().contiguous(), _nhwc2d(dx), True, False, acc.dy, acc.mask,
+                                          **bn_kw)
             acc = None
         elif isinstance(acc, MaskedGrad):
             acc = acc.dense()
@@ -300,8 +308,12 @@ class _Conv1x1Fn(torch.autograd.Function):
                 cands["ours"] = ours_d
             algo = _pick(("bwd_data", _dtype_name(x), M, Ci, Co), cands)
             if algo == "ours" and acc is not None and acc.is_contiguous(memory_format=torch.channels_last):
-                native().conv1x1_gemm(g2, wt, _nhwc2d(acc), True, False)  # dx = dres + dY W, in place
+                # dx = dres + dY W, in place
+                gpart = native().conv1x1_gemm(g2, wt, _nhwc2d(acc), True, False, **bn_kw)
                 dx, acc = acc, None
+            elif algo == "ours" and acc is None:
+                dx = torch.empty_like(x)
+                gpart = native().conv1x1_gemm(g2, wt, _nhwc2d(dx), False, False, **bn_kw)
             elif algo == "ours":
                 dx = ours_d()
             elif algo == "gemm" and acc is not None and acc.is_contiguous(memory_format=torch.channels_last):
@@ -317,6 +329,8 @@ class _Conv1x1Fn(torch.autograd.Function):
             dx = acc
         if strided is not None and dx is not None:
             strided.add_into(dx)
+        if gpart is not None and dx is not None:
+            gs.deposit(gpart, dx)
         if first and dx is not None:  # first of the two branches: leave dx for the partner to add to
             ctx.link.grad, dx = dx, None
         if ctx.needs_input_grad[1]:
@@ -330,7 +344,7 @@ class _Conv1x1Fn(torch.autograd.Function):
             else:
                 wfn = lambda: conv_bwd([False, True, False])[1]  # noqa: E731
             dw = _on_side_stream(wfn, weight, gy, x) if _wgrad_stream_enabled() else wfn()
-        return dx, dw, None, None
+        return dx, dw, None, None, None
 
 
 class StridedGrad:
@@ -459,9 +473,10 @@ class _Conv3x3Fn(torch.autograd.Function):
     transposed (conv3x3_flip); weight gradient = MIOpen (optionally on the side stream)."""
 
     @staticmethod
-    def forward(ctx, x, weight, stats_out=None):
+    def forward(ctx, x, weight, stats_out=None, gsrc=None):
         from ._native import native
         ctx.save_for_backward(x, weight)
+        ctx.gsrc = gsrc  # x is a BatchNorm output: the dgrad kernel can take that BN's backward reduction
         if stats_out is not None:  # BatchNorm statistics in the epilogue (halo kernel shapes)
             r = native().conv3x3s1_fwd_stats(x, weight)
             if len(r) == 2:
@@ -476,12 +491,19 @@ class _Conv3x3Fn(torch.autograd.Function):
         gy = gy.contiguous(memory_format=torch.channels_last)
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            dx = native().conv3x3s1_fwd(gy, native().conv3x3_flip(weight))
+            gs = ctx.gsrc if ctx.gsrc is not None and ctx.gsrc.ready() else None
+            if gs is not None:  # dx is the gradient at a BatchNorm's output: its reduction in the epilogue
+                r = native().conv3x3s1_fwd_bnbwd(gy, native().conv3x3_flip(weight), gs.x, gs.mask, gs.mean)
+                dx = r[0]
+                if len(r) == 2:
+                    gs.deposit(r[1], dx)
+            else:
+                dx = native().conv3x3s1_fwd(gy, native().conv3x3_flip(weight))
         if ctx.needs_input_grad[1]:
             args = (gy, x, weight, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1)
             wfn = lambda: torch.ops.aten.convolution_backward(*args, [False, True, False])[1]  # noqa: E731
             dw = _on_side_stream(wfn, weight, gy, x) if _wgrad_stream_enabled() else wfn()
-        return dx, dw, None
+        return dx, dw, None, None
 
 
 def _stats_enabled() -> bool:
@@ -551,7 +573,9 @@ class SplitConv2d(nn.Conv2d):
         if conv3x3_eligible(self, x):
             holder = [] if (self.emit_bn_stats and self.training and torch.is_grad_enabled()
                             and _stats_enabled()) else None
-            y = _Conv3x3Fn.apply(x, self.weight, holder)
+            from .batchnorm import grad_stats_source_of
+            y = _Conv3x3Fn.apply(x, self.weight, holder,
+                                 grad_stats_source_of(x) if self.training and torch.is_grad_enabled() else None)
             if holder:
                 y._pdt_bn_stats = BNStats(holder[0], y._version)
             return y
@@ -604,7 +628,9 @@ class Conv1x1(nn.Conv2d):
         if self.gemm_eligible(x):
             holder = [] if (self.emit_bn_stats and self.training and torch.is_grad_enabled()
                             and _stats_enabled()) else None
-            y = _Conv1x1Fn.apply(x, self.weight, res_link, holder)
+            from .batchnorm import grad_stats_source_of
+            y = _Conv1x1Fn.apply(x, self.weight, res_link, holder,
+                                 grad_stats_source_of(x) if self.training and torch.is_grad_enabled() else None)
             if holder:
                 y._pdt_bn_stats = BNStats(holder[0], y._version)
             return y

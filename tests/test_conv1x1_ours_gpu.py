@@ -191,3 +191,105 @@ def test_identity_block_masked_residual_matches_plain(monkeypatch, masked):
     for a, b in zip(out[True], out[False]):
         err = ((a - b).norm() / (b.norm() + 1e-12)).item()
         assert err < 2e-2, err
+
+
+def _bits_mask(M, N, p=0.4, seed=7):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    bits = torch.rand(M, N, device="cuda", generator=g) > p
+    mask = (bits.view(-1, 8).to(torch.uint8) << torch.arange(8, device="cuda", dtype=torch.uint8)).sum(1)
+    return bits, mask.to(torch.uint8)
+
+
+@pytest.mark.parametrize("acc", [False, True])
+@pytest.mark.parametrize("M,K,N", [(1000, 256, 64), (777, 64, 256), (4096, 128, 128), (300, 512, 2048)])
+def test_gemm_bn_backward_stats_epilogue(M, K, N, acc):
+    """BSTATS: the GEMM writes dy (optionally dy = C*cmask + A B^T) and returns the per-tile sums of
+    dz = dy*mask and dz*(x - mean) of the BatchNorm whose output gradient dy is (fp32 reference
+    from the bf16 dy actually written)."""
+    a, b = _ab(M, K, N, 11)
+    xb = (torch.randn(M, N, device="cuda") * 2 + 1).bfloat16()
+    mean = xb.float().mean(0)
+    bits, mask = _bits_mask(M, N)
+    out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    kw = dict(bn_x=xb, bn_mask=mask, bn_mean=mean)
+    if acc:
+        cin = torch.randn(M, N, device="cuda").bfloat16()
+        cbits, cmask = _bits_mask(M, N, 0.5, 3)
+        part = _native().conv1x1_gemm(a, b, out, True, False, cin, cmask, **kw)
+        ref = torch.where(cbits, cin.float(), 0) + a.float() @ b.float().t()
+    else:
+        part = _native().conv1x1_gemm(a, b, out, False, False, **kw)
+        ref = a.float() @ b.float().t()
+    torch.testing.assert_close(out.float(), ref, rtol=2e-2, atol=2e-2)
+    T = (M + 255) // 256
+    assert part.shape == (2, T, N)
+    dz = torch.where(bits, out.float(), 0)
+    pad = T * 256 - M
+    dzt = torch.cat([dz, dz.new_zeros(pad, N)]).view(T, 256, N)
+    xt = torch.cat([xb.float() - mean, dz.new_zeros(pad, N)]).view(T, 256, N)
+    torch.testing.assert_close(part[0], dzt.sum(1), rtol=1e-4, atol=2e-3)
+    torch.testing.assert_close(part[1], (dzt * xt).sum(1), rtol=1e-4, atol=5e-3)
+    # no mask: every element counts
+    part2 = _native().conv1x1_gemm(a, b, out, False, False, bn_x=xb, bn_mean=mean) if not acc else None
+    if part2 is not None:
+        o = torch.cat([out.float(), dz.new_zeros(pad, N)]).view(T, 256, N)
+        torch.testing.assert_close(part2[0], o.sum(1), rtol=1e-4, atol=2e-3)
+
+
+@pytest.mark.parametrize("relu,res", [(True, False), (True, True), (False, False)])
+def test_bn_backward_from_tiles_matches_reduce(relu, res):
+    """bn_bwd_train_tiles with partials from the GEMM epilogue == bn_bwd_train's own reduce."""
+    N, C, H, W = 6, 128, 13, 11
+    M = N * H * W
+    x = (torch.randn(N, C, H, W, device="cuda") + 0.3).bfloat16().contiguous(memory_format=torch.channels_last)
+    w = torch.rand(C, device="cuda") + 0.5
+    bb = torch.randn(C, device="cuda")
+    y, mask, mean, invstd = _native().bn_fwd_train(x, None, w, bb, None, None, 0.1, 1e-5, relu)
+    a, b = _ab(M, 64, C, 13)
+    dy = torch.empty_like(x)
+    part = _native().conv1x1_gemm(a, b, dy.permute(0, 2, 3, 1).reshape(M, C), False, False,
+                                  bn_x=x, bn_mask=mask if relu else None, bn_mean=mean)
+    t = _native().bn_bwd_train_tiles(dy, x, part, mask, w, mean, invstd, relu, res, True)
+    r = _native().bn_bwd_train(dy, x, mask, w, mean, invstd, relu, res, True)
+    torch.testing.assert_close(t[2], r[2], rtol=1e-3, atol=1e-3)  # dgamma
+    torch.testing.assert_close(t[3], r[3], rtol=1e-3, atol=1e-3)  # dbeta
+    torch.testing.assert_close(t[0].float(), r[0].float(), rtol=1e-2, atol=1e-2)
+    if res:
+        torch.testing.assert_close(t[1], r[1], rtol=0, atol=0)
+
+
+def test_bottleneck_chain_takes_bn_backward_stats(monkeypatch):
+    """Two Bottlenecks (downsample + identity): with the BN-backward hand-off on, bn2 (conv3's
+    dgrad) and the first block's bn3 (the second block's conv1 dgrad, shortcut accumulated) take
+    their reduction from the GEMM epilogue — and every gradient matches the hand-off-off run."""
+    from pytorch_distributed_training_example_amd.models import resnet as R
+    from pytorch_distributed_training_example_amd.models.precision import to_bf16_mixed
+    from pytorch_distributed_training_example_amd.ops import batchnorm as B
+    torch.manual_seed(0)
+    ds = R._Downsample(R.conv1x1(64, 256, 1), R._bn(256))
+    net = to_bf16_mixed(torch.nn.Sequential(R.Bottleneck(64, 64, 1, ds), R.Bottleneck(256, 64, 1, None))
+                        .cuda().to(memory_format=torch.channels_last))
+    x0 = torch.randn(8, 64, 28, 28, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    monkeypatch.setenv("PDT_CONV1X1", "ours")
+    used = []
+    orig = B.GradStatsSource.take
+
+    def spy(self, dy):
+        p = orig(self, dy)
+        used.append(p is not None)
+        return p
+    monkeypatch.setattr(B.GradStatsSource, "take", spy)
+    out = {}
+    for on in ("1", "0"):
+        monkeypatch.setenv("PDT_BN_BWD_STATS", on)
+        used.clear()
+        net.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_(True)
+        y = net(x)
+        y.backward(torch.ones_like(y) * 0.01 + y.detach() * 0.1)
+        out[on] = [x.grad.float()] + [p.grad.float().clone() for p in net.parameters()]
+        if on == "1":
+            assert sum(used) >= 3, used  # bn2 of both blocks + block 0's bn3
+    for a, b in zip(out["1"], out["0"]):
+        err = ((a - b).norm() / (b.norm() + 1e-12)).item()
+        assert err < 2e-2, err
