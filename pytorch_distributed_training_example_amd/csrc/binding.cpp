@@ -90,6 +90,10 @@ int pdt_conv1x1_tile_rows();
 int pdt_conv1x1_gemm(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t* c, const uint8_t* cm,
                      float* part, int M, int K, int N, const uint16_t* bn_x, const uint8_t* bn_mask,
                      const float* bn_mean, float* bn_part, hipStream_t s);
+int pdt_maxpool_bn_parts(int N, int H);
+int pdt_maxpool3s2_bwd_bn(const uint16_t* dy, const uint8_t* code, uint16_t* dz, int N, int H, int W, int C,
+                          const uint16_t* x, const float* gamma, const float* mean, const float* invstd, uint16_t* dx,
+                          float* dgamma, float* dbeta, float* part, float* ws, hipStream_t s);
 int pdt_bn_bwd_train_tiles(const float* part, int T, int BMt, const uint16_t* dy, const uint16_t* x,
                            const uint8_t* mask, const float* gamma, const float* mean, const float* invstd, int64_t M,
                            int C, int relu, int has_res, uint16_t* dx, uint16_t* dres, float* dgamma, float* dbeta,
@@ -437,6 +441,41 @@ std::vector<Tensor> bn_bwd_train(Tensor dy, Tensor x, c10::optional<Tensor> mask
                             ws.data_ptr<float>(), bn_counters(x), stream());
   TORCH_CHECK(rc == 0, "pdt_bn_bwd_train failed");
   return {dx, dres, dg, db};
+}
+
+// ResNet stem backward: max-pool gradient (the BN's dz, never returned) with the stem BatchNorm's
+// backward reduction fused in, then BN finalize + apply. x: the BN input [N,64,H,W] channels_last.
+// Returns {dx, dgamma, dbeta}.
+std::vector<Tensor> maxpool3s2_bwd_bn(Tensor dy, Tensor code, Tensor x, c10::optional<Tensor> weight, Tensor mean,
+                                      Tensor invstd, bool need_dgamma) {
+  check_nhwc_bf16(dy, "dy");
+  check_nhwc_bf16(x, "x");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(C == 64, "maxpool3s2_bwd_bn: C == 64");
+  TORCH_CHECK(dy.size(0) == N && dy.size(1) == C && dy.size(2) == (H - 1) / 2 + 1 && dy.size(3) == (W - 1) / 2 + 1,
+              "maxpool3s2_bwd_bn: dy shape");
+  TORCH_CHECK(code.scalar_type() == at::kByte && code.numel() == dy.numel(), "maxpool3s2_bwd_bn: code");
+  auto dz = at::empty_like(x);
+  auto dx = at::empty_like(x);
+  auto fopt = x.options().dtype(at::kFloat);
+  Tensor dg, db;
+  if (need_dgamma) {
+    dg = at::empty({C}, fopt);
+    db = at::empty({C}, fopt);
+  }
+  const int T = pdt_maxpool_bn_parts((int)N, (int)H);
+  auto part = at::empty({2 * (int64_t)T * C}, fopt);
+  auto ws = at::empty({pdt_bn_tiles_ws_floats(T, (int)C) + 2 * C}, fopt);
+  const int rc = pdt_maxpool3s2_bwd_bn(reinterpret_cast<const uint16_t*>(dy.data_ptr()), code.data_ptr<uint8_t>(),
+                                       reinterpret_cast<uint16_t*>(dz.data_ptr()), (int)N, (int)H, (int)W, (int)C,
+                                       reinterpret_cast<const uint16_t*>(x.data_ptr()), opt_fptr(weight),
+                                       mean.data_ptr<float>(), invstd.data_ptr<float>(),
+                                       reinterpret_cast<uint16_t*>(dx.data_ptr()),
+                                       need_dgamma ? dg.data_ptr<float>() : nullptr,
+                                       need_dgamma ? db.data_ptr<float>() : nullptr, part.data_ptr<float>(),
+                                       ws.data_ptr<float>(), stream());
+  TORCH_CHECK(rc == 0, "pdt_maxpool3s2_bwd_bn failed: ", rc);
+  return {dx, dg, db};
 }
 
 // BN training backward with the reduction taken from the dy producer's per-tile partials
@@ -1104,6 +1143,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("c_in") = py::none(), py::arg("c_mask") = py::none(), py::arg("bn_x") = py::none(),
         py::arg("bn_mask") = py::none(), py::arg("bn_mean") = py::none());
   m.def("bn_bwd_train_tiles", &bn_bwd_train_tiles);
+  m.def("maxpool3s2_bwd_bn", &maxpool3s2_bwd_bn);
   m.def("bn_fwd_train_tiles", &bn_fwd_train_tiles);
   m.def("conv3x3s1_fwd", &conv3x3s1_fwd);
   m.def("conv3x3s1_fwd_stats", &conv3x3s1_fwd_stats);

@@ -19,6 +19,7 @@
 //   reduce+finalize : Σdz, Σdz(x-mean) with dz = dy·mask → dgamma, dbeta, dx coefficients
 //   apply           : dx = A·dz + B·(x-mean) + D (and dres = dz for the residual branch)
 #include "../common.h"
+#include "../tile_stats.h"
 
 using namespace pdt;
 
@@ -819,39 +820,73 @@ __global__ __launch_bounds__(256) void bn_apply_pool_kernel(const uint16_t* __re
 // Gradient of the fused stem w.r.t. the BN output's pre-ReLU value: a gather over the (up to 4)
 // pooled windows that contain each input position — every input written exactly once, no atomics,
 // fixed summation order.
+// BNRED (C == 64): also the stem BatchNorm's backward reduction — sum dz, sum dz (x - mean) of every
+// dz it writes (x: the BN input at the same place), per workgroup into part [2][gridDim.x][64] (the
+// tiles layout, tile_stats.h): the reduce pass over (dz, x) disappears (bn_bwd_from_partials).
+template <bool BNRED>
 __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const uint16_t* __restrict__ dy,
                                                           const uint8_t* __restrict__ code, uint16_t* __restrict__ dz,
-                                                          int N, int H, int W, int C, int Ho, int Wo) {
+                                                          int N, int H, int W, int C, int Ho, int Wo,
+                                                          const uint16_t* __restrict__ xb, const float* __restrict__ mean,
+                                                          float* __restrict__ part) {
   // one workgroup per input row (n, ih), threads over (iw, c8): 32-bit index math per element
   // (64-bit div/mod per element made this kernel VALU-bound: 545 us at 1.5 TB/s, batch 512)
   const int C8 = C >> 3;
   const int per_row = W * C8;
+  float s1[8], s2[8], mu[8];
+  if constexpr (BNRED) {  // blockDim 256 is a multiple of C8 = 8: a thread's channel chunk never changes
+    const int c8 = threadIdx.x % 8;
+    ld8_f32(mean + c8 * 8, mu);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { s1[j] = 0.f; s2[j] = 0.f; }
+  }
   for (int64_t row = blockIdx.x; row < (int64_t)N * H; row += gridDim.x) {
    const int ih = (int)(row % H);
    const int n = (int)(row / H);
    for (int e = threadIdx.x; e < per_row; e += blockDim.x) {
     const int iw = e / C8, c8 = e - iw * C8;
     const int64_t i = row * per_row + e;
-    float g[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    // the (up to) 2 x 2 pooled windows containing (ih, iw): all loads issued before any use
+    // (clamped duplicates count once: window index idx never matches for a duplicate)
     const int oh0 = ih >> 1, oh1 = min(Ho - 1, (ih + 1) >> 1);
     const int ow0 = iw >> 1, ow1 = min(Wo - 1, (iw + 1) >> 1);
-    for (int oh = oh0; oh <= oh1; ++oh)
-      for (int ow = ow0; ow <= ow1; ++ow) {
-        const uint32_t idx = (uint32_t)((ih - (2 * oh - 1)) * 3 + (iw - (2 * ow - 1)));
-        const int64_t o = (((int64_t)n * Ho + oh) * Wo + ow) * C + c8 * 8;
-        const uint2 cw = *reinterpret_cast<const uint2*>(code + o);
-        uint32_t hit = 0;
+    uint2 cw[4];
+    uint4 dv[4];
+    uint4 xv;
+    if constexpr (BNRED) xv = *reinterpret_cast<const uint4*>(xb + i * 8);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) hit |= ((((j < 4 ? cw.x : cw.y) >> (8 * (j & 3))) & 0xffu) == idx) << j;
-        if (!hit) continue;
-        float v[8];
-        ld8_bf16(dy + o, v);
+    for (int q = 0; q < 4; ++q) {
+      const int oh = q < 2 ? oh0 : oh1, ow = (q & 1) ? ow1 : ow0;
+      const int64_t o = (((int64_t)n * Ho + oh) * Wo + ow) * C + c8 * 8;
+      cw[q] = *reinterpret_cast<const uint2*>(code + o);
+      dv[q] = *reinterpret_cast<const uint4*>(dy + o);
+    }
+    float g[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (hit & (1u << j)) g[j] += v[j];
+    for (int q = 0; q < 4; ++q) {
+      const int oh = q < 2 ? oh0 : oh1, ow = (q & 1) ? ow1 : ow0;
+      const bool dup = (q >= 2 && oh1 == oh0) || ((q & 1) && ow1 == ow0);
+      const uint32_t idx = dup ? 0xffu : (uint32_t)((ih - (2 * oh - 1)) * 3 + (iw - (2 * ow - 1)));
+      float v[8];
+      unpack8(dv[q], v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t cj = ((j < 4 ? cw[q].x : cw[q].y) >> (8 * (j & 3))) & 0xffu;
+        g[j] += cj == idx ? v[j] : 0.f;
       }
-    st8_bf16(dz + i * 8, g);
+    }
+    uint4 st;  // the rounded values the BN backward reads back
+    st.x = (uint32_t)f2bf(g[0]) | ((uint32_t)f2bf(g[1]) << 16);
+    st.y = (uint32_t)f2bf(g[2]) | ((uint32_t)f2bf(g[3]) << 16);
+    st.z = (uint32_t)f2bf(g[4]) | ((uint32_t)f2bf(g[5]) << 16);
+    st.w = (uint32_t)f2bf(g[6]) | ((uint32_t)f2bf(g[7]) << 16);
+    *reinterpret_cast<uint4*>(dz + i * 8) = st;
+    if constexpr (BNRED) bn_bwd_accum8(st, xv, 0xffu, mu, s1, s2);
    }
+  }
+  if constexpr (BNRED) {
+    __shared__ float red[4 * 2 * 64];
+    bn_bwd_tile_store<64, 4>(s1, s2, red, part, (int)gridDim.x, (int)blockIdx.x, 64, 0);
   }
 }
 
@@ -988,6 +1023,36 @@ inline int apply_grid(int64_t nvec) {
   return (int)(g < cap ? (g < 1 ? 1 : g) : cap);
 }
 
+// Backward finalize (from per-tile / per-workgroup partials [2][T][C]: sum dz, sum dz (x - mean)) + apply.
+int bn_bwd_from_partials(const float* part, int T, int BMt, const uint16_t* dy, const uint16_t* x,
+                         const uint8_t* mask, const float* gamma, const float* mean, const float* invstd, int64_t M,
+                         int C, int relu, int has_res, uint16_t* dx, uint16_t* dres, float* dgamma, float* dbeta,
+                         float* ws, hipStream_t s) {
+  if (relu && !mask) return -2;
+  const int P = (T + kTilesPerBlock - 1) / kTilesPerBlock;
+  double* lv = reinterpret_cast<double*>(ws);
+  float* A = ws + 4 * (int64_t)P * C;
+  float* B = A + C;
+  float* D = B + C;
+  FinArgs fa{};
+  fa.gamma = gamma; fa.invstd = invstd; fa.dgamma = dgamma; fa.dbeta = dbeta; fa.A = A; fa.B = B; fa.D = D;
+  fa.M = M;
+  hipLaunchKernelGGL(bn_tiles_l1_kernel<false>, dim3(C / 64, P), dim3(1024), 0, s, part, T, BMt, M, C, lv);
+  hipLaunchKernelGGL(bn_tiles_l2b_kernel, dim3((C + 255) / 256), dim3(256), 0, s, lv, P, C, fa);
+  const int64_t nvec = M * C / 8;
+  const int fixed = (2048 % C) == 0;
+  const int grid = apply_grid(nvec);
+#define PDT_BAPPLY(RL, RS)                                                                                      \
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<RL, RS, 1>), dim3(grid), dim3(256), 0, s, dy, x, mask, mean, A, B, D, \
+                     dx, dres, nvec, C, fixed)
+  if (relu && has_res) PDT_BAPPLY(true, true);
+  else if (relu) PDT_BAPPLY(true, false);
+  else if (has_res) PDT_BAPPLY(false, true);
+  else PDT_BAPPLY(false, false);
+#undef PDT_BAPPLY
+  return 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1104,8 +1169,8 @@ int pdt_maxpool3s2_bwd(const uint16_t* dy, const uint8_t* code, uint16_t* dz, in
   const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
   const int64_t nvec = (int64_t)N * H * W * (C / 8);
   if (nvec == 0) return 0;
-  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(row_grid((int64_t)N * H)), dim3(256), 0, s, dy, code, dz, N, H, W, C, Ho,
-                     Wo);
+  hipLaunchKernelGGL(maxpool_bwd_kernel<false>, dim3(row_grid((int64_t)N * H)), dim3(256), 0, s, dy, code, dz, N, H, W,
+                     C, Ho, Wo, nullptr, nullptr, nullptr);
   return 0;
 }
 
@@ -1168,29 +1233,27 @@ int pdt_bn_bwd_train_tiles(const float* part, int T, int BMt, const uint16_t* dy
                            int C, int relu, int has_res, uint16_t* dx, uint16_t* dres, float* dgamma, float* dbeta,
                            float* ws, hipStream_t s) {
   if (C % kCC != 0 || M < 1 || T != (int)((M + BMt - 1) / BMt)) return -1;
-  if (relu && !mask) return -2;
-  const int P = (T + kTilesPerBlock - 1) / kTilesPerBlock;
-  double* lv = reinterpret_cast<double*>(ws);
-  float* A = ws + 4 * (int64_t)P * C;
-  float* B = A + C;
-  float* D = B + C;
-  FinArgs fa{};
-  fa.gamma = gamma; fa.invstd = invstd; fa.dgamma = dgamma; fa.dbeta = dbeta; fa.A = A; fa.B = B; fa.D = D;
-  fa.M = M;
-  hipLaunchKernelGGL(bn_tiles_l1_kernel<false>, dim3(C / 64, P), dim3(1024), 0, s, part, T, BMt, M, C, lv);
-  hipLaunchKernelGGL(bn_tiles_l2b_kernel, dim3((C + 255) / 256), dim3(256), 0, s, lv, P, C, fa);
-  const int64_t nvec = M * C / 8;
-  const int fixed = (2048 % C) == 0;
-  const int grid = apply_grid(nvec);
-#define PDT_BAPPLY(RL, RS)                                                                                      \
-  hipLaunchKernelGGL((bn_bwd_apply_kernel<RL, RS, 1>), dim3(grid), dim3(256), 0, s, dy, x, mask, mean, A, B, D, \
-                     dx, dres, nvec, C, fixed)
-  if (relu && has_res) PDT_BAPPLY(true, true);
-  else if (relu) PDT_BAPPLY(true, false);
-  else if (has_res) PDT_BAPPLY(false, true);
-  else PDT_BAPPLY(false, false);
-#undef PDT_BAPPLY
-  return 0;
+  return bn_bwd_from_partials(part, T, BMt, dy, x, mask, gamma, mean, invstd, M, C, relu, has_res, dx, dres, dgamma,
+                              dbeta, ws, s);
+}
+
+// Stem backward: max-pool gradient dz (written) with the stem BatchNorm's backward reduction fused,
+// then the BN finalize + apply -> dx. C == 64. ws: pdt_bn_tiles_ws_floats(pdt_maxpool_bn_parts(), C)
+// + 2C floats; part: 2 * pdt_maxpool_bn_parts() * C floats.
+int pdt_maxpool_bn_parts(int N, int H) { return row_grid((int64_t)N * H); }
+
+int pdt_maxpool3s2_bwd_bn(const uint16_t* dy, const uint8_t* code, uint16_t* dz, int N, int H, int W, int C,
+                          const uint16_t* x, const float* gamma, const float* mean, const float* invstd, uint16_t* dx,
+                          float* dgamma, float* dbeta, float* part, float* ws, hipStream_t s) {
+  if (C != 64) return -1;
+  const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  const int64_t M = (int64_t)N * H * W;
+  if (M < 1) return -1;
+  const int T = pdt_maxpool_bn_parts(N, H);
+  hipLaunchKernelGGL(maxpool_bwd_kernel<true>, dim3(T), dim3(256), 0, s, dy, code, dz, N, H, W, C, Ho, Wo, x, mean,
+                     part);
+  return bn_bwd_from_partials(part, T, 1, dz, x, nullptr, gamma, mean, invstd, M, C, 0, 0, dx, nullptr, dgamma, dbeta,
+                              ws, s);
 }
 
 }  // extern "C"

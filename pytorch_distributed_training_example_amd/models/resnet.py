@@ -13,6 +13,7 @@ tail ``relu(bn3(conv3) + identity)`` is ONE kernel.
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional, Type
 
 import torch
@@ -39,6 +40,7 @@ class _Downsample(nn.Sequential):
 
 _NORM = {"pdt": BatchNorm2d, "torch": nn.BatchNorm2d}
 RESIDUAL_GRAD_LINK = [True]  # identity-block residual gradient accumulated in conv1's dgrad GEMM
+DS_MASKED_GRAD = [True]  # downsample blocks: bn3 hands the shortcut gradient to the shortcut BN as (dy, mask)
 _norm_kind = ["pdt"]
 
 
@@ -109,7 +111,14 @@ class Bottleneck(nn.Module):
             # shortcut built AFTER the main branch so its backward nodes run first (higher
             # autograd sequence numbers): the shortcut conv deposits, conv1 accumulates. Either
             # order is correct (whichever branch finishes second adds), this one saves a pass.
-            identity = bn_act(self.downsample[1], linked_conv(self.downsample[0], x, link))
+            ds_bn = self.downsample[1]
+            if isinstance(ds_bn, BatchNorm2d) and DS_MASKED_GRAD[0] and os.environ.get("PDT_DS_MASKED", "1") != "0":
+                # bn3's backward hands the shortcut gradient to the downsample BN as (dy, ReLU mask):
+                # the masked copy dres is never written
+                glink = ResidualGradLink(lazy=True)
+                identity = ds_bn(linked_conv(self.downsample[0], x, link), grad_link=glink)
+                return self.bn3(out, residual=identity, relu=True, res_link=glink)
+            identity = bn_act(ds_bn, linked_conv(self.downsample[0], x, link))
             return bn_act(self.bn3, out, residual=identity, relu=True)
         identity = x if self.downsample is None else self.downsample(x)
         out = bn_act(self.bn1, self.conv1(x), relu=True)

@@ -113,7 +113,7 @@ class MaskedGrad:
 class _BNTrainFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, residual, weight, bias, running_mean, running_var, momentum, eps, relu, link=None,
-                part=None, gsrc=None):
+                part=None, gsrc=None, glink=None):
         C = native()
         if part is not None:  # statistics from the producing conv's epilogue: no reduce pass over x
             y, mask, mean, invstd = C.bn_fwd_train_tiles(x, part, residual, weight, bias, running_mean,
@@ -126,6 +126,11 @@ class _BNTrainFn(torch.autograd.Function):
         ctx.has_weight = weight is not None
         ctx.link = link
         ctx.gsrc = gsrc
+        # glink: this output's only consumer (a residual BatchNorm) may hand its gradient over as
+        # (dy, ReLU mask) and give autograd None — backward then runs with dy = None
+        ctx.glink = glink
+        if glink is not None:
+            ctx.set_materialize_grads(False)
         if gsrc is not None:  # what the consumer's dgrad GEMM needs for this BN's backward reduction
             gsrc.x, gsrc.mask, gsrc.mean = x, (mask if relu else None), mean
         # backward needs the BN input and a 1-bit ReLU mask, never the output y
@@ -135,9 +140,19 @@ class _BNTrainFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, mask, weight, mean, invstd = ctx.saved_tensors
+        tail = (None,) * 9
+        need_w = ctx.has_weight and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3])
+        if dy is None:  # gradient handed over through glink as (dy, mask): a ReLU'd dy of the consumer
+            g = ctx.glink.take() if ctx.glink is not None else None
+            if g is None:
+                return (None,) * 4 + tail
+            if isinstance(g, MaskedGrad):
+                dx, _, dg, db = native().bn_bwd_train(g.dy, x, g.mask, weight, mean, invstd, True, False, need_w)
+            else:
+                dx, _, dg, db = native().bn_bwd_train(g, x, None, weight, mean, invstd, False, False, need_w)
+            return (dx, None, dg if need_w else None, db if need_w else None) + tail
         fmt = torch.channels_last if x.dim() == 4 else torch.contiguous_format
         dy = dy.contiguous(memory_format=fmt)
-        need_w = ctx.has_weight and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3])
         # the reduction over (dy, x), if the kernel that wrote dy already took it (GradStatsSource)
         part = ctx.gsrc.take(dy) if ctx.gsrc is not None else None
 
@@ -146,7 +161,6 @@ class _BNTrainFn(torch.autograd.Function):
                 return native().bn_bwd_train_tiles(dy, x, part, mask, weight, mean, invstd, relu, has_res, need_w)
             return native().bn_bwd_train(dy, x, mask, weight, mean, invstd, relu, has_res, need_w)
 
-        tail = (None,) * 8
         if ctx.has_res and ctx.link is not None and ctx.link.lazy and ctx.relu:
             # the shortcut gradient dy*mask is never written: the consumer's GEMM masks dy itself
             dx, _, dg, db = bwd(True, False)
@@ -179,11 +193,13 @@ class _BNEvalFn(torch.autograd.Function):
 
 
 def batch_norm_act(x, residual, weight, bias, running_mean, running_var, training, momentum, eps, relu,
-                   res_link: Optional[ResidualGradLink] = None):
+                   res_link: Optional[ResidualGradLink] = None, grad_link: Optional[ResidualGradLink] = None):
     """Functional fused BN(+add)(+ReLU). Native when x is a channels_last bf16 GPU tensor.
     ``res_link``: route the residual gradient through it instead of returning it (see
     ``ResidualGradLink``); only honoured on the native training path — callers check
-    ``res_link.grad`` is set before relying on it."""
+    ``res_link.grad`` is set before relying on it. ``grad_link``: the output's gradient may arrive
+    through this link instead of autograd (the output is the ``residual`` of a BatchNorm given
+    the same link as ``res_link``: a ResNet downsample shortcut's BN)."""
     nhwc = x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last) or \
         (x.dim() == 2 and x.is_contiguous())
     if (use_native(x) and x.dtype == torch.bfloat16 and nhwc and x.shape[1] % 64 == 0
@@ -197,7 +213,7 @@ def batch_norm_act(x, residual, weight, bias, running_mean, running_var, trainin
             gsrc = (GradStatsSource() if x.dim() == 4 and torch.is_grad_enabled() and bwd_stats_enabled()
                     and (x.requires_grad or (weight is not None and weight.requires_grad)) else None)
             y = _BNTrainFn.apply(x, residual, weight, bias, running_mean, running_var,
-                                 float(momentum), float(eps), bool(relu), res_link, part, gsrc)
+                                 float(momentum), float(eps), bool(relu), res_link, part, gsrc, grad_link)
             if gsrc is not None:  # a consumer conv may take this BN's backward reduction (ops/conv.py)
                 gsrc.out_version = y._version
                 y._pdt_gsrc = gsrc
@@ -221,8 +237,13 @@ class _BNReluMaxPoolFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, code, weight, mean, invstd = ctx.saved_tensors
-        dz = native().maxpool3s2_bwd(dy, code, ctx.hw[0], ctx.hw[1])
         need_w = ctx.has_weight and (ctx.needs_input_grad[1] or ctx.needs_input_grad[2])
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        if x.shape[1] == 64 and os.environ.get("PDT_STEM_BWD_FUSED", "1") != "0":
+            # the pool gradient kernel also takes the BN's backward reduction: no pass over (dz, x)
+            dx, dg, db = native().maxpool3s2_bwd_bn(dy, code, x, weight, mean, invstd, need_w)
+            return dx, (dg if need_w else None), (db if need_w else None), None, None, None, None
+        dz = native().maxpool3s2_bwd(dy, code, ctx.hw[0], ctx.hw[1])
         dx, _, dg, db = native().bn_bwd_train(dz, x, None, weight, mean, invstd, False, False, need_w)
         return dx, (dg if need_w else None), (db if need_w else None), None, None, None, None
 
@@ -247,7 +268,8 @@ class BatchNorm2d(nn.BatchNorm2d):
         self._nbt = 0  # host-side num_batches_tracked (synced into the buffer on save)
 
     def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
-                relu: Optional[bool] = None, res_link: Optional[ResidualGradLink] = None) -> torch.Tensor:
+                relu: Optional[bool] = None, res_link: Optional[ResidualGradLink] = None,
+                grad_link: Optional[ResidualGradLink] = None) -> torch.Tensor:
         relu = self.fused_relu if relu is None else relu
         training = self.training or not self.track_running_stats
         momentum = self.momentum
@@ -260,7 +282,7 @@ class BatchNorm2d(nn.BatchNorm2d):
         w = self.weight if self.affine else None
         b = self.bias if self.affine else None
         return batch_norm_act(x, residual, w, b, rm, rv, training, momentum if momentum is not None else 0.0,
-                              self.eps, relu, res_link)
+                              self.eps, relu, res_link, grad_link)
 
     def forward_relu_maxpool(self, x: torch.Tensor) -> torch.Tensor:
         """``max_pool2d(relu(bn(x)), 3, 2, 1)`` (ResNet stem) with the pool fused into the BN apply."""

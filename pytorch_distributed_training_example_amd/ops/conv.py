@@ -200,10 +200,20 @@ def _time(fn, reps: int = 3) -> float:
     return e0.elapsed_time(e1)
 
 
+def _prefer_ours() -> str:
+    """``PDT_CONV1X1_PREFER``: comma list of directions (``fwd``, ``bwd_data``) that take our GEMM
+    wherever it applies, regardless of the measured table — the table times the conv alone, while
+    our kernel also removes the consuming BatchNorm's reduce pass (forward statistics / backward
+    reduction in its epilogue)."""
+    return os.environ.get("PDT_CONV1X1_PREFER", "")
+
+
 def _pick(key: Tuple, cands: Dict[str, callable]) -> str:
     mode = _mode()
     if mode in cands:
         return mode
+    if "ours" in cands and key[0] in _prefer_ours().split(","):
+        return "ours"
     _ensure_table()
     c = _CHOICE.get(key)
     if c is not None:  # a decided back end that is switched off here: the GEMM library, untimed

@@ -293,3 +293,57 @@ def test_bottleneck_chain_takes_bn_backward_stats(monkeypatch):
     for a, b in zip(out["1"], out["0"]):
         err = ((a - b).norm() / (b.norm() + 1e-12)).item()
         assert err < 2e-2, err
+
+
+@pytest.mark.parametrize("shape", [(4, 64, 56, 56), (3, 64, 17, 23)])
+def test_stem_pool_backward_fused_reduction(monkeypatch, shape):
+    """Stem BN+ReLU+MaxPool backward: the pool-gradient kernel taking the BN's backward reduction
+    (PDT_STEM_BWD_FUSED=1) gives the same dx / dgamma / dbeta as the separate reduce pass."""
+    from pytorch_distributed_training_example_amd.ops.batchnorm import BatchNorm2d
+    torch.manual_seed(0)
+    bn = BatchNorm2d(shape[1], fused_relu=True).cuda()
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+    x0 = torch.randn(*shape, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    out = {}
+    gy = None
+    for fused in ("1", "0"):
+        monkeypatch.setenv("PDT_STEM_BWD_FUSED", fused)
+        bn.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_(True)
+        y = bn.forward_relu_maxpool(x)
+        if gy is None:
+            gy = (torch.randn_like(y.float()) * 0.1).to(y.dtype)
+        y.backward(gy)
+        out[fused] = [x.grad.float(), bn.weight.grad.clone(), bn.bias.grad.clone()]
+    for a, b in zip(out["1"], out["0"]):
+        torch.testing.assert_close(a, b, rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("ds_masked", [True, False])
+def test_downsample_block_masked_shortcut_grad(ds_masked):
+    """Downsample Bottleneck: bn3 handing the shortcut gradient to the downsample BN as (dy, mask)
+    (no dres written) gives the gradients of the plain autograd path (residual link off)."""
+    from pytorch_distributed_training_example_amd.models import resnet as R
+    from pytorch_distributed_training_example_amd.models.precision import to_bf16_mixed
+    torch.manual_seed(0)
+    ds = R._Downsample(R.conv1x1(128, 256, 1), R._bn(256))
+    blk = to_bf16_mixed(R.Bottleneck(128, 64, 1, ds).cuda().to(memory_format=torch.channels_last))
+    x0 = torch.randn(8, 128, 14, 14, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    out = {}
+    for linked in (True, False):
+        R.RESIDUAL_GRAD_LINK[0] = linked
+        R.DS_MASKED_GRAD[0] = ds_masked
+        try:
+            blk.zero_grad(set_to_none=True)
+            x = x0.clone().requires_grad_(True)
+            y = blk(x)
+            y.backward(torch.ones_like(y) * 0.01 + y.detach() * 0.1)
+            out[linked] = [x.grad.float()] + [p.grad.float().clone() for p in blk.parameters()]
+        finally:
+            R.RESIDUAL_GRAD_LINK[0] = True
+            R.DS_MASKED_GRAD[0] = True
+    for a, b in zip(out[True], out[False]):
+        err = ((a - b).norm() / (b.norm() + 1e-12)).item()
+        assert err < 2e-2, err
