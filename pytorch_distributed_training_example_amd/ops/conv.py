@@ -55,7 +55,7 @@ def load_table(path: str | None = None) -> int:
         tab = json.load(f)
     for k, v in tab.items():
         d, dt, *dims = k.split(",")
-        if v in ("miopen", "gemm", "ours") and len(dims) == 3:
+        if (v in ("miopen", "gemm", "ours") or v.startswith("splitk")) and len(dims) == 3:
             _CHOICE.setdefault((d, dt, *map(int, dims)), v)
     return len(tab)
 
@@ -231,6 +231,20 @@ def choices() -> Dict[Tuple, str]:
     return dict(_CHOICE)
 
 
+_SPLITK = (8, 16, 32, 64)
+
+
+def _wgrad_splitk(g2: torch.Tensor, x2: torch.Tensor, sk: int) -> torch.Tensor:
+    """1x1-conv weight gradient dW[Co, Ci] = dY^T X over K = M pixels as ``sk`` batched GEMMs of
+    M/sk pixels each (hipBLASLt) summed in fp32: with K ~1e5 and both operands pixel-major, one
+    GEMM (or MIOpen's kernel) keeps too few tiles busy — ResNet-50 layer2-4 shapes measured
+    0.5-0.75x of MIOpen's time (tools/wgrad_split_bench.py)."""
+    M, Co = g2.shape
+    Ci = x2.shape[1]
+    part = torch.bmm(g2.view(sk, M // sk, Co).transpose(1, 2), x2.view(sk, M // sk, Ci))
+    return part.sum(0)  # bf16 out, fp32 accumulation
+
+
 def _nhwc2d(t: torch.Tensor) -> torch.Tensor:
     """[N,C,H,W] channels_last -> [N*H*W, C] view."""
     return t.permute(0, 2, 3, 1).reshape(-1, t.shape[1])
@@ -344,13 +358,19 @@ class _Conv1x1Fn(torch.autograd.Function):
         if first and dx is not None:  # first of the two branches: leave dx for the partner to add to
             ctx.link.grad, dx = dx, None
         if ctx.needs_input_grad[1]:
-            algo = _pick(("bwd_weight", _dtype_name(x), M, Ci, Co), {
-                "miopen": lambda: conv_bwd([False, True, False]),
-                "gemm": lambda: torch.mm(g2.t(), x2),
-            })
+            cands = {"miopen": lambda: conv_bwd([False, True, False]), "gemm": lambda: torch.mm(g2.t(), x2)}
+            splitk_on = os.environ.get("PDT_WGRAD_SPLITK", "1") != "0"
+            for sk in _SPLITK if splitk_on else ():
+                if M % sk == 0 and M // sk >= 256:
+                    cands[f"splitk{sk}"] = (lambda sk=sk: _wgrad_splitk(g2, x2, sk))
+            key = ("bwd_weight", _dtype_name(x), M, Ci, Co)
+            algo = "miopen" if not splitk_on and str(_CHOICE.get(key, "")).startswith("splitk") else _pick(key, cands)
+            # a 1x1 kernel has the same element order in NCHW and NHWC: keep weight's strides
             if algo == "gemm":
-                # a 1x1 kernel has the same element order in NCHW and NHWC: keep weight's strides
                 wfn = lambda: torch.mm(g2.t(), x2).as_strided(weight.shape, weight.stride())  # noqa: E731
+            elif algo.startswith("splitk"):
+                sk = int(algo[6:])
+                wfn = lambda: _wgrad_splitk(g2, x2, sk).as_strided(weight.shape, weight.stride())  # noqa: E731
             else:
                 wfn = lambda: conv_bwd([False, True, False])[1]  # noqa: E731
             dw = _on_side_stream(wfn, weight, gy, x) if _wgrad_stream_enabled() else wfn()

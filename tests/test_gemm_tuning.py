@@ -69,7 +69,21 @@ def test_conv1x1_decision_table_roundtrip(tmp_path, monkeypatch):
     assert C._pick(("bwd_weight", "bf16", 802816, 64, 256), {"miopen": None, "gemm": None}) == "miopen"
     import json
     tab = json.load(open(C.TABLE))  # the committed table parses and holds only valid choices
-    assert set(tab.values()) <= {"miopen", "gemm", "ours"}
+    assert set(tab.values()) <= {"miopen", "gemm", "ours", "splitk8", "splitk16", "splitk32", "splitk64"}
+    # split-K weight-gradient decisions load and are picked when the candidate exists
+    key = ("bwd_weight", "bf16", 100352, 256, 1024)
+    C._CHOICE.clear()
+    C.load_table(C.TABLE)
+    assert C._pick(key, {"miopen": None, "gemm": None, "splitk32": None}) == tab["bwd_weight,bf16,100352,256,1024"]
+
+
+def test_wgrad_splitk_matches_mm():
+    """The split-K batched-GEMM weight gradient equals dY^T X (CPU, fp32)."""
+    import torch
+    from pytorch_distributed_training_example_amd.ops import conv as C
+    g = torch.randn(512, 24)
+    x = torch.randn(512, 40)
+    torch.testing.assert_close(C._wgrad_splitk(g, x, 8), g.t() @ x, rtol=1e-4, atol=1e-4)
 
 
 def test_conv1x1_table_covers_bench_default_resnet50():

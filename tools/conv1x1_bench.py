@@ -95,6 +95,26 @@ def main():
         del x, y, dx, part
         torch.cuda.empty_cache()
     print("per step (ms, ours_* = best of both): " + "  ".join(f"{k} {v / 1e3:.2f}" for k, v in tot.items()))
+    # weight gradient dW[co, ci] = dY^T X (library kernels), against the HBM floor of reading dY and X once
+    print(f"{'(n, Ci, Co, H)':<22} | {'miopen_w':>8} {'mm_w':>6} | {'floor':>6} (us at 5.3 TB/s)")
+    wsum = fsum = 0.0
+    for n, ci, co, h in SHAPES:
+        B = a.batch
+        M = B * h * h
+        x = torch.randn(B, ci, h, h, device=dev).bfloat16().contiguous(memory_format=torch.channels_last)
+        w = (torch.randn(co, ci, 1, 1, device=dev) / ci ** 0.5).bfloat16()
+        gy = torch.randn(B, co, h, h, device=dev).bfloat16().contiguous(memory_format=torch.channels_last)
+        x2, g2 = x.permute(0, 2, 3, 1).reshape(M, ci), gy.permute(0, 2, 3, 1).reshape(M, co)
+        t_cw = timeit(lambda: torch.ops.aten.convolution_backward(gy, x, w, None, [1, 1], [0, 0], [1, 1], False,
+                                                                 [0, 0], 1, [False, True, False]), a.reps)
+        t_mw = timeit(lambda: torch.mm(g2.t(), x2), a.reps)
+        floor = M * (ci + co) * 2 / 5.3e12 * 1e6
+        wsum += n * min(t_cw, t_mw)
+        fsum += n * floor
+        print(f"{str((n, ci, co, h)):<22} | {t_cw:8.0f} {t_mw:6.0f} | {floor:6.0f}", flush=True)
+        del x, gy
+        torch.cuda.empty_cache()
+    print(f"wgrad per step: best library {wsum / 1e3:.2f} ms, HBM floor {fsum / 1e3:.2f} ms")
     import json
     print("TABLE " + json.dumps(table, sort_keys=True))
 
