@@ -404,15 +404,24 @@ class _Conv1x1StridedFn(torch.autograd.Function):
     positions, so no full-size zero tensor is ever written."""
 
     @staticmethod
-    def forward(ctx, x, weight, s, link):
+    def forward(ctx, x, weight, s, link, stats_out=None):
         N, Ci, H, W = x.shape
         Co = weight.shape[0]
         xs = x[:, :, ::s, ::s].contiguous(memory_format=torch.channels_last)
         Hs, Ws = xs.shape[2], xs.shape[3]
-        y = torch.mm(_nhwc2d(xs), weight.reshape(Co, Ci).t()).view(N, Hs, Ws, Co).permute(0, 3, 1, 2)
+        M = N * Hs * Ws
         ctx.save_for_backward(xs, weight)
         ctx.s, ctx.link, ctx.xshape = s, link, x.shape
-        return y
+        if x.dtype == torch.bfloat16 and _ours_ok("fwd", M, Ci, Co):
+            # our GEMM, with the consuming (downsample) BatchNorm's statistics in the epilogue
+            from ._native import native
+            y = torch.empty((N, Co, Hs, Ws), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+            part = native().conv1x1_gemm(_nhwc2d(xs), weight.reshape(Co, Ci).contiguous(), _nhwc2d(y), False,
+                                         stats_out is not None)
+            if stats_out is not None:
+                stats_out.append(part)
+            return y
+        return torch.mm(_nhwc2d(xs), weight.reshape(Co, Ci).t()).view(N, Hs, Ws, Co).permute(0, 3, 1, 2)
 
     @staticmethod
     def backward(ctx, gy):
@@ -421,9 +430,16 @@ class _Conv1x1StridedFn(torch.autograd.Function):
         Co = weight.shape[0]
         gy = gy.contiguous(memory_format=torch.channels_last)
         g2, w2 = _nhwc2d(gy), weight.reshape(Co, Ci)
+        M = g2.shape[0]
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            compact = StridedGrad(torch.mm(g2, w2).view(N, Hs, Ws, Ci).permute(0, 3, 1, 2), ctx.s)
+            if gy.dtype == torch.bfloat16 and _ours_ok("dgrad", M, Co, Ci):
+                from ._native import native
+                d = torch.empty((N, Ci, Hs, Ws), dtype=gy.dtype, device=gy.device, memory_format=torch.channels_last)
+                native().conv1x1_gemm(g2, w2.t().contiguous(), _nhwc2d(d), False, False)
+            else:
+                d = torch.mm(g2, w2).view(N, Hs, Ws, Ci).permute(0, 3, 1, 2)
+            compact = StridedGrad(d, ctx.s)
             acc = ctx.link.take() if ctx.link is not None else None
             if ctx.link is not None and acc is None:
                 ctx.link.grad = compact  # first: conv1's backward adds it into its full gradient
@@ -432,8 +448,12 @@ class _Conv1x1StridedFn(torch.autograd.Function):
             else:
                 dx = compact.dense(ctx.xshape)
         if ctx.needs_input_grad[1]:
-            dw = torch.mm(g2.t(), _nhwc2d(xs)).as_strided(weight.shape, weight.stride())
-        return dx, dw, None, None
+            sk = max(8, min(64, 1 << max(0, (M // 3136).bit_length() - 1)))  # ~3-6K pixels per slice
+            if M % sk == 0 and M // sk >= 256:
+                dw = _wgrad_splitk(g2, _nhwc2d(xs), sk).as_strided(weight.shape, weight.stride())
+            else:
+                dw = torch.mm(g2.t(), _nhwc2d(xs)).as_strided(weight.shape, weight.stride())
+        return dx, dw, None, None, None
 
 
 class _LinkedConvFn(torch.autograd.Function):
@@ -648,9 +668,9 @@ class Conv1x1(nn.Conv2d):
 
     def strided_gemm_eligible(self, x: torch.Tensor) -> bool:
         s = self.stride[0]
-        # opt-in: measured 1.2% slower end to end on ResNet-50 than MIOpen's strided kernels
-        # (10,352-10,394 vs 10,496-10,509 img/s; tools/gpu_s2.sh)
-        return s > 1 and self.stride == (s, s) and self._gemm_ok(x) and os.environ.get("PDT_CONV1X1_S2", "0") == "1"
+        # gather + our GEMM (BN statistics fused) + split-K weight gradient: ResNet-50 +1.7% over
+        # MIOpen's strided kernels (12,318 vs 12,118 img/s, tools/gpu_s2b.sh; PDT_CONV1X1_S2=0 = MIOpen)
+        return s > 1 and self.stride == (s, s) and self._gemm_ok(x) and os.environ.get("PDT_CONV1X1_S2", "1") == "1"
 
     def forward(self, x: torch.Tensor, res_link=None) -> torch.Tensor:
         """``res_link``: a ``ResidualGradLink`` whose gradient (the other branch's gradient of
@@ -665,6 +685,11 @@ class Conv1x1(nn.Conv2d):
                 y._pdt_bn_stats = BNStats(holder[0], y._version)
             return y
         if self.strided_gemm_eligible(x):
-            return _Conv1x1StridedFn.apply(x, self.weight, self.stride[0], res_link)
+            holder = [] if (self.emit_bn_stats and self.training and torch.is_grad_enabled()
+                            and _stats_enabled()) else None
+            y = _Conv1x1StridedFn.apply(x, self.weight, self.stride[0], res_link, holder)
+            if holder:
+                y._pdt_bn_stats = BNStats(holder[0], y._version)
+            return y
         assert res_link is None, "res_link needs a GEMM path"
         return super().forward(x)
