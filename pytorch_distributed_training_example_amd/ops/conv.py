@@ -208,10 +208,29 @@ def _prefer_ours() -> str:
     return os.environ.get("PDT_CONV1X1_PREFER", "")
 
 
+_OVERRIDE_CACHE: Dict[str, Dict[str, str]] = {}
+
+
+def _override(key: Tuple):
+    """``PDT_CONV1X1_OVERRIDE="fwd,bf16,M,Ci,Co=ours+..."`` (``+`` or ``;`` separated): per-shape decisions over the table (read
+    per call, so one process can A/B them: tools/ab_env.py)."""
+    ov = os.environ.get("PDT_CONV1X1_OVERRIDE")
+    if not ov:
+        return None
+    d = _OVERRIDE_CACHE.get(ov)
+    if d is None:
+        d = dict(p.split("=", 1) for p in ov.replace("+", ";").split(";") if "=" in p)
+        _OVERRIDE_CACHE[ov] = d
+    return d.get(_key_str(key))
+
+
 def _pick(key: Tuple, cands: Dict[str, callable]) -> str:
     mode = _mode()
     if mode in cands:
         return mode
+    o = _override(key)
+    if o is not None and o in cands:
+        return o
     if "ours" in cands and key[0] in _prefer_ours().split(","):
         return "ours"
     _ensure_table()
