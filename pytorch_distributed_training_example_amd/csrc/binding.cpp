@@ -89,7 +89,7 @@ int pdt_maxpool3s2_bwd(const uint16_t* dy, const uint8_t* code, uint16_t* dz, in
 int pdt_conv1x1_tile_rows();
 int pdt_conv1x1_gemm(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t* c, const uint8_t* cm,
                      float* part, int M, int K, int N, const uint16_t* bn_x, const uint8_t* bn_mask,
-                     const float* bn_mean, float* bn_part, hipStream_t s);
+                     const float* bn_mean, float* bn_part, int c_s, int c_H, int c_W, hipStream_t s);
 int pdt_maxpool_bn_parts(int N, int H);
 int pdt_maxpool3s2_bwd_bn(const uint16_t* dy, const uint8_t* code, uint16_t* dz, int N, int H, int W, int C,
                           const uint16_t* x, const float* gamma, const float* mean, const float* invstd, uint16_t* dx,
@@ -528,7 +528,7 @@ std::vector<Tensor> bn_bwd_train_tiles(Tensor dy, Tensor x, Tensor part, c10::op
 c10::optional<Tensor> conv1x1_gemm(Tensor a, Tensor b, Tensor out, bool acc, bool stats,
                                    c10::optional<Tensor> c_in, c10::optional<Tensor> c_mask,
                                    c10::optional<Tensor> bn_x, c10::optional<Tensor> bn_mask,
-                                   c10::optional<Tensor> bn_mean) {
+                                   c10::optional<Tensor> bn_mean, int64_t c_stride, int64_t c_H, int64_t c_W) {
   for (const Tensor* t : {&a, &b, &out}) {
     check_cuda(*t, "conv1x1_gemm operand");
     TORCH_CHECK(t->scalar_type() == at::kBFloat16 && t->dim() == 2 && t->is_contiguous(),
@@ -544,7 +544,11 @@ c10::optional<Tensor> conv1x1_gemm(Tensor a, Tensor b, Tensor out, bool acc, boo
   if (c_in.has_value() && c_in->defined()) {
     TORCH_CHECK(acc, "conv1x1_gemm: c_in needs acc");
     check_cuda(*c_in, "c_in");
-    TORCH_CHECK(c_in->scalar_type() == at::kBFloat16 && c_in->numel() == M * N && c_in->is_contiguous(
+    // c_stride > 0: c_in is the compact [M / (c_H c_W) * Hs * Ws, N] gradient of a stride subsampling
+    TORCH_CHECK(c_stride <= 0 || (c_H > 0 && c_W > 0 && M % (c_H * c_W) == 0), "conv1x1_gemm: c_H * c_W must divide M");
+    TORCH_CHECK(c_stride <= 0 || !(c_mask.has_value() && c_mask->defined()), "conv1x1_gemm: c_stride excludes c_mask");
+    const int64_t cm_rows = c_stride > 0 ? M / (c_H * c_W) * ((c_H - 1) / c_stride + 1) * ((c_W - 1) / c_stride + 1) : M;
+    TORCH_CHECK(c_in->scalar_type() == at::kBFloat16 && c_in->numel() == cm_rows * N && c_in->is_contiguous(
                     c_in->dim() == 4 ? at::MemoryFormat::ChannelsLast : at::MemoryFormat::Contiguous),
                 "conv1x1_gemm: c_in must be [M, N] bf16 (channels_last when 4-D)");
     cp = reinterpret_cast<const uint16_t*>(c_in->data_ptr());
@@ -554,6 +558,7 @@ c10::optional<Tensor> conv1x1_gemm(Tensor a, Tensor b, Tensor out, bool acc, boo
                 "conv1x1_gemm: c_mask must be uint8 [M * N / 8] with acc");
     mp = c_mask->data_ptr<uint8_t>();
   }
+  TORCH_CHECK(c_stride <= 0 || (c_in.has_value() && c_in->defined()), "conv1x1_gemm: c_stride needs c_in");
   c10::optional<Tensor> part;
   const int64_t T = (M + pdt_conv1x1_tile_rows() - 1) / pdt_conv1x1_tile_rows();
   if (stats) part = at::empty({2, T, N}, a.options().dtype(at::kFloat));
@@ -583,7 +588,8 @@ c10::optional<Tensor> conv1x1_gemm(Tensor a, Tensor b, Tensor out, bool acc, boo
                                   reinterpret_cast<const uint16_t*>(b.data_ptr()),
                                   reinterpret_cast<uint16_t*>(out.data_ptr()), cp, mp,
                                   stats ? part->data_ptr<float>() : nullptr, (int)M, (int)K, (int)N, bx, bm, bmean,
-                                  bstats ? part->data_ptr<float>() : nullptr, stream());
+                                  bstats ? part->data_ptr<float>() : nullptr, (int)c_stride, (int)c_H, (int)c_W,
+                                  stream());
   TORCH_CHECK(rc == 0, "pdt_conv1x1_gemm failed: ", rc);
   return part;
 }
@@ -1141,7 +1147,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("maxpool3s2_bwd", &maxpool3s2_bwd);
   m.def("conv1x1_gemm", &conv1x1_gemm, py::arg("a"), py::arg("b"), py::arg("out"), py::arg("acc"), py::arg("stats"),
         py::arg("c_in") = py::none(), py::arg("c_mask") = py::none(), py::arg("bn_x") = py::none(),
-        py::arg("bn_mask") = py::none(), py::arg("bn_mean") = py::none());
+        py::arg("bn_mask") = py::none(), py::arg("bn_mean") = py::none(), py::arg("c_stride") = 0,
+        py::arg("c_H") = 0, py::arg("c_W") = 0);
   m.def("bn_bwd_train_tiles", &bn_bwd_train_tiles);
   m.def("maxpool3s2_bwd_bn", &maxpool3s2_bwd_bn);
   m.def("bn_fwd_train_tiles", &bn_fwd_train_tiles);

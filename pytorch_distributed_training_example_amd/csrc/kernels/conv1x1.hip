@@ -91,11 +91,19 @@ __device__ __forceinline__ void wait_vm() {
 // part (STATS): [T][N] tile sums, then [T][N] centred tile sums of squares (T = ceil(M / 256)).
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
+// Strided accumulate source (ACC): Cin is the COMPACT gradient of a stride-s subsampling of Y's
+// pixels (a ResNet stride-2 shortcut's data gradient, [N*Hs*Ws, N] with Hs = (H-1)/s+1): Y row
+// m = (n, h, w) adds Cin row (n, h/s, w/s) when s divides h and w, nothing otherwise. s = 0: Cin
+// has Y's rows (plain accumulate).
+struct CGeom {
+  int s, H, W, Hs, Ws;
+};
+
 // NT: streaming (non-temporal) output stores
 template <class Cf, bool ACC, bool STATS, bool NT, bool BSTATS>
 __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv1x1_kernel(
     const uint16_t* __restrict__ A, const uint16_t* __restrict__ B, uint16_t* Y, const uint16_t* Cin,
-    const uint8_t* __restrict__ Cmask, float* __restrict__ part, int M, int K, int N, BnSrc bs) {
+    const uint8_t* __restrict__ Cmask, float* __restrict__ part, int M, int K, int N, BnSrc bs, CGeom cg) {
   constexpr int BM = Cf::BM, BN = Cf::BN;
   constexpr int WROWS = BM / Cf::WM, WCOLS = BN / Cf::WN;
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -209,12 +217,20 @@ __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv1x1_kernel(
       if (bs.mask) bmk = bs.mask[off >> 3];
     }
     if constexpr (ACC) {
-      float a[8], cc[8];
+      float a[8], cc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
       const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
       for (int k = 0; k < 4; ++k) { a[2 * k] = __uint_as_float(w[k] << 16); a[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u); }
-      ld8_bf16(Cin + off, cc);
-      const unsigned mb = Cmask ? Cmask[off >> 3] : 0xffu;  // C = Cin * mask: a ReLU's masked gradient
+      unsigned mb = Cmask ? Cmask[off >> 3] : 0xffu;  // C = Cin * mask: a ReLU's masked gradient
+      if (cg.s) {  // compact strided source
+        const int w = m % cg.W, t = m / cg.W, h = t % cg.H, n = t / cg.H;
+        if (h % cg.s == 0 && w % cg.s == 0)
+          ld8_bf16(Cin + ((int64_t)(n * cg.Hs + h / cg.s) * cg.Ws + w / cg.s) * N + n0 + c * 8, cc);
+        else
+          mb = 0u;
+      } else {
+        ld8_bf16(Cin + off, cc);
+      }
 #pragma unroll
       for (int k = 0; k < 8; ++k) a[k] += (mb >> k) & 1u ? cc[k] : 0.f;
       v.x = (uint32_t)f2bf(a[0]) | ((uint32_t)f2bf(a[1]) << 16);
@@ -239,7 +255,7 @@ int g_nt = 0;  // PDT_GEMM_NT=1: non-temporal output stores (experiment switch)
 
 template <class Cf, bool ACC, bool STATS, bool NT, bool BSTATS>
 int launch_nt(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t* c, const uint8_t* cm, float* part,
-              int M, int K, int N, const BnSrc& bs, hipStream_t s) {
+              int M, int K, int N, const BnSrc& bs, const CGeom& cg, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(&conv1x1_kernel<Cf, ACC, STATS, NT, BSTATS>),
@@ -249,17 +265,17 @@ int launch_nt(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t*
   }
   const int64_t grid = (int64_t)(M + Cf::BM - 1) / Cf::BM * (N / Cf::BN);
   hipLaunchKernelGGL((conv1x1_kernel<Cf, ACC, STATS, NT, BSTATS>), dim3((unsigned)grid), dim3(Cf::kThreads), Cf::kLds,
-                     s, a, b, y, c, cm, part, M, K, N, bs);
+                     s, a, b, y, c, cm, part, M, K, N, bs, cg);
   return 0;
 }
 
 template <class Cf, bool ACC, bool STATS, bool BSTATS = false>
 int launch(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t* c, const uint8_t* cm, float* part, int M,
-           int K, int N, const BnSrc& bs, hipStream_t s) {
+           int K, int N, const BnSrc& bs, const CGeom& cg, hipStream_t s) {
   const char* e = getenv("PDT_GEMM_NT");  // read per launch (A/B inside one process)
   g_nt = (e && e[0] == '1') ? 1 : 0;
-  if (g_nt) return launch_nt<Cf, ACC, STATS, true, BSTATS>(a, b, y, c, cm, part, M, K, N, bs, s);
-  return launch_nt<Cf, ACC, STATS, false, BSTATS>(a, b, y, c, cm, part, M, K, N, bs, s);
+  if (g_nt) return launch_nt<Cf, ACC, STATS, true, BSTATS>(a, b, y, c, cm, part, M, K, N, bs, cg, s);
+  return launch_nt<Cf, ACC, STATS, false, BSTATS>(a, b, y, c, cm, part, M, K, N, bs, cg, s);
 }
 
 using GWide = G1<128, 4, 2>;   // N % 128 == 0: 8 waves of 64x64
@@ -267,16 +283,16 @@ using GNarrow = G1<64, 4, 1>;  // N == 64 (or odd multiples of 64): 4 waves of 6
 
 template <class Cf>
 int dispatch(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t* c, const uint8_t* cm, float* part,
-             int M, int K, int N, const BnSrc& bs, hipStream_t s) {
-  if ((c && part) || (cm && !c) || (part && bs.part)) return -1;  // not instantiated (no caller needs both)
+             int M, int K, int N, const BnSrc& bs, const CGeom& cg, hipStream_t s) {
+  if ((c && part) || (cm && !c) || (part && bs.part) || (cg.s && (!c || cm))) return -1;  // not instantiated
   if (bs.part) {
     if (!bs.x || !bs.mean) return -1;
-    if (c) return launch<Cf, true, false, true>(a, b, y, c, cm, part, M, K, N, bs, s);
-    return launch<Cf, false, false, true>(a, b, y, c, cm, part, M, K, N, bs, s);
+    if (c) return launch<Cf, true, false, true>(a, b, y, c, cm, part, M, K, N, bs, cg, s);
+    return launch<Cf, false, false, true>(a, b, y, c, cm, part, M, K, N, bs, cg, s);
   }
-  if (c) return launch<Cf, true, false>(a, b, y, c, cm, part, M, K, N, bs, s);
-  if (part) return launch<Cf, false, true>(a, b, y, c, cm, part, M, K, N, bs, s);
-  return launch<Cf, false, false>(a, b, y, c, cm, part, M, K, N, bs, s);
+  if (c) return launch<Cf, true, false>(a, b, y, c, cm, part, M, K, N, bs, cg, s);
+  if (part) return launch<Cf, false, true>(a, b, y, c, cm, part, M, K, N, bs, cg, s);
+  return launch<Cf, false, false>(a, b, y, c, cm, part, M, K, N, bs, cg, s);
 }
 
 }  // namespace
@@ -291,14 +307,21 @@ int pdt_conv1x1_tile_rows() { return 256; }
 // bn_x / bn_mask / bn_mean / bn_part (BSTATS, all null = off): y is the gradient at the output of a
 // BatchNorm with input bn_x [M,N], ReLU mask bn_mask (or null) and mean bn_mean [N]; bn_part
 // [2][T][N] receives that BatchNorm's backward per-tile sums (see the header). Not with part.
+// c_s, c_H, c_W (c_s > 0): c is the compact gradient of the stride-c_s subsampling of y's pixels
+// (y rows = [n][c_H][c_W]), see CGeom; needs c, no cm.
 int pdt_conv1x1_gemm(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t* c, const uint8_t* cm,
                      float* part, int M, int K, int N, const uint16_t* bn_x, const uint8_t* bn_mask,
-                     const float* bn_mean, float* bn_part, hipStream_t s) {
+                     const float* bn_mean, float* bn_part, int c_s, int c_H, int c_W, hipStream_t s) {
   if (M < 1 || K < 32 || K % 32 != 0 || N < 64 || N % 64 != 0) return -1;
   if ((int64_t)M * (K > N ? K : N) >= ((int64_t)1 << 31) || (int64_t)N * K >= ((int64_t)1 << 31)) return -2;
   const BnSrc bs{bn_x, bn_mask, bn_mean, bn_part};
-  if (N % 128 == 0) return dispatch<GWide>(a, b, y, c, cm, part, M, K, N, bs, s);
-  return dispatch<GNarrow>(a, b, y, c, cm, part, M, K, N, bs, s);
+  CGeom cg{0, 1, 1, 1, 1};
+  if (c_s > 0) {
+    if (c_H < 1 || c_W < 1 || M % (c_H * c_W) != 0) return -1;
+    cg = CGeom{c_s, c_H, c_W, (c_H - 1) / c_s + 1, (c_W - 1) / c_s + 1};
+  }
+  if (N % 128 == 0) return dispatch<GWide>(a, b, y, c, cm, part, M, K, N, bs, cg, s);
+  return dispatch<GNarrow>(a, b, y, c, cm, part, M, K, N, bs, cg, s);
 }
 
 }  // extern "C"

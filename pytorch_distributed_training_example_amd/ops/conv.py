@@ -321,13 +321,28 @@ class _Conv1x1Fn(torch.autograd.Function):
         if isinstance(acc, StridedGrad):  # a stride-2 shortcut's compact gradient: added below
             strided, acc = acc, None
         from .batchnorm import MaskedGrad
+        if (strided is not None and ctx.needs_input_grad[0] and gy.dtype == torch.bfloat16
+                and _ours_ok("dgrad", M, Co, Ci) and os.environ.get("PDT_STRIDED_ACC", "0") == "1"):
+            # the stride-2 shortcut's compact gradient is added in our GEMM's epilogue (at the sampled
+            # pixels) instead of a strided add pass afterwards: dx leaves the GEMM final. Opt-in:
+            # measured 0.4% slower on ResNet-50 (12,235 vs 12,284 img/s, tools/gpu_sacc.sh) — these
+            # three dgrad shapes run faster on hipBLASLt than the add pass + BN reduce it saves
+            strided_src, strided = strided, None
+        else:
+            strided_src = None
         # dx is final (nothing is added to it after the GEMM) unless this is the first of two linked
         # branches or a strided shortcut's gradient is added below: only then can the GEMM's epilogue
         # take the producing BatchNorm's backward reduction (GradStatsSource)
         gs = ctx.gsrc if (ctx.gsrc is not None and ctx.gsrc.ready() and not first and strided is None) else None
         bn_kw = dict(bn_x=gs.x, bn_mask=gs.mask, bn_mean=gs.mean) if gs is not None else {}
         gpart = None
-        if isinstance(acc, MaskedGrad) and ctx.needs_input_grad[0] and _ours_ok("dgrad", M, Co, Ci):
+        if strided_src is not None:
+            from ._native import native
+            dx = torch.empty_like(x)
+            gpart = native().conv1x1_gemm(g2, w2.t().contiguous(), _nhwc2d(dx), True, False, strided_src.t,
+                                          c_stride=strided_src.s, c_H=H, c_W=W, **bn_kw)
+            acc = None
+        elif isinstance(acc, MaskedGrad) and ctx.needs_input_grad[0] and _ours_ok("dgrad", M, Co, Ci):
             # dx = dy*mask + dY W: the shortcut's ReLU-masked gradient applied in the GEMM epilogue
             from ._native import native
             dx = torch.empty_like(x)

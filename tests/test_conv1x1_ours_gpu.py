@@ -370,3 +370,45 @@ def test_conv1x1_wgrad_splitk_matches_miopen(monkeypatch, shape):
     assert grads["splitk16"].shape == conv.weight.shape
     err = ((grads["splitk16"] - grads["miopen"]).norm() / grads["miopen"].norm()).item()
     assert err < 1e-2, err
+
+
+def test_gemm_accumulates_strided_compact_source():
+    """ACC from a stride-2 shortcut's COMPACT gradient: added only at the sampled pixels."""
+    n, H, W, K, N = 3, 9, 14, 64, 128
+    M = n * H * W
+    a, b = _ab(M, K, N, 21)
+    Hs, Ws = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    cmp = torch.randn(n, N, Hs, Ws, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    out = torch.empty(n, N, H, W, device="cuda", dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    _native().conv1x1_gemm(a, b, out.permute(0, 2, 3, 1).reshape(M, N), True, False, cmp, c_stride=2, c_H=H, c_W=W)
+    ref = (a.float() @ b.float().t()).view(n, H, W, N).permute(0, 3, 1, 2).clone()
+    ref[:, :, ::2, ::2] += cmp.float()
+    torch.testing.assert_close(out.float(), ref, rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("strided_acc", ["1", "0"])
+def test_downsample_stride2_block_strided_acc(monkeypatch, strided_acc):
+    """Stride-2 downsample Bottleneck (gathered shortcut GEMM): conv1's dgrad adding the shortcut's
+    compact gradient in its epilogue matches the strided add pass and the plain autograd path."""
+    from pytorch_distributed_training_example_amd.models import resnet as R
+    from pytorch_distributed_training_example_amd.models.precision import to_bf16_mixed
+    torch.manual_seed(0)
+    ds = R._Downsample(R.conv1x1(256, 512, 2), R._bn(512))
+    blk = to_bf16_mixed(R.Bottleneck(256, 128, 2, ds).cuda().to(memory_format=torch.channels_last))
+    x0 = torch.randn(8, 256, 14, 14, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    monkeypatch.setenv("PDT_STRIDED_ACC", strided_acc)  # opt-in path ("1") and the default ("0")
+    monkeypatch.setenv("PDT_CONV1X1", "ours")
+    out = {}
+    for linked in (True, False):
+        R.RESIDUAL_GRAD_LINK[0] = linked
+        try:
+            blk.zero_grad(set_to_none=True)
+            x = x0.clone().requires_grad_(True)
+            y = blk(x)
+            y.backward(torch.ones_like(y) * 0.01 + y.detach() * 0.1)
+            out[linked] = [x.grad.float()] + [p.grad.float().clone() for p in blk.parameters()]
+        finally:
+            R.RESIDUAL_GRAD_LINK[0] = True
+    for a, b in zip(out[True], out[False]):
+        err = ((a - b).norm() / (b.norm() + 1e-12)).item()
+        assert err < 2e-2, err
