@@ -32,7 +32,7 @@ def linear(x, mod: nn.Linear, bias=True):
     if fp8 is not None:
         from ..ops.fp8 import fp8_linear
         return fp8_linear(x, mod.weight, b, fp8[0], fp8[1])
-    return _linear(x, mod.weight, b) if b is not None else F.linear(x, mod.weight)
+    return _linear(x, mod.weight, b)
 
 
 class SelfAttention(nn.Module):

@@ -106,3 +106,14 @@ def test_clip_grad_norm_cpu():
     assert abs(float(n) - ref) < 1e-4
     total = torch.sqrt(sum((g ** 2).sum() for g in gs))
     assert abs(float(total) - 1.0) < 1e-4
+
+
+def test_linear_wgrad_splitk_cpu_matches():
+    """ops/linear.py: the split-K weight-gradient helper equals dY^T X (CPU path keeps the single
+    GEMM; the helper itself is checked directly)."""
+    import torch
+    from pytorch_distributed_training_example_amd.ops import linear as L
+    dy, x = torch.randn(64, 24), torch.randn(64, 40)
+    torch.testing.assert_close(L._wgrad(dy, x), dy.t() @ x)
+    from pytorch_distributed_training_example_amd.ops.conv import _wgrad_splitk
+    torch.testing.assert_close(_wgrad_splitk(dy, x, 4), dy.t() @ x, rtol=1e-5, atol=1e-5)
