@@ -111,6 +111,7 @@ int pdt_p2p_allreduce(const void* in, void* out, int64_t n, int dtype, char* con
                       uint32_t* const* flag_ptrs, int rank, int world, int64_t cap, uint32_t epoch,
                       float post_scale, int* err, int max_blocks, hipStream_t s);
 int pdt_colsum(const void* x, int dtype, int64_t N, int D, void* out, int odtype, float* ws, hipStream_t s);
+int pdt_slice_sum_bf16(const uint16_t* x, uint16_t* out, int S, int64_t n, hipStream_t s);
 int pdt_lenet_stem_fwd(const float* x, const float* w, const float* b, int64_t N, float slope, float* y,
                        uint8_t* code, hipStream_t s);
 int64_t pdt_lenet_stem_slab_floats(int64_t N, int ipb);
@@ -900,6 +901,18 @@ void attn_bwd_out(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor ls
 }
 
 // bias gradient of a Linear layer: column sum of dy [*, D] -> [D] in out_dtype (fp32 / bf16)
+// out = x.sum(0) for a contiguous bf16 [S, ...] tensor (S = 2..64, a power of two), fp32 accumulation.
+Tensor slice_sum(Tensor x) {
+  check_cuda(x, "slice_sum");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.is_contiguous() && x.dim() >= 2, "slice_sum: contiguous bf16 [S, ...]");
+  const int64_t S = x.size(0), n = x.numel() / S;
+  auto out = at::empty(x.sizes().slice(1), x.options());
+  const int rc = pdt_slice_sum_bf16(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                                    reinterpret_cast<uint16_t*>(out.data_ptr()), (int)S, n, stream());
+  TORCH_CHECK(rc == 0, "pdt_slice_sum_bf16 failed: ", rc);
+  return out;
+}
+
 Tensor colsum(Tensor dy, at::ScalarType out_dtype) {
   check_cuda(dy, "dy");
   TORCH_CHECK(dy.is_contiguous(), "colsum: contiguous input");
@@ -1151,6 +1164,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("c_H") = 0, py::arg("c_W") = 0);
   m.def("bn_bwd_train_tiles", &bn_bwd_train_tiles);
   m.def("maxpool3s2_bwd_bn", &maxpool3s2_bwd_bn);
+  m.def("slice_sum", &slice_sum);
   m.def("bn_fwd_train_tiles", &bn_fwd_train_tiles);
   m.def("conv3x3s1_fwd", &conv3x3s1_fwd);
   m.def("conv3x3s1_fwd_stats", &conv3x3s1_fwd_stats);

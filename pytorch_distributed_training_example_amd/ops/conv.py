@@ -261,7 +261,11 @@ def _wgrad_splitk(g2: torch.Tensor, x2: torch.Tensor, sk: int) -> torch.Tensor:
     M, Co = g2.shape
     Ci = x2.shape[1]
     part = torch.bmm(g2.view(sk, M // sk, Co).transpose(1, 2), x2.view(sk, M // sk, Ci))
-    return part.sum(0)  # bf16 out, fp32 accumulation
+    if (part.is_cuda and part.dtype == torch.bfloat16 and (Co * Ci) % 8 == 0
+            and os.environ.get("PDT_SLICE_SUM", "1") != "0"):
+        from ._native import native
+        return native().slice_sum(part)  # csrc/kernels/slice_sum.hip: bf16 out, fp32 accumulation
+    return part.sum(0)
 
 
 def _nhwc2d(t: torch.Tensor) -> torch.Tensor:

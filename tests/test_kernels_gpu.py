@@ -394,3 +394,13 @@ def test_flash_attention_qkv(B, T, H, causal):
         a = qkv.grad.float().view(B, T, 3, H, Dh)[:, :, i]
         b = ref_in.grad.view(B, T, 3, H, Dh)[:, :, i]
         assert (a - b).norm() / (b.norm() + 1e-6) < 3e-2, (i, ((a - b).norm() / b.norm()).item())
+
+
+@pytest.mark.parametrize("S,shape", [(2, (64, 8)), (4, (3072, 1024)), (16, (768, 768)), (64, (128, 512))])
+def test_slice_sum_matches_fp32(S, shape):
+    """csrc/kernels/slice_sum.hip: sum over the leading slice dimension (split-K weight gradients)."""
+    from pytorch_distributed_training_example_amd.ops._native import native
+    x = torch.randn(S, *shape, device="cuda").bfloat16()
+    out = native().slice_sum(x)
+    assert out.shape == shape and out.dtype == torch.bfloat16
+    torch.testing.assert_close(out.float(), x.float().sum(0), rtol=1e-2, atol=1e-2)
