@@ -40,11 +40,12 @@ from pytorch_distributed_training_example_amd.parallel import launcher  # noqa: 
 
 WORKLOADS = {
     # name: (metric, unit, default per-GPU batch, optimizer)
-    # 512 images per GPU: sized for 288 GB of HBM (bs 256: 9.29k, 384: 9.57k, 512: 10.04k img/s on
-    # one MI355X, tools/gpu_batchsweep.sh) and a 2x larger compute window per all-reduce at N > 1
+    # 1024 images per GPU: sized for 288 GB of HBM (round 1: bs 256: 9.29k, 384: 9.57k, 512: 10.04k
+    # img/s, tools/gpu_batchsweep.sh; round 2: 512: 12.24k, 1024: 13.08k, tools/gpu_bsz.sh) and a 4x
+    # larger compute window per all-reduce at N > 1 than 256
     # metric string verbatim from BASELINE.json:2 (the driver computes the scaling efficiency)
     "resnet50": ("images/sec (whole node) ResNet-50 DDP at 1/2/4/8 MI355X; scaling efficiency",
-                 "images/sec", 512, "sgd"),
+                 "images/sec", 1024, "sgd"),
     "vit_b16": ("images/sec (whole node) ViT-B/16 DDP", "images/sec", 128, "adamw"),
     "gpt2_medium": ("tokens/sec (whole node) GPT-2-medium DDP", "tokens/sec", 8, "adamw"),
     # the reference's own workload (train.py:82-105): LeNet on MNIST-shaped data, fp32, Adadelta,
