@@ -112,6 +112,8 @@ int pdt_p2p_allreduce(const void* in, void* out, int64_t n, int dtype, char* con
                       float post_scale, int* err, int max_blocks, hipStream_t s);
 int pdt_colsum(const void* x, int dtype, int64_t N, int D, void* out, int odtype, float* ws, hipStream_t s);
 int pdt_slice_sum_bf16(const uint16_t* x, uint16_t* out, int S, int64_t n, hipStream_t s);
+int pdt_subsample_gather(const uint16_t* x, uint16_t* xs, int N, int H, int W, int C, int s, hipStream_t st);
+int pdt_subsample_scatter_add(const uint16_t* t, uint16_t* full, int N, int H, int W, int C, int s, hipStream_t st);
 int pdt_lenet_stem_fwd(const float* x, const float* w, const float* b, int64_t N, float slope, float* y,
                        uint8_t* code, hipStream_t s);
 int64_t pdt_lenet_stem_slab_floats(int64_t N, int ipb);
@@ -901,6 +903,32 @@ void attn_bwd_out(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor ls
 }
 
 // bias gradient of a Linear layer: column sum of dy [*, D] -> [D] in out_dtype (fp32 / bf16)
+// xs = x[:, :, ::s, ::s] for a channels_last bf16 [N, C, H, W] tensor (C % 8 == 0), channels_last out.
+Tensor subsample_gather(Tensor x, int64_t s) {
+  check_nhwc_bf16(x, "x");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(C % 8 == 0 && s >= 1, "subsample_gather: C % 8 == 0, s >= 1");
+  auto xs = at::empty({N, C, (H - 1) / s + 1, (W - 1) / s + 1}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const int rc = pdt_subsample_gather(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                                      reinterpret_cast<uint16_t*>(xs.data_ptr()), (int)N, (int)H, (int)W, (int)C,
+                                      (int)s, stream());
+  TORCH_CHECK(rc == 0, "pdt_subsample_gather failed: ", rc);
+  return xs;
+}
+
+// full[:, :, ::s, ::s] += t (in place; both channels_last bf16).
+void subsample_scatter_add(Tensor t, Tensor full, int64_t s) {
+  check_nhwc_bf16(t, "t");
+  check_nhwc_bf16(full, "full");
+  const int64_t N = full.size(0), C = full.size(1), H = full.size(2), W = full.size(3);
+  TORCH_CHECK(t.size(0) == N && t.size(1) == C && t.size(2) == (H - 1) / s + 1 && t.size(3) == (W - 1) / s + 1 &&
+              C % 8 == 0, "subsample_scatter_add: shape");
+  const int rc = pdt_subsample_scatter_add(reinterpret_cast<const uint16_t*>(t.data_ptr()),
+                                           reinterpret_cast<uint16_t*>(full.data_ptr()), (int)N, (int)H, (int)W,
+                                           (int)C, (int)s, stream());
+  TORCH_CHECK(rc == 0, "pdt_subsample_scatter_add failed: ", rc);
+}
+
 // out = x.sum(0) for a contiguous bf16 [S, ...] tensor (S = 2..64, a power of two), fp32 accumulation.
 Tensor slice_sum(Tensor x) {
   check_cuda(x, "slice_sum");
@@ -1165,6 +1193,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_bwd_train_tiles", &bn_bwd_train_tiles);
   m.def("maxpool3s2_bwd_bn", &maxpool3s2_bwd_bn);
   m.def("slice_sum", &slice_sum);
+  m.def("subsample_gather", &subsample_gather);
+  m.def("subsample_scatter_add", &subsample_scatter_add);
   m.def("bn_fwd_train_tiles", &bn_fwd_train_tiles);
   m.def("conv3x3s1_fwd", &conv3x3s1_fwd);
   m.def("conv3x3s1_fwd_stats", &conv3x3s1_fwd_stats);

@@ -415,6 +415,12 @@ class _Conv1x1Fn(torch.autograd.Function):
         return dx, dw, None, None, None
 
 
+def _subsample_native(t: torch.Tensor) -> bool:
+    return (t.is_cuda and t.dtype == torch.bfloat16 and t.dim() == 4 and t.shape[1] % 8 == 0
+            and t.is_contiguous(memory_format=torch.channels_last) and not disabled()
+            and os.environ.get("PDT_SUBSAMPLE_NATIVE", "1") != "0")
+
+
 class StridedGrad:
     """Gradient of a strided subsampling ``x[:, :, ::s, ::s]`` kept compact (only the sampled
     positions are non-zero) until it is added into a full-size gradient of ``x``."""
@@ -425,7 +431,11 @@ class StridedGrad:
         self.t, self.s = t, s
 
     def add_into(self, full: torch.Tensor) -> torch.Tensor:
-        full[:, :, ::self.s, ::self.s].add_(self.t)
+        if _subsample_native(full) and _subsample_native(self.t):
+            from ._native import native
+            native().subsample_scatter_add(self.t, full, self.s)  # csrc/kernels/subsample.hip
+        else:
+            full[:, :, ::self.s, ::self.s].add_(self.t)
         return full
 
     def dense(self, shape) -> torch.Tensor:
@@ -445,7 +455,11 @@ class _Conv1x1StridedFn(torch.autograd.Function):
     def forward(ctx, x, weight, s, link, stats_out=None):
         N, Ci, H, W = x.shape
         Co = weight.shape[0]
-        xs = x[:, :, ::s, ::s].contiguous(memory_format=torch.channels_last)
+        if _subsample_native(x):
+            from ._native import native
+            xs = native().subsample_gather(x, s)  # csrc/kernels/subsample.hip
+        else:
+            xs = x[:, :, ::s, ::s].contiguous(memory_format=torch.channels_last)
         Hs, Ws = xs.shape[2], xs.shape[3]
         M = N * Hs * Ws
         ctx.save_for_backward(xs, weight)

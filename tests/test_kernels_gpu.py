@@ -404,3 +404,20 @@ def test_slice_sum_matches_fp32(S, shape):
     out = native().slice_sum(x)
     assert out.shape == shape and out.dtype == torch.bfloat16
     torch.testing.assert_close(out.float(), x.float().sum(0), rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("shape,s", [((4, 256, 56, 56), 2), ((3, 64, 9, 14), 2), ((2, 24, 7, 7), 3)])
+def test_subsample_gather_and_scatter_add(shape, s):
+    """csrc/kernels/subsample.hip: x[:, :, ::s, ::s] and its adjoint full[:, :, ::s, ::s] += t."""
+    from pytorch_distributed_training_example_amd.ops._native import native
+    x = torch.randn(*shape, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    xs = native().subsample_gather(x, s)
+    ref = x[:, :, ::s, ::s]
+    assert xs.shape == ref.shape and xs.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(xs, ref, rtol=0, atol=0)
+    full = torch.randn(*shape, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    t = torch.randn_like(xs)
+    exp = full.float()
+    exp[:, :, ::s, ::s] += t.float()
+    native().subsample_scatter_add(t, full, s)
+    torch.testing.assert_close(full.float(), exp, rtol=1e-2, atol=1e-2)
