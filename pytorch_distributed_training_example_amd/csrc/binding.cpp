@@ -34,7 +34,8 @@ int pdt_l2norm_sq(int n, void* const* x, const int64_t* numel, int dtype, float*
 int pdt_clip_coef(const float* sumsq, float max_norm, float* coef, float* norm, hipStream_t s);
 int64_t pdt_bn_workspace_floats(int64_t M, int C);
 void pdt_bn_tune(int variant, int target_blocks, int u_fwd, int u_bwd);
-int pdt_bn_fwd_train(const uint16_t* x, const uint16_t* res, const float* gamma, const float* beta,
+int pdt_bn_fwd_train(const uint16_t* x, const uint16_t* res, const float* res_a, const float* res_b,
+                     const float* gamma, const float* beta,
                      float* running_mean, float* running_var, float momentum, float eps, int64_t M, int C, int relu,
                      uint16_t* y, uint8_t* mask, float* mean, float* invstd, float* ws, unsigned* counters,
                      hipStream_t s);
@@ -100,6 +101,7 @@ int pdt_bn_bwd_train_tiles(const float* part, int T, int BMt, const uint16_t* dy
                            float* ws, hipStream_t s);
 int64_t pdt_bn_tiles_ws_floats(int T, int C);
 int pdt_bn_fwd_train_tiles(const float* part, int T, int BMt, const uint16_t* x, const uint16_t* res,
+                           const float* res_a, const float* res_b,
                            const float* gamma, const float* beta, float* running_mean, float* running_var,
                            float momentum, float eps, int64_t M, int C, int relu, uint16_t* y, uint8_t* mask,
                            float* mean, float* invstd, float* ws, hipStream_t s);
@@ -332,16 +334,29 @@ unsigned* bn_counters(const Tensor& like) {
   return reinterpret_cast<unsigned*>(it->second.data_ptr<int>());
 }
 
+// res_ab [2, C] (optional): the residual is a deferred BatchNorm's input, added as ab[0]*res + ab[1].
+// apply = false: statistics only -> {undefined, undefined, mean, invstd, ab [2, C]} (the y = a x + b
+// coefficients, for a consumer that applies them itself).
+std::pair<const float*, const float*> res_ab_ptrs(const c10::optional<Tensor>& res_ab, int64_t C) {
+  if (!res_ab.has_value() || !res_ab->defined()) return {nullptr, nullptr};
+  TORCH_CHECK(res_ab->scalar_type() == at::kFloat && res_ab->is_contiguous() && res_ab->numel() == 2 * C &&
+              res_ab->is_cuda(), "pdt bn: res_ab must be fp32 [2, C]");
+  return {res_ab->data_ptr<float>(), res_ab->data_ptr<float>() + C};
+}
+
 std::vector<Tensor> bn_fwd_train(Tensor x, c10::optional<Tensor> res, c10::optional<Tensor> weight,
                                  c10::optional<Tensor> bias, c10::optional<Tensor> running_mean,
-                                 c10::optional<Tensor> running_var, double momentum, double eps, bool relu) {
+                                 c10::optional<Tensor> running_var, double momentum, double eps, bool relu,
+                                 c10::optional<Tensor> res_ab, bool apply) {
   check_nhwc_bf16(x, "x");
   const int64_t C = x.size(1);
   const int64_t M = x.numel() / C;
   TORCH_CHECK(C % 64 == 0 && C <= 64 * 4096, "pdt bn: C must be a multiple of 64");
-  auto y = at::empty_like(x);
+  const auto rab = res_ab_ptrs(res_ab, C);
+  Tensor y;
+  if (apply) y = at::empty_like(x);
   Tensor mask;
-  if (relu) mask = at::empty({M * C / 8}, x.options().dtype(at::kByte));
+  if (relu && apply) mask = at::empty({M * C / 8}, x.options().dtype(at::kByte));
   auto fopt = x.options().dtype(at::kFloat);
   auto mean = at::empty({C}, fopt), invstd = at::empty({C}, fopt);
   auto ws = at::empty({bn_ws_floats(M, C)}, fopt);
@@ -353,11 +368,14 @@ std::vector<Tensor> bn_fwd_train(Tensor x, c10::optional<Tensor> res, c10::optio
   }
   float* rm = running_mean.has_value() && running_mean->defined() ? running_mean->data_ptr<float>() : nullptr;
   float* rv = running_var.has_value() && running_var->defined() ? running_var->data_ptr<float>() : nullptr;
-  int rc = pdt_bn_fwd_train(reinterpret_cast<const uint16_t*>(x.data_ptr()), rp, opt_fptr(weight), opt_fptr(bias), rm, rv,
-                            (float)momentum, (float)eps, M, (int)C, relu, reinterpret_cast<uint16_t*>(y.data_ptr()),
-                            relu ? mask.data_ptr<uint8_t>() : nullptr, mean.data_ptr<float>(),
+  int rc = pdt_bn_fwd_train(reinterpret_cast<const uint16_t*>(x.data_ptr()), rp, rab.first, rab.second,
+                            opt_fptr(weight), opt_fptr(bias), rm, rv,
+                            (float)momentum, (float)eps, M, (int)C, relu,
+                            apply ? reinterpret_cast<uint16_t*>(y.data_ptr()) : nullptr,
+                            (relu && apply) ? mask.data_ptr<uint8_t>() : nullptr, mean.data_ptr<float>(),
                             invstd.data_ptr<float>(), ws.data_ptr<float>(), bn_counters(x), stream());
-  TORCH_CHECK(rc == 0, "pdt_bn_fwd_train failed");
+  TORCH_CHECK(rc == 0, "pdt_bn_fwd_train failed: ", rc);
+  if (!apply) return {Tensor(), Tensor(), mean, invstd, ws.narrow(0, bn_ws_floats(M, C) - 4 * C, 2 * C).view({2, C})};
   return {y, mask, mean, invstd};
 }
 
@@ -600,7 +618,8 @@ c10::optional<Tensor> conv1x1_gemm(Tensor a, Tensor b, Tensor out, bool acc, boo
 // BN training forward with the statistics taken from conv1x1_gemm's per-tile partials.
 std::vector<Tensor> bn_fwd_train_tiles(Tensor x, Tensor part, c10::optional<Tensor> res, c10::optional<Tensor> weight,
                                        c10::optional<Tensor> bias, c10::optional<Tensor> running_mean,
-                                       c10::optional<Tensor> running_var, double momentum, double eps, bool relu) {
+                                       c10::optional<Tensor> running_var, double momentum, double eps, bool relu,
+                                       c10::optional<Tensor> res_ab, bool apply) {
   check_nhwc_bf16(x, "x");
   const int64_t C = x.size(1);
   const int64_t M = x.numel() / C;
@@ -609,9 +628,11 @@ std::vector<Tensor> bn_fwd_train_tiles(Tensor x, Tensor part, c10::optional<Tens
   TORCH_CHECK(C % 64 == 0, "pdt bn: C must be a multiple of 64");
   TORCH_CHECK(part.scalar_type() == at::kFloat && part.is_contiguous() && part.dim() == 3 && part.size(0) == 2 &&
               part.size(1) == T && part.size(2) == C, "bn_fwd_train_tiles: partials [2, T, C] fp32 expected");
-  auto y = at::empty_like(x);
+  const auto rab = res_ab_ptrs(res_ab, C);
+  Tensor y;
+  if (apply) y = at::empty_like(x);
   Tensor mask;
-  if (relu) mask = at::empty({M * C / 8}, x.options().dtype(at::kByte));
+  if (relu && apply) mask = at::empty({M * C / 8}, x.options().dtype(at::kByte));
   auto fopt = x.options().dtype(at::kFloat);
   auto mean = at::empty({C}, fopt), invstd = at::empty({C}, fopt);
   auto ws = at::empty({pdt_bn_tiles_ws_floats((int)T, (int)C)}, fopt);
@@ -624,11 +645,16 @@ std::vector<Tensor> bn_fwd_train_tiles(Tensor x, Tensor part, c10::optional<Tens
   float* rm = running_mean.has_value() && running_mean->defined() ? running_mean->data_ptr<float>() : nullptr;
   float* rv = running_var.has_value() && running_var->defined() ? running_var->data_ptr<float>() : nullptr;
   const int rc = pdt_bn_fwd_train_tiles(part.data_ptr<float>(), (int)T, BMt, reinterpret_cast<const uint16_t*>(x.data_ptr()),
-                                        rp, opt_fptr(weight), opt_fptr(bias), rm, rv, (float)momentum, (float)eps, M,
-                                        (int)C, relu, reinterpret_cast<uint16_t*>(y.data_ptr()),
-                                        relu ? mask.data_ptr<uint8_t>() : nullptr, mean.data_ptr<float>(),
+                                        rp, rab.first, rab.second, opt_fptr(weight), opt_fptr(bias), rm, rv,
+                                        (float)momentum, (float)eps, M, (int)C, relu,
+                                        apply ? reinterpret_cast<uint16_t*>(y.data_ptr()) : nullptr,
+                                        (relu && apply) ? mask.data_ptr<uint8_t>() : nullptr, mean.data_ptr<float>(),
                                         invstd.data_ptr<float>(), ws.data_ptr<float>(), stream());
   TORCH_CHECK(rc == 0, "pdt_bn_fwd_train_tiles failed: ", rc);
+  if (!apply) {
+    const int64_t P = (T + 127) / 128;
+    return {Tensor(), Tensor(), mean, invstd, ws.narrow(0, 4 * P * C, 2 * C).view({2, C})};
+  }
   return {y, mask, mean, invstd};
 }
 
@@ -1182,7 +1208,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_tune", [](int variant, int target_blocks, int u_fwd, int u_bwd) {
     pdt_bn_tune(variant, target_blocks, u_fwd, u_bwd);
   }, py::arg("variant") = 0, py::arg("target_blocks") = 0, py::arg("u_fwd") = 0, py::arg("u_bwd") = 0);
-  m.def("bn_fwd_train", &bn_fwd_train);
+  m.def("bn_fwd_train", &bn_fwd_train, py::arg("x"), py::arg("res"), py::arg("weight"), py::arg("bias"),
+        py::arg("running_mean"), py::arg("running_var"), py::arg("momentum"), py::arg("eps"), py::arg("relu"),
+        py::arg("res_ab") = py::none(), py::arg("apply") = true);
   m.def("bn_fwd_eval", &bn_fwd_eval);
   m.def("bn_relu_maxpool_fwd", &bn_relu_maxpool_fwd);
   m.def("maxpool3s2_bwd", &maxpool3s2_bwd);
@@ -1195,7 +1223,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("slice_sum", &slice_sum);
   m.def("subsample_gather", &subsample_gather);
   m.def("subsample_scatter_add", &subsample_scatter_add);
-  m.def("bn_fwd_train_tiles", &bn_fwd_train_tiles);
+  m.def("bn_fwd_train_tiles", &bn_fwd_train_tiles, py::arg("x"), py::arg("part"), py::arg("res"), py::arg("weight"),
+        py::arg("bias"), py::arg("running_mean"), py::arg("running_var"), py::arg("momentum"), py::arg("eps"),
+        py::arg("relu"), py::arg("res_ab") = py::none(), py::arg("apply") = true);
   m.def("conv3x3s1_fwd", &conv3x3s1_fwd);
   m.def("conv3x3s1_fwd_stats", &conv3x3s1_fwd_stats);
   m.def("conv3x3s1_fwd_bnbwd", &conv3x3s1_fwd_bnbwd);

@@ -653,18 +653,21 @@ __global__ void bn_eval_coef_kernel(int C, const float* __restrict__ gamma, cons
 // Apply passes: grid-stride over 16-B vectors (8 workgroups of 256 per CU), U vectors per thread
 // per iteration with all loads issued first. U = 1 is used: U = 4 (apply) / 2 (backward) measured
 // 5-10 % SLOWER on the ResNet-50 shapes (tools/bn_trace.py, 822 MB: 350 vs 318 us, 520 vs 469 us).
-template <bool RELU, bool RES, bool MASK, int U>
+// RA: the residual is a BatchNorm's INPUT whose apply was deferred to here (ResNet downsample
+// shortcut): the added term is ra*res + rb per channel, so that BN's output is never written.
+template <bool RELU, bool RES, bool MASK, int U, bool RA = false>
 __global__ __launch_bounds__(256) void bn_apply_kernel(
     const uint16_t* __restrict__ x, const uint16_t* __restrict__ res, const float* __restrict__ a,
     const float* __restrict__ b, uint16_t* __restrict__ y, uint8_t* __restrict__ mask, int64_t nvec, int C,
-    int fixed) {
+    int fixed, const float* __restrict__ ra = nullptr, const float* __restrict__ rb = nullptr) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  float av[8], bv[8];
+  float av[8], bv[8], rav[8], rbv[8];
   if (fixed && i < nvec) {  // stride % (C/8) == 0: every vector of this thread has the same channels
     const int c = (int)((i * 8) % C);
     ld8_f32(a + c, av);
     ld8_f32(b + c, bv);
+    if (RA) { ld8_f32(ra + c, rav); ld8_f32(rb + c, rbv); }
   }
   for (; i < nvec; i += U * stride) {
     uint4 xv[U], rv[U];
@@ -684,6 +687,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(
         const int c = (int)((k * 8) % C);
         ld8_f32(a + c, av);
         ld8_f32(b + c, bv);
+        if (RA) { ld8_f32(ra + c, rav); ld8_f32(rb + c, rbv); }
       }
       float v[8], r[8];
       unpack8(xv[u], v);
@@ -692,7 +696,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         float t = v[j] * av[j] + bv[j];
-        if (RES) t += r[j];
+        if (RES) t += RA ? r[j] * rav[j] + rbv[j] : r[j];
         if (RELU) {
           mb |= (t > 0.f ? 1u : 0u) << j;
           t = t > 0.f ? t : 0.f;
@@ -1078,7 +1082,10 @@ void pdt_bn_tune(int variant, int target_blocks, int u_fwd, int u_bwd) {
 
 // Training forward. Outputs: y (bf16), mask (uint8, M*C/8, when relu), mean/invstd (f32 [C]);
 // updates running stats. counters: >= C/64 zeroed uint32 (self-resetting).
-int pdt_bn_fwd_train(const uint16_t* x, const uint16_t* res, const float* gamma, const float* beta,
+// res_a / res_b (nullable): the residual is a deferred BatchNorm's input, added as res_a*res + res_b.
+// y == nullptr: statistics and coefficients only (a, b at ws + pdt_bn_workspace_floats - 4C), no apply.
+int pdt_bn_fwd_train(const uint16_t* x, const uint16_t* res, const float* res_a, const float* res_b,
+                     const float* gamma, const float* beta,
                      float* running_mean, float* running_var, float momentum, float eps, int64_t M, int C,
                      int relu, uint16_t* y, uint8_t* mask, float* mean, float* invstd, float* ws,
                      unsigned* counters, hipStream_t s) {
@@ -1091,14 +1098,20 @@ int pdt_bn_fwd_train(const uint16_t* x, const uint16_t* res, const float* gamma,
   fa.b_out = b; fa.running_mean = running_mean; fa.running_var = running_var; fa.momentum = momentum;
   fa.eps = eps; fa.M = M;
   launch_reduce<0>(x, nullptr, nullptr, nullptr, M, C, ws, counters, fa, s);
+  if (!y) return 0;
   const int64_t nvec = M * C / 8;
   const int fixed = (2048 % C) == 0;
   const int grid = apply_grid(nvec);
 #define PDT_APPLY(RL, RS, MK)                                                                                 \
   hipLaunchKernelGGL((bn_apply_kernel<RL, RS, MK, 1>), dim3(grid), dim3(256), 0, s, x, res, a, b, y, mask, \
-                     nvec, C, fixed)
+                     nvec, C, fixed, nullptr, nullptr)
+#define PDT_APPLY_RA()                                                                                         \
+  hipLaunchKernelGGL((bn_apply_kernel<true, true, true, 1, true>), dim3(grid), dim3(256), 0, s, x, res, a, b, y, \
+                     mask, nvec, C, fixed, res_a, res_b)
   const bool mk = mask != nullptr;
-  if (relu && res) { if (mk) PDT_APPLY(true, true, true); else PDT_APPLY(true, true, false); }
+  if (res_a && !(relu && res && mk)) return -3;  // the deferred-residual form exists for relu+res+mask only
+  if (res_a) PDT_APPLY_RA();
+  else if (relu && res) { if (mk) PDT_APPLY(true, true, true); else PDT_APPLY(true, true, false); }
   else if (relu) { if (mk) PDT_APPLY(true, false, true); else PDT_APPLY(true, false, false); }
   else if (res) PDT_APPLY(false, true, false);
   else PDT_APPLY(false, false, false);
@@ -1114,6 +1127,7 @@ int64_t pdt_bn_tiles_ws_floats(int T, int C) {
 // Training forward whose statistics come from a producer's per-tile partials (see
 // bn_tiles_l1_kernel) instead of a reduce pass over x: finalize (2 small launches) + apply.
 int pdt_bn_fwd_train_tiles(const float* part, int T, int BMt, const uint16_t* x, const uint16_t* res,
+                           const float* res_a, const float* res_b,
                            const float* gamma, const float* beta, float* running_mean, float* running_var,
                            float momentum, float eps, int64_t M, int C, int relu, uint16_t* y, uint8_t* mask,
                            float* mean, float* invstd, float* ws, hipStream_t s) {
@@ -1128,11 +1142,14 @@ int pdt_bn_fwd_train_tiles(const float* part, int T, int BMt, const uint16_t* x,
   fa.eps = eps; fa.M = M;
   hipLaunchKernelGGL(bn_tiles_l1_kernel<true>, dim3(C / 64, P), dim3(1024), 0, s, part, T, BMt, M, C, lv);
   hipLaunchKernelGGL(bn_tiles_l2_kernel, dim3((C + 255) / 256), dim3(256), 0, s, lv, P, C, fa);
+  if (!y) return 0;
   const int64_t nvec = M * C / 8;
   const int fixed = (2048 % C) == 0;
   const int grid = apply_grid(nvec);
   const bool mk = mask != nullptr;
-  if (relu && res) { if (mk) PDT_APPLY(true, true, true); else PDT_APPLY(true, true, false); }
+  if (res_a && !(relu && res && mk)) return -3;
+  if (res_a) PDT_APPLY_RA();
+  else if (relu && res) { if (mk) PDT_APPLY(true, true, true); else PDT_APPLY(true, true, false); }
   else if (relu) { if (mk) PDT_APPLY(true, false, true); else PDT_APPLY(true, false, false); }
   else if (res) PDT_APPLY(false, true, false);
   else PDT_APPLY(false, false, false);
@@ -1192,6 +1209,7 @@ int pdt_bn_fwd_eval(const uint16_t* x, const uint16_t* res, const float* gamma, 
   else if (res) PDT_APPLY(false, true, false);
   else PDT_APPLY(false, false, false);
 #undef PDT_APPLY
+#undef PDT_APPLY_RA
   return 0;
 }
 

@@ -116,7 +116,10 @@ class Bottleneck(nn.Module):
                 # bn3's backward hands the shortcut gradient to the downsample BN as (dy, ReLU mask):
                 # the masked copy dres is never written
                 glink = ResidualGradLink(lazy=True)
-                identity = ds_bn(linked_conv(self.downsample[0], x, link), grad_link=glink)
+                # and its apply is deferred into bn3's (a_ds x_ds + b_ds added there): the shortcut
+                # BN's output is never written (PDT_DS_DEFER=0: written as before)
+                identity = ds_bn(linked_conv(self.downsample[0], x, link), grad_link=glink,
+                                 defer_apply=os.environ.get("PDT_DS_DEFER", "1") != "0")
                 return self.bn3(out, residual=identity, relu=True, res_link=glink)
             identity = bn_act(ds_bn, linked_conv(self.downsample[0], x, link))
             return bn_act(self.bn3, out, residual=identity, relu=True)

@@ -113,14 +113,23 @@ class MaskedGrad:
 class _BNTrainFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, residual, weight, bias, running_mean, running_var, momentum, eps, relu, link=None,
-                part=None, gsrc=None, glink=None):
+                part=None, gsrc=None, glink=None, res_ab=None, defer=None):
         C = native()
-        if part is not None:  # statistics from the producing conv's epilogue: no reduce pass over x
+        if defer is not None:  # statistics only: the consumer applies y = a x + b itself (deferred apply)
+            if part is not None:
+                _, _, mean, invstd, ab = C.bn_fwd_train_tiles(x, part, None, weight, bias, running_mean,
+                                                              running_var, momentum, eps, False, apply=False)
+            else:
+                _, _, mean, invstd, ab = C.bn_fwd_train(x, None, weight, bias, running_mean, running_var,
+                                                        momentum, eps, False, apply=False)
+            defer.append(ab)
+            y, mask = x.view_as(x), None
+        elif part is not None:  # statistics from the producing conv's epilogue: no reduce pass over x
             y, mask, mean, invstd = C.bn_fwd_train_tiles(x, part, residual, weight, bias, running_mean,
-                                                         running_var, momentum, eps, relu)
+                                                         running_var, momentum, eps, relu, res_ab=res_ab)
         else:
             y, mask, mean, invstd = C.bn_fwd_train(x, residual, weight, bias, running_mean, running_var,
-                                                   momentum, eps, relu)
+                                                   momentum, eps, relu, res_ab=res_ab)
         ctx.relu = relu
         ctx.has_res = residual is not None
         ctx.has_weight = weight is not None
@@ -140,7 +149,7 @@ class _BNTrainFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, mask, weight, mean, invstd = ctx.saved_tensors
-        tail = (None,) * 9
+        tail = (None,) * 11
         need_w = ctx.has_weight and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3])
         if dy is None:  # gradient handed over through glink as (dy, mask): a ReLU'd dy of the consumer
             g = ctx.glink.take() if ctx.glink is not None else None
@@ -192,18 +201,44 @@ class _BNEvalFn(torch.autograd.Function):
         return dx, (dz if ctx.has_res else None), None, None, None, None, None, None
 
 
+def deferred_affine_of(t: torch.Tensor):
+    """(a, b) [2, C] if ``t`` is a BatchNorm output whose apply was deferred (t holds the BN's INPUT;
+    its value is a*t + b per channel), else None."""
+    d = getattr(t, "_pdt_res_affine", None)
+    if d is not None and d[1] == t._version:
+        return d[0]
+    return None
+
+
+def materialize(t: torch.Tensor) -> torch.Tensor:
+    """The value of a possibly apply-deferred BatchNorm output."""
+    ab = deferred_affine_of(t)
+    if ab is None:
+        return t
+    shape = (1, -1, 1, 1) if t.dim() == 4 else (1, -1)
+    return (t.float() * ab[0].view(shape) + ab[1].view(shape)).to(t.dtype)
+
+
 def batch_norm_act(x, residual, weight, bias, running_mean, running_var, training, momentum, eps, relu,
-                   res_link: Optional[ResidualGradLink] = None, grad_link: Optional[ResidualGradLink] = None):
+                   res_link: Optional[ResidualGradLink] = None, grad_link: Optional[ResidualGradLink] = None,
+                   defer_apply: bool = False):
     """Functional fused BN(+add)(+ReLU). Native when x is a channels_last bf16 GPU tensor.
     ``res_link``: route the residual gradient through it instead of returning it (see
     ``ResidualGradLink``); only honoured on the native training path — callers check
     ``res_link.grad`` is set before relying on it. ``grad_link``: the output's gradient may arrive
     through this link instead of autograd (the output is the ``residual`` of a BatchNorm given
-    the same link as ``res_link``: a ResNet downsample shortcut's BN)."""
+    the same link as ``res_link``: a ResNet downsample shortcut's BN). ``defer_apply``: compute the
+    statistics only and return x itself tagged with the affine (a, b); the consumer BN (this output
+    as its ``residual``) adds a*x + b in its own apply pass, so this output is never written — the
+    tag is honoured only by that native path, every other reader goes through ``materialize``."""
+    ab = deferred_affine_of(residual) if residual is not None else None
     nhwc = x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last) or \
         (x.dim() == 2 and x.is_contiguous())
-    if (use_native(x) and x.dtype == torch.bfloat16 and nhwc and x.shape[1] % 64 == 0
-            and (residual is None or (residual.shape == x.shape and residual.dtype == x.dtype))):
+    native_ok = (use_native(x) and x.dtype == torch.bfloat16 and nhwc and x.shape[1] % 64 == 0
+                 and (residual is None or (residual.shape == x.shape and residual.dtype == x.dtype)))
+    if ab is not None and not (native_ok and training and relu):
+        residual, ab = materialize(residual), None  # only the native relu+residual apply takes (a, b)
+    if native_ok:
         if residual is not None:
             residual = residual.contiguous(memory_format=torch.channels_last if x.dim() == 4
                                            else torch.contiguous_format)
@@ -212,8 +247,13 @@ def batch_norm_act(x, residual, weight, bias, running_mean, running_var, trainin
             part = bn_stats_of(x) if x.dim() == 4 else None
             gsrc = (GradStatsSource() if x.dim() == 4 and torch.is_grad_enabled() and bwd_stats_enabled()
                     and (x.requires_grad or (weight is not None and weight.requires_grad)) else None)
+            defer = [] if (defer_apply and residual is None and not relu and x.dim() == 4) else None
+            if defer is not None:
+                gsrc = None
             y = _BNTrainFn.apply(x, residual, weight, bias, running_mean, running_var,
-                                 float(momentum), float(eps), bool(relu), res_link, part, gsrc, grad_link)
+                                 float(momentum), float(eps), bool(relu), res_link, part, gsrc, grad_link, ab, defer)
+            if defer:
+                y._pdt_res_affine = (defer[0], y._version)
             if gsrc is not None:  # a consumer conv may take this BN's backward reduction (ops/conv.py)
                 gsrc.out_version = y._version
                 y._pdt_gsrc = gsrc
@@ -269,7 +309,7 @@ class BatchNorm2d(nn.BatchNorm2d):
 
     def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
                 relu: Optional[bool] = None, res_link: Optional[ResidualGradLink] = None,
-                grad_link: Optional[ResidualGradLink] = None) -> torch.Tensor:
+                grad_link: Optional[ResidualGradLink] = None, defer_apply: bool = False) -> torch.Tensor:
         relu = self.fused_relu if relu is None else relu
         training = self.training or not self.track_running_stats
         momentum = self.momentum
@@ -282,7 +322,7 @@ class BatchNorm2d(nn.BatchNorm2d):
         w = self.weight if self.affine else None
         b = self.bias if self.affine else None
         return batch_norm_act(x, residual, w, b, rm, rv, training, momentum if momentum is not None else 0.0,
-                              self.eps, relu, res_link, grad_link)
+                              self.eps, relu, res_link, grad_link, defer_apply)
 
     def forward_relu_maxpool(self, x: torch.Tensor) -> torch.Tensor:
         """``max_pool2d(relu(bn(x)), 3, 2, 1)`` (ResNet stem) with the pool fused into the BN apply."""

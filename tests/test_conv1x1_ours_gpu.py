@@ -412,3 +412,42 @@ def test_downsample_stride2_block_strided_acc(monkeypatch, strided_acc):
     for a, b in zip(out[True], out[False]):
         err = ((a - b).norm() / (b.norm() + 1e-12)).item()
         assert err < 2e-2, err
+
+
+@pytest.mark.parametrize("stride", [1, 2])
+def test_downsample_bn_deferred_apply(monkeypatch, stride):
+    """Downsample Bottleneck with the shortcut BN's apply deferred into bn3's (PDT_DS_DEFER=1, the
+    shortcut BN output never written) == the materialised shortcut (=0): output, input and
+    parameter gradients, running statistics."""
+    from pytorch_distributed_training_example_amd.models import resnet as R
+    from pytorch_distributed_training_example_amd.models.precision import to_bf16_mixed
+    torch.manual_seed(0)
+    ds = R._Downsample(R.conv1x1(128, 256, stride), R._bn(256))
+    blk = to_bf16_mixed(R.Bottleneck(128, 64, stride, ds).cuda().to(memory_format=torch.channels_last))
+    x0 = torch.randn(8, 128, 14, 14, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    out = {}
+    for defer in ("1", "0"):
+        monkeypatch.setenv("PDT_DS_DEFER", defer)
+        blk.zero_grad(set_to_none=True)
+        ds[1].running_mean.zero_()
+        ds[1].running_var.fill_(1)
+        x = x0.clone().requires_grad_(True)
+        y = blk(x)
+        y.backward(torch.ones_like(y) * 0.01 + y.detach() * 0.1)
+        out[defer] = ([y.float(), x.grad.float()] + [p.grad.float().clone() for p in blk.parameters()]
+                      + [ds[1].running_mean.clone(), ds[1].running_var.clone()])
+    for a, b in zip(out["1"], out["0"]):
+        err = ((a - b).norm() / (b.norm() + 1e-12)).item()
+        assert err < 1e-2, err
+
+
+def test_deferred_affine_materializes_for_other_readers():
+    """A deferred BN output read by anything but the native residual apply is materialised."""
+    from pytorch_distributed_training_example_amd.ops.batchnorm import BatchNorm2d, materialize
+    torch.manual_seed(0)
+    bn = BatchNorm2d(64).cuda()
+    x = torch.randn(4, 64, 8, 8, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    y_def = bn(x, defer_apply=True)
+    bn2 = BatchNorm2d(64).cuda()
+    y_ref = bn2(x)
+    torch.testing.assert_close(materialize(y_def).float(), y_ref.float(), rtol=2e-2, atol=2e-2)
