@@ -4,14 +4,16 @@
 BASELINE.json metric: "images/sec (whole node) ResNet-50 DDP at 1/2/4/8 MI355X". The reference
 publishes no number, so ``vs_baseline`` is null.
 
-  python bench.py --gpus N --steps K --warmup W            # N=1: plain process
-  torchrun --nproc-per-node N ... bench.py --gpus N ...    # N>1: one rank per GPU (RCCL)
+  python bench.py --gpus N --steps K --warmup W            # launches N ranks itself (N>1)
+  torchrun --nproc-per-node N ... bench.py --gpus N ...    # same, under an external launcher
+                                                           # (WORLD_SIZE must equal N)
 
 Each step is a full training step on synthetic data with random-init weights: forward, loss,
 backward, bucketed RCCL all-reduce overlapped with backward, fused optimizer update. W
 warm-up steps are untimed; exactly K steps are timed between barrier + device synchronize on
 both sides; the reported time is the MAX over ranks; ``value`` is the total over all N GPUs
-(weak scaling: per-GPU batch fixed).
+(weak scaling: per-GPU batch fixed; ``--global-batch G`` = strong scaling with the reference's
+global-batch semantics, ceil(G/N) per rank, train.py:82).
 
 --model resnet50 (default, headline) | vit_b16 | gpt2_medium (other north-star configs)
         | lenet (the reference's own LeNet/MNIST workload, fp32, Adadelta)
@@ -61,6 +63,9 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--model", default="resnet50", choices=sorted(WORKLOADS))
     ap.add_argument("--batch-size", type=int, default=None, help="per-GPU batch (default per model)")
+    ap.add_argument("--global-batch", type=int, default=None,
+                    help="strong scaling with the reference's semantics (train.py:82): per-rank batch = "
+                         "ceil(G / N); overrides --batch-size")
     ap.add_argument("--grad-accum", type=int, default=1, help="micro-batches per step (no_sync)")
     ap.add_argument("--image-size", type=int, default=224)
     ap.add_argument("--seq-len", type=int, default=1024)
@@ -68,6 +73,9 @@ def parse(argv=None):
     ap.add_argument("--graph", type=int, default=0,
                     help="hipGraph-capture the step (ours; excludes the capture-unsafe MIOpen solvers)")
     ap.add_argument("--bucket-cap-mb", type=float, default=25.0)
+    ap.add_argument("--reduce-single-rank", type=int, default=1,
+                    help="ours at N=1: still pack buckets and issue the (1-rank RCCL) all-reduce, as torch "
+                         "DDP does, so N=1 carries the same per-step reducer work as N>1")
     ap.add_argument("--comm-hook", default="none", choices=["none", "p2p"],
                     help="p2p: one-shot xGMI P2P all-reduce for buckets <= 1 MiB, RCCL above (ours, N>1)")
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp8", "amp_bf16", "fp32"],
@@ -106,7 +114,8 @@ def build(args, ctx):
         from pytorch_distributed_training_example_amd.optim import FusedAdadelta, FusedAdamW, FusedSGD
         from pytorch_distributed_training_example_amd.parallel import DistributedDataParallel
         ddp = DistributedDataParallel(model, bucket_cap_mb=args.bucket_cap_mb, broadcast_buffers=False,
-                                      gradient_as_bucket_view=True)
+                                      gradient_as_bucket_view=True,
+                                      reduce_single_rank=bool(args.reduce_single_rank))
         if args.comm_hook == "p2p" and world > 1:
             from pytorch_distributed_training_example_amd.parallel.p2p import (P2PAllReduce, P2PHookState,
                                                                                 p2p_allreduce_hook)
@@ -140,6 +149,8 @@ def setup(args):
     if args.impl != "ours":
         # stock baseline: every op (BN, LN, GELU, attention, CE) on PyTorch's own kernels
         os.environ["PDT_DISABLE_NATIVE"] = "1"
+        from pytorch_distributed_training_example_amd.config import SW
+        SW.reload()  # switches are read once per process
     if args.impl == "ours" and args.graph:
         # two MIOpen CK solvers replay wrong gradients under capture (tools/diag_conv_graph.py);
         # MIOpen reads the switch once, so this must precede the first convolution
@@ -147,12 +158,10 @@ def setup(args):
         make_miopen_capture_safe()
     from pytorch_distributed_training_example_amd.engine.miopen_cache import use_repo_miopen_cache
     use_repo_miopen_cache()  # persisted conv-algorithm find-db + kernel cache (after the solver switches)
-    # measured hipBLASLt/rocBLAS solution per GEMM shape (read-only table). Not for LeNet or eager
-    # micro-batched steps: TunableOp's per-call host lookup then costs more than the tuned kernels
-    # save (LeNet 177k -> 131k img/s; ViT 4 x 32 micro-batches 3,190 -> 2,999); a hipGraph replay
-    # pays the lookup once, at capture
-    if args.impl == "ours" and args.model != "lenet" and (args.grad_accum == 1 or args.graph):
-        from pytorch_distributed_training_example_amd.engine.gemm_tuning import use_repo_gemm_tuning
+    # measured hipBLASLt/rocBLAS solution per GEMM shape (read-only table), same predicate as cli.py
+    from pytorch_distributed_training_example_amd.engine.gemm_tuning import (use_repo_gemm_tuning,
+                                                                             wants_gemm_tuning)
+    if args.impl == "ours" and wants_gemm_tuning(args.model, args.grad_accum, args.graph):
         use_repo_gemm_tuning()
     return launcher.init_distributed(backend=args.backend or ("nccl" if torch.cuda.is_available() else "gloo"),
                                      use_gpu=torch.cuda.is_available())
@@ -166,6 +175,8 @@ def run(args, ctx):
     dsync = torch.cuda.synchronize if dev.type == "cuda" else (lambda: None)
     metric, unit, default_b, _ = WORKLOADS[args.model]
     B = args.batch_size or default_b
+    if args.global_batch:  # the reference's --batch-size is global: ceil(1024 / N) per rank (train.py:82)
+        B = -(-args.global_batch // world)
     torch.backends.cudnn.benchmark = bool(args.cudnn_benchmark)
     det = max(args.deterministic, 0)
     torch.backends.cudnn.deterministic = bool(det)
@@ -265,20 +276,59 @@ def run(args, ctx):
     result = {
         "metric": metric, "value": round(value, 2), "unit": unit, "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": {"fp32": "fp32", "fp8": "fp8_e4m3+bf16"}.get(precision, "bf16"),
+        "scaling": "strong" if args.global_batch else "weak", "vs_baseline": None, "dtype": {"fp32": "fp32", "fp8": "fp8_e4m3+bf16"}.get(precision, "bf16"),
         "data": "synthetic (random inputs and labels, random-init weights)",
         "config": {"model": args.model, "global_batch": B * world, "per_gpu_batch": B,
                    "seq_len": T if is_lm else None, "image_size": None if is_lm else S,
                    "parallelism": f"dp{world}", "grad_accum": args.grad_accum, "impl": args.impl,
                    "graph": bool(runner is not None), "precision": precision, "bucket_cap_mb": args.bucket_cap_mb,
-                   "comm_hook": args.comm_hook,
+                   "comm_hook": args.comm_hook, "reducer_active": bool(getattr(ddp, "_active", lambda: False)()),
                    "deterministic": bool(det), "final_loss": round(float(loss.float().item()), 4)},
     }
     return result
 
 
+def self_launch(args, argv) -> int | None:
+    """``--gpus N`` is authoritative: one command uses N GPUs, like the reference's
+    ``spawn(..., nprocs=torch.cuda.device_count())`` (/root/reference/train.py:138,147).
+
+    * under a launcher (``WORLD_SIZE`` set): the world size must equal N, else exit non-zero —
+      a silent mismatch would report an N-GPU number measured on another rank count;
+    * no launcher and N > 1: start ``torch.distributed.run`` with N ranks on 127.0.0.1 as a CHILD
+      process (never exec: nothing here has touched the GPU, and the ranks own their devices) and
+      return its exit code. Rank 0's JSON line comes out on this process's stdout.
+    Returns None when this process should run the benchmark itself."""
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None:
+        if int(env_world) != args.gpus:
+            print(f"[bench] --gpus {args.gpus} but WORLD_SIZE={env_world}: refusing to report a "
+                  f"{env_world}-rank measurement as {args.gpus} GPUs", file=sys.stderr, flush=True)
+            return 2
+        return None
+    if args.gpus <= 1:
+        return None
+    # device_count() does not initialise HIP on this image (the children bind their own GPUs)
+    ngpu = torch.cuda.device_count()
+    if ngpu and ngpu < args.gpus and (args.backend in (None, "nccl")):
+        print(f"[bench] --gpus {args.gpus} but only {ngpu} visible GPU(s): RCCL needs one GPU per rank",
+              file=sys.stderr, flush=True)
+        return 2
+    import subprocess
+    port = os.environ.get("MASTER_PORT") or str(launcher.find_free_port())
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    env.setdefault("OMP_NUM_THREADS", "4")
+    print(f"[bench] launching {args.gpus} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
     args = parse(argv)
+    rc = self_launch(args, argv)
+    if rc is not None:
+        return rc
     if os.environ.get("PDT_STACK_DUMP"):  # periodic Python stacks: where a slow warm-up spends time
         import faulthandler
         faulthandler.dump_traceback_later(float(os.environ["PDT_STACK_DUMP"]), repeat=True)

@@ -262,10 +262,8 @@ def configure_process(args) -> None:
     spawning parent, whose environment every child would inherit."""
     from .engine.miopen_cache import use_repo_miopen_cache
     use_repo_miopen_cache()  # persisted conv-algorithm find-db (engine/miopen_cache.py)
-    # measured GEMM solutions pay off for big GEMMs only: TunableOp's per-call host lookup costs
-    # more than it saves on launch-bound models (LeNet, MLP) and micro-batched steps
-    if args.model not in ("lenet", "mlp") and args.grad_accum == 1:
-        from .engine.gemm_tuning import use_repo_gemm_tuning
+    from .engine.gemm_tuning import use_repo_gemm_tuning, wants_gemm_tuning
+    if wants_gemm_tuning(args.model, args.grad_accum, getattr(args, "hipgraph", False)):
         use_repo_gemm_tuning()  # measured GEMM solutions (engine/gemm_tuning.py), read-only
 
 

@@ -1,0 +1,79 @@
+"""Process-wide switches, read from the environment ONCE (at import) instead of on every op call.
+
+Round 2 read ``os.environ`` inside every convolution / BatchNorm call (28 ``PDT_*`` lookups per
+conv, ``tools/host_overhead.py``: 9 ms of host time per ResNet-50 step, binding at the reference's
+128 images per GPU). The hot path now reads plain attributes of ``SW``. Tests and A/B tools that
+flip a switch inside one process set the variable and call ``SW.reload()`` (tests: the ``switch``
+fixture in ``tests/conftest.py``).
+
+Switch                      default      meaning
+PDT_DISABLE_NATIVE          0            1: every op on its PyTorch reference path (stock baseline)
+PDT_CONV1X1                 auto         1x1 conv backend: auto (measured table) | ours | gemm | miopen | off
+PDT_CONV1X1_OURS            fwd,dgrad    directions allowed on our MFMA GEMM
+PDT_CONV1X1_PREFER          ""           directions that take our GEMM regardless of the table
+PDT_CONV1X1_OVERRIDE        ""           per-shape decisions "dir,dtype,M,Ci,Co=algo;..." (A/B tools)
+PDT_CONV1X1_TABLE           1            0: ignore tuning/conv1x1_gfx950.json
+PDT_CONV1X1_DUMP            ""           write the decisions to this path at exit
+PDT_CONV1X1_S2              1            stride-2 1x1 shortcut as gather + GEMM
+PDT_CONV3X3                 ours         3x3 convs on our kernels (ours | miopen)
+PDT_CONV3X3_WGRAD           ours         3x3 weight gradient on our kernel (ours | miopen)
+PDT_CONV_STEM               ours         7x7 stem on our kernels (ours | miopen)
+PDT_CONV_BN_STATS           1            BatchNorm statistics in conv epilogues
+PDT_BN_BWD_STATS            1            BatchNorm backward reduction in dgrad epilogues
+PDT_RES_MASKED              1            ReLU'd residual gradient handed over as (dy, mask)
+PDT_STEM_BWD_FUSED          1            stem pool backward takes the BN backward reduction
+PDT_WGRAD_SPLITK            1            split-K 1x1 weight gradients
+PDT_SLICE_SUM               1            split-K partial sums on our slice_sum kernel
+PDT_SUBSAMPLE_NATIVE        1            stride-2 gather / scatter-add kernels
+PDT_LINEAR_SPLITK           1            split-K Linear weight gradients
+PDT_FUSED_ADDLN             1            residual add fused into LayerNorm
+PDT_EMBEDDING_NATIVE        1            GPT-2 token/position embedding on our kernels
+PDT_LINEAR_EPILOGUE         1            Linear bias(+GELU) epilogues on our GEMM kernel
+"""
+from __future__ import annotations
+
+import os
+
+
+class _Switches:
+    __slots__ = ("disable_native", "conv1x1", "conv1x1_ours", "conv1x1_prefer", "conv1x1_override",
+                 "conv1x1_table", "conv1x1_dump", "conv1x1_s2", "conv3x3", "conv3x3_wgrad", "conv_stem",
+                 "conv_bn_stats", "bn_bwd_stats", "res_masked", "stem_bwd_fused", "wgrad_splitk", "slice_sum",
+                 "subsample_native", "linear_splitk", "fused_addln", "embedding_native", "linear_epilogue")
+
+    def __init__(self):
+        self.reload()
+
+    def reload(self) -> "_Switches":
+        e = os.environ.get
+
+        def on(name: str, default: str = "1") -> bool:
+            return e(name, default) != "0"
+
+        self.disable_native = e("PDT_DISABLE_NATIVE", "0") == "1"
+        self.conv1x1 = e("PDT_CONV1X1", "auto")
+        self.conv1x1_ours = tuple(e("PDT_CONV1X1_OURS", "fwd,dgrad").split(","))
+        self.conv1x1_prefer = tuple(p for p in e("PDT_CONV1X1_PREFER", "").split(",") if p)
+        ov = e("PDT_CONV1X1_OVERRIDE", "")
+        self.conv1x1_override = dict(p.split("=", 1) for p in ov.replace("+", ";").split(";") if "=" in p)
+        self.conv1x1_table = on("PDT_CONV1X1_TABLE")
+        self.conv1x1_dump = e("PDT_CONV1X1_DUMP") or None
+        self.conv1x1_s2 = e("PDT_CONV1X1_S2", "1") == "1"
+        self.conv3x3 = e("PDT_CONV3X3", "ours")
+        self.conv3x3_wgrad = e("PDT_CONV3X3_WGRAD", "ours")
+        self.conv_stem = e("PDT_CONV_STEM", "ours")
+        self.conv_bn_stats = on("PDT_CONV_BN_STATS")
+        self.bn_bwd_stats = on("PDT_BN_BWD_STATS")
+        self.res_masked = on("PDT_RES_MASKED")
+        self.stem_bwd_fused = on("PDT_STEM_BWD_FUSED")
+        self.wgrad_splitk = on("PDT_WGRAD_SPLITK")
+        self.slice_sum = on("PDT_SLICE_SUM")
+        self.subsample_native = on("PDT_SUBSAMPLE_NATIVE")
+        self.linear_splitk = on("PDT_LINEAR_SPLITK")
+        self.fused_addln = on("PDT_FUSED_ADDLN")
+        self.embedding_native = on("PDT_EMBEDDING_NATIVE")
+        self.linear_epilogue = on("PDT_LINEAR_EPILOGUE")
+        return self
+
+
+SW = _Switches()

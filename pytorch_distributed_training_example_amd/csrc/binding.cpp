@@ -109,9 +109,10 @@ int pdt_fp8_cast_transpose(const uint16_t* x, int64_t M, int64_t K, const float*
                            uint8_t* out_t, float* amax, hipStream_t s);
 int pdt_fp8_update_scales(float* state, int n, int L, float margin_scale, hipStream_t s);
 int64_t pdt_p2p_flags_bytes();
+int64_t pdt_p2p_data_bytes(int64_t cap);
 int pdt_p2p_allreduce(const void* in, void* out, int64_t n, int dtype, char* const* data_ptrs,
-                      uint32_t* const* flag_ptrs, int rank, int world, int64_t cap, uint32_t epoch,
-                      float post_scale, int* err, int max_blocks, hipStream_t s);
+                      uint32_t* const* flag_ptrs, int rank, int world, int64_t cap, float post_scale,
+                      uint32_t* st, int algo, int max_blocks, hipStream_t s);
 int pdt_colsum(const void* x, int dtype, int64_t N, int D, void* out, int odtype, float* ws, hipStream_t s);
 int pdt_slice_sum_bf16(const uint16_t* x, uint16_t* out, int S, int64_t n, hipStream_t s);
 int pdt_subsample_gather(const uint16_t* x, uint16_t* xs, int N, int H, int W, int C, int s, hipStream_t st);
@@ -1035,10 +1036,9 @@ class P2PComm {
     flags_bytes_ = pdt_p2p_flags_bytes();
     // uncached: peers poll/read these over xGMI; no stale L2 lines on either side
     PDT_HIP_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&flags_), flags_bytes_, hipDeviceMallocUncached));
-    PDT_HIP_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&data_), 2 * cap_, hipDeviceMallocUncached));
+    PDT_HIP_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&data_), pdt_p2p_data_bytes(cap_),
+                                        hipDeviceMallocUncached));
     PDT_HIP_CHECK(hipMemset(flags_, 0, flags_bytes_));
-    PDT_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&err_), sizeof(int)));
-    PDT_HIP_CHECK(hipMemset(err_, 0, sizeof(int)));
     PDT_HIP_CHECK(hipDeviceSynchronize());
     data_ptrs_.assign(world_, nullptr);
     flag_ptrs_.assign(world_, nullptr);
@@ -1053,7 +1053,6 @@ class P2PComm {
       }
     (void)hipFree(flags_);
     (void)hipFree(data_);
-    (void)hipFree(err_);
   }
   // 2 x hipIpcMemHandle_t (data, flags) as bytes, to be exchanged through the c10d store
   py::bytes handles() const {
@@ -1080,25 +1079,24 @@ class P2PComm {
     }
     opened_ = true;
   }
-  // out = post_scale * sum over ranks of `in` (out may alias in); enqueued on the current stream
-  void allreduce(Tensor in, Tensor out, double post_scale) {
+  // out = post_scale * sum over ranks of `in` (out may alias in); enqueued on the current stream.
+  // st: int32 [3] device state owned by the caller, zero-initialised ([0] epoch, [1] finished-block
+  // counter, [2] sticky error flag) — advanced by the kernel itself (hipGraph-capture safe).
+  // algo 0 = one-shot, 1 = two-shot (reduce-scatter + all-gather).
+  void allreduce(Tensor in, Tensor out, double post_scale, Tensor st, int64_t algo) {
     TORCH_CHECK(opened_ || world_ == 1, "p2p: open() the peer handles first");
     check_cuda(in, "in");
     TORCH_CHECK(in.is_contiguous() && out.is_contiguous() && in.numel() == out.numel() &&
                     in.scalar_type() == out.scalar_type(), "p2p: contiguous in/out of equal size and dtype");
     TORCH_CHECK(in.numel() % 8 == 0, "p2p: numel must be a multiple of 8");
     TORCH_CHECK(in.numel() * in.element_size() <= cap_, "p2p: tensor larger than the staging capacity");
-    ++epoch_;
+    check_cuda(st, "st");
+    TORCH_CHECK(st.scalar_type() == at::kInt && st.numel() >= 3 && st.is_contiguous(), "p2p: st int32 [3]");
+    TORCH_CHECK(algo == 0 || algo == 1, "p2p: algo 0 (one-shot) or 1 (two-shot)");
     int rc = pdt_p2p_allreduce(in.data_ptr(), out.data_ptr(), in.numel(), dcode(in), data_ptrs_.data(),
-                               flag_ptrs_.data(), rank_, world_, cap_, epoch_, (float)post_scale, err_,
-                               max_blocks_, stream());
+                               flag_ptrs_.data(), rank_, world_, cap_, (float)post_scale,
+                               reinterpret_cast<uint32_t*>(st.data_ptr<int>()), (int)algo, max_blocks_, stream());
     TORCH_CHECK(rc == 0, "pdt_p2p_allreduce failed (", rc, ")");
-  }
-  // 1 if any peer failed to arrive within the spin limit since the last reset (host sync)
-  int error() {
-    int h = 0;
-    PDT_HIP_CHECK(hipMemcpy(&h, err_, sizeof(int), hipMemcpyDeviceToHost));
-    return h;
   }
   int64_t capacity() const { return cap_; }
 
@@ -1109,8 +1107,6 @@ class P2PComm {
   int64_t flags_bytes_ = 0;
   char* data_ = nullptr;
   uint32_t* flags_ = nullptr;
-  int* err_ = nullptr;
-  uint32_t epoch_ = 0;
   bool opened_ = false;
   std::vector<char*> data_ptrs_;
   std::vector<uint32_t*> flag_ptrs_;
@@ -1249,7 +1245,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("handles", &P2PComm::handles)
       .def("open", &P2PComm::open)
       .def("allreduce", &P2PComm::allreduce)
-      .def("error", &P2PComm::error)
       .def("capacity", &P2PComm::capacity);
   m.def("fp8_cast_transpose", &fp8_cast_transpose);
   m.def("fp8_update_scales", &fp8_update_scales);

@@ -123,96 +123,8 @@ __device__ __forceinline__ void bn_finalize(int ch, float S1, float S2, const Fi
   }
 }
 
-template <int MODE>
-__global__ __launch_bounds__(kThreads) void bn_reduce_kernel(
-    const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy, const uint8_t* __restrict__ mask,
-    const float* __restrict__ mean, int64_t M, int C, int64_t rows_per_block, int nrow,
-    float* __restrict__ part, unsigned* __restrict__ counters, FinArgs fa) {
-  // ONE shared array (LDS reduction, last-arriver flag, finalize reduction)
-  __shared__ __attribute__((aligned(16))) float sm[2 * kR * kCC + 4];
-  const int tid = threadIdx.x;
-  const int chunk = blockIdx.y;
-  const int l = tid & (kL - 1), r = tid >> 3;
-  const int c = chunk * kCC + l * 8;
-  const int64_t m0 = (int64_t)blockIdx.x * rows_per_block;
-  const int64_t m1 = min(M, m0 + rows_per_block);
-  float k[8], s1[8], s2[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) { s1[j] = 0.f; s2[j] = 0.f; }
-  if (MODE == 0) ld8_bf16(x + c, k);  // shift: first row (same for every block)
-  else ld8_f32(mean + c, k);
-  int64_t m = m0 + r;
-  // 4 independent rows in flight per lane (≈16-48 KB per workgroup outstanding)
-  for (; m + 3 * kR < m1; m += 4 * kR) {
-    accum_row<MODE>(x, dy, mask, m, C, c, k, s1, s2);
-    accum_row<MODE>(x, dy, mask, m + kR, C, c, k, s1, s2);
-    accum_row<MODE>(x, dy, mask, m + 2 * kR, C, c, k, s1, s2);
-    accum_row<MODE>(x, dy, mask, m + 3 * kR, C, c, k, s1, s2);
-  }
-  for (; m < m1; m += kR) accum_row<MODE>(x, dy, mask, m, C, c, k, s1, s2);
-
-  // reduce the 32 row-groups through LDS: sm[0][r][64] = s1, sm[1][r][64] = s2
-  float* d0 = &sm[r * kCC + l * 8];
-  float* d1 = &sm[kR * kCC + r * kCC + l * 8];
-  *reinterpret_cast<float4*>(d0) = make_float4(s1[0], s1[1], s1[2], s1[3]);
-  *reinterpret_cast<float4*>(d0 + 4) = make_float4(s1[4], s1[5], s1[6], s1[7]);
-  *reinterpret_cast<float4*>(d1) = make_float4(s2[0], s2[1], s2[2], s2[3]);
-  *reinterpret_cast<float4*>(d1 + 4) = make_float4(s2[4], s2[5], s2[6], s2[7]);
-  __syncthreads();
-  float* slab = part + ((int64_t)chunk * nrow + blockIdx.x) * (2 * kCC);
-  if (tid < 2 * kCC) {
-    const int which = tid / kCC, cl = tid % kCC;
-    const float* src = &sm[which * kR * kCC + cl];
-    float a = 0.f;
-#pragma unroll 8
-    for (int rr = 0; rr < kR; ++rr) a += src[rr * kCC];
-    slab[tid] = a;  // [0..63] = S1, [64..127] = S2
-  }
-  // publish the slab, take a ticket (G16 counter form)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned t = __hip_atomic_fetch_add(&counters[chunk], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    sm[2 * kR * kCC] = (t == (unsigned)(nrow - 1)) ? 1.f : 0.f;
-  }
-  __syncthreads();
-  if (sm[2 * kR * kCC] == 0.f) return;
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-  // last arriver: fixed-order reduction of the chunk's nrow slabs. The slabs were written by
-  // other CUs/XCDs, so every load is a cross-XCD round trip: issue them 16 at a time as
-  // independent float4 loads (thread t owns float4 column t&31 of every 8th slab).
-  const int col = tid & 31, bg = tid >> 5;
-  const float4* base4 = reinterpret_cast<const float4*>(part + (int64_t)chunk * nrow * (2 * kCC));
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int b0 = bg; b0 < nrow; b0 += 8 * 16) {
-    float4 v[16];
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const int blk = b0 + 8 * u;
-      v[u] = blk < nrow ? base4[(int64_t)blk * 32 + col] : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-#pragma unroll
-    for (int u = 0; u < 16; ++u) { acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w; }
-  }
-  __syncthreads();
-  reinterpret_cast<float4*>(sm)[bg * 32 + col] = acc;
-  __syncthreads();
-  if (tid == 0) counters[chunk] = 0u;  // self-reset for the next launch (stream-ordered)
-  if (tid >= kCC) return;
-  const int ch = chunk * kCC + tid;
-  float S1 = 0.f, S2 = 0.f;
-#pragma unroll
-  for (int q = 0; q < 8; ++q) { S1 += sm[q * 128 + tid]; S2 += sm[q * 128 + kCC + tid]; }
-  bn_finalize<MODE>(ch, S1, S2, fa);
-}
-
-// ---- v2 reduce: U rows in flight per lane, tunable grid, two-level deterministic finalize.
+// ---- deterministic two-level finalize (the v1 single-level and v2 fixed-64-channel reduce kernels
+// were measured slower and removed: v2 3.0-3.8 TB/s vs v3's 5.2-5.6, tools/r50_roofline.py).
 // Blocks of a chunk are grouped kG at a time: the last block to arrive in a group sums the
 // group's slabs (fixed order) into a group slab, and the last group to arrive sums the group
 // slabs (fixed order) and finalizes. The serial tail is then <= kG + nrow/kG slab reads instead
@@ -233,95 +145,6 @@ __device__ __forceinline__ float sum_slabs(const float* __restrict__ base, int n
   }
   for (; i < n; ++i) a += base[(int64_t)i * (2 * kCC) + tid];
   return a;
-}
-
-template <int MODE, int U>
-__global__ __launch_bounds__(kThreads) void bn_reduce2_kernel(
-    const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy, const uint8_t* __restrict__ mask,
-    const float* __restrict__ mean, int64_t M, int C, int64_t rows_per_block, int nrow,
-    float* __restrict__ part, float* __restrict__ gpart, unsigned* __restrict__ counters, FinArgs fa) {
-  __shared__ __attribute__((aligned(16))) float sm[2 * kR * kCC + 4];
-  const int tid = threadIdx.x;
-  const int chunk = blockIdx.y;
-  const int l = tid & (kL - 1), r = tid >> 3;
-  const int c = chunk * kCC + l * 8;
-  const int64_t m0 = (int64_t)blockIdx.x * rows_per_block;
-  const int64_t m1 = min(M, m0 + rows_per_block);
-  float k[8], s1[8], s2[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) { s1[j] = 0.f; s2[j] = 0.f; }
-  if (MODE == 0) ld8_bf16(x + c, k);
-  else ld8_f32(mean + c, k);
-  int64_t m = m0 + r;
-  for (; m + (U - 1) * kR < m1; m += U * kR) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) accum_row<MODE>(x, dy, mask, m + u * kR, C, c, k, s1, s2);
-  }
-  for (; m < m1; m += kR) accum_row<MODE>(x, dy, mask, m, C, c, k, s1, s2);
-
-  float* d0 = &sm[r * kCC + l * 8];
-  float* d1 = &sm[kR * kCC + r * kCC + l * 8];
-  *reinterpret_cast<float4*>(d0) = make_float4(s1[0], s1[1], s1[2], s1[3]);
-  *reinterpret_cast<float4*>(d0 + 4) = make_float4(s1[4], s1[5], s1[6], s1[7]);
-  *reinterpret_cast<float4*>(d1) = make_float4(s2[0], s2[1], s2[2], s2[3]);
-  *reinterpret_cast<float4*>(d1 + 4) = make_float4(s2[4], s2[5], s2[6], s2[7]);
-  __syncthreads();
-  const int ngroups = (nrow + kG - 1) / kG;
-  const int g = blockIdx.x / kG;
-  const int gsize = min(kG, nrow - g * kG);
-  float* slabs = part + (int64_t)chunk * nrow * (2 * kCC);
-  float* gslabs = gpart + (int64_t)chunk * ngroups * (2 * kCC);
-  unsigned* ctr = counters + chunk * (ngroups + 1);
-  float tot = 0.f;  // thread tid < 2*kCC: running column value
-  if (tid < 2 * kCC) {
-    const int which = tid / kCC, cl = tid % kCC;
-    const float* src = &sm[which * kR * kCC + cl];
-#pragma unroll 8
-    for (int rr = 0; rr < kR; ++rr) tot += src[rr * kCC];
-    if (gsize > 1) slabs[(int64_t)blockIdx.x * (2 * kCC) + tid] = tot;
-  }
-  // level 1: last arriver of the group
-  if (gsize > 1) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      const unsigned t = __hip_atomic_fetch_add(&ctr[g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      sm[2 * kR * kCC] = (t == (unsigned)(gsize - 1)) ? 1.f : 0.f;
-    }
-    __syncthreads();
-    if (sm[2 * kR * kCC] == 0.f) return;
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      ctr[g] = 0u;  // self-reset (stream-ordered for the next launch)
-    }
-    __syncthreads();
-    if (tid < 2 * kCC) tot = sum_slabs(slabs + (int64_t)g * kG * (2 * kCC), gsize, tid);
-  }
-  // level 2: last group
-  if (ngroups > 1) {
-    if (tid < 2 * kCC) gslabs[(int64_t)g * (2 * kCC) + tid] = tot;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      const unsigned t = __hip_atomic_fetch_add(&ctr[ngroups], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      sm[2 * kR * kCC + 1] = (t == (unsigned)(ngroups - 1)) ? 1.f : 0.f;
-    }
-    __syncthreads();
-    if (sm[2 * kR * kCC + 1] == 0.f) return;
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      ctr[ngroups] = 0u;
-    }
-    __syncthreads();
-    if (tid < 2 * kCC) tot = sum_slabs(gslabs, ngroups, tid);
-  }
-  __syncthreads();
-  if (tid < 2 * kCC) sm[tid] = tot;
-  __syncthreads();
-  if (tid >= kCC) return;
-  bn_finalize<MODE>(chunk * kCC + tid, sm[tid], sm[kCC + tid], fa);
 }
 
 // ---- v3 reduce: wide channel chunks + software-pipelined loads.
@@ -899,22 +722,9 @@ struct ReduceGeo {
   int64_t rows_per_block;
 };
 
-inline ReduceGeo reduce_geo(int64_t M, int C) {
-  ReduceGeo g;
-  g.nchunks = C / kCC;
-  int64_t nrow = 1024 / g.nchunks;
-  if (nrow > 512) nrow = 512;
-  if (nrow < 4) nrow = 4;
-  const int64_t max_rows = (M + 2 * kR - 1) / (2 * kR);  // >= 2 passes per block
-  if (nrow > max_rows) nrow = max_rows;
-  if (nrow < 1) nrow = 1;
-  g.rows_per_block = (M + nrow - 1) / nrow;
-  g.nrow = (int)((M + g.rows_per_block - 1) / g.rows_per_block);
-  return g;
-}
-
-// Reduce-kernel tuning (bn_tune): variant 1 = single-level finalize, 2 = two-level; total
-// workgroups targeted per call; rows in flight per lane for the forward / backward reduce.
+// Reduce-kernel tuning (bn_tune): variant 3/4 = in-kernel last-arriver finalize (4: also the
+// centred second pass), 5 = separate finalize kernel; total workgroups targeted per call; rows in
+// flight per lane for the forward / backward reduce.
 struct BnTune {
   int variant = 5;
   int target_blocks = 512;  // tools/bn_reduce_sweep.py: 2 workgroups per CU beat 4-16 (10.5 vs 11.5+ ms/step)
@@ -922,24 +732,6 @@ struct BnTune {
   int u_bwd = 4;
 };
 BnTune g_tune;
-
-inline ReduceGeo reduce_geo2(int64_t M, int C, int U) {
-  ReduceGeo g;
-  g.nchunks = C / kCC;
-  int64_t nrow = g_tune.target_blocks / g.nchunks;
-  if (nrow > 1024) nrow = 1024;
-  const int64_t max_rows = (M + (int64_t)U * kR - 1) / ((int64_t)U * kR);  // >= 1 full pass per block
-  if (nrow > max_rows) nrow = max_rows;
-  if (nrow < 1) nrow = 1;
-  g.rows_per_block = (M + nrow - 1) / nrow;
-  g.nrow = (int)((M + g.rows_per_block - 1) / g.rows_per_block);
-  return g;
-}
-
-inline int64_t slab_floats2(const ReduceGeo& g) {
-  const int ngroups = (g.nrow + kG - 1) / kG;
-  return (int64_t)g.nchunks * (g.nrow + ngroups) * 2 * kCC;
-}
 
 // v3: chunk = min(C, 512) channels (C is a multiple of 64; chunks must tile C exactly)
 inline int chunk3(int C) {
@@ -973,14 +765,8 @@ inline int64_t slab_floats3(const ReduceGeo& g, int C) {
 template <int MODE>
 int64_t launch_reduce(const uint16_t* x, const uint16_t* dy, const uint8_t* mask, const float* mean, int64_t M,
                       int C, float* ws, unsigned* counters, const FinArgs& fa, hipStream_t s) {
-  if (g_tune.variant == 1) {
-    const ReduceGeo g = reduce_geo(M, C);
-    hipLaunchKernelGGL(bn_reduce_kernel<MODE>, dim3(g.nrow, g.nchunks), dim3(kThreads), 0, s, x, dy, mask, mean, M,
-                       C, g.rows_per_block, g.nrow, ws, counters, fa);
-    return (int64_t)g.nchunks * g.nrow * 2 * kCC;
-  }
   const int U = MODE == 0 ? g_tune.u_fwd : g_tune.u_bwd;
-  if (g_tune.variant >= 3) {
+  {
     const ReduceGeo g = reduce_geo3(M, C, U);
     float* part = ws;
     float* gpart = ws + (int64_t)g.nrow * 2 * C;
@@ -1002,18 +788,6 @@ int64_t launch_reduce(const uint16_t* x, const uint16_t* dy, const uint8_t* mask
       hipLaunchKernelGGL(bn_fin_kernel<MODE>, dim3(C / 64), dim3(1024), 0, s, part, g.nrow, cc, fa);
     return slab_floats3(g, C);
   }
-  const ReduceGeo g = reduce_geo2(M, C, U);
-  float* part = ws;
-  float* gpart = ws + (int64_t)g.nchunks * g.nrow * 2 * kCC;
-#define PDT_R2(UU)                                                                                          \
-  hipLaunchKernelGGL((bn_reduce2_kernel<MODE, UU>), dim3(g.nrow, g.nchunks), dim3(kThreads), 0, s, x, dy,   \
-                     mask, mean, M, C, g.rows_per_block, g.nrow, part, gpart, counters, fa)
-  if (U >= 16) PDT_R2(16);
-  else if (U >= 8) PDT_R2(8);
-  else if (U >= 4) PDT_R2(4);
-  else PDT_R2(2);
-#undef PDT_R2
-  return slab_floats2(g);
 }
 
 inline int row_grid(int64_t rows) {  // row-wise stem kernels: <= 16 workgroups per CU, grid-stride
@@ -1063,18 +837,12 @@ extern "C" {
 
 // Workspace floats needed by a train fwd/bwd call (partial slabs + per-channel coefficients).
 int64_t pdt_bn_workspace_floats(int64_t M, int C) {
-  const ReduceGeo g1 = reduce_geo(M, C);
-  const int64_t v1 = (int64_t)g1.nchunks * g1.nrow * 2 * kCC;
-  const int64_t v2 = slab_floats2(reduce_geo2(M, C, 2));  // U = 2 gives the most rows
-  const int64_t v3 = slab_floats3(reduce_geo3(M, C, 2), C);
-  int64_t v = v1 > v2 ? v1 : v2;
-  v = v > v3 ? v : v3;
-  return v + 4 * (int64_t)C;
+  return slab_floats3(reduce_geo3(M, C, 2), C) + 4 * (int64_t)C;  // U = 2 gives the most rows
 }
 
 // Select the reduce implementation / grid (benchmarking). Values <= 0 keep the current setting.
 void pdt_bn_tune(int variant, int target_blocks, int u_fwd, int u_bwd) {
-  if (variant > 0) g_tune.variant = variant;
+  if (variant >= 3 && variant <= 5) g_tune.variant = variant;
   if (target_blocks > 0) g_tune.target_blocks = target_blocks;
   if (u_fwd > 0) g_tune.u_fwd = u_fwd;
   if (u_bwd > 0) g_tune.u_bwd = u_bwd;

@@ -251,8 +251,6 @@ __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv1x1_kernel(
     bn_bwd_tile_store<BN, Cf::kWaves>(bs1, bs2, reinterpret_cast<float*>(lds), bs.part, (M + BM - 1) / BM, mt, N, n0);
 }
 
-int g_nt = 0;  // PDT_GEMM_NT=1: non-temporal output stores (experiment switch)
-
 template <class Cf, bool ACC, bool STATS, bool NT, bool BSTATS>
 int launch_nt(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t* c, const uint8_t* cm, float* part,
               int M, int K, int N, const BnSrc& bs, const CGeom& cg, hipStream_t s) {
@@ -272,9 +270,8 @@ int launch_nt(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t*
 template <class Cf, bool ACC, bool STATS, bool BSTATS = false>
 int launch(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t* c, const uint8_t* cm, float* part, int M,
            int K, int N, const BnSrc& bs, const CGeom& cg, hipStream_t s) {
-  const char* e = getenv("PDT_GEMM_NT");  // read per launch (A/B inside one process)
-  g_nt = (e && e[0] == '1') ? 1 : 0;
-  if (g_nt) return launch_nt<Cf, ACC, STATS, true, BSTATS>(a, b, y, c, cm, part, M, K, N, bs, cg, s);
+  // (non-temporal output stores, NT = true, measured no gain: default-policy stores keep the
+  // output in L2 for the consuming BatchNorm)
   return launch_nt<Cf, ACC, STATS, false, BSTATS>(a, b, y, c, cm, part, M, K, N, bs, cg, s);
 }
 

@@ -26,6 +26,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 TABLE = os.path.join(ROOT, "tuning", "tunableop_gfx950.csv")
 
 
+def wants_gemm_tuning(model: str, grad_accum: int, hipgraph: bool) -> bool:
+    """One predicate for every entry point (bench.py, cli.py): the measured table pays off for big
+    GEMMs only. TunableOp's per-call host lookup costs more than it saves on launch-bound models
+    (LeNet, MLP: 177k -> 131k img/s) and on eager micro-batched steps (ViT 4 x 32: 3,190 -> 2,999);
+    a hipGraph replay pays the lookup once, at capture."""
+    return model not in ("lenet", "mlp") and (grad_accum == 1 or bool(hipgraph))
+
+
 def use_repo_gemm_tuning(device_index: int | None = None, table: str | None = None) -> str | None:
     """Enable TunableOp with the committed table. Returns the filename pattern used, or None
     when disabled (``PDT_GEMM_TUNING=0``) or when the table is missing. Explicit

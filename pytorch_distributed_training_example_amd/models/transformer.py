@@ -12,13 +12,13 @@ Not in the reference (LeNet only). MI355X-first choices:
 from __future__ import annotations
 
 import math
-import os
 from typing import Optional
 
 import torch
 import torch.nn.functional as F
 from torch import nn
 
+from ..config import SW
 from ..ops.attention import attention_qkv
 from ..ops.gelu import bias_gelu
 from ..ops.layernorm import LayerNorm, add_layer_norm
@@ -88,7 +88,7 @@ def run_blocks(blocks, x: torch.Tensor, final_ln: nn.Module) -> torch.Tensor:
     one add+LN kernel per residual step forward and one LN-backward-with-accumulate backward,
     instead of separate add kernels each way (ops/layernorm.py add_layer_norm)."""
     blocks = list(blocks)
-    if not blocks or os.environ.get("PDT_FUSED_ADDLN", "1") == "0":
+    if not blocks or not SW.fused_addln:
         for blk in blocks:
             x = blk(x)
         return final_ln(x)

@@ -8,7 +8,8 @@ Set ``PDT_DISABLE_NATIVE=1`` to force the reference path (A/B benchmarking only)
 from __future__ import annotations
 
 import importlib
-import os
+
+from ..config import SW
 
 _mod = None
 _err: Exception | None = None
@@ -31,7 +32,7 @@ def available() -> bool:
 
 
 def disabled() -> bool:
-    return os.environ.get("PDT_DISABLE_NATIVE", "0") == "1"
+    return SW.disable_native
 
 
 def native():

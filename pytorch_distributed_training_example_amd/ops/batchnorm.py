@@ -13,13 +13,13 @@ CPU tests and as the numerics oracle.
 """
 from __future__ import annotations
 
-import os
 from typing import Optional
 
 import torch
 import torch.nn.functional as F
 from torch import nn
 
+from ..config import SW
 from ._native import native, use_native
 
 
@@ -85,7 +85,7 @@ class GradStatsSource:
 
 
 def bwd_stats_enabled() -> bool:
-    return os.environ.get("PDT_BN_BWD_STATS", "1") != "0"
+    return SW.bn_bwd_stats
 
 
 def grad_stats_source_of(x: torch.Tensor):
@@ -201,22 +201,43 @@ class _BNEvalFn(torch.autograd.Function):
         return dx, (dz if ctx.has_res else None), None, None, None, None, None, None
 
 
-def deferred_affine_of(t: torch.Tensor):
-    """(a, b) [2, C] if ``t`` is a BatchNorm output whose apply was deferred (t holds the BN's INPUT;
-    its value is a*t + b per channel), else None."""
-    d = getattr(t, "_pdt_res_affine", None)
-    if d is not None and d[1] == t._version:
-        return d[0]
-    return None
+class _MaterializeFn(torch.autograd.Function):
+    """y = a*t + b per channel, where ``t`` is a deferred BatchNorm's autograd output (its storage
+    holds the BN INPUT): the gradient passes through UNCHANGED, because ``_BNTrainFn.backward``
+    already applies the BN chain rule (gamma * invstd and the mean/var terms) to the gradient it
+    receives as the gradient of its output."""
+
+    @staticmethod
+    def forward(ctx, t, ab):
+        shape = (1, -1, 1, 1) if t.dim() == 4 else (1, -1)
+        return (t.float() * ab[0].view(shape) + ab[1].view(shape)).to(t.dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g, None
 
 
-def materialize(t: torch.Tensor) -> torch.Tensor:
-    """The value of a possibly apply-deferred BatchNorm output."""
-    ab = deferred_affine_of(t)
-    if ab is None:
-        return t
-    shape = (1, -1, 1, 1) if t.dim() == 4 else (1, -1)
-    return (t.float() * ab[0].view(shape) + ab[1].view(shape)).to(t.dtype)
+class DeferredBNOutput:
+    """Internal handle for a BatchNorm output whose apply pass was deferred (statistics only; the
+    value is ``a*raw + b`` per channel with ``ab`` = [2, C] fp32). It is NOT a tensor, so nothing
+    can read it as the BN output by accident: the only consumer that takes it as-is is the native
+    fused ``relu(bn3(x) + a*raw + b)`` apply (``batch_norm_act`` with it as ``residual``); every
+    other use must call ``materialize()``. Only ``Bottleneck`` creates one, through
+    ``BatchNorm2d._forward_stats_only`` (never through the public module call, so forward hooks
+    on the BN always see a real output)."""
+
+    __slots__ = ("raw", "ab")
+
+    def __init__(self, raw: torch.Tensor, ab: torch.Tensor):
+        self.raw, self.ab = raw, ab
+
+    def materialize(self) -> torch.Tensor:
+        return _MaterializeFn.apply(self.raw, self.ab)
+
+
+def materialize(t):
+    """The value of a possibly apply-deferred BatchNorm output (a tensor passes through)."""
+    return t.materialize() if isinstance(t, DeferredBNOutput) else t
 
 
 def batch_norm_act(x, residual, weight, bias, running_mean, running_var, training, momentum, eps, relu,
@@ -227,17 +248,20 @@ def batch_norm_act(x, residual, weight, bias, running_mean, running_var, trainin
     ``ResidualGradLink``); only honoured on the native training path — callers check
     ``res_link.grad`` is set before relying on it. ``grad_link``: the output's gradient may arrive
     through this link instead of autograd (the output is the ``residual`` of a BatchNorm given
-    the same link as ``res_link``: a ResNet downsample shortcut's BN). ``defer_apply``: compute the
-    statistics only and return x itself tagged with the affine (a, b); the consumer BN (this output
-    as its ``residual``) adds a*x + b in its own apply pass, so this output is never written — the
-    tag is honoured only by that native path, every other reader goes through ``materialize``."""
-    ab = deferred_affine_of(residual) if residual is not None else None
+    the same link as ``res_link``: a ResNet downsample shortcut's BN). ``defer_apply`` (internal):
+    compute the statistics only and return a ``DeferredBNOutput`` handle (when the native path
+    applies; a plain tensor otherwise); the consumer BN (the handle as its ``residual``) adds
+    a*x + b in its own apply pass, so this output is never written."""
+    ab = None
+    if isinstance(residual, DeferredBNOutput):
+        residual, ab = residual.raw, residual.ab
     nhwc = x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last) or \
         (x.dim() == 2 and x.is_contiguous())
     native_ok = (use_native(x) and x.dtype == torch.bfloat16 and nhwc and x.shape[1] % 64 == 0
                  and (residual is None or (residual.shape == x.shape and residual.dtype == x.dtype)))
     if ab is not None and not (native_ok and training and relu):
-        residual, ab = materialize(residual), None  # only the native relu+residual apply takes (a, b)
+        # only the native relu+residual apply takes (a, b)
+        residual, ab = DeferredBNOutput(residual, ab).materialize(), None
     if native_ok:
         if residual is not None:
             residual = residual.contiguous(memory_format=torch.channels_last if x.dim() == 4
@@ -253,7 +277,7 @@ def batch_norm_act(x, residual, weight, bias, running_mean, running_var, trainin
             y = _BNTrainFn.apply(x, residual, weight, bias, running_mean, running_var,
                                  float(momentum), float(eps), bool(relu), res_link, part, gsrc, grad_link, ab, defer)
             if defer:
-                y._pdt_res_affine = (defer[0], y._version)
+                return DeferredBNOutput(y, defer[0])
             if gsrc is not None:  # a consumer conv may take this BN's backward reduction (ops/conv.py)
                 gsrc.out_version = y._version
                 y._pdt_gsrc = gsrc
@@ -279,7 +303,7 @@ class _BNReluMaxPoolFn(torch.autograd.Function):
         x, code, weight, mean, invstd = ctx.saved_tensors
         need_w = ctx.has_weight and (ctx.needs_input_grad[1] or ctx.needs_input_grad[2])
         dy = dy.contiguous(memory_format=torch.channels_last)
-        if x.shape[1] == 64 and os.environ.get("PDT_STEM_BWD_FUSED", "1") != "0":
+        if x.shape[1] == 64 and SW.stem_bwd_fused:
             # the pool gradient kernel also takes the BN's backward reduction: no pass over (dz, x)
             dx, dg, db = native().maxpool3s2_bwd_bn(dy, code, x, weight, mean, invstd, need_w)
             return dx, (dg if need_w else None), (db if need_w else None), None, None, None, None
@@ -309,7 +333,7 @@ class BatchNorm2d(nn.BatchNorm2d):
 
     def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
                 relu: Optional[bool] = None, res_link: Optional[ResidualGradLink] = None,
-                grad_link: Optional[ResidualGradLink] = None, defer_apply: bool = False) -> torch.Tensor:
+                grad_link: Optional[ResidualGradLink] = None) -> torch.Tensor:
         relu = self.fused_relu if relu is None else relu
         training = self.training or not self.track_running_stats
         momentum = self.momentum
@@ -322,7 +346,30 @@ class BatchNorm2d(nn.BatchNorm2d):
         w = self.weight if self.affine else None
         b = self.bias if self.affine else None
         return batch_norm_act(x, residual, w, b, rm, rv, training, momentum if momentum is not None else 0.0,
-                              self.eps, relu, res_link, grad_link, defer_apply)
+                              self.eps, relu, res_link, grad_link)
+
+    def has_hooks(self) -> bool:
+        """Forward (pre-)hooks registered on this module or globally: they must see real outputs."""
+        from torch.nn.modules import module as _m
+        return bool(self._forward_hooks or self._forward_pre_hooks or _m._global_forward_hooks
+                    or _m._global_forward_pre_hooks)
+
+    def _forward_stats_only(self, x: torch.Tensor, grad_link: Optional[ResidualGradLink] = None):
+        """Internal (``Bottleneck``'s shortcut BN): statistics + running-stat update only, returned
+        as a ``DeferredBNOutput`` on the native training path (a normal output tensor otherwise).
+        Bypasses the module call, so callers use it only when ``has_hooks()`` is False."""
+        training = self.training or not self.track_running_stats
+        momentum = self.momentum
+        if self.training and self.track_running_stats:
+            self._nbt += 1
+            if momentum is None:
+                momentum = 1.0 / float(self._nbt + int(self.num_batches_tracked.item()))
+        rm = self.running_mean if (not self.training or self.track_running_stats) else None
+        rv = self.running_var if (not self.training or self.track_running_stats) else None
+        w = self.weight if self.affine else None
+        b = self.bias if self.affine else None
+        return batch_norm_act(x, None, w, b, rm, rv, training, momentum if momentum is not None else 0.0,
+                              self.eps, False, None, grad_link, defer_apply=True)
 
     def forward_relu_maxpool(self, x: torch.Tensor) -> torch.Tensor:
         """``max_pool2d(relu(bn(x)), 3, 2, 1)`` (ResNet stem) with the pool fused into the BN apply."""

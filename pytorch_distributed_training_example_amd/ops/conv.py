@@ -34,6 +34,7 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
+from ..config import SW
 from ._native import disabled
 
 _CHOICE: Dict[Tuple, str] = {}
@@ -81,93 +82,21 @@ def _ensure_table() -> None:
     if _TABLE_LOADED[0]:
         return
     _TABLE_LOADED[0] = True
-    if os.environ.get("PDT_CONV1X1_TABLE", "1") != "0" and _table_arch_ok():
+    if SW.conv1x1_table and _table_arch_ok():
         load_table()
-    out = os.environ.get("PDT_CONV1X1_DUMP")
-    if out:
-        atexit.register(dump_table, out)
+    if SW.conv1x1_dump:
+        atexit.register(dump_table, SW.conv1x1_dump)
 
-# ---------------------------------------------------------------- weight gradients off the critical path
-# A convolution's weight gradient is needed only by the optimizer / all-reduce, while its data
-# gradient feeds the rest of backward. Issuing the weight-gradient kernel on a side HIP stream
-# lets it run concurrently with the next layers' data-gradient and (bandwidth-bound) BatchNorm
-# backward kernels. The current stream re-joins the side stream (one event wait) before any
-# gradient is read: at every DDP bucket launch and at the end of backward (an autograd-engine
-# callback queued with the first deferred weight gradient of a backward pass).
-# Opt-in (PDT_WGRAD_STREAM=1): measured on one MI355X the concurrency makes ResNet-50 SLOWER
-# (10,212 vs 10,617-10,631 img/s at 512/GPU, tools/gpu_wgrad.sh) — both streams' kernels already
-# fill the chip, and running them together costs cache locality — so the default is in-stream.
-_SIDE: Dict[int, "torch.cuda.Stream"] = {}
-_PENDING: Dict[int, "torch.cuda.Event"] = {}
-_CALLBACK_QUEUED = [False]
-
-
-def _wgrad_stream_enabled() -> bool:
-    return os.environ.get("PDT_WGRAD_STREAM", "0") == "1"
-
-
-def join_wgrad_streams() -> None:
-    """Make the current stream wait for every weight gradient issued on the side stream."""
-    if not _PENDING:
-        return
-    cur = torch.cuda.current_stream()
-    for ev in _PENDING.values():
-        cur.wait_event(ev)
-    _PENDING.clear()
-
-
-def _end_of_backward() -> None:
-    _CALLBACK_QUEUED[0] = False
-    join_wgrad_streams()
-
-
-def _on_side_stream(fn, weight, *used):
-    """Run ``fn()`` (returns ``weight``'s gradient) on the side stream, ordered after the current
-    stream's work; tensors in ``used`` are protected from reuse until the side stream is done.
-
-    The deferral is only safe when autograd will merely *steal* the returned tensor into
-    ``weight.grad`` (no grad yet, strides obeying the parameter's layout); when it would instead
-    accumulate or re-layout on the current stream (gradient accumulation, ``zero_grad(False)``),
-    the current stream joins the side stream immediately — still overlapped with nothing, but
-    correct."""
-    cur = torch.cuda.current_stream()
-    dev = cur.device.index
-    side = _SIDE.get(dev)
-    if side is None:
-        side = _SIDE[dev] = torch.cuda.Stream(device=cur.device)
-    side.wait_stream(cur)
-    with torch.cuda.stream(side):
-        dw = fn()
-    for t in used:
-        t.record_stream(side)
-    dw.record_stream(cur)
-    if weight.grad is not None or dw.stride() != weight.stride():
-        cur.wait_stream(side)
-        return dw
-    ev = torch.cuda.Event()
-    ev.record(side)
-    _PENDING[dev] = ev  # events of one stream complete in order: the latest suffices
-    if not _CALLBACK_QUEUED[0]:
-        _CALLBACK_QUEUED[0] = True
-        torch.autograd.Variable._execution_engine.queue_callback(_end_of_backward)
-    return dw
-
-
-def _mode() -> str:
-    return os.environ.get("PDT_CONV1X1", "auto")
-
-
-def _ours_dirs() -> str:
-    """Directions of stride-1 1x1 convs that run on our MFMA GEMM (csrc/kernels/conv1x1.hip):
-    ``PDT_CONV1X1_OURS`` = comma list of ``fwd`` (with the consuming BatchNorm's statistics
-    fused into the epilogue) and ``dgrad`` (with the shortcut gradient accumulated in place),
-    or ``none``."""
-    return os.environ.get("PDT_CONV1X1_OURS", "fwd,dgrad")
+# Weight gradients run in-stream: a side stream for them measured 4 % SLOWER on ResNet-50 (10,212
+# vs 10,617 img/s, round 2) — both streams' kernels already fill the chip — and was removed.
 
 
 def _ours_ok(direction: str, M: int, K: int, N: int) -> bool:
-    return (direction in _ours_dirs().split(",") and K % 32 == 0 and N % 64 == 0
-            and M * max(K, N) < 2 ** 31 and _mode() in ("auto", "ours"))
+    """Stride-1 1x1 conv direction on our MFMA GEMM (csrc/kernels/conv1x1.hip): ``fwd`` (with the
+    consuming BatchNorm's statistics in the epilogue) or ``dgrad`` (shortcut gradient accumulated
+    in place), if listed in ``PDT_CONV1X1_OURS`` (config.SW)."""
+    return (direction in SW.conv1x1_ours and K % 32 == 0 and N % 64 == 0
+            and M * max(K, N) < 2 ** 31 and SW.conv1x1 in ("auto", "ours"))
 
 
 class BNStats:
@@ -200,38 +129,17 @@ def _time(fn, reps: int = 3) -> float:
     return e0.elapsed_time(e1)
 
 
-def _prefer_ours() -> str:
-    """``PDT_CONV1X1_PREFER``: comma list of directions (``fwd``, ``bwd_data``) that take our GEMM
-    wherever it applies, regardless of the measured table — the table times the conv alone, while
-    our kernel also removes the consuming BatchNorm's reduce pass (forward statistics / backward
-    reduction in its epilogue)."""
-    return os.environ.get("PDT_CONV1X1_PREFER", "")
-
-
-_OVERRIDE_CACHE: Dict[str, Dict[str, str]] = {}
-
-
-def _override(key: Tuple):
-    """``PDT_CONV1X1_OVERRIDE="fwd,bf16,M,Ci,Co=ours+..."`` (``+`` or ``;`` separated): per-shape decisions over the table (read
-    per call, so one process can A/B them: tools/ab_env.py)."""
-    ov = os.environ.get("PDT_CONV1X1_OVERRIDE")
-    if not ov:
-        return None
-    d = _OVERRIDE_CACHE.get(ov)
-    if d is None:
-        d = dict(p.split("=", 1) for p in ov.replace("+", ";").split(";") if "=" in p)
-        _OVERRIDE_CACHE[ov] = d
-    return d.get(_key_str(key))
-
-
 def _pick(key: Tuple, cands: Dict[str, callable]) -> str:
-    mode = _mode()
+    """Backend for one (direction, dtype, M, Ci, Co): forced mode > per-shape override >
+    ``PDT_CONV1X1_PREFER`` (our GEMM also removes the consuming BN's reduce pass, which the
+    conv-only timing does not see) > measured table > time the candidates once."""
+    mode = SW.conv1x1
     if mode in cands:
         return mode
-    o = _override(key)
+    o = SW.conv1x1_override.get(_key_str(key)) if SW.conv1x1_override else None
     if o is not None and o in cands:
         return o
-    if "ours" in cands and key[0] in _prefer_ours().split(","):
+    if "ours" in cands and key[0] in SW.conv1x1_prefer:
         return "ours"
     _ensure_table()
     c = _CHOICE.get(key)
@@ -261,8 +169,7 @@ def _wgrad_splitk(g2: torch.Tensor, x2: torch.Tensor, sk: int) -> torch.Tensor:
     M, Co = g2.shape
     Ci = x2.shape[1]
     part = torch.bmm(g2.view(sk, M // sk, Co).transpose(1, 2), x2.view(sk, M // sk, Ci))
-    if (part.is_cuda and part.dtype == torch.bfloat16 and (Co * Ci) % 8 == 0
-            and os.environ.get("PDT_SLICE_SUM", "1") != "0"):
+    if part.is_cuda and part.dtype == torch.bfloat16 and (Co * Ci) % 8 == 0 and SW.slice_sum:
         from ._native import native
         return native().slice_sum(part)  # csrc/kernels/slice_sum.hip: bf16 out, fp32 accumulation
     return part.sum(0)
@@ -325,28 +232,16 @@ class _Conv1x1Fn(torch.autograd.Function):
         if isinstance(acc, StridedGrad):  # a stride-2 shortcut's compact gradient: added below
             strided, acc = acc, None
         from .batchnorm import MaskedGrad
-        if (strided is not None and ctx.needs_input_grad[0] and gy.dtype == torch.bfloat16
-                and _ours_ok("dgrad", M, Co, Ci) and os.environ.get("PDT_STRIDED_ACC", "0") == "1"):
-            # the stride-2 shortcut's compact gradient is added in our GEMM's epilogue (at the sampled
-            # pixels) instead of a strided add pass afterwards: dx leaves the GEMM final. Opt-in:
-            # measured 0.4% slower on ResNet-50 (12,235 vs 12,284 img/s, tools/gpu_sacc.sh) — these
-            # three dgrad shapes run faster on hipBLASLt than the add pass + BN reduce it saves
-            strided_src, strided = strided, None
-        else:
-            strided_src = None
+        # (the stride-2 shortcut's compact gradient added in our GEMM's epilogue instead of the
+        # strided add pass below measured 0.4 % slower on ResNet-50 — hipBLASLt dgrad + add wins on
+        # those three shapes — and was removed; the kernel keeps the c_stride epilogue)
         # dx is final (nothing is added to it after the GEMM) unless this is the first of two linked
         # branches or a strided shortcut's gradient is added below: only then can the GEMM's epilogue
         # take the producing BatchNorm's backward reduction (GradStatsSource)
         gs = ctx.gsrc if (ctx.gsrc is not None and ctx.gsrc.ready() and not first and strided is None) else None
         bn_kw = dict(bn_x=gs.x, bn_mask=gs.mask, bn_mean=gs.mean) if gs is not None else {}
         gpart = None
-        if strided_src is not None:
-            from ._native import native
-            dx = torch.empty_like(x)
-            gpart = native().conv1x1_gemm(g2, w2.t().contiguous(), _nhwc2d(dx), True, False, strided_src.t,
-                                          c_stride=strided_src.s, c_H=H, c_W=W, **bn_kw)
-            acc = None
-        elif isinstance(acc, MaskedGrad) and ctx.needs_input_grad[0] and _ours_ok("dgrad", M, Co, Ci):
+        if isinstance(acc, MaskedGrad) and ctx.needs_input_grad[0] and _ours_ok("dgrad", M, Co, Ci):
             # dx = dy*mask + dY W: the shortcut's ReLU-masked gradient applied in the GEMM epilogue
             from ._native import native
             dx = torch.empty_like(x)
@@ -397,7 +292,7 @@ class _Conv1x1Fn(torch.autograd.Function):
             ctx.link.grad, dx = dx, None
         if ctx.needs_input_grad[1]:
             cands = {"miopen": lambda: conv_bwd([False, True, False]), "gemm": lambda: torch.mm(g2.t(), x2)}
-            splitk_on = os.environ.get("PDT_WGRAD_SPLITK", "1") != "0"
+            splitk_on = SW.wgrad_splitk
             for sk in _SPLITK if splitk_on else ():
                 if M % sk == 0 and M // sk >= 256:
                     cands[f"splitk{sk}"] = (lambda sk=sk: _wgrad_splitk(g2, x2, sk))
@@ -411,14 +306,13 @@ class _Conv1x1Fn(torch.autograd.Function):
                 wfn = lambda: _wgrad_splitk(g2, x2, sk).as_strided(weight.shape, weight.stride())  # noqa: E731
             else:
                 wfn = lambda: conv_bwd([False, True, False])[1]  # noqa: E731
-            dw = _on_side_stream(wfn, weight, gy, x) if _wgrad_stream_enabled() else wfn()
+            dw = wfn()
         return dx, dw, None, None, None
 
 
 def _subsample_native(t: torch.Tensor) -> bool:
     return (t.is_cuda and t.dtype == torch.bfloat16 and t.dim() == 4 and t.shape[1] % 8 == 0
-            and t.is_contiguous(memory_format=torch.channels_last) and not disabled()
-            and os.environ.get("PDT_SUBSAMPLE_NATIVE", "1") != "0")
+            and t.is_contiguous(memory_format=torch.channels_last) and not disabled() and SW.subsample_native)
 
 
 class StridedGrad:
@@ -529,8 +423,7 @@ class _LinkedConvFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = torch.ops.aten.convolution_backward(*args, [True, False, False])[0]
         if ctx.needs_input_grad[1]:
-            wfn = lambda: torch.ops.aten.convolution_backward(*args, [False, True, False])[1]  # noqa: E731
-            dw = _on_side_stream(wfn, weight, gy, x) if _wgrad_stream_enabled() else wfn()
+            dw = torch.ops.aten.convolution_backward(*args, [False, True, False])[1]
         if dx is not None:
             acc = ctx.link.take()
             if acc is None:
@@ -540,39 +433,10 @@ class _LinkedConvFn(torch.autograd.Function):
         return dx, dw, None, None, None
 
 
-class _SplitConvFn(torch.autograd.Function):
-    """Bias-free convolution whose weight gradient runs on the side stream (see above)."""
-
-    @staticmethod
-    def forward(ctx, x, weight, stride, padding, dilation, groups):
-        ctx.save_for_backward(x, weight)
-        ctx.cfg = (list(stride), list(padding), list(dilation), groups)
-        return F.conv2d(x, weight, None, stride, padding, dilation, groups)
-
-    @staticmethod
-    def backward(ctx, gy):
-        x, weight = ctx.saved_tensors
-        stride, padding, dilation, groups = ctx.cfg
-        gy = gy.contiguous(memory_format=torch.channels_last) if x.is_contiguous(
-            memory_format=torch.channels_last) else gy.contiguous()
-        args = (gy, x, weight, None, stride, padding, dilation, False, [0, 0], groups)
-        dx = dw = None
-        if ctx.needs_input_grad[0]:
-            dx = torch.ops.aten.convolution_backward(*args, [True, False, False])[0]
-        if ctx.needs_input_grad[1]:
-            wfn = lambda: torch.ops.aten.convolution_backward(*args, [False, True, False])[1]  # noqa: E731
-            dw = _on_side_stream(wfn, weight, gy, x)
-        return dx, dw, None, None, None, None
-
-
-def _conv3x3_mode() -> str:
-    return os.environ.get("PDT_CONV3X3", "ours")
-
-
 class _Conv3x3Fn(torch.autograd.Function):
     """Stride-1 pad-1 3x3 convolution on our MFMA implicit-GEMM kernels (csrc/kernels/conv3x3.hip):
     forward = conv3x3s1(x, w); data gradient = the SAME kernel on dY with the weights flipped and
-    transposed (conv3x3_flip); weight gradient = MIOpen (optionally on the side stream)."""
+    transposed (conv3x3_flip); weight gradient = MIOpen."""
 
     @staticmethod
     def forward(ctx, x, weight, stats_out=None, gsrc=None):
@@ -603,14 +467,8 @@ class _Conv3x3Fn(torch.autograd.Function):
                 dx = native().conv3x3s1_fwd(gy, native().conv3x3_flip(weight))
         if ctx.needs_input_grad[1]:
             args = (gy, x, weight, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1)
-            wfn = lambda: torch.ops.aten.convolution_backward(*args, [False, True, False])[1]  # noqa: E731
-            dw = _on_side_stream(wfn, weight, gy, x) if _wgrad_stream_enabled() else wfn()
+            dw = torch.ops.aten.convolution_backward(*args, [False, True, False])[1]
         return dx, dw, None, None
-
-
-def _stats_enabled() -> bool:
-    """``PDT_CONV_BN_STATS=0`` turns off the BatchNorm statistics epilogues of our convs."""
-    return os.environ.get("PDT_CONV_BN_STATS", "1") != "0"
 
 
 def conv3x3_eligible(conv: nn.Conv2d, x: torch.Tensor) -> bool:
@@ -620,7 +478,7 @@ def conv3x3_eligible(conv: nn.Conv2d, x: torch.Tensor) -> bool:
             and conv.dilation == (1, 1) and conv.groups == 1 and conv.bias is None and conv.padding_mode == "zeros"
             and x.is_cuda and x.dim() == 4 and x.dtype == torch.bfloat16 and conv.weight.dtype == torch.bfloat16
             and x.is_contiguous(memory_format=torch.channels_last) and x.shape[1] % 64 == 0
-            and conv.out_channels % 64 == 0 and _conv3x3_mode() == "ours" and not disabled())
+            and conv.out_channels % 64 == 0 and SW.conv3x3 == "ours" and not disabled())
 
 
 class _StemConvFn(torch.autograd.Function):
@@ -645,10 +503,9 @@ class _StemConvFn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             if x.shape[3] <= 224:
                 from ._native import native
-                wfn = lambda: native().stem_conv_wgrad(x, gy)  # noqa: E731
+                dw = native().stem_conv_wgrad(x, gy)
             else:
-                wfn = lambda: torch.ops.aten.convolution_backward(*args, [False, True, False])[1]  # noqa: E731
-            dw = _on_side_stream(wfn, weight, gy, x) if _wgrad_stream_enabled() else wfn()
+                dw = torch.ops.aten.convolution_backward(*args, [False, True, False])[1]
         return dx, dw
 
 
@@ -660,21 +517,20 @@ def stem_eligible(conv: nn.Conv2d, x: torch.Tensor) -> bool:
             and conv.in_channels == 3 and conv.out_channels == 64 and x.is_cuda and x.dim() == 4
             and x.dtype == torch.bfloat16 and conv.weight.dtype == torch.bfloat16
             and x.is_contiguous(memory_format=torch.channels_last) and x.shape[3] % 32 == 0
-            and os.environ.get("PDT_CONV_STEM", "ours") == "ours" and not disabled())
+            and SW.conv_stem == "ours" and not disabled())
 
 
 class SplitConv2d(nn.Conv2d):
     """``nn.Conv2d`` (same parameters / state_dict). On the GPU, stride-1 3x3 convolutions and
     the ResNet stem run on our MFMA kernels (``_Conv3x3Fn`` / ``_StemConvFn``;
-    ``PDT_CONV3X3=miopen`` / ``PDT_CONV_STEM=miopen`` switch back); the training backward can
-    issue the weight gradient on a side stream (``PDT_WGRAD_STREAM=1``)."""
+    ``PDT_CONV3X3=miopen`` / ``PDT_CONV_STEM=miopen`` switch back)."""
 
     emit_bn_stats = True  # output feeds a BatchNorm: fuse its statistics where our kernel runs
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if conv3x3_eligible(self, x):
             holder = [] if (self.emit_bn_stats and self.training and torch.is_grad_enabled()
-                            and _stats_enabled()) else None
+                            and SW.conv_bn_stats) else None
             from .batchnorm import grad_stats_source_of
             y = _Conv3x3Fn.apply(x, self.weight, holder,
                                  grad_stats_source_of(x) if self.training and torch.is_grad_enabled() else None)
@@ -683,9 +539,6 @@ class SplitConv2d(nn.Conv2d):
             return y
         if stem_eligible(self, x):
             return _StemConvFn.apply(x, self.weight)
-        if (self.bias is None and x.is_cuda and self.padding_mode == "zeros" and torch.is_grad_enabled()
-                and self.weight.requires_grad and _wgrad_stream_enabled() and not disabled()):
-            return _SplitConvFn.apply(x, self.weight, self.stride, self.padding, self.dilation, self.groups)
         return super().forward(x)
 
 
@@ -706,7 +559,7 @@ class Conv1x1(nn.Conv2d):
 
     def _gemm_ok(self, x: torch.Tensor) -> bool:
         return (x.is_cuda and x.dim() == 4 and x.dtype == self.weight.dtype and self.padding == (0, 0)
-                and x.is_contiguous(memory_format=torch.channels_last) and _mode() != "off" and not disabled())
+                and x.is_contiguous(memory_format=torch.channels_last) and SW.conv1x1 != "off" and not disabled())
 
     def gemm_eligible(self, x: torch.Tensor) -> bool:
         return self.stride == (1, 1) and self._gemm_ok(x)
@@ -715,21 +568,21 @@ class Conv1x1(nn.Conv2d):
         """Our dgrad GEMM can take the shortcut gradient as (dy, ReLU mask) (``MaskedGrad``):
         ``PDT_RES_MASKED=0`` turns the hand-off off."""
         N, Ci, H, W = x.shape
-        return (os.environ.get("PDT_RES_MASKED", "1") != "0" and x.dtype == torch.bfloat16
+        return (SW.res_masked and x.dtype == torch.bfloat16
                 and self.gemm_eligible(x) and _ours_ok("dgrad", N * H * W, self.out_channels, Ci))
 
     def strided_gemm_eligible(self, x: torch.Tensor) -> bool:
         s = self.stride[0]
         # gather + our GEMM (BN statistics fused) + split-K weight gradient: ResNet-50 +1.7% over
         # MIOpen's strided kernels (12,318 vs 12,118 img/s, tools/gpu_s2b.sh; PDT_CONV1X1_S2=0 = MIOpen)
-        return s > 1 and self.stride == (s, s) and self._gemm_ok(x) and os.environ.get("PDT_CONV1X1_S2", "1") == "1"
+        return s > 1 and self.stride == (s, s) and self._gemm_ok(x) and SW.conv1x1_s2
 
     def forward(self, x: torch.Tensor, res_link=None) -> torch.Tensor:
         """``res_link``: a ``ResidualGradLink`` whose gradient (the other branch's gradient of
         ``x``) meets this conv's input gradient; requires one of the GEMM paths."""
         if self.gemm_eligible(x):
             holder = [] if (self.emit_bn_stats and self.training and torch.is_grad_enabled()
-                            and _stats_enabled()) else None
+                            and SW.conv_bn_stats) else None
             from .batchnorm import grad_stats_source_of
             y = _Conv1x1Fn.apply(x, self.weight, res_link, holder,
                                  grad_stats_source_of(x) if self.training and torch.is_grad_enabled() else None)
@@ -738,7 +591,7 @@ class Conv1x1(nn.Conv2d):
             return y
         if self.strided_gemm_eligible(x):
             holder = [] if (self.emit_bn_stats and self.training and torch.is_grad_enabled()
-                            and _stats_enabled()) else None
+                            and SW.conv_bn_stats) else None
             y = _Conv1x1StridedFn.apply(x, self.weight, self.stride[0], res_link, holder)
             if holder:
                 y._pdt_bn_stats = BNStats(holder[0], y._version)

@@ -7,12 +7,12 @@ HBM rate (profiles/r1_steady_gpt2_medium_ours.md: 73 ``reduce_kernel`` calls, 1.
 """
 from __future__ import annotations
 
-import os
 from typing import Dict, Optional, Tuple
 
 import torch
 import torch.nn.functional as F
 
+from ..config import SW
 from ._native import native, use_native
 
 # weight gradient dW = dY^T X sums over all tokens (K = 6K-25K): one hipBLASLt GEMM leaves most of
@@ -26,7 +26,7 @@ _WG_CHOICE: Dict[Tuple, int] = {}
 def _wgrad(dy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
     from .conv import _wgrad_splitk
     T = dy2.shape[0]
-    if os.environ.get("PDT_LINEAR_SPLITK", "1") == "0" or not dy2.is_cuda:
+    if not SW.linear_splitk or not dy2.is_cuda:
         return dy2.t() @ x2
     key = (T, dy2.shape[1], x2.shape[1], dy2.dtype)
     sk = _WG_CHOICE.get(key)

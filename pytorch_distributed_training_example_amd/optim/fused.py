@@ -26,7 +26,6 @@ import torch
 from torch.optim import Optimizer
 
 from ..ops._native import native, use_native
-from ..ops.conv import join_wgrad_streams
 
 
 def _capturing() -> bool:
@@ -92,7 +91,6 @@ class _FusedOptimizer(Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
-        join_wgrad_streams()  # no-op unless a backward left side-stream weight gradients pending
         for gi, group in enumerate(self.param_groups):
             for key, ps in self._buckets(group).items():
                 self._init_state(group, ps)

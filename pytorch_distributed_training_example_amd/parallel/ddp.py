@@ -36,7 +36,6 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from ..ops import multi_tensor
-from ..ops.conv import join_wgrad_streams
 from .buckets import (DEFAULT_BUCKET_CAP_MB, DEFAULT_FIRST_BUCKET_BYTES, BucketSpec,
                       compute_bucket_assignment)
 
@@ -124,7 +123,7 @@ class _Bucket:
 def _default_avg_op(pg) -> tuple[Any, bool]:
     """(op, needs_divide). RCCL averages in-collective; gloo has no AVG."""
     backend = dist.get_backend(pg)
-    if backend == "nccl":
+    if backend == "nccl" or (backend == "pdt_p2p" and torch.cuda.is_available()):
         return dist.ReduceOp.AVG, False
     return dist.ReduceOp.SUM, True
 
@@ -149,6 +148,7 @@ class DistributedDataParallel(nn.Module):
         first_bucket_mb: Optional[float] = None,
         reduce_dtype: Optional[torch.dtype] = None,
         rebuild_buckets: bool = True,
+        reduce_single_rank: bool = False,
     ):
         super().__init__()
         self.module = module
@@ -171,6 +171,11 @@ class DistributedDataParallel(nn.Module):
         self._comm_hook: Optional[Callable] = None
         self._comm_hook_state: Any = None
         self._rebuild_enabled = rebuild_buckets and not static_graph
+        # torch DDP packs buckets and issues the all-reduce even with ONE rank; ours skips that work
+        # at world 1 unless asked (bench.py asks, so its N=1 point carries the same per-step
+        # reducer work — pack copies, RCCL launch, stream joins — as N>1, and a captured step
+        # holds a real collective)
+        self.reduce_single_rank = bool(reduce_single_rank) and self.process_group is not None
         self._ready_order: List[int] = []
         self._rebuilt = False
         self._rebuild_pending = False
@@ -189,7 +194,7 @@ class DistributedDataParallel(nn.Module):
             self._params.append(p)
             self._param_names.append(name)
         self._buffers_to_sync = [b for n, b in module.named_buffers() if n not in ignore]
-        if self.process_group is not None and self.world_size > 1:
+        if self.process_group is not None and (self.world_size > 1 or self.reduce_single_rank):
             self._avg_op, self._needs_div = _default_avg_op(self.process_group)
         else:
             self._avg_op, self._needs_div = None, False
@@ -265,8 +270,8 @@ class DistributedDataParallel(nn.Module):
         return hook
 
     def _active(self) -> bool:
-        """Buckets/collectives are only needed with >1 rank or a comm hook."""
-        return self.world_size > 1 or self._comm_hook is not None
+        """Buckets/collectives are only needed with >1 rank, a comm hook, or ``reduce_single_rank``."""
+        return self.world_size > 1 or self._comm_hook is not None or self.reduce_single_rank
 
     def _on_grad_ready(self, index: int, param: torch.Tensor) -> None:
         if not self.require_backward_grad_sync or not self._active():
@@ -313,7 +318,6 @@ class DistributedDataParallel(nn.Module):
 
     def _launch(self, bucket: _Bucket) -> None:
         bucket.launched = True
-        join_wgrad_streams()  # weight gradients issued on the side stream (ops/conv.py)
         self._pack(bucket)
         if bucket.comm_buffer is not bucket.buffer:
             multi_tensor.copy_([bucket.buffer], [bucket.comm_buffer])

@@ -117,7 +117,10 @@ def init_distributed(
             torch.cuda.set_device(dev_idx)
         device = torch.device("cuda", dev_idx)
 
-    if world_size > 1 or backend == "nccl" or os.environ.get("PDT_FORCE_PG"):
+    if backend == "pdt_p2p":  # xGMI P2P all-reduce + RCCL for the rest (parallel/p2p.py)
+        from .p2p import register_backend
+        register_backend()
+    if world_size > 1 or backend in ("nccl", "pdt_p2p") or os.environ.get("PDT_FORCE_PG"):
         if not dist.is_initialized():
             kwargs: dict[str, Any] = dict(
                 backend=backend,

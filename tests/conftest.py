@@ -16,6 +16,28 @@ make_miopen_capture_safe()
 use_repo_miopen_cache()
 
 
+@pytest.fixture(autouse=True)
+def _reload_switches():
+    """Switches are read once per process (config.SW): re-read them after every test so a test's
+    env changes (monkeypatch, undone at teardown) never leak into the next one."""
+    yield
+    from pytorch_distributed_training_example_amd.config import SW
+    SW.reload()
+
+
+@pytest.fixture
+def switch(monkeypatch):
+    """switch("PDT_X", "v"): set a PDT_* switch for this test (env + config.SW reload)."""
+    from pytorch_distributed_training_example_amd.config import SW
+
+    def set_(name, value):
+        monkeypatch.setenv(name, value)
+        SW.reload()
+    yield set_
+    monkeypatch.undo()
+    SW.reload()
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (runs via gpurun)")
     config.addinivalue_line("markers", "slow: long-running test")

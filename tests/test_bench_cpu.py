@@ -13,11 +13,15 @@ KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "
         "scaling", "vs_baseline", "dtype", "data", "config"}
 
 
-def _run(nproc, port, extra=()):
+def _run(nproc, port, extra=(), self_launch=False):
     env = dict(os.environ, OMP_NUM_THREADS="2", MASTER_ADDR="127.0.0.1")
-    args = ["--steps", "2", "--warmup", "1", "--batch-size", "2", "--image-size", "32", *extra]
-    if nproc == 1:
-        cmd = [sys.executable, "bench.py", *args]
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_PORT"):
+        env.pop(k, None)
+    args = ["--steps", "2", "--warmup", "1", "--image-size", "32", *extra]
+    if not any(a in ("--batch-size", "--global-batch") for a in extra):
+        args += ["--batch-size", "2"]
+    if nproc == 1 or self_launch:
+        cmd = [sys.executable, "bench.py", "--gpus", str(nproc), *args]
     else:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
                "--master-addr", "127.0.0.1", f"--master-port={port}", "bench.py", "--gpus", str(nproc), *args]
@@ -40,3 +44,26 @@ def test_bench_json_contract(nproc, port):
     assert r["scaling"] == "weak" and r["higher_is_better"] is True and r["dtype"] == "bf16"
     # value is the whole-job aggregate derived from the (max over ranks) step time
     assert r["value"] == pytest.approx(2 * nproc / (r["ms_per_step"] / 1e3), rel=1e-2)
+
+
+def test_bench_gpus_flag_self_launches():
+    """``python bench.py --gpus 4`` (no launcher) must run 4 ranks itself, like the reference's one
+    command that uses every GPU (train.py:138,147)."""
+    r = _run(4, 0, self_launch=True)
+    assert r["n_gpus"] == 4 and r["config"]["parallelism"] == "dp4"
+    assert r["config"]["global_batch"] == 8
+
+
+def test_bench_world_size_mismatch_refused():
+    env = dict(os.environ, OMP_NUM_THREADS="2", WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "4", "--steps", "1", "--warmup", "0"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=200)
+    assert p.returncode != 0 and "WORLD_SIZE=2" in p.stderr
+    assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_bench_global_batch_strong_scaling():
+    """--global-batch G: per-rank ceil(G/N) (train.py:82), reported as strong scaling."""
+    r = _run(2, 0, extra=("--global-batch", "5"), self_launch=True)
+    assert r["scaling"] == "strong" and r["config"]["per_gpu_batch"] == 3
+    assert r["config"]["global_batch"] == 6 and r["n_gpus"] == 2

@@ -95,7 +95,7 @@ def test_bn_from_tile_stats_matches_reduce_bn(relu, res, shape):
     torch.testing.assert_close(ot[3], (var + 1e-5).rsqrt(), rtol=1e-3, atol=1e-4)
 
 
-def test_resnet_bottleneck_uses_fused_stats(monkeypatch):
+def test_resnet_bottleneck_uses_fused_stats(monkeypatch, switch):
     """A training Bottleneck on the fused path matches the same block with our GEMM off
     (library GEMMs + reduce-pass BatchNorm): outputs, input and parameter gradients."""
     from pytorch_distributed_training_example_amd.models import resnet as R
@@ -107,8 +107,8 @@ def test_resnet_bottleneck_uses_fused_stats(monkeypatch):
     x0 = torch.randn(16, 64, 28, 28, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
     res = {}
     for ours in ("fwd,dgrad", "none"):
-        monkeypatch.setenv("PDT_CONV1X1_OURS", ours)
-        monkeypatch.setenv("PDT_CONV1X1", "ours" if ours != "none" else "gemm")
+        switch("PDT_CONV1X1_OURS", ours)
+        switch("PDT_CONV1X1", "ours" if ours != "none" else "gemm")
         blk.zero_grad(set_to_none=True)
         x = x0.clone().requires_grad_(True)
         h = blk.conv1(x)
@@ -167,7 +167,7 @@ def test_gemm_accumulates_masked_source():
 
 
 @pytest.mark.parametrize("masked", ["1", "0"])
-def test_identity_block_masked_residual_matches_plain(monkeypatch, masked):
+def test_identity_block_masked_residual_matches_plain(monkeypatch, masked, switch):
     """Identity Bottleneck: bn3 handing the shortcut gradient over as (dy, mask) gives the same
     gradients as the materialised dres path and as autograd's own add (link off)."""
     from pytorch_distributed_training_example_amd.models import resnet as R
@@ -175,8 +175,8 @@ def test_identity_block_masked_residual_matches_plain(monkeypatch, masked):
     torch.manual_seed(0)
     blk = to_bf16_mixed(R.Bottleneck(256, 64, 1, None).cuda().to(memory_format=torch.channels_last))
     x0 = torch.randn(8, 256, 14, 14, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
-    monkeypatch.setenv("PDT_RES_MASKED", masked)
-    monkeypatch.setenv("PDT_CONV1X1", "ours")
+    switch("PDT_RES_MASKED", masked)
+    switch("PDT_CONV1X1", "ours")
     out = {}
     for linked in (True, False):
         R.RESIDUAL_GRAD_LINK[0] = linked
@@ -258,7 +258,7 @@ def test_bn_backward_from_tiles_matches_reduce(relu, res):
         torch.testing.assert_close(t[1], r[1], rtol=0, atol=0)
 
 
-def test_bottleneck_chain_takes_bn_backward_stats(monkeypatch):
+def test_bottleneck_chain_takes_bn_backward_stats(monkeypatch, switch):
     """Two Bottlenecks (downsample + identity): with the BN-backward hand-off on, bn2 (conv3's
     dgrad) and the first block's bn3 (the second block's conv1 dgrad, shortcut accumulated) take
     their reduction from the GEMM epilogue — and every gradient matches the hand-off-off run."""
@@ -270,7 +270,7 @@ def test_bottleneck_chain_takes_bn_backward_stats(monkeypatch):
     net = to_bf16_mixed(torch.nn.Sequential(R.Bottleneck(64, 64, 1, ds), R.Bottleneck(256, 64, 1, None))
                         .cuda().to(memory_format=torch.channels_last))
     x0 = torch.randn(8, 64, 28, 28, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
-    monkeypatch.setenv("PDT_CONV1X1", "ours")
+    switch("PDT_CONV1X1", "ours")
     used = []
     orig = B.GradStatsSource.take
 
@@ -281,7 +281,7 @@ def test_bottleneck_chain_takes_bn_backward_stats(monkeypatch):
     monkeypatch.setattr(B.GradStatsSource, "take", spy)
     out = {}
     for on in ("1", "0"):
-        monkeypatch.setenv("PDT_BN_BWD_STATS", on)
+        switch("PDT_BN_BWD_STATS", on)
         used.clear()
         net.zero_grad(set_to_none=True)
         x = x0.clone().requires_grad_(True)
@@ -296,7 +296,7 @@ def test_bottleneck_chain_takes_bn_backward_stats(monkeypatch):
 
 
 @pytest.mark.parametrize("shape", [(4, 64, 56, 56), (3, 64, 17, 23)])
-def test_stem_pool_backward_fused_reduction(monkeypatch, shape):
+def test_stem_pool_backward_fused_reduction(monkeypatch, shape, switch):
     """Stem BN+ReLU+MaxPool backward: the pool-gradient kernel taking the BN's backward reduction
     (PDT_STEM_BWD_FUSED=1) gives the same dx / dgamma / dbeta as the separate reduce pass."""
     from pytorch_distributed_training_example_amd.ops.batchnorm import BatchNorm2d
@@ -309,7 +309,7 @@ def test_stem_pool_backward_fused_reduction(monkeypatch, shape):
     out = {}
     gy = None
     for fused in ("1", "0"):
-        monkeypatch.setenv("PDT_STEM_BWD_FUSED", fused)
+        switch("PDT_STEM_BWD_FUSED", fused)
         bn.zero_grad(set_to_none=True)
         x = x0.clone().requires_grad_(True)
         y = bn.forward_relu_maxpool(x)
@@ -386,18 +386,16 @@ def test_gemm_accumulates_strided_compact_source():
     torch.testing.assert_close(out.float(), ref, rtol=2e-2, atol=2e-2)
 
 
-@pytest.mark.parametrize("strided_acc", ["1", "0"])
-def test_downsample_stride2_block_strided_acc(monkeypatch, strided_acc):
-    """Stride-2 downsample Bottleneck (gathered shortcut GEMM): conv1's dgrad adding the shortcut's
-    compact gradient in its epilogue matches the strided add pass and the plain autograd path."""
+def test_downsample_stride2_block_strided_grad(monkeypatch, switch):
+    """Stride-2 downsample Bottleneck (gathered shortcut GEMM): the shortcut's compact gradient
+    added into conv1's full gradient matches the plain autograd path."""
     from pytorch_distributed_training_example_amd.models import resnet as R
     from pytorch_distributed_training_example_amd.models.precision import to_bf16_mixed
     torch.manual_seed(0)
     ds = R._Downsample(R.conv1x1(256, 512, 2), R._bn(512))
     blk = to_bf16_mixed(R.Bottleneck(256, 128, 2, ds).cuda().to(memory_format=torch.channels_last))
     x0 = torch.randn(8, 256, 14, 14, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
-    monkeypatch.setenv("PDT_STRIDED_ACC", strided_acc)  # opt-in path ("1") and the default ("0")
-    monkeypatch.setenv("PDT_CONV1X1", "ours")
+    switch("PDT_CONV1X1", "ours")
     out = {}
     for linked in (True, False):
         R.RESIDUAL_GRAD_LINK[0] = linked
@@ -414,40 +412,90 @@ def test_downsample_stride2_block_strided_acc(monkeypatch, strided_acc):
         assert err < 2e-2, err
 
 
-@pytest.mark.parametrize("stride", [1, 2])
-def test_downsample_bn_deferred_apply(monkeypatch, stride):
-    """Downsample Bottleneck with the shortcut BN's apply deferred into bn3's (PDT_DS_DEFER=1, the
-    shortcut BN output never written) == the materialised shortcut (=0): output, input and
-    parameter gradients, running statistics."""
+def _ds_block_run(blk, x0, defer, bn3_eval=False):
     from pytorch_distributed_training_example_amd.models import resnet as R
-    from pytorch_distributed_training_example_amd.models.precision import to_bf16_mixed
-    torch.manual_seed(0)
-    ds = R._Downsample(R.conv1x1(128, 256, stride), R._bn(256))
-    blk = to_bf16_mixed(R.Bottleneck(128, 64, stride, ds).cuda().to(memory_format=torch.channels_last))
-    x0 = torch.randn(8, 128, 14, 14, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
-    out = {}
-    for defer in ("1", "0"):
-        monkeypatch.setenv("PDT_DS_DEFER", defer)
+    ds = blk.downsample
+    old = R.DS_DEFER_APPLY[0]
+    R.DS_DEFER_APPLY[0] = defer
+    try:
+        blk.train()
+        if bn3_eval:
+            blk.bn3.eval()
         blk.zero_grad(set_to_none=True)
         ds[1].running_mean.zero_()
         ds[1].running_var.fill_(1)
         x = x0.clone().requires_grad_(True)
         y = blk(x)
         y.backward(torch.ones_like(y) * 0.01 + y.detach() * 0.1)
-        out[defer] = ([y.float(), x.grad.float()] + [p.grad.float().clone() for p in blk.parameters()]
-                      + [ds[1].running_mean.clone(), ds[1].running_var.clone()])
-    for a, b in zip(out["1"], out["0"]):
+        return ([y.float(), x.grad.float()] + [p.grad.float().clone() for p in blk.parameters()]
+                + [ds[1].running_mean.clone(), ds[1].running_var.clone()])
+    finally:
+        R.DS_DEFER_APPLY[0] = old
+
+
+def _make_ds_block(stride, cin=128, planes=64):
+    from pytorch_distributed_training_example_amd.models import resnet as R
+    from pytorch_distributed_training_example_amd.models.precision import to_bf16_mixed
+    torch.manual_seed(0)
+    ds = R._Downsample(R.conv1x1(cin, planes * 4, stride), R._bn(planes * 4))
+    return to_bf16_mixed(R.Bottleneck(cin, planes, stride, ds).cuda().to(memory_format=torch.channels_last))
+
+
+@pytest.mark.parametrize("stride", [1, 2])
+def test_downsample_bn_deferred_apply(stride):
+    """Downsample Bottleneck with the shortcut BN's apply deferred into bn3's (DS_DEFER_APPLY, the
+    shortcut BN output never written) == the materialised shortcut: output, input and parameter
+    gradients, running statistics."""
+    blk = _make_ds_block(stride)
+    x0 = torch.randn(8, 128, 14, 14, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    a_all, b_all = _ds_block_run(blk, x0, True), _ds_block_run(blk, x0, False)
+    for a, b in zip(a_all, b_all):
+        err = ((a - b).norm() / (b.norm() + 1e-12)).item()
+        assert err < 1e-2, err
+
+
+def test_deferred_shortcut_bn3_eval_gradients():
+    """The deferred shortcut BN materialised for a non-fused consumer (bn3 frozen in eval while the
+    block trains) must pass its gradient through unchanged: x / downsample grads equal the
+    non-deferred run (the materialisation used to multiply the gradient by gamma*invstd again)."""
+    blk = _make_ds_block(1)
+    x0 = torch.randn(8, 128, 14, 14, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    a_all, b_all = _ds_block_run(blk, x0, True, bn3_eval=True), _ds_block_run(blk, x0, False, bn3_eval=True)
+    for a, b in zip(a_all, b_all):
+        err = ((a - b).norm() / (b.norm() + 1e-12)).item()
+        assert err < 1e-2, err
+
+
+def test_deferred_shortcut_forward_hook_sees_real_output():
+    """A forward hook on downsample.1 sees the real BN output (deferral is skipped for hooked BNs)
+    and the block's output is unchanged."""
+    blk = _make_ds_block(1)
+    x0 = torch.randn(8, 128, 14, 14, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    seen = []
+    h = blk.downsample[1].register_forward_hook(lambda m, i, o: seen.append((i[0].detach().clone(), o)))
+    try:
+        hooked = _ds_block_run(blk, x0, True)
+    finally:
+        h.remove()
+    assert len(seen) == 1 and isinstance(seen[0][1], torch.Tensor)
+    xin, out = seen[0]
+    ref = torch.nn.functional.batch_norm(xin.float(), None, None, blk.downsample[1].weight.float(),
+                                         blk.downsample[1].bias.float(), True, 0.0, 1e-5)
+    torch.testing.assert_close(out.float(), ref, rtol=2e-2, atol=2e-2)
+    plain = _ds_block_run(blk, x0, True)
+    for a, b in zip(hooked, plain):
         err = ((a - b).norm() / (b.norm() + 1e-12)).item()
         assert err < 1e-2, err
 
 
 def test_deferred_affine_materializes_for_other_readers():
-    """A deferred BN output read by anything but the native residual apply is materialised."""
-    from pytorch_distributed_training_example_amd.ops.batchnorm import BatchNorm2d, materialize
+    """A deferred BN output is an internal handle; materialize() gives the BN's value."""
+    from pytorch_distributed_training_example_amd.ops.batchnorm import BatchNorm2d, DeferredBNOutput
     torch.manual_seed(0)
     bn = BatchNorm2d(64).cuda()
     x = torch.randn(4, 64, 8, 8, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
-    y_def = bn(x, defer_apply=True)
+    h = bn._forward_stats_only(x)
+    assert isinstance(h, DeferredBNOutput) and not isinstance(h, torch.Tensor)
     bn2 = BatchNorm2d(64).cuda()
     y_ref = bn2(x)
-    torch.testing.assert_close(materialize(y_def).float(), y_ref.float(), rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(h.materialize().float(), y_ref.float(), rtol=2e-2, atol=2e-2)

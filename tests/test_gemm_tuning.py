@@ -37,10 +37,10 @@ def test_read_only_env_and_per_device_copy(tmp_path, monkeypatch):
     assert open(copy).read() == table.read_text()
 
 
-def test_disabled_and_explicit_env_win(tmp_path, monkeypatch):
+def test_disabled_and_explicit_env_win(tmp_path, monkeypatch, switch):
     table = tmp_path / "t.csv"
     _write(table, ["Validator,PT_VERSION,2.10.0"])
-    monkeypatch.setenv("PDT_GEMM_TUNING", "0")
+    switch("PDT_GEMM_TUNING", "0")
     assert gemm_tuning.use_repo_gemm_tuning(table=str(table)) is None
     monkeypatch.delenv("PDT_GEMM_TUNING")
     monkeypatch.setenv("PYTORCH_TUNABLEOP_ENABLED", "0")

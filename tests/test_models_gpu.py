@@ -31,12 +31,15 @@ def _compare(name, make_input, loss_fn, slack=1.3, **kw):
         base = base.to(memory_format=torch.channels_last)
     x, y = make_input()
     xb = x.bfloat16() if x.is_floating_point() else x
+    from pytorch_distributed_training_example_amd.config import SW
     os.environ["PDT_DISABLE_NATIVE"] = "1"
+    SW.reload()
     try:
         l32, g32 = _grads(copy.deepcopy(base), x, y, loss_fn)
         l_ref, g_ref = _grads(to_bf16_mixed(copy.deepcopy(base)), xb, y, loss_fn)
     finally:
         os.environ.pop("PDT_DISABLE_NATIVE")
+        SW.reload()
     l_nat, g_nat = _grads(to_bf16_mixed(copy.deepcopy(base)), xb, y, loss_fn)
     assert abs(l_nat - l32) <= slack * abs(l_ref - l32) + 0.02 * max(1.0, abs(l32)), (l_nat, l_ref, l32)
     e = lambda a, b: ((a - b).norm() / (b.norm() + 1e-9)).item()

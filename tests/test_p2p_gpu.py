@@ -17,30 +17,102 @@ def _allreduce_worker(rank, world, sizes):
     from pytorch_distributed_training_example_amd.parallel.p2p import P2PAllReduce
     p2p = P2PAllReduce(capacity_bytes=4 << 20)
     res = []
-    for rep in range(3):  # cycles the staging parity and the epoch counter
-        for dtype in (torch.float32, torch.bfloat16):
-            for n in sizes:
-                x = _inputs(rank, n, dtype).cuda() * (rep + 1)
-                y = torch.empty_like(x)
-                p2p.all_reduce(x, average=False, out=y)
-                x2 = x.clone()
-                p2p.all_reduce(x2, average=True)  # in place
-                torch.cuda.synchronize()
-                res.append((rep, str(dtype), n, y.cpu(), x2.cpu()))
+    for rep in range(3):  # cycles the staging parity and the device epoch counter
+        for algo in (0, 1):  # one-shot, two-shot (interleaved: shared epoch sequence)
+            for dtype in (torch.float32, torch.bfloat16):
+                for n in sizes:
+                    x = _inputs(rank, n, dtype).cuda() * (rep + 1)
+                    y = torch.empty_like(x)
+                    p2p.all_reduce(x, average=False, out=y, algo=algo)
+                    x2 = x.clone()
+                    p2p.all_reduce(x2, average=True, algo=algo)  # in place
+                    torch.cuda.synchronize()
+                    res.append((rep, algo, str(dtype), n, y.cpu(), x2.cpu()))
     p2p.check()
-    return res
+    return res, int(p2p.state[0].item())
 
 
-def test_p2p_allreduce_exact_two_ranks():
-    sizes = [8, 4096, 100000, 1 << 20]
-    out = run_ranks(_allreduce_worker, 2, (sizes,), use_gpu=True)
-    for (rep, dt, n, y0, a0), (_, _, _, y1, a1) in zip(out[0], out[1]):
+@pytest.mark.parametrize("world", [2, 3])
+def test_p2p_allreduce_exact(world):
+    """One-shot and two-shot (uneven chunks at world 3) sums and means equal the fp32 sum of the
+    ranks' inputs (rounded once), bit-identical on every rank; the device epoch counts every call."""
+    sizes = [8, 4096, 100000 - 8, 1 << 20]
+    out = run_ranks(_allreduce_worker, world, (sizes,), use_gpu=True)
+    calls = 3 * 2 * 2 * len(sizes) * 2
+    for r in range(world):
+        assert out[r][1] == calls, (r, out[r][1])
+    for rows in zip(*[o[0] for o in out]):
+        rep, algo, dt, n, y0, a0 = rows[0]
         dtype = torch.float32 if "float32" in dt else torch.bfloat16
-        xs = [_inputs(r, n, dtype) * (rep + 1) for r in range(2)]
-        ref = (xs[0].float() + xs[1].float())
-        assert torch.equal(y0, y1) and torch.equal(a0, a1), "replicas must be bit-identical"
-        assert torch.equal(y0, ref.to(dtype)), (dt, n)
-        assert torch.equal(a0, (ref * 0.5).to(dtype)), (dt, n)
+        xs = [_inputs(r, n, dtype) * (rep + 1) for r in range(world)]
+        ref = sum(x.float() for x in xs)
+        for row in rows[1:]:
+            assert torch.equal(row[4], y0) and torch.equal(row[5], a0), "replicas must be bit-identical"
+        assert torch.equal(y0, ref.to(dtype)), (algo, dt, n)
+        assert torch.equal(a0, (ref * (1.0 / world)).to(dtype)), (algo, dt, n)
+
+
+def _graph_worker(rank, world, n, replays):
+    """The P2P all-reduce captured in a hipGraph and replayed: the epoch advances on the device, so
+    each replay synchronises with the peers' matching replay (a host-side epoch baked into the
+    captured node would let replays read peers' half-written staging)."""
+    from pytorch_distributed_training_example_amd.parallel.p2p import P2PAllReduce
+    p2p = P2PAllReduce(capacity_bytes=4 << 20)
+    static_in = torch.zeros(n, device="cuda")
+    static_out = torch.zeros(n, device="cuda")
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):  # warm-up (eager) call
+        p2p.all_reduce(static_in, average=False, out=static_out)
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        p2p.all_reduce(static_in, average=False, out=static_out, algo=1 if n >= 4096 else 0)
+    outs = []
+    for i in range(replays):
+        static_in.copy_(_inputs(rank, n, torch.float32).cuda() * (i + 2))
+        g.replay()
+        outs.append(static_out.cpu())
+    torch.cuda.synchronize()
+    p2p.check()
+    return outs, int(p2p.state[0].item())
+
+
+@pytest.mark.parametrize("n", [1024, 262144])
+def test_p2p_allreduce_graph_replay_exact(n):
+    replays = 6
+    out = run_ranks(_graph_worker, 2, (n, replays), use_gpu=True)
+    for r in range(2):
+        assert out[r][1] == 1 + replays  # warm-up + every replay advanced the device epoch
+    for i in range(replays):
+        ref = sum(_inputs(r, n, torch.float32) * (i + 2) for r in range(2))
+        assert torch.equal(out[0][0][i], ref) and torch.equal(out[1][0][i], ref), i
+
+
+def _timeout_worker(rank, world):
+    """Rank 1 never joins the collective: rank 0's kernel gives up after its spin limit, sets the
+    error word and writes NaN instead of a partial sum; check() raises."""
+    from pytorch_distributed_training_example_amd.parallel.p2p import P2PAllReduce
+    p2p = P2PAllReduce(capacity_bytes=1 << 20)
+    x = torch.ones(4096, device="cuda")
+    raised = None
+    if rank == 0:
+        p2p.all_reduce(x, average=False)
+        torch.cuda.synchronize()
+        try:
+            p2p.check()
+        except RuntimeError as e:
+            raised = str(e)
+    torch.distributed.barrier()
+    return raised, bool(torch.isnan(x).all().item()) if rank == 0 else None
+
+
+def test_p2p_lost_peer_raises_and_poisons():
+    out = run_ranks(_timeout_worker, 2, use_gpu=True)
+    raised, all_nan = out[0]
+    assert raised is not None and "did not arrive" in raised
+    assert all_nan, "a lost peer must never produce a partial sum"
 
 
 def _ddp_worker(rank, world):
@@ -50,7 +122,7 @@ def _ddp_worker(rank, world):
     torch.manual_seed(0)
     model = torch.nn.Sequential(torch.nn.Linear(32, 64), torch.nn.ReLU(), torch.nn.Linear(64, 8)).cuda()
     ddp = DistributedDataParallel(model, bucket_cap_mb=0.004, first_bucket_mb=0.002)
-    state = P2PHookState(P2PAllReduce(capacity_bytes=1 << 20), max_bytes=1 << 20)
+    state = P2PHookState(P2PAllReduce(capacity_bytes=1 << 20))
     ddp.register_comm_hook(state, p2p_allreduce_hook)
     g = torch.Generator().manual_seed(rank)
     x, t = torch.randn(16, 32, generator=g).cuda(), torch.randn(16, 8, generator=g).cuda()
@@ -74,3 +146,32 @@ def test_ddp_p2p_hook_matches_full_batch_grads():
     loss.backward()
     for a, p in zip(g0, model.parameters()):
         torch.testing.assert_close(a, p.grad, rtol=1e-5, atol=1e-6)
+
+
+def _backend_worker(rank, world):
+    """dist.init_process_group("pdt_p2p") as the default group: GPU all-reduces take the P2P kernels
+    (counted), the rest goes to the inner group (gloo here: two ranks share the one GPU)."""
+    import os
+    import torch.distributed as dist
+    from pytorch_distributed_training_example_amd.parallel import launcher
+    launcher.destroy()
+    os.environ["MASTER_PORT"] = str(int(os.environ["MASTER_PORT"]) + 1)
+    os.environ["PDT_P2P_INNER"] = "gloo"
+    launcher.init_distributed(backend="pdt_p2p", use_gpu=True, timeout_s=60)
+    pg = dist.distributed_c10d._get_default_group()
+    t = torch.full((4096,), float(rank + 1), device="cuda", dtype=torch.bfloat16)
+    dist.all_reduce(t)
+    a = torch.full((1024,), float(rank + 1), device="cuda")
+    dist.all_reduce(a, op=dist.ReduceOp.AVG)
+    c = torch.full((16,), float(rank))
+    dist.all_reduce(c)  # CPU: inner group
+    torch.cuda.synchronize()
+    pg.check()
+    return t.float().cpu(), a.cpu(), c, pg.p2p_calls
+
+
+def test_pdt_p2p_backend_gpu():
+    out = run_ranks(_backend_worker, 2, use_gpu=True)
+    for t, a, c, calls in out:
+        assert torch.equal(t, torch.full((4096,), 3.0)) and torch.equal(a, torch.full((1024,), 1.5))
+        assert torch.equal(c, torch.full((16,), 1.0)) and calls == 2

@@ -25,10 +25,10 @@ def _has(names, needle):
     return any(needle in n for n in names)
 
 
-def test_resnet_step_runs_our_kernels(monkeypatch):
+def test_resnet_step_runs_our_kernels(monkeypatch, switch):
     # stride-1 1x1 convs on the GEMM path: the per-shape timing (ops/conv.py) may otherwise pick
     # MIOpen for a data gradient at these toy shapes, whose residual gradient then needs an add
-    monkeypatch.setenv("PDT_CONV1X1", "gemm")
+    switch("PDT_CONV1X1", "gemm")
     from pytorch_distributed_training_example_amd.models import get_model
     from pytorch_distributed_training_example_amd.models.precision import to_bf16_mixed
     from pytorch_distributed_training_example_amd.ops.cross_entropy import cross_entropy

@@ -20,12 +20,12 @@ def _probe(rank, world, out_dir):
         json.dump(env, f)
 
 
-def test_spawned_ranks_get_own_gemm_table_and_private_miopen_db(tmp_path, monkeypatch):
+def test_spawned_ranks_get_own_gemm_table_and_private_miopen_db(tmp_path, monkeypatch, switch):
     for k in list(os.environ):
         if k.startswith(("PYTORCH_TUNABLEOP_", "MIOPEN_", "PDT_")):
             monkeypatch.delenv(k, raising=False)
     cache = tmp_path / "miopen"
-    monkeypatch.setenv("PDT_MIOPEN_CACHE", str(cache))
+    switch("PDT_MIOPEN_CACHE", str(cache))
     launcher.spawn(_probe, 2, args=(str(tmp_path),), backend="gloo", use_gpu=False)
     envs = [json.load(open(tmp_path / f"r{r}.json")) for r in range(2)]
     for r, env in enumerate(envs):
