@@ -92,11 +92,33 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
     return out
 
 
+def build_host_selftest(out: str | None = None) -> str:
+    """The host-logic self-test (csrc/host/host_selftest.cpp) under AddressSanitizer +
+    UndefinedBehaviorSanitizer. The sanitizers apply to the HOST half only (-Xarch_host): GPU
+    sanitizer runs are not available on this pool, and the binary makes no HIP runtime call, so it
+    runs on a CPU-only machine. Returns the executable path."""
+    src = os.path.join(CSRC, "host", "host_selftest.cpp")
+    out = out or os.path.join(BUILD, "host_selftest_asan")
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    deps = _headers() + glob.glob(os.path.join(CSRC, "kernels", "*.hip"))
+    if _stale(out, src, deps):
+        _run([HIPCC, "-x", "hip", "-std=c++17", "-O1", "-g", f"--offload-arch={ARCH}",
+              "-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined",
+              "-Xarch_host", "-fno-sanitize-recover=undefined", "-Xarch_host", "-fno-omit-frame-pointer",
+              src, "-o", out])
+    return out
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", "--jobs", type=int, default=None)
+    ap.add_argument("--host-selftest", action="store_true",
+                    help="build and run the ASan/UBSan host-logic self-test instead")
     a = ap.parse_args(argv)
+    if a.host_selftest:
+        exe = build_host_selftest()
+        return subprocess.run([exe]).returncode
     print(build(force=a.force, jobs=a.jobs, verbose=True))
     return 0
 

@@ -74,6 +74,10 @@ int pdt_bn_relu_maxpool_fwd_train(const uint16_t* x, const float* gamma, const f
 int pdt_conv3x3s1_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int N, int H, int W, int Ci, int Co,
                       hipStream_t s);
 int pdt_conv3x3_flip_weights(const uint16_t* w, uint16_t* wf, int Co, int Ci, hipStream_t s);
+int64_t pdt_conv3x3_wgrad_ws_floats(int N, int H, int W, int Ci, int Co, int* nsplit_out);
+int pdt_conv3x3s1_wgrad(const uint16_t* x, const uint16_t* dy, uint16_t* dw, float* ws, int N, int H, int W, int Ci,
+                        int Co, hipStream_t s);
+void pdt_conv3x3_wgrad_tune(int target_wgs, int co_tile);
 int pdt_conv3x3s1_fwd_bnbwd(const uint16_t* x, const uint16_t* w, uint16_t* y, const uint16_t* bn_x,
                             const uint8_t* bn_mask, const float* bn_mean, float* bn_part, int N, int H, int W, int Ci,
                             int Co, hipStream_t s);
@@ -108,6 +112,11 @@ int pdt_bn_fwd_train_tiles(const float* part, int T, int BMt, const uint16_t* x,
 int pdt_fp8_cast_transpose(const uint16_t* x, int64_t M, int64_t K, const float* scale, uint8_t* out,
                            uint8_t* out_t, float* amax, hipStream_t s);
 int pdt_fp8_update_scales(float* state, int n, int L, float margin_scale, hipStream_t s);
+int pdt_embedding_fwd(const int64_t* idx, const uint16_t* wte, const uint16_t* wpe, uint16_t* out, int64_t n, int T,
+                      int D, hipStream_t s);
+int64_t pdt_embedding_bwd_ws_ints(int64_t n, int V);
+int pdt_embedding_bwd(const int64_t* idx, const uint16_t* dout, uint16_t* dwte, uint16_t* dwpe, int* ws, int64_t n,
+                      int B, int T, int V, int D, hipStream_t s);
 int64_t pdt_p2p_flags_bytes();
 int64_t pdt_p2p_data_bytes(int64_t cap);
 int pdt_p2p_allreduce(const void* in, void* out, int64_t n, int dtype, char* const* data_ptrs,
@@ -733,6 +742,28 @@ std::vector<Tensor> conv3x3s1_fwd_bnbwd(Tensor x, Tensor w, Tensor bn_x, c10::op
 }
 
 // Data-gradient weights: wf [Ci, Co, 3, 3] (channels_last storage [Ci][3][3][Co]) with
+// Weight gradient of the stride-1 pad-1 3x3 conv (csrc/kernels/conv3x3_wgrad.hip): dw [Co, Ci, 3, 3]
+// channels_last bf16 from channels_last bf16 x [N, Ci, H, W] and dy [N, Co, H, W]. Returns an
+// undefined tensor for a shape the kernel does not take (caller falls back).
+Tensor conv3x3s1_wgrad(Tensor x, Tensor dy) {
+  check_nhwc_bf16(x, "x");
+  check_nhwc_bf16(dy, "dy");
+  const int64_t N = x.size(0), Ci = x.size(1), H = x.size(2), W = x.size(3), Co = dy.size(1);
+  TORCH_CHECK(dy.size(0) == N && dy.size(2) == H && dy.size(3) == W, "conv3x3s1_wgrad: dy [N, Co, H, W]");
+  int ns = 0;
+  const int64_t wsf = pdt_conv3x3_wgrad_ws_floats((int)N, (int)H, (int)W, (int)Ci, (int)Co, &ns);
+  if (wsf == 0 || N * H * W * std::max(Ci, Co) >= ((int64_t)1 << 31)) return Tensor();
+  auto ws = at::empty({wsf}, x.options().dtype(at::kFloat));
+  auto dw = at::empty({Co, Ci, 3, 3}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const int rc = pdt_conv3x3s1_wgrad(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                                     reinterpret_cast<const uint16_t*>(dy.data_ptr()),
+                                     reinterpret_cast<uint16_t*>(dw.data_ptr()), ws.data_ptr<float>(), (int)N, (int)H,
+                                     (int)W, (int)Ci, (int)Co, stream());
+  if (rc == -4) return Tensor();
+  TORCH_CHECK(rc == 0, "pdt_conv3x3s1_wgrad failed: ", rc);
+  return dw;
+}
+
 // wf[ci, co, kh, kw] = w[co, ci, 2 - kh, 2 - kw], so dx = conv3x3s1_fwd(dy, wf).
 Tensor conv3x3_flip(Tensor w) {
   check_cuda(w, "w");
@@ -1112,6 +1143,45 @@ class P2PComm {
   std::vector<uint32_t*> flag_ptrs_;
 };
 
+// ---- GPT-2 token + position embedding (csrc/kernels/embedding.hip) ----
+// out [B, T, D] = wte[idx] + wpe[arange(T)] (bf16). idx int64 [B, T]; values must be < V (checked on
+// the host only in debug paths: an out-of-range id is a caller bug, as for nn.Embedding).
+Tensor embedding_fwd(Tensor idx, Tensor wte, Tensor wpe) {
+  check_cuda(idx, "idx");
+  check_cuda(wte, "wte");
+  check_cuda(wpe, "wpe");
+  TORCH_CHECK(idx.scalar_type() == at::kLong && idx.dim() == 2 && idx.is_contiguous(), "embedding: idx int64 [B, T]");
+  TORCH_CHECK(wte.scalar_type() == at::kBFloat16 && wpe.scalar_type() == at::kBFloat16 && wte.is_contiguous() &&
+                  wpe.is_contiguous() && wte.dim() == 2 && wpe.dim() == 2 && wte.size(1) == wpe.size(1),
+              "embedding: wte [V, D], wpe [P, D] contiguous bf16");
+  const int64_t B = idx.size(0), T = idx.size(1), D = wte.size(1);
+  TORCH_CHECK(T <= wpe.size(0) && D % 8 == 0, "embedding: T <= P, D % 8 == 0");
+  auto out = at::empty({B, T, D}, wte.options());
+  TORCH_CHECK(pdt_embedding_fwd(idx.data_ptr<int64_t>(), reinterpret_cast<const uint16_t*>(wte.data_ptr()),
+                                reinterpret_cast<const uint16_t*>(wpe.data_ptr()),
+                                reinterpret_cast<uint16_t*>(out.data_ptr()), B * T, (int)T, (int)D, stream()) == 0,
+              "pdt_embedding_fwd failed");
+  return out;
+}
+
+// (dwte [V, D], dwpe [P, D]) from dout [B, T, D]: deterministic (counting sort + ordered row sums).
+std::vector<Tensor> embedding_bwd(Tensor idx, Tensor dout, int64_t V, int64_t P) {
+  check_cuda(idx, "idx");
+  check_cuda(dout, "dout");
+  dout = dout.contiguous();
+  TORCH_CHECK(dout.scalar_type() == at::kBFloat16 && dout.dim() == 3 && dout.size(0) == idx.size(0) &&
+                  dout.size(1) == idx.size(1), "embedding_bwd: dout [B, T, D] bf16");
+  const int64_t B = idx.size(0), T = idx.size(1), D = dout.size(2), n = B * T;
+  auto ws = at::zeros({pdt_embedding_bwd_ws_ints(n, (int)V)}, idx.options().dtype(at::kInt));
+  auto dwte = at::empty({V, D}, dout.options());
+  auto dwpe = T == P ? at::empty({P, D}, dout.options()) : at::zeros({P, D}, dout.options());
+  TORCH_CHECK(pdt_embedding_bwd(idx.data_ptr<int64_t>(), reinterpret_cast<const uint16_t*>(dout.data_ptr()),
+                                reinterpret_cast<uint16_t*>(dwte.data_ptr()), reinterpret_cast<uint16_t*>(dwpe.data_ptr()),
+                                ws.data_ptr<int>(), n, (int)B, (int)T, (int)V, (int)D, stream()) == 0,
+              "pdt_embedding_bwd failed");
+  return {dwte, dwpe};
+}
+
 // ---- LeNet (reference model) ops: csrc/kernels/lenet.hip ----
 constexpr int kStemIpb = 4;  // images per workgroup in the conv1 weight-gradient reduction
 
@@ -1228,6 +1298,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv3x3_flip", &conv3x3_flip);
   m.def("stem_conv_fwd", &stem_conv_fwd);
   m.def("stem_conv_wgrad", &stem_conv_wgrad);
+  m.def("conv3x3s1_wgrad", &conv3x3s1_wgrad);
+  m.def("embedding_fwd", &embedding_fwd);
+  m.def("embedding_bwd", &embedding_bwd);
+  m.def("conv3x3_wgrad_tune", [](int target_wgs, int co_tile) { pdt_conv3x3_wgrad_tune(target_wgs, co_tile); });
   m.def("bn_bwd_train", &bn_bwd_train);
   m.def("ce_fwd", &ce_fwd);
   m.def("ce_bwd", &ce_bwd);

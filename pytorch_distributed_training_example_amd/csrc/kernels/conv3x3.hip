@@ -762,213 +762,8 @@ __global__ __launch_bounds__(Cf::kThreads, 1) void conv3x3wst_kernel(const uint1
   }
 }
 
-// ---------------------------------------------------------------- weight gradient
-//   dW[co, tap, ci] = sum_m dY[m, co] * X[pixel(m) + shift(tap), ci]
-// A GEMM over K = pixels whose operands are both pixel-major in NHWC: fragments are gathered by
-// the hardware transposed LDS read (ds_read_b64_tr_b16: each lane names one pixel row, the 16
-// lanes of a group receive one channel column of 4 pixels), so no transpose pass exists. A
-// workgroup owns a 64 (co) x 64 (ci) block of all nine taps (147 KB of fp32 accumulators in the
-// registers of 8 waves: wave w = 2 co-subblocks x 1 ci-subblock x 9 taps) and a contiguous range
-// of 128-pixel tiles. Per tile the dY tile [128 px][64 co] and the padded X halo [<=512 rows][64 ci]
-// are staged in LDS with a 144-B row pitch (16 B of padding: 8 consecutive rows land on 8
-// different 32-B bank slots, so the transposed reads are conflict-free with a plain row*144
-// address — an XOR swizzle cost ~8 VALU per read address, which made the first, LDS-DMA version
-// VALU-bound at 0.27-0.44 PF). Staging goes through registers: the next tile's global loads are
-// in flight while the current tile is computed. Per-split fp32 partials go to a workspace that
-// conv3x3_wgrad_reduce sums in a fixed order (deterministic).
-// Measured (tools/gpu_wgrad.sh, batch 512): 384/268/223/217 us at L1-L4, slower than MIOpen's
-// 284/~200 us; the MFMA-only probe (no staging) takes 230/141/123/117 us. A wave map with all 4
-// co blocks per wave (8 + 18 transposed reads per 36 MFMAs instead of 4 + 18 per 18) measured
-// the same in both, so LDS read bandwidth is not the limit; the register staging + 2 barriers
-// per 128-pixel tile are.
-struct GCfg {
-  static constexpr int BM = 128, kThreads = 512;
-  static constexpr int kPitch = 144;
-  static constexpr int kHaloRows = 512;
-  static constexpr int kDyBytes = BM * kPitch, kHaloBytes = kHaloRows * kPitch;
-  static constexpr int kTable = BM * 4;  // halo row of each tile pixel
-  static constexpr int kLds = kDyBytes + kHaloBytes + kTable;
-  static constexpr int kDyPieces = BM * 8 / kThreads, kHPieces = kHaloRows * 8 / kThreads;  // 16-B pieces per thread
-};
-
-typedef short s4v __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ s4v tr4p(const char* base_plus_col, int row) {
-  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (__attribute__((address_space(3))) s4v*)(base_plus_col + row * GCfg::kPitch));
-}
-__device__ __forceinline__ bf16x8 cat2(s4v a, s4v b) {
-  typedef short s8 __attribute__((ext_vector_type(8)));
-  s8 r = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
-  return __builtin_bit_cast(bf16x8, r);
-}
-
-__global__ __launch_bounds__(GCfg::kThreads, 2) void conv3x3_wgrad_kernel(
-    const uint16_t* __restrict__ X, const uint16_t* __restrict__ dY, float* __restrict__ ws, int N, int H, int W,
-    int Ci, int Co, int tiles_per_split) {
-  using Cf = GCfg;
-  constexpr int BM = Cf::BM;
-  extern __shared__ __attribute__((aligned(16))) char lds[];
-  char* const dyb = lds;
-  char* const hb = lds + Cf::kDyBytes;
-  int* const table = reinterpret_cast<int*>(lds + Cf::kDyBytes + Cf::kHaloBytes);
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int HW = H * W, M = N * HW, W2 = W + 2, H2 = H + 2;
-  const int nblk_ci = Ci / 64;
-  const int split = blockIdx.x;
-  const int cb = blockIdx.y / nblk_ci, ib = blockIdx.y % nblk_ci;
-  const int co0 = cb * 64, ci0 = ib * 64;
-  const int ntile = (M + BM - 1) / BM;
-  const int t_begin = split * tiles_per_split;
-  const int t_end = min(ntile, t_begin + tiles_per_split);
-
-  auto geo = [&](int tl, int& m0, int& mlast, int& pr0, int& Q) {
-    m0 = tl * BM;
-    mlast = min(m0 + BM, M) - 1;
-    pr0 = (m0 / HW) * H2 + (m0 % HW) / W;
-    Q = ((mlast / HW) * H2 + (mlast % HW) / W + 2 - pr0 + 1) * W2;
-  };
-  uint4 pf[Cf::kDyPieces + Cf::kHPieces];
-  int hrow_pf = 0;
-  const uint4 zero4 = make_uint4(0u, 0u, 0u, 0u);
-  auto load_regs = [&](int tl) {
-    int m0, mlast, pr0, Q;
-    geo(tl, m0, mlast, pr0, Q);
-    // conditional loads (hipcc branches around each): measured 2.6x FASTER here than unconditional
-    // loads from clamped addresses, which also fetch the ~half of the 512 halo rows past Q
-#pragma unroll
-    for (int i = 0; i < Cf::kDyPieces; ++i) {
-      const int piece = tid + i * Cf::kThreads, r = piece >> 3, c = piece & 7;
-      const int m = m0 + r;
-      pf[i] = m <= mlast ? *reinterpret_cast<const uint4*>(dY + ((int64_t)m * Co + co0 + c * 8)) : zero4;
-    }
-    {
-      // halo piece i of this thread: row q = q0 + 64 i (column c fixed). Integer division is a
-      // ~20-instruction VALU sequence on gfx950, so (slot, col) and (image, padded row) are
-      // advanced incrementally from piece 0 instead of divided per piece.
-      const int c = tid & 7, q0 = tid >> 3;
-      const int da = 64 / W2, db = 64 % W2;
-      int slot = q0 / W2, col = q0 % W2;
-      int PR = pr0 + slot;
-      int n = PR / H2, ihp = PR % H2;  // padded row index 0..H+1 (input row ihp - 1)
-#pragma unroll
-      for (int i = 0; i < Cf::kHPieces; ++i) {
-        const int q = q0 + 64 * i;
-        const int ih = ihp - 1, iw = col - 1;
-        uint4 v = zero4;
-        if (q < Q && ih >= 0 && ih < H && iw >= 0 && iw < W && n < N)
-          v = *reinterpret_cast<const uint4*>(X + ((int64_t)((n * H + ih) * W + iw) * Ci + ci0 + c * 8));
-        pf[Cf::kDyPieces + i] = v;
-        const int wrapc = col + db >= W2;
-        col += db - wrapc * W2;
-        ihp += da + wrapc;
-        const int wrapr = ihp >= H2;  // one wrap at most: 64 / (W+2) + 1 < H + 2 (host-checked)
-        ihp -= wrapr * H2;
-        n += wrapr;
-      }
-    }
-    if (tid < BM) {  // halo row (tap 0,0) of tile pixel tid
-      const int m = min(m0 + tid, mlast), rem = m % HW;
-      hrow_pf = ((m / HW) * H2 + rem / W - pr0) * W2 + rem % W;
-    }
-  };
-  auto write_lds = [&]() {
-#pragma unroll
-    for (int i = 0; i < Cf::kDyPieces; ++i) {
-      const int piece = tid + i * Cf::kThreads;
-      *reinterpret_cast<uint4*>(dyb + (piece >> 3) * Cf::kPitch + (piece & 7) * 16) = pf[i];
-    }
-#pragma unroll
-    for (int i = 0; i < Cf::kHPieces; ++i) {
-      const int piece = tid + i * Cf::kThreads;
-      *reinterpret_cast<uint4*>(hb + (piece >> 3) * Cf::kPitch + (piece & 7) * 16) = pf[Cf::kDyPieces + i];
-    }
-    if (tid < BM) table[tid] = hrow_pf;
-  };
-
-  const int g = lane >> 4, li = lane & 15, rsub = li >> 2, csub = li & 3;
-  const int cpair = wid & 1, isub = wid >> 1;  // co-subblocks 2*cpair, 2*cpair+1; ci-subblock isub
-  const char* dyc0 = dyb + (2 * cpair) * 32 + csub * 8;
-  const char* dyc1 = dyc0 + 32;
-  const char* hc = hb + isub * 32 + csub * 8;
-  f4 acc[9][2];
-#pragma unroll
-  for (int t = 0; t < 9; ++t) acc[t][0] = acc[t][1] = f4{0.f, 0.f, 0.f, 0.f};
-
-  if (t_begin < t_end) {
-    load_regs(t_begin);
-    write_lds();
-  }
-  __syncthreads();
-#ifndef PDT_WG_PIPE
-#define PDT_WG_PIPE 0
-#endif
-#ifndef PDT_WG_PROBE
-#define PDT_WG_PROBE 0  // diagnostics: 1 = staging only, 2 = MFMA only
-#endif
-  for (int tl = t_begin; tl < t_end; ++tl) {
-    if (PDT_WG_PROBE != 2 && tl + 1 < t_end) load_regs(tl + 1);  // in flight during this tile's MFMAs
-#pragma unroll
-    for (int kk = 0; kk < (PDT_WG_PROBE == 1 ? 0 : BM / 32); ++kk) {
-      // the 8 pixels of this lane group: rows 4g+rsub and 16+4g+rsub of the 32-pixel k-step
-      // (the same permuted k order on both operands; attention.hip uses it too)
-      const int r0 = kk * 32 + 4 * g + rsub, r1 = r0 + 16;
-      const int hq0 = table[r0], hq1 = table[r1];
-      const bf16x8 a0 = cat2(tr4p(dyc0, r0), tr4p(dyc0, r1));
-      const bf16x8 a1 = cat2(tr4p(dyc1, r0), tr4p(dyc1, r1));
-#if PDT_WG_PIPE
-      bf16x8 bx[2];
-      bx[0] = cat2(tr4p(hc, hq0), tr4p(hc, hq1));
-#pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        if (t < 8) {  // next tap's fragment under this tap's MFMAs
-          const int toff = ((t + 1) / 3) * W2 + ((t + 1) % 3);
-          bx[(t + 1) & 1] = cat2(tr4p(hc, hq0 + toff), tr4p(hc, hq1 + toff));
-        }
-        acc[t][0] = mfma(a0, bx[t & 1], acc[t][0]);  // D[co][ci]
-        acc[t][1] = mfma(a1, bx[t & 1], acc[t][1]);
-      }
-#else
-#pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const int toff = (t / 3) * W2 + (t % 3);
-        const bf16x8 bx = cat2(tr4p(hc, hq0 + toff), tr4p(hc, hq1 + toff));
-        acc[t][0] = mfma(a0, bx, acc[t][0]);  // D[co][ci]
-        acc[t][1] = mfma(a1, bx, acc[t][1]);
-      }
-#endif
-    }
-    __syncthreads();  // every wave done reading this tile
-    if (PDT_WG_PROBE != 2 && tl + 1 < t_end) {
-      write_lds();
-      __syncthreads();
-    }
-  }
-  // partials: ws[split][tap][co][ci]; lane holds D[co = 4*(l>>4) + j][ci = l&15] of each block
-  float* wsp = ws + (int64_t)split * 9 * Co * Ci;
-#pragma unroll
-  for (int t = 0; t < 9; ++t)
-#pragma unroll
-    for (int c = 0; c < 2; ++c)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int co = co0 + (2 * cpair + c) * 16 + 4 * g + j;
-        const int ci = ci0 + isub * 16 + li;
-        wsp[((int64_t)t * Co + co) * Ci + ci] = acc[t][c][j];
-      }
-}
-
-// dw[co][tap][ci] (bf16, the channels_last storage of [Co, Ci, 3, 3]) = sum over splits, fixed order
-__global__ void conv3x3_wgrad_reduce_kernel(const float* __restrict__ ws, uint16_t* __restrict__ dw, int nsplit,
-                                            int Co, int Ci) {
-  const int64_t per = (int64_t)9 * Co * Ci;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < per; i += (int64_t)gridDim.x * blockDim.x) {
-    float s = 0.f;
-    for (int k = 0; k < nsplit; ++k) s += ws[(int64_t)k * per + i];
-    const int t = (int)(i / ((int64_t)Co * Ci)), rem = (int)(i % ((int64_t)Co * Ci));
-    const int co = rem / Ci, ci = rem % Ci;
-    dw[((int64_t)co * 9 + t) * Ci + ci] = __builtin_bit_cast(uint16_t, (__bf16)s);
-  }
-}
+// (The weight gradient lives in conv3x3_wgrad.hip: a first version here, register-staged with
+// 16x16x32 MFMAs and a 128-pixel tile of arbitrary rows, ran slower than MIOpen and was replaced.)
 
 // Upper bound of the padded-halo rows of a 256-pixel tile (kernel's Q).
 inline int64_t halo_rows_bound(int H, int W, int BM) {
@@ -1123,47 +918,6 @@ int pdt_conv3x3s1_fwd_bnbwd(const uint16_t* x, const uint16_t* w, uint16_t* y, c
   const BnSrc bs{bn_x, bn_mask, bn_mean, bn_part};
   return Co % 128 == 0 ? launch_h<HWide, false, true>(x, w, y, N, H, W, Ci, Co, s, nullptr, bs)
                        : launch_h<HNarrow, false, true>(x, w, y, N, H, W, Ci, Co, s, nullptr, bs);
-}
-
-// Weight gradient of the stride-1 pad-1 3x3 conv: dw[Co,3,3,Ci] (bf16) from x[N,H,W,Ci] and
-// dy[N,H,W,Co]. ws: fp32 workspace of pdt_conv3x3_wgrad_ws_floats() floats. Ci, Co % 64 == 0.
-int64_t pdt_conv3x3_wgrad_ws_floats(int N, int H, int W, int Ci, int Co, int* nsplit_out) {
-  const int64_t M = (int64_t)N * H * W;
-  const int64_t ntile = (M + GCfg::BM - 1) / GCfg::BM;
-  const int64_t blocks = (int64_t)(Co / 64) * (Ci / 64);
-  int64_t ns = (512 + blocks - 1) / blocks;  // ~2 workgroups per CU in total
-  if (ns > ntile) ns = ntile;
-  if (ns < 1) ns = 1;
-  const int64_t tps = (ntile + ns - 1) / ns;
-  ns = (ntile + tps - 1) / tps;
-  if (nsplit_out) *nsplit_out = (int)ns;
-  return ns * 9 * (int64_t)Co * Ci;
-}
-
-int pdt_conv3x3s1_wgrad(const uint16_t* x, const uint16_t* dy, uint16_t* dw, float* ws, int N, int H, int W, int Ci,
-                        int Co, hipStream_t s) {
-  if (Ci % 64 != 0 || Co % 64 != 0 || N < 1) return -1;
-  const int64_t M = (int64_t)N * H * W;
-  if (M * (Ci > Co ? Ci : Co) >= (int64_t)1 << 31) return -2;
-  if (halo_rows_bound(H, W, GCfg::BM) > GCfg::kHaloRows) return -4;
-  if (64 / (W + 2) + 1 >= H + 2) return -4;  // the staging's incremental row walk wraps at most once
-  static bool attr = false;
-  if (!attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_wgrad_kernel),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, GCfg::kLds) != hipSuccess)
-      return -3;
-    attr = true;
-  }
-  int ns = 1;
-  pdt_conv3x3_wgrad_ws_floats(N, H, W, Ci, Co, &ns);
-  const int64_t ntile = (M + GCfg::BM - 1) / GCfg::BM;
-  const int tps = (int)((ntile + ns - 1) / ns);
-  hipLaunchKernelGGL(conv3x3_wgrad_kernel, dim3(ns, (Co / 64) * (Ci / 64)), dim3(GCfg::kThreads), GCfg::kLds, s, x,
-                     dy, ws, N, H, W, Ci, Co, tps);
-  const int64_t per = (int64_t)9 * Co * Ci;
-  const int grid = (int)((per + 255) / 256 < 2048 ? (per + 255) / 256 : 2048);
-  hipLaunchKernelGGL(conv3x3_wgrad_reduce_kernel, dim3(grid), dim3(256), 0, s, ws, dw, ns, Co, Ci);
-  return 0;
 }
 
 // wf[Ci,3,3,Co] (the data-gradient weights) from w[Co,3,3,Ci].

@@ -14,6 +14,7 @@ import torch
 from torch import nn
 
 from ..ops.cross_entropy import cross_entropy
+from ..ops.embedding import token_position_embedding
 from ..ops.layernorm import LayerNorm
 from .transformer import Block, init_weights, run_blocks
 
@@ -43,9 +44,8 @@ class GPT(nn.Module):
         init_weights(self, n_layer=cfg.n_layer)
 
     def forward(self, idx: torch.Tensor, targets: torch.Tensor | None = None):
-        B, T = idx.shape
-        pos = torch.arange(T, device=idx.device)
-        x = self.transformer.wte(idx) + self.transformer.wpe(pos)
+        # one fused gather pass forward, deterministic scatter backward (ops/embedding.py)
+        x = token_position_embedding(idx, self.transformer.wte.weight, self.transformer.wpe.weight)
         x = run_blocks(self.transformer.h, x, self.transformer.ln_f)  # == ln_f(h[-1](...h[0](x)))
         logits = self.lm_head(x)
         if targets is None:

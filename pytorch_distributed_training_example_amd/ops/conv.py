@@ -129,10 +129,11 @@ def _time(fn, reps: int = 3) -> float:
     return e0.elapsed_time(e1)
 
 
-def _pick(key: Tuple, cands: Dict[str, callable]) -> str:
+def _pick(key: Tuple, cands: Dict[str, callable], fused: bool = False) -> str:
     """Backend for one (direction, dtype, M, Ci, Co): forced mode > per-shape override >
-    ``PDT_CONV1X1_PREFER`` (our GEMM also removes the consuming BN's reduce pass, which the
-    conv-only timing does not see) > measured table > time the candidates once."""
+    ``PDT_CONV1X1_PREFER`` > measured table > ``fused`` (our GEMM would also take the consuming
+    BatchNorm's statistics / backward reduction in its epilogue, removing a whole reduce pass that
+    a conv-only timing cannot see: take it untimed) > time the candidates once."""
     mode = SW.conv1x1
     if mode in cands:
         return mode
@@ -145,6 +146,9 @@ def _pick(key: Tuple, cands: Dict[str, callable]) -> str:
     c = _CHOICE.get(key)
     if c is not None:  # a decided back end that is switched off here: the GEMM library, untimed
         return c if c in cands else "gemm"
+    if fused and "ours" in cands:
+        _CHOICE[key] = "ours"
+        return "ours"
     if torch.cuda.is_current_stream_capturing():
         return "miopen"
     times = {name: _time(fn) for name, fn in cands.items()}
@@ -199,7 +203,7 @@ class _Conv1x1Fn(torch.autograd.Function):
                 y = torch.empty((N, Co, H, W), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
                 return y, native().conv1x1_gemm(x2, w2.contiguous(), _nhwc2d(y), False, stats)
             cands["ours"] = ours
-        algo = _pick(("fwd", _dtype_name(x), M, Ci, Co), cands)
+        algo = _pick(("fwd", _dtype_name(x), M, Ci, Co), cands, fused=stats_out is not None)
         if algo == "ours":  # with the consuming BatchNorm's statistics in the epilogue
             y, part = cands["ours"](stats_out is not None)
             if stats_out is not None:
@@ -263,7 +267,7 @@ class _Conv1x1Fn(torch.autograd.Function):
                     native().conv1x1_gemm(g2, wt, _nhwc2d(d), False, False)
                     return d
                 cands["ours"] = ours_d
-            algo = _pick(("bwd_data", _dtype_name(x), M, Ci, Co), cands)
+            algo = _pick(("bwd_data", _dtype_name(x), M, Ci, Co), cands, fused=gs is not None)
             if algo == "ours" and acc is not None and acc.is_contiguous(memory_format=torch.channels_last):
                 # dx = dres + dY W, in place
                 gpart = native().conv1x1_gemm(g2, wt, _nhwc2d(acc), True, False, **bn_kw)
@@ -434,9 +438,10 @@ class _LinkedConvFn(torch.autograd.Function):
 
 
 class _Conv3x3Fn(torch.autograd.Function):
-    """Stride-1 pad-1 3x3 convolution on our MFMA implicit-GEMM kernels (csrc/kernels/conv3x3.hip):
-    forward = conv3x3s1(x, w); data gradient = the SAME kernel on dY with the weights flipped and
-    transposed (conv3x3_flip); weight gradient = MIOpen."""
+    """Stride-1 pad-1 3x3 convolution on our MFMA kernels: forward = conv3x3s1(x, w)
+    (csrc/kernels/conv3x3.hip); data gradient = the SAME kernel on dY with the weights flipped and
+    transposed (conv3x3_flip); weight gradient = the halo-tiled split-K MFMA kernel
+    (csrc/kernels/conv3x3_wgrad.hip; ``PDT_CONV3X3_WGRAD=miopen`` or an unsupported shape: MIOpen)."""
 
     @staticmethod
     def forward(ctx, x, weight, stats_out=None, gsrc=None):
@@ -466,8 +471,11 @@ class _Conv3x3Fn(torch.autograd.Function):
             else:
                 dx = native().conv3x3s1_fwd(gy, native().conv3x3_flip(weight))
         if ctx.needs_input_grad[1]:
-            args = (gy, x, weight, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1)
-            dw = torch.ops.aten.convolution_backward(*args, [False, True, False])[1]
+            if SW.conv3x3_wgrad == "ours":
+                dw = native().conv3x3s1_wgrad(x, gy)
+            if dw is None:
+                args = (gy, x, weight, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1)
+                dw = torch.ops.aten.convolution_backward(*args, [False, True, False])[1]
         return dx, dw, None, None
 
 

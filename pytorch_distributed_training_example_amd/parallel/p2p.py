@@ -213,7 +213,8 @@ class P2PProcessGroup(dist.ProcessGroup):
         if opts is None:
             opts = dist.AllreduceOptions()
         op = opts.reduceOp
-        if len(tensors) == 1 and op in (dist.ReduceOp.SUM, dist.ReduceOp.AVG):
+        # (ReduceOp == RedOpType works, ``op in (SUM, AVG)`` does not)
+        if len(tensors) == 1 and (op == dist.ReduceOp.SUM or op == dist.ReduceOp.AVG):
             p2p = self._p2p_for(tensors[0])
             if p2p is not None:
                 self.p2p_calls += 1

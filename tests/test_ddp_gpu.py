@@ -43,7 +43,9 @@ def _worker(rank, world, model_name, reduce_dtype):
         torch.cuda.synchronize()
         got.append([p.grad.float().cpu() for p in model.parameters()])
     # views: every gradient IS its bucket slice (channels_last strides kept)
-    views_ok = all(p.grad.data_ptr() == v.data_ptr() and p.grad.stride() == p.stride()
+    def same_layout(a, b):  # strides of size-1 dims are irrelevant
+        return all(sa == sb for sa, sb, n in zip(a.stride(), b.stride(), a.shape) if n > 1)
+    views_ok = all(p.grad.data_ptr() == v.data_ptr() and same_layout(p.grad, p)
                    for p, v in ddp.parameters_and_views())
     # reference: the two ranks' half-batches one after the other, loss averaged
     ref.zero_grad(set_to_none=True)

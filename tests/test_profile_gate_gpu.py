@@ -25,10 +25,10 @@ def _has(names, needle):
     return any(needle in n for n in names)
 
 
-def test_resnet_step_runs_our_kernels(monkeypatch, switch):
-    # stride-1 1x1 convs on the GEMM path: the per-shape timing (ops/conv.py) may otherwise pick
-    # MIOpen for a data gradient at these toy shapes, whose residual gradient then needs an add
-    switch("PDT_CONV1X1", "gemm")
+def test_resnet_step_runs_our_kernels():
+    """Default switches (no backend forced): 1x1 convs whose output feeds a BatchNorm take our MFMA
+    GEMM with the BN statistics / backward reduction fused (ops/conv.py _pick ``fused``), 3x3 convs
+    (forward, data and weight gradient) our halo kernels."""
     from pytorch_distributed_training_example_amd.models import get_model
     from pytorch_distributed_training_example_amd.models.precision import to_bf16_mixed
     from pytorch_distributed_training_example_amd.ops.cross_entropy import cross_entropy
@@ -49,7 +49,7 @@ def test_resnet_step_runs_our_kernels(monkeypatch, switch):
     for ours in ("bn_reduce3_kernel", "bn_fin_kernel", "bn_apply_kernel", "bn_bwd_apply_kernel",
                  "bn_apply_pool_kernel", "maxpool_bwd_kernel", "ce_fwd_kernel", "ce_bwd_kernel", "mt_kernel",
                  "conv3x3wst_kernel", "conv3x3h_kernel", "conv3x3_flip_kernel", "stem_conv_kernel",
-                 "stem_wgrad_kernel"):
+                 "stem_wgrad_kernel", "conv1x1_kernel", "conv3x3_wgrad_kernel", "conv3x3_wgrad_reduce_kernel"):
         assert _has(names, ours), (ours, sorted(set(names))[:40])
     for stock in ("MIOpenBatchNorm", "batch_norm", "max_pool", "nll_loss", "log_softmax"):
         assert not _has(names, stock), (stock, [n for n in names if stock in n][:5])

@@ -41,23 +41,6 @@ __global__ void ref_kernel(const uint16_t* x, const uint16_t* w, float* y, int N
   }
 }
 
-// naive wgrad reference: one thread per dW element (co, tap, ci), fp32 over all pixels
-__global__ void ref_wgrad_kernel(const uint16_t* x, const uint16_t* dy, float* dw, int N, int H, int W, int Ci, int Co) {
-  const int64_t total = (int64_t)Co * 9 * Ci;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const int ci = (int)(i % Ci), t = (int)((i / Ci) % 9), co = (int)(i / (9 * Ci));
-    const int kh = t / 3, kw = t % 3;
-    float acc = 0.f;
-    for (int n = 0; n < N; ++n)
-      for (int oh = 0; oh < H; ++oh)
-        for (int ow = 0; ow < W; ++ow) {
-          const int ih = oh + kh - 1, iw = ow + kw - 1;
-          if (ih < 0 || ih >= H || iw < 0 || iw >= W) continue;
-          acc += bf2f(dy[(((int64_t)n * H + oh) * W + ow) * Co + co]) * bf2f(x[(((int64_t)n * H + ih) * W + iw) * Ci + ci]);
-        }
-    dw[i] = acc;
-  }
-}
 
 static float h_bf(uint16_t v) { uint32_t u = (uint32_t)v << 16; float f; memcpy(&f, &u, 4); return f; }
 
@@ -124,68 +107,9 @@ static void check(int N, int H, int W, int Ci, int Co, bool dgrad, int iters) {
   if (bad && !getenv("PROBE")) exit(2);
 }
 
-static void check_wgrad(int N, int H, int W, int Ci, int Co, bool ref, int iters) {
-  const int64_t M = (int64_t)N * H * W;
-  uint16_t *x, *dy, *dw;
-  float *ws, *dwr;
-  int ns = 0;
-  const int64_t wsf = pdt_conv3x3_wgrad_ws_floats(N, H, W, Ci, Co, &ns);
-  CK(hipMalloc(&x, M * Ci * 2)); CK(hipMalloc(&dy, M * Co * 2)); CK(hipMalloc(&dw, (int64_t)Co * 9 * Ci * 2));
-  CK(hipMalloc(&ws, wsf * 4)); CK(hipMalloc(&dwr, (int64_t)Co * 9 * Ci * 4));
-  hipLaunchKernelGGL(fill_kernel, dim3(2048), dim3(256), 0, 0, x, M * Ci, 17u, 1.f);
-  hipLaunchKernelGGL(fill_kernel, dim3(2048), dim3(256), 0, 0, dy, M * Co, 23u, 1.f);
-  int rc = pdt_conv3x3s1_wgrad(x, dy, dw, ws, N, H, W, Ci, Co, 0);
-  if (rc) { printf("wgrad launch rc %d\n", rc); exit(1); }
-  double maxerr = 0, maxref = 0;
-  int64_t bad = 0;
-  if (ref) {
-    hipLaunchKernelGGL(ref_wgrad_kernel, dim3(((int64_t)Co * 9 * Ci + 255) / 256), dim3(256), 0, 0, x, dy, dwr, N, H, W, Ci, Co);
-    CK(hipDeviceSynchronize());
-    const int64_t tot = (int64_t)Co * 9 * Ci;
-    std::vector<uint16_t> h(tot);
-    std::vector<float> r(tot);
-    CK(hipMemcpy(h.data(), dw, tot * 2, hipMemcpyDeviceToHost));
-    CK(hipMemcpy(r.data(), dwr, tot * 4, hipMemcpyDeviceToHost));
-    for (int64_t i = 0; i < tot; ++i) {
-      const double d = fabs((double)h_bf(h[i]) - r[i]);
-      maxerr = d > maxerr ? d : maxerr;
-      maxref = fabs(r[i]) > maxref ? fabs(r[i]) : maxref;
-      if (d > 0.01 * fabs(r[i]) + 0.01 * sqrt((double)M)) ++bad;
-    }
-  }
-  double us = 0;
-  if (iters > 0) {
-    hipEvent_t e0, e1;
-    CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-    for (int i = 0; i < 3; ++i) pdt_conv3x3s1_wgrad(x, dy, dw, ws, N, H, W, Ci, Co, 0);
-    CK(hipEventRecord(e0));
-    for (int i = 0; i < iters; ++i) pdt_conv3x3s1_wgrad(x, dy, dw, ws, N, H, W, Ci, Co, 0);
-    CK(hipEventRecord(e1));
-    CK(hipEventSynchronize(e1));
-    float ms; CK(hipEventElapsedTime(&ms, e0, e1));
-    us = ms * 1e3 / iters;
-  }
-  const double flops = 2.0 * M * Ci * Co * 9;
-  printf("wgrad N=%4d H=%3d Ci=%4d Co=%4d splits %3d  maxerr %.3e (max|ref| %.2f) bad %lld  %8.1f us  %6.0f TF/s\n",
-         N, H, Ci, Co, ns, maxerr, maxref, (long long)bad, us, us > 0 ? flops / us / 1e6 : 0.0);
-  fflush(stdout);
-  CK(hipFree(x)); CK(hipFree(dy)); CK(hipFree(dw)); CK(hipFree(ws)); CK(hipFree(dwr));
-  if (bad && !getenv("PROBE")) exit(2);
-}
 
 int main(int argc, char** argv) {
-  if (getenv("WGRAD")) {
-    check_wgrad(3, 13, 11, 64, 64, true, 0);
-    check_wgrad(2, 9, 7, 128, 192, true, 0);
-    check_wgrad(16, 56, 56, 64, 64, true, 0);
-    check_wgrad(16, 7, 7, 512, 512, true, 0);
-    const int it = argc > 1 ? atoi(argv[1]) : 20;
-    check_wgrad(512, 56, 56, 64, 64, false, it);
-    check_wgrad(512, 28, 28, 128, 128, false, it);
-    check_wgrad(512, 14, 14, 256, 256, false, it);
-    check_wgrad(512, 7, 7, 512, 512, false, it);
-    return 0;
-  }
+  // (the weight gradient has its own harness: tools/convbench/wgrad3x3_bench.cpp)
   if (getenv("ONLY")) {  // one ResNet-50 layer (1..4), forward, for counter collection
     const int l = atoi(getenv("ONLY"));
     const int hw[5] = {0, 56, 28, 14, 7}, c[5] = {0, 64, 128, 256, 512};
