@@ -43,11 +43,13 @@ constexpr int kTileTarget = 112;  // pixels per tile (R whole rows)
 constexpr int kHaloMax = 256;     // halo pixel rows per tile (LDS: 32 KB; ResNet-50: <= 240)
 constexpr int kKpMax = 128;       // K rows (pixels, padded to 16) per tile
 
-template <int CO_T_, bool PF_, bool ALLB_ = false>
+// (An LDS-DMA staging variant — global_load_lds into 1 or 2 LDS buffers, source-swizzled — measured
+// 5-11 % SLOWER than the register staging below on every ResNet-50 shape, e.g. 336 vs 302 us at
+// 28x28x128, 493 vs 445 us at 56x56x64: the loop is bound by LDS-read latency, not by staging VGPRs.)
+template <int CO_T_, bool PF_>
 struct WCfg {
   static constexpr int CO_T = CO_T_, CI_T = 64;
-  static constexpr bool PF = PF_;      // next tile's loads in registers under this tile's MFMAs
-  static constexpr bool ALLB = ALLB_;  // all 9 B fragments of a k-step read before its MFMAs
+  static constexpr bool PF = PF_;      // register staging: next tile's loads under this tile's MFMAs
   static constexpr int kWaves = (CO_T / 32) * (CI_T / 32);
   static constexpr int kThreads = kWaves * 64;
   static constexpr int kRowY = CO_T * 2;                 // dY LDS row bytes
@@ -140,7 +142,7 @@ __global__ __launch_bounds__(Cf::kThreads, 2) void conv3x3_wgrad_kernel(const ui
       pfx[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
     }
   };
-  auto write_table = [&]() {
+  auto write_table = [&]() {  // into `table` (the current buffer)
     for (int j = tid; j < KP; j += Cf::kThreads) {
       int hr = 0;  // pad pixels (dY rows are zero): any finite halo row
       if (j < pf_pv) {
@@ -349,15 +351,18 @@ inline bool geo_of(int N, int H, int W, int Ci, int Co, int co_t, int target_wgs
   return true;
 }
 
-int g_target_wgs = 512;  // 2 workgroups per CU
+int g_target_wgs = 0;    // 0: by tile (CO_T 128: 256 = one per CU; CO_T 64: 512 = two per CU)
 int g_co_tile = 0;       // 0: by shape; 64 / 128 forced (tuning)
-int g_allb = 0;          // 1: CO_T = 64 reads all nine B fragments of a k-step up front
 
-// CO_T = 128: 8 waves, 80.5 KB LDS -> one workgroup (2 waves/SIMD) per CU, half the dY staging
-// per FLOP; CO_T = 64: 4 waves, 64.5 KB -> two workgroups per CU overlapping each other's staging
+// CO_T = 128 (Co % 128 == 0): 8 waves, next tile prefetched in registers, one workgroup (2
+// waves/SIMD) per CU, half the dY staging per FLOP — fastest on ResNet-50 layers 2-4 (302 / 282 / 284
+// us vs 329-341 / 305-319 / 313-324 for CO_T = 64 at batch 1024); CO_T = 64 (layer 1): 4 waves,
+// 48.5 KB LDS, two workgroups per CU overlapping each other's staging.
+inline int target_wgs(int co_t) { return g_target_wgs > 0 ? g_target_wgs : (co_t == 128 ? 256 : 512); }
+
 inline int co_tile_of(int Co) {
   if (g_co_tile == 64 || (g_co_tile == 128 && Co % 128 == 0)) return g_co_tile;
-  return 64;
+  return Co % 128 == 0 ? 128 : 64;
 }
 
 template <class Cf>
@@ -384,7 +389,8 @@ extern "C" {
 // fp32 workspace floats for pdt_conv3x3s1_wgrad at this shape (0: unsupported shape).
 int64_t pdt_conv3x3_wgrad_ws_floats(int N, int H, int W, int Ci, int Co, int* nsplit_out) {
   Geo g;
-  if (Ci % 64 != 0 || Co % 64 != 0 || !geo_of(N, H, W, Ci, Co, co_tile_of(Co), g_target_wgs, g)) return 0;
+  const int co_t = co_tile_of(Co);
+  if (Ci % 64 != 0 || Co % 64 != 0 || !geo_of(N, H, W, Ci, Co, co_t, target_wgs(co_t), g)) return 0;
   if (nsplit_out) *nsplit_out = g.nsplit;
   return (int64_t)g.nsplit * 9 * Co * Ci;
 }
@@ -398,18 +404,17 @@ int pdt_conv3x3s1_wgrad(const uint16_t* x, const uint16_t* dy, uint16_t* dw, flo
   if ((int64_t)N * H * W * (Ci > Co ? Ci : Co) >= (int64_t)1 << 31) return -2;  // 32-bit buffer offsets
   Geo g;
   const int co_t = co_tile_of(Co);
-  if (!geo_of(N, H, W, Ci, Co, co_t, g_target_wgs, g)) return -4;
-  if (co_t == 128) return launch<WCfg<128, true>>(x, dy, dw, ws, g, s);
-  return g_allb ? launch<WCfg<64, false, true>>(x, dy, dw, ws, g, s) : launch<WCfg<64, false>>(x, dy, dw, ws, g, s);
+  if (!geo_of(N, H, W, Ci, Co, co_t, target_wgs(co_t), g)) return -4;
+  return co_t == 128 ? launch<WCfg<128, true>>(x, dy, dw, ws, g, s) : launch<WCfg<64, false>>(x, dy, dw, ws, g, s);
 }
 
 void pdt_conv3x3_wgrad_probe(int probe) { g_probe = probe; }
 
+// Tuning / A-B hooks (tools/convbench/wgrad3x3_bench.cpp): target workgroups (0 = by tile) and
+// forced CO_T (0 = by shape).
 void pdt_conv3x3_wgrad_tune(int target_wgs, int co_tile) {
-  if (target_wgs > 0) g_target_wgs = target_wgs;
-  if (co_tile >= 0) g_co_tile = co_tile % 1000;
-  if (co_tile >= 1000) g_allb = 1;
-  else if (co_tile >= 0) g_allb = 0;
+  if (target_wgs >= 0) g_target_wgs = target_wgs;
+  if (co_tile >= 0) g_co_tile = co_tile;
 }
 
 }  // extern "C"

@@ -183,22 +183,32 @@ class _BNTrainFn(torch.autograd.Function):
 
 
 class _BNEvalFn(torch.autograd.Function):
+    """Inference-statistics BatchNorm (+residual)(+ReLU): native forward; backward in PyTorch ops
+    (not a hot path) including the affine gradients — a BN frozen in eval mode inside a training
+    model (fine-tuning) still trains gamma / beta, as in torch."""
+
     @staticmethod
     def forward(ctx, x, residual, weight, bias, running_mean, running_var, eps, relu):
         y = native().bn_fwd_eval(x, residual, weight, bias, running_mean, running_var, eps, relu)
         ctx.relu, ctx.has_res, ctx.eps = relu, residual is not None, eps
-        ctx.save_for_backward(y if relu else None, weight, running_var)
+        ctx.save_for_backward(x, y if relu else None, weight, running_mean, running_var)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        y, weight, rv = ctx.saved_tensors
-        dz = dy * (y > 0) if ctx.relu else dy
-        a = torch.rsqrt(rv + ctx.eps)
-        if weight is not None:
-            a = a * weight
-        dx = (dz.float() * a.view(1, -1, 1, 1) if dz.dim() == 4 else dz.float() * a).to(dz.dtype)
-        return dx, (dz if ctx.has_res else None), None, None, None, None, None, None
+        x, y, weight, rm, rv = ctx.saved_tensors
+        dz = (dy * (y > 0) if ctx.relu else dy).float()
+        shape = (1, -1, 1, 1) if dz.dim() == 4 else (1, -1)
+        dims = (0, 2, 3) if dz.dim() == 4 else (0,)
+        invstd = torch.rsqrt(rv.float() + ctx.eps)
+        a = invstd * weight.float() if weight is not None else invstd
+        dx = (dz * a.view(shape)).to(dy.dtype)
+        dw = db = None
+        if weight is not None and ctx.needs_input_grad[2]:
+            dw = (dz * ((x.float() - rm.float().view(shape)) * invstd.view(shape))).sum(dims).to(weight.dtype)
+        if ctx.needs_input_grad[3]:
+            db = dz.sum(dims).to(weight.dtype if weight is not None else dz.dtype)
+        return dx, (dz.to(dy.dtype) if ctx.has_res else None), dw, db, None, None, None, None
 
 
 class _MaterializeFn(torch.autograd.Function):

@@ -14,7 +14,7 @@ from dist_utils import run_ranks
 
 pytestmark = pytest.mark.gpu
 
-N_PER_RANK, HW, CLASSES = 4, 64, 16
+N_PER_RANK, HW, CLASSES = 4, 96, 16
 
 
 def _data(r):
@@ -25,6 +25,11 @@ def _data(r):
 
 
 def _worker(rank, world, model_name, reduce_dtype):
+    # deterministic MIOpen solvers for the convs still on MIOpen (stride-2 3x3): their atomic split-K
+    # weight gradients differ run to run, and a random-init ResNet's BatchNorms over tiny late-stage
+    # maps amplify that into O(10 %) gradient differences between two otherwise identical passes
+    torch.backends.cudnn.deterministic = True
+    torch.backends.cudnn.benchmark = False
     from pytorch_distributed_training_example_amd.models import get_model
     from pytorch_distributed_training_example_amd.models.precision import to_bf16_mixed
     from pytorch_distributed_training_example_amd.ops.cross_entropy import cross_entropy
@@ -65,9 +70,12 @@ def test_ddp_two_ranks_resnet_matches_half_batch_reference(model_name, reduce_dt
     for it in range(2):
         for a, b in zip(g0[it], g1[it]):
             assert torch.equal(a, b), "replicas must hold identical averaged gradients"
-    errs = []
-    for a, b in zip(g0[1], want0):
-        errs.append(((a - b).norm() / (b.norm() + 1e-6)).item())
-    errs = torch.tensor(errs)
-    # bf16 compute, different reduction orders (per-rank BN statistics, bucketed averaging)
-    assert errs.median() < 2e-2 and errs.max() < 0.15, (errs.median(), errs.max())
+    rel = lambda a, b: ((a - b).norm() / (b.norm() + 1e-6)).item()  # noqa: E731
+    errs = torch.tensor([rel(a, b) for a, b in zip(g0[1], want0)])
+    # bf16 compute through 50 layers (per-rank BN statistics over tiny late-stage maps amplify
+    # rounding) and a different summation order (bucketed averaging vs two accumulated backward
+    # passes): measured median 1-2 %. The wrong answers are far away: the SUM instead of the mean
+    # is 50 % off and a single rank's gradient 70 %.
+    assert errs.median() < 4e-2 and errs.max() < 0.2, (errs.median(), errs.max())
+    sums = torch.tensor([rel(a, 2 * b) for a, b in zip(g0[1], want0)])
+    assert sums.median() > 0.3, "averaging check has no power"
