@@ -12,6 +12,13 @@ Two sweeps, one process per GPU (launch with torchrun, 127.0.0.1 rendezvous):
 
   torchrun --nproc-per-node 8 --master-addr 127.0.0.1 tools/bucket_sweep.py --caps 1,5,10,25,50,100
   python tools/bucket_sweep.py --mode collectives --backend gloo   # CPU plumbing check
+  python tools/bucket_sweep.py --nproc 8 --nchannels 4,8,16,32 --caps 10,25,50
+      # third axis: RCCL channel count (NCCL_MIN/MAX_NCHANNELS, read once per process at communicator
+      # creation, so each value runs as its own torchrun job; every JSON line carries "nchannels")
+
+xGMI is point-to-point (7 links x ~153 GB/s per GPU): a single ring is bound by ONE link, so the
+bucket size that hides the last bucket's all-reduce under backward and the number of RCCL channels
+(parallel rings over different links) have to be chosen together.
 
 The reference issues one un-bucketed fp32 all-reduce per parameter after backward
 (/root/reference/train.py:34-39); its sizes are printed for comparison (--reference-sizes).
@@ -61,15 +68,15 @@ def time_allreduce(numel: int, dtype, dev, iters: int, warmup: int) -> float:
     return float(m.item())
 
 
-def time_p2p(p2p, numel: int, dtype, dev, iters: int, warmup: int) -> float:
+def time_p2p(p2p, numel: int, dtype, dev, iters: int, warmup: int, algo: int = 0) -> float:
     t = torch.ones(numel, dtype=dtype, device=dev)
     for _ in range(warmup):
-        p2p.all_reduce(t)
+        p2p.all_reduce(t, algo=algo)
     _sync(dev)
     launcher.barrier()
     t0 = time.perf_counter()
     for _ in range(iters):
-        p2p.all_reduce(t)
+        p2p.all_reduce(t, algo=algo)
     _sync(dev)
     el = (time.perf_counter() - t0) / iters
     m = torch.tensor([el], dtype=torch.float64, device=dev)
@@ -98,9 +105,10 @@ def sweep_collectives(args, ctx, emit):
               "n_ranks": n, "us": round(sec * 1e6, 2), "algbw_GBps": round(algbw, 2),
               "busbw_GBps": round(algbw * 2 * (n - 1) / max(n, 1), 2), "backend": dist.get_backend()})
         if p2p is not None and numel % 8 == 0 and numel * esize <= p2p.capacity:
-            sec = time_p2p(p2p, numel, dtype, ctx.device, args.iters, args.warmup)
-            emit({"sweep": "collectives", "op": "p2p_oneshot", "bytes": numel * esize, "dtype": str(dtype),
-                  "n_ranks": n, "us": round(sec * 1e6, 2), "algbw_GBps": round(numel * esize / sec / 1e9, 2)})
+            for algo, name in ((0, "p2p_oneshot"), (1, "p2p_twoshot")):
+                sec = time_p2p(p2p, numel, dtype, ctx.device, args.iters, args.warmup, algo)
+                emit({"sweep": "collectives", "op": name, "bytes": numel * esize, "dtype": str(dtype),
+                      "n_ranks": n, "us": round(sec * 1e6, 2), "algbw_GBps": round(numel * esize / sec / 1e9, 2)})
     if p2p is not None:
         p2p.check()
 
@@ -122,8 +130,38 @@ def sweep_train(args, ctx, emit):
             torch.cuda.empty_cache()
 
 
+def channel_sweep(args, argv) -> int:
+    """One torchrun job per RCCL channel count; the child jobs print JSON lines tagged with it."""
+    import subprocess
+    rest, skip = [], False
+    for a in argv:  # drop --nchannels / --nproc and their values
+        if skip:
+            skip = False
+            continue
+        if a in ("--nchannels", "--nproc"):
+            skip = True
+            continue
+        if a.startswith("--nchannels=") or a.startswith("--nproc="):
+            continue
+        rest.append(a)
+    nproc = args.nproc or max(1, torch.cuda.device_count())
+    rc = 0
+    for ch in [int(c) for c in args.nchannels.split(",")]:
+        env = dict(os.environ, NCCL_MIN_NCHANNELS=str(ch), NCCL_MAX_NCHANNELS=str(ch), PDT_SWEEP_NCHANNELS=str(ch),
+                   MASTER_ADDR="127.0.0.1", HSA_ENABLE_IPC_MODE_LEGACY="0")
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+               "--master-addr", "127.0.0.1", f"--master-port={launcher.find_free_port()}",
+               os.path.abspath(__file__), *rest]
+        rc |= subprocess.run(cmd, env=env).returncode
+    return rc
+
+
 def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--nchannels", default=None,
+                    help="comma list of RCCL channel counts: one child job each (NCCL_MIN/MAX_NCHANNELS)")
+    ap.add_argument("--nproc", type=int, default=None, help="ranks per child job (default: visible GPUs)")
     ap.add_argument("--mode", default="both", choices=["collectives", "train", "both"])
     ap.add_argument("--backend", default=None)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
@@ -141,6 +179,8 @@ def main(argv=None):
     ap.add_argument("--train-warmup", type=int, default=5)
     ap.add_argument("--out", default=None)
     args = ap.parse_args(argv)
+    if args.nchannels and "WORLD_SIZE" not in os.environ:
+        return channel_sweep(args, argv)
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     gpu = torch.cuda.is_available() and args.backend in (None, "nccl")
     if args.mode != "collectives" and args.graph and gpu:
@@ -150,7 +190,11 @@ def main(argv=None):
     ctx = launcher.init_distributed(backend=args.backend, use_gpu=gpu)
     lines = []
 
+    nch = os.environ.get("PDT_SWEEP_NCHANNELS")
+
     def emit(d):
+        if nch:
+            d = dict(d, nchannels=int(nch))
         lines.append(d)
         if ctx.rank == 0:
             print(json.dumps(d), flush=True)
