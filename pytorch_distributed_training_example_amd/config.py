@@ -28,7 +28,8 @@ PDT_SUBSAMPLE_NATIVE        1            stride-2 gather / scatter-add kernels
 PDT_LINEAR_SPLITK           1            split-K Linear weight gradients
 PDT_FUSED_ADDLN             1            residual add fused into LayerNorm
 PDT_EMBEDDING_NATIVE        1            GPT-2 token/position embedding on our kernels
-PDT_LINEAR_EPILOGUE         1            Linear bias(+GELU) epilogues on our GEMM kernel
+PDT_LINEAR_EPILOGUE         0            1: Linear forward GEMMs (+bias, MLP fc1+bias+GELU) on our MFMA kernel
+                                         (gemm.hip; 0.61-0.94x of tuned hipBLASLt, so off)
 """
 from __future__ import annotations
 
@@ -72,7 +73,7 @@ class _Switches:
         self.linear_splitk = on("PDT_LINEAR_SPLITK")
         self.fused_addln = on("PDT_FUSED_ADDLN")
         self.embedding_native = on("PDT_EMBEDDING_NATIVE")
-        self.linear_epilogue = on("PDT_LINEAR_EPILOGUE")
+        self.linear_epilogue = e("PDT_LINEAR_EPILOGUE", "0") == "1"
         return self
 
 

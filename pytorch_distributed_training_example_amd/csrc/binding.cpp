@@ -115,6 +115,8 @@ int pdt_fp8_update_scales(float* state, int n, int L, float margin_scale, hipStr
 int pdt_embedding_fwd(const int64_t* idx, const uint16_t* wte, const uint16_t* wpe, uint16_t* out, int64_t n, int T,
                       int D, hipStream_t s);
 int64_t pdt_embedding_bwd_ws_ints(int64_t n, int V);
+int pdt_gemm_nt(const uint16_t* A, const uint16_t* B, uint16_t* C, uint16_t* G, const void* bias, int bias_f32,
+                int epi, int tanh_form, int M, int N, int K, hipStream_t s);
 int pdt_embedding_bwd(const int64_t* idx, const uint16_t* dout, uint16_t* dwte, uint16_t* dwpe, int* ws, int64_t n,
                       int B, int T, int V, int D, hipStream_t s);
 int64_t pdt_p2p_flags_bytes();
@@ -1182,6 +1184,36 @@ std::vector<Tensor> embedding_bwd(Tensor idx, Tensor dout, int64_t V, int64_t P)
   return {dwte, dwpe};
 }
 
+// ---- Linear GEMM with fused epilogues (csrc/kernels/gemm.hip) ----
+// a [M, K], b [N, K] contiguous bf16 -> {C [M, N]} (epi 0: a·bᵀ, 1: a·bᵀ + bias) or {C, G} (epi 2:
+// C = a·bᵀ, G = gelu(C + bias)). bias [N] fp32 or bf16. N % 256 == 0, K % 64 == 0 (gemm_nt_ok).
+std::vector<Tensor> gemm_nt(Tensor a, Tensor b, c10::optional<Tensor> bias, int64_t epi, bool tanh_form) {
+  check_cuda(a, "a");
+  check_cuda(b, "b");
+  TORCH_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 && a.dim() == 2 && b.dim() == 2 &&
+                  a.is_contiguous() && b.is_contiguous() && a.size(1) == b.size(1),
+              "gemm_nt: a [M, K], b [N, K] contiguous bf16");
+  const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
+  const void* bp = nullptr;
+  int bf32 = 0;
+  if (bias.has_value() && bias->defined()) {
+    TORCH_CHECK(bias->is_contiguous() && bias->numel() == N &&
+                    (bias->scalar_type() == at::kFloat || bias->scalar_type() == at::kBFloat16),
+                "gemm_nt: bias [N] fp32 or bf16");
+    bp = bias->data_ptr();
+    bf32 = bias->scalar_type() == at::kFloat;
+  }
+  auto c = at::empty({M, N}, a.options());
+  Tensor g = epi == 2 ? at::empty({M, N}, a.options()) : Tensor();
+  const int rc = pdt_gemm_nt(reinterpret_cast<const uint16_t*>(a.data_ptr()), reinterpret_cast<const uint16_t*>(b.data_ptr()),
+                             reinterpret_cast<uint16_t*>(c.data_ptr()),
+                             epi == 2 ? reinterpret_cast<uint16_t*>(g.data_ptr()) : nullptr, bp, bf32, (int)epi,
+                             tanh_form ? 1 : 0, (int)M, (int)N, (int)K, stream());
+  TORCH_CHECK(rc == 0, "pdt_gemm_nt failed (", rc, ") for M=", M, " N=", N, " K=", K);
+  if (epi == 2) return {c, g};
+  return {c};
+}
+
 // ---- LeNet (reference model) ops: csrc/kernels/lenet.hip ----
 constexpr int kStemIpb = 4;  // images per workgroup in the conv1 weight-gradient reduction
 
@@ -1300,6 +1332,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("stem_conv_wgrad", &stem_conv_wgrad);
   m.def("conv3x3s1_wgrad", &conv3x3s1_wgrad);
   m.def("embedding_fwd", &embedding_fwd);
+  m.def("gemm_nt", &gemm_nt);
   m.def("embedding_bwd", &embedding_bwd);
   m.def("conv3x3_wgrad_tune", [](int target_wgs, int co_tile) { pdt_conv3x3_wgrad_tune(target_wgs, co_tile); });
   m.def("bn_bwd_train", &bn_bwd_train);

@@ -23,6 +23,7 @@ from ..ops.attention import attention_qkv
 from ..ops.gelu import bias_gelu
 from ..ops.layernorm import LayerNorm, add_layer_norm
 from ..ops.linear import linear as _linear
+from ..ops.linear import linear_gelu
 
 
 def linear(x, mod: nn.Linear, bias=True):
@@ -59,6 +60,10 @@ class MLP(nn.Module):
         self.approximate = approximate
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if getattr(self.c_fc, "_fp8", None) is None:
+            g = linear_gelu(x, self.c_fc.weight, self.c_fc.bias, self.approximate)  # PDT_LINEAR_EPILOGUE=1
+            if g is not None:
+                return linear(g, self.c_proj)
         h = linear(x, self.c_fc, bias=False)  # bias is fused into the GELU kernel
         b = self.c_fc.bias
         h = bias_gelu(h, b.float() if b is not None and b.dtype != torch.float32 else b, self.approximate)

@@ -4,6 +4,11 @@ Forward is one hipBLASLt GEMM with the bias fused in its epilogue (``F.linear``)
 two library GEMMs (dX = dY·W, dW = dYᵀ·X) plus ``colsum`` for dbias — aten would reduce dY with a
 generic ``sum(0)`` reduction kernel, which streams a [tokens, D] bf16 gradient at a fraction of
 HBM rate (profiles/r1_steady_gpt2_medium_ours.md: 73 ``reduce_kernel`` calls, 1.6 ms/step).
+
+``PDT_LINEAR_EPILOGUE=1`` runs the forward GEMMs on our MFMA kernel instead (csrc/kernels/gemm.hip:
+bias epilogue, and the MLP's fc1 + bias + GELU in one pass, ``linear_gelu``). Default OFF: measured
+at 0.61-0.94x of the tuned hipBLASLt GEMM (+ standalone GELU kernel) on every ViT-B/16 and
+GPT-2-medium shape (profiles/r3/gemm_vs_hipblaslt.md).
 """
 from __future__ import annotations
 
@@ -43,11 +48,25 @@ def _wgrad(dy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
     return dy2.t() @ x2 if sk == 1 else _wgrad_splitk(dy2, x2, sk)
 
 
+def gemm_nt_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
+    """Shapes our GEMM kernel serves: bf16, out features % 256, in features % 64."""
+    return (x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and w.dim() == 2
+            and w.shape[0] % 256 == 0 and w.shape[1] % 64 == 0 and x.shape[-1] == w.shape[1] and x.numel() > 0)
+
+
+def _ours(x: torch.Tensor, w: torch.Tensor) -> bool:
+    return SW.linear_epilogue and gemm_nt_ok(x, w)
+
+
 class _LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b):
         ctx.save_for_backward(x, w)
         ctx.has_b = b is not None
+        if _ours(x, w):
+            x2 = x.reshape(-1, x.shape[-1]).contiguous()
+            y = native().gemm_nt(x2, w.contiguous(), b, 1 if b is not None else 0, False)[0]
+            return y.view(*x.shape[:-1], w.shape[0])
         return F.linear(x, w, b)
 
     @staticmethod
@@ -71,3 +90,38 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] =
             and (bias is None or bias.dtype == x.dtype) and weight.shape[0] % 8 == 0):
         return _LinearFn.apply(x, weight, bias)
     return F.linear(x, weight, bias)
+
+
+class _LinearGeluFn(torch.autograd.Function):
+    """g = gelu(x·Wᵀ + b) with the GEMM, bias and GELU in one kernel (EPI_GELU); h = x·Wᵀ is kept for
+    the backward, which is the column-strip GELU-backward + bias-gradient kernel and two GEMMs."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, tanh_form):
+        x2 = x.reshape(-1, x.shape[-1]).contiguous()
+        bf = b.float() if b is not None else None
+        h, g = native().gemm_nt(x2, w.contiguous(), bf, 2, tanh_form)
+        ctx.save_for_backward(x2, w, h, bf)
+        ctx.tanh_form, ctx.xshape, ctx.has_b, ctx.bdtype = tanh_form, x.shape, b is not None, (
+            b.dtype if b is not None else None)
+        return g.view(*x.shape[:-1], w.shape[0])
+
+    @staticmethod
+    def backward(ctx, dg):
+        x2, w, h, bf = ctx.saved_tensors
+        dh, db = native().bias_gelu_bwd(dg.reshape(h.shape).contiguous(), h, bf, ctx.tanh_form)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = (dh @ w).view(ctx.xshape)
+        if ctx.needs_input_grad[1]:
+            dw = _wgrad(dh, x2)
+        dbias = db.to(ctx.bdtype) if ctx.has_b and ctx.needs_input_grad[2] else None
+        return dx, dw, dbias, None
+
+
+def linear_gelu(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor], approximate: str) -> Optional[torch.Tensor]:
+    """gelu(linear(x, weight, bias)) on the fused-epilogue kernel, or None when it does not apply
+    (switch off, unsupported shape/dtype): the caller then runs linear + bias_gelu."""
+    if not (use_native(x) and _ours(x, weight)) or (bias is not None and bias.dtype not in (torch.bfloat16, torch.float32)):
+        return None
+    return _LinearGeluFn.apply(x, weight, bias, approximate == "tanh")
