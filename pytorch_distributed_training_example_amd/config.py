@@ -17,6 +17,7 @@ PDT_CONV1X1_DUMP            ""           write the decisions to this path at exi
 PDT_CONV1X1_S2              1            stride-2 1x1 shortcut as gather + GEMM
 PDT_CONV3X3                 ours         3x3 convs on our kernels (ours | miopen)
 PDT_CONV3X3_WGRAD           ours         3x3 weight gradient on our kernel (ours | miopen)
+PDT_CONV3X3_S2              ours         stride-2 3x3 convs on our kernels (ours | miopen)
 PDT_CONV_STEM               ours         7x7 stem on our kernels (ours | miopen)
 PDT_CONV_BN_STATS           1            BatchNorm statistics in conv epilogues
 PDT_BN_BWD_STATS            1            BatchNorm backward reduction in dgrad epilogues
@@ -38,7 +39,7 @@ import os
 
 class _Switches:
     __slots__ = ("disable_native", "conv1x1", "conv1x1_ours", "conv1x1_prefer", "conv1x1_override",
-                 "conv1x1_table", "conv1x1_dump", "conv1x1_s2", "conv3x3", "conv3x3_wgrad", "conv_stem",
+                 "conv1x1_table", "conv1x1_dump", "conv1x1_s2", "conv3x3", "conv3x3_wgrad", "conv3x3_s2", "conv_stem",
                  "conv_bn_stats", "bn_bwd_stats", "res_masked", "stem_bwd_fused", "wgrad_splitk", "slice_sum",
                  "subsample_native", "linear_splitk", "fused_addln", "embedding_native", "linear_epilogue")
 
@@ -62,6 +63,7 @@ class _Switches:
         self.conv1x1_s2 = e("PDT_CONV1X1_S2", "1") == "1"
         self.conv3x3 = e("PDT_CONV3X3", "ours")
         self.conv3x3_wgrad = e("PDT_CONV3X3_WGRAD", "ours")
+        self.conv3x3_s2 = e("PDT_CONV3X3_S2", "ours")
         self.conv_stem = e("PDT_CONV_STEM", "ours")
         self.conv_bn_stats = on("PDT_CONV_BN_STATS")
         self.bn_bwd_stats = on("PDT_BN_BWD_STATS")

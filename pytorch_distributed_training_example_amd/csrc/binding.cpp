@@ -81,6 +81,15 @@ void pdt_conv3x3_wgrad_tune(int target_wgs, int co_tile);
 int pdt_conv3x3s1_fwd_bnbwd(const uint16_t* x, const uint16_t* w, uint16_t* y, const uint16_t* bn_x,
                             const uint8_t* bn_mask, const float* bn_mean, float* bn_part, int N, int H, int W, int Ci,
                             int Co, hipStream_t s);
+int pdt_conv3x3s2_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, float* part, int N, int H, int W, int Ci,
+                      int Co, hipStream_t s);
+int pdt_conv3x3s2_dgrad(const uint16_t* dy, const uint16_t* wf, uint16_t* dx, const uint16_t* bn_x,
+                        const uint8_t* bn_mask, const float* bn_mean, float* bn_part, int N, int H, int W, int Ci,
+                        int Co, hipStream_t s);
+int pdt_conv3x3s2_dgrad_tiles(int N, int H, int W);
+int64_t pdt_conv3x3s2_wgrad_ws_floats(int N, int H, int W, int Ci, int Co, int* nsplit_out);
+int pdt_conv3x3s2_wgrad(const uint16_t* x, const uint16_t* dy, uint16_t* dw, float* ws, int N, int H, int W, int Ci,
+                        int Co, hipStream_t s);
 int pdt_conv3x3s1_fwd_stats(const uint16_t* x, const uint16_t* w, uint16_t* y, float* part, int N, int H, int W,
                             int Ci, int Co, hipStream_t s);
 int64_t pdt_stem_conv_wprep_elems();
@@ -521,10 +530,11 @@ std::vector<Tensor> bn_bwd_train_tiles(Tensor dy, Tensor x, Tensor part, c10::op
   const int64_t C = x.size(1);
   const int64_t M = x.numel() / C;
   const int BMt = pdt_conv1x1_tile_rows();
-  const int64_t T = (M + BMt - 1) / BMt;
+  // any tile count: backward partials are plain sums (stride-2 data gradient: 4 phases of tiles)
+  const int64_t T = part.dim() == 3 ? part.size(1) : 0;
   TORCH_CHECK(C % 64 == 0, "pdt bn bwd: C must be a multiple of 64");
   TORCH_CHECK(part.scalar_type() == at::kFloat && part.is_contiguous() && part.dim() == 3 && part.size(0) == 2 &&
-              part.size(1) == T && part.size(2) == C, "bn_bwd_train_tiles: partials [2, T, C] fp32 expected");
+              T >= 1 && part.size(2) == C, "bn_bwd_train_tiles: partials [2, T, C] fp32 expected");
   auto dx = at::empty_like(x);
   Tensor dres;
   if (has_res) dres = at::empty_like(x);
@@ -741,6 +751,96 @@ std::vector<Tensor> conv3x3s1_fwd_bnbwd(Tensor x, Tensor w, Tensor bn_x, c10::op
   if (rc == -5) return {conv3x3s1_fwd(x, w)};
   TORCH_CHECK(rc == 0, "pdt_conv3x3s1_fwd_bnbwd failed: ", rc);
   return {y, part};
+}
+
+// ----------------------------------------------------------------------------- 3x3 conv (stride 2, pad 1)
+// y = conv2d(x, w, stride=2, padding=1), channels_last bf16 (csrc/kernels/conv3x3_s2.hip); stats: also
+// the per-tile BatchNorm statistics of y -> {y, part [2, T, Co]}. Ci, Co % 128 == 0 (checked by caller:
+// returns {} for a shape the kernel does not take).
+std::vector<Tensor> conv3x3s2_fwd(Tensor x, Tensor w, bool stats) {
+  check_nhwc_bf16(x, "x");
+  TORCH_CHECK(w.dim() == 4 && w.size(2) == 3 && w.size(3) == 3 && w.size(1) == x.size(1) &&
+              w.scalar_type() == at::kBFloat16, "conv3x3s2: weight [Co, Ci, 3, 3] bf16");
+  w = w.contiguous(at::MemoryFormat::ChannelsLast);
+  const int64_t N = x.size(0), Ci = x.size(1), H = x.size(2), W = x.size(3), Co = w.size(0);
+  const int64_t Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  auto y = at::empty({N, Co, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  Tensor part;
+  if (stats) part = at::empty({2, (N * Ho * Wo + 255) / 256, Co}, x.options().dtype(at::kFloat));
+  const int rc = pdt_conv3x3s2_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                                   reinterpret_cast<const uint16_t*>(w.data_ptr()),
+                                   reinterpret_cast<uint16_t*>(y.data_ptr()), stats ? part.data_ptr<float>() : nullptr,
+                                   (int)N, (int)H, (int)W, (int)Ci, (int)Co, stream());
+  if (rc == -1 || rc == -2) return {};
+  TORCH_CHECK(rc == 0, "pdt_conv3x3s2_fwd failed: ", rc);
+  if (stats) return {y, part};
+  return {y};
+}
+
+// dx [N, Ci, H, W] of that conv from dy [N, Co, Ho, Wo] and wf = conv3x3_flip(w). With bn_x / bn_mean
+// (bn_mask optional): dx is the gradient at a BatchNorm's output -> {dx, partials [2, T, Ci]} of its
+// backward reduction (T = 4 phases of tiles). Returns {} for a shape the kernel does not take.
+std::vector<Tensor> conv3x3s2_dgrad(Tensor dy, Tensor wf, int64_t H, int64_t W, c10::optional<Tensor> bn_x,
+                                    c10::optional<Tensor> bn_mask, c10::optional<Tensor> bn_mean) {
+  check_nhwc_bf16(dy, "dy");
+  TORCH_CHECK(wf.dim() == 4 && wf.size(2) == 3 && wf.size(3) == 3 && wf.size(1) == dy.size(1) &&
+              wf.scalar_type() == at::kBFloat16, "conv3x3s2_dgrad: flipped weight [Ci, Co, 3, 3] bf16");
+  wf = wf.contiguous(at::MemoryFormat::ChannelsLast);
+  const int64_t N = dy.size(0), Co = dy.size(1), Ci = wf.size(0);
+  TORCH_CHECK(dy.size(2) == (H - 1) / 2 + 1 && dy.size(3) == (W - 1) / 2 + 1, "conv3x3s2_dgrad: dy spatial size");
+  auto dx = at::empty({N, Ci, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const bool bst = bn_x.has_value() && bn_x->defined();
+  const uint16_t* bx = nullptr;
+  const uint8_t* bm = nullptr;
+  const float* bmean = nullptr;
+  Tensor part;
+  if (bst) {
+    check_nhwc_bf16(*bn_x, "bn_x");
+    TORCH_CHECK(bn_x->sizes() == dx.sizes(), "conv3x3s2_dgrad: bn_x must have dx's shape");
+    TORCH_CHECK(bn_mean.has_value() && bn_mean->defined() && bn_mean->scalar_type() == at::kFloat &&
+                bn_mean->numel() == Ci && bn_mean->is_contiguous() && bn_mean->is_cuda(),
+                "conv3x3s2_dgrad: bn_mean fp32 [Ci]");
+    if (bn_mask.has_value() && bn_mask->defined()) {
+      TORCH_CHECK(bn_mask->scalar_type() == at::kByte && bn_mask->numel() == N * H * W * Ci / 8 && bn_mask->is_cuda(),
+                  "conv3x3s2_dgrad: bn_mask uint8 [M * Ci / 8]");
+      bm = bn_mask->data_ptr<uint8_t>();
+    }
+    bx = reinterpret_cast<const uint16_t*>(bn_x->data_ptr());
+    bmean = bn_mean->data_ptr<float>();
+    part = at::empty({2, (int64_t)pdt_conv3x3s2_dgrad_tiles((int)N, (int)H, (int)W), Ci},
+                     dy.options().dtype(at::kFloat));
+  }
+  const int rc = pdt_conv3x3s2_dgrad(reinterpret_cast<const uint16_t*>(dy.data_ptr()),
+                                     reinterpret_cast<const uint16_t*>(wf.data_ptr()),
+                                     reinterpret_cast<uint16_t*>(dx.data_ptr()), bx, bm, bmean,
+                                     bst ? part.data_ptr<float>() : nullptr, (int)N, (int)H, (int)W, (int)Ci, (int)Co,
+                                     stream());
+  if (rc == -1 || rc == -2) return {};
+  TORCH_CHECK(rc == 0, "pdt_conv3x3s2_dgrad failed: ", rc);
+  if (bst) return {dx, part};
+  return {dx};
+}
+
+// Weight gradient of the stride-2 pad-1 3x3 conv (conv3x3_wgrad.hip, S = 2): dw [Co, Ci, 3, 3]
+// channels_last bf16 from x [N, Ci, H, W] and dy [N, Co, Ho, Wo]; undefined for an unsupported shape.
+Tensor conv3x3s2_wgrad(Tensor x, Tensor dy) {
+  check_nhwc_bf16(x, "x");
+  check_nhwc_bf16(dy, "dy");
+  const int64_t N = x.size(0), Ci = x.size(1), H = x.size(2), W = x.size(3), Co = dy.size(1);
+  TORCH_CHECK(dy.size(0) == N && dy.size(2) == (H - 1) / 2 + 1 && dy.size(3) == (W - 1) / 2 + 1,
+              "conv3x3s2_wgrad: dy [N, Co, Ho, Wo]");
+  int ns = 0;
+  const int64_t wsf = pdt_conv3x3s2_wgrad_ws_floats((int)N, (int)H, (int)W, (int)Ci, (int)Co, &ns);
+  if (wsf == 0 || N * H * W * std::max(Ci, Co) >= ((int64_t)1 << 31)) return Tensor();
+  auto ws = at::empty({wsf}, x.options().dtype(at::kFloat));
+  auto dw = at::empty({Co, Ci, 3, 3}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const int rc = pdt_conv3x3s2_wgrad(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                                     reinterpret_cast<const uint16_t*>(dy.data_ptr()),
+                                     reinterpret_cast<uint16_t*>(dw.data_ptr()), ws.data_ptr<float>(), (int)N, (int)H,
+                                     (int)W, (int)Ci, (int)Co, stream());
+  if (rc == -4 || rc == -1 || rc == -2) return Tensor();
+  TORCH_CHECK(rc == 0, "pdt_conv3x3s2_wgrad failed: ", rc);
+  return dw;
 }
 
 // Data-gradient weights: wf [Ci, Co, 3, 3] (channels_last storage [Ci][3][3][Co]) with
@@ -1328,6 +1428,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv3x3s1_fwd_stats", &conv3x3s1_fwd_stats);
   m.def("conv3x3s1_fwd_bnbwd", &conv3x3s1_fwd_bnbwd);
   m.def("conv3x3_flip", &conv3x3_flip);
+  m.def("conv3x3s2_fwd", &conv3x3s2_fwd);
+  m.def("conv3x3s2_wgrad", &conv3x3s2_wgrad);
+  m.def("conv3x3s2_dgrad", &conv3x3s2_dgrad, py::arg("dy"), py::arg("wf"), py::arg("H"), py::arg("W"),
+        py::arg("bn_x") = py::none(), py::arg("bn_mask") = py::none(), py::arg("bn_mean") = py::none());
   m.def("stem_conv_fwd", &stem_conv_fwd);
   m.def("stem_conv_wgrad", &stem_conv_wgrad);
   m.def("conv3x3s1_wgrad", &conv3x3s1_wgrad);

@@ -1014,11 +1014,13 @@ int pdt_bn_bwd_train(const uint16_t* dy, const uint16_t* x, const uint8_t* mask,
 // Training backward whose reduction (sum dz, sum dz (x - mean), dz = dy * mask) comes from the
 // per-tile partials [2][T][C] written by the kernel that produced dy (conv1x1.hip BSTATS): finalize
 // (2 small launches) + apply, no reduce pass over (dy, x). ws: pdt_bn_tiles_ws_floats(T, C) + 2C floats.
+// The backward partials are plain sums, so T is free (the stride-2 data gradient writes 4 phases of
+// ceil(M/4/256) tiles, conv3x3_s2.hip); BMt is unused here.
 int pdt_bn_bwd_train_tiles(const float* part, int T, int BMt, const uint16_t* dy, const uint16_t* x,
                            const uint8_t* mask, const float* gamma, const float* mean, const float* invstd, int64_t M,
                            int C, int relu, int has_res, uint16_t* dx, uint16_t* dres, float* dgamma, float* dbeta,
                            float* ws, hipStream_t s) {
-  if (C % kCC != 0 || M < 1 || T != (int)((M + BMt - 1) / BMt)) return -1;
+  if (C % kCC != 0 || M < 1 || T < 1) return -1;
   return bn_bwd_from_partials(part, T, BMt, dy, x, mask, gamma, mean, invstd, M, C, relu, has_res, dx, dres, dgamma,
                               dbeta, ws, s);
 }

@@ -29,6 +29,13 @@
 //     XOR chunk swizzle keep the 4-row transposed reads conflict-free; 2 workgroups per CU;
 //   * block -> (split, channel block) map XCD-aware: all channel blocks of one split (same pixel
 //     range: shared dY / X tiles) run on one XCD's L2.
+//
+// Stride 2 (S = 2, ResNet-50's layer2-4 block-0 conv2; MIOpen's igemm_wrw before): output pixel
+// (oh, ow) tap (kh, kw) reads padded input (2 oh + kh, 2 ow + kw). The halo stores each padded input
+// row with its columns DE-INTERLEAVED (even columns, then odd ones, HALF = pad4((W_in + 2) / 2)
+// each), so consecutive output pixels still read consecutive halo rows (the 4-row transposed reads
+// stay conflict-free) and tap (kh, kw) is the row shift kh * 2 HALF + {0, HALF, 1}[kw]. About 4
+// input pixels per output pixel are staged (vs ~1.5 at stride 1), so tiles are 2-8 output rows.
 #include "../common.h"
 
 using namespace pdt;
@@ -40,15 +47,21 @@ typedef float f16v __attribute__((ext_vector_type(16)));
 typedef short s4v __attribute__((ext_vector_type(4)));
 
 constexpr int kTileTarget = 112;  // pixels per tile (R whole rows)
-constexpr int kHaloMax = 256;     // halo pixel rows per tile (LDS: 32 KB; ResNet-50: <= 240)
-constexpr int kKpMax = 128;       // K rows (pixels, padded to 16) per tile
+// K rows (pixels, padded to 16) per tile: 128 at stride 1; 64 at stride 2, whose tiles are halo-
+// limited to 2-8 output rows anyway — halving the dY prefetch registers keeps the 8-wave prefetching
+// workgroup under 256 VGPRs without spilling
+constexpr int kp_max(int S) { return S == 1 ? 128 : 64; }
+// halo pixel rows per tile: stride 1 -> 256 (LDS 32 KB; ResNet-50: <= 240); stride 2 -> 320 (R = 2-8
+// output rows on ResNet-50: a 640-row halo would need 40 prefetch VGPRs and spill heavily)
+constexpr int halo_max(int S) { return S == 1 ? 256 : 320; }
 
 // (An LDS-DMA staging variant — global_load_lds into 1 or 2 LDS buffers, source-swizzled — measured
 // 5-11 % SLOWER than the register staging below on every ResNet-50 shape, e.g. 336 vs 302 us at
 // 28x28x128, 493 vs 445 us at 56x56x64: the loop is bound by LDS-read latency, not by staging VGPRs.)
-template <int CO_T_, bool PF_>
+template <int CO_T_, bool PF_, int S_ = 1>
 struct WCfg {
-  static constexpr int CO_T = CO_T_, CI_T = 64;
+  static constexpr int CO_T = CO_T_, CI_T = 64, S = S_;
+  static constexpr int kHaloMax = halo_max(S), kKpMax = kp_max(S);
   static constexpr bool PF = PF_;      // register staging: next tile's loads under this tile's MFMAs
   static constexpr int kWaves = (CO_T / 32) * (CI_T / 32);
   static constexpr int kThreads = kWaves * 64;
@@ -80,7 +93,8 @@ __device__ __forceinline__ bf16x8 cat2(s4v a, s4v b) {
 }
 
 struct Geo {
-  int N, H, W, Ci, Co, R, NH, ntiles, tiles_per_split, nsplit, nblk;
+  int N, H, W, Ci, Co, R, NH, ntiles, tiles_per_split, nsplit, nblk;  // H, W: OUTPUT (= dY) size
+  int Hi, Wi;  // input size (= H, W at stride 1)
   int probe;  // diagnostics (wgrad3x3_bench): 1 = staging only, 2 = MFMA only (first tile staged)
 };
 
@@ -95,8 +109,13 @@ __global__ __launch_bounds__(Cf::kThreads, 2) void conv3x3_wgrad_kernel(const ui
   int* const table = reinterpret_cast<int*>(lds + Cf::kDyBytes + Cf::kHaloBytes);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   // halo rows of one padded image row: W + 2 rounded up to a multiple of 4, so the tap offset kh*W2
-  // never changes a row's chunk swizzle (it depends on row bit 1)
-  const int H = g.H, W = g.W, W2 = (W + 2 + 3) & ~3, H2 = H + 2;
+  // never changes a row's chunk swizzle (it depends on row bit 1); stride 2: two de-interleaved
+  // halves of HALF (a multiple of 4) rows
+  constexpr int S = Cf::S;
+  const int H = g.H, W = g.W, Hi = g.Hi, Wi = g.Wi;
+  const int HALF = S == 1 ? 0 : ((Wi + 3) / 2 + 3) & ~3;
+  const int W2 = S == 1 ? (W + 2 + 3) & ~3 : 2 * HALF, H2 = Hi + 2;
+  const int kwo1 = S == 1 ? 1 : HALF, kwo2 = S == 1 ? 2 : 1;  // row shift of taps kw = 1, 2
   const int nblk_ci = g.Ci / 64;
   // XCD-aware: consecutive logical ids (one split's channel blocks) on one XCD
   const int L = xcd_remap(blockIdx.x, gridDim.x);
@@ -114,15 +133,15 @@ __global__ __launch_bounds__(Cf::kThreads, 2) void conv3x3_wgrad_kernel(const ui
   int pf_pv = 0, pf_prs = 0, pf_g0 = 0;
   constexpr uint32_t kOob = 0xfffffff0u;
   const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<uint16_t*>(X), (short)0, (uint32_t)((int64_t)g.NH * W * g.Ci * 2), 0x00020000);
+      const_cast<uint16_t*>(X), (short)0, (uint32_t)((int64_t)g.N * Hi * Wi * g.Ci * 2), 0x00020000);
   const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<uint16_t*>(dY), (short)0, (uint32_t)((int64_t)g.NH * W * g.Co * 2), 0x00020000);
 
   auto load_tile = [&](int t) {
     const int g0 = t * g.R, gl = min(g0 + g.R, g.NH) - 1;
     const int pv = (gl - g0 + 1) * W;
-    const int prs = (g0 / H) * H2 + g0 % H;      // first halo padded row (= PR(g0) - 1)
-    const int pre = (gl / H) * H2 + gl % H + 2;  // last halo padded row (= PR(gl) + 1)
+    const int prs = (g0 / H) * H2 + S * (g0 % H);      // first halo padded row (tap kh = 0 of row g0)
+    const int pre = (gl / H) * H2 + S * (gl % H) + 2;  // last halo padded row (tap kh = 2 of row gl)
     const int nh = (pre - prs + 1) * W2;
     pf_pv = pv; pf_prs = prs; pf_g0 = g0;
     const uint32_t ybase = (uint32_t)g0 * W * g.Co * 2 + co0 * 2;
@@ -136,9 +155,10 @@ __global__ __launch_bounds__(Cf::kThreads, 2) void conv3x3_wgrad_kernel(const ui
     for (int i = 0; i < Cf::kPfX; ++i) {
       const int c = tid + i * Cf::kThreads, row = c >> 3, ch = c & 7;
       const int r = row / W2, col = row - r * W2;
-      const int pr = prs + r, n = pr / H2, ih = pr - n * H2 - 1, iw = col - 1;
-      const bool ok = row < nh && ih >= 0 && ih < H && iw >= 0 && iw < W;
-      const uint32_t off = ok ? (uint32_t)((((n * H + ih) * W + iw) * g.Ci + ci0 + ch * 8) * 2) : kOob;
+      const int pc = S == 1 ? col : (col < HALF ? 2 * col : 2 * (col - HALF) + 1);  // padded input column
+      const int pr = prs + r, n = pr / H2, ih = pr - n * H2 - 1, iw = pc - 1;
+      const bool ok = row < nh && ih >= 0 && ih < Hi && iw >= 0 && iw < Wi;
+      const uint32_t off = ok ? (uint32_t)((((n * Hi + ih) * Wi + iw) * g.Ci + ci0 + ch * 8) * 2) : kOob;
       pfx[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
     }
   };
@@ -147,7 +167,7 @@ __global__ __launch_bounds__(Cf::kThreads, 2) void conv3x3_wgrad_kernel(const ui
       int hr = 0;  // pad pixels (dY rows are zero): any finite halo row
       if (j < pf_pv) {
         const int gg = pf_g0 + j / W, w = j % W;
-        hr = ((gg / H) * H2 + gg % H - pf_prs) * W2 + w;  // tap (0, 0) of pixel j
+        hr = ((gg / H) * H2 + S * (gg % H) - pf_prs) * W2 + w;  // tap (0, 0) of pixel j
       }
       table[j] = hr;
     }
@@ -212,11 +232,12 @@ __global__ __launch_bounds__(Cf::kThreads, 2) void conv3x3_wgrad_kernel(const ui
     };
     int bx0[3], bx1[3];
     auto bases = [&](int h0_, int h1_) {
-#pragma unroll
-      for (int kw = 0; kw < 3; ++kw) {
-        bx0[kw] = addrX(h0_ + kw);
-        bx1[kw] = addrX(h1_ + kw);
-      }
+      bx0[0] = addrX(h0_);
+      bx1[0] = addrX(h1_);
+      bx0[1] = addrX(h0_ + kwo1);
+      bx1[1] = addrX(h1_ + kwo1);
+      bx0[2] = addrX(h0_ + kwo2);
+      bx1[2] = addrX(h1_ + kwo2);
     };
     auto rdB = [&](int, int, int t) {
       const int kh = t / 3, kw = t % 3;
@@ -320,26 +341,41 @@ inline int rows_per_tile(int W) {
 
 // Largest halo (padded pixel rows) of any tile: tiles start at global rows t*R, whose offsets in
 // their image cycle through {t*R mod H}; a tile starting at offset o touches (o + R - 1)/H + 1 images
-// and stages R real rows plus 2 pad rows per image.
-inline int64_t halo_rows(int R, int H, int W) {
-  int imgs = 1;
-  for (int t = 0, o = 0; t < H; ++t, o = (o + R) % H) {
-    const int k = (o + R - 1) / H + 1;
-    imgs = k > imgs ? k : imgs;
+// and stages R real rows plus 2 pad rows per image. Stride 2 (input Hi x Wi, output H x W): padded
+// input rows pr(g) = (g / H)(Hi + 2) + 2 (g % H) .. pr(last) + 2.
+inline int64_t halo_rows(int R, int H, int W, int S = 1, int Hi = 0, int Wi = 0) {
+  if (S == 1) {
+    int imgs = 1;
+    for (int t = 0, o = 0; t < H; ++t, o = (o + R) % H) {
+      const int k = (o + R - 1) / H + 1;
+      imgs = k > imgs ? k : imgs;
+    }
+    return (int64_t)(R + 2 * imgs) * ((W + 2 + 3) & ~3);
   }
-  return (int64_t)(R + 2 * imgs) * ((W + 2 + 3) & ~3);
+  int64_t rows = 0;
+  for (int t = 0, o = 0; t < H; ++t, o = (o + R) % H) {
+    const int last = o + R - 1;
+    const int64_t r = (int64_t)(last / H) * (Hi + 2) + 2 * (last % H) + 2 - 2 * o + 1;
+    rows = r > rows ? r : rows;
+  }
+  return rows * 2 * (((Wi + 3) / 2 + 3) & ~3);
 }
 
 int g_probe = 0;
 
-inline bool geo_of(int N, int H, int W, int Ci, int Co, int co_t, int target_wgs, Geo& g) {
-  g.N = N; g.H = H; g.W = W; g.Ci = Ci; g.Co = Co;
+// H, W: output (dY) size; Hi, Wi: input size (stride S)
+inline bool geo_of(int N, int H, int W, int Ci, int Co, int co_t, int target_wgs, Geo& g, int S = 1, int Hi = 0,
+                   int Wi = 0) {
+  if (S == 1) { Hi = H; Wi = W; }
+  g.N = N; g.H = H; g.W = W; g.Ci = Ci; g.Co = Co; g.Hi = Hi; g.Wi = Wi;
+  const int hmax = halo_max(S), kpmax = kp_max(S);
   g.R = rows_per_tile(W);
-  while (g.R > 1 && halo_rows(g.R, H, W) > kHaloMax) --g.R;  // tiny images: more pad rows per tile
+  // tiny images: more pad rows per tile; stride 2: also the K-row cap
+  while (g.R > 1 && (halo_rows(g.R, H, W, S, Hi, Wi) > hmax || ((g.R * W + 15) & ~15) > kpmax)) --g.R;
   g.NH = N * H;
   const int P = g.R * W, KP = (P + 15) & ~15;
-  if (KP > kKpMax) return false;
-  if (halo_rows(g.R, H, W) > kHaloMax) return false;
+  if (KP > kpmax) return false;
+  if (halo_rows(g.R, H, W, S, Hi, Wi) > hmax) return false;
   g.ntiles = (g.NH + g.R - 1) / g.R;
   g.nblk = (Co / co_t) * (Ci / 64);
   int ns = (target_wgs + g.nblk - 1) / g.nblk;
@@ -406,6 +442,30 @@ int pdt_conv3x3s1_wgrad(const uint16_t* x, const uint16_t* dy, uint16_t* dw, flo
   const int co_t = co_tile_of(Co);
   if (!geo_of(N, H, W, Ci, Co, co_t, target_wgs(co_t), g)) return -4;
   return co_t == 128 ? launch<WCfg<128, true>>(x, dy, dw, ws, g, s) : launch<WCfg<64, false>>(x, dy, dw, ws, g, s);
+}
+
+// Stride 2 / pad 1 (input x [N,H,W,Ci], dy [N,Ho,Wo,Co], Ho = (H-1)/2+1), Ci % 64 == 0, Co % 64 == 0.
+// CO_T 128 (one 8-wave workgroup per CU, next tile prefetched in registers) unless forced to 64
+// (pdt_conv3x3_wgrad_tune) or Co % 128 != 0: 4 waves, 2 workgroups per CU, synchronous staging.
+inline int s2_co_tile(int Co) { return (g_co_tile == 64 || Co % 128 != 0) ? 64 : 128; }
+
+int64_t pdt_conv3x3s2_wgrad_ws_floats(int N, int H, int W, int Ci, int Co, int* nsplit_out) {
+  Geo g;
+  if (Ci % 64 != 0 || Co % 64 != 0 || H < 2 || W < 2) return 0;
+  const int co_t = s2_co_tile(Co);
+  if (!geo_of(N, (H - 1) / 2 + 1, (W - 1) / 2 + 1, Ci, Co, co_t, target_wgs(co_t), g, 2, H, W)) return 0;
+  if (nsplit_out) *nsplit_out = g.nsplit;
+  return (int64_t)g.nsplit * 9 * Co * Ci;
+}
+
+int pdt_conv3x3s2_wgrad(const uint16_t* x, const uint16_t* dy, uint16_t* dw, float* ws, int N, int H, int W, int Ci,
+                        int Co, hipStream_t s) {
+  if (Ci % 64 != 0 || Co % 64 != 0 || N < 1 || H < 2 || W < 2) return -1;
+  if ((int64_t)N * H * W * (Ci > Co ? Ci : Co) >= (int64_t)1 << 31) return -2;  // 32-bit buffer offsets
+  Geo g;
+  const int co_t = s2_co_tile(Co);
+  if (!geo_of(N, (H - 1) / 2 + 1, (W - 1) / 2 + 1, Ci, Co, co_t, target_wgs(co_t), g, 2, H, W)) return -4;
+  return co_t == 128 ? launch<WCfg<128, true, 2>>(x, dy, dw, ws, g, s) : launch<WCfg<64, false, 2>>(x, dy, dw, ws, g, s);
 }
 
 void pdt_conv3x3_wgrad_probe(int probe) { g_probe = probe; }

@@ -479,6 +479,63 @@ class _Conv3x3Fn(torch.autograd.Function):
         return dx, dw, None, None
 
 
+class _Conv3x3S2Fn(torch.autograd.Function):
+    """Stride-2 pad-1 3x3 convolution on our MFMA kernels (csrc/kernels/conv3x3_s2.hip): forward =
+    gathered implicit GEMM with the consuming BatchNorm's statistics in the epilogue; data gradient =
+    the four output-parity phases of the transposed conv in one launch (with the producing BatchNorm's
+    backward reduction in the epilogue); weight gradient = the halo-tiled split-K kernel at stride 2
+    (conv3x3_wgrad.hip). Replaces MIOpen's ck grouped_conv_fwd / igemm_bwd / igemm_wrw on ResNet-50's
+    layer2-4 block-0 conv2."""
+
+    @staticmethod
+    def forward(ctx, x, weight, stats_out=None, gsrc=None):
+        from ._native import native
+        ctx.save_for_backward(x, weight)
+        ctx.gsrc = gsrc
+        r = native().conv3x3s2_fwd(x, weight, stats_out is not None)
+        if not r:  # shape the kernel does not take
+            return F.conv2d(x, weight, None, 2, 1)
+        if stats_out is not None:
+            stats_out.append(r[1])
+        return r[0]
+
+    @staticmethod
+    def backward(ctx, gy):
+        from ._native import native
+        x, weight = ctx.saved_tensors
+        gy = gy.contiguous(memory_format=torch.channels_last)
+        args = (gy, x, weight, None, [2, 2], [1, 1], [1, 1], False, [0, 0], 1)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            H, W = x.shape[2], x.shape[3]
+            gs = ctx.gsrc if ctx.gsrc is not None and ctx.gsrc.ready() else None
+            kw = dict(bn_x=gs.x, bn_mask=gs.mask, bn_mean=gs.mean) if gs is not None else {}
+            r = native().conv3x3s2_dgrad(gy, native().conv3x3_flip(weight), H, W, **kw)
+            if r:
+                dx = r[0]
+                if len(r) == 2:
+                    gs.deposit(r[1], dx)
+            else:
+                dx = torch.ops.aten.convolution_backward(*args, [True, False, False])[0]
+        if ctx.needs_input_grad[1]:
+            if SW.conv3x3_wgrad == "ours":
+                dw = native().conv3x3s2_wgrad(x, gy)
+            if dw is None:
+                dw = torch.ops.aten.convolution_backward(*args, [False, True, False])[1]
+        return dx, dw, None, None
+
+
+def conv3x3s2_eligible(conv: nn.Conv2d, x: torch.Tensor) -> bool:
+    """Our stride-2 3x3 kernels apply: stride 2, padding 1, no bias/groups/dilation, channels_last
+    bf16 GPU input with Ci % 128 == 0 and Co % 128 == 0 (ResNet-50: layer2-4 block-0 conv2)."""
+    return (conv.kernel_size == (3, 3) and conv.stride == (2, 2) and conv.padding == (1, 1)
+            and conv.dilation == (1, 1) and conv.groups == 1 and conv.bias is None and conv.padding_mode == "zeros"
+            and x.is_cuda and x.dim() == 4 and x.dtype == torch.bfloat16 and conv.weight.dtype == torch.bfloat16
+            and x.is_contiguous(memory_format=torch.channels_last) and x.shape[1] % 128 == 0
+            and conv.out_channels % 128 == 0 and x.shape[2] >= 2 and x.shape[3] >= 2
+            and SW.conv3x3_s2 == "ours" and not disabled())
+
+
 def conv3x3_eligible(conv: nn.Conv2d, x: torch.Tensor) -> bool:
     """Our 3x3 kernel applies: stride 1, padding 1, no bias/groups/dilation, channels_last bf16 GPU
     input with Ci % 64 == 0 and Co % 64 == 0 (the data gradient swaps them; ResNet-50: 13 of 16 3x3 convs)."""
@@ -529,19 +586,22 @@ def stem_eligible(conv: nn.Conv2d, x: torch.Tensor) -> bool:
 
 
 class SplitConv2d(nn.Conv2d):
-    """``nn.Conv2d`` (same parameters / state_dict). On the GPU, stride-1 3x3 convolutions and
-    the ResNet stem run on our MFMA kernels (``_Conv3x3Fn`` / ``_StemConvFn``;
-    ``PDT_CONV3X3=miopen`` / ``PDT_CONV_STEM=miopen`` switch back)."""
+    """``nn.Conv2d`` (same parameters / state_dict). On the GPU, stride-1 and stride-2 3x3
+    convolutions and the ResNet stem run on our MFMA kernels (``_Conv3x3Fn`` / ``_Conv3x3S2Fn`` /
+    ``_StemConvFn``; ``PDT_CONV3X3=miopen`` / ``PDT_CONV3X3_S2=miopen`` / ``PDT_CONV_STEM=miopen``
+    switch back)."""
 
     emit_bn_stats = True  # output feeds a BatchNorm: fuse its statistics where our kernel runs
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        if conv3x3_eligible(self, x):
+        s1 = conv3x3_eligible(self, x)
+        if s1 or conv3x3s2_eligible(self, x):
             holder = [] if (self.emit_bn_stats and self.training and torch.is_grad_enabled()
                             and SW.conv_bn_stats) else None
             from .batchnorm import grad_stats_source_of
-            y = _Conv3x3Fn.apply(x, self.weight, holder,
-                                 grad_stats_source_of(x) if self.training and torch.is_grad_enabled() else None)
+            fn = _Conv3x3Fn if s1 else _Conv3x3S2Fn
+            y = fn.apply(x, self.weight, holder,
+                         grad_stats_source_of(x) if self.training and torch.is_grad_enabled() else None)
             if holder:
                 y._pdt_bn_stats = BNStats(holder[0], y._version)
             return y
