@@ -9,7 +9,7 @@ fixture in ``tests/conftest.py``).
 Switch                      default      meaning
 PDT_DISABLE_NATIVE          0            1: every op on its PyTorch reference path (stock baseline)
 PDT_CONV1X1                 auto         1x1 conv backend: auto (measured table) | ours | gemm | miopen | off
-PDT_CONV1X1_OURS            fwd,dgrad    directions allowed on our MFMA GEMM
+PDT_CONV1X1_OURS            fwd,dgrad,wgrad  directions allowed on our MFMA kernels (conv1x1.hip, conv1x1_wgrad.hip)
 PDT_CONV1X1_PREFER          ""           directions that take our GEMM regardless of the table
 PDT_CONV1X1_OVERRIDE        ""           per-shape decisions "dir,dtype,M,Ci,Co=algo;..." (A/B tools)
 PDT_CONV1X1_TABLE           1            0: ignore tuning/conv1x1_gfx950.json
@@ -54,7 +54,7 @@ class _Switches:
 
         self.disable_native = e("PDT_DISABLE_NATIVE", "0") == "1"
         self.conv1x1 = e("PDT_CONV1X1", "auto")
-        self.conv1x1_ours = tuple(e("PDT_CONV1X1_OURS", "fwd,dgrad").split(","))
+        self.conv1x1_ours = tuple(e("PDT_CONV1X1_OURS", "fwd,dgrad,wgrad").split(","))
         self.conv1x1_prefer = tuple(p for p in e("PDT_CONV1X1_PREFER", "").split(",") if p)
         ov = e("PDT_CONV1X1_OVERRIDE", "")
         self.conv1x1_override = dict(p.split("=", 1) for p in ov.replace("+", ";").split(";") if "=" in p)

@@ -101,6 +101,10 @@ int pdt_stem_conv_wgrad(const uint16_t* x, const uint16_t* dy, uint16_t* dw, flo
 int pdt_maxpool3s2_bwd(const uint16_t* dy, const uint8_t* code, uint16_t* dz, int N, int H, int W, int C,
                        hipStream_t s);
 int pdt_conv1x1_tile_rows();
+int64_t pdt_conv1x1_wgrad_ws_floats(int M, int Ci, int Co, int* nsplit_out);
+int pdt_conv1x1_wgrad(const uint16_t* x, const uint16_t* dy, uint16_t* dw, float* ws, int M, int Ci, int Co,
+                      hipStream_t s);
+void pdt_conv1x1_wgrad_tune(int target_wgs);
 int pdt_conv1x1_gemm(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t* c, const uint8_t* cm,
                      float* part, int M, int K, int N, const uint16_t* bn_x, const uint8_t* bn_mask,
                      const float* bn_mean, float* bn_part, int c_s, int c_H, int c_W, hipStream_t s);
@@ -635,6 +639,32 @@ c10::optional<Tensor> conv1x1_gemm(Tensor a, Tensor b, Tensor out, bool acc, boo
                                   stream());
   TORCH_CHECK(rc == 0, "pdt_conv1x1_gemm failed: ", rc);
   return part;
+}
+
+// Weight gradient of a stride-1 1x1 conv (csrc/kernels/conv1x1_wgrad.hip): dw [Co, Ci] bf16 =
+// dy[M, Co]^T x[M, Ci] from the row-major bf16 NHWC views (split-K over pixels, fixed-order fp32
+// reduction). Returns an undefined tensor for a shape the kernel does not take (caller falls back).
+Tensor conv1x1_wgrad(Tensor x, Tensor dy) {
+  check_cuda(x, "x");
+  check_cuda(dy, "dy");
+  TORCH_CHECK(x.dim() == 2 && dy.dim() == 2 && x.size(0) == dy.size(0), "conv1x1_wgrad: x [M, Ci], dy [M, Co]");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && dy.scalar_type() == at::kBFloat16 && x.is_contiguous() &&
+                  dy.is_contiguous(),
+              "conv1x1_wgrad: contiguous bf16 operands");
+  const int64_t M = x.size(0), Ci = x.size(1), Co = dy.size(1);
+  if (M * std::max(Ci, Co) >= ((int64_t)1 << 31)) return Tensor();
+  int ns = 0;
+  const int64_t wsf = pdt_conv1x1_wgrad_ws_floats((int)M, (int)Ci, (int)Co, &ns);
+  if (wsf == 0) return Tensor();
+  auto ws = at::empty({wsf}, x.options().dtype(at::kFloat));
+  auto dw = at::empty({Co, Ci}, x.options());
+  const int rc = pdt_conv1x1_wgrad(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                                   reinterpret_cast<const uint16_t*>(dy.data_ptr()),
+                                   reinterpret_cast<uint16_t*>(dw.data_ptr()), ws.data_ptr<float>(), (int)M, (int)Ci,
+                                   (int)Co, stream());
+  if (rc == -1 || rc == -2) return Tensor();
+  TORCH_CHECK(rc == 0, "pdt_conv1x1_wgrad failed: ", rc);
+  return dw;
 }
 
 // BN training forward with the statistics taken from conv1x1_gemm's per-tile partials.
@@ -1435,6 +1465,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("stem_conv_fwd", &stem_conv_fwd);
   m.def("stem_conv_wgrad", &stem_conv_wgrad);
   m.def("conv3x3s1_wgrad", &conv3x3s1_wgrad);
+  m.def("conv1x1_wgrad", &conv1x1_wgrad);
+  m.def("conv1x1_wgrad_tune", [](int target_wgs) { pdt_conv1x1_wgrad_tune(target_wgs); });
   m.def("embedding_fwd", &embedding_fwd);
   m.def("gemm_nt", &gemm_nt);
   m.def("embedding_bwd", &embedding_bwd);

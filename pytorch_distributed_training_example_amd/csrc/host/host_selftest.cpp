@@ -10,6 +10,10 @@
 //   * conv3x3_wgrad.hip geo_of / halo_rows: for every tile of an accepted shape the halo the kernel
 //     stages fits the LDS buffer and the prefetch registers (brute force over all tiles), K rows fit,
 //     the tiles cover every image row exactly once, and the splits cover every tile;
+//   * conv3x3_wgrad.hip stride 2: the ResNet-50 block-0 shapes are accepted;
+//   * conv1x1_wgrad.hip geo_of: the pixel splits cover every 32-pixel stage exactly once, the
+//     workspace holds every split's partials, and the DMA source swizzle is a permutation of each
+//     LDS row's chunks (every staged byte lands exactly once);
 //   * batchnorm.hip reduce_geo3: the row blocks tile M exactly;
 //   * embedding.hip workspace arithmetic.
 // Build + run: python -m pytorch_distributed_training_example_amd._build --host-selftest
@@ -27,6 +31,9 @@ namespace bn {
 #include "../kernels/batchnorm.hip"
 }
 #include "../kernels/embedding.hip"
+namespace w1 {
+#include "../kernels/conv1x1_wgrad.hip"
+}
 
 static int g_fail = 0;
 #define EXPECT(c, ...)                         \
@@ -81,13 +88,13 @@ static void test_wgrad_geometry() {
           ++accepted;
           const int W2 = (W + 2 + 3) & ~3, H2 = H + 2;
           const int KP = (g.R * W + 15) & ~15;
-          EXPECT(KP <= kKpMax, "KP %d", KP);
+          EXPECT(KP <= kp_max(1), "KP %d", KP);
           int64_t rows = 0;
           for (int t = 0; t < g.ntiles; ++t) {  // mirror of the kernel's load_tile
             const int g0 = t * g.R, gl = std::min(g0 + g.R, g.NH) - 1;
             const int prs = (g0 / H) * H2 + g0 % H, pre = (gl / H) * H2 + gl % H + 2;
             const int nh = (pre - prs + 1) * W2;
-            EXPECT(nh <= kHaloMax, "N%d H%d W%d tile %d halo %d > %d", N, H, W, t, nh, kHaloMax);
+            EXPECT(nh <= halo_max(1), "N%d H%d W%d tile %d halo %d > %d", N, H, W, t, nh, halo_max(1));
             // the deepest B read (last pixel, tap 2,2) stays inside the staged rows
             const int gg = gl, w = W - 1;
             const int hr = ((gg / H) * H2 + gg % H - prs) * W2 + w + 2 * W2 + 2;
@@ -100,8 +107,8 @@ static void test_wgrad_geometry() {
           // exact prefetch tiling: the register pieces cover the LDS buffers exactly
           using C64 = WCfg<64, false>;
           using C128 = WCfg<128, true>;
-          EXPECT(C64::kPfX * C64::kThreads == kHaloMax * 8, "pfx");
-          EXPECT(C128::kPfY * C128::kThreads == kKpMax * 16, "pfy");
+          EXPECT(C64::kPfX * C64::kThreads == halo_max(1) * 8, "pfx");
+          EXPECT(C128::kPfY * C128::kThreads == kp_max(1) * 16, "pfy");
         }
       }
   EXPECT(accepted > 1000, "only %d shapes accepted", accepted);
@@ -109,6 +116,37 @@ static void test_wgrad_geometry() {
   for (int hw : {56, 28, 14, 7}) {
     Geo g;
     EXPECT(geo_of(1024, hw, hw, 64, 64, 64, 512, g), "ResNet-50 %dx%d rejected", hw, hw);
+  }
+}
+
+static void test_wgrad1x1_geometry() {
+  int accepted = 0;
+  for (int M : {1, 31, 32, 33, 777, 4096, 50176, 200704, 3211264})
+    for (int Ci : {64, 128, 192, 256, 512, 2048})
+      for (int Co : {64, 128, 256, 320, 512, 2048}) {
+        w1::W1Geo g;
+        if (!w1::geo_of(M, Ci, Co, g)) continue;
+        ++accepted;
+        EXPECT(g.ntiles * 32 >= M && (g.ntiles - 1) * 32 < M, "stages M=%d", M);
+        EXPECT((int64_t)g.nsplit * g.tiles_per_split >= g.ntiles && (g.nsplit - 1) * g.tiles_per_split < g.ntiles,
+               "splits M=%d Ci=%d Co=%d", M, Ci, Co);
+        int cob, cib, occ;
+        w1::block_dims(w1::pick_block(Co, Ci), cob, cib, occ);
+        EXPECT(Co % cob == 0 && Ci % cib == 0 && g.nblk == (Co / cob) * (Ci / cib), "blocks Ci=%d Co=%d", Ci, Co);
+        int ns = 0;
+        EXPECT(w1::pdt_conv1x1_wgrad_ws_floats(M, Ci, Co, &ns) == (int64_t)ns * Ci * Co && ns == g.nsplit, "ws");
+      }
+  EXPECT(accepted > 300, "only %d 1x1 wgrad shapes accepted", accepted);
+  for (int rowb : {128, 256, 512}) {
+    for (int row = 0; row < 32; ++row) {
+      std::vector<int> seen(rowb / 16, 0);
+      for (int slot = 0; slot < rowb / 16; ++slot) {
+        const int ch = rowb == 128 ? w1::swz<128>(row, slot) : (rowb == 256 ? w1::swz<256>(row, slot) : w1::swz<512>(row, slot));
+        EXPECT(ch >= 0 && ch < rowb / 16, "swizzle range");
+        if (ch >= 0 && ch < rowb / 16) ++seen[ch];
+      }
+      for (int c = 0; c < rowb / 16; ++c) EXPECT(seen[c] == 1, "swizzle not a permutation rowb %d row %d", rowb, row);
+    }
   }
 }
 
@@ -127,6 +165,12 @@ int main() {
   test_mt_batches(rng);
   test_wgrad_geometry();
   test_bn_geometry();
+  test_wgrad1x1_geometry();
+  for (int hw : {56, 28, 14}) {
+    Geo g;
+    EXPECT(geo_of(1024, (hw - 1) / 2 + 1, (hw - 1) / 2 + 1, 2 * 64, 2 * 64, 128, 256, g, 2, hw, hw),
+           "ResNet-50 stride-2 %dx%d rejected", hw, hw);
+  }
   EXPECT(pdt_embedding_bwd_ws_ints(8192, 50304) == 3 * 50304 + 2 * 8192, "embedding ws");
   std::printf(g_fail ? "host selftest: %d failures\n" : "host selftest: all passed (%d)\n", g_fail);
   return g_fail ? 1 : 0;

@@ -1,0 +1,314 @@
+// Weight gradient of a 1x1 convolution on MFMA (gfx950), NHWC bf16, fp32 accumulate:
+//
+//   dW[co, ci] = sum_m dY[m, co] * X[m, ci]          (m = (n, h, w): K = N*H*W pixels)
+//
+// Not in the reference (LeNet has no 1x1 convs, /root/reference/cnn.py:10-16). Replaces MIOpen's
+// igemm_wrw kernels on ResNet-50's layer-1 1x1 convs (M = 3.2M pixels at 1024/GPU; 7 calls,
+// 2.6 ms/step with their zero-fill / cast passes, profiles/r3) — the last MIOpen kernels of the
+// ResNet-50 step, and the ones whose run-time compile dominated the fresh-box first step.
+//
+// These shapes are HBM-bound (a 64x256 wgrad reads 2 GB for 105 GFLOP), so the design goal is
+// one pass over dY and X at full bandwidth:
+//   * a workgroup owns the WHOLE channel block CO_B x CI_B (all of dW for layer-1 shapes) and a
+//     contiguous pixel range (split-K over pixels): every dY / X byte crosses HBM once; fp32
+//     partials per split are summed in a fixed order by conv1x1_wgrad_reduce_kernel
+//     (deterministic, no atomics);
+//   * a stage = 32 pixels of dY [32 x CO_B] and X [32 x CI_B] — contiguous global rows — staged
+//     by LDS-DMA (global_load_lds_dwordx4) through a 4-slot ring, issued 3 stages ahead, one
+//     s_barrier per stage, counted vmcnt so the DMA stays in flight across barriers;
+//   * both operands are pixel-major (K-strided); fragments come from LDS through the transposed
+//     read ds_read_b64_tr_b16 (4 pixel rows x 16 channels per 16-lane group, each lane receiving one
+//     channel's 4 pixels), as in conv3x3_wgrad.hip; rows XOR-swizzled (by permuting each lane's
+//     DMA SOURCE chunk — the DMA writes LDS linearly) so 4 consecutive rows hit 4 distinct 64-B
+//     bank groups;
+//   * waves tile the block as WCO x WCI of v_mfma_f32_32x32x16_bf16 32x32 accumulators.
+#include "../common.h"
+
+using namespace pdt;
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f16v __attribute__((ext_vector_type(16)));
+typedef short s4v __attribute__((ext_vector_type(4)));
+#define PDT_LDS __attribute__((address_space(3)))
+
+__device__ __attribute__((aligned(256))) uint4 g_wg1_zero[16];  // zero page for pixels past M (never written)
+
+constexpr int kKP = 32;     // pixels per stage
+constexpr int kSlots = 4;   // LDS ring
+constexpr int kAhead = 3;   // stages in flight
+
+template <int CO_B_, int CI_B_, int WCO_, int WCI_>
+struct W1Cfg {
+  static constexpr int CO_B = CO_B_, CI_B = CI_B_, WCO = WCO_, WCI = WCI_;
+  static constexpr int kWaves = (CO_B / WCO) * (CI_B / WCI), kThreads = kWaves * 64;
+  static constexpr int kRowY = CO_B * 2, kRowX = CI_B * 2;  // LDS row bytes
+  static constexpr int kYBytes = kKP * kRowY, kXBytes = kKP * kRowX, kSlot = kYBytes + kXBytes;
+  static constexpr int kLds = kSlots * kSlot;
+  static constexpr int kYLd = kYBytes / 1024 / kWaves, kXLd = kXBytes / 1024 / kWaves;  // DMA per wave per stage
+  static constexpr int kG = kYLd + kXLd;
+  static constexpr int kMI = WCO / 32, kNJ = WCI / 32;
+  static constexpr int kOcc = (160 * 1024) / kLds;  // workgroups per CU (LDS-limited)
+  static constexpr int kMinWaves = kOcc * kWaves / 4 < 1 ? 1 : (kOcc * kWaves / 4 > 4 ? 4 : kOcc * kWaves / 4);  // per SIMD
+  static_assert(kYLd * 1024 * kWaves == kYBytes && kXLd * 1024 * kWaves == kXBytes, "DMA split");
+  static_assert(kWaves <= 8 && kLds <= 160 * 1024, "workgroup");
+};
+
+// 16-B chunk swizzle: 4 consecutive rows of a transposed read on 4 distinct 64-B bank groups.
+// 128-B rows: rows r, r+1 are the two halves of a 256-B bank row, r+2, r+3 flip chunk bit 2;
+// >= 256-B rows: chunk bits 2-3 ^= row & 3. Both are involutions (used to permute DMA sources).
+template <int ROWB>
+__host__ __device__ __forceinline__ int swz(int row, int ch) {
+  if constexpr (ROWB == 128) return ch ^ (((row >> 1) & 1) << 2);
+  else return ch ^ ((row & 3) << 2);
+}
+template <int ROWB>
+__device__ __forceinline__ int chunk_off(int row, int ch) { return row * ROWB + (swz<ROWB>(row, ch) << 4); }
+
+__device__ __forceinline__ s4v tr_read(const char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((PDT_LDS s4v*)(p));
+}
+__device__ __forceinline__ bf16x8 cat2(s4v a, s4v b) {
+  typedef short s8 __attribute__((ext_vector_type(8)));
+  s8 r = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  return __builtin_bit_cast(bf16x8, r);
+}
+__device__ __forceinline__ void dma16(const void* src, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds(src, (PDT_LDS void*)lds_wave_base, 16, 0, 0);
+}
+// s_waitcnt vmcnt(N) leaving expcnt / lgkmcnt unconstrained (gfx9 simm16 encoding)
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+
+struct W1Geo {
+  int M, Ci, Co, ntiles, tiles_per_split, nsplit, nblk;
+};
+
+template <class Cf>
+__global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv1x1_wgrad_kernel(const uint16_t* __restrict__ X,
+                                                                               const uint16_t* __restrict__ dY,
+                                                                               float* __restrict__ ws, W1Geo g) {
+  constexpr int CO_B = Cf::CO_B, CI_B = Cf::CI_B, RY = Cf::kRowY, RX = Cf::kRowX;
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  // XCD-aware: consecutive logical ids (one split's channel blocks: same pixels) on one XCD
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = L / g.nblk, bt = L % g.nblk;
+  const int nci = g.Ci / CI_B;
+  const int co0 = (bt / nci) * CO_B, ci0 = (bt % nci) * CI_B;
+  const int t_begin = split * g.tiles_per_split;
+  const int S = min(g.ntiles, t_begin + g.tiles_per_split) - t_begin;
+
+  // per-lane DMA pieces (stage independent): row in the tile and element offset from its first pixel
+  int yrow[Cf::kYLd], yoff[Cf::kYLd], xrow[Cf::kXLd], xoff[Cf::kXLd];
+#pragma unroll
+  for (int i = 0; i < Cf::kYLd; ++i) {
+    const int o = (wid * Cf::kYLd + i) * 1024 + lane * 16, row = o / RY, slot = (o % RY) >> 4;
+    yrow[i] = row;
+    yoff[i] = row * g.Co + co0 + swz<RY>(row, slot) * 8;
+  }
+#pragma unroll
+  for (int i = 0; i < Cf::kXLd; ++i) {
+    const int o = (wid * Cf::kXLd + i) * 1024 + lane * 16, row = o / RX, slot = (o % RX) >> 4;
+    xrow[i] = row;
+    xoff[i] = row * g.Ci + ci0 + swz<RX>(row, slot) * 8;
+  }
+  auto issue = [&](int s) {
+    char* slot = lds + (s % kSlots) * Cf::kSlot;
+    const int p0 = (t_begin + s) * kKP;
+    const uint16_t* yb = dY + (int64_t)p0 * g.Co;
+    const uint16_t* xb = X + (int64_t)p0 * g.Ci;
+#pragma unroll
+    for (int i = 0; i < Cf::kYLd; ++i) {
+      const void* src = p0 + yrow[i] < g.M ? (const void*)(yb + yoff[i]) : (const void*)g_wg1_zero;
+      dma16(src, slot + (wid * Cf::kYLd + i) * 1024);
+    }
+#pragma unroll
+    for (int i = 0; i < Cf::kXLd; ++i) {
+      const void* src = p0 + xrow[i] < g.M ? (const void*)(xb + xoff[i]) : (const void*)g_wg1_zero;
+      dma16(src, slot + Cf::kYBytes + (wid * Cf::kXLd + i) * 1024);
+    }
+  };
+
+  // wave -> WCO x WCI block; lane roles of the transposed reads (see conv3x3_wgrad.hip)
+  constexpr int nwci = CI_B / Cf::WCI;
+  const int wco = wid / nwci, wci = wid % nwci;
+  const int grp = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int prow = 8 * (grp >> 1) + q;
+  const int half8 = (p & 1) * 8;
+  int ya[Cf::kMI], xa[Cf::kNJ];  // LDS byte offsets of this lane's pieces in row `prow`
+#pragma unroll
+  for (int i = 0; i < Cf::kMI; ++i) ya[i] = chunk_off<RY>(prow, (wco * Cf::WCO + 32 * i + 16 * (grp & 1) + 4 * p) >> 3) + half8;
+#pragma unroll
+  for (int j = 0; j < Cf::kNJ; ++j) xa[j] = chunk_off<RX>(prow, (wci * Cf::WCI + 32 * j + 16 * (grp & 1) + 4 * p) >> 3) + half8;
+  // rows prow + 4 and prow + 16 k: the swizzles depend on row bits 0-1 (>= 256-B rows) or bit 1
+  // (128-B rows), which adding 4 or 16 leaves alone -> constant offsets
+  f16v acc[Cf::kMI][Cf::kNJ];
+#pragma unroll
+  for (int i = 0; i < Cf::kMI; ++i)
+#pragma unroll
+    for (int j = 0; j < Cf::kNJ; ++j)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
+
+#pragma unroll
+  for (int s = 0; s < kAhead; ++s)
+    if (s < S) issue(s);
+  for (int s = 0; s < S; ++s) {
+    // this stage's DMA is complete once at most the later in-flight stages' remain outstanding
+    const int later = min(S - 1, s + kAhead - 1) - s;
+    if (later >= 2) wait_vm<2 * Cf::kG>();
+    else if (later == 1) wait_vm<Cf::kG>();
+    else wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (s + kAhead < S) issue(s + kAhead);  // its slot was last read at stage s - 1: every wave is past it
+    const char* ys = lds + (s % kSlots) * Cf::kSlot;
+    const char* xs = ys + Cf::kYBytes;
+#pragma unroll
+    for (int kk = 0; kk < kKP / 16; ++kk) {
+      bf16x8 a[Cf::kMI], b[Cf::kNJ];
+#pragma unroll
+      for (int i = 0; i < Cf::kMI; ++i) {
+        const char* pp = ys + ya[i] + kk * 16 * RY;
+        a[i] = cat2(tr_read(pp), tr_read(pp + 4 * RY));
+      }
+#pragma unroll
+      for (int j = 0; j < Cf::kNJ; ++j) {
+        const char* pp = xs + xa[j] + kk * 16 * RX;
+        b[j] = cat2(tr_read(pp), tr_read(pp + 4 * RX));
+      }
+#pragma unroll
+      for (int i = 0; i < Cf::kMI; ++i)
+#pragma unroll
+        for (int j = 0; j < Cf::kNJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);  // D[co][ci]
+    }
+  }
+  // partials ws[split][co][ci]; 32x32 accumulator: lane holds ci = l % 32,
+  // co = 8 (v / 4) + 4 (l / 32) + v % 4 for v = 0..15
+  float* wsp = ws + (int64_t)split * g.Co * g.Ci;
+#pragma unroll
+  for (int i = 0; i < Cf::kMI; ++i)
+#pragma unroll
+    for (int j = 0; j < Cf::kNJ; ++j) {
+      const int ci = ci0 + wci * Cf::WCI + 32 * j + (lane & 31);
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const int co = co0 + wco * Cf::WCO + 32 * i + 8 * (v >> 2) + 4 * (lane >> 5) + (v & 3);
+        wsp[(int64_t)co * g.Ci + ci] = acc[i][j][v];
+      }
+    }
+}
+
+// dw[co][ci] (bf16) = sum over splits in a fixed order
+__global__ __launch_bounds__(256) void conv1x1_wgrad_reduce_kernel(const float* __restrict__ ws,
+                                                                   uint16_t* __restrict__ dw, int nsplit, int64_t n4) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int k = 0; k < nsplit; ++k) {
+      const float4 v = reinterpret_cast<const float4*>(ws + (int64_t)k * n4 * 4)[i];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    const uint32_t lo = (uint32_t)f2bf(s.x) | ((uint32_t)f2bf(s.y) << 16);
+    const uint32_t hi = (uint32_t)f2bf(s.z) | ((uint32_t)f2bf(s.w) << 16);
+    reinterpret_cast<uint2*>(dw)[i] = make_uint2(lo, hi);
+  }
+}
+
+// Channel-block configurations (the block covers all of dW for ResNet-50's layer-1 shapes)
+using C64x64 = W1Cfg<64, 64, 32, 32>;     // 4 waves, 32 KB LDS
+using C256x64 = W1Cfg<256, 64, 64, 64>;   // 4 waves, 80 KB
+using C64x256 = W1Cfg<64, 256, 64, 64>;   // 4 waves, 80 KB
+using C128x256 = W1Cfg<128, 256, 64, 64>; // 8 waves, 96 KB
+
+enum class Blk { k64x64, k256x64, k64x256, k128x256 };
+
+inline Blk pick_block(int Co, int Ci) {
+  if (Co % 128 == 0 && Ci % 256 == 0) return Blk::k128x256;
+  if (Co % 256 == 0 && Ci % 64 == 0) return Blk::k256x64;
+  if (Co % 64 == 0 && Ci % 256 == 0) return Blk::k64x256;
+  return Blk::k64x64;
+}
+
+inline void block_dims(Blk b, int& cob, int& cib, int& occ) {
+  switch (b) {
+    case Blk::k128x256: cob = 128; cib = 256; occ = C128x256::kOcc; break;
+    case Blk::k256x64: cob = 256; cib = 64; occ = C256x64::kOcc; break;
+    case Blk::k64x256: cob = 64; cib = 256; occ = C64x256::kOcc; break;
+    default: cob = 64; cib = 64; occ = C64x64::kOcc; break;
+  }
+}
+
+int g_target_wgs = 0;  // 0: occupancy x 256 CUs
+
+inline bool geo_of(int M, int Ci, int Co, W1Geo& g) {
+  if (M < 1 || Ci % 64 != 0 || Co % 64 != 0) return false;
+  int cob, cib, occ;
+  block_dims(pick_block(Co, Ci), cob, cib, occ);
+  g.M = M; g.Ci = Ci; g.Co = Co;
+  g.ntiles = (M + kKP - 1) / kKP;
+  g.nblk = (Co / cob) * (Ci / cib);
+  const int target = g_target_wgs > 0 ? g_target_wgs : occ * 256;
+  int ns = (target + g.nblk - 1) / g.nblk;
+  if (ns > g.ntiles) ns = g.ntiles;
+  if (ns < 1) ns = 1;
+  g.tiles_per_split = (g.ntiles + ns - 1) / ns;
+  g.nsplit = (g.ntiles + g.tiles_per_split - 1) / g.tiles_per_split;
+  return true;
+}
+
+template <class Cf>
+int launch(const uint16_t* x, const uint16_t* dy, uint16_t* dw, float* ws, const W1Geo& g, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&conv1x1_wgrad_kernel<Cf>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, Cf::kLds) != hipSuccess)
+      return -3;
+    attr = true;
+  }
+  hipLaunchKernelGGL(conv1x1_wgrad_kernel<Cf>, dim3(g.nsplit * g.nblk), dim3(Cf::kThreads), Cf::kLds, s, x, dy, ws, g);
+  const int64_t n4 = (int64_t)g.Co * g.Ci / 4;
+  const int grid = (int)((n4 + 255) / 256 < 1024 ? (n4 + 255) / 256 : 1024);
+  hipLaunchKernelGGL(conv1x1_wgrad_reduce_kernel, dim3(grid), dim3(256), 0, s, ws, dw, g.nsplit, n4);
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+// fp32 workspace floats for pdt_conv1x1_wgrad at this shape (0: unsupported shape).
+int64_t pdt_conv1x1_wgrad_ws_floats(int M, int Ci, int Co, int* nsplit_out) {
+  W1Geo g;
+  if (!geo_of(M, Ci, Co, g)) return 0;
+  if (nsplit_out) *nsplit_out = g.nsplit;
+  return (int64_t)g.nsplit * Co * Ci;
+}
+
+// dw[Co, Ci] (bf16) = dy[M, Co]^T x[M, Ci] (row-major bf16: the NHWC views of a stride-1 1x1 conv's
+// output gradient and input). ws: pdt_conv1x1_wgrad_ws_floats() floats. Ci, Co % 64 == 0,
+// M * max(Ci, Co) < 2^31. Returns 0, or < 0 for an unsupported shape (caller falls back).
+int pdt_conv1x1_wgrad(const uint16_t* x, const uint16_t* dy, uint16_t* dw, float* ws, int M, int Ci, int Co,
+                      hipStream_t s) {
+  if ((int64_t)M * (Ci > Co ? Ci : Co) >= ((int64_t)1 << 31)) return -2;
+  W1Geo g;
+  if (!geo_of(M, Ci, Co, g)) return -1;
+  switch (pick_block(Co, Ci)) {
+    case Blk::k128x256: return launch<C128x256>(x, dy, dw, ws, g, s);
+    case Blk::k256x64: return launch<C256x64>(x, dy, dw, ws, g, s);
+    case Blk::k64x256: return launch<C64x256>(x, dy, dw, ws, g, s);
+    default: return launch<C64x64>(x, dy, dw, ws, g, s);
+  }
+}
+
+// Tuning hook (tools/conv1x1_wgrad_bench.py): target workgroups (0 = occupancy x 256 CUs).
+void pdt_conv1x1_wgrad_tune(int target_wgs) {
+  if (target_wgs >= 0) g_target_wgs = target_wgs;
+}
+
+}  // extern "C"

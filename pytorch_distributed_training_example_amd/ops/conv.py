@@ -92,9 +92,10 @@ def _ensure_table() -> None:
 
 
 def _ours_ok(direction: str, M: int, K: int, N: int) -> bool:
-    """Stride-1 1x1 conv direction on our MFMA GEMM (csrc/kernels/conv1x1.hip): ``fwd`` (with the
-    consuming BatchNorm's statistics in the epilogue) or ``dgrad`` (shortcut gradient accumulated
-    in place), if listed in ``PDT_CONV1X1_OURS`` (config.SW)."""
+    """Stride-1 1x1 conv direction on our MFMA kernels: ``fwd`` (csrc/kernels/conv1x1.hip, with the
+    consuming BatchNorm's statistics in the epilogue), ``dgrad`` (same GEMM, shortcut gradient
+    accumulated in place) or ``wgrad`` (conv1x1_wgrad.hip; K = Ci, N = Co), if listed in
+    ``PDT_CONV1X1_OURS`` (config.SW)."""
     return (direction in SW.conv1x1_ours and K % 32 == 0 and N % 64 == 0
             and M * max(K, N) < 2 ** 31 and SW.conv1x1 in ("auto", "ours"))
 
@@ -300,11 +301,17 @@ class _Conv1x1Fn(torch.autograd.Function):
             for sk in _SPLITK if splitk_on else ():
                 if M % sk == 0 and M // sk >= 256:
                     cands[f"splitk{sk}"] = (lambda sk=sk: _wgrad_splitk(g2, x2, sk))
+            if x.dtype == torch.bfloat16 and _ours_ok("wgrad", M, Ci, Co) and Ci % 64 == 0:
+                from ._native import native
+                # csrc/kernels/conv1x1_wgrad.hip: one HBM pass over dY and X (split-K over pixels)
+                cands["ours"] = lambda: native().conv1x1_wgrad(x2, g2)
             key = ("bwd_weight", _dtype_name(x), M, Ci, Co)
             algo = "miopen" if not splitk_on and str(_CHOICE.get(key, "")).startswith("splitk") else _pick(key, cands)
             # a 1x1 kernel has the same element order in NCHW and NHWC: keep weight's strides
             if algo == "gemm":
                 wfn = lambda: torch.mm(g2.t(), x2).as_strided(weight.shape, weight.stride())  # noqa: E731
+            elif algo == "ours":
+                wfn = lambda: cands["ours"]().as_strided(weight.shape, weight.stride())  # noqa: E731
             elif algo.startswith("splitk"):
                 sk = int(algo[6:])
                 wfn = lambda: _wgrad_splitk(g2, x2, sk).as_strided(weight.shape, weight.stride())  # noqa: E731
