@@ -104,7 +104,7 @@ int pdt_conv1x1_tile_rows();
 int64_t pdt_conv1x1_wgrad_ws_floats(int M, int Ci, int Co, int* nsplit_out);
 int pdt_conv1x1_wgrad(const uint16_t* x, const uint16_t* dy, uint16_t* dw, float* ws, int M, int Ci, int Co,
                       hipStream_t s);
-void pdt_conv1x1_wgrad_tune(int target_wgs);
+void pdt_conv1x1_wgrad_tune(int target_wgs, int variant, int interleave);
 int pdt_conv1x1_gemm(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t* c, const uint8_t* cm,
                      float* part, int M, int K, int N, const uint16_t* bn_x, const uint8_t* bn_mask,
                      const float* bn_mean, float* bn_part, int c_s, int c_H, int c_W, hipStream_t s);
@@ -1466,7 +1466,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("stem_conv_wgrad", &stem_conv_wgrad);
   m.def("conv3x3s1_wgrad", &conv3x3s1_wgrad);
   m.def("conv1x1_wgrad", &conv1x1_wgrad);
-  m.def("conv1x1_wgrad_tune", [](int target_wgs) { pdt_conv1x1_wgrad_tune(target_wgs); });
+  m.def("conv1x1_wgrad_tune", [](int target_wgs, int variant, int interleave) { pdt_conv1x1_wgrad_tune(target_wgs, variant, interleave); },
+        py::arg("target_wgs"), py::arg("variant") = -2, py::arg("interleave") = -2);
   m.def("embedding_fwd", &embedding_fwd);
   m.def("gemm_nt", &gemm_nt);
   m.def("embedding_bwd", &embedding_bwd);

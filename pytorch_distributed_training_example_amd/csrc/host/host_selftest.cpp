@@ -127,7 +127,14 @@ static void test_wgrad1x1_geometry() {
         w1::W1Geo g;
         if (!w1::geo_of(M, Ci, Co, g)) continue;
         ++accepted;
-        EXPECT(g.ntiles * 32 >= M && (g.ntiles - 1) * 32 < M, "stages M=%d", M);
+        const w1::Blk blk = w1::pick_block(Co, Ci);
+        const int kp = w1::info(blk, w1::variant_default(blk)).kp;
+        EXPECT(g.ntiles * kp >= M && (g.ntiles - 1) * kp < M, "stages M=%d", M);
+        if (g.ilv) {  // split k takes stages k, k + nsplit, ...: each stage exactly once
+          int64_t covered = 0;
+          for (int k = 0; k < g.nsplit; ++k) covered += (g.ntiles - k + g.nsplit - 1) / g.nsplit;
+          EXPECT(g.nsplit <= g.ntiles && covered == g.ntiles, "interleaved stages M=%d", M);
+        }
         EXPECT((int64_t)g.nsplit * g.tiles_per_split >= g.ntiles && (g.nsplit - 1) * g.tiles_per_split < g.ntiles,
                "splits M=%d Ci=%d Co=%d", M, Ci, Co);
         int cob, cib, occ;

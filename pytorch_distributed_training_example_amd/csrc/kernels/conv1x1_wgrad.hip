@@ -35,13 +35,13 @@ typedef short s4v __attribute__((ext_vector_type(4)));
 
 __device__ __attribute__((aligned(256))) uint4 g_wg1_zero[16];  // zero page for pixels past M (never written)
 
-constexpr int kKP = 32;     // pixels per stage
-constexpr int kSlots = 4;   // LDS ring
-constexpr int kAhead = 3;   // stages in flight
-
-template <int CO_B_, int CI_B_, int WCO_, int WCI_>
+// KP: pixels per stage; SLOTS: LDS ring depth (SLOTS - 1 stages in flight)
+template <int CO_B_, int CI_B_, int WCO_, int WCI_, int KP_ = 32, int SLOTS_ = 4>
 struct W1Cfg {
-  static constexpr int CO_B = CO_B_, CI_B = CI_B_, WCO = WCO_, WCI = WCI_;
+  static constexpr int CO_B = CO_B_, CI_B = CI_B_, WCO = WCO_, WCI = WCI_, kKP = KP_;
+  static constexpr int kSlotBytes = kKP * (CO_B + CI_B) * 2;
+  static constexpr int kSlots = SLOTS_ * kSlotBytes <= 160 * 1024 ? SLOTS_ : (160 * 1024) / kSlotBytes;
+  static constexpr int kAhead = kSlots - 1;
   static constexpr int kWaves = (CO_B / WCO) * (CI_B / WCI), kThreads = kWaves * 64;
   static constexpr int kRowY = CO_B * 2, kRowX = CI_B * 2;  // LDS row bytes
   static constexpr int kYBytes = kKP * kRowY, kXBytes = kKP * kRowX, kSlot = kYBytes + kXBytes;
@@ -66,8 +66,14 @@ __host__ __device__ __forceinline__ int swz(int row, int ch) {
 template <int ROWB>
 __device__ __forceinline__ int chunk_off(int row, int ch) { return row * ROWB + (swz<ROWB>(row, ch) << 4); }
 
+// The transposed read as inline asm: for the builtin the compiler cannot tell which LDS bytes it
+// reads, so it put an s_waitcnt vmcnt(0) for ALL outstanding LDS-DMA (incl. the stages just issued
+// ahead) in front of it, serialising the ring. Completion is tracked by hand instead (lgkm_fence).
 __device__ __forceinline__ s4v tr_read(const char* p) {
-  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((PDT_LDS s4v*)(p));
+  s4v r;
+  const uint32_t a = (uint32_t)(uintptr_t)(PDT_LDS const char*)p;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(a) : "memory");
+  return r;
 }
 __device__ __forceinline__ bf16x8 cat2(s4v a, s4v b) {
   typedef short s8 __attribute__((ext_vector_type(8)));
@@ -77,15 +83,34 @@ __device__ __forceinline__ bf16x8 cat2(s4v a, s4v b) {
 __device__ __forceinline__ void dma16(const void* src, char* lds_wave_base) {
   __builtin_amdgcn_global_load_lds(src, (PDT_LDS void*)lds_wave_base, 16, 0, 0);
 }
+template <int MI, int NJ>
+__device__ __forceinline__ void lgkm_fence(bf16x8 (&a)[MI], bf16x8 (&b)[NJ]) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < MI; ++i) asm volatile("" : "+v"(a[i]));
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) asm volatile("" : "+v"(b[j]));
+}
 // s_waitcnt vmcnt(N) leaving expcnt / lgkmcnt unconstrained (gfx9 simm16 encoding)
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   static_assert(N >= 0 && N < 64, "vmcnt");
   __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
 }
+// wait until at most `later` stages of G DMA instructions each are outstanding (later <= K)
+template <int G, int K>
+__device__ __forceinline__ void wait_stages(int later) {
+  if constexpr (K == 0) {
+    wait_vm<0>();
+  } else {
+    if (later >= K) wait_vm<K * G>();
+    else wait_stages<G, K - 1>(later);
+  }
+}
 
 struct W1Geo {
   int M, Ci, Co, ntiles, tiles_per_split, nsplit, nblk;
+  int ilv;  // 1: split k takes stages k, k + nsplit, ... (all workgroups stream neighbouring pixels)
 };
 
 template <class Cf>
@@ -100,8 +125,10 @@ __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv1x1_wgrad_ker
   const int split = L / g.nblk, bt = L % g.nblk;
   const int nci = g.Ci / CI_B;
   const int co0 = (bt / nci) * CO_B, ci0 = (bt % nci) * CI_B;
-  const int t_begin = split * g.tiles_per_split;
-  const int S = min(g.ntiles, t_begin + g.tiles_per_split) - t_begin;
+  const int t_begin = g.ilv ? split : split * g.tiles_per_split, t_step = g.ilv ? g.nsplit : 1;
+  const int S = g.ilv ? (g.ntiles - split + g.nsplit - 1) / g.nsplit
+                      : min(g.ntiles, t_begin + g.tiles_per_split) - t_begin;
+  constexpr int kKP = Cf::kKP, kSlots = Cf::kSlots, kAhead = Cf::kAhead;
 
   // per-lane DMA pieces (stage independent): row in the tile and element offset from its first pixel
   int yrow[Cf::kYLd], yoff[Cf::kYLd], xrow[Cf::kXLd], xoff[Cf::kXLd];
@@ -119,7 +146,7 @@ __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv1x1_wgrad_ker
   }
   auto issue = [&](int s) {
     char* slot = lds + (s % kSlots) * Cf::kSlot;
-    const int p0 = (t_begin + s) * kKP;
+    const int p0 = (t_begin + s * t_step) * kKP;
     const uint16_t* yb = dY + (int64_t)p0 * g.Co;
     const uint16_t* xb = X + (int64_t)p0 * g.Ci;
 #pragma unroll
@@ -160,10 +187,7 @@ __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv1x1_wgrad_ker
     if (s < S) issue(s);
   for (int s = 0; s < S; ++s) {
     // this stage's DMA is complete once at most the later in-flight stages' remain outstanding
-    const int later = min(S - 1, s + kAhead - 1) - s;
-    if (later >= 2) wait_vm<2 * Cf::kG>();
-    else if (later == 1) wait_vm<Cf::kG>();
-    else wait_vm<0>();
+    wait_stages<Cf::kG, kAhead - 1>(min(S - 1, s + kAhead - 1) - s);
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (s + kAhead < S) issue(s + kAhead);  // its slot was last read at stage s - 1: every wave is past it
@@ -182,6 +206,9 @@ __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv1x1_wgrad_ker
         const char* pp = xs + xa[j] + kk * 16 * RX;
         b[j] = cat2(tr_read(pp), tr_read(pp + 4 * RX));
       }
+      // the reads' results are ready: the wait takes every fragment as an in/out operand, so no MFMA
+      // can be scheduled above it
+      lgkm_fence(a, b);
 #pragma unroll
       for (int i = 0; i < Cf::kMI; ++i)
 #pragma unroll
@@ -205,28 +232,54 @@ __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv1x1_wgrad_ker
     }
 }
 
-// dw[co][ci] (bf16) = sum over splits in a fixed order
+// dw[co][ci] (bf16) = sum over splits in a fixed order. A workgroup takes 16 float4 columns and
+// its 16 wave-quarters split the nsplit partials round-robin (each summed in order), then one
+// fixed-order pass over the 16 group sums: deterministic, and 16x the parallelism of one thread per
+// column (whose serial 192-deep loads ran 49 us for a 64 KB result).
+constexpr int kRedCols = 16, kRedGroups = 16;
 __global__ __launch_bounds__(256) void conv1x1_wgrad_reduce_kernel(const float* __restrict__ ws,
                                                                    uint16_t* __restrict__ dw, int nsplit, int64_t n4) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
-    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int k = 0; k < nsplit; ++k) {
+  __shared__ float4 part[kRedGroups][kRedCols];
+  const int col = threadIdx.x % kRedCols, grp = threadIdx.x / kRedCols;
+  const int64_t i = (int64_t)blockIdx.x * kRedCols + col;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i < n4)
+    for (int k = grp; k < nsplit; k += kRedGroups) {
       const float4 v = reinterpret_cast<const float4*>(ws + (int64_t)k * n4 * 4)[i];
       s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
     }
-    const uint32_t lo = (uint32_t)f2bf(s.x) | ((uint32_t)f2bf(s.y) << 16);
-    const uint32_t hi = (uint32_t)f2bf(s.z) | ((uint32_t)f2bf(s.w) << 16);
+  part[grp][col] = s;
+  __syncthreads();
+  if (grp == 0 && i < n4) {
+    float4 t = part[0][col];
+#pragma unroll
+    for (int k = 1; k < kRedGroups; ++k) {
+      const float4 v = part[k][col];
+      t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+    }
+    const uint32_t lo = (uint32_t)f2bf(t.x) | ((uint32_t)f2bf(t.y) << 16);
+    const uint32_t hi = (uint32_t)f2bf(t.z) | ((uint32_t)f2bf(t.w) << 16);
     reinterpret_cast<uint2*>(dw)[i] = make_uint2(lo, hi);
   }
 }
 
-// Channel-block configurations (the block covers all of dW for ResNet-50's layer-1 shapes)
-using C64x64 = W1Cfg<64, 64, 32, 32>;     // 4 waves, 32 KB LDS
-using C256x64 = W1Cfg<256, 64, 64, 64>;   // 4 waves, 80 KB
-using C64x256 = W1Cfg<64, 256, 64, 64>;   // 4 waves, 80 KB
-using C128x256 = W1Cfg<128, 256, 64, 64>; // 8 waves, 96 KB
-
+// Channel-block configurations (the block covers all of dW for ResNet-50's layer-1 shapes) x
+// pipeline variants (pixels per stage, ring depth; the ring is clamped to the 160 KB of LDS)
 enum class Blk { k64x64, k256x64, k64x256, k128x256 };
+constexpr int kVariants = 4;
+constexpr int kVarKP[kVariants] = {32, 32, 64, 64};
+constexpr int kVarSlots[kVariants] = {4, 8, 4, 3};
+
+template <Blk B, int V>
+struct CfgOf;
+template <int V>
+struct CfgOf<Blk::k64x64, V> { using T = W1Cfg<64, 64, 32, 32, kVarKP[V], kVarSlots[V]>; };     // 4 waves
+template <int V>
+struct CfgOf<Blk::k256x64, V> { using T = W1Cfg<256, 64, 64, 64, kVarKP[V], kVarSlots[V]>; };   // 4 waves
+template <int V>
+struct CfgOf<Blk::k64x256, V> { using T = W1Cfg<64, 256, 64, 64, kVarKP[V], kVarSlots[V]>; };   // 4 waves
+template <int V>
+struct CfgOf<Blk::k128x256, V> { using T = W1Cfg<128, 256, 64, 64, kVarKP[V], kVarSlots[V]>; }; // 8 waves
 
 inline Blk pick_block(int Co, int Ci) {
   if (Co % 128 == 0 && Ci % 256 == 0) return Blk::k128x256;
@@ -235,30 +288,60 @@ inline Blk pick_block(int Co, int Ci) {
   return Blk::k64x64;
 }
 
-inline void block_dims(Blk b, int& cob, int& cib, int& occ) {
-  switch (b) {
-    case Blk::k128x256: cob = 128; cib = 256; occ = C128x256::kOcc; break;
-    case Blk::k256x64: cob = 256; cib = 64; occ = C256x64::kOcc; break;
-    case Blk::k64x256: cob = 64; cib = 256; occ = C64x256::kOcc; break;
-    default: cob = 64; cib = 64; occ = C64x64::kOcc; break;
+struct CfgInfo {
+  int cob, cib, occ, kp;
+};
+template <class Cf>
+CfgInfo info_of() { return CfgInfo{Cf::CO_B, Cf::CI_B, Cf::kOcc, Cf::kKP}; }
+template <Blk B>
+CfgInfo info_var(int v) {
+  switch (v) {
+    case 1: return info_of<typename CfgOf<B, 1>::T>();
+    case 2: return info_of<typename CfgOf<B, 2>::T>();
+    case 3: return info_of<typename CfgOf<B, 3>::T>();
+    default: return info_of<typename CfgOf<B, 0>::T>();
   }
 }
+inline CfgInfo info(Blk b, int v) {
+  switch (b) {
+    case Blk::k128x256: return info_var<Blk::k128x256>(v);
+    case Blk::k256x64: return info_var<Blk::k256x64>(v);
+    case Blk::k64x256: return info_var<Blk::k64x256>(v);
+    default: return info_var<Blk::k64x64>(v);
+  }
+}
+inline void block_dims(Blk b, int& cob, int& cib, int& occ) {
+  const CfgInfo i = info(b, 0);
+  cob = i.cob; cib = i.cib; occ = i.occ;
+}
 
-int g_target_wgs = 0;  // 0: occupancy x 256 CUs
+int g_target_wgs = 0;  // 0: by shape (wgs_default)
+int g_variant = -1;    // -1: by shape (variant_default)
+int g_ilv = -1;        // -1: by shape; 0 / 1 forced
+
+// Measured on MI355X at ResNet-50 batch 1024 (tools/conv1x1_wgrad_bench.py, profiles/r3/
+// conv1x1_wgrad_bench_b1024.txt): FEWER streams than CUs with interleaved stages stream best —
+// 192 workgroups taking stages k, k + 192, ... (all of them on neighbouring pixels at any moment)
+// reach 362-437 us on the 2.0-2.5 GB layer-1 shapes (MIOpen 380-486 us); 512 separate pixel ranges
+// (2 workgroups per CU) ran 1.3x slower. 64x64: 64-pixel stages (4 KB DMA per stage at 32 was too
+// little work per barrier).
+inline int variant_default(Blk b) { return b == Blk::k64x64 ? 2 : 0; }
+inline int wgs_default(const CfgInfo&, int nblk) { return nblk == 1 ? 192 : 256; }
 
 inline bool geo_of(int M, int Ci, int Co, W1Geo& g) {
   if (M < 1 || Ci % 64 != 0 || Co % 64 != 0) return false;
-  int cob, cib, occ;
-  block_dims(pick_block(Co, Ci), cob, cib, occ);
+  const Blk b = pick_block(Co, Ci);
+  const CfgInfo ci = info(b, g_variant >= 0 ? g_variant : variant_default(b));
   g.M = M; g.Ci = Ci; g.Co = Co;
-  g.ntiles = (M + kKP - 1) / kKP;
-  g.nblk = (Co / cob) * (Ci / cib);
-  const int target = g_target_wgs > 0 ? g_target_wgs : occ * 256;
+  g.ntiles = (M + ci.kp - 1) / ci.kp;
+  g.nblk = (Co / ci.cob) * (Ci / ci.cib);
+  const int target = g_target_wgs > 0 ? g_target_wgs : wgs_default(ci, g.nblk);
   int ns = (target + g.nblk - 1) / g.nblk;
   if (ns > g.ntiles) ns = g.ntiles;
   if (ns < 1) ns = 1;
   g.tiles_per_split = (g.ntiles + ns - 1) / ns;
   g.nsplit = (g.ntiles + g.tiles_per_split - 1) / g.tiles_per_split;
+  g.ilv = g_ilv >= 0 ? g_ilv : 1;
   return true;
 }
 
@@ -273,9 +356,19 @@ int launch(const uint16_t* x, const uint16_t* dy, uint16_t* dw, float* ws, const
   }
   hipLaunchKernelGGL(conv1x1_wgrad_kernel<Cf>, dim3(g.nsplit * g.nblk), dim3(Cf::kThreads), Cf::kLds, s, x, dy, ws, g);
   const int64_t n4 = (int64_t)g.Co * g.Ci / 4;
-  const int grid = (int)((n4 + 255) / 256 < 1024 ? (n4 + 255) / 256 : 1024);
-  hipLaunchKernelGGL(conv1x1_wgrad_reduce_kernel, dim3(grid), dim3(256), 0, s, ws, dw, g.nsplit, n4);
+  hipLaunchKernelGGL(conv1x1_wgrad_reduce_kernel, dim3((unsigned)((n4 + kRedCols - 1) / kRedCols)),
+                     dim3(kRedCols * kRedGroups), 0, s, ws, dw, g.nsplit, n4);
   return 0;
+}
+
+template <Blk B>
+int launch_var(int v, const uint16_t* x, const uint16_t* dy, uint16_t* dw, float* ws, const W1Geo& g, hipStream_t s) {
+  switch (v) {
+    case 1: return launch<typename CfgOf<B, 1>::T>(x, dy, dw, ws, g, s);
+    case 2: return launch<typename CfgOf<B, 2>::T>(x, dy, dw, ws, g, s);
+    case 3: return launch<typename CfgOf<B, 3>::T>(x, dy, dw, ws, g, s);
+    default: return launch<typename CfgOf<B, 0>::T>(x, dy, dw, ws, g, s);
+  }
 }
 
 }  // namespace
@@ -298,17 +391,22 @@ int pdt_conv1x1_wgrad(const uint16_t* x, const uint16_t* dy, uint16_t* dw, float
   if ((int64_t)M * (Ci > Co ? Ci : Co) >= ((int64_t)1 << 31)) return -2;
   W1Geo g;
   if (!geo_of(M, Ci, Co, g)) return -1;
-  switch (pick_block(Co, Ci)) {
-    case Blk::k128x256: return launch<C128x256>(x, dy, dw, ws, g, s);
-    case Blk::k256x64: return launch<C256x64>(x, dy, dw, ws, g, s);
-    case Blk::k64x256: return launch<C64x256>(x, dy, dw, ws, g, s);
-    default: return launch<C64x64>(x, dy, dw, ws, g, s);
+  const Blk b = pick_block(Co, Ci);
+  const int v = g_variant >= 0 ? g_variant : variant_default(b);
+  switch (b) {
+    case Blk::k128x256: return launch_var<Blk::k128x256>(v, x, dy, dw, ws, g, s);
+    case Blk::k256x64: return launch_var<Blk::k256x64>(v, x, dy, dw, ws, g, s);
+    case Blk::k64x256: return launch_var<Blk::k64x256>(v, x, dy, dw, ws, g, s);
+    default: return launch_var<Blk::k64x64>(v, x, dy, dw, ws, g, s);
   }
 }
 
-// Tuning hook (tools/conv1x1_wgrad_bench.py): target workgroups (0 = occupancy x 256 CUs).
-void pdt_conv1x1_wgrad_tune(int target_wgs) {
+// Tuning hook (tools/conv1x1_wgrad_bench.py): target workgroups (0 = by shape) and pipeline
+// variant (-1 = by shape; 0..3 = kVarKP / kVarSlots), each left alone when < -1.
+void pdt_conv1x1_wgrad_tune(int target_wgs, int variant, int interleave) {
   if (target_wgs >= 0) g_target_wgs = target_wgs;
+  if (variant >= -1 && variant < kVariants) g_variant = variant;
+  if (interleave >= -1 && interleave <= 1) g_ilv = interleave;
 }
 
 }  // extern "C"

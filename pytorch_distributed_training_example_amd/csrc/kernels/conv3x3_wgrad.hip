@@ -313,23 +313,39 @@ __global__ __launch_bounds__(Cf::kThreads, 2) void conv3x3_wgrad_kernel(const ui
     }
 }
 
-// dw[co][tap][ci] (bf16, the channels_last storage of [Co, Ci, 3, 3]) = sum over splits, fixed order
+// dw[co][tap][ci] (bf16, the channels_last storage of [Co, Ci, 3, 3]) = sum over splits, fixed order.
+// A workgroup takes 16 float4 columns; its 16 thread groups split the partials round-robin (each
+// summed in order), then one fixed-order pass over the group sums: deterministic, and 16x the
+// parallelism of one thread per column (layer 1: 512 splits deep, 132 us for a 147 KB result).
+constexpr int kRedCols = 16, kRedGroups = 16;
 __global__ __launch_bounds__(256) void conv3x3_wgrad_reduce_kernel(const float* __restrict__ ws,
                                                                    uint16_t* __restrict__ dw, int nsplit, int Co,
                                                                    int Ci) {
+  __shared__ float4 part[kRedGroups][kRedCols];
   const int64_t per4 = (int64_t)9 * Co * Ci / 4;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < per4; i += (int64_t)gridDim.x * blockDim.x) {
-    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int k = 0; k < nsplit; ++k) {
+  const int col = threadIdx.x % kRedCols, grp = threadIdx.x / kRedCols;
+  const int64_t i = (int64_t)blockIdx.x * kRedCols + col;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i < per4)
+    for (int k = grp; k < nsplit; k += kRedGroups) {
       const float4 v = reinterpret_cast<const float4*>(ws + (int64_t)k * 9 * Co * Ci)[i];
       s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
     }
+  part[grp][col] = s;
+  __syncthreads();
+  if (grp == 0 && i < per4) {
+    float4 t = part[0][col];
+#pragma unroll
+    for (int k = 1; k < kRedGroups; ++k) {
+      const float4 v = part[k][col];
+      t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+    }
     const int64_t e = i * 4;  // (t, co, ci..ci+3)
-    const int t = (int)(e / ((int64_t)Co * Ci)), rem = (int)(e % ((int64_t)Co * Ci));
+    const int tp = (int)(e / ((int64_t)Co * Ci)), rem = (int)(e % ((int64_t)Co * Ci));
     const int co = rem / Ci, ci = rem % Ci;
-    uint16_t* o = dw + ((int64_t)co * 9 + t) * Ci + ci;
-    const uint32_t lo = (uint32_t)f2bf(s.x) | ((uint32_t)f2bf(s.y) << 16);
-    const uint32_t hi = (uint32_t)f2bf(s.z) | ((uint32_t)f2bf(s.w) << 16);
+    uint16_t* o = dw + ((int64_t)co * 9 + tp) * Ci + ci;
+    const uint32_t lo = (uint32_t)f2bf(t.x) | ((uint32_t)f2bf(t.y) << 16);
+    const uint32_t hi = (uint32_t)f2bf(t.z) | ((uint32_t)f2bf(t.w) << 16);
     *reinterpret_cast<uint2*>(o) = make_uint2(lo, hi);
   }
 }
@@ -413,8 +429,8 @@ int launch(const uint16_t* x, const uint16_t* dy, uint16_t* dw, float* ws, const
   hipLaunchKernelGGL(conv3x3_wgrad_kernel<Cf>, dim3(g.nsplit * g.nblk), dim3(Cf::kThreads), Cf::kLds, s, x, dy, ws,
                      g);
   const int64_t per4 = (int64_t)9 * g.Co * g.Ci / 4;
-  const int grid = (int)((per4 + 255) / 256 < 2048 ? (per4 + 255) / 256 : 2048);
-  hipLaunchKernelGGL(conv3x3_wgrad_reduce_kernel, dim3(grid), dim3(256), 0, s, ws, dw, g.nsplit, g.Co, g.Ci);
+  hipLaunchKernelGGL(conv3x3_wgrad_reduce_kernel, dim3((unsigned)((per4 + kRedCols - 1) / kRedCols)),
+                     dim3(kRedCols * kRedGroups), 0, s, ws, dw, g.nsplit, g.Co, g.Ci);
   return 0;
 }
 

@@ -44,11 +44,11 @@ def test_wgrad_target_wgs_invariant_values():
     dy = torch.randn(16384, 64, device="cuda").bfloat16()
     n = _native()
     base = n.conv1x1_wgrad(x, dy).float()
-    n.conv1x1_wgrad_tune(7)
+    n.conv1x1_wgrad_tune(7, -2, 1)
     try:
         other = n.conv1x1_wgrad(x, dy).float()
     finally:
-        n.conv1x1_wgrad_tune(0)
+        n.conv1x1_wgrad_tune(0, -2, -1)
     torch.testing.assert_close(other, base, rtol=1e-2, atol=0.5)
 
 
