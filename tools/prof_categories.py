@@ -21,19 +21,24 @@ def family(n):
     return "other"
 
 
-rows = list(csv.DictReader(open(sys.argv[1])))
-steps = float(sys.argv[2]) if len(sys.argv) > 2 else 5.0
-cat = {}
-other = []
-for r in rows:
-    ms = float(r["TotalDurationNs"]) / 1e6 / steps
-    f = family(r["Name"])
-    cat[f] = cat.get(f, 0.0) + ms
-    if f == "other":
-        other.append((ms, r["Name"][:80]))
-print("| family | ms/step |\n|---|---:|")
-for k, v in sorted(cat.items(), key=lambda x: -x[1]):
-    print(f"| {k} | {v:.2f} |")
-print(f"| total busy | {sum(cat.values()):.2f} |")
-for ms, n in sorted(other, reverse=True)[:8]:
-    print(f"  other: {ms:.3f} {n}", file=sys.stderr)
+def main():
+    rows = list(csv.DictReader(open(sys.argv[1])))
+    steps = float(sys.argv[2]) if len(sys.argv) > 2 else 5.0
+    cat = {}
+    other = []
+    for r in rows:
+        ms = float(r["TotalDurationNs"]) / 1e6 / steps
+        f = family(r["Name"])
+        cat[f] = cat.get(f, 0.0) + ms
+        if f == "other":
+            other.append((ms, r["Name"][:80]))
+    print("| family | ms/step |\n|---|---:|")
+    for k, v in sorted(cat.items(), key=lambda x: -x[1]):
+        print(f"| {k} | {v:.2f} |")
+    print(f"| total busy | {sum(cat.values()):.2f} |")
+    for ms, n in sorted(other, reverse=True)[:8]:
+        print(f"  other: {ms:.3f} {n}", file=sys.stderr)
+
+
+if __name__ == "__main__":
+    main()
