@@ -122,10 +122,11 @@ def test_resnet_bottleneck_uses_fused_stats(monkeypatch, switch):
 
 
 @pytest.mark.parametrize("shape", [(4, 128, 128, 28, 28), (8, 256, 256, 14, 14), (2, 64, 128, 9, 11),
-                                   (4, 64, 64, 14, 14)])
+                                   (4, 64, 64, 14, 14), (3, 64, 64, 13, 11), (32, 64, 64, 56, 56)])
 def test_conv3x3_stats_epilogue(shape):
-    """The 3x3 halo kernel's statistics epilogue: same y as the plain launch, per-tile partials
-    match an fp32 recomputation from y (64 -> 64 runs the weight-stationary kernel: no partials)."""
+    """The 3x3 statistics epilogue (halo kernel; 64 -> 64: the weight-stationary kernel, whose waves
+    merge four 64-row chunks per tile — ragged last tile, and > 1 tile per persistent workgroup at
+    32 x 56 x 56): same y as the plain launch, per-tile partials match an fp32 recomputation from y."""
     N, Ci, Co, H, W = shape
     torch.manual_seed(0)
     x = torch.randn(N, Ci, H, W, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
@@ -133,9 +134,7 @@ def test_conv3x3_stats_epilogue(shape):
     r = _native().conv3x3s1_fwd_stats(x, w)
     y0 = _native().conv3x3s1_fwd(x, w)
     torch.testing.assert_close(r[0], y0, rtol=0, atol=0)
-    if Ci == 64 and Co == 64:
-        assert len(r) == 1
-        return
+    assert len(r) == 2
     part = r[1]
     M = N * H * W
     T = (M + 255) // 256
@@ -147,6 +146,37 @@ def test_conv3x3_stats_epilogue(shape):
     m2 = torch.where(valid, (yf - mu[:, None]) ** 2, 0).sum(1)
     torch.testing.assert_close(part[0], s, rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(part[1], m2, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("shape", [(4, 128, 128, 28, 28), (3, 64, 64, 13, 11), (32, 64, 64, 56, 56)])
+@pytest.mark.parametrize("with_mask", [True, False])
+def test_conv3x3_bn_backward_epilogue(shape, with_mask):
+    """The 3x3 data-gradient launch that also takes the BatchNorm backward reduction (halo kernel):
+    per 256-row tile, sum(dz) and sum(dz * (x - mean)) with dz = y * ReLU mask, against an fp32
+    recomputation from the y it wrote. 64 -> 64 (weight-stationary kernel) returns y alone: the
+    caller's reduce pass takes the statistics."""
+    N, Ci, Co, H, W = shape
+    torch.manual_seed(1)
+    x = torch.randn(N, Ci, H, W, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(Co, Ci, 3, 3, device="cuda") / (9 * Ci) ** 0.5).bfloat16()
+    bx = (torch.randn(N, Co, H, W, device="cuda") + 0.3).bfloat16().contiguous(memory_format=torch.channels_last)
+    M = N * H * W
+    mean = bx.float().permute(0, 2, 3, 1).reshape(M, Co).mean(0).contiguous()
+    bits, mask = _bits_mask(M, Co) if with_mask else (torch.ones(M, Co, dtype=torch.bool, device="cuda"), None)
+    r = _native().conv3x3s1_fwd_bnbwd(x, w, bx, mask, mean)
+    torch.testing.assert_close(r[0], _native().conv3x3s1_fwd(x, w), rtol=0, atol=0)
+    if Ci == 64 and Co == 64:
+        assert len(r) == 1
+        return
+    assert len(r) == 2
+    T = (M + 255) // 256
+    dz = torch.where(bits, r[0].permute(0, 2, 3, 1).reshape(M, Co).float(), 0)
+    xc = bx.permute(0, 2, 3, 1).reshape(M, Co).float() - mean
+    pad = T * 256 - M
+    dzt = torch.cat([dz, torch.zeros(pad, Co, device="cuda")]).view(T, 256, Co)
+    xct = torch.cat([xc, torch.zeros(pad, Co, device="cuda")]).view(T, 256, Co)
+    torch.testing.assert_close(r[1][0], dzt.sum(1), rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(r[1][1], (dzt * xct).sum(1), rtol=1e-4, atol=1e-3)
 
 
 def test_gemm_accumulates_masked_source():
