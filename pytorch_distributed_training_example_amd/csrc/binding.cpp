@@ -93,13 +93,6 @@ int pdt_conv3x3s2_wgrad(const uint16_t* x, const uint16_t* dy, uint16_t* dw, flo
 int pdt_conv3x3s1_fwd_stats(const uint16_t* x, const uint16_t* w, uint16_t* y, float* part, int N, int H, int W,
                             int Ci, int Co, hipStream_t s);
 int64_t pdt_stem_conv_wprep_elems();
-int pdt_stem_conv_fwd_stats(const uint16_t* x, const uint16_t* w, uint16_t* wp, uint16_t* y, float* part, int N,
-                            int H, int W, hipStream_t s);
-int pdt_stem_stats_tile_rows(int H, int W);
-int pdt_bn_relu_maxpool_fwd_train_tiles(const float* part, int T, int BMt, const uint16_t* x, const float* gamma,
-                                        const float* beta, float* running_mean, float* running_var, float momentum,
-                                        float eps, int N, int H, int W, int C, uint16_t* y, uint8_t* code, float* mean,
-                                        float* invstd, float* ws, hipStream_t s);
 int pdt_stem_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* wp, uint16_t* y, int N, int H, int W,
                       hipStream_t s);
 int64_t pdt_stem_wgrad_ws_floats();
@@ -412,36 +405,6 @@ std::vector<Tensor> bn_fwd_train(Tensor x, c10::optional<Tensor> res, c10::optio
 }
 
 // ResNet stem tail (train): BN + ReLU + MaxPool2d(3, 2, 1) -> {y_pooled, code, mean, invstd}
-// bn_relu_maxpool_fwd with the statistics taken by the producing conv: part [2, T, C] per-tile
-// partials of M / T rows each (the stem conv's epilogue, stem_conv_fwd_stats).
-std::vector<Tensor> bn_relu_maxpool_fwd_tiles(Tensor x, Tensor part, c10::optional<Tensor> weight,
-                                              c10::optional<Tensor> bias, c10::optional<Tensor> running_mean,
-                                              c10::optional<Tensor> running_var, double momentum, double eps) {
-  check_nhwc_bf16(x, "x");
-  TORCH_CHECK(x.dim() == 4, "bn_relu_maxpool: 4-D NHWC input");
-  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3), M = N * H * W;
-  TORCH_CHECK(C % 64 == 0, "pdt bn: C must be a multiple of 64");
-  TORCH_CHECK(part.scalar_type() == at::kFloat && part.is_contiguous() && part.dim() == 3 && part.size(0) == 2 &&
-              part.size(2) == C && part.size(1) > 0 && M % part.size(1) == 0,
-              "bn_relu_maxpool_fwd_tiles: partials [2, T, C] fp32 with T dividing the rows");
-  const int64_t T = part.size(1), BMt = M / T;
-  const int64_t Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
-  auto y = at::empty({N, C, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
-  auto code = at::empty({N * Ho * Wo * C}, x.options().dtype(at::kByte));
-  auto fopt = x.options().dtype(at::kFloat);
-  auto mean = at::empty({C}, fopt), invstd = at::empty({C}, fopt);
-  auto ws = at::empty({pdt_bn_tiles_ws_floats((int)T, (int)C)}, fopt);
-  float* rm = running_mean.has_value() && running_mean->defined() ? running_mean->data_ptr<float>() : nullptr;
-  float* rv = running_var.has_value() && running_var->defined() ? running_var->data_ptr<float>() : nullptr;
-  const int rc = pdt_bn_relu_maxpool_fwd_train_tiles(
-      part.data_ptr<float>(), (int)T, (int)BMt, reinterpret_cast<const uint16_t*>(x.data_ptr()), opt_fptr(weight),
-      opt_fptr(bias), rm, rv, (float)momentum, (float)eps, (int)N, (int)H, (int)W, (int)C,
-      reinterpret_cast<uint16_t*>(y.data_ptr()), code.data_ptr<uint8_t>(), mean.data_ptr<float>(),
-      invstd.data_ptr<float>(), ws.data_ptr<float>(), stream());
-  TORCH_CHECK(rc == 0, "pdt_bn_relu_maxpool_fwd_train_tiles failed: ", rc);
-  return {y, code, mean, invstd};
-}
-
 std::vector<Tensor> bn_relu_maxpool_fwd(Tensor x, c10::optional<Tensor> weight, c10::optional<Tensor> bias,
                                         c10::optional<Tensor> running_mean, c10::optional<Tensor> running_var,
                                         double momentum, double eps) {
@@ -966,29 +929,6 @@ Tensor stem_conv_fwd(Tensor x, Tensor w) {
   return y;
 }
 
-// stem_conv_fwd + the per-tile BatchNorm statistics of y from its epilogue: {y, part [2, T, 64]}
-// with tiles of pdt_stem_stats_tile_rows() rows, or {y} at a shape without the epilogue.
-std::vector<Tensor> stem_conv_fwd_stats(Tensor x, Tensor w) {
-  check_nhwc_bf16(x, "x");
-  TORCH_CHECK(x.size(1) == 3 && x.size(3) % 32 == 0, "stem_conv: x [N, 3, H, W] with W % 32 == 0");
-  const int64_t N = x.size(0), H = x.size(2), W = x.size(3), OH = (H - 1) / 2 + 1, OW = W / 2;
-  const int rows = pdt_stem_stats_tile_rows((int)H, (int)W);
-  if (rows == 0) return {stem_conv_fwd(x, w)};
-  TORCH_CHECK(w.dim() == 4 && w.size(0) == 64 && w.size(1) == 3 && w.size(2) == 7 && w.size(3) == 7 &&
-              w.scalar_type() == at::kBFloat16, "stem_conv: weight [64, 3, 7, 7] bf16");
-  w = w.contiguous(at::MemoryFormat::ChannelsLast);
-  auto wp = at::empty({pdt_stem_conv_wprep_elems()}, w.options());
-  auto y = at::empty({N, 64, OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
-  auto part = at::empty({2, N * OH * OW / rows, 64}, x.options().dtype(at::kFloat));
-  const int rc = pdt_stem_conv_fwd_stats(reinterpret_cast<const uint16_t*>(x.data_ptr()),
-                                         reinterpret_cast<const uint16_t*>(w.data_ptr()),
-                                         reinterpret_cast<uint16_t*>(wp.data_ptr()),
-                                         reinterpret_cast<uint16_t*>(y.data_ptr()), part.data_ptr<float>(), (int)N,
-                                         (int)H, (int)W, stream());
-  TORCH_CHECK(rc == 0, "pdt_stem_conv_fwd_stats failed: ", rc);
-  return {y, part};
-}
-
 // Weight gradient of stem_conv_fwd: dw [64, 3, 7, 7] (channels_last) from x and dy [N, 64, OH, OW]
 // (channels_last); W % 32 == 0 and W <= 224.
 Tensor stem_conv_wgrad(Tensor x, Tensor dy) {
@@ -1501,8 +1441,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("res_ab") = py::none(), py::arg("apply") = true);
   m.def("bn_fwd_eval", &bn_fwd_eval);
   m.def("bn_relu_maxpool_fwd", &bn_relu_maxpool_fwd);
-  m.def("bn_relu_maxpool_fwd_tiles", &bn_relu_maxpool_fwd_tiles);
-  m.def("stem_conv_fwd_stats", &stem_conv_fwd_stats);
   m.def("maxpool3s2_bwd", &maxpool3s2_bwd);
   m.def("conv1x1_gemm", &conv1x1_gemm, py::arg("a"), py::arg("b"), py::arg("out"), py::arg("acc"), py::arg("stats"),
         py::arg("c_in") = py::none(), py::arg("c_mask") = py::none(), py::arg("bn_x") = py::none(),

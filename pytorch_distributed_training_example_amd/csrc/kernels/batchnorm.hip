@@ -947,31 +947,6 @@ int pdt_bn_relu_maxpool_fwd_train(const uint16_t* x, const float* gamma, const f
   return 0;
 }
 
-// The same with the statistics already taken by the producing conv (the stem conv's epilogue,
-// conv_stem.hip STATS): per-tile partials part [2][T][C] of BMt rows each -> finalize (2 small
-// launches) + the fused apply/ReLU/pool; no reduce pass over x. ws: pdt_bn_tiles_ws_floats(T, C).
-int pdt_bn_relu_maxpool_fwd_train_tiles(const float* part, int T, int BMt, const uint16_t* x, const float* gamma,
-                                        const float* beta, float* running_mean, float* running_var, float momentum,
-                                        float eps, int N, int H, int W, int C, uint16_t* y, uint8_t* code, float* mean,
-                                        float* invstd, float* ws, hipStream_t s) {
-  const int64_t M = (int64_t)N * H * W;
-  if (C % kCC != 0 || M < 1 || T != (int)((M + BMt - 1) / BMt)) return -1;
-  const int P = (T + kTilesPerBlock - 1) / kTilesPerBlock;
-  double* lv = reinterpret_cast<double*>(ws);
-  float* a = ws + 4 * (int64_t)P * C;
-  float* b = a + C;
-  FinArgs fa{};
-  fa.gamma = gamma; fa.beta = beta; fa.mean_out = mean; fa.invstd_out = invstd; fa.a_out = a;
-  fa.b_out = b; fa.running_mean = running_mean; fa.running_var = running_var; fa.momentum = momentum;
-  fa.eps = eps; fa.M = M;
-  hipLaunchKernelGGL(bn_tiles_l1_kernel<true>, dim3(C / 64, P), dim3(1024), 0, s, part, T, BMt, M, C, lv);
-  hipLaunchKernelGGL(bn_tiles_l2_kernel, dim3((C + 255) / 256), dim3(256), 0, s, lv, P, C, fa);
-  const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
-  hipLaunchKernelGGL(bn_apply_pool_kernel, dim3(row_grid((int64_t)N * Ho)), dim3(256), 0, s, x, a, b, y, code, N, H, W, C,
-                     Ho, Wo);
-  return 0;
-}
-
 // dz [N,H,W,C] (gradient at the BN output, ReLU folded in) from the pooled gradient dy [N,Ho,Wo,C].
 int pdt_maxpool3s2_bwd(const uint16_t* dy, const uint8_t* code, uint16_t* dz, int N, int H, int W, int C,
                        hipStream_t s) {

@@ -25,6 +25,9 @@
 //     and out as 16-B pieces, 1 KB contiguous per store instruction. Storing the accumulators
 //     directly (8 B per lane, 16 cache lines per instruction) ran the kernel at 2.6 TB/s — the
 //     no-store probe took 165 us of its 380;
+//   * (A BatchNorm-statistics epilogue here — per-lane sums, Chan merges across lanes and rows —
+//     measured 686 us vs 390 us + the 321 us reduce pass it replaces: the extra registers spill
+//     in this 250-VGPR kernel; not kept.)
 //   * the kernel is HBM-store bound, not MFMA bound (28 MFMAs per 16 x 64 outputs); a first
 //     non-persistent version (4-row tiles, 3 workgroups per CU, weights re-staged and the window
 //     loaded then waited on per tile) ran 384 us at batch 512 vs MIOpen's 860 us.
@@ -58,8 +61,7 @@ constexpr int kWPitch = kWRow + 16;           // +16 B: conflict-free 16-row fra
 constexpr int kLdsIn = kInRows * kInPitch;    // 25,584 B
 constexpr int kStPitch = kCo * 2 + 16;        // epilogue staging row (one pixel), +16 B vs bank conflicts
 constexpr int kStage = 16 * kStPitch;         // per wave: one 16-pixel block
-constexpr int kStat = kRowsOut * 2 * kCo * 4;  // STATS: per wave (row) the (mean, M2) of its 112 x 64 outputs
-constexpr int kLds = kLdsIn + kCo * kWPitch + kRowsOut * kStage + kStat;  // 66,544 B: window, weights, staging, stats
+constexpr int kLds = kLdsIn + kCo * kWPitch + kRowsOut * kStage;  // 64,496 B: window, weights, staging
 constexpr int kWPrepElems = kCo * 7 * 32;
 
 __device__ __forceinline__ f4 mfma(bf16x8 a, bf16x8 b, f4 c) {
@@ -130,19 +132,11 @@ __device__ __forceinline__ void store_window(const Window& wv, char* lin, int ti
 #ifndef PDT_STEM_PROBE
 #define PDT_STEM_PROBE 0  // diagnostics only (tools/convbench/stem_bench.cpp): 1 = no Y stores, 2 = no MFMA, 3 = no window loads
 #endif
-// STATS (host-checked: OW == 112 and OH % 4 == 0, so tile t is exactly the 448 output rows
-// [448 t, 448 t + 448) of the NHWC output): the BatchNorm statistics of each tile in the
-// tile_stats.h layout with BM = 448 (sum, CENTRED sum of squares), so the stem BatchNorm never
-// re-reads the 1.64 GB output for them (a 321 us reduce pass at batch 1024). Each lane sums its 14
-// values per channel (and their squares), then the 8 lanes of a channel chunk and the 4 rows
-// (waves) of the tile merge their (mean, centred M2) pairwise (Chan, equal counts); wave 0 merges
-// the rows after the next barrier.
-template <bool FULL, bool STATS = false>  // FULL: every column tile is 112 wide (OW % 112 == 0): no per-block predicates
+template <bool FULL>  // FULL: every column tile is 112 wide (OW % 112 == 0): no per-block predicates
 __global__ __launch_bounds__(kThreads, 2) void stem_conv_kernel(const uint16_t* __restrict__ X,
                                                           const uint16_t* __restrict__ Wp,
                                                           uint16_t* __restrict__ Y, int H, int W, int OH, int OW,
-                                                          int nrt, int nct, int ntiles, float* __restrict__ part) {
-  static_assert(!STATS || FULL, "statistics need whole 112-column tiles");
+                                                          int nrt, int nct, int ntiles) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   char* const lw = lds + kLdsIn;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -172,31 +166,10 @@ __global__ __launch_bounds__(kThreads, 2) void stem_conv_kernel(const uint16_t* 
   const int pl = lane & 15, g = lane >> 4;
   const char* wrow = lw + pl * kWPitch + g * 16;
   char* const stage = lw + kCo * kWPitch + wid * kStage;
-  float* const statb = reinterpret_cast<float*>(lw + kCo * kWPitch + kRowsOut * kStage);  // [wave][2][64]
-  // merge the 4 rows' (mean, M2) of tile tt (wave 0, one channel per lane; 112 values per row)
-  auto merge = [&](int tt) {
-    float mu[4], m2[4];
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      mu[w] = statb[(w * 2) * kCo + lane];
-      m2[w] = statb[(w * 2 + 1) * kCo + lane];
-    }
-    const float d01 = mu[0] - mu[1], d23 = mu[2] - mu[3];
-    const float ma = 0.5f * (mu[0] + mu[1]), mb = 0.5f * (mu[2] + mu[3]);
-    const float qa = m2[0] + m2[1] + d01 * d01 * 56.f, qb = m2[2] + m2[3] + d23 * d23 * 56.f;
-    const float dab = ma - mb;
-    part[(int64_t)tt * kCo + lane] = (ma + mb) * 224.f;  // tile sum = mean x 448
-    part[((int64_t)ntiles + tt) * kCo + lane] = qa + qb + dab * dab * 112.f;
-  };
-  int pending = -1;
   for (int k = 0; k < cnt; ++k) {
     const int t = t0 + k;
     coords(t, n, oh0, ow0);
     __syncthreads();  // window k visible
-    if constexpr (STATS) {  // the previous tile's rows were parked before this barrier
-      if (pending >= 0 && wid == 0) merge(pending);
-      pending = -1;
-    }
 
     const char* lin = lds;
     const int nb = min(kMB, (OW - ow0) >> 4);
@@ -239,9 +212,6 @@ __global__ __launch_bounds__(kThreads, 2) void stem_conv_kernel(const uint16_t* 
     // ---- epilogue: lane = pixel pl of each block, channels 16j + 4g .. +3 -> the wave's LDS
     // staging block [16 px][64 ch] -> 16-B pieces, each store instruction 1 KB contiguous of Y
     const int oh = oh0 + wid;
-    // STATS: this lane's channels 8 (lane & 7) .. +7, 14 pixels (2 per block): sum and sum of squares
-    // (only 14 values per lane before the centred merges; the register budget has no room for a shift)
-    float ss[8], sq[8];
     if (oh < OH) {
       uint16_t* yrow = Y + ((int64_t)(n * OH + oh) * OW + ow0) * kCo;
 #pragma unroll
@@ -257,58 +227,16 @@ __global__ __launch_bounds__(kThreads, 2) void stem_conv_kernel(const uint16_t* 
           for (int h = 0; h < 2; ++h) {  // the wave's own LDS writes above complete in order first
             const int idx = lane + 64 * h, px = idx >> 3, c = idx & 7;
             const uint4 pv = *reinterpret_cast<const uint4*>(stage + px * kStPitch + c * 16);
-            if constexpr (STATS) {
-              const uint32_t wv[4] = {pv.x, pv.y, pv.z, pv.w};
-#pragma unroll
-              for (int e = 0; e < 8; ++e) {
-                const float x = __uint_as_float(e & 1 ? (wv[e >> 1] & 0xffff0000u) : (wv[e >> 1] << 16));
-                ss[e] = (i == 0 && h == 0) ? x : ss[e] + x;
-                sq[e] = (i == 0 && h == 0) ? x * x : fmaf(x, x, sq[e]);
-              }
-            }
             if (PDT_STEM_PROBE == 1 && pv.x != 12345u) continue;
             *reinterpret_cast<uint4*>(yrow + (int64_t)(i * 16 + px) * kCo + c * 8) = pv;
           }
         }
       }
     }
-    if constexpr (STATS) {
-      // lane: (mean, M2) of 14 values; then the 8 lanes of each channel chunk (lane bits 3-5)
-      float mu[8], m2[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        mu[e] = ss[e] * (1.f / 14.f);
-        m2[e] = fmaxf(sq[e] - ss[e] * mu[e], 0.f);
-      }
-      float nh = 7.f;  // half the merged count: 14 -> 28 -> 56 -> 112
-#pragma unroll
-      for (int sh = 8; sh < 64; sh <<= 1) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float om = __shfl_xor(mu[e], sh, 64), oq = __shfl_xor(m2[e], sh, 64);
-          const float d = mu[e] - om;
-          m2[e] = m2[e] + oq + d * d * nh;
-          mu[e] = 0.5f * (mu[e] + om);
-        }
-        nh *= 2.f;
-      }
-      if (lane < 8) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          statb[(wid * 2) * kCo + lane * 8 + e] = mu[e];
-          statb[(wid * 2 + 1) * kCo + lane * 8 + e] = m2[e];
-        }
-      }
-      pending = t;
-    }
     if (PDT_STEM_PROBE != 3 && k + 1 < cnt) {
       __syncthreads();  // every wave is done reading window k
       store_window(wv, lds, tid);
     }
-  }
-  if constexpr (STATS) {  // the last tile's rows
-    __syncthreads();
-    if (pending >= 0 && wid == 0) merge(pending);
   }
 }
 
@@ -555,50 +483,28 @@ extern "C" int64_t pdt_stem_conv_wprep_elems() { return kWPrepElems; }
 
 // y[N, 64, OH, OW] (channels_last) = conv2d(x[N, 3, H, W] (channels_last), w[64, 3, 7, 7]
 // (channels_last storage [64][7][7][3]), stride 2, padding 3); wp: kWPrepElems bf16 scratch.
-extern "C" int pdt_stem_conv_fwd_stats(const uint16_t* x, const uint16_t* w, uint16_t* wp, uint16_t* y, float* part,
-                                       int N, int H, int W, hipStream_t s);
-
 extern "C" int pdt_stem_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* wp, uint16_t* y, int N, int H,
                                  int W, hipStream_t s) {
-  return pdt_stem_conv_fwd_stats(x, w, wp, y, nullptr, N, H, W, s);
-}
-
-// Rows per statistics tile of pdt_stem_conv_fwd_stats (0: no statistics epilogue at this shape).
-extern "C" int pdt_stem_stats_tile_rows(int H, int W) {
-  const int OH = (H - 1) / 2 + 1, OW = W / 2;
-  return (OW == kTW && OH % kRowsOut == 0) ? kRowsOut * kTW : 0;
-}
-
-// part (or null): [2][N * OH / 4][64] per-448-row-tile statistics of y (see STATS); returns -5 when
-// part is given at a shape without the epilogue (pdt_stem_stats_tile_rows() == 0).
-extern "C" int pdt_stem_conv_fwd_stats(const uint16_t* x, const uint16_t* w, uint16_t* wp, uint16_t* y, float* part,
-                                       int N, int H, int W, hipStream_t s) {
   if (N < 1 || H < 1 || W < 32 || W % 32 != 0) return -1;
   const int OH = (H - 1) / 2 + 1, OW = W / 2;
-  if (part && pdt_stem_stats_tile_rows(H, W) == 0) return -5;
   static const bool attr_ok =
       hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_conv_kernel<true>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, kLds) == hipSuccess &&
       hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_conv_kernel<false>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, kLds) == hipSuccess &&
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_conv_kernel<true, true>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, kLds) == hipSuccess;
   if (!attr_ok) return -2;
   const int ncu = stem_ncu();
   const int nrt = (OH + kRowsOut - 1) / kRowsOut, nct = (OW + kTW - 1) / kTW;
   const int64_t ntiles = (int64_t)N * nrt * nct;
   if (ntiles > 0x7fffffff || (int64_t)N * H > 0x7fffffff / 4) return -3;
-  const int grid = (int)std::min<int64_t>(ntiles, 2 * ncu);  // 2 workgroups (65 KB LDS each) per CU: out of phase
+  const int grid = (int)std::min<int64_t>(ntiles, 2 * ncu);  // 2 workgroups (61.4 KB LDS each) per CU: out of phase
   hipLaunchKernelGGL(stem_wprep_kernel, dim3((kWPrepElems + 255) / 256), dim3(256), 0, s, w, wp);
-  if (part)
-    hipLaunchKernelGGL((stem_conv_kernel<true, true>), dim3(grid), dim3(kThreads), kLds, s, x, wp, y, H, W, OH, OW, nrt,
-                       nct, (int)ntiles, part);
-  else if (OW % kTW == 0)
-    hipLaunchKernelGGL((stem_conv_kernel<true>), dim3(grid), dim3(kThreads), kLds, s, x, wp, y, H, W, OH, OW, nrt, nct,
-                       (int)ntiles, nullptr);
+  if (OW % kTW == 0)
+    hipLaunchKernelGGL(stem_conv_kernel<true>, dim3(grid), dim3(kThreads), kLds, s, x, wp, y, H, W, OH, OW, nrt, nct,
+                       (int)ntiles);
   else
-    hipLaunchKernelGGL((stem_conv_kernel<false>), dim3(grid), dim3(kThreads), kLds, s, x, wp, y, H, W, OH, OW, nrt, nct,
-                       (int)ntiles, nullptr);
+    hipLaunchKernelGGL(stem_conv_kernel<false>, dim3(grid), dim3(kThreads), kLds, s, x, wp, y, H, W, OH, OW, nrt, nct,
+                       (int)ntiles);
   return hipGetLastError() == hipSuccess ? 0 : -4;
 }
 

@@ -301,13 +301,8 @@ class _BNReluMaxPoolFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps):
-        st = getattr(x, "_pdt_stem_stats", None)  # statistics from the stem conv's epilogue
-        if st is not None and st.version == x._version:
-            y, code, mean, invstd = native().bn_relu_maxpool_fwd_tiles(x, st.part, weight, bias, running_mean,
-                                                                       running_var, momentum, eps)
-        else:
-            y, code, mean, invstd = native().bn_relu_maxpool_fwd(x, weight, bias, running_mean, running_var,
-                                                                 momentum, eps)
+        y, code, mean, invstd = native().bn_relu_maxpool_fwd(x, weight, bias, running_mean, running_var,
+                                                             momentum, eps)
         ctx.has_weight = weight is not None
         ctx.hw = (x.shape[2], x.shape[3])
         ctx.save_for_backward(x, code, weight, mean, invstd)

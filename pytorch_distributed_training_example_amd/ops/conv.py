@@ -559,14 +559,9 @@ class _StemConvFn(torch.autograd.Function):
     never asks for (the images need none) — on MIOpen."""
 
     @staticmethod
-    def forward(ctx, x, weight, stats_out=None):
+    def forward(ctx, x, weight):
         from ._native import native
         ctx.save_for_backward(x, weight)
-        if stats_out is not None:  # the stem BatchNorm's statistics from the conv's epilogue
-            r = native().stem_conv_fwd_stats(x, weight)
-            if len(r) == 2:
-                stats_out.append(r[1])
-            return r[0]
         return native().stem_conv_fwd(x, weight)
 
     @staticmethod
@@ -583,7 +578,7 @@ class _StemConvFn(torch.autograd.Function):
                 dw = native().stem_conv_wgrad(x, gy)
             else:
                 dw = torch.ops.aten.convolution_backward(*args, [False, True, False])[1]
-        return dx, dw, None
+        return dx, dw
 
 
 def stem_eligible(conv: nn.Conv2d, x: torch.Tensor) -> bool:
@@ -618,12 +613,7 @@ class SplitConv2d(nn.Conv2d):
                 y._pdt_bn_stats = BNStats(holder[0], y._version)
             return y
         if stem_eligible(self, x):
-            holder = [] if (self.emit_bn_stats and self.training and torch.is_grad_enabled()
-                            and SW.conv_bn_stats) else None
-            y = _StemConvFn.apply(x, self.weight, holder)
-            if holder:  # tiles of pdt_stem_stats_tile_rows() rows: only the stem BN+ReLU+pool reads them
-                y._pdt_stem_stats = BNStats(holder[0], y._version)
-            return y
+            return _StemConvFn.apply(x, self.weight)
         return super().forward(x)
 
 
