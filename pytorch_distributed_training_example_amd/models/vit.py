@@ -11,6 +11,7 @@ from __future__ import annotations
 import torch
 from torch import nn
 
+from ..ops.conv import PatchConv2d
 from ..ops.layernorm import LayerNorm
 from .transformer import Block, init_weights, run_blocks
 
@@ -43,7 +44,8 @@ class VisionTransformer(nn.Module):
         super().__init__()
         self.patch_size = patch_size
         n = (image_size // patch_size) ** 2
-        self.conv_proj = nn.Conv2d(3, dim, kernel_size=patch_size, stride=patch_size)
+        # patchify + one GEMM on the GPU (ops/conv.py PatchConv2d; nn.Conv2d parameters / state_dict)
+        self.conv_proj = PatchConv2d(3, dim, kernel_size=patch_size, stride=patch_size)
         self.class_token = nn.Parameter(torch.zeros(1, 1, dim))
         self.encoder = _Encoder(n + 1, dim, depth, heads, mlp_ratio)
         self.heads = _Heads(dim, num_classes)

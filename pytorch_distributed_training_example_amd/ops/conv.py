@@ -617,6 +617,35 @@ class SplitConv2d(nn.Conv2d):
         return super().forward(x)
 
 
+class PatchConv2d(nn.Conv2d):
+    """``nn.Conv2d`` (same parameters / state_dict) for a non-overlapping patch embedding — kernel ==
+    stride, no padding, no dilation, groups 1 (ViT's ``conv_proj``). On the GPU it runs as patchify
+    (one reshape copy of the input into [B * gh * gw, C * p * p] rows, the weight's (c, kh, kw)
+    order) + ONE GEMM through ``ops.linear`` (hipBLASLt forward with the bias in its epilogue,
+    split-K weight gradient, column-strip bias gradient), instead of MIOpen's strided implicit-GEMM
+    forward / weight-gradient kernels, their transposes and their run-time compile on a fresh box.
+    The output is returned as the [B, D, gh, gw] view of the GEMM's [B, gh, gw, D] rows, so
+    ``flatten(2).transpose(1, 2)`` (the token sequence) is contiguous again without a copy."""
+
+    def _patch_ok(self, x: torch.Tensor) -> bool:
+        k = self.kernel_size
+        return (x.is_cuda and x.dim() == 4 and k == self.stride and self.padding == (0, 0)
+                and self.dilation == (1, 1) and self.groups == 1 and self.padding_mode == "zeros"
+                and x.dtype == self.weight.dtype and not disabled())
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if not self._patch_ok(x):
+            return super().forward(x)
+        from .linear import linear
+        ph, pw = self.kernel_size
+        B, C, H, W = x.shape
+        gh, gw = H // ph, W // pw
+        xp = (x[:, :, :gh * ph, :gw * pw].reshape(B, C, gh, ph, gw, pw).permute(0, 2, 4, 1, 3, 5)
+              .reshape(B * gh * gw, C * ph * pw))
+        y = linear(xp, self.weight.reshape(self.out_channels, -1), self.bias)
+        return y.view(B, gh, gw, self.out_channels).permute(0, 3, 1, 2)
+
+
 def linked_conv(conv: nn.Conv2d, x: torch.Tensor, link) -> torch.Tensor:
     """``conv(x)`` whose input gradient is summed with the partner branch's through ``link``."""
     if isinstance(conv, Conv1x1) and (conv.gemm_eligible(x) or conv.strided_gemm_eligible(x)):
