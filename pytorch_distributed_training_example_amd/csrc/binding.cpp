@@ -98,6 +98,8 @@ int pdt_stem_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* wp, uint16
 int64_t pdt_stem_wgrad_ws_floats();
 int pdt_stem_conv_wgrad(const uint16_t* x, const uint16_t* dy, uint16_t* dw, float* ws, int N, int H, int W,
                         hipStream_t s);
+int pdt_stem_conv_wgrad_bn(const uint16_t* x, const uint16_t* dz, const uint16_t* xb, const float* coef,
+                           const float* mean, uint16_t* dw, float* ws, int N, int H, int W, hipStream_t s);
 int pdt_maxpool3s2_bwd(const uint16_t* dy, const uint8_t* code, uint16_t* dz, int N, int H, int W, int C,
                        hipStream_t s);
 int pdt_conv1x1_tile_rows();
@@ -112,6 +114,9 @@ int pdt_maxpool_bn_parts(int N, int H);
 int pdt_maxpool3s2_bwd_bn(const uint16_t* dy, const uint8_t* code, uint16_t* dz, int N, int H, int W, int C,
                           const uint16_t* x, const float* gamma, const float* mean, const float* invstd, uint16_t* dx,
                           float* dgamma, float* dbeta, float* part, float* ws, hipStream_t s);
+int pdt_maxpool3s2_bwd_bn_coef(const uint16_t* dy, const uint8_t* code, uint16_t* dz, int N, int H, int W, int C,
+                               const uint16_t* x, const float* gamma, const float* mean, const float* invstd,
+                               float* coef, float* dgamma, float* dbeta, float* part, float* ws, hipStream_t s);
 int pdt_bn_bwd_train_tiles(const float* part, int T, int BMt, const uint16_t* dy, const uint16_t* x,
                            const uint8_t* mask, const float* gamma, const float* mean, const float* invstd, int64_t M,
                            int C, int relu, int has_res, uint16_t* dx, uint16_t* dres, float* dgamma, float* dbeta,
@@ -522,6 +527,38 @@ std::vector<Tensor> maxpool3s2_bwd_bn(Tensor dy, Tensor code, Tensor x, c10::opt
                                        ws.data_ptr<float>(), stream());
   TORCH_CHECK(rc == 0, "pdt_maxpool3s2_bwd_bn failed: ", rc);
   return {dx, dg, db};
+}
+
+// Same without the BN apply: returns {dz (the max-pool gradient = dy at the BN output), coef [3, 64]
+// (A, B, D: dx = A dz + B (x - mean) + D), dgamma, dbeta} for stem_conv_wgrad_bn.
+std::vector<Tensor> maxpool3s2_bwd_bn_coef(Tensor dy, Tensor code, Tensor x, c10::optional<Tensor> weight,
+                                           Tensor mean, Tensor invstd, bool need_dgamma) {
+  check_nhwc_bf16(dy, "dy");
+  check_nhwc_bf16(x, "x");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(C == 64, "maxpool3s2_bwd_bn_coef: C == 64");
+  TORCH_CHECK(dy.size(0) == N && dy.size(1) == C && dy.size(2) == (H - 1) / 2 + 1 && dy.size(3) == (W - 1) / 2 + 1,
+              "maxpool3s2_bwd_bn_coef: dy shape");
+  TORCH_CHECK(code.scalar_type() == at::kByte && code.numel() == dy.numel(), "maxpool3s2_bwd_bn_coef: code");
+  auto dz = at::empty_like(x);
+  auto fopt = x.options().dtype(at::kFloat);
+  auto coef = at::empty({3, C}, fopt);
+  Tensor dg, db;
+  if (need_dgamma) {
+    dg = at::empty({C}, fopt);
+    db = at::empty({C}, fopt);
+  }
+  const int T = pdt_maxpool_bn_parts((int)N, (int)H);
+  auto part = at::empty({2 * (int64_t)T * C}, fopt);
+  auto ws = at::empty({pdt_bn_tiles_ws_floats(T, (int)C) + 2 * C}, fopt);
+  const int rc = pdt_maxpool3s2_bwd_bn_coef(
+      reinterpret_cast<const uint16_t*>(dy.data_ptr()), code.data_ptr<uint8_t>(),
+      reinterpret_cast<uint16_t*>(dz.data_ptr()), (int)N, (int)H, (int)W, (int)C,
+      reinterpret_cast<const uint16_t*>(x.data_ptr()), opt_fptr(weight), mean.data_ptr<float>(),
+      invstd.data_ptr<float>(), coef.data_ptr<float>(), need_dgamma ? dg.data_ptr<float>() : nullptr,
+      need_dgamma ? db.data_ptr<float>() : nullptr, part.data_ptr<float>(), ws.data_ptr<float>(), stream());
+  TORCH_CHECK(rc == 0, "pdt_maxpool3s2_bwd_bn_coef failed: ", rc);
+  return {dz, coef, dg, db};
 }
 
 // BN training backward with the reduction taken from the dy producer's per-tile partials
@@ -945,6 +982,32 @@ Tensor stem_conv_wgrad(Tensor x, Tensor dy) {
                                      reinterpret_cast<uint16_t*>(dw.data_ptr()), ws.data_ptr<float>(), (int)N, (int)H,
                                      (int)W, stream());
   TORCH_CHECK(rc == 0, "pdt_stem_conv_wgrad failed: ", rc);
+  return dw;
+}
+
+// stem_conv_wgrad with the stem BatchNorm's backward apply fused into the gradient load: the conv's
+// output gradient is A dz + B (xb - mean) + D (coef [3, 64] = A, B, D from maxpool3s2_bwd_bn_coef;
+// xb: the BN input = the stem conv output, dz: the gradient at the BN output, both [N, 64, OH, OW]).
+Tensor stem_conv_wgrad_bn(Tensor x, Tensor dz, Tensor xb, Tensor coef, Tensor mean) {
+  check_nhwc_bf16(x, "x");
+  check_nhwc_bf16(dz, "dz");
+  check_nhwc_bf16(xb, "xb");
+  const int64_t N = x.size(0), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(x.size(1) == 3 && W % 32 == 0 && W <= 224, "stem_conv_wgrad_bn: x [N, 3, H, W], W % 32 == 0, W <= 224");
+  TORCH_CHECK(dz.size(0) == N && dz.size(1) == 64 && dz.size(2) == (H - 1) / 2 + 1 && dz.size(3) == W / 2,
+              "stem_conv_wgrad_bn: dz [N, 64, OH, OW]");
+  TORCH_CHECK(xb.sizes() == dz.sizes(), "stem_conv_wgrad_bn: xb shape");
+  TORCH_CHECK(coef.is_cuda() && coef.scalar_type() == at::kFloat && coef.is_contiguous() && coef.numel() == 3 * 64,
+              "stem_conv_wgrad_bn: coef [3, 64] f32");
+  TORCH_CHECK(mean.is_cuda() && mean.scalar_type() == at::kFloat && mean.is_contiguous() && mean.numel() == 64,
+              "stem_conv_wgrad_bn: mean [64] f32");
+  auto ws = at::empty({pdt_stem_wgrad_ws_floats()}, x.options().dtype(at::kFloat));
+  auto dw = at::empty({64, 3, 7, 7}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const int rc = pdt_stem_conv_wgrad_bn(
+      reinterpret_cast<const uint16_t*>(x.data_ptr()), reinterpret_cast<const uint16_t*>(dz.data_ptr()),
+      reinterpret_cast<const uint16_t*>(xb.data_ptr()), coef.data_ptr<float>(), mean.data_ptr<float>(),
+      reinterpret_cast<uint16_t*>(dw.data_ptr()), ws.data_ptr<float>(), (int)N, (int)H, (int)W, stream());
+  TORCH_CHECK(rc == 0, "pdt_stem_conv_wgrad_bn failed: ", rc);
   return dw;
 }
 
@@ -1448,6 +1511,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("c_H") = 0, py::arg("c_W") = 0);
   m.def("bn_bwd_train_tiles", &bn_bwd_train_tiles);
   m.def("maxpool3s2_bwd_bn", &maxpool3s2_bwd_bn);
+  m.def("maxpool3s2_bwd_bn_coef", &maxpool3s2_bwd_bn_coef);
   m.def("slice_sum", &slice_sum);
   m.def("subsample_gather", &subsample_gather);
   m.def("subsample_scatter_add", &subsample_scatter_add);
@@ -1464,6 +1528,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("bn_x") = py::none(), py::arg("bn_mask") = py::none(), py::arg("bn_mean") = py::none());
   m.def("stem_conv_fwd", &stem_conv_fwd);
   m.def("stem_conv_wgrad", &stem_conv_wgrad);
+  m.def("stem_conv_wgrad_bn", &stem_conv_wgrad_bn);
   m.def("conv3x3s1_wgrad", &conv3x3s1_wgrad);
   m.def("conv1x1_wgrad", &conv1x1_wgrad);
   m.def("conv1x1_wgrad_tune", [](int target_wgs, int variant, int interleave) { pdt_conv1x1_wgrad_tune(target_wgs, variant, interleave); },

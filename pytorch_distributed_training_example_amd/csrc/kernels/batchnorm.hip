@@ -805,11 +805,11 @@ inline int apply_grid(int64_t nvec) {
 int bn_bwd_from_partials(const float* part, int T, int BMt, const uint16_t* dy, const uint16_t* x,
                          const uint8_t* mask, const float* gamma, const float* mean, const float* invstd, int64_t M,
                          int C, int relu, int has_res, uint16_t* dx, uint16_t* dres, float* dgamma, float* dbeta,
-                         float* ws, hipStream_t s) {
+                         float* ws, hipStream_t s, float* coef = nullptr) {
   if (relu && !mask) return -2;
   const int P = (T + kTilesPerBlock - 1) / kTilesPerBlock;
   double* lv = reinterpret_cast<double*>(ws);
-  float* A = ws + 4 * (int64_t)P * C;
+  float* A = coef ? coef : ws + 4 * (int64_t)P * C;  // coef: the caller's [3][C] (A, B, D)
   float* B = A + C;
   float* D = B + C;
   FinArgs fa{};
@@ -817,6 +817,7 @@ int bn_bwd_from_partials(const float* part, int T, int BMt, const uint16_t* dy, 
   fa.M = M;
   hipLaunchKernelGGL(bn_tiles_l1_kernel<false>, dim3(C / 64, P), dim3(1024), 0, s, part, T, BMt, M, C, lv);
   hipLaunchKernelGGL(bn_tiles_l2b_kernel, dim3((C + 255) / 256), dim3(256), 0, s, lv, P, C, fa);
+  if (!dx) return 0;  // coefficients only: the consumer applies them (pdt_stem_conv_wgrad_bn)
   const int64_t nvec = M * C / 8;
   const int fixed = (2048 % C) == 0;
   const int grid = apply_grid(nvec);
@@ -1042,6 +1043,22 @@ int pdt_maxpool3s2_bwd_bn(const uint16_t* dy, const uint8_t* code, uint16_t* dz,
                      part);
   return bn_bwd_from_partials(part, T, 1, dz, x, nullptr, gamma, mean, invstd, M, C, 0, 0, dx, nullptr, dgamma, dbeta,
                               ws, s);
+}
+
+// Same, without the apply: dz and the dx coefficients coef [3][C] = A, B, D (dx = A dz + B (x - mean)
+// + D) for a consumer that applies them on load (the stem weight gradient).
+int pdt_maxpool3s2_bwd_bn_coef(const uint16_t* dy, const uint8_t* code, uint16_t* dz, int N, int H, int W, int C,
+                               const uint16_t* x, const float* gamma, const float* mean, const float* invstd,
+                               float* coef, float* dgamma, float* dbeta, float* part, float* ws, hipStream_t s) {
+  if (C != 64 || !coef) return -1;
+  const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  const int64_t M = (int64_t)N * H * W;
+  if (M < 1) return -1;
+  const int T = pdt_maxpool_bn_parts(N, H);
+  hipLaunchKernelGGL(maxpool_bwd_kernel<true>, dim3(T), dim3(256), 0, s, dy, code, dz, N, H, W, C, Ho, Wo, x, mean,
+                     part);
+  return bn_bwd_from_partials(part, T, 1, dz, x, nullptr, gamma, mean, invstd, M, C, 0, 0, nullptr, nullptr, dgamma,
+                              dbeta, ws, s, coef);
 }
 
 }  // extern "C"

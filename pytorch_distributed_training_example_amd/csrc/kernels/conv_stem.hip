@@ -257,6 +257,11 @@ __global__ __launch_bounds__(kThreads, 2) void stem_conv_kernel(const uint16_t* 
 //     channels) goes through registers like the forward's; one barrier per tile;
 //   * persistent, 1 workgroup per CU; the 4 pixel groups are summed through LDS at the end and
 //     each workgroup writes one fp32 partial, summed in a fixed order by stem_wgrad_reduce_kernel.
+//   * BNA: the stem BatchNorm's backward apply happens on the way in. dY is then the gradient at
+//     the BN output (the max-pool gradient dz) and Xb the BN input: both tiles arrive by LDS-DMA
+//     and one in-place pass turns them into dx = A dz + B (xb - mean) + D (the formula and the bf16
+//     rounding of bn_bwd_apply_kernel), so the BN's dx — written and re-read once each by the
+//     separate apply pass — never exists in HBM.
 constexpr int kGThreads = 512;
 constexpr int kGRowsOut = 2;
 constexpr int kGInRows = 2 * kGRowsOut + 5;  // 9
@@ -268,7 +273,9 @@ constexpr int kGInPitch = kGCols * 8;  // unpadded: a patch half (4 pixels) is 3
 constexpr int kGMaxPx = kGRowsOut * kTW;     // 224
 constexpr int kGDy = kGMaxPx * 128;          // dY tile [224 px][64 co] bf16
 constexpr int kGBuf = kGDy + kGInRows * kGInPitch;
-constexpr int kGLds = 2 * kGBuf;             // 90,768 B
+constexpr int kGLds = 2 * kGBuf;             // 90,752 B
+constexpr int kGBufB = kGBuf + kGDy;         // BNA: + the BN input tile
+constexpr int kGLdsB = 2 * kGBufB + 4 * 64 * 4;  // + the coefficient table A, B, D, mean: 148,864 B
 constexpr int kGK = 7 * 32;                  // padded patch length (kh x kw 8 x ci 4)
 constexpr int kGPairs = kGCols / 2;
 constexpr int kGItems = kGInRows * kGPairs;  // 1,044 pixel pairs per window
@@ -298,11 +305,24 @@ __device__ __forceinline__ bf16x8 tr8(const char* p0, const char* p1) {
 #ifndef PDT_STEM_WG_PROBE
 #define PDT_STEM_WG_PROBE 0  // diagnostics only: 1 = staging without compute, 2 = compute without staging
 #endif
+template <bool BNA>
 __global__ __launch_bounds__(kGThreads, 1) void stem_wgrad_kernel(const uint16_t* __restrict__ X,
                                                                   const uint16_t* __restrict__ dY,
                                                                   float* __restrict__ ws, int H, int W, int OH,
-                                                                  int OW, int nrt, int ntiles) {
+                                                                  int OW, int nrt, int ntiles,
+                                                                  const uint16_t* __restrict__ Xb = nullptr,
+                                                                  const float* __restrict__ coef = nullptr,
+                                                                  const float* __restrict__ mean = nullptr) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
+  constexpr int kBuf = BNA ? kGBufB : kGBuf;
+  float* const ctab = reinterpret_cast<float*>(lds + 2 * kGBufB);  // BNA: [A | B | D | mean][64]
+  if (BNA && threadIdx.x < 64) {
+    const int c = threadIdx.x;
+    ctab[c] = coef[c];
+    ctab[64 + c] = coef[64 + c];
+    ctab[128 + c] = coef[128 + c];
+    ctab[192 + c] = mean[c];
+  }
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int per = ntiles / gridDim.x, rem = ntiles % gridDim.x;
   const int t0 = blockIdx.x * per + min((int)blockIdx.x, rem);
@@ -311,15 +331,59 @@ __global__ __launch_bounds__(kGThreads, 1) void stem_wgrad_kernel(const uint16_t
   const int nks = P >> 5;
 
   // ---- staging: dY tile by DMA (P/8 instructions of 8 rows; instruction q by wave q % 8)
-  auto dma_dy = [&](int t, char* buf) {
+  auto dma_tile = [&](const uint16_t* base, int t, char* buf) {
     const int n = t / nrt, oh0 = (t - n * nrt) * kGRowsOut;
-    const uint16_t* src0 = dY + (int64_t)(n * OH + oh0) * OW * 64;
+    const uint16_t* src0 = base + (int64_t)(n * OH + oh0) * OW * 64;
     const int vrows = min(kGRowsOut, OH - oh0) * OW;  // valid pixel rows of the tile
     for (int q = wid; q < (P >> 3); q += 8) {
       const int r = q * 8 + (lane >> 3), pos = lane & 7;
       const int chunk = pos ^ (((r >> 1) & 3) << 1);
       const void* src = r < vrows ? (const void*)(src0 + (int64_t)r * 64 + chunk * 8) : (const void*)g_stem_zero;
       dma16_opaque(src, buf + q * 1024);
+    }
+  };
+  auto dma_dy = [&](int t, char* buf) {
+    dma_tile(dY, t, buf);
+    if (BNA) dma_tile(Xb, t, buf + kGBuf);
+  };
+  // BNA: dz tile (buf) and BN input tile (buf + kGBuf), same swizzled layout -> dx in place of dz.
+  // Thread: channel chunk tid % 8 (its 8 coefficients), rows tid / 8 + 64 u; LDS position of its
+  // chunk in row r = chunk ^ swizzle(r). Rows past the tile's valid pixels stay zero.
+  auto bn_apply_tile = [&](int t, char* buf) {
+    const int n = t / nrt, oh0 = (t - n * nrt) * kGRowsOut;
+    const int vrows = min(kGRowsOut, OH - oh0) * OW;
+    // one row at a time, coefficients re-read from LDS per row, and the thread index passed through
+    // an opaque move so its derived addresses are not hoisted out of the tile loop: this kernel's
+    // compute phase already holds 256 VGPRs, so nothing of the apply may stay live across it
+    int tix;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(tix) : "v"((int)threadIdx.x));
+    const int cc = tix & 7;
+#pragma unroll 1
+    for (int u = 0; u < (kGMaxPx + 63) / 64; ++u) {
+      const int r = (tix >> 3) + 64 * u;
+      if (r >= P) break;
+      char* pz = buf + r * 128 + ((cc ^ (((r >> 1) & 3) << 1)) * 16);
+      float o[8];
+      if (r < vrows) {
+        float g[8], xf[8], av[8], bv[8], dv[8], mv[8];
+        ld8_bf16(reinterpret_cast<const uint16_t*>(pz), g);
+        ld8_bf16(reinterpret_cast<const uint16_t*>(pz + kGBuf), xf);
+        const float4* ct = reinterpret_cast<const float4*>(ctab + cc * 8);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const float4 a4 = ct[h], b4 = ct[16 + h], d4 = ct[32 + h], m4 = ct[48 + h];
+          av[4 * h] = a4.x; av[4 * h + 1] = a4.y; av[4 * h + 2] = a4.z; av[4 * h + 3] = a4.w;
+          bv[4 * h] = b4.x; bv[4 * h + 1] = b4.y; bv[4 * h + 2] = b4.z; bv[4 * h + 3] = b4.w;
+          dv[4 * h] = d4.x; dv[4 * h + 1] = d4.y; dv[4 * h + 2] = d4.z; dv[4 * h + 3] = d4.w;
+          mv[4 * h] = m4.x; mv[4 * h + 1] = m4.y; mv[4 * h + 2] = m4.z; mv[4 * h + 3] = m4.w;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = av[j] * g[j] + bv[j] * (xf[j] - mv[j]) + dv[j];
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = 0.f;
+      }
+      st8_bf16(reinterpret_cast<uint16_t*>(pz), o);
     }
   };
   uint3 xv[kGRounds];
@@ -375,9 +439,14 @@ __global__ __launch_bounds__(kGThreads, 1) void stem_wgrad_kernel(const uint16_t
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   for (int k = 0; k < cnt; ++k) {
-    char* const buf = lds + (k & 1) * kGBuf;
-    char* const nbuf = lds + ((k + 1) & 1) * kGBuf;
-    if (PDT_STEM_WG_PROBE != 2 && k + 1 < cnt) {
+    char* const buf = lds + (k & 1) * kBuf;
+    char* const nbuf = lds + ((k + 1) & 1) * kBuf;
+    if (BNA) {  // this tile's DMA landed before the last barrier; the next tile's goes to nbuf
+      if (k + 1 < cnt) dma_dy(t0 + k + 1, nbuf);
+      bn_apply_tile(t0 + k, buf);
+      __syncthreads();
+      if (k + 1 < cnt) load_x(t0 + k + 1);  // after the apply: its registers are not live across it
+    } else if (PDT_STEM_WG_PROBE != 2 && k + 1 < cnt) {
       load_x(t0 + k + 1);
       dma_dy(t0 + k + 1, nbuf);
     }
@@ -386,32 +455,46 @@ __global__ __launch_bounds__(kGThreads, 1) void stem_wgrad_kernel(const uint16_t
     // steps' fragments are read before the first MFMA so the second batch of reads overlaps it
     const int j0 = (pgrp - (t0 + k)) & 3;
     const int nj = PDT_STEM_WG_PROBE == 1 ? 0 : (j0 < nks) + (j0 + 4 < nks);
-    bf16x8 a[2][4], bx[2][7];
+    auto frags = [&](int u, bf16x8 (&au)[4], bf16x8 (&bu)[7]) {
+      const int r0 = (j0 + 4 * u) * 32 + 4 * g + rsub, r1 = r0 + 16;
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      if (u < nj) {
-        const int r0 = (j0 + 4 * u) * 32 + 4 * g + rsub, r1 = r0 + 16;
+      for (int cb = 0; cb < 4; ++cb) au[cb] = tr8(buf + r0 * 128 + dyo[cb], buf + r1 * 128 + dyo[cb]);
+      // window address of pixel r: row 2 (r >= OW), column 2 (r mod OW) + 1, plus this lane's piece
+      const int h0 = r0 >= OW, h1 = r1 >= OW;
+      const char* x0 = win + 2 * h0 * kGInPitch + (2 * (r0 - h0 * OW) + csub + 1) * 8;
+      const char* x1 = win + 2 * h1 * kGInPitch + (2 * (r1 - h1 * OW) + csub + 1) * 8;
 #pragma unroll
-        for (int cb = 0; cb < 4; ++cb) a[u][cb] = tr8(buf + r0 * 128 + dyo[cb], buf + r1 * 128 + dyo[cb]);
-        // window address of pixel r: row 2 (r >= OW), column 2 (r mod OW) + 1, plus this lane's piece
-        const int h0 = r0 >= OW, h1 = r1 >= OW;
-        const char* x0 = win + 2 * h0 * kGInPitch + (2 * (r0 - h0 * OW) + csub + 1) * 8;
-        const char* x1 = win + 2 * h1 * kGInPitch + (2 * (r1 - h1 * OW) + csub + 1) * 8;
+      for (int b = 0; b < 7; ++b) {
+        const int kb = 7 * khalf + b;
+        const int off = (kb >> 1) * kGInPitch + (kb & 1) * 32;
+        bu[b] = tr8(x0 + off, x1 + off);
+      }
+    };
+    if constexpr (BNA) {  // one k-step's fragments at a time: 44 fewer live VGPRs (no spills)
 #pragma unroll
-        for (int b = 0; b < 7; ++b) {
-          const int kb = 7 * khalf + b;
-          const int off = (kb >> 1) * kGInPitch + (kb & 1) * 32;
-          bx[u][b] = tr8(x0 + off, x1 + off);
+      for (int u = 0; u < 2; ++u) {
+        if (u < nj) {
+          bf16x8 a[4], bx[7];
+          frags(u, a, bx);
+#pragma unroll
+          for (int b = 0; b < 7; ++b)
+#pragma unroll
+            for (int cb = 0; cb < 4; ++cb) acc[cb][b] = mfma(a[cb], bx[b], acc[cb][b]);
         }
       }
-    }
+    } else {
+      bf16x8 a[2][4], bx[2][7];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      if (u < nj) {
+      for (int u = 0; u < 2; ++u)
+        if (u < nj) frags(u, a[u], bx[u]);
 #pragma unroll
-        for (int b = 0; b < 7; ++b)
+      for (int u = 0; u < 2; ++u) {
+        if (u < nj) {
 #pragma unroll
-          for (int cb = 0; cb < 4; ++cb) acc[cb][b] = mfma(a[u][cb], bx[u][b], acc[cb][b]);  // D[co][patch k]
+          for (int b = 0; b < 7; ++b)
+#pragma unroll
+            for (int cb = 0; cb < 4; ++cb) acc[cb][b] = mfma(a[u][cb], bx[u][b], acc[cb][b]);  // D[co][patch k]
+        }
       }
     }
     if (PDT_STEM_WG_PROBE != 2 && k + 1 < cnt) store_x(nbuf + kGDy);
@@ -520,21 +603,44 @@ static int stem_ncu() {
 // fp32 workspace floats for pdt_stem_conv_wgrad (one [64][224] partial per workgroup).
 extern "C" int64_t pdt_stem_wgrad_ws_floats() { return (int64_t)stem_ncu() * 64 * kGK; }
 
-// dw [64, 3, 7, 7] (channels_last storage [64][7][7][3], bf16) of the stem conv from x [N, 3, H, W]
-// and dy [N, 64, OH, OW] (both channels_last). Requires W % 32 == 0 and W <= 224 (OW <= 112).
-extern "C" int pdt_stem_conv_wgrad(const uint16_t* x, const uint16_t* dy, uint16_t* dw, float* ws, int N, int H,
-                                   int W, hipStream_t s) {
+namespace {
+int stem_wgrad_launch(const uint16_t* x, const uint16_t* dy, const uint16_t* xb, const float* coef, const float* mean,
+                      uint16_t* dw, float* ws, int N, int H, int W, hipStream_t s) {
   if (N < 1 || H < 1 || W < 32 || W % 32 != 0 || W > 2 * kTW) return -1;
   const int OH = (H - 1) / 2 + 1, OW = W / 2;
-  static const bool attr_ok = hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_wgrad_kernel),
-                                                  hipFuncAttributeMaxDynamicSharedMemorySize, kGLds) == hipSuccess;
+  static const bool attr_ok =
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_wgrad_kernel<false>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, kGLds) == hipSuccess &&
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_wgrad_kernel<true>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, kGLdsB) == hipSuccess;
   if (!attr_ok) return -2;
   const int nrt = (OH + kGRowsOut - 1) / kGRowsOut;
   const int64_t ntiles = (int64_t)N * nrt;
   if (ntiles > 0x7fffffff || (int64_t)N * OH * OW * 64 > 0x7fffffffLL * 4) return -3;
   const int grid = (int)std::min<int64_t>(ntiles, stem_ncu());
-  hipLaunchKernelGGL(stem_wgrad_kernel, dim3(grid), dim3(kGThreads), kGLds, s, x, dy, ws, H, W, OH, OW, nrt,
-                     (int)ntiles);
+  if (xb)
+    hipLaunchKernelGGL(stem_wgrad_kernel<true>, dim3(grid), dim3(kGThreads), kGLdsB, s, x, dy, ws, H, W, OH, OW, nrt,
+                       (int)ntiles, xb, coef, mean);
+  else
+    hipLaunchKernelGGL(stem_wgrad_kernel<false>, dim3(grid), dim3(kGThreads), kGLds, s, x, dy, ws, H, W, OH, OW, nrt,
+                       (int)ntiles, nullptr, nullptr, nullptr);
   hipLaunchKernelGGL(stem_wgrad_reduce_kernel, dim3(64 * kGK / 256), dim3(1024), 0, s, ws, grid, dw);
   return hipGetLastError() == hipSuccess ? 0 : -4;
+}
+}  // namespace
+
+// dw [64, 3, 7, 7] (channels_last storage [64][7][7][3], bf16) of the stem conv from x [N, 3, H, W]
+// and dy [N, 64, OH, OW] (both channels_last). Requires W % 32 == 0 and W <= 224 (OW <= 112).
+extern "C" int pdt_stem_conv_wgrad(const uint16_t* x, const uint16_t* dy, uint16_t* dw, float* ws, int N, int H,
+                                   int W, hipStream_t s) {
+  return stem_wgrad_launch(x, dy, nullptr, nullptr, nullptr, dw, ws, N, H, W, s);
+}
+
+// Same, with the stem BatchNorm's backward apply fused into the dY load: dz [N, 64, OH, OW] is the
+// gradient at the BN output, xb the BN input (the stem conv output), coef [3][64] = A, B, D and mean
+// [64] as bn_bwd_apply_kernel takes them; the conv's dY = A dz + B (xb - mean) + D (bf16).
+extern "C" int pdt_stem_conv_wgrad_bn(const uint16_t* x, const uint16_t* dz, const uint16_t* xb, const float* coef,
+                                      const float* mean, uint16_t* dw, float* ws, int N, int H, int W, hipStream_t s) {
+  if (!xb || !coef || !mean) return -1;
+  return stem_wgrad_launch(x, dz, xb, coef, mean, dw, ws, N, H, W, s);
 }

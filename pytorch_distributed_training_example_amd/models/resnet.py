@@ -20,7 +20,7 @@ import torch
 from torch import nn
 
 from ..ops.batchnorm import BatchNorm2d, ResidualGradLink
-from ..ops.conv import Conv1x1, SplitConv2d, linked_conv
+from ..ops.conv import Conv1x1, SplitConv2d, linked_conv, stem_block
 
 
 def conv3x3(inp: int, out: int, stride: int = 1, groups: int = 1, dilation: int = 1) -> nn.Conv2d:
@@ -183,7 +183,10 @@ class ResNet(nn.Module):
         return nn.Sequential(*layers)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        if hasattr(self.bn1, "forward_relu_maxpool"):  # fused BN+ReLU+pool: stem output never stored
+        y = stem_block(self.conv1, self.bn1, x)  # one node: the BN's backward apply goes into the wgrad
+        if y is not None:
+            x = y
+        elif hasattr(self.bn1, "forward_relu_maxpool"):  # fused BN+ReLU+pool: stem output never stored
             x = self.bn1.forward_relu_maxpool(self.conv1(x))
         else:
             x = self.maxpool(bn_act(self.bn1, self.conv1(x), relu=True))

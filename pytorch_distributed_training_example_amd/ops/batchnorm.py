@@ -381,8 +381,9 @@ class BatchNorm2d(nn.BatchNorm2d):
         return batch_norm_act(x, None, w, b, rm, rv, training, momentum if momentum is not None else 0.0,
                               self.eps, False, None, grad_link, defer_apply=True)
 
-    def forward_relu_maxpool(self, x: torch.Tensor) -> torch.Tensor:
-        """``max_pool2d(relu(bn(x)), 3, 2, 1)`` (ResNet stem) with the pool fused into the BN apply."""
+    def _step_args(self):
+        """Per-call arguments of a training / eval forward (counts the batch, as ``forward`` does):
+        (training, weight, bias, running_mean, running_var, momentum, eps)."""
         training = self.training or not self.track_running_stats
         momentum = self.momentum
         if self.training and self.track_running_stats:
@@ -393,8 +394,18 @@ class BatchNorm2d(nn.BatchNorm2d):
         rv = self.running_var if (not self.training or self.track_running_stats) else None
         w = self.weight if self.affine else None
         b = self.bias if self.affine else None
-        return batch_norm_relu_maxpool(x, w, b, rm, rv, training, momentum if momentum is not None else 0.0,
-                                       self.eps)
+        return training, w, b, rm, rv, float(momentum if momentum is not None else 0.0), float(self.eps)
+
+    def forward_relu_maxpool(self, x: torch.Tensor) -> torch.Tensor:
+        """``max_pool2d(relu(bn(x)), 3, 2, 1)`` (ResNet stem) with the pool fused into the BN apply."""
+        training, w, b, rm, rv, momentum, eps = self._step_args()
+        return batch_norm_relu_maxpool(x, w, b, rm, rv, training, momentum, eps)
+
+    def stem_params(self):
+        """(weight, bias, running_mean, running_var, momentum, eps) of one training forward of the
+        stem's fused conv + BN + ReLU + pool node (``ops.conv.stem_block``); counts the batch."""
+        _, w, b, rm, rv, momentum, eps = self._step_args()
+        return w, b, rm, rv, momentum, eps
 
     def sync_num_batches_tracked(self) -> None:
         if self.track_running_stats and self._nbt:

@@ -592,6 +592,64 @@ def stem_eligible(conv: nn.Conv2d, x: torch.Tensor) -> bool:
             and SW.conv_stem == "ours" and not disabled())
 
 
+class _StemBlockFn(torch.autograd.Function):
+    """ResNet stem in training: conv 7x7/s2 -> BatchNorm -> ReLU -> MaxPool2d(3, 2, 1) as ONE autograd
+    node, so its backward can hand the BatchNorm's backward apply to the stem weight-gradient kernel:
+    the pool-gradient kernel takes the BN reduction and yields dz (the gradient at the BN output) and
+    the dx coefficients, and ``stem_conv_wgrad_bn`` forms dx = A dz + B (x - mean) + D while loading
+    its operand — the BN's dx (1.6 GB at batch 1024) is never written or read back. Forward is the
+    same two kernels as the unfused modules (stem conv, BN + ReLU + pool)."""
+
+    @staticmethod
+    def forward(ctx, img, weight, gamma, beta, running_mean, running_var, momentum, eps):
+        from ._native import native
+        n = native()
+        xb = n.stem_conv_fwd(img, weight)
+        y, code, mean, invstd = n.bn_relu_maxpool_fwd(xb, gamma, beta, running_mean, running_var, momentum, eps)
+        ctx.save_for_backward(img, weight, xb, code, gamma, mean, invstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from ._native import native
+        n = native()
+        img, weight, xb, code, gamma, mean, invstd = ctx.saved_tensors
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        need_bn = ctx.needs_input_grad[2] or ctx.needs_input_grad[3]
+        dimg = dw = None
+        if ctx.needs_input_grad[0]:  # training never asks for the image gradient: the unfused chain
+            dx, dg, db = n.maxpool3s2_bwd_bn(dy, code, xb, gamma, mean, invstd, need_bn)
+            args = (dx, img, weight, None, [2, 2], [3, 3], [1, 1], False, [0, 0], 1)
+            dimg = torch.ops.aten.convolution_backward(*args, [True, False, False])[0]
+            if ctx.needs_input_grad[1]:
+                dw = n.stem_conv_wgrad(img, dx)
+        else:
+            dz, coef, dg, db = n.maxpool3s2_bwd_bn_coef(dy, code, xb, gamma, mean, invstd, need_bn)
+            if ctx.needs_input_grad[1]:
+                dw = n.stem_conv_wgrad_bn(img, dz, xb, coef, mean)
+        return dimg, dw, (dg if need_bn else None), (db if need_bn else None), None, None, None, None
+
+
+def _has_hooks(m: nn.Module) -> bool:
+    from torch.nn.modules import module as _m
+    return bool(m._forward_hooks or m._forward_pre_hooks or _m._global_forward_hooks
+                or _m._global_forward_pre_hooks)
+
+
+def stem_block(conv: nn.Conv2d, bn: nn.Module, x: torch.Tensor):
+    """``max_pool2d(relu(bn(conv(x))), 3, 2, 1)`` as one ``_StemBlockFn`` node when our stem kernels
+    and the fused BN + pool path both apply in training (affine BN with running statistics, images
+    of width <= 224, no module hooks, ``PDT_STEM_BN_WGRAD=1``); None otherwise (the caller runs the
+    modules)."""
+    if not (SW.stem_bn_wgrad and SW.stem_bwd_fused and bn.training and torch.is_grad_enabled()
+            and isinstance(conv, SplitConv2d) and stem_eligible(conv, x) and x.shape[3] <= 224
+            and getattr(bn, "affine", False) and getattr(bn, "track_running_stats", False)
+            and hasattr(bn, "stem_params") and not _has_hooks(conv) and not bn.has_hooks()):
+        return None
+    w, b, rm, rv, momentum, eps = bn.stem_params()
+    return _StemBlockFn.apply(x, conv.weight, w, b, rm, rv, momentum, eps)
+
+
 class SplitConv2d(nn.Conv2d):
     """``nn.Conv2d`` (same parameters / state_dict). On the GPU, stride-1 and stride-2 3x3
     convolutions and the ResNet stem run on our MFMA kernels (``_Conv3x3Fn`` / ``_Conv3x3S2Fn`` /

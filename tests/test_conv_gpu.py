@@ -122,3 +122,66 @@ def test_stem_conv_ours_matches_fp32(monkeypatch, N, H, W, switch):
         err = ((a.float() - b).norm() / b.norm()).item()
         assert err < 1e-2, err
     torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=2e-2 * yr.abs().max().item() ** 0.5)
+
+
+@pytest.mark.parametrize("N,H,W", [(2, 224, 224), (3, 17, 64), (1, 9, 32), (2, 30, 96)])
+def test_stem_wgrad_with_fused_bn_apply(N, H, W):
+    """Stem weight gradient with the stem BatchNorm's backward apply fused into its load
+    (stem_conv_wgrad_bn, from maxpool3s2_bwd_bn_coef's dz and coefficients) against (a) the unfused
+    chain (maxpool3s2_bwd_bn's dx into stem_conv_wgrad) and (b) an fp32 weight gradient of the fp32
+    dx = A dz + B (xb - mean) + D. Odd output heights leave a partial last row tile."""
+    from pytorch_distributed_training_example_amd.ops._native import native
+    n = native()
+    cl = torch.channels_last
+    g = torch.Generator(device="cuda").manual_seed(N * H + W)
+    img = (torch.randn(N, 3, H, W, device="cuda", generator=g) + 0.5).bfloat16().contiguous(memory_format=cl)
+    w = (torch.randn(64, 3, 7, 7, device="cuda", generator=g) * 0.1).bfloat16().contiguous(memory_format=cl)
+    gamma = torch.rand(64, device="cuda", generator=g) + 0.5
+    beta = torch.randn(64, device="cuda", generator=g) * 0.1
+    rm, rv = torch.zeros(64, device="cuda"), torch.ones(64, device="cuda")
+    xb = n.stem_conv_fwd(img, w)
+    y, code, mean, invstd = n.bn_relu_maxpool_fwd(xb, gamma, beta, rm, rv, 0.1, 1e-5)
+    dy = torch.randn(y.shape, device="cuda", generator=g).bfloat16().contiguous(memory_format=cl)
+    dz, coef, dg, db = n.maxpool3s2_bwd_bn_coef(dy, code, xb, gamma, mean, invstd, True)
+    dx, dg2, db2 = n.maxpool3s2_bwd_bn(dy, code, xb, gamma, mean, invstd, True)
+    assert coef.shape == (3, 64) and torch.equal(dg, dg2) and torch.equal(db, db2)
+    dx32 = coef[0].view(1, 64, 1, 1) * dz.float() + coef[1].view(1, 64, 1, 1) * (
+        xb.float() - mean.view(1, 64, 1, 1)) + coef[2].view(1, 64, 1, 1)
+    torch.testing.assert_close(dx.float(), dx32, rtol=1e-2, atol=1e-2 * dx32.abs().max().item())
+    fused = n.stem_conv_wgrad_bn(img, dz, xb, coef, mean).float()
+    unfused = n.stem_conv_wgrad(img, dx).float()
+    assert ((fused - unfused).norm() / unfused.norm()).item() < 1e-3
+    ref = torch.nn.grad.conv2d_weight(img.float(), (64, 3, 7, 7), dx32, stride=2, padding=3)
+    assert ((fused - ref).norm() / ref.norm()).item() < 1e-2
+
+
+def test_resnet_stem_block_node(switch):
+    """ResNet-50's stem as one node (conv + BN + ReLU + pool, BN backward apply inside the weight-
+    gradient kernel; PDT_STEM_BN_WGRAD=1) gives the forward output, running statistics and stem
+    gradients of the separate-module path (=0), and its kernel is the one that ran."""
+    from pytorch_distributed_training_example_amd.models import resnet as R
+    from pytorch_distributed_training_example_amd.models.precision import to_bf16_mixed
+    from pytorch_distributed_training_example_amd.ops import conv as C
+    torch.manual_seed(0)
+    net = to_bf16_mixed(R.resnet50(num_classes=10).cuda().to(memory_format=torch.channels_last))
+    x = torch.randn(2, 3, 64, 96, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    out, calls = {}, []
+    orig = C._StemBlockFn.apply
+    for on in ("1", "0"):
+        switch("PDT_STEM_BN_WGRAD", on)
+        net.zero_grad(set_to_none=True)
+        rm0 = net.bn1.running_mean.clone()
+        C._StemBlockFn.apply = staticmethod(lambda *a: calls.append(on) or orig(*a))
+        try:
+            y = net(x)
+        finally:
+            C._StemBlockFn.apply = orig
+        y.float().square().mean().backward()
+        out[on] = [y.float(), net.bn1.running_mean - rm0, net.conv1.weight.grad.float(),
+                   net.bn1.weight.grad.float(), net.bn1.bias.grad.float()]
+        with torch.no_grad():
+            net.bn1.running_mean.copy_(rm0)
+    assert calls == ["1"]
+    for a, b in zip(out["1"], out["0"]):
+        err = ((a - b).norm() / (b.norm() + 1e-12)).item()
+        assert err < 1e-2, err
