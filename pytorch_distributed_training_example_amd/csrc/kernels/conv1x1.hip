@@ -204,32 +204,63 @@ __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv1x1_kernel(
 #pragma unroll
     for (int k = 0; k < 8; ++k) { bs1[k] = 0.f; bs2[k] = 0.f; }
   }
-  for (int idx = tid; idx < BM * kChunks; idx += Cf::kThreads) {
-    const int r = idx / kChunks, c = idx % kChunks;
+  // A thread keeps one 8-channel chunk c and rows r0 + kRowStep * it. Every global load of the
+  // epilogue (the accumulate source, its ReLU mask, the BSTATS input and mask) is issued for all
+  // kIt rows before the first use: one memory latency per tile instead of one per row (issued per
+  // row, the dgrad+accumulate kernels ran at ~2.7 TB/s, latency bound in this epilogue). The loads
+  // of a row precede its store, and no other thread touches it, so c may alias y.
+  // (Both sources at 128 VGPRs — the 8-wave tile with ACC and BSTATS — go in two batches of rows:
+  // all eight rows at once spilled there.)
+  constexpr int kRowStep = Cf::kThreads / kChunks, kIt = BM / kRowStep;
+  constexpr int kB = (ACC && BSTATS && Cf::kWaves == 8) ? kIt / 2 : kIt;
+  static_assert(kRowStep * kIt == BM && kIt % kB == 0, "epilogue rows");
+  const int r0 = tid / kChunks, c = tid % kChunks;
+#pragma unroll 1
+  for (int h = 0; h < kIt; h += kB) {
+  uint4 cv[kB], xbv[kB];
+  unsigned cmk[kB], bmkv[kB];
+#pragma unroll
+  for (int it = 0; it < kB; ++it) {
+    const int m = m0 + r0 + kRowStep * (h + it);
+    cmk[it] = 0u;
+    bmkv[it] = 0xffu;
+    if (m >= M) continue;
+    const int64_t off = (int64_t)m * N + n0 + c * 8;
+    if constexpr (BSTATS) {
+      xbv[it] = *reinterpret_cast<const uint4*>(bs.x + off);
+      if (bs.mask) bmkv[it] = bs.mask[off >> 3];
+    }
+    if constexpr (ACC) {
+      cmk[it] = Cmask ? Cmask[off >> 3] : 0xffu;  // C = Cin * mask: a ReLU's masked gradient
+      if (cg.s) {  // compact strided source
+        const int w = m % cg.W, t = m / cg.W, h = t % cg.H, n = t / cg.H;
+        if (h % cg.s == 0 && w % cg.s == 0)
+          cv[it] = *reinterpret_cast<const uint4*>(Cin + ((int64_t)(n * cg.Hs + h / cg.s) * cg.Ws + w / cg.s) * N +
+                                                   n0 + c * 8);
+        else
+          cmk[it] = 0u;
+      } else {
+        cv[it] = *reinterpret_cast<const uint4*>(Cin + off);
+      }
+    }
+  }
+#pragma unroll
+  for (int it = 0; it < kB; ++it) {
+    const int r = r0 + kRowStep * (h + it);
     const int m = m0 + r;
     if (m >= M) continue;
     uint4 v = *reinterpret_cast<const uint4*>(lds + r * Cf::kEpiStride + c * 16);
     const int64_t off = (int64_t)m * N + n0 + c * 8;
-    uint4 xb;
-    unsigned bmk = 0xffu;
-    if constexpr (BSTATS) {  // issued before the accumulate's loads: both in flight together
-      xb = *reinterpret_cast<const uint4*>(bs.x + off);
-      if (bs.mask) bmk = bs.mask[off >> 3];
-    }
     if constexpr (ACC) {
       float a[8], cc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
       const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
       for (int k = 0; k < 4; ++k) { a[2 * k] = __uint_as_float(w[k] << 16); a[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u); }
-      unsigned mb = Cmask ? Cmask[off >> 3] : 0xffu;  // C = Cin * mask: a ReLU's masked gradient
-      if (cg.s) {  // compact strided source
-        const int w = m % cg.W, t = m / cg.W, h = t % cg.H, n = t / cg.H;
-        if (h % cg.s == 0 && w % cg.s == 0)
-          ld8_bf16(Cin + ((int64_t)(n * cg.Hs + h / cg.s) * cg.Ws + w / cg.s) * N + n0 + c * 8, cc);
-        else
-          mb = 0u;
-      } else {
-        ld8_bf16(Cin + off, cc);
+      const unsigned mb = cmk[it];
+      if (mb) {
+        const uint32_t cw[4] = {cv[it].x, cv[it].y, cv[it].z, cv[it].w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) { cc[2 * k] = __uint_as_float(cw[k] << 16); cc[2 * k + 1] = __uint_as_float(cw[k] & 0xffff0000u); }
       }
 #pragma unroll
       for (int k = 0; k < 8; ++k) a[k] += (mb >> k) & 1u ? cc[k] : 0.f;
@@ -238,13 +269,14 @@ __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv1x1_kernel(
       v.z = (uint32_t)f2bf(a[4]) | ((uint32_t)f2bf(a[5]) << 16);
       v.w = (uint32_t)f2bf(a[6]) | ((uint32_t)f2bf(a[7]) << 16);
     }
-    if constexpr (BSTATS) bn_bwd_accum8(v, xb, bmk, bmu, bs1, bs2);
+    if constexpr (BSTATS) bn_bwd_accum8(v, xbv[it], bmkv[it], bmu, bs1, bs2);
     if constexpr (NT) {
       const u32x4 t = {v.x, v.y, v.z, v.w};
       __builtin_nontemporal_store(t, reinterpret_cast<u32x4*>(Y + off));
     } else {
       *reinterpret_cast<uint4*>(Y + off) = v;
     }
+  }
   }
 
   if constexpr (BSTATS)  // every wave is done reading the staged tile: its LDS holds the block sums
