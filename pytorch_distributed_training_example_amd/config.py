@@ -30,6 +30,8 @@ PDT_SUBSAMPLE_NATIVE        1            stride-2 gather / scatter-add kernels
 PDT_LINEAR_SPLITK           1            split-K Linear weight gradients
 PDT_FUSED_ADDLN             1            residual add fused into LayerNorm
 PDT_EMBEDDING_NATIVE        1            GPT-2 token/position embedding on our kernels
+PDT_BWD_FUSED               1            bottleneck conv3 + bn3 backward as one kernel (conv1x1_bwd_fused.hip):
+                                         bn3's backward apply formed on load, conv3 dgrad + wgrad + bn2 reduction
 PDT_LINEAR_EPILOGUE         0            1: Linear forward GEMMs (+bias, MLP fc1+bias+GELU) on our MFMA kernel
                                          (gemm.hip; 0.61-0.94x of tuned hipBLASLt, so off)
 """
@@ -42,7 +44,8 @@ class _Switches:
     __slots__ = ("disable_native", "conv1x1", "conv1x1_ours", "conv1x1_prefer", "conv1x1_override",
                  "conv1x1_table", "conv1x1_dump", "conv1x1_s2", "conv3x3", "conv3x3_wgrad", "conv3x3_s2", "conv_stem",
                  "conv_bn_stats", "bn_bwd_stats", "res_masked", "stem_bwd_fused", "stem_bn_wgrad", "wgrad_splitk", "slice_sum",
-                 "subsample_native", "linear_splitk", "fused_addln", "embedding_native", "linear_epilogue")
+                 "subsample_native", "linear_splitk", "fused_addln", "embedding_native", "linear_epilogue",
+                 "bwd_fused")
 
     def __init__(self):
         self.reload()
@@ -78,6 +81,7 @@ class _Switches:
         self.fused_addln = on("PDT_FUSED_ADDLN")
         self.embedding_native = on("PDT_EMBEDDING_NATIVE")
         self.linear_epilogue = e("PDT_LINEAR_EPILOGUE", "0") == "1"
+        self.bwd_fused = on("PDT_BWD_FUSED")
         return self
 
 

@@ -33,6 +33,18 @@ int pdt_mt_copy(int n, void* const* src, void* const* dst, const int64_t* numel,
 int pdt_l2norm_sq(int n, void* const* x, const int64_t* numel, int dtype, float* out, hipStream_t s);
 int pdt_clip_coef(const float* sumsq, float max_norm, float* coef, float* norm, hipStream_t s);
 int64_t pdt_bn_workspace_floats(int64_t M, int C);
+int pdt_bn_bwd_coef(const uint16_t* dy, const uint16_t* x, const uint8_t* mask, const float* gamma, const float* mean,
+                    const float* invstd, int64_t M, int C, int relu, float* coef, float* dgamma, float* dbeta, float* ws,
+                    unsigned* counters, hipStream_t s);
+int pdt_bn_bwd_coef_tiles(const float* part, int T, const float* gamma, const float* invstd, int64_t M, int C,
+                          float* coef, float* dgamma, float* dbeta, float* ws, hipStream_t s);
+int pdt_conv1x1_bwd_fused_ok(int C4, int CW);
+int pdt_conv1x1_bwd_fused_grid(int M);
+int pdt_conv1x1_bwd_fused(const uint16_t* dy, const uint16_t* z, const uint8_t* mz, const float* mean, const float* A,
+                          const float* B, const float* D, const uint16_t* wt, const uint16_t* xa, const uint16_t* bx,
+                          const uint8_t* bm, const float* bmean, float* bpart, uint16_t* dxa, uint16_t* dw, float* ws,
+                          int M, int C4, int CW, hipStream_t s);
+void pdt_conv1x1_bwd_fused_tune(int grid);
 void pdt_bn_tune(int variant, int target_blocks, int u_fwd, int u_bwd);
 int pdt_bn_fwd_train(const uint16_t* x, const uint16_t* res, const float* res_a, const float* res_b,
                      const float* gamma, const float* beta,
@@ -131,17 +143,17 @@ int pdt_fp8_cast_transpose(const uint16_t* x, int64_t M, int64_t K, const float*
                            uint8_t* out_t, float* amax, hipStream_t s);
 int pdt_fp8_update_scales(float* state, int n, int L, float margin_scale, hipStream_t s);
 int pdt_embedding_fwd(const int64_t* idx, const uint16_t* wte, const uint16_t* wpe, uint16_t* out, int64_t n, int T,
-                      int D, hipStream_t s);
+                      int D, int V, int* err, hipStream_t s);
 int64_t pdt_embedding_bwd_ws_ints(int64_t n, int V);
 int pdt_gemm_nt(const uint16_t* A, const uint16_t* B, uint16_t* C, uint16_t* G, const void* bias, int bias_f32,
                 int epi, int tanh_form, int M, int N, int K, hipStream_t s);
 int pdt_embedding_bwd(const int64_t* idx, const uint16_t* dout, uint16_t* dwte, uint16_t* dwpe, int* ws, int64_t n,
-                      int B, int T, int V, int D, hipStream_t s);
+                      int B, int T, int V, int D, int* err, hipStream_t s);
 int64_t pdt_p2p_flags_bytes();
 int64_t pdt_p2p_data_bytes(int64_t cap);
 int pdt_p2p_allreduce(const void* in, void* out, int64_t n, int dtype, char* const* data_ptrs,
                       uint32_t* const* flag_ptrs, int rank, int world, int64_t cap, float post_scale,
-                      uint32_t* st, int algo, int max_blocks, hipStream_t s);
+                      uint32_t* st, int algo, int max_blocks, double timeout_s, hipStream_t s);
 int pdt_colsum(const void* x, int dtype, int64_t N, int D, void* out, int odtype, float* ws, hipStream_t s);
 int pdt_slice_sum_bf16(const uint16_t* x, uint16_t* out, int S, int64_t n, hipStream_t s);
 int pdt_subsample_gather(const uint16_t* x, uint16_t* xs, int N, int H, int W, int C, int s, hipStream_t st);
@@ -600,6 +612,106 @@ std::vector<Tensor> bn_bwd_train_tiles(Tensor dy, Tensor x, Tensor part, c10::op
                                         need_dgamma ? db.data_ptr<float>() : nullptr, ws.data_ptr<float>(), stream());
   TORCH_CHECK(rc == 0, "pdt_bn_bwd_train_tiles failed: ", rc);
   return {dx, dres, dg, db};
+}
+
+// BN training backward WITHOUT the apply: {coef [3, C] (A, B, D: dx = A dy m + B (x - mean) + D),
+// dgamma, dbeta} for a consumer that forms dx while loading its operand (conv1x1_bwd_fused). The
+// reduction comes from the dy producer's partials [2, T, C] when given, else from a pass over (dy, x).
+std::vector<Tensor> bn_bwd_coef(Tensor dy, Tensor x, c10::optional<Tensor> part, c10::optional<Tensor> mask,
+                                c10::optional<Tensor> weight, Tensor mean, Tensor invstd, bool relu, bool need_dgamma) {
+  check_nhwc_bf16(x, "x");
+  const int64_t C = x.size(1);
+  const int64_t M = x.numel() / C;
+  TORCH_CHECK(C % 64 == 0, "pdt bn coef: C must be a multiple of 64");
+  auto fopt = x.options().dtype(at::kFloat);
+  auto coef = at::empty({3, C}, fopt);
+  Tensor dg, db;
+  if (need_dgamma) {
+    dg = at::empty({C}, fopt);
+    db = at::empty({C}, fopt);
+  }
+  int rc;
+  if (part.has_value() && part->defined()) {
+    TORCH_CHECK(part->scalar_type() == at::kFloat && part->is_contiguous() && part->dim() == 3 && part->size(0) == 2 &&
+                part->size(1) >= 1 && part->size(2) == C, "bn_bwd_coef: partials [2, T, C] fp32 expected");
+    const int T = (int)part->size(1);
+    auto ws = at::empty({pdt_bn_tiles_ws_floats(T, (int)C)}, fopt);
+    rc = pdt_bn_bwd_coef_tiles(part->data_ptr<float>(), T, opt_fptr(weight), invstd.data_ptr<float>(), M, (int)C,
+                               coef.data_ptr<float>(), need_dgamma ? dg.data_ptr<float>() : nullptr,
+                               need_dgamma ? db.data_ptr<float>() : nullptr, ws.data_ptr<float>(), stream());
+  } else {
+    TORCH_CHECK(dy.sizes() == x.sizes() && dy.strides() == x.strides(), "pdt bn coef: dy layout mismatch");
+    const uint8_t* mp = nullptr;
+    if (relu) {
+      TORCH_CHECK(mask.has_value() && mask->defined() && mask->numel() == M * C / 8, "pdt bn coef: relu needs the mask");
+      mp = mask->data_ptr<uint8_t>();
+    }
+    auto ws = at::empty({bn_ws_floats(M, C)}, fopt);
+    rc = pdt_bn_bwd_coef(reinterpret_cast<const uint16_t*>(dy.data_ptr()), reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                         mp, opt_fptr(weight), mean.data_ptr<float>(), invstd.data_ptr<float>(), M, (int)C, relu,
+                         coef.data_ptr<float>(), need_dgamma ? dg.data_ptr<float>() : nullptr,
+                         need_dgamma ? db.data_ptr<float>() : nullptr, ws.data_ptr<float>(), bn_counters(x), stream());
+  }
+  TORCH_CHECK(rc == 0, "pdt bn_bwd_coef failed: ", rc);
+  return {coef, dg, db};
+}
+
+// Fused backward of a bottleneck's last 1x1 conv (w [C4, CW, 1, 1]: CW -> C4) and the BatchNorm that
+// follows it (csrc/kernels/conv1x1_bwd_fused.hip): from dy (gradient at that BN's output), z (its
+// input), mz (its ReLU bits), mean and coef [3, C4] (A, B, D of bn_bwd_coef) and the conv input xa,
+// returns {dxa, dw, part}: the conv's data and weight gradients and, when bn_x / bn_mean are given
+// (xa is the output of a BatchNorm with input bn_x, ReLU bits bn_mask, batch mean bn_mean), that
+// BatchNorm's backward partials [2, G, CW] (else undefined). Empty list: shape not taken.
+std::vector<Tensor> conv1x1_bwd_fused(Tensor dy, Tensor z, Tensor mz, Tensor mean, Tensor coef, Tensor w, Tensor xa,
+                                      c10::optional<Tensor> bn_x, c10::optional<Tensor> bn_mask,
+                                      c10::optional<Tensor> bn_mean) {
+  check_nhwc_bf16(dy, "dy");
+  check_nhwc_bf16(z, "z");
+  check_nhwc_bf16(xa, "xa");
+  const int64_t C4 = z.size(1), CW = xa.size(1);
+  const int64_t M = z.numel() / C4;
+  if (!pdt_conv1x1_bwd_fused_ok((int)C4, (int)CW) || M * C4 >= ((int64_t)1 << 31)) return {};
+  TORCH_CHECK(dy.sizes() == z.sizes() && dy.strides() == z.strides(), "conv1x1_bwd_fused: dy / z layout mismatch");
+  TORCH_CHECK(xa.numel() == M * CW, "conv1x1_bwd_fused: xa pixels");
+  TORCH_CHECK(mz.scalar_type() == at::kByte && mz.numel() == M * C4 / 8 && mz.is_cuda(), "conv1x1_bwd_fused: mask");
+  TORCH_CHECK(mean.scalar_type() == at::kFloat && mean.numel() == C4 && coef.scalar_type() == at::kFloat &&
+              coef.is_contiguous() && coef.numel() == 3 * C4, "conv1x1_bwd_fused: mean [C4], coef [3, C4] fp32");
+  TORCH_CHECK(w.scalar_type() == at::kBFloat16 && w.numel() == C4 * CW && w.size(0) == C4,
+              "conv1x1_bwd_fused: weight [C4, CW, 1, 1] bf16");
+  auto wt = w.reshape({C4, CW}).t().contiguous();
+  auto dxa = at::empty_like(xa);
+  auto dw = at::empty({C4, CW}, w.options());
+  const int G = pdt_conv1x1_bwd_fused_grid((int)M);
+  auto fopt = z.options().dtype(at::kFloat);
+  auto ws = at::empty({(int64_t)G * C4 * CW}, fopt);
+  const bool bst = bn_x.has_value() && bn_x->defined();
+  Tensor part;
+  const uint16_t* bx = nullptr;
+  const uint8_t* bm = nullptr;
+  const float* bmu = nullptr;
+  if (bst) {
+    check_nhwc_bf16(*bn_x, "bn_x");
+    TORCH_CHECK(bn_x->numel() == M * CW && bn_mean.has_value() && bn_mean->defined() &&
+                bn_mean->scalar_type() == at::kFloat && bn_mean->numel() == CW, "conv1x1_bwd_fused: bn_x / bn_mean");
+    if (bn_mask.has_value() && bn_mask->defined()) {
+      TORCH_CHECK(bn_mask->scalar_type() == at::kByte && bn_mask->numel() == M * CW / 8, "conv1x1_bwd_fused: bn_mask");
+      bm = bn_mask->data_ptr<uint8_t>();
+    }
+    bx = reinterpret_cast<const uint16_t*>(bn_x->data_ptr());
+    bmu = bn_mean->data_ptr<float>();
+    part = at::empty({2, G, CW}, fopt);
+  }
+  const float* cp = coef.data_ptr<float>();
+  const int rc = pdt_conv1x1_bwd_fused(reinterpret_cast<const uint16_t*>(dy.data_ptr()),
+                                       reinterpret_cast<const uint16_t*>(z.data_ptr()), mz.data_ptr<uint8_t>(),
+                                       mean.data_ptr<float>(), cp, cp + C4, cp + 2 * C4,
+                                       reinterpret_cast<const uint16_t*>(wt.data_ptr()),
+                                       reinterpret_cast<const uint16_t*>(xa.data_ptr()), bx, bm, bmu,
+                                       bst ? part.data_ptr<float>() : nullptr, reinterpret_cast<uint16_t*>(dxa.data_ptr()),
+                                       reinterpret_cast<uint16_t*>(dw.data_ptr()), ws.data_ptr<float>(), (int)M, (int)C4,
+                                       (int)CW, stream());
+  TORCH_CHECK(rc == 0, "pdt_conv1x1_bwd_fused failed: ", rc);
+  return {dxa, dw.view(w.sizes()), part};
 }
 
 // ----------------------------------------------------------------------------- 1x1 conv GEMM (+ BN stats)
@@ -1309,7 +1421,7 @@ class P2PComm {
   // st: int32 [3] device state owned by the caller, zero-initialised ([0] epoch, [1] finished-block
   // counter, [2] sticky error flag) — advanced by the kernel itself (hipGraph-capture safe).
   // algo 0 = one-shot, 1 = two-shot (reduce-scatter + all-gather).
-  void allreduce(Tensor in, Tensor out, double post_scale, Tensor st, int64_t algo) {
+  void allreduce(Tensor in, Tensor out, double post_scale, Tensor st, int64_t algo, double timeout_s) {
     TORCH_CHECK(opened_ || world_ == 1, "p2p: open() the peer handles first");
     check_cuda(in, "in");
     TORCH_CHECK(in.is_contiguous() && out.is_contiguous() && in.numel() == out.numel() &&
@@ -1321,7 +1433,8 @@ class P2PComm {
     TORCH_CHECK(algo == 0 || algo == 1, "p2p: algo 0 (one-shot) or 1 (two-shot)");
     int rc = pdt_p2p_allreduce(in.data_ptr(), out.data_ptr(), in.numel(), dcode(in), data_ptrs_.data(),
                                flag_ptrs_.data(), rank_, world_, cap_, (float)post_scale,
-                               reinterpret_cast<uint32_t*>(st.data_ptr<int>()), (int)algo, max_blocks_, stream());
+                               reinterpret_cast<uint32_t*>(st.data_ptr<int>()), (int)algo, max_blocks_, timeout_s,
+                               stream());
     TORCH_CHECK(rc == 0, "pdt_p2p_allreduce failed (", rc, ")");
   }
   int64_t capacity() const { return cap_; }
@@ -1341,6 +1454,16 @@ class P2PComm {
 // ---- GPT-2 token + position embedding (csrc/kernels/embedding.hip) ----
 // out [B, T, D] = wte[idx] + wpe[arange(T)] (bf16). idx int64 [B, T]; values must be < V (checked on
 // the host only in debug paths: an out-of-range id is a caller bug, as for nn.Embedding).
+// Per-device error word of the embedding kernels (an out-of-range token id sets it; never cleared
+// by the kernels). Allocated at the first call (before any graph capture of the model).
+Tensor embedding_err(const Tensor& like) {
+  static std::map<int, Tensor> bufs;
+  const int dev = like.get_device();
+  auto it = bufs.find(dev);
+  if (it == bufs.end()) it = bufs.emplace(dev, at::zeros({1}, like.options().dtype(at::kInt))).first;
+  return it->second;
+}
+
 Tensor embedding_fwd(Tensor idx, Tensor wte, Tensor wpe) {
   check_cuda(idx, "idx");
   check_cuda(wte, "wte");
@@ -1354,7 +1477,8 @@ Tensor embedding_fwd(Tensor idx, Tensor wte, Tensor wpe) {
   auto out = at::empty({B, T, D}, wte.options());
   TORCH_CHECK(pdt_embedding_fwd(idx.data_ptr<int64_t>(), reinterpret_cast<const uint16_t*>(wte.data_ptr()),
                                 reinterpret_cast<const uint16_t*>(wpe.data_ptr()),
-                                reinterpret_cast<uint16_t*>(out.data_ptr()), B * T, (int)T, (int)D, stream()) == 0,
+                                reinterpret_cast<uint16_t*>(out.data_ptr()), B * T, (int)T, (int)D, (int)wte.size(0),
+                                embedding_err(idx).data_ptr<int>(), stream()) == 0,
               "pdt_embedding_fwd failed");
   return out;
 }
@@ -1372,7 +1496,8 @@ std::vector<Tensor> embedding_bwd(Tensor idx, Tensor dout, int64_t V, int64_t P)
   auto dwpe = T == P ? at::empty({P, D}, dout.options()) : at::zeros({P, D}, dout.options());
   TORCH_CHECK(pdt_embedding_bwd(idx.data_ptr<int64_t>(), reinterpret_cast<const uint16_t*>(dout.data_ptr()),
                                 reinterpret_cast<uint16_t*>(dwte.data_ptr()), reinterpret_cast<uint16_t*>(dwpe.data_ptr()),
-                                ws.data_ptr<int>(), n, (int)B, (int)T, (int)V, (int)D, stream()) == 0,
+                                ws.data_ptr<int>(), n, (int)B, (int)T, (int)V, (int)D,
+                                embedding_err(idx).data_ptr<int>(), stream()) == 0,
               "pdt_embedding_bwd failed");
   return {dwte, dwpe};
 }
@@ -1536,8 +1661,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("embedding_fwd", &embedding_fwd);
   m.def("gemm_nt", &gemm_nt);
   m.def("embedding_bwd", &embedding_bwd);
+  m.def("embedding_err", &embedding_err);
   m.def("conv3x3_wgrad_tune", [](int target_wgs, int co_tile) { pdt_conv3x3_wgrad_tune(target_wgs, co_tile); });
   m.def("bn_bwd_train", &bn_bwd_train);
+  m.def("bn_bwd_coef", &bn_bwd_coef);
+  m.def("conv1x1_bwd_fused", &conv1x1_bwd_fused);
+  m.def("conv1x1_bwd_fused_tune", [](int grid) { pdt_conv1x1_bwd_fused_tune(grid); });
   m.def("ce_fwd", &ce_fwd);
   m.def("ce_bwd", &ce_bwd);
   m.def("ln_fwd", &ln_fwd, py::arg("x"), py::arg("w"), py::arg("b"), py::arg("eps"), py::arg("res") = py::none());

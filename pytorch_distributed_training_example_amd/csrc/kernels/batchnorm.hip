@@ -1012,6 +1012,32 @@ int pdt_bn_bwd_train(const uint16_t* dy, const uint16_t* x, const uint8_t* mask,
   return 0;
 }
 
+// Training backward WITHOUT the apply: the reduction (a pass over dy, x, mask) and the finalize into
+// coef [3][C] = A, B, D (dx = A dy m + B (x - mean) + D) + dgamma / dbeta, for a consumer that forms
+// dx while loading its operand (conv1x1_bwd_fused.hip). ws: pdt_bn_workspace_floats(M, C).
+int pdt_bn_bwd_coef(const uint16_t* dy, const uint16_t* x, const uint8_t* mask, const float* gamma, const float* mean,
+                    const float* invstd, int64_t M, int C, int relu, float* coef, float* dgamma, float* dbeta, float* ws,
+                    unsigned* counters, hipStream_t s) {
+  if (C % kCC != 0 || M < 1 || !coef) return -1;
+  if (relu && !mask) return -2;
+  FinArgs fa{};
+  fa.gamma = gamma; fa.invstd = invstd; fa.dgamma = dgamma; fa.dbeta = dbeta;
+  fa.A = coef; fa.B = coef + C; fa.D = coef + 2 * C;
+  fa.M = M;
+  if (relu) launch_reduce<2>(x, dy, mask, mean, M, C, ws, counters, fa, s);
+  else launch_reduce<1>(x, dy, mask, mean, M, C, ws, counters, fa, s);
+  return 0;
+}
+
+// Same from a producer's per-tile partials [2][T][C] (no pass over dy): finalize only.
+// ws: pdt_bn_tiles_ws_floats(T, C) floats.
+int pdt_bn_bwd_coef_tiles(const float* part, int T, const float* gamma, const float* invstd, int64_t M, int C,
+                          float* coef, float* dgamma, float* dbeta, float* ws, hipStream_t s) {
+  if (C % kCC != 0 || M < 1 || T < 1 || !coef) return -1;
+  return bn_bwd_from_partials(part, T, 1, nullptr, nullptr, nullptr, gamma, nullptr, invstd, M, C, 0, 0, nullptr,
+                              nullptr, dgamma, dbeta, ws, s, coef);
+}
+
 // Training backward whose reduction (sum dz, sum dz (x - mean), dz = dy * mask) comes from the
 // per-tile partials [2][T][C] written by the kernel that produced dy (conv1x1.hip BSTATS): finalize
 // (2 small launches) + apply, no reduce pass over (dy, x). ws: pdt_bn_tiles_ws_floats(T, C) + 2C floats.

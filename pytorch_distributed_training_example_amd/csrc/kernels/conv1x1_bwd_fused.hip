@@ -1,0 +1,478 @@
+// Fused backward of a ResNet bottleneck's LAST 1x1 convolution and the BatchNorm that follows it
+// (gfx950, NHWC bf16, fp32 accumulate). One pass over the incoming gradient produces everything:
+//
+//   dz[m, c]  = A[c] * dy[m, c] * relu_mask[m, c] + B[c] * (z[m, c] - mean[c]) + D[c]
+//               (the BatchNorm's backward apply, bn3: never written to memory)
+//   dxa[m, k] = sum_c dz[m, c] * W[c, k]            (data gradient of the conv, k < CW)
+//   dW[c, k]  = sum_m dz[m, c] * xa[m, k]           (weight gradient of the conv)
+//   part      = per-workgroup sum(g), sum(g * (xb - mean_b)) with g = dxa * relu_mask_b
+//               (the backward reduction of the BatchNorm that produced xa, bn2 — optional)
+//
+// Not in the reference (LeNet has no BN or residual blocks, /root/reference/cnn.py:9-23). Unfused,
+// the same work is four HBM passes: the BN backward apply (read dy, z, mask; write dz), the dgrad GEMM
+// (read dz, write dxa; its epilogue re-reads xb for the bn2 reduction) and the wgrad GEMM (read dz and
+// xa) — 22 "T" of traffic per layer-1 block (T = one 64-channel activation) against 10.3 T here.
+//
+// Structure (one persistent workgroup per CU, 4 waves, memory bound by design):
+//   * a stage = KP = 32 pixels. dy, z (512-B rows), the bn3 mask bits, xa and xb (128-B rows,
+//     XOR-swizzled by permuting each lane's DMA source chunk) and the bn2 mask bits are staged by
+//     LDS-DMA (global_load_lds, 16 / 4 / 1 bytes per lane) through a 3-slot ring, two stages in
+//     flight, counted vmcnt, raw s_barrier (cdna_hip_programming.md §5 "Pipelining across barriers");
+//   * a transform pass turns (dy, z, mask) into dz in a separate LDS tile whose rows are swizzled
+//     with chunk ^ (((r & 3) << 2) | ((r >> 2) & 2)): conflict-free for BOTH readers, the dgrad's
+//     ds_read_b128 (16 pixel rows, one 16-B chunk) and the wgrad's ds_read_b64_tr_b16 (4 rows x 64 B);
+//   * dgrad: v_mfma_f32_16x16x32_bf16 with W^T as the A operand held in VGPRs for the whole kernel
+//     (a wave owns 16 output channels x all C4 inputs = 32 VGPRs), dz as B;
+//   * wgrad: v_mfma_f32_32x32x16_bf16, dz^T and xa through transposed reads, a wave owns a 64 x CW
+//     block of dW in AGPR/VGPR accumulators for the whole kernel; fp32 partials per workgroup summed
+//     afterwards in a fixed order (deterministic);
+//   * the dgrad tile leaves through an LDS staging tile as 16-B rows; the bn2 reduction is taken from
+//     the rounded bf16 values, exactly as conv1x1.hip's BSTATS epilogue does.
+#include "../common.h"
+#include "../tile_stats.h"
+
+using namespace pdt;
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef float f16v __attribute__((ext_vector_type(16)));
+typedef short s4v __attribute__((ext_vector_type(4)));
+#define PDT_LDS __attribute__((address_space(3)))
+
+__device__ __attribute__((aligned(256))) uint4 g_fb_zero[64];  // zero page for pixels past M (never written)
+__device__ uint4 g_fb_sink[256];  // epilogue stores of rows past M land here (keeps the vmcnt count exact)
+
+template <int C4_, int CW_, bool BSTATS_>
+struct FB {
+  static constexpr int C4 = C4_, CW = CW_, KP = 32, kSlots = 3, kWaves = 4, kThreads = 256;
+  static constexpr bool BSTATS = BSTATS_;
+  static constexpr int kRowY = C4 * 2, kRowX = CW * 2;
+  static constexpr int kY = KP * kRowY, kMZ = KP * C4 / 8, kXA = KP * kRowX, kMB = KP * CW / 8;
+  static constexpr int oY = 0, oZ = kY, oMZ = 2 * kY, oXA = oMZ + kMZ, oXB = oXA + kXA;
+  static constexpr int oMB = BSTATS ? oXB + kXA : oXB;
+  static constexpr int kSlot = ((BSTATS ? oMB + kMB : oMB) + 255) / 256 * 256;
+  static constexpr int oDZ = kSlots * kSlot;
+  static constexpr int kLds = oDZ + kY;
+  // DMA instructions per wave per stage: 16-B pieces (1 KB / instr), mask bits 4 B (256 B) / 1 B (64 B)
+  static constexpr int nY = kY / 1024 / kWaves, nMZ = kMZ / 256 / kWaves, nXA = kXA / 1024 / kWaves;
+  static constexpr int nMB = kMB / 64 / kWaves;
+  static constexpr int kG = 2 * nY + nMZ + nXA + (BSTATS ? nXA + nMB : 0);
+  // epilogue: one 16-B chunk of the dgrad tile per thread per stage (stored -> counted in vmcnt)
+  static constexpr int kEpiChunks = KP * CW / 8 / kThreads;
+  static constexpr int kStageOps = kG + kEpiChunks;
+  static constexpr int kStgStride = kRowX + 16;  // staging rows padded: conflict-free 8-B writes
+  // dgrad: a wave owns 16 output channels; wgrad: a wave owns C4 / 4 rows of dW
+  static constexpr int kKS = C4 / 32;         // 16x16x32 k-steps over the input channels
+  static constexpr int kPB = KP / 16;         // pixel blocks of the dgrad tile
+  static constexpr int kWR = C4 / kWaves;     // dW rows per wave
+  static constexpr int kMI = kWR / 32, kNJ = CW / 32;
+  static_assert(CW == 16 * kWaves, "a wave owns 16 dgrad channels");
+  static_assert(nY * 1024 * kWaves == kY && nMZ * 256 * kWaves == kMZ && nXA * 1024 * kWaves == kXA, "DMA split");
+  static_assert(!BSTATS || nMB * 64 * kWaves == kMB, "DMA split (mask b)");
+  static_assert(kEpiChunks == 1, "one epilogue chunk per thread");
+  static_assert(KP * kStgStride <= kY, "staging fits the dead z region");
+  static_assert(kLds <= 160 * 1024, "LDS");
+};
+
+// dz tile swizzle (512-B rows; 16-B chunk index ^= g(row)), an involution within the row.
+__device__ __forceinline__ int swz_dz(int row, int ch) { return ch ^ (((row & 3) << 2) | ((row >> 2) & 2)); }
+// 128-B rows of the transposed-read operands (conv1x1_wgrad.hip): rows r, r+1 are the two halves of
+// a 256-B bank row, r+2, r+3 flip chunk bit 2.
+__device__ __forceinline__ int swz128(int row, int ch) { return ch ^ (((row >> 1) & 1) << 2); }
+
+__device__ __forceinline__ s4v tr_read(const char* p) {
+  s4v r;
+  const uint32_t a = (uint32_t)(uintptr_t)(PDT_LDS const char*)p;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(a) : "memory");
+  return r;
+}
+__device__ __forceinline__ bf16x8 cat2(s4v a, s4v b) {
+  typedef short s8 __attribute__((ext_vector_type(8)));
+  s8 r = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  return __builtin_bit_cast(bf16x8, r);
+}
+// LDS-DMA (lane i's SZ bytes land at M0 + SZ i) issued from inline asm: the builtin makes the
+// compiler assume the DMA may alias every later LDS access and put a vmcnt(0) in front of the
+// transform pass's reads and writes — i.e. wait for the prefetch it was meant to overlap (seen in
+// this kernel's ISA; conv_stem.hip has the same note). Ordering is by the counted vmcnt waits and
+// barriers below instead.
+template <int SZ>
+__device__ __forceinline__ void dma(const void* src, char* lds_wave_base) {
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(PDT_LDS const char*)lds_wave_base);
+  if constexpr (SZ == 16)
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(m0) : "memory");
+  else if constexpr (SZ == 4)
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(src), "s"(m0) : "memory");
+  else
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_ubyte %0, off" ::"v"(src), "s"(m0) : "memory");
+}
+// s_waitcnt vmcnt(N) leaving expcnt / lgkmcnt unconstrained (gfx9 simm16 encoding)
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+struct FBArgs {
+  const uint16_t* dy;   // [M][C4] gradient at the BatchNorm output
+  const uint16_t* z;    // [M][C4] BatchNorm input (= conv output)
+  const uint8_t* mz;    // [M*C4/8] BatchNorm ReLU bits
+  const float* mean;    // [C4]
+  const float* A;       // [C4] dz = A dy m + B (z - mean) + D
+  const float* B;
+  const float* D;
+  const uint16_t* wt;   // [CW][C4] conv weight transposed (W^T)
+  const uint16_t* xa;   // [M][CW] conv input
+  BnSrc bs;             // bn2: input xb [M][CW], mask, mean; part [2][G][CW]
+  uint16_t* dxa;        // [M][CW]
+  float* ws;            // [G][C4][CW] wgrad partials
+  int M, ntiles;
+};
+
+template <class Cf>
+__global__ __launch_bounds__(Cf::kThreads, 1) void conv1x1_bwd_fused_kernel(FBArgs a) {
+  constexpr int C4 = Cf::C4, CW = Cf::CW, KP = Cf::KP, RY = Cf::kRowY, RX = Cf::kRowX;
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int G = gridDim.x, g = blockIdx.x;
+  const int S = (a.ntiles - g + G - 1) / G;  // stages of this workgroup: tiles g, g + G, ...
+
+  // ---- kernel-lifetime registers: W^T fragments (dgrad A operand), the transform coefficients
+  bf16x8 wf[Cf::kKS];
+#pragma unroll
+  for (int ks = 0; ks < Cf::kKS; ++ks)
+    wf[ks] = *reinterpret_cast<const bf16x8*>(a.wt + (16 * wid + (lane & 15)) * C4 + 32 * ks + 8 * (lane >> 4));
+  const int tc = tid % (C4 / 8);  // transform pass: this thread's 8-channel chunk
+  float cm[8], cA[8], cB[8], cD[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    cm[k] = a.mean[tc * 8 + k]; cA[k] = a.A[tc * 8 + k]; cB[k] = a.B[tc * 8 + k]; cD[k] = a.D[tc * 8 + k];
+  }
+  const int ec = tid % (CW / 8);  // epilogue: this thread's chunk of the dgrad tile
+  float bmu[8], bs1[8], bs2[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { bs1[k] = 0.f; bs2[k] = 0.f; bmu[k] = 0.f; }
+  if constexpr (Cf::BSTATS) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) bmu[k] = a.bs.mean[ec * 8 + k];
+  }
+  // the loads above complete before any DMA is issued (no vmcnt(0) inside the ring)
+#pragma unroll
+  for (int ks = 0; ks < Cf::kKS; ++ks) asm volatile("" : "+v"(wf[ks]));
+#pragma unroll
+  for (int k = 0; k < 8; ++k) asm volatile("" : "+v"(cm[k]), "+v"(cA[k]), "+v"(cB[k]), "+v"(cD[k]), "+v"(bmu[k]));
+
+  // ---- per-lane DMA pieces (stage independent): pixel row in the stage and source offset
+  int yrow[Cf::nY], yoff[Cf::nY];
+#pragma unroll
+  for (int i = 0; i < Cf::nY; ++i) {
+    const int o = (wid * Cf::nY + i) * 1024 + lane * 16;
+    yrow[i] = o / RY;
+    yoff[i] = yrow[i] * C4 + ((o % RY) >> 4) * 8;
+  }
+  int mzrow[Cf::nMZ], mzoff[Cf::nMZ];
+#pragma unroll
+  for (int i = 0; i < Cf::nMZ; ++i) {
+    const int o = (wid * Cf::nMZ + i) * 256 + lane * 4;
+    mzrow[i] = o / (C4 / 8);
+    mzoff[i] = o;  // bytes from the stage's first mask byte
+  }
+  int xrow[Cf::nXA], xoff[Cf::nXA];
+#pragma unroll
+  for (int i = 0; i < Cf::nXA; ++i) {
+    const int o = (wid * Cf::nXA + i) * 1024 + lane * 16;
+    xrow[i] = o / RX;
+    xoff[i] = xrow[i] * CW + swz128(xrow[i], (o % RX) >> 4) * 8;
+  }
+  int mbrow[Cf::nMB > 0 ? Cf::nMB : 1], mboff[Cf::nMB > 0 ? Cf::nMB : 1];
+#pragma unroll
+  for (int i = 0; i < Cf::nMB; ++i) {
+    const int o = (wid * Cf::nMB + i) * 64 + lane;
+    mbrow[i] = o / (CW / 8);
+    mboff[i] = o;
+  }
+  auto issue = [&](int s) {
+    char* slot = lds + (s % Cf::kSlots) * Cf::kSlot;
+    const int p0 = (g + s * G) * KP;
+    const uint16_t* yb = a.dy + (int64_t)p0 * C4;
+    const uint16_t* zb = a.z + (int64_t)p0 * C4;
+#pragma unroll
+    for (int i = 0; i < Cf::nY; ++i) {
+      const bool ok = p0 + yrow[i] < a.M;
+      dma<16>(ok ? (const void*)(yb + yoff[i]) : (const void*)g_fb_zero, slot + Cf::oY + (wid * Cf::nY + i) * 1024);
+    }
+#pragma unroll
+    for (int i = 0; i < Cf::nY; ++i) {
+      const bool ok = p0 + yrow[i] < a.M;
+      dma<16>(ok ? (const void*)(zb + yoff[i]) : (const void*)g_fb_zero, slot + Cf::oZ + (wid * Cf::nY + i) * 1024);
+    }
+#pragma unroll
+    for (int i = 0; i < Cf::nMZ; ++i) {
+      const bool ok = p0 + mzrow[i] < a.M;
+      dma<4>(ok ? (const void*)(a.mz + (int64_t)p0 * (C4 / 8) + mzoff[i]) : (const void*)g_fb_zero,
+             slot + Cf::oMZ + (wid * Cf::nMZ + i) * 256);
+    }
+#pragma unroll
+    for (int i = 0; i < Cf::nXA; ++i) {
+      const bool ok = p0 + xrow[i] < a.M;
+      dma<16>(ok ? (const void*)(a.xa + (int64_t)p0 * CW + xoff[i]) : (const void*)g_fb_zero,
+              slot + Cf::oXA + (wid * Cf::nXA + i) * 1024);
+    }
+    if constexpr (Cf::BSTATS) {
+#pragma unroll
+      for (int i = 0; i < Cf::nXA; ++i) {
+        const bool ok = p0 + xrow[i] < a.M;
+        dma<16>(ok ? (const void*)(a.bs.x + (int64_t)p0 * CW + xoff[i]) : (const void*)g_fb_zero,
+                slot + Cf::oXB + (wid * Cf::nXA + i) * 1024);
+      }
+#pragma unroll
+      for (int i = 0; i < Cf::nMB; ++i) {
+        const bool ok = p0 + mbrow[i] < a.M;
+        dma<1>(ok ? (const void*)(a.bs.mask + (int64_t)p0 * (CW / 8) + mboff[i]) : (const void*)g_fb_zero,
+               slot + Cf::oMB + (wid * Cf::nMB + i) * 64);
+      }
+    }
+  };
+
+  // ---- wgrad lane roles (transposed reads; conv1x1_wgrad.hip)
+  const int grp = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int prow = 8 * (grp >> 1) + q, half8 = (p & 1) * 8;
+  int ya[Cf::kMI], xa[Cf::kNJ];
+#pragma unroll
+  for (int i = 0; i < Cf::kMI; ++i)
+    ya[i] = prow * RY + (swz_dz(prow, (wid * Cf::kWR + 32 * i + 16 * (grp & 1) + 4 * p) >> 3) << 4) + half8;
+#pragma unroll
+  for (int j = 0; j < Cf::kNJ; ++j)
+    xa[j] = prow * RX + (swz128(prow, (32 * j + 16 * (grp & 1) + 4 * p) >> 3) << 4) + half8;
+  f16v acc[Cf::kMI][Cf::kNJ];
+#pragma unroll
+  for (int i = 0; i < Cf::kMI; ++i)
+#pragma unroll
+    for (int j = 0; j < Cf::kNJ; ++j)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
+
+  char* const dzs = lds + Cf::oDZ;
+#pragma unroll
+  for (int s = 0; s < Cf::kSlots - 1; ++s)
+    if (s < S) issue(s);
+  for (int s = 0; s < S; ++s) {
+    // stage s's DMA is done once only the next stage's DMA (+ the previous stage's epilogue store,
+    // issued after it) is pending; every count is exact (rows past M store to a sink)
+    if (s + 1 >= S) wait_vm<0>();
+    else if (s == 0) wait_vm<Cf::kG>();
+    else wait_vm<Cf::kStageOps>();
+    lds_barrier();  // B1: DMA(s) visible to all waves; every wave is past stage s-1
+    if (s + Cf::kSlots - 1 < S) issue(s + Cf::kSlots - 1);  // its slot was last used in stage s-1
+    const char* slot = lds + (s % Cf::kSlots) * Cf::kSlot;
+    const int p0 = (g + s * G) * KP;
+
+    // ---- transform: dz = A dy m + B (z - mean) + D -> swizzled dz tile (rows past M: zero)
+#pragma unroll
+    for (int i = 0; i < KP * C4 / 8 / Cf::kThreads; ++i) {
+      const int r = tid / (C4 / 8) + i * (Cf::kThreads / (C4 / 8));
+      const uint4 gv = *reinterpret_cast<const uint4*>(slot + Cf::oY + r * RY + tc * 16);
+      const uint4 zv = *reinterpret_cast<const uint4*>(slot + Cf::oZ + r * RY + tc * 16);
+      const unsigned mk = *reinterpret_cast<const uint8_t*>(slot + Cf::oMZ + r * (C4 / 8) + tc);
+      const uint32_t gw[4] = {gv.x, gv.y, gv.z, gv.w}, zw[4] = {zv.x, zv.y, zv.z, zv.w};
+      float o[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float gk = __uint_as_float(k & 1 ? (gw[k >> 1] & 0xffff0000u) : (gw[k >> 1] << 16));
+        const float zk = __uint_as_float(k & 1 ? (zw[k >> 1] & 0xffff0000u) : (zw[k >> 1] << 16));
+        const float gm = (mk >> k) & 1u ? gk : 0.f;
+        o[k] = cA[k] * gm + cB[k] * (zk - cm[k]) + cD[k];
+      }
+      uint4 ov;
+      if (p0 + r < a.M) {
+        ov.x = (uint32_t)f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16);
+        ov.y = (uint32_t)f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16);
+        ov.z = (uint32_t)f2bf(o[4]) | ((uint32_t)f2bf(o[5]) << 16);
+        ov.w = (uint32_t)f2bf(o[6]) | ((uint32_t)f2bf(o[7]) << 16);
+      } else {
+        ov = make_uint4(0u, 0u, 0u, 0u);
+      }
+      *reinterpret_cast<uint4*>(dzs + r * RY + (swz_dz(r, tc) << 4)) = ov;
+    }
+    lds_barrier();  // B2: dz tile complete; z region of this slot is dead (reused as staging)
+
+    // ---- dgrad: D[ci][px] = sum_c W^T[ci][c] dz[px][c]; lane holds 4 consecutive ci of one pixel
+    f4 dacc[Cf::kPB];
+#pragma unroll
+    for (int pb = 0; pb < Cf::kPB; ++pb) dacc[pb] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < Cf::kKS; ++ks) {
+#pragma unroll
+      for (int pb = 0; pb < Cf::kPB; ++pb) {
+        const int row = 16 * pb + (lane & 15), ch = 4 * ks + (lane >> 4);
+        const bf16x8 b = *reinterpret_cast<const bf16x8*>(dzs + row * RY + (swz_dz(row, ch) << 4));
+        dacc[pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ks], b, dacc[pb], 0, 0, 0);
+      }
+    }
+    // ---- wgrad: dW[c][k] += sum_px dz[px][c] xa[px][k]
+    const char* xas = slot + Cf::oXA;
+#pragma unroll
+    for (int kk = 0; kk < KP / 16; ++kk) {
+      bf16x8 fa[Cf::kMI], fb[Cf::kNJ];
+#pragma unroll
+      for (int i = 0; i < Cf::kMI; ++i) {
+        const char* pp = dzs + ya[i] + kk * 16 * RY;
+        fa[i] = cat2(tr_read(pp), tr_read(pp + 4 * RY));
+      }
+#pragma unroll
+      for (int j = 0; j < Cf::kNJ; ++j) {
+        const char* pp = xas + xa[j] + kk * 16 * RX;
+        fb[j] = cat2(tr_read(pp), tr_read(pp + 4 * RX));
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int i = 0; i < Cf::kMI; ++i) asm volatile("" : "+v"(fa[i]));
+#pragma unroll
+      for (int j = 0; j < Cf::kNJ; ++j) asm volatile("" : "+v"(fb[j]));
+#pragma unroll
+      for (int i = 0; i < Cf::kMI; ++i)
+#pragma unroll
+        for (int j = 0; j < Cf::kNJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+
+    // ---- epilogue: stage the bf16 dgrad tile [KP][CW] in the dead z region, then 16-B rows out
+    char* stg = const_cast<char*>(slot) + Cf::oZ;
+#pragma unroll
+    for (int pb = 0; pb < Cf::kPB; ++pb) {
+      const int px = 16 * pb + (lane & 15), ci = 16 * wid + 4 * (lane >> 4);
+      const f4 v = dacc[pb];
+      uint2 pk;
+      pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+      pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+      *reinterpret_cast<uint2*>(stg + px * Cf::kStgStride + ci * 2) = pk;
+    }
+    lds_barrier();  // B3
+    {
+      const int px = tid / (CW / 8);
+      const uint4 v = *reinterpret_cast<const uint4*>(stg + px * Cf::kStgStride + ec * 16);
+      if (p0 + px < a.M) {
+        if constexpr (Cf::BSTATS) {
+          const uint4 xb = *reinterpret_cast<const uint4*>(slot + Cf::oXB + px * RX + (swz128(px, ec) << 4));
+          const unsigned mk = *reinterpret_cast<const uint8_t*>(slot + Cf::oMB + px * (CW / 8) + ec);
+          bn_bwd_accum8(v, xb, a.bs.mask ? mk : 0xffu, bmu, bs1, bs2);
+        }
+        *reinterpret_cast<uint4*>(a.dxa + (int64_t)(p0 + px) * CW + ec * 8) = v;
+      } else {
+        g_fb_sink[tid] = v;  // one store per thread per stage, always (exact vmcnt counts)
+      }
+    }
+  }
+  wait_vm<0>();
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+  // ---- wgrad partials ws[g][c][k]; 32x32 accumulator: lane holds k = l % 32,
+  // c = 8 (v / 4) + 4 (l / 32) + v % 4 for v = 0..15
+  float* wsp = a.ws + (int64_t)g * C4 * CW;
+#pragma unroll
+  for (int i = 0; i < Cf::kMI; ++i)
+#pragma unroll
+    for (int j = 0; j < Cf::kNJ; ++j) {
+      const int k = 32 * j + (lane & 31);
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const int c = wid * Cf::kWR + 32 * i + 8 * (v >> 2) + 4 * (lane >> 5) + (v & 3);
+        wsp[(int64_t)c * CW + k] = acc[i][j][v];
+      }
+    }
+  if constexpr (Cf::BSTATS)
+    bn_bwd_tile_store<CW, Cf::kWaves>(bs1, bs2, reinterpret_cast<float*>(lds), a.bs.part, G, g, CW, 0);
+}
+
+// dw[c][k] (bf16) = sum over the G workgroup partials in a fixed order (conv1x1_wgrad.hip's scheme:
+// 16 groups take the partials round-robin, then one fixed-order pass over the group sums).
+constexpr int kRedCols = 16, kRedGroups = 16;
+__global__ __launch_bounds__(256) void fb_reduce_kernel(const float* __restrict__ ws, uint16_t* __restrict__ dw,
+                                                        int nsplit, int64_t n4) {
+  __shared__ float4 part[kRedGroups][kRedCols];
+  const int col = threadIdx.x % kRedCols, grp = threadIdx.x / kRedCols;
+  const int64_t i = (int64_t)blockIdx.x * kRedCols + col;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i < n4)
+    for (int k = grp; k < nsplit; k += kRedGroups) {
+      const float4 v = reinterpret_cast<const float4*>(ws + (int64_t)k * n4 * 4)[i];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+  part[grp][col] = s;
+  __syncthreads();
+  if (grp == 0 && i < n4) {
+    float4 t = part[0][col];
+#pragma unroll
+    for (int k = 1; k < kRedGroups; ++k) {
+      const float4 v = part[k][col];
+      t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+    }
+    const uint32_t lo = (uint32_t)f2bf(t.x) | ((uint32_t)f2bf(t.y) << 16);
+    const uint32_t hi = (uint32_t)f2bf(t.z) | ((uint32_t)f2bf(t.w) << 16);
+    reinterpret_cast<uint2*>(dw)[i] = make_uint2(lo, hi);
+  }
+}
+
+int g_grid = 0;  // 0: one workgroup per CU (256)
+
+inline int grid_of(int ntiles) {
+  const int want = g_grid > 0 ? g_grid : 256;
+  return ntiles < want ? ntiles : want;
+}
+
+template <class Cf>
+int launch(const FBArgs& a0, uint16_t* dw, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&conv1x1_bwd_fused_kernel<Cf>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, Cf::kLds) != hipSuccess)
+      return -3;
+    attr = true;
+  }
+  const int G = grid_of(a0.ntiles);
+  hipLaunchKernelGGL(conv1x1_bwd_fused_kernel<Cf>, dim3(G), dim3(Cf::kThreads), Cf::kLds, s, a0);
+  const int64_t n4 = (int64_t)Cf::C4 * Cf::CW / 4;
+  hipLaunchKernelGGL(fb_reduce_kernel, dim3((unsigned)((n4 + kRedCols - 1) / kRedCols)), dim3(kRedCols * kRedGroups),
+                     0, s, a0.ws, dw, G, n4);
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+// Shapes the fused kernel takes: (C4, CW) = (256, 64) (ResNet-50 layer 1).
+int pdt_conv1x1_bwd_fused_ok(int C4, int CW) { return C4 == 256 && CW == 64; }
+
+// Workgroups (= partial slabs) of a call: wgrad workspace G*C4*CW floats, bn2 partials [2][G][CW].
+int pdt_conv1x1_bwd_fused_grid(int M) { return grid_of((M + 31) / 32); }
+
+// See the header. dy, z: [M][C4]; mz: M*C4/8 bytes; mean/A/B/D: [C4]; wt: [CW][C4]; xa: [M][CW];
+// bx / bm / bmean / bpart (all null = no bn2 reduction; bm may be null = no ReLU): bn2's input
+// [M][CW], mask, mean [CW] and the [2][G][CW] partials out; dxa: [M][CW]; dw: [C4][CW] bf16;
+// ws: G*C4*CW floats. Returns 0, -1 for an unsupported shape.
+int pdt_conv1x1_bwd_fused(const uint16_t* dy, const uint16_t* z, const uint8_t* mz, const float* mean, const float* A,
+                          const float* B, const float* D, const uint16_t* wt, const uint16_t* xa, const uint16_t* bx,
+                          const uint8_t* bm, const float* bmean, float* bpart, uint16_t* dxa, uint16_t* dw, float* ws,
+                          int M, int C4, int CW, hipStream_t s) {
+  if (!pdt_conv1x1_bwd_fused_ok(C4, CW) || M < 1 || (int64_t)M * C4 >= ((int64_t)1 << 31)) return -1;
+  if ((bx != nullptr) != (bpart != nullptr) || (bx && !bmean)) return -1;
+  FBArgs a{dy, z, mz, mean, A, B, D, wt, xa, BnSrc{bx, bm, bmean, bpart}, dxa, ws, M, (M + 31) / 32};
+  if (bx) return launch<FB<256, 64, true>>(a, dw, s);
+  return launch<FB<256, 64, false>>(a, dw, s);
+}
+
+// Tuning hook: workgroups per call (0 = one per CU).
+void pdt_conv1x1_bwd_fused_tune(int grid) {
+  if (grid >= 0) g_grid = grid;
+}
+
+}  // extern "C"

@@ -13,6 +13,10 @@
 // 0.16 tokens per row on average for 8K tokens over GPT-2's 50K vocabulary) and sums the rows in
 // increasing token order. Every row of dwte is written exactly once (zeros for absent tokens), so
 // no separate zero-fill pass exists. Replicas and reruns produce bit-identical gradients.
+//
+// Token ids are range-checked in every kernel: an id < 0 or >= V never indexes memory (its output
+// row is zeros, its gradient row is dropped) and sets a device error word that the host reads
+// (ops/embedding.py: raised like nn.Embedding's index error), instead of out-of-bounds atomics.
 #include "../common.h"
 
 using namespace pdt;
@@ -21,13 +25,21 @@ namespace {
 
 __global__ __launch_bounds__(256) void emb_fwd_kernel(const int64_t* __restrict__ idx, const uint16_t* __restrict__ wte,
                                                       const uint16_t* __restrict__ wpe, uint16_t* __restrict__ out,
-                                                      int64_t n, int T, int D) {
+                                                      int64_t n, int T, int D, int V, int* __restrict__ err) {
   const int per = D / 8;  // 16-B pieces per row
   for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n * per; q += (int64_t)gridDim.x * blockDim.x) {
     const int64_t i = q / per;
     const int c = (int)(q % per) * 8;
+    const int64_t v = idx[i];
     float a[8], b[8];
-    ld8_bf16(wte + idx[i] * D + c, a);
+    if (v < 0 || v >= V) {  // out of range: zeros, and report (never read past the table)
+      if (c == 0) atomicOr(err, 1);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[j] = 0.f;
+      st8_bf16(out + i * D + c, a);
+      continue;
+    }
+    ld8_bf16(wte + v * D + c, a);
     ld8_bf16(wpe + (int64_t)(i % T) * D + c, b);
 #pragma unroll
     for (int j = 0; j < 8; ++j) a[j] += b[j];
@@ -35,9 +47,16 @@ __global__ __launch_bounds__(256) void emb_fwd_kernel(const int64_t* __restrict_
   }
 }
 
-__global__ __launch_bounds__(256) void emb_hist_kernel(const int64_t* __restrict__ idx, int* __restrict__ cnt, int64_t n) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    atomicAdd(cnt + idx[i], 1);
+__global__ __launch_bounds__(256) void emb_hist_kernel(const int64_t* __restrict__ idx, int* __restrict__ cnt, int64_t n,
+                                                       int V, int* __restrict__ err) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t v = idx[i];
+    if (v < 0 || v >= V) {
+      atomicOr(err, 1);
+      continue;
+    }
+    atomicAdd(cnt + v, 1);
+  }
 }
 
 // Exclusive scan of cnt[V] into off[V] by one 1024-thread workgroup (V ~ 50K: 49 per thread).
@@ -62,9 +81,10 @@ __global__ __launch_bounds__(1024) void emb_scan_kernel(const int* __restrict__ 
 }
 
 __global__ __launch_bounds__(256) void emb_place_kernel(const int64_t* __restrict__ idx, const int* __restrict__ off,
-                                                        int* __restrict__ fill, int* __restrict__ pos, int64_t n) {
+                                                        int* __restrict__ fill, int* __restrict__ pos, int64_t n, int V) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t v = idx[i];
+    if (v < 0 || v >= V) continue;  // reported by emb_hist_kernel
     pos[off[v] + atomicAdd(fill + v, 1)] = (int)i;
   }
 }
@@ -124,30 +144,32 @@ inline int grid_of(int64_t work) {
 
 extern "C" {
 
-// out[B*T, D] = wte[idx] + wpe[pos]; idx int64 [B*T] (values < V: caller-checked), D % 8 == 0.
+// out[B*T, D] = wte[idx] + wpe[pos]; idx int64 [B*T], D % 8 == 0. An id outside [0, V) gives a zero
+// row and sets *err (device int, never cleared here).
 int pdt_embedding_fwd(const int64_t* idx, const uint16_t* wte, const uint16_t* wpe, uint16_t* out, int64_t n, int T,
-                      int D, hipStream_t s) {
-  if (D % 8 != 0 || T < 1) return -1;
+                      int D, int V, int* err, hipStream_t s) {
+  if (D % 8 != 0 || T < 1 || V < 1 || !err) return -1;
   if (n == 0) return 0;
-  hipLaunchKernelGGL(emb_fwd_kernel, dim3(grid_of(n * D / 8)), dim3(256), 0, s, idx, wte, wpe, out, n, T, D);
+  hipLaunchKernelGGL(emb_fwd_kernel, dim3(grid_of(n * D / 8)), dim3(256), 0, s, idx, wte, wpe, out, n, T, D, V, err);
   return 0;
 }
 
 // Workspace ints: cnt[V], off[V], fill[V], pos[n], sorted[n]. cnt and fill must be zero on entry.
 int64_t pdt_embedding_bwd_ws_ints(int64_t n, int V) { return 3 * (int64_t)V + 2 * n; }
 
-// dwte[V, D] (every row written), dwpe[T, D] (nullable) from dout[B*T, D]; n = B*T.
+// dwte[V, D] (every row written), dwpe[T, D] (nullable) from dout[B*T, D]; n = B*T. Ids outside
+// [0, V) contribute nothing and set *err.
 int pdt_embedding_bwd(const int64_t* idx, const uint16_t* dout, uint16_t* dwte, uint16_t* dwpe, int* ws, int64_t n,
-                      int B, int T, int V, int D, hipStream_t s) {
-  if (D % 8 != 0 || n != (int64_t)B * T || V < 1) return -1;
+                      int B, int T, int V, int D, int* err, hipStream_t s) {
+  if (D % 8 != 0 || n != (int64_t)B * T || V < 1 || !err) return -1;
   int* cnt = ws;
   int* off = cnt + V;
   int* fill = off + V;
   int* pos = fill + V;
   int* sorted = pos + n;
-  hipLaunchKernelGGL(emb_hist_kernel, dim3(grid_of(n)), dim3(256), 0, s, idx, cnt, n);
+  hipLaunchKernelGGL(emb_hist_kernel, dim3(grid_of(n)), dim3(256), 0, s, idx, cnt, n, V, err);
   hipLaunchKernelGGL(emb_scan_kernel, dim3(1), dim3(1024), 0, s, cnt, off, V);
-  hipLaunchKernelGGL(emb_place_kernel, dim3(grid_of(n)), dim3(256), 0, s, idx, off, fill, pos, n);
+  hipLaunchKernelGGL(emb_place_kernel, dim3(grid_of(n)), dim3(256), 0, s, idx, off, fill, pos, n, V);
   hipLaunchKernelGGL(emb_bwd_rows_kernel, dim3((V + 3) / 4), dim3(256), 0, s, dout, cnt, off, pos, sorted, dwte, V, D);
   if (dwpe) hipLaunchKernelGGL(emb_bwd_pos_kernel, dim3(grid_of((int64_t)T * D / 8)), dim3(256), 0, s, dout, dwpe, B, T, D);
   return 0;

@@ -15,9 +15,12 @@
 // same kernel node advances the epoch exactly like an eager call (a host-side epoch baked into a
 // captured node would make every replay see last replay's flags and skip the barrier).
 //
-// Failure: a barrier wait is bounded (spin limit). On expiry the block sets st[2] = 1 (sticky)
-// and writes NaN to its output slice instead of a partial sum, so a lost peer is never a silently
-// wrong gradient: the DDP hook checks st[2] (parallel/p2p.py) and NaN trips the AMP inf-check.
+// Failure: a barrier wait is bounded in WALL-CLOCK time (s_memrealtime, 100 MHz), by a timeout the
+// host derives from the process group's (parallel/p2p.py) — a legitimately late peer (first-step
+// skew, rank-0-only host work) is waited for like an RCCL peer would be. On expiry the block sets
+// st[2] = 1 (sticky until the host resets it) and writes NaN to its output slice instead of a
+// partial sum, so a lost peer is never a silently wrong gradient: the DDP hook checks st[2] and NaN
+// trips the AMP inf-check.
 //
 // One-shot (small): block b copies slice b of the input into staging[parity], fences (system
 // scope), release-stores `epoch` into flags[parity][b][me] of every peer, waits for every peer's
@@ -93,17 +96,17 @@ __device__ __forceinline__ void finish_epoch(uint32_t* st, uint32_t epoch) {
 // Signal `epoch` into slot `slot` of every rank's flags for block b, then wait until every rank
 // signalled this block. Returns false (and sets the sticky error word) if a peer never arrived.
 __device__ __forceinline__ bool block_barrier(const P2PPeers& peers, int rank, int world, int slot_kind, int b,
-                                              uint32_t epoch, uint32_t* st, int64_t spin_limit, int* sh_ok) {
+                                              uint32_t epoch, uint32_t* st, uint64_t timeout_ticks, int* sh_ok) {
   const int slot = (slot_kind * PDT_P2P_MAX_BLOCKS + b) * PDT_P2P_MAX_RANKS;
   if (threadIdx.x == 0) sh_ok[0] = 1;
   __syncthreads();
   if (threadIdx.x < world) {
     __hip_atomic_store(peers.flags[threadIdx.x] + slot + rank, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     const uint32_t* f = peers.flags[rank] + slot + threadIdx.x;
-    int64_t it = 0;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != epoch) {
       __builtin_amdgcn_s_sleep(2);
-      if (++it > spin_limit) {  // a peer never arrived: report, never hang the GPU
+      if (__builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks) {  // a peer never arrived: report, never hang
         __hip_atomic_store(reinterpret_cast<int*>(st + 2), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         sh_ok[0] = 0;
         break;
@@ -126,7 +129,7 @@ template <typename T>
 __global__ __launch_bounds__(256) void p2p_oneshot_kernel(const T* __restrict__ in, T* __restrict__ out, int64_t n,
                                                           P2PPeers peers, int rank, int world, int64_t cap,
                                                           float post_scale, uint32_t* __restrict__ st,
-                                                          int64_t spin_limit) {
+                                                          uint64_t timeout_ticks) {
   __shared__ uint32_t sh[2];
   const uint32_t epoch = read_epoch(st, sh);
   const int parity = (int)(epoch & 1u);
@@ -137,7 +140,7 @@ __global__ __launch_bounds__(256) void p2p_oneshot_kernel(const T* __restrict__ 
   T* mine = reinterpret_cast<T*>(peers.data[rank] + (int64_t)parity * cap);
   for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) V8<T>::cp(in + i * 8, mine + i * 8);
   __threadfence_system();
-  if (!block_barrier(peers, rank, world, parity, b, epoch, st, spin_limit, reinterpret_cast<int*>(sh + 1))) {
+  if (!block_barrier(peers, rank, world, parity, b, epoch, st, timeout_ticks, reinterpret_cast<int*>(sh + 1))) {
     poison(out, lo, hi);
   } else {
     for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
@@ -168,7 +171,7 @@ template <typename T>
 __global__ __launch_bounds__(256) void p2p_twoshot_kernel(const T* __restrict__ in, T* __restrict__ out, int64_t n,
                                                           P2PPeers peers, int rank, int world, int64_t cap,
                                                           float post_scale, uint32_t* __restrict__ st,
-                                                          int64_t spin_limit) {
+                                                          uint64_t timeout_ticks) {
   __shared__ uint32_t sh[2];
   const uint32_t epoch = read_epoch(st, sh);
   const int parity = (int)(epoch & 1u);
@@ -182,7 +185,7 @@ __global__ __launch_bounds__(256) void p2p_twoshot_kernel(const T* __restrict__ 
     for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) V8<T>::cp(in + i * 8, mine + i * 8);
   }
   __threadfence_system();
-  bool ok = block_barrier(peers, rank, world, 2, b, epoch, st, spin_limit, reinterpret_cast<int*>(sh + 1));
+  bool ok = block_barrier(peers, rank, world, 2, b, epoch, st, timeout_ticks, reinterpret_cast<int*>(sh + 1));
   // phase 2: reduce my chunk's sub-slice b over all ranks (rank order), into result + out
   int64_t mlo, mhi;
   sub_slice(n8, world, rank, b, nb, mlo, mhi);
@@ -202,7 +205,7 @@ __global__ __launch_bounds__(256) void p2p_twoshot_kernel(const T* __restrict__ 
       V8<T>::st(out + i * 8, acc);
     }
     __threadfence_system();
-    ok = block_barrier(peers, rank, world, 3, b, epoch, st, spin_limit, reinterpret_cast<int*>(sh + 1));
+    ok = block_barrier(peers, rank, world, 3, b, epoch, st, timeout_ticks, reinterpret_cast<int*>(sh + 1));
   }
   // phase 3: gather the other chunks' sub-slice b from their owners' result regions
   for (int j = 0; j < world; ++j) {
@@ -234,9 +237,10 @@ int64_t pdt_p2p_data_bytes(int64_t cap) { return 3 * cap; }
 // pdt_p2p_flags_bytes() long, data regions pdt_p2p_data_bytes(cap). dtype 0 = fp32, 1 = bf16.
 // n % 8 == 0, n * esize <= cap. st: this rank's private device state, 3 uint32 zero-initialised
 // ([0] epoch, [1] finished-block counter, [2] sticky error). algo 0 = one-shot, 1 = two-shot.
+// timeout_s: how long a block waits for a peer (wall clock) before poisoning its output.
 int pdt_p2p_allreduce(const void* in, void* out, int64_t n, int dtype, char* const* data_ptrs,
                       uint32_t* const* flag_ptrs, int rank, int world, int64_t cap, float post_scale,
-                      uint32_t* st, int algo, int max_blocks, hipStream_t s) {
+                      uint32_t* st, int algo, int max_blocks, double timeout_s, hipStream_t s) {
   if (world < 1 || world > PDT_P2P_MAX_RANKS || n % 8 != 0 || !st) return -1;
   const int64_t esize = dtype == 0 ? 4 : 2;
   if (n * esize > cap) return -2;
@@ -251,10 +255,12 @@ int pdt_p2p_allreduce(const void* in, void* out, int64_t n, int dtype, char* con
   int64_t nb = algo == 1 ? (n * esize / world + 16383) / 16384 : (n * esize + 16383) / 16384;
   if (nb > mb) nb = mb;
   if (nb < 1) nb = 1;
-  const int64_t spin_limit = 20000000;  // ~1-2 s of polling
+  // s_memrealtime ticks at 100 MHz; at least 1 ms, at most a day
+  const double ts = timeout_s < 1e-3 ? 1e-3 : (timeout_s > 86400.0 ? 86400.0 : timeout_s);
+  const uint64_t timeout_ticks = (uint64_t)(ts * 1e8);
 #define PDT_P2P_LAUNCH(K, T)                                                                                 \
   hipLaunchKernelGGL(K<T>, dim3((unsigned)nb), dim3(256), 0, s, (const T*)in, (T*)out, n, peers, rank, world, \
-                     cap, post_scale, st, spin_limit)
+                     cap, post_scale, st, timeout_ticks)
   if (algo == 1) {
     if (dtype == 0) PDT_P2P_LAUNCH(p2p_twoshot_kernel, float);
     else PDT_P2P_LAUNCH(p2p_twoshot_kernel, uint16_t);

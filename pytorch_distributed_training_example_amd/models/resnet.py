@@ -19,7 +19,7 @@ from typing import List, Optional, Type
 import torch
 from torch import nn
 
-from ..ops.batchnorm import BatchNorm2d, ResidualGradLink
+from ..ops.batchnorm import BatchNorm2d, BNGradLink, ResidualGradLink
 from ..ops.conv import Conv1x1, SplitConv2d, linked_conv, stem_block
 
 
@@ -109,9 +109,12 @@ class Bottleneck(nn.Module):
             link = ResidualGradLink(lazy=self.downsample is None and self.conv1.masked_residual_ok(x))
             out = bn_act(self.bn1, self.conv1(x, res_link=link), relu=True)
             out = bn_act(self.bn2, self.conv2(out), relu=True)
-            out = self.conv3(out)
+            # conv3 + bn3 backward as one kernel: bn3 hands its input gradient to conv3 in deferred form
+            blink = BNGradLink() if (self.conv3.fused_bwd_ok(out) and not self.bn3.has_hooks()
+                                     and (link.lazy or self.downsample is not None)) else None
+            out = self.conv3(out, bwd_link=blink)
             if self.downsample is None:  # identity: bn3's backward deposits the shortcut gradient
-                return self.bn3(out, residual=x, relu=True, res_link=link)
+                return self.bn3(out, residual=x, relu=True, res_link=link, out_link=blink)
             # shortcut built AFTER the main branch so its backward nodes run first (higher
             # autograd sequence numbers): the shortcut conv deposits, conv1 accumulates. Either
             # order is correct (whichever branch finishes second adds), this one saves a pass.
@@ -127,9 +130,9 @@ class Bottleneck(nn.Module):
                     identity = ds_bn._forward_stats_only(xs, grad_link=glink)
                 else:
                     identity = ds_bn(xs, grad_link=glink)
-                return self.bn3(out, residual=identity, relu=True, res_link=glink)
+                return self.bn3(out, residual=identity, relu=True, res_link=glink, out_link=blink)
             identity = bn_act(ds_bn, linked_conv(self.downsample[0], x, link))
-            return bn_act(self.bn3, out, residual=identity, relu=True)
+            return bn_act(self.bn3, out, residual=identity, relu=True)  # (blink unused: conv3 gets a dense gy)
         identity = x if self.downsample is None else self.downsample(x)
         out = bn_act(self.bn1, self.conv1(x), relu=True)
         out = bn_act(self.bn2, self.conv2(out), relu=True)

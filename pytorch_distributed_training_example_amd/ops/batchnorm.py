@@ -110,10 +110,49 @@ class MaskedGrad:
         return self.dy * bits.view(self.dy.permute(0, 2, 3, 1).shape).permute(0, 3, 1, 2).to(self.dy.dtype)
 
 
+class DeferredBNGrad:
+    """The gradient at a BatchNorm's INPUT, not materialised: ``dx = A dy m + B (x - mean) + D`` per
+    channel (``coef`` = [3, C] fp32 = A, B, D; ``m`` = the 1-bit ReLU mask, or none). Handed by the
+    BatchNorm's backward to the conv that produced ``x`` through a ``BNGradLink``: that conv's fused
+    backward (csrc/kernels/conv1x1_bwd_fused.hip) forms dx while loading it, so the BatchNorm's apply
+    pass — a read of (dy, x, mask) and a write of dx, then two re-reads of dx — never runs."""
+
+    __slots__ = ("dy", "x", "mask", "mean", "coef")
+
+    def __init__(self, dy, x, mask, mean, coef):
+        self.dy, self.x, self.mask, self.mean, self.coef = dy, x, mask, mean, coef
+
+    def materialize(self) -> torch.Tensor:
+        """dx as a tensor (fallback when the consumer cannot take the deferred form)."""
+        sh = (1, -1, 1, 1) if self.x.dim() == 4 else (1, -1)
+        g = self.dy.float()
+        if self.mask is not None:
+            g = g * MaskedGrad(torch.ones_like(self.dy), self.mask).dense().float()
+        a, b, d = (c.view(sh) for c in self.coef)
+        dx = a * g + b * (self.x.float() - self.mean.view(sh)) + d
+        fmt = torch.channels_last if self.x.dim() == 4 else torch.contiguous_format
+        return dx.to(self.x.dtype).contiguous(memory_format=fmt)
+
+
+class BNGradLink:
+    """One-way hand-off of a ``DeferredBNGrad`` from a BatchNorm's backward (which then returns None
+    as its input gradient) to the backward of the conv that produced the BatchNorm's input (which
+    runs next, with its output gradient None: ``set_materialize_grads(False)``)."""
+
+    __slots__ = ("grad",)
+
+    def __init__(self):
+        self.grad = None
+
+    def take(self):
+        g, self.grad = self.grad, None
+        return g
+
+
 class _BNTrainFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, residual, weight, bias, running_mean, running_var, momentum, eps, relu, link=None,
-                part=None, gsrc=None, glink=None, res_ab=None, defer=None):
+                part=None, gsrc=None, glink=None, res_ab=None, defer=None, out_link=None):
         C = native()
         if defer is not None:  # statistics only: the consumer applies y = a x + b itself (deferred apply)
             if part is not None:
@@ -135,6 +174,9 @@ class _BNTrainFn(torch.autograd.Function):
         ctx.has_weight = weight is not None
         ctx.link = link
         ctx.gsrc = gsrc
+        # out_link: the conv that produced x takes this BatchNorm's input gradient in deferred form
+        # (DeferredBNGrad) when the residual gradient needs no dense tensor either
+        ctx.out_link = out_link if (defer is None and (residual is None or (link is not None and link.lazy))) else None
         # glink: this output's only consumer (a residual BatchNorm) may hand its gradient over as
         # (dy, ReLU mask) and give autograd None — backward then runs with dy = None
         ctx.glink = glink
@@ -149,7 +191,7 @@ class _BNTrainFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, mask, weight, mean, invstd = ctx.saved_tensors
-        tail = (None,) * 11
+        tail = (None,) * 12
         need_w = ctx.has_weight and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3])
         if dy is None:  # gradient handed over through glink as (dy, mask): a ReLU'd dy of the consumer
             g = ctx.glink.take() if ctx.glink is not None else None
@@ -170,6 +212,14 @@ class _BNTrainFn(torch.autograd.Function):
                 return native().bn_bwd_train_tiles(dy, x, part, mask, weight, mean, invstd, relu, has_res, need_w)
             return native().bn_bwd_train(dy, x, mask, weight, mean, invstd, relu, has_res, need_w)
 
+        if ctx.out_link is not None and (not ctx.relu or mask is not None):
+            # coefficients only: the producing conv's fused backward forms dx = A dy m + B (x - mean) + D
+            coef, dg, db = native().bn_bwd_coef(dy, x, part, mask if ctx.relu else None, weight, mean, invstd,
+                                                ctx.relu, need_w)
+            ctx.out_link.grad = DeferredBNGrad(dy, x, mask if ctx.relu else None, mean, coef)
+            if ctx.has_res:  # lazy link (checked in forward): the shortcut gets (dy, mask) as before
+                ctx.link.grad = MaskedGrad(dy, mask) if ctx.relu else dy
+            return (None, None, dg if need_w else None, db if need_w else None) + tail
         if ctx.has_res and ctx.link is not None and ctx.link.lazy and ctx.relu:
             # the shortcut gradient dy*mask is never written: the consumer's GEMM masks dy itself
             dx, _, dg, db = bwd(True, False)
@@ -252,7 +302,7 @@ def materialize(t):
 
 def batch_norm_act(x, residual, weight, bias, running_mean, running_var, training, momentum, eps, relu,
                    res_link: Optional[ResidualGradLink] = None, grad_link: Optional[ResidualGradLink] = None,
-                   defer_apply: bool = False):
+                   defer_apply: bool = False, out_link: Optional[BNGradLink] = None):
     """Functional fused BN(+add)(+ReLU). Native when x is a channels_last bf16 GPU tensor.
     ``res_link``: route the residual gradient through it instead of returning it (see
     ``ResidualGradLink``); only honoured on the native training path — callers check
@@ -285,7 +335,8 @@ def batch_norm_act(x, residual, weight, bias, running_mean, running_var, trainin
             if defer is not None:
                 gsrc = None
             y = _BNTrainFn.apply(x, residual, weight, bias, running_mean, running_var,
-                                 float(momentum), float(eps), bool(relu), res_link, part, gsrc, grad_link, ab, defer)
+                                 float(momentum), float(eps), bool(relu), res_link, part, gsrc, grad_link, ab, defer,
+                                 out_link)
             if defer:
                 return DeferredBNOutput(y, defer[0])
             if gsrc is not None:  # a consumer conv may take this BN's backward reduction (ops/conv.py)
@@ -343,7 +394,7 @@ class BatchNorm2d(nn.BatchNorm2d):
 
     def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
                 relu: Optional[bool] = None, res_link: Optional[ResidualGradLink] = None,
-                grad_link: Optional[ResidualGradLink] = None) -> torch.Tensor:
+                grad_link: Optional[ResidualGradLink] = None, out_link: Optional[BNGradLink] = None) -> torch.Tensor:
         relu = self.fused_relu if relu is None else relu
         training = self.training or not self.track_running_stats
         momentum = self.momentum
@@ -356,7 +407,7 @@ class BatchNorm2d(nn.BatchNorm2d):
         w = self.weight if self.affine else None
         b = self.bias if self.affine else None
         return batch_norm_act(x, residual, w, b, rm, rv, training, momentum if momentum is not None else 0.0,
-                              self.eps, relu, res_link, grad_link)
+                              self.eps, relu, res_link, grad_link, out_link=out_link)
 
     def has_hooks(self) -> bool:
         """Forward (pre-)hooks registered on this module or globally: they must see real outputs."""

@@ -187,7 +187,7 @@ def _nhwc2d(t: torch.Tensor) -> torch.Tensor:
 
 class _Conv1x1Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, link=None, stats_out=None, gsrc=None):
+    def forward(ctx, x, weight, link=None, stats_out=None, gsrc=None, bwd_link=None):
         N, Ci, H, W = x.shape
         Co = weight.shape[0]
         x2 = _nhwc2d(x)
@@ -195,6 +195,11 @@ class _Conv1x1Fn(torch.autograd.Function):
         M = x2.shape[0]
         ctx.link = link
         ctx.gsrc = gsrc  # x is a BatchNorm output: our dgrad GEMM can take that BN's backward reduction
+        # bwd_link: the BatchNorm consuming y may hand its input gradient over in deferred form
+        # (ops/batchnorm.py DeferredBNGrad) and give autograd None: backward then runs with gy = None
+        ctx.bwd_link = bwd_link
+        if bwd_link is not None:
+            ctx.set_materialize_grads(False)
         ctx.save_for_backward(x, weight)
         cands = {"miopen": lambda: F.conv2d(x, weight), "gemm": lambda: torch.mm(x2, w2.t())}
         if x.dtype == torch.bfloat16 and _ours_ok("fwd", M, Ci, Co):
@@ -221,6 +226,14 @@ class _Conv1x1Fn(torch.autograd.Function):
         x, weight = ctx.saved_tensors
         N, Ci, H, W = x.shape
         Co = weight.shape[0]
+        if gy is None:  # the consuming BatchNorm handed its input gradient over (or there is none)
+            d = ctx.bwd_link.take() if ctx.bwd_link is not None else None
+            if d is None:
+                return None, None, None, None, None, None
+            r = _bwd_fused(ctx, d, x, weight)
+            if r is not None:
+                return r[0], r[1], None, None, None, None
+            gy = d.materialize()
         gy = gy.contiguous(memory_format=torch.channels_last)
         x2, g2, w2 = _nhwc2d(x), _nhwc2d(gy), weight.reshape(Co, Ci)
         M = x2.shape[0]
@@ -318,7 +331,32 @@ class _Conv1x1Fn(torch.autograd.Function):
             else:
                 wfn = lambda: conv_bwd([False, True, False])[1]  # noqa: E731
             dw = wfn()
-        return dx, dw, None, None, None
+        return dx, dw, None, None, None, None
+
+
+def _bwd_fused(ctx, d, x, weight):
+    """conv3 + bn3 backward of a bottleneck as ONE kernel (csrc/kernels/conv1x1_bwd_fused.hip): from the
+    BatchNorm's deferred input gradient ``d`` (DeferredBNGrad) -> (dx, dw), with the producing BatchNorm's
+    backward reduction deposited in its GradStatsSource. None when the kernel does not take the shape
+    (the caller materialises d and runs the unfused path)."""
+    if not (SW.bwd_fused and ctx.link is None and ctx.needs_input_grad[0] and ctx.needs_input_grad[1]
+            and d.mask is not None and fused_bwd_shape_ok(weight)):
+        return None
+    from ._native import native
+    gs = ctx.gsrc if (ctx.gsrc is not None and ctx.gsrc.ready()) else None
+    r = native().conv1x1_bwd_fused(d.dy.contiguous(memory_format=torch.channels_last), d.x, d.mask, d.mean, d.coef,
+                                   weight, x, gs.x if gs else None, gs.mask if gs else None, gs.mean if gs else None)
+    if not r:
+        return None
+    dx, dw, part = r
+    if gs is not None and part is not None:
+        gs.deposit(part, dx)
+    return dx, dw
+
+
+def fused_bwd_shape_ok(weight: torch.Tensor) -> bool:
+    """(Co, Ci) of a 1x1 conv whose backward conv1x1_bwd_fused takes (ResNet-50 layer-1 conv3)."""
+    return weight.dim() == 4 and tuple(weight.shape[:2]) == (256, 64) and weight.dtype == torch.bfloat16
 
 
 def _subsample_native(t: torch.Tensor) -> bool:
@@ -739,15 +777,18 @@ class Conv1x1(nn.Conv2d):
         # MIOpen's strided kernels (12,318 vs 12,118 img/s, tools/gpu_s2b.sh; PDT_CONV1X1_S2=0 = MIOpen)
         return s > 1 and self.stride == (s, s) and self._gemm_ok(x) and SW.conv1x1_s2
 
-    def forward(self, x: torch.Tensor, res_link=None) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, res_link=None, bwd_link=None) -> torch.Tensor:
         """``res_link``: a ``ResidualGradLink`` whose gradient (the other branch's gradient of
-        ``x``) meets this conv's input gradient; requires one of the GEMM paths."""
+        ``x``) meets this conv's input gradient; requires one of the GEMM paths. ``bwd_link``: a
+        ``BNGradLink`` through which the BatchNorm consuming the output may hand over its input
+        gradient in deferred form (stride-1 GEMM path only; check ``fused_bwd_ok``)."""
         if self.gemm_eligible(x):
             holder = [] if (self.emit_bn_stats and self.training and torch.is_grad_enabled()
                             and SW.conv_bn_stats) else None
             from .batchnorm import grad_stats_source_of
             y = _Conv1x1Fn.apply(x, self.weight, res_link, holder,
-                                 grad_stats_source_of(x) if self.training and torch.is_grad_enabled() else None)
+                                 grad_stats_source_of(x) if self.training and torch.is_grad_enabled() else None,
+                                 bwd_link)
             if holder:
                 y._pdt_bn_stats = BNStats(holder[0], y._version)
             return y
@@ -758,5 +799,12 @@ class Conv1x1(nn.Conv2d):
             if holder:
                 y._pdt_bn_stats = BNStats(holder[0], y._version)
             return y
-        assert res_link is None, "res_link needs a GEMM path"
+        assert res_link is None and bwd_link is None, "res_link / bwd_link need a GEMM path"
         return super().forward(x)
+
+    def fused_bwd_ok(self, x: torch.Tensor) -> bool:
+        """This conv's backward can take its consuming BatchNorm's input gradient in deferred form
+        (``bwd_link``) and run it as one fused kernel (``PDT_BWD_FUSED=0`` turns it off)."""
+        return (SW.bwd_fused and self.training and torch.is_grad_enabled() and x.dtype == torch.bfloat16
+                and self.gemm_eligible(x) and fused_bwd_shape_ok(self.weight) and not _has_hooks(self)
+                and not self._backward_hooks and not self._backward_pre_hooks)

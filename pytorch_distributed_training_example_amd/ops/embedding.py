@@ -9,14 +9,48 @@ batch in order. Reruns and replicas give bit-identical ``wte``/``wpe`` gradients
 Not in the reference (its only model is LeNet, /root/reference/cnn.py); SURVEY.md §2.3 lists the
 embedding among the kernels the GPT-2 north-star config needs. CPU / fp32 / disabled-native inputs
 take the PyTorch reference path (same math).
+
+Token ids are range-checked on the device: an id outside [0, V) reads nothing (zero output row, no
+gradient) and sets an error word. Without a host sync, that word is copied to pinned memory behind
+every forward and checked at the next call (``IndexError``, one step late, like an asynchronous
+device assert); ``check_ids()`` syncs and checks now. ``PDT_EMBEDDING_CHECK=1`` checks every call.
 """
 from __future__ import annotations
 
 import torch
 import torch.nn.functional as F
 
+import os
+
 from ..config import SW
 from ._native import native, use_native
+
+_ERR = {"host": None, "event": None}
+_SYNC_CHECK = os.environ.get("PDT_EMBEDDING_CHECK", "0") == "1"
+
+
+def _raise_if_bad(err_value: int) -> None:
+    if err_value:
+        raise IndexError("token_position_embedding: a token id is outside [0, vocab size) "
+                         "(its rows were zeroed; the error word stays set: see check_ids)")
+
+
+def _poll_previous() -> None:
+    ev = _ERR["event"]
+    if ev is not None and not torch.cuda.is_current_stream_capturing() and ev.query():
+        _raise_if_bad(int(_ERR["host"][0]))
+
+
+def check_ids(device=None) -> None:
+    """Host sync: raise IndexError if any embedding call so far saw an out-of-range id."""
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else device
+    _raise_if_bad(int(native().embedding_err(torch.empty(0, device=dev)).item()))
+
+
+def reset_id_errors(device=None) -> None:
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else device
+    native().embedding_err(torch.empty(0, device=dev)).zero_()
+    _ERR["event"] = None
 
 
 class _EmbeddingFn(torch.autograd.Function):
@@ -24,7 +58,18 @@ class _EmbeddingFn(torch.autograd.Function):
     def forward(ctx, idx, wte, wpe):
         ctx.save_for_backward(idx)
         ctx.V, ctx.P = wte.shape[0], wpe.shape[0]
-        return native().embedding_fwd(idx, wte, wpe)
+        _poll_previous()
+        out = native().embedding_fwd(idx, wte, wpe)
+        if _SYNC_CHECK:
+            check_ids(idx.device)
+        elif not torch.cuda.is_current_stream_capturing():
+            if _ERR["host"] is None:
+                _ERR["host"] = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+            _ERR["host"].copy_(native().embedding_err(idx), non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            _ERR["event"] = ev
+        return out
 
     @staticmethod
     def backward(ctx, dout):

@@ -130,7 +130,9 @@ def _default_avg_op(pg) -> tuple[Any, bool]:
     if dist.get_world_size(pg) == 1:
         return dist.ReduceOp.SUM, False
     backend = dist.get_backend(pg)
-    if backend == "nccl" or (backend == "pdt_p2p" and torch.cuda.is_available()):
+    # pdt_p2p takes AVG for every tensor: P2P kernels, RCCL inner group, or SUM + divide when its
+    # inner group is gloo (parallel/p2p.py P2PProcessGroup.allreduce)
+    if backend in ("nccl", "pdt_p2p"):
         return dist.ReduceOp.AVG, False
     return dist.ReduceOp.SUM, True
 

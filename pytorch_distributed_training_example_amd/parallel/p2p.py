@@ -15,9 +15,14 @@ node every GPU has a direct xGMI link to every other one, so:
   * every chunk is summed in rank order with fp32 accumulation: bit-identical replicas;
   * the call counter lives in device memory and is advanced by the kernel, so the kernel can be
     captured in a hipGraph and replayed (round 2's host-side epoch could not);
-  * a peer that never arrives sets a sticky device error word and the output slice becomes NaN —
-    never a partial sum; ``check()`` raises, and the DDP hook raises on its next call (the error
-    word is copied to pinned memory behind each kernel, read without a sync).
+  * a peer that has not arrived within ``timeout_s`` of WALL-CLOCK time (default: the process
+    group's timeout, capped at ``MAX_TIMEOUT_S``; the kernel bounds its wait by s_memrealtime) sets a
+    sticky device error word and the output slice becomes NaN — never a partial sum; ``check()``
+    raises, and the DDP hook raises on its next call (the error word is copied to pinned memory
+    behind each kernel, read without a sync); ``reset_error()`` clears it.
+  * calls are serialised on ONE internal stream per group (joined to the caller's stream both
+    ways), as RCCL serialises its work: the device epoch and the staging parity assume stream-ordered
+    calls, so two all-reduces issued from different caller streams must never overlap.
 
 All ranks of the group must be on one node (IPC). Ranks may share a GPU (tests do this).
 """
@@ -34,20 +39,29 @@ import torch.distributed as dist
 from ..ops._native import native
 
 ONESHOT_MAX_BYTES = 256 << 10  # one-shot below, two-shot above (latency vs bytes moved per GPU)
+DEFAULT_TIMEOUT_S = 300.0  # a peer may be this late (wall clock) before the call poisons its output
+MAX_TIMEOUT_S = 1800.0
 
 
 class P2PAllReduce:
     def __init__(self, group=None, capacity_bytes: int = 8 << 20, max_blocks: int = 64,
                  device: Optional[torch.device] = None, oneshot_max_bytes: int = ONESHOT_MAX_BYTES,
-                 rank: Optional[int] = None, world: Optional[int] = None, store=None):
+                 rank: Optional[int] = None, world: Optional[int] = None, store=None,
+                 timeout_s: Optional[float] = None):
         """``store`` (with ``rank``/``world``): exchange the IPC handles through a c10d store instead
-        of a process group (used by the registered backend, which IS the group being built)."""
+        of a process group (used by the registered backend, which IS the group being built).
+        ``timeout_s``: how long (wall clock) a call waits for a late peer; default the group's
+        timeout (``DEFAULT_TIMEOUT_S`` when unknown), at most ``MAX_TIMEOUT_S``."""
         self.group = group
         self.rank = dist.get_rank(group) if rank is None else rank
         self.world = dist.get_world_size(group) if world is None else world
         dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.device = dev
         self.oneshot_max_bytes = int(oneshot_max_bytes)
+        if timeout_s is None:
+            timeout_s = _group_timeout_s(group)
+        self.timeout_s = float(min(max(timeout_s, 1e-3), MAX_TIMEOUT_S))
+        self.stream = torch.cuda.Stream(device=dev)
         self.comm = native().P2PComm(self.rank, self.world, int(capacity_bytes), int(max_blocks), dev.index)
         # [0] epoch, [1] finished-block counter, [2] sticky error: advanced by the kernel itself
         self.state = torch.zeros(4, dtype=torch.int32, device=dev)
@@ -84,8 +98,22 @@ class P2PAllReduce:
         out = t if out is None else out
         if algo is None:
             algo = self.algo_for(t.numel() * t.element_size())
-        self.comm.allreduce(t, out, 1.0 / self.world if average else 1.0, self.state, int(algo))
+        cur = torch.cuda.current_stream(self.device)
+        if cur == self.stream:  # already on the group's stream (e.g. the DDP hook's)
+            self.comm.allreduce(t, out, 1.0 / self.world if average else 1.0, self.state, int(algo), self.timeout_s)
+            return out
+        self.stream.wait_stream(cur)
+        with torch.cuda.stream(self.stream):
+            self.comm.allreduce(t, out, 1.0 / self.world if average else 1.0, self.state, int(algo), self.timeout_s)
+        cur.wait_stream(self.stream)
+        t.record_stream(self.stream)
+        if out is not t:
+            out.record_stream(self.stream)
         return out
+
+    def reset_error(self) -> None:
+        """Clear the sticky error word after a handled failure (stream-ordered, no sync)."""
+        self.state[2].zero_()
 
     def error(self) -> bool:
         """Host sync: True if a peer failed to arrive in any call so far."""
@@ -94,8 +122,28 @@ class P2PAllReduce:
     def check(self) -> None:
         """Raise if any peer failed to arrive (host sync; call outside the hot loop)."""
         if self.error():
-            raise RuntimeError("P2P all-reduce: a peer did not arrive within the spin limit "
+            raise RuntimeError(f"P2P all-reduce: a peer did not arrive within {self.timeout_s:g} s "
                                "(the affected outputs were set to NaN)")
+
+
+def _group_timeout_s(group) -> float:
+    """The process group's timeout in seconds (its backend's ``options._timeout``; for our own
+    registered backend the timeout it was built with); ``DEFAULT_TIMEOUT_S`` when it cannot be read."""
+    try:
+        pg = group if group is not None else dist.distributed_c10d._get_default_group()
+        for dev in ("cuda", "cpu"):
+            try:
+                b = pg._get_backend(torch.device(dev))
+            except Exception:  # noqa: BLE001 — no backend for this device type
+                continue
+            t = getattr(b, "_timeout_s", None)
+            if t is None and hasattr(b, "options"):
+                t = b.options._timeout.total_seconds()
+            if t:
+                return float(t)
+    except Exception:  # noqa: BLE001 — no group: the default
+        pass
+    return DEFAULT_TIMEOUT_S
 
 
 class _StreamFuture:
@@ -120,7 +168,7 @@ class P2PHookState:
         self.p2p = p2p
         self.max_bytes = p2p.capacity if max_bytes is None else max_bytes
         self.process_group = process_group
-        self.stream = torch.cuda.Stream(device=p2p.device)
+        self.stream = p2p.stream  # the group's one stream: every P2P call is ordered on it
         self.p2p_calls = 0
         self.rccl_calls = 0
         # the device error word, copied behind every P2P kernel: read (no sync) on the next call
@@ -131,8 +179,8 @@ class P2PHookState:
         ev = self._err_event
         if ev is not None and not torch.cuda.is_current_stream_capturing() and ev.query() \
                 and int(self._err_host[0]) != 0:
-            raise RuntimeError("P2P all-reduce: a peer did not arrive within the spin limit in an "
-                               "earlier bucket; its gradients were poisoned with NaN")
+            raise RuntimeError(f"P2P all-reduce: a peer did not arrive within {self.p2p.timeout_s:g} s in "
+                               "an earlier bucket; its gradients were poisoned with NaN")
 
 
 def p2p_allreduce_hook(state: P2PHookState, bucket):
@@ -186,8 +234,10 @@ class P2PProcessGroup(dist.ProcessGroup):
         super().__init__(rank, world)
         self._store, self._rank, self._world = store, rank, world
         self._capacity = capacity_bytes
+        self._timeout_s = timeout.total_seconds() if hasattr(timeout, "total_seconds") else DEFAULT_TIMEOUT_S
         if inner_backend is None:
             inner_backend = "nccl" if torch.cuda.is_available() else "gloo"
+        self.inner_backend = inner_backend
         prefix = dist.PrefixStore("pdt_p2p_inner", store)
         if inner_backend == "nccl":
             opts = dist.ProcessGroupNCCL.Options()
@@ -206,7 +256,8 @@ class P2PProcessGroup(dist.ProcessGroup):
             return None
         if self._p2p is None:  # lazily: the device is bound by now
             self._p2p = P2PAllReduce(capacity_bytes=self._capacity, device=t.device, rank=self._rank,
-                                     world=self._world, store=dist.PrefixStore("pdt_p2p_ipc", self._store))
+                                     world=self._world, store=dist.PrefixStore("pdt_p2p_ipc", self._store),
+                                     timeout_s=self._timeout_s)
         return self._p2p if self._p2p.fits(t) and t.device == self._p2p.device else None
 
     def allreduce(self, tensors, opts=None):
@@ -220,6 +271,15 @@ class P2PProcessGroup(dist.ProcessGroup):
                 self.p2p_calls += 1
                 p2p.all_reduce(tensors[0], average=op == dist.ReduceOp.AVG)
                 return _DoneWork(tensors)
+        if op == dist.ReduceOp.AVG and self.inner_backend != "nccl":
+            # gloo has no AVG: SUM, then divide (this path: CPU tensors, or buckets the staging
+            # buffer cannot take, e.g. past its capacity or numel % 8 != 0)
+            sum_opts = dist.AllreduceOptions()
+            sum_opts.reduceOp = dist.ReduceOp.SUM
+            self.inner.allreduce(tensors, sum_opts).wait()
+            for t in tensors:
+                t.div_(self._world)
+            return _DoneWork(tensors)
         return self.inner.allreduce(tensors, opts)
 
     def allreduce_coalesced(self, tensors, opts=None):

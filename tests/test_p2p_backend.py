@@ -18,6 +18,8 @@ def _worker(rank, world):
     assert dist.get_backend() == "pdt_p2p" and ctx.world_size == world
     t = torch.arange(8, dtype=torch.float32) * (rank + 1)
     dist.all_reduce(t)
+    avg = torch.arange(8, dtype=torch.float32) * (rank + 1)
+    dist.all_reduce(avg, op=dist.ReduceOp.AVG)  # gloo has no AVG: the backend sums and divides
     b = torch.full((3,), float(rank))
     dist.broadcast(b, src=1)
     outs = [torch.zeros(2) for _ in range(world)]
@@ -31,14 +33,15 @@ def _worker(rank, world):
     x = torch.ones(3, 4) * (rank + 1)
     ddp(x).sum().backward()
     pg = dist.distributed_c10d._get_default_group()
-    return t, b, torch.stack(outs), m.weight.grad.clone(), isinstance(pg, P2PProcessGroup) or "pdt_p2p"
+    return t, b, torch.stack(outs), m.weight.grad.clone(), isinstance(pg, P2PProcessGroup) or "pdt_p2p", avg
 
 
 def test_pdt_p2p_backend_delegates_on_cpu():
     out = run_ranks(_worker, 2)
     for r in range(2):
-        t, b, g, wg, kind = out[r]
+        t, b, g, wg, kind, avg = out[r]
         assert torch.equal(t, torch.arange(8, dtype=torch.float32) * 3)
+        assert torch.equal(avg, torch.arange(8, dtype=torch.float32) * 1.5)
         assert torch.equal(b, torch.ones(3))
         assert torch.equal(g, torch.tensor([[0., 0.], [1., 1.]]))
         # mean over ranks of sum_batch(x) = 3 * mean(1, 2) = 4.5 per weight entry

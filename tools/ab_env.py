@@ -15,6 +15,23 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
 import bench  # noqa: E402
+from pytorch_distributed_training_example_amd.config import SW  # noqa: E402
+
+
+def apply_env(base: dict, env: dict) -> None:
+    """Make a configuration's switches live: the PDT_* switches are read ONCE into config.SW (and a
+    few decisions are cached per process), so editing os.environ alone changes nothing. Re-read SW,
+    forget the per-shape 1x1 conv decisions (re-seeded from the table under the new switches) and
+    re-read the import-time ResNet switch."""
+    os.environ.clear()
+    os.environ.update(base)
+    os.environ.update(env)
+    SW.reload()
+    from pytorch_distributed_training_example_amd.ops import conv as conv_ops
+    from pytorch_distributed_training_example_amd.models import resnet
+    conv_ops._CHOICE.clear()
+    conv_ops._TABLE_LOADED[0] = False
+    resnet.DS_DEFER_APPLY[0] = os.environ.get("PDT_DS_DEFER", "1") != "0"
 
 
 def main():
@@ -33,9 +50,7 @@ def main():
     res = {n: [] for n, _ in cfgs}
     for rep in range(a.reps):
         for name, env in cfgs:
-            os.environ.clear()
-            os.environ.update(base)
-            os.environ.update(env)
+            apply_env(base, env)
             r = bench.run(args, ctx)
             res[name].append(r["value"])
             print(f"[ab] rep {rep} {name:>12}: {r['value']:9.1f} {r['config'].get('model')} "
