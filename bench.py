@@ -255,6 +255,9 @@ def run(args, ctx):
     dsync()
     launcher.barrier()
     dsync()
+    timing = args.impl == "ours" and runner is None and hasattr(ddp, "enable_comm_timing") and dev.type == "cuda"
+    if timing:  # events only (no host sync inside the timed region)
+        ddp.enable_comm_timing(True)
     if dev.type == "cuda":
         torch.cuda.nvtx.range_push("timed")
     t0 = time.perf_counter()
@@ -266,10 +269,14 @@ def run(args, ctx):
     elapsed = time.perf_counter() - t0
     if dev.type == "cuda":
         torch.cuda.nvtx.range_pop()
+    exposed = ddp.comm_exposed_ms() if timing else None
+    if timing:
+        ddp.enable_comm_timing(False)
     if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed, exposed if exposed is not None else -1.0], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = float(t[0].item())
+        exposed = float(t[1].item()) if t[1].item() >= 0 else None
     ms = elapsed / args.steps * 1e3
     per_step = B * (T if is_lm else 1)
     value = per_step * world * args.steps / elapsed
@@ -283,6 +290,11 @@ def run(args, ctx):
                    "parallelism": f"dp{world}", "grad_accum": args.grad_accum, "impl": args.impl,
                    "graph": bool(runner is not None), "precision": precision, "bucket_cap_mb": args.bucket_cap_mb,
                    "comm_hook": args.comm_hook, "reducer_active": bool(getattr(ddp, "_active", lambda: False)()),
+                   # exposed (not overlapped) communication per step, max over ranks: the compute stream's
+                   # wait on the all-reduces after backward (parallel/ddp.py enable_comm_timing)
+                   "comm_exposed_ms": None if exposed is None else round(exposed, 3),
+                   "bucket_mb": ([round(b / 2 ** 20, 2) for b in ddp.bucket_bytes()]
+                                 if hasattr(ddp, "bucket_bytes") else None),
                    "deterministic": bool(det), "final_loss": round(float(loss.float().item()), 4)},
     }
     return result

@@ -33,13 +33,22 @@ int pdt_mt_copy(int n, void* const* src, void* const* dst, const int64_t* numel,
 int pdt_l2norm_sq(int n, void* const* x, const int64_t* numel, int dtype, float* out, hipStream_t s);
 int pdt_clip_coef(const float* sumsq, float max_norm, float* coef, float* norm, hipStream_t s);
 int64_t pdt_bn_workspace_floats(int64_t M, int C);
+int pdt_lenet_tail_fwd(const float* p1, const float* w2, const float* b2, const float* w3, const float* b3,
+                       const float* fw1, const float* fb1, const float* fw2, const float* fb2, float slope, int N,
+                       float* logits, uint8_t* code2, float* p2, float* h3, float* h4, hipStream_t s);
+int64_t pdt_lenet_tail_ws_floats(int N);
+int pdt_lenet_tail_bwd(const float* dl, const float* p1, const float* w2, const float* b2, const float* w3,
+                       const float* b3, const float* fw1, const float* fb1, const float* fw2, const float* fb2,
+                       float slope, int N, const uint8_t* code2, const float* p2, const float* h3, const float* h4,
+                       float* ws, float* dp1, float* dw2, float* db2, float* dw3, float* db3, float* dfw1, float* dfb1,
+                       float* dfw2, float* dfb2, hipStream_t s);
 int pdt_bn_bwd_coef(const uint16_t* dy, const uint16_t* x, const uint8_t* mask, const float* gamma, const float* mean,
                     const float* invstd, int64_t M, int C, int relu, float* coef, float* dgamma, float* dbeta, float* ws,
                     unsigned* counters, hipStream_t s);
 int pdt_bn_bwd_coef_tiles(const float* part, int T, const float* gamma, const float* invstd, int64_t M, int C,
                           float* coef, float* dgamma, float* dbeta, float* ws, hipStream_t s);
 int pdt_conv1x1_bwd_fused_ok(int C4, int CW);
-int pdt_conv1x1_bwd_fused_grid(int M);
+int pdt_conv1x1_bwd_fused_grid(int M, int C4, int CW);
 int pdt_conv1x1_bwd_fused(const uint16_t* dy, const uint16_t* z, const uint8_t* mz, const float* mean, const float* A,
                           const float* B, const float* D, const uint16_t* wt, const uint16_t* xa, const uint16_t* bx,
                           const uint8_t* bm, const float* bmean, float* bpart, uint16_t* dxa, uint16_t* dw, float* ws,
@@ -681,7 +690,7 @@ std::vector<Tensor> conv1x1_bwd_fused(Tensor dy, Tensor z, Tensor mz, Tensor mea
   auto wt = w.reshape({C4, CW}).t().contiguous();
   auto dxa = at::empty_like(xa);
   auto dw = at::empty({C4, CW}, w.options());
-  const int G = pdt_conv1x1_bwd_fused_grid((int)M);
+  const int G = pdt_conv1x1_bwd_fused_grid((int)M, (int)C4, (int)CW);
   auto fopt = z.options().dtype(at::kFloat);
   auto ws = at::empty({(int64_t)G * C4 * CW}, fopt);
   const bool bst = bn_x.has_value() && bn_x->defined();
@@ -712,6 +721,65 @@ std::vector<Tensor> conv1x1_bwd_fused(Tensor dy, Tensor z, Tensor mz, Tensor mea
                                        (int)CW, stream());
   TORCH_CHECK(rc == 0, "pdt_conv1x1_bwd_fused failed: ", rc);
   return {dxa, dw.view(w.sizes()), part};
+}
+
+// ----------------------------------------------------------------------------- LeNet tail (fp32)
+// The reference LeNet after the stem (cnn.py:13-22) in one forward kernel / two backward kernels
+// (csrc/kernels/lenet_tail.hip). ws: the 8 tail parameters in module order (w2, b2, w3, b3, fw1, fb1,
+// fw2, fb2), contiguous fp32.
+void check_tail_params(const std::vector<Tensor>& w) {
+  TORCH_CHECK(w.size() == 8, "lenet_tail: 8 parameters (conv2 w/b, conv3 w/b, fc1 w/b, fc2 w/b)");
+  const int64_t numel[8] = {2400, 16, 48000, 120, 10080, 84, 840, 10};
+  for (int i = 0; i < 8; ++i) {
+    check_cuda(w[i], "lenet_tail param");
+    TORCH_CHECK(w[i].scalar_type() == at::kFloat && w[i].is_contiguous() && w[i].numel() == numel[i],
+                "lenet_tail: parameter ", i, " must be contiguous fp32 with ", numel[i], " elements");
+  }
+}
+
+std::vector<Tensor> lenet_tail_fwd(Tensor p1, std::vector<Tensor> w, double slope) {
+  check_tail_params(w);
+  check_cuda(p1, "p1");
+  TORCH_CHECK(p1.scalar_type() == at::kFloat && p1.is_contiguous() && p1.dim() == 4 && p1.size(1) == 6 &&
+              p1.size(2) == 14 && p1.size(3) == 14, "lenet_tail_fwd: p1 [N,6,14,14] contiguous fp32");
+  const int64_t N = p1.size(0);
+  auto o = p1.options();
+  auto logits = at::empty({N, 10}, o);
+  auto code2 = at::empty({N, 400}, o.dtype(at::kByte));
+  auto p2 = at::empty({N, 400}, o), h3 = at::empty({N, 120}, o), h4 = at::empty({N, 84}, o);
+  const int rc = pdt_lenet_tail_fwd(p1.data_ptr<float>(), w[0].data_ptr<float>(), w[1].data_ptr<float>(),
+                                    w[2].data_ptr<float>(), w[3].data_ptr<float>(), w[4].data_ptr<float>(),
+                                    w[5].data_ptr<float>(), w[6].data_ptr<float>(), w[7].data_ptr<float>(),
+                                    (float)slope, (int)N, logits.data_ptr<float>(), code2.data_ptr<uint8_t>(),
+                                    p2.data_ptr<float>(), h3.data_ptr<float>(), h4.data_ptr<float>(), stream());
+  TORCH_CHECK(rc == 0, "pdt_lenet_tail_fwd failed: ", rc);
+  return {logits, code2, p2, h3, h4};
+}
+
+// -> {dp1, dw2, db2, dw3, db3, dfw1, dfb1, dfw2, dfb2} (parameter gradients in the parameters' shapes)
+std::vector<Tensor> lenet_tail_bwd(Tensor dl, Tensor p1, std::vector<Tensor> w, double slope, Tensor code2, Tensor p2,
+                                   Tensor h3, Tensor h4) {
+  check_tail_params(w);
+  const int64_t N = p1.size(0);
+  dl = dl.contiguous().to(at::kFloat);
+  TORCH_CHECK(dl.numel() == N * 10 && code2.numel() == N * 400 && p2.numel() == N * 400 && h3.numel() == N * 120 &&
+              h4.numel() == N * 84, "lenet_tail_bwd: saved tensor sizes");
+  auto o = p1.options();
+  auto ws = at::empty({pdt_lenet_tail_ws_floats((int)N)}, o);
+  auto dp1 = at::empty_like(p1);
+  std::vector<Tensor> g;
+  for (const auto& t : w) g.push_back(at::empty_like(t));
+  const int rc = pdt_lenet_tail_bwd(dl.data_ptr<float>(), p1.data_ptr<float>(), w[0].data_ptr<float>(),
+                                    w[1].data_ptr<float>(), w[2].data_ptr<float>(), w[3].data_ptr<float>(),
+                                    w[4].data_ptr<float>(), w[5].data_ptr<float>(), w[6].data_ptr<float>(),
+                                    w[7].data_ptr<float>(), (float)slope, (int)N, code2.data_ptr<uint8_t>(),
+                                    p2.data_ptr<float>(), h3.data_ptr<float>(), h4.data_ptr<float>(),
+                                    ws.data_ptr<float>(), dp1.data_ptr<float>(), g[0].data_ptr<float>(),
+                                    g[1].data_ptr<float>(), g[2].data_ptr<float>(), g[3].data_ptr<float>(),
+                                    g[4].data_ptr<float>(), g[5].data_ptr<float>(), g[6].data_ptr<float>(),
+                                    g[7].data_ptr<float>(), stream());
+  TORCH_CHECK(rc == 0, "pdt_lenet_tail_bwd failed: ", rc);
+  return {dp1, g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7]};
 }
 
 // ----------------------------------------------------------------------------- 1x1 conv GEMM (+ BN stats)
@@ -1690,5 +1758,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lenet_stem_bwd", &lenet_stem_bwd);
   m.def("leaky_pool_fwd", &leaky_pool_fwd);
   m.def("leaky_pool_bwd", &leaky_pool_bwd);
+  m.def("lenet_tail_fwd", &lenet_tail_fwd);
+  m.def("lenet_tail_bwd", &lenet_tail_bwd);
   m.def("softmax_nll_small", &softmax_nll_small);
 }

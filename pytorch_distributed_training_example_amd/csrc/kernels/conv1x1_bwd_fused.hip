@@ -44,34 +44,44 @@ typedef short s4v __attribute__((ext_vector_type(4)));
 __device__ __attribute__((aligned(256))) uint4 g_fb_zero[64];  // zero page for pixels past M (never written)
 __device__ uint4 g_fb_sink[256];  // epilogue stores of rows past M land here (keeps the vmcnt count exact)
 
+// C4: the BatchNorm's channels (conv output), CW: the conv's input channels. A workgroup owns a
+// 64-channel slice of CW ("role"; CW / 64 roles, each role's workgroup computes the full dz of its
+// pixels — the roles of one pixel group are placed on one XCD, so the second read of dy / z is an
+// L2 hit), the dgrad output of its slice and the wgrad columns of its slice.
 template <int C4_, int CW_, bool BSTATS_>
 struct FB {
-  static constexpr int C4 = C4_, CW = CW_, KP = 32, kSlots = 3, kWaves = 4, kThreads = 256;
+  static constexpr int C4 = C4_, CW = CW_, NR = CW / 64, kSlots = 3, kWaves = 4, kThreads = 256;
+  static constexpr int KP = C4 >= 512 ? 16 : 32;  // pixels per stage (LDS: 3 slots + the dz tile)
   static constexpr bool BSTATS = BSTATS_;
-  static constexpr int kRowY = C4 * 2, kRowX = CW * 2;
-  static constexpr int kY = KP * kRowY, kMZ = KP * C4 / 8, kXA = KP * kRowX, kMB = KP * CW / 8;
+  static constexpr int kRowY = C4 * 2, kRowX = 128;  // LDS rows: dy / z / dz; the 64-channel slices
+  static constexpr int kY = KP * kRowY, kMZ = KP * C4 / 8, kXA = KP * kRowX, kMB = KP * 8;
+  // 16-B DMA pieces (1 KB per wave instruction): Y, Z, XA (, XB), padded to a multiple of the waves
+  static constexpr int pY = kY / 1024, pX = kXA / 1024;
+  static constexpr int p16 = 2 * pY + pX * (BSTATS ? 2 : 1);
+  static constexpr int n16 = (p16 + kWaves - 1) / kWaves;
+  // mask bits: bn3's by 4-B DMA (256 B per instruction), bn2's slice by 1-B DMA (64 B)
+  static constexpr int nMZ = kMZ / 256 / kWaves;
+  static constexpr int pMB = BSTATS ? kMB / 64 : 0;
+  static constexpr int nMB = (pMB + kWaves - 1) / kWaves;
   static constexpr int oY = 0, oZ = kY, oMZ = 2 * kY, oXA = oMZ + kMZ, oXB = oXA + kXA;
-  static constexpr int oMB = BSTATS ? oXB + kXA : oXB;
-  static constexpr int kSlot = ((BSTATS ? oMB + kMB : oMB) + 255) / 256 * 256;
+  static constexpr int oMB = oXB + (BSTATS ? kXA : 0);
+  static constexpr int oPad = oMB + nMB * kWaves * 64;        // dummy pieces land here
+  static constexpr int kSlot = (oPad + (n16 * kWaves > p16 ? 1024 : 0) + 255) / 256 * 256;
   static constexpr int oDZ = kSlots * kSlot;
   static constexpr int kLds = oDZ + kY;
-  // DMA instructions per wave per stage: 16-B pieces (1 KB / instr), mask bits 4 B (256 B) / 1 B (64 B)
-  static constexpr int nY = kY / 1024 / kWaves, nMZ = kMZ / 256 / kWaves, nXA = kXA / 1024 / kWaves;
-  static constexpr int nMB = kMB / 64 / kWaves;
-  static constexpr int kG = 2 * nY + nMZ + nXA + (BSTATS ? nXA + nMB : 0);
-  // epilogue: one 16-B chunk of the dgrad tile per thread per stage (stored -> counted in vmcnt)
-  static constexpr int kEpiChunks = KP * CW / 8 / kThreads;
-  static constexpr int kStageOps = kG + kEpiChunks;
+  static constexpr int kG = n16 + nMZ + nMB;  // DMA instructions per wave per stage
+  // epilogue: one 16-B chunk of the dgrad slice per thread per stage (threads past the tile store
+  // to a sink: every thread stores once, so the vmcnt counts are exact)
+  static constexpr int kStageOps = kG + 1;
   static constexpr int kStgStride = kRowX + 16;  // staging rows padded: conflict-free 8-B writes
-  // dgrad: a wave owns 16 output channels; wgrad: a wave owns C4 / 4 rows of dW
-  static constexpr int kKS = C4 / 32;         // 16x16x32 k-steps over the input channels
-  static constexpr int kPB = KP / 16;         // pixel blocks of the dgrad tile
-  static constexpr int kWR = C4 / kWaves;     // dW rows per wave
-  static constexpr int kMI = kWR / 32, kNJ = CW / 32;
-  static_assert(CW == 16 * kWaves, "a wave owns 16 dgrad channels");
-  static_assert(nY * 1024 * kWaves == kY && nMZ * 256 * kWaves == kMZ && nXA * 1024 * kWaves == kXA, "DMA split");
-  static_assert(!BSTATS || nMB * 64 * kWaves == kMB, "DMA split (mask b)");
-  static_assert(kEpiChunks == 1, "one epilogue chunk per thread");
+  static constexpr int kKS = C4 / 32;   // 16x16x32 k-steps of the dgrad (W^T fragments in VGPRs)
+  static constexpr int kPB = KP / 16;   // pixel blocks of the dgrad tile
+  static constexpr int kWR = C4 / kWaves;  // dW rows per wave
+  static constexpr int kMI = kWR / 32, kNJ = 2;
+  static_assert(CW % 64 == 0 && C4 % 256 == 0, "shapes");
+  static_assert(nMZ * 256 * kWaves == kMZ, "DMA split (bn3 mask)");
+  static_assert(KP * 8 <= kThreads, "one epilogue chunk per thread at most");
+  static_assert(KP * C4 / 8 % kThreads == 0, "transform chunks");
   static_assert(KP * kStgStride <= kY, "staging fits the dead z region");
   static_assert(kLds <= 160 * 1024, "LDS");
 };
@@ -130,38 +140,44 @@ struct FBArgs {
   const float* D;
   const uint16_t* wt;   // [CW][C4] conv weight transposed (W^T)
   const uint16_t* xa;   // [M][CW] conv input
-  BnSrc bs;             // bn2: input xb [M][CW], mask, mean; part [2][G][CW]
+  BnSrc bs;             // bn2: input xb [M][CW], mask, mean; part [2][Gp][CW]
   uint16_t* dxa;        // [M][CW]
-  float* ws;            // [G][C4][CW] wgrad partials
-  int M, ntiles;
+  float* ws;            // [Gp][C4][CW] wgrad partials
+  int M, ntiles, Gp;    // Gp: pixel groups (workgroups per role)
 };
 
 template <class Cf>
 __global__ __launch_bounds__(Cf::kThreads, 1) void conv1x1_bwd_fused_kernel(FBArgs a) {
-  constexpr int C4 = Cf::C4, CW = Cf::CW, KP = Cf::KP, RY = Cf::kRowY, RX = Cf::kRowX;
+  constexpr int C4 = Cf::C4, CW = Cf::CW, KP = Cf::KP, RY = Cf::kRowY, RX = Cf::kRowX, NR = Cf::NR;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int G = gridDim.x, g = blockIdx.x;
-  const int S = (a.ntiles - g + G - 1) / G;  // stages of this workgroup: tiles g, g + G, ...
+  // block -> (pixel group, role): the NR roles of a pixel group are blocks b, b + 8, ... (one XCD
+  // under round-robin placement: the second read of dy / z hits L2 — speed only, never correctness)
+  const int b = blockIdx.x;
+  const int role = (b / 8) % NR, pg = (b % 8) + 8 * (b / (8 * NR));
+  const int Gp = a.Gp, cs = role * 64;  // this workgroup's slice of CW
+  if (pg >= Gp) return;  // the grid is rounded up to whole XCD pairings (uniform exit, no barrier yet)
+  const int S = (a.ntiles - pg + Gp - 1) / Gp;  // tiles pg, pg + Gp, ... (Gp <= ntiles: S >= 1)
 
   // ---- kernel-lifetime registers: W^T fragments (dgrad A operand), the transform coefficients
   bf16x8 wf[Cf::kKS];
 #pragma unroll
   for (int ks = 0; ks < Cf::kKS; ++ks)
-    wf[ks] = *reinterpret_cast<const bf16x8*>(a.wt + (16 * wid + (lane & 15)) * C4 + 32 * ks + 8 * (lane >> 4));
+    wf[ks] = *reinterpret_cast<const bf16x8*>(a.wt + (int64_t)(cs + 16 * wid + (lane & 15)) * C4 + 32 * ks +
+                                              8 * (lane >> 4));
   const int tc = tid % (C4 / 8);  // transform pass: this thread's 8-channel chunk
   float cm[8], cA[8], cB[8], cD[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     cm[k] = a.mean[tc * 8 + k]; cA[k] = a.A[tc * 8 + k]; cB[k] = a.B[tc * 8 + k]; cD[k] = a.D[tc * 8 + k];
   }
-  const int ec = tid % (CW / 8);  // epilogue: this thread's chunk of the dgrad tile
+  const int ec = tid % 8, er = tid / 8;  // epilogue: chunk / pixel row of the dgrad slice tile
   float bmu[8], bs1[8], bs2[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) { bs1[k] = 0.f; bs2[k] = 0.f; bmu[k] = 0.f; }
   if constexpr (Cf::BSTATS) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) bmu[k] = a.bs.mean[ec * 8 + k];
+    for (int k = 0; k < 8; ++k) bmu[k] = a.bs.mean[cs + ec * 8 + k];
   }
   // the loads above complete before any DMA is issued (no vmcnt(0) inside the ring)
 #pragma unroll
@@ -169,88 +185,74 @@ __global__ __launch_bounds__(Cf::kThreads, 1) void conv1x1_bwd_fused_kernel(FBAr
 #pragma unroll
   for (int k = 0; k < 8; ++k) asm volatile("" : "+v"(cm[k]), "+v"(cA[k]), "+v"(cB[k]), "+v"(cD[k]), "+v"(bmu[k]));
 
-  // ---- per-lane DMA pieces (stage independent): pixel row in the stage and source offset
-  int yrow[Cf::nY], yoff[Cf::nY];
+  // ---- per-lane 16-B DMA pieces (stage independent). Piece q = wid + kWaves * i of the stage's
+  // list [Y pieces][Z pieces][XA pieces][XB pieces][dummies]: source = base + p0 * stride + off,
+  // valid while the pixel row is < M (else the zero page), LDS destination = slot + dst.
+  const uint16_t* pbase[Cf::n16];
+  int pstride[Cf::n16], prow[Cf::n16], poff[Cf::n16], pdst[Cf::n16];
 #pragma unroll
-  for (int i = 0; i < Cf::nY; ++i) {
-    const int o = (wid * Cf::nY + i) * 1024 + lane * 16;
-    yrow[i] = o / RY;
-    yoff[i] = yrow[i] * C4 + ((o % RY) >> 4) * 8;
-  }
-  int mzrow[Cf::nMZ], mzoff[Cf::nMZ];
-#pragma unroll
-  for (int i = 0; i < Cf::nMZ; ++i) {
-    const int o = (wid * Cf::nMZ + i) * 256 + lane * 4;
-    mzrow[i] = o / (C4 / 8);
-    mzoff[i] = o;  // bytes from the stage's first mask byte
-  }
-  int xrow[Cf::nXA], xoff[Cf::nXA];
-#pragma unroll
-  for (int i = 0; i < Cf::nXA; ++i) {
-    const int o = (wid * Cf::nXA + i) * 1024 + lane * 16;
-    xrow[i] = o / RX;
-    xoff[i] = xrow[i] * CW + swz128(xrow[i], (o % RX) >> 4) * 8;
-  }
-  int mbrow[Cf::nMB > 0 ? Cf::nMB : 1], mboff[Cf::nMB > 0 ? Cf::nMB : 1];
-#pragma unroll
-  for (int i = 0; i < Cf::nMB; ++i) {
-    const int o = (wid * Cf::nMB + i) * 64 + lane;
-    mbrow[i] = o / (CW / 8);
-    mboff[i] = o;
+  for (int i = 0; i < Cf::n16; ++i) {
+    const int q = wid + Cf::kWaves * i;
+    if (q < 2 * Cf::pY) {  // dy / z: linear 512-B / 1-KB rows
+      const int o = (q % Cf::pY) * 1024 + lane * 16;
+      pbase[i] = q < Cf::pY ? a.dy : a.z;
+      pstride[i] = C4;
+      prow[i] = o / RY;
+      poff[i] = prow[i] * C4 + ((o % RY) >> 4) * 8;
+      pdst[i] = (q < Cf::pY ? Cf::oY : Cf::oZ) + (q % Cf::pY) * 1024;
+    } else if (q < 2 * Cf::pY + (Cf::BSTATS ? 2 : 1) * Cf::pX) {  // xa / xb slices: swizzled 128-B rows
+      const int qq = q - 2 * Cf::pY, k = qq % Cf::pX;
+      const int o = k * 1024 + lane * 16;
+      pbase[i] = (qq < Cf::pX ? a.xa : a.bs.x) + cs;
+      pstride[i] = CW;
+      prow[i] = o / RX;
+      poff[i] = prow[i] * CW + swz128(prow[i], (o % RX) >> 4) * 8;
+      pdst[i] = (qq < Cf::pX ? Cf::oXA : Cf::oXB) + k * 1024;
+    } else {  // dummy: zero page -> the slot's pad area (keeps every wave's DMA count equal)
+      pbase[i] = reinterpret_cast<const uint16_t*>(g_fb_zero);
+      pstride[i] = 0;
+      prow[i] = 0;
+      poff[i] = 0;
+      pdst[i] = Cf::oPad;
+    }
   }
   auto issue = [&](int s) {
     char* slot = lds + (s % Cf::kSlots) * Cf::kSlot;
-    const int p0 = (g + s * G) * KP;
-    const uint16_t* yb = a.dy + (int64_t)p0 * C4;
-    const uint16_t* zb = a.z + (int64_t)p0 * C4;
+    const int p0 = (pg + s * Gp) * KP;
 #pragma unroll
-    for (int i = 0; i < Cf::nY; ++i) {
-      const bool ok = p0 + yrow[i] < a.M;
-      dma<16>(ok ? (const void*)(yb + yoff[i]) : (const void*)g_fb_zero, slot + Cf::oY + (wid * Cf::nY + i) * 1024);
-    }
-#pragma unroll
-    for (int i = 0; i < Cf::nY; ++i) {
-      const bool ok = p0 + yrow[i] < a.M;
-      dma<16>(ok ? (const void*)(zb + yoff[i]) : (const void*)g_fb_zero, slot + Cf::oZ + (wid * Cf::nY + i) * 1024);
+    for (int i = 0; i < Cf::n16; ++i) {
+      const bool ok = p0 + prow[i] < a.M;
+      dma<16>(ok ? (const void*)(pbase[i] + (int64_t)p0 * pstride[i] + poff[i]) : (const void*)g_fb_zero,
+              slot + pdst[i]);
     }
 #pragma unroll
     for (int i = 0; i < Cf::nMZ; ++i) {
-      const bool ok = p0 + mzrow[i] < a.M;
-      dma<4>(ok ? (const void*)(a.mz + (int64_t)p0 * (C4 / 8) + mzoff[i]) : (const void*)g_fb_zero,
+      const int o = (wid * Cf::nMZ + i) * 256 + lane * 4;
+      const bool ok = p0 + o / (C4 / 8) < a.M;
+      dma<4>(ok ? (const void*)(a.mz + (int64_t)p0 * (C4 / 8) + o) : (const void*)g_fb_zero,
              slot + Cf::oMZ + (wid * Cf::nMZ + i) * 256);
     }
 #pragma unroll
-    for (int i = 0; i < Cf::nXA; ++i) {
-      const bool ok = p0 + xrow[i] < a.M;
-      dma<16>(ok ? (const void*)(a.xa + (int64_t)p0 * CW + xoff[i]) : (const void*)g_fb_zero,
-              slot + Cf::oXA + (wid * Cf::nXA + i) * 1024);
-    }
-    if constexpr (Cf::BSTATS) {
-#pragma unroll
-      for (int i = 0; i < Cf::nXA; ++i) {
-        const bool ok = p0 + xrow[i] < a.M;
-        dma<16>(ok ? (const void*)(a.bs.x + (int64_t)p0 * CW + xoff[i]) : (const void*)g_fb_zero,
-                slot + Cf::oXB + (wid * Cf::nXA + i) * 1024);
-      }
-#pragma unroll
-      for (int i = 0; i < Cf::nMB; ++i) {
-        const bool ok = p0 + mbrow[i] < a.M;
-        dma<1>(ok ? (const void*)(a.bs.mask + (int64_t)p0 * (CW / 8) + mboff[i]) : (const void*)g_fb_zero,
-               slot + Cf::oMB + (wid * Cf::nMB + i) * 64);
-      }
+    for (int i = 0; i < Cf::nMB; ++i) {  // bn2's mask bytes of the slice: 8 per pixel
+      const int q = wid + Cf::kWaves * i;
+      const int o = q * 64 + lane, row = o / 8;
+      const bool real = q < Cf::pMB && a.bs.mask != nullptr;
+      const bool ok = real && p0 + row < a.M;
+      dma<1>(ok ? (const void*)(a.bs.mask + ((int64_t)(p0 + row) * CW + cs) / 8 + (o % 8)) : (const void*)g_fb_zero,
+             slot + (real ? Cf::oMB + q * 64 : Cf::oPad));
     }
   };
 
   // ---- wgrad lane roles (transposed reads; conv1x1_wgrad.hip)
   const int grp = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-  const int prow = 8 * (grp >> 1) + q, half8 = (p & 1) * 8;
+  const int prw = 8 * (grp >> 1) + q, half8 = (p & 1) * 8;
   int ya[Cf::kMI], xa[Cf::kNJ];
 #pragma unroll
   for (int i = 0; i < Cf::kMI; ++i)
-    ya[i] = prow * RY + (swz_dz(prow, (wid * Cf::kWR + 32 * i + 16 * (grp & 1) + 4 * p) >> 3) << 4) + half8;
+    ya[i] = prw * RY + (swz_dz(prw, (wid * Cf::kWR + 32 * i + 16 * (grp & 1) + 4 * p) >> 3) << 4) + half8;
 #pragma unroll
   for (int j = 0; j < Cf::kNJ; ++j)
-    xa[j] = prow * RX + (swz128(prow, (32 * j + 16 * (grp & 1) + 4 * p) >> 3) << 4) + half8;
+    xa[j] = prw * RX + (swz128(prw, (32 * j + 16 * (grp & 1) + 4 * p) >> 3) << 4) + half8;
   f16v acc[Cf::kMI][Cf::kNJ];
 #pragma unroll
   for (int i = 0; i < Cf::kMI; ++i)
@@ -265,14 +267,14 @@ __global__ __launch_bounds__(Cf::kThreads, 1) void conv1x1_bwd_fused_kernel(FBAr
     if (s < S) issue(s);
   for (int s = 0; s < S; ++s) {
     // stage s's DMA is done once only the next stage's DMA (+ the previous stage's epilogue store,
-    // issued after it) is pending; every count is exact (rows past M store to a sink)
+    // issued after it) is pending; every count is exact
     if (s + 1 >= S) wait_vm<0>();
     else if (s == 0) wait_vm<Cf::kG>();
     else wait_vm<Cf::kStageOps>();
     lds_barrier();  // B1: DMA(s) visible to all waves; every wave is past stage s-1
     if (s + Cf::kSlots - 1 < S) issue(s + Cf::kSlots - 1);  // its slot was last used in stage s-1
     const char* slot = lds + (s % Cf::kSlots) * Cf::kSlot;
-    const int p0 = (g + s * G) * KP;
+    const int p0 = (pg + s * Gp) * KP;
 
     // ---- transform: dz = A dy m + B (z - mean) + D -> swizzled dz tile (rows past M: zero)
 #pragma unroll
@@ -312,11 +314,11 @@ __global__ __launch_bounds__(Cf::kThreads, 1) void conv1x1_bwd_fused_kernel(FBAr
 #pragma unroll
       for (int pb = 0; pb < Cf::kPB; ++pb) {
         const int row = 16 * pb + (lane & 15), ch = 4 * ks + (lane >> 4);
-        const bf16x8 b = *reinterpret_cast<const bf16x8*>(dzs + row * RY + (swz_dz(row, ch) << 4));
-        dacc[pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ks], b, dacc[pb], 0, 0, 0);
+        const bf16x8 bv = *reinterpret_cast<const bf16x8*>(dzs + row * RY + (swz_dz(row, ch) << 4));
+        dacc[pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ks], bv, dacc[pb], 0, 0, 0);
       }
     }
-    // ---- wgrad: dW[c][k] += sum_px dz[px][c] xa[px][k]
+    // ---- wgrad: dW[c][cs + k] += sum_px dz[px][c] xa[px][cs + k]
     const char* xas = slot + Cf::oXA;
 #pragma unroll
     for (int kk = 0; kk < KP / 16; ++kk) {
@@ -343,7 +345,7 @@ __global__ __launch_bounds__(Cf::kThreads, 1) void conv1x1_bwd_fused_kernel(FBAr
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
     }
 
-    // ---- epilogue: stage the bf16 dgrad tile [KP][CW] in the dead z region, then 16-B rows out
+    // ---- epilogue: stage the bf16 dgrad slice [KP][64] in the dead z region, then 16-B rows out
     char* stg = const_cast<char*>(slot) + Cf::oZ;
 #pragma unroll
     for (int pb = 0; pb < Cf::kPB; ++pb) {
@@ -356,15 +358,15 @@ __global__ __launch_bounds__(Cf::kThreads, 1) void conv1x1_bwd_fused_kernel(FBAr
     }
     lds_barrier();  // B3
     {
-      const int px = tid / (CW / 8);
-      const uint4 v = *reinterpret_cast<const uint4*>(stg + px * Cf::kStgStride + ec * 16);
-      if (p0 + px < a.M) {
+      const bool in_tile = er < KP;
+      const uint4 v = *reinterpret_cast<const uint4*>(stg + (in_tile ? er : 0) * Cf::kStgStride + ec * 16);
+      if (in_tile && p0 + er < a.M) {
         if constexpr (Cf::BSTATS) {
-          const uint4 xb = *reinterpret_cast<const uint4*>(slot + Cf::oXB + px * RX + (swz128(px, ec) << 4));
-          const unsigned mk = *reinterpret_cast<const uint8_t*>(slot + Cf::oMB + px * (CW / 8) + ec);
+          const uint4 xb = *reinterpret_cast<const uint4*>(slot + Cf::oXB + er * RX + (swz128(er, ec) << 4));
+          const unsigned mk = *reinterpret_cast<const uint8_t*>(slot + Cf::oMB + er * 8 + ec);
           bn_bwd_accum8(v, xb, a.bs.mask ? mk : 0xffu, bmu, bs1, bs2);
         }
-        *reinterpret_cast<uint4*>(a.dxa + (int64_t)(p0 + px) * CW + ec * 8) = v;
+        *reinterpret_cast<uint4*>(a.dxa + (int64_t)(p0 + er) * CW + cs + ec * 8) = v;
       } else {
         g_fb_sink[tid] = v;  // one store per thread per stage, always (exact vmcnt counts)
       }
@@ -374,9 +376,9 @@ __global__ __launch_bounds__(Cf::kThreads, 1) void conv1x1_bwd_fused_kernel(FBAr
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
 
-  // ---- wgrad partials ws[g][c][k]; 32x32 accumulator: lane holds k = l % 32,
+  // ---- wgrad partials ws[pg][c][cs + k]; 32x32 accumulator: lane holds k = l % 32,
   // c = 8 (v / 4) + 4 (l / 32) + v % 4 for v = 0..15
-  float* wsp = a.ws + (int64_t)g * C4 * CW;
+  float* wsp = a.ws + (int64_t)pg * C4 * CW + cs;
 #pragma unroll
   for (int i = 0; i < Cf::kMI; ++i)
 #pragma unroll
@@ -389,7 +391,7 @@ __global__ __launch_bounds__(Cf::kThreads, 1) void conv1x1_bwd_fused_kernel(FBAr
       }
     }
   if constexpr (Cf::BSTATS)
-    bn_bwd_tile_store<CW, Cf::kWaves>(bs1, bs2, reinterpret_cast<float*>(lds), a.bs.part, G, g, CW, 0);
+    bn_bwd_tile_store<64, Cf::kWaves>(bs1, bs2, reinterpret_cast<float*>(lds), a.bs.part, Gp, pg, CW, cs);
 }
 
 // dw[c][k] (bf16) = sum over the G workgroup partials in a fixed order (conv1x1_wgrad.hip's scheme:
@@ -421,10 +423,13 @@ __global__ __launch_bounds__(256) void fb_reduce_kernel(const float* __restrict_
   }
 }
 
-int g_grid = 0;  // 0: one workgroup per CU (256)
+int g_grid = 0;  // 0: by shape (one workgroup per CU)
 
-inline int grid_of(int ntiles) {
-  const int want = g_grid > 0 ? g_grid : 256;
+// pixel groups: one workgroup per CU in all (NR roles each), a multiple of 8 (XCD pairing)
+inline int groups_of(int ntiles, int nr) {
+  int want = g_grid > 0 ? g_grid : 256;
+  want = want / nr / 8 * 8;
+  if (want < 8) want = 8;
   return ntiles < want ? ntiles : want;
 }
 
@@ -437,40 +442,54 @@ int launch(const FBArgs& a0, uint16_t* dw, hipStream_t s) {
       return -3;
     attr = true;
   }
-  const int G = grid_of(a0.ntiles);
-  hipLaunchKernelGGL(conv1x1_bwd_fused_kernel<Cf>, dim3(G), dim3(Cf::kThreads), Cf::kLds, s, a0);
+  // every role of every pixel group: Gp groups x NR roles, with the pairing of the block map
+  // (groups past ntiles run zero stages; the grid stays a multiple of 8 * NR)
+  const int nblk = ((a0.Gp + 7) / 8) * 8 * Cf::NR;
+  hipLaunchKernelGGL(conv1x1_bwd_fused_kernel<Cf>, dim3(nblk), dim3(Cf::kThreads), Cf::kLds, s, a0);
   const int64_t n4 = (int64_t)Cf::C4 * Cf::CW / 4;
   hipLaunchKernelGGL(fb_reduce_kernel, dim3((unsigned)((n4 + kRedCols - 1) / kRedCols)), dim3(kRedCols * kRedGroups),
-                     0, s, a0.ws, dw, G, n4);
+                     0, s, a0.ws, dw, a0.Gp, n4);
   return 0;
 }
+
+inline int kp_of(int C4) { return C4 >= 512 ? 16 : 32; }
 
 }  // namespace
 
 extern "C" {
 
-// Shapes the fused kernel takes: (C4, CW) = (256, 64) (ResNet-50 layer 1).
-int pdt_conv1x1_bwd_fused_ok(int C4, int CW) { return C4 == 256 && CW == 64; }
+// Shapes the fused kernel takes: (C4, CW) = (256, 64) and (512, 128) (ResNet-50 layers 1 and 2).
+int pdt_conv1x1_bwd_fused_ok(int C4, int CW) { return (C4 == 256 && CW == 64) || (C4 == 512 && CW == 128); }
 
-// Workgroups (= partial slabs) of a call: wgrad workspace G*C4*CW floats, bn2 partials [2][G][CW].
-int pdt_conv1x1_bwd_fused_grid(int M) { return grid_of((M + 31) / 32); }
+// Pixel groups of a call = wgrad partial slabs (workspace Gp*C4*CW floats) = bn2 partial rows
+// ([2][Gp][CW]).
+int pdt_conv1x1_bwd_fused_grid(int M, int C4, int CW) {
+  const int kp = kp_of(C4);
+  return groups_of((M + kp - 1) / kp, CW / 64);
+}
 
 // See the header. dy, z: [M][C4]; mz: M*C4/8 bytes; mean/A/B/D: [C4]; wt: [CW][C4]; xa: [M][CW];
 // bx / bm / bmean / bpart (all null = no bn2 reduction; bm may be null = no ReLU): bn2's input
-// [M][CW], mask, mean [CW] and the [2][G][CW] partials out; dxa: [M][CW]; dw: [C4][CW] bf16;
-// ws: G*C4*CW floats. Returns 0, -1 for an unsupported shape.
+// [M][CW], mask, mean [CW] and the [2][Gp][CW] partials out; dxa: [M][CW]; dw: [C4][CW] bf16;
+// ws: Gp*C4*CW floats. Returns 0, -1 for an unsupported shape.
 int pdt_conv1x1_bwd_fused(const uint16_t* dy, const uint16_t* z, const uint8_t* mz, const float* mean, const float* A,
                           const float* B, const float* D, const uint16_t* wt, const uint16_t* xa, const uint16_t* bx,
                           const uint8_t* bm, const float* bmean, float* bpart, uint16_t* dxa, uint16_t* dw, float* ws,
                           int M, int C4, int CW, hipStream_t s) {
   if (!pdt_conv1x1_bwd_fused_ok(C4, CW) || M < 1 || (int64_t)M * C4 >= ((int64_t)1 << 31)) return -1;
   if ((bx != nullptr) != (bpart != nullptr) || (bx && !bmean)) return -1;
-  FBArgs a{dy, z, mz, mean, A, B, D, wt, xa, BnSrc{bx, bm, bmean, bpart}, dxa, ws, M, (M + 31) / 32};
-  if (bx) return launch<FB<256, 64, true>>(a, dw, s);
-  return launch<FB<256, 64, false>>(a, dw, s);
+  const int kp = kp_of(C4), ntiles = (M + kp - 1) / kp;
+  FBArgs a{dy, z, mz, mean, A, B, D, wt, xa, BnSrc{bx, bm, bmean, bpart}, dxa, ws, M, ntiles,
+           pdt_conv1x1_bwd_fused_grid(M, C4, CW)};
+  if (C4 == 256) {
+    if (bx) return launch<FB<256, 64, true>>(a, dw, s);
+    return launch<FB<256, 64, false>>(a, dw, s);
+  }
+  if (bx) return launch<FB<512, 128, true>>(a, dw, s);
+  return launch<FB<512, 128, false>>(a, dw, s);
 }
 
-// Tuning hook: workgroups per call (0 = one per CU).
+// Tuning hook: total workgroups per call (0 = one per CU).
 void pdt_conv1x1_bwd_fused_tune(int grid) {
   if (grid >= 0) g_grid = grid;
 }

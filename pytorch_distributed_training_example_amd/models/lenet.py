@@ -9,15 +9,16 @@ so ``mnist_cnn.pt`` files are interchangeable with the reference's.
 ``nll_loss``, cnn.py:23 + train.py:48); ``output='logits'`` drops the final Softmax so a
 proper cross-entropy can be used (the default training path here).
 
-On MI355X the conv stack runs through the fused LeNet kernels (ops/lenet.py,
-csrc/kernels/lenet.hip): upsample+conv1+LeakyReLU+pool in one kernel, conv2 on MIOpen
-followed by a fused LeakyReLU+pool, conv3 on MIOpen. ``fused=False`` keeps the plain
-``nn.Sequential`` path (same parameters, same results up to fp32 rounding).
+On MI355X the whole network runs on our LeNet kernels (ops/lenet.py): upsample + conv1 + LeakyReLU
++ pool in one kernel (csrc/kernels/lenet.hip), then conv2 + LeakyReLU + pool + conv3 + LeakyReLU +
+fc1 + LeakyReLU + fc2 in ONE more kernel (csrc/kernels/lenet_tail.hip); backward is the tail's two
+kernels + the stem's weight-gradient kernel — no MIOpen, no hipBLASLt, no aten elementwise ops.
+``fused=False`` keeps the plain ``nn.Sequential`` path (same parameters, same results up to fp32
+rounding).
 """
 from __future__ import annotations
 
 import torch
-import torch.nn.functional as F
 from torch import nn
 
 from ..ops._native import disabled as _native_disabled
@@ -43,23 +44,33 @@ class LeNet(nn.Module):
         )
         self.FC = nn.Sequential(nn.Linear(120, 84), nn.LeakyReLU(0.2), nn.Linear(84, 10))
 
-    def _features_fused(self, img: torch.Tensor) -> torch.Tensor:
-        from ..ops.lenet import leaky_pool, lenet_stem
+    def _tail_params(self):
+        c, f = self.ConvNet, self.FC
+        return (c[4].weight, c[4].bias, c[7].weight, c[7].bias, f[0].weight, f[0].bias, f[2].weight, f[2].bias)
+
+    def _logits_fused(self, img: torch.Tensor) -> torch.Tensor:
+        from ..ops.lenet import lenet_stem, lenet_tail
         c = self.ConvNet
         y = lenet_stem(img, c[1].weight, c[1].bias, c[2].negative_slope)
-        y = leaky_pool(F.conv2d(y, c[4].weight, c[4].bias), c[5].negative_slope)
-        return F.leaky_relu(F.conv2d(y, c[7].weight, c[7].bias), c[8].negative_slope)
+        return lenet_tail(y, self._tail_params(), c[5].negative_slope)
 
     def _can_fuse(self, img: torch.Tensor) -> bool:
         if not (self.fused and img.is_cuda) or _native_disabled():
             return False
+        from torch.nn.modules import module as _m
+        if _m._global_forward_hooks or _m._global_forward_pre_hooks or any(
+                m._forward_hooks or m._forward_pre_hooks for m in self.modules() if m is not self):
+            return False  # submodule hooks must see their modules run
+        slopes = {self.ConvNet[i].negative_slope for i in (2, 5, 8)} | {self.FC[1].negative_slope}
         from ..ops.lenet import stem_native_ok
-        return stem_native_ok(img, self.ConvNet[1].weight)
+        return len(slopes) == 1 and stem_native_ok(img, self.ConvNet[1].weight)
 
     def forward(self, img: torch.Tensor) -> torch.Tensor:
-        out = self._features_fused(img) if self._can_fuse(img) else self.ConvNet(img)
-        out = out.reshape(out.shape[0], -1)
-        logits = self.FC(out)
+        if self._can_fuse(img):
+            logits = self._logits_fused(img)
+        else:
+            out = self.ConvNet(img)
+            logits = self.FC(out.reshape(out.shape[0], -1))
         if self.output == "probs":
             return torch.softmax(logits, dim=-1)
         if self.output == "log_probs":

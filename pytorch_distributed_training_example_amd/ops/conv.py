@@ -355,8 +355,8 @@ def _bwd_fused(ctx, d, x, weight):
 
 
 def fused_bwd_shape_ok(weight: torch.Tensor) -> bool:
-    """(Co, Ci) of a 1x1 conv whose backward conv1x1_bwd_fused takes (ResNet-50 layer-1 conv3)."""
-    return weight.dim() == 4 and tuple(weight.shape[:2]) == (256, 64) and weight.dtype == torch.bfloat16
+    """(Co, Ci) of a 1x1 conv whose backward conv1x1_bwd_fused takes (ResNet-50 layer-1 / layer-2 conv3)."""
+    return weight.dim() == 4 and tuple(weight.shape[:2]) in ((256, 64), (512, 128)) and weight.dtype == torch.bfloat16
 
 
 def _subsample_native(t: torch.Tensor) -> bool:

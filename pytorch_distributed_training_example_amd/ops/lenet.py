@@ -4,6 +4,9 @@
                         (/root/reference/cnn.py:9-12) in one kernel; backward gives conv1's dW/db only
                         (the input is data, it needs no gradient).
   * ``leaky_pool``      LeakyReLU + 2×2 max-pool with a 1-byte argmax/sign code (cnn.py:14-15).
+  * ``lenet_tail``      everything after the stem — conv2 + LeakyReLU + pool, conv3 + LeakyReLU, fc1 +
+                        LeakyReLU, fc2 (cnn.py:13-22) — as one forward kernel and two backward kernels
+                        (csrc/kernels/lenet_tail.hip); returns the logits.
   * ``softmax_nll``     fused softmax loss for small class counts: ``mode='ce'`` cross-entropy, or
                         ``mode='prob_nll'`` — the reference's ``nll_loss`` on softmax probabilities
                         (cnn.py:23 + train.py:48, loss = −mean p_y) computed from logits. Forward
@@ -67,6 +70,45 @@ class _LeakyPoolFn(torch.autograd.Function):
     def backward(ctx, dy):
         (code,) = ctx.saved_tensors
         return native().leaky_pool_bwd(dy, code, ctx.shape[2], ctx.shape[3], ctx.slope), None
+
+
+class _TailFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, p1, slope, *params):
+        logits, code2, p2, h3, h4 = native().lenet_tail_fwd(p1, list(params), slope)
+        ctx.save_for_backward(p1, code2, p2, h3, h4, *params)
+        ctx.slope = slope
+        return logits
+
+    @staticmethod
+    def backward(ctx, dl):
+        p1, code2, p2, h3, h4, *params = ctx.saved_tensors
+        dp1, *g = native().lenet_tail_bwd(dl, p1, list(params), ctx.slope, code2, p2, h3, h4)
+        return (dp1, None, *g)
+
+
+def tail_reference(p1, params, slope=SLOPE):
+    w2, b2, w3, b3, fw1, fb1, fw2, fb2 = params
+    y = F.max_pool2d(F.leaky_relu(F.conv2d(p1, w2, b2), slope), 2)
+    y = F.leaky_relu(F.conv2d(y, w3, b3), slope).reshape(p1.shape[0], -1)
+    return F.linear(F.leaky_relu(F.linear(y, fw1, fb1), slope), fw2, fb2)
+
+
+_TAIL_SHAPES = ((16, 6, 5, 5), (16,), (120, 16, 5, 5), (120,), (84, 120), (84,), (10, 84), (10,))
+
+
+def tail_native_ok(p1, params) -> bool:
+    return (p1.dim() == 4 and tuple(p1.shape[1:]) == (6, 14, 14) and p1.dtype == torch.float32
+            and len(params) == 8 and all(tuple(p.shape) == s and p.dtype == torch.float32
+                                         for p, s in zip(params, _TAIL_SHAPES)))
+
+
+def lenet_tail(p1, params, slope=SLOPE):
+    """Logits of the reference LeNet from the stem's pooled output p1 [N,6,14,14]; ``params`` = (conv2
+    weight, bias, conv3 weight, bias, fc1 weight, bias, fc2 weight, bias)."""
+    if use_native(p1) and tail_native_ok(p1, params):
+        return _TailFn.apply(p1.contiguous(), float(slope), *[p.contiguous() for p in params])
+    return tail_reference(p1, params, slope)
 
 
 _MODES = {"ce": 0, "prob_nll": 1}

@@ -191,6 +191,10 @@ class DistributedDataParallel(nn.Module):
         self._callback_queued = False
         self._next_bucket = 0
         self._num_iterations = 0
+        # exposed-communication timing (enable_comm_timing): per backward, events on the compute
+        # stream at the start of _finalize_backward and after the last bucket's wait
+        self._comm_timing = False
+        self._comm_events: List[tuple] = []
 
         ignore = getattr(module, "_ddp_params_and_buffers_to_ignore", set())
         seen = set()
@@ -339,6 +343,10 @@ class DistributedDataParallel(nn.Module):
                                       group=self.process_group, async_op=True)
 
     def _finalize_backward(self) -> None:
+        timing = self._comm_timing and torch.cuda.is_available() and not torch.cuda.is_current_stream_capturing()
+        if timing:  # backward's compute is all queued: from here the compute stream waits on comm
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record()
         # Parameters that did not take part in this backward (unused / frozen branch)
         # contribute zeros so every rank launches the same collectives in the same order.
         for bucket in self._buckets:
@@ -369,6 +377,10 @@ class DistributedDataParallel(nn.Module):
                     elif p.grad.data_ptr() != v.data_ptr():
                         p.grad.copy_(v)
             bucket.reset()
+        if timing:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            self._comm_events.append((e0, e1))
         self._next_bucket = 0
         self._callback_queued = False
         self._num_iterations += 1
@@ -405,6 +417,29 @@ class DistributedDataParallel(nn.Module):
             yield
         finally:
             self.require_backward_grad_sync = old
+
+    def enable_comm_timing(self, on: bool = True) -> None:
+        """Time the EXPOSED communication of each backward: GPU time between the end of backward's
+        compute (the start of the finalize callback, where the last buckets launch) and the moment
+        the compute stream may proceed past every bucket's all-reduce (the waits + unpack copies).
+        Communication hidden under backward does not count; a reducer with no overlap shows its
+        whole all-reduce time here. Events only, no host sync until ``comm_exposed_ms``."""
+        self._comm_timing = bool(on)
+        self._comm_events = []
+
+    def comm_exposed_ms(self, reset: bool = True) -> Optional[float]:
+        """Mean exposed-communication ms per timed backward (synchronises); None if none timed."""
+        ev = self._comm_events
+        if reset:
+            self._comm_events = []
+        if not ev:
+            return None
+        torch.cuda.synchronize()
+        return sum(a.elapsed_time(b) for a, b in ev) / len(ev)
+
+    def bucket_bytes(self) -> List[int]:
+        """Bytes of each gradient bucket, in launch order."""
+        return [b.comm_buffer.numel() * b.comm_buffer.element_size() for b in self._buckets]
 
     def register_comm_hook(self, state: Any, hook: Callable) -> None:
         if self._comm_hook is not None:

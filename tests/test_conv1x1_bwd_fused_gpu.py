@@ -30,10 +30,10 @@ def _nhwc(t2d, N, H, W):
 
 @pytest.mark.parametrize("N,H,W", [(2, 56, 56), (3, 7, 7), (1, 5, 13), (16, 14, 14)])
 @pytest.mark.parametrize("bstats", [True, False])
-def test_fused_matches_fp32(N, H, W, bstats):
-    C4, CW = 256, 64
+@pytest.mark.parametrize("C4,CW", [(256, 64), (512, 128)])
+def test_fused_matches_fp32(N, H, W, bstats, C4, CW):
     M = N * H * W
-    g = torch.Generator(device="cuda").manual_seed(M + bstats)
+    g = torch.Generator(device="cuda").manual_seed(M + bstats + C4)
     r = lambda *s: torch.randn(*s, device="cuda", generator=g)  # noqa: E731
     dy = r(M, C4).bfloat16()
     z = (r(M, C4) + 0.3).bfloat16()
@@ -70,8 +70,9 @@ def test_fused_matches_fp32(N, H, W, bstats):
         assert part is None
 
 
-def test_fused_is_deterministic():
-    N, H, W, C4, CW = 4, 28, 28, 256, 64
+@pytest.mark.parametrize("C4,CW", [(256, 64), (512, 128)])
+def test_fused_is_deterministic(C4, CW):
+    N, H, W = 4, 28, 28
     M = N * H * W
     torch.manual_seed(0)
     dy = torch.randn(M, C4, device="cuda").bfloat16()
@@ -157,7 +158,7 @@ def test_resnet50_grads_fused_vs_unfused(switch):
         ga = _grads()
     finally:
         conv_ops._bwd_fused = orig
-    assert calls == [True] * 3, calls  # the three layer-1 blocks, all on the fused kernel
+    assert calls == [True] * 7, calls  # the three layer-1 and four layer-2 blocks, all on the fused kernel
     switch("PDT_BWD_FUSED", "0")
     gb = _grads()
     assert ga.keys() == gb.keys()

@@ -83,3 +83,52 @@ def test_lenet_fused_matches_module_path():
     torch.nn.functional.cross_entropy(outr, t).backward()
     for (n, p), pr in zip(m.named_parameters(), ref.parameters()):
         torch.testing.assert_close(p.grad, pr.grad, rtol=2e-3, atol=2e-4, msg=n)
+
+
+def _tail_params(g):
+    from pytorch_distributed_training_example_amd.ops.lenet import _TAIL_SHAPES
+    ps = []
+    for s in _TAIL_SHAPES:
+        fan = 1
+        for d in s[1:]:
+            fan *= d
+        ps.append((torch.randn(*s, device="cuda", generator=g) / max(fan, 1) ** 0.5).requires_grad_())
+    return ps
+
+
+@pytest.mark.parametrize("n", [1, 5, 128])
+def test_tail_fwd_bwd_matches_fp32(n):
+    """conv2 + pool + conv3 + fc1 + fc2 (csrc/kernels/lenet_tail.hip) against the aten ops in fp32:
+    logits, every parameter gradient and the gradient of the stem output."""
+    from pytorch_distributed_training_example_amd.ops.lenet import lenet_tail, tail_reference
+    g = torch.Generator(device="cuda").manual_seed(100 + n)
+    p1 = torch.randn(n, 6, 14, 14, device="cuda", generator=g).requires_grad_()
+    ps = _tail_params(g)
+    p1r = p1.detach().clone().requires_grad_()
+    psr = [p.detach().clone().requires_grad_() for p in ps]
+    y, yr = lenet_tail(p1, ps), tail_reference(p1r, psr)
+    _close(y, yr, 1e-4)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    yr.backward(dy)
+    _close(p1.grad, p1r.grad, 1e-4)
+    for a, b in zip(ps, psr):
+        _close(a.grad, b.grad, 2e-4 * max(1, n) ** 0.5)
+
+
+def test_lenet_model_fused_matches_modules():
+    """The whole reference model on our kernels (stem + tail) vs the plain nn.Sequential path."""
+    import copy
+    from pytorch_distributed_training_example_amd.models.lenet import LeNet
+    torch.manual_seed(0)
+    m = LeNet(output="probs").cuda()
+    mr = copy.deepcopy(m)
+    mr.fused = False
+    x = torch.randn(64, 1, 28, 28, device="cuda")
+    t = torch.randint(0, 10, (64,), device="cuda")
+    y, yr = m(x), mr(x)
+    _close(y, yr, 1e-5)
+    torch.nn.functional.nll_loss(y, t).backward()
+    torch.nn.functional.nll_loss(yr, t).backward()
+    for (na, a), (_, b) in zip(m.named_parameters(), mr.named_parameters()):
+        torch.testing.assert_close(a.grad, b.grad, rtol=1e-3, atol=1e-5, msg=na)
