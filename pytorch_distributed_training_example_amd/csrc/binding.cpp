@@ -51,8 +51,8 @@ int pdt_conv1x1_bwd_fused_ok(int C4, int CW);
 int pdt_conv1x1_bwd_fused_grid(int M, int C4, int CW);
 int pdt_conv1x1_bwd_fused(const uint16_t* dy, const uint16_t* z, const uint8_t* mz, const float* mean, const float* A,
                           const float* B, const float* D, const uint16_t* wt, const uint16_t* xa, const uint16_t* bx,
-                          const uint8_t* bm, const float* bmean, float* bpart, uint16_t* dxa, uint16_t* dw, float* ws,
-                          int M, int C4, int CW, hipStream_t s);
+                          const uint8_t* bm, const float* bmean, float* bpart, const float* xcoef, uint8_t* mask_out,
+                          uint16_t* dxa, uint16_t* dw, float* ws, int M, int C4, int CW, hipStream_t s);
 void pdt_conv1x1_bwd_fused_tune(int grid);
 void pdt_bn_tune(int variant, int target_blocks, int u_fwd, int u_bwd);
 int pdt_bn_fwd_train(const uint16_t* x, const uint16_t* res, const float* res_a, const float* res_b,
@@ -130,7 +130,8 @@ int pdt_conv1x1_wgrad(const uint16_t* x, const uint16_t* dy, uint16_t* dw, float
 void pdt_conv1x1_wgrad_tune(int target_wgs, int variant, int interleave);
 int pdt_conv1x1_gemm(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t* c, const uint8_t* cm,
                      float* part, int M, int K, int N, const uint16_t* bn_x, const uint8_t* bn_mask,
-                     const float* bn_mean, float* bn_part, int c_s, int c_H, int c_W, hipStream_t s);
+                     const float* bn_mean, float* bn_part, int c_s, int c_H, int c_W, const float* acoef,
+                     hipStream_t s);
 int pdt_maxpool_bn_parts(int N, int H);
 int pdt_maxpool3s2_bwd_bn(const uint16_t* dy, const uint8_t* code, uint16_t* dz, int N, int H, int W, int C,
                           const uint16_t* x, const float* gamma, const float* mean, const float* invstd, uint16_t* dx,
@@ -671,12 +672,17 @@ std::vector<Tensor> bn_bwd_coef(Tensor dy, Tensor x, c10::optional<Tensor> part,
 // returns {dxa, dw, part}: the conv's data and weight gradients and, when bn_x / bn_mean are given
 // (xa is the output of a BatchNorm with input bn_x, ReLU bits bn_mask, batch mean bn_mean), that
 // BatchNorm's backward partials [2, G, CW] (else undefined). Empty list: shape not taken.
+// xcoef [2, CW] (with bn_x / bn_mean): that BatchNorm's apply was deferred to the conv's forward — xa
+// (only its shape is used) is recomputed as relu(xcoef[0] bn_x + xcoef[1]), and its ReLU bits are
+// computed and written into bn_mask (an output then, M*CW/8 bytes).
 std::vector<Tensor> conv1x1_bwd_fused(Tensor dy, Tensor z, Tensor mz, Tensor mean, Tensor coef, Tensor w, Tensor xa,
                                       c10::optional<Tensor> bn_x, c10::optional<Tensor> bn_mask,
-                                      c10::optional<Tensor> bn_mean) {
+                                      c10::optional<Tensor> bn_mean, c10::optional<Tensor> xcoef) {
   check_nhwc_bf16(dy, "dy");
   check_nhwc_bf16(z, "z");
-  check_nhwc_bf16(xa, "xa");
+  TORCH_CHECK(xa.dim() == 4 && xa.is_cuda() && xa.scalar_type() == at::kBFloat16, "conv1x1_bwd_fused: xa");
+  const bool recomp = xcoef.has_value() && xcoef->defined();
+  if (!recomp) check_nhwc_bf16(xa, "xa");
   const int64_t C4 = z.size(1), CW = xa.size(1);
   const int64_t M = z.numel() / C4;
   if (!pdt_conv1x1_bwd_fused_ok((int)C4, (int)CW) || M * C4 >= ((int64_t)1 << 31)) return {};
@@ -688,7 +694,7 @@ std::vector<Tensor> conv1x1_bwd_fused(Tensor dy, Tensor z, Tensor mz, Tensor mea
   TORCH_CHECK(w.scalar_type() == at::kBFloat16 && w.numel() == C4 * CW && w.size(0) == C4,
               "conv1x1_bwd_fused: weight [C4, CW, 1, 1] bf16");
   auto wt = w.reshape({C4, CW}).t().contiguous();
-  auto dxa = at::empty_like(xa);
+  auto dxa = at::empty({xa.size(0), CW, xa.size(2), xa.size(3)}, xa.options().memory_format(at::MemoryFormat::ChannelsLast));
   auto dw = at::empty({C4, CW}, w.options());
   const int G = pdt_conv1x1_bwd_fused_grid((int)M, (int)C4, (int)CW);
   auto fopt = z.options().dtype(at::kFloat);
@@ -710,13 +716,24 @@ std::vector<Tensor> conv1x1_bwd_fused(Tensor dy, Tensor z, Tensor mz, Tensor mea
     bmu = bn_mean->data_ptr<float>();
     part = at::empty({2, G, CW}, fopt);
   }
+  const float* xcp = nullptr;
+  uint8_t* mout = nullptr;
+  if (recomp) {
+    TORCH_CHECK(bst && bm, "conv1x1_bwd_fused: xcoef needs bn_x, bn_mean and the bn_mask output");
+    TORCH_CHECK(xcoef->scalar_type() == at::kFloat && xcoef->is_contiguous() && xcoef->numel() == 2 * CW,
+                "conv1x1_bwd_fused: xcoef [2, CW] fp32");
+    xcp = xcoef->data_ptr<float>();
+    mout = bn_mask->data_ptr<uint8_t>();
+    bm = nullptr;
+  }
   const float* cp = coef.data_ptr<float>();
   const int rc = pdt_conv1x1_bwd_fused(reinterpret_cast<const uint16_t*>(dy.data_ptr()),
                                        reinterpret_cast<const uint16_t*>(z.data_ptr()), mz.data_ptr<uint8_t>(),
                                        mean.data_ptr<float>(), cp, cp + C4, cp + 2 * C4,
                                        reinterpret_cast<const uint16_t*>(wt.data_ptr()),
-                                       reinterpret_cast<const uint16_t*>(xa.data_ptr()), bx, bm, bmu,
-                                       bst ? part.data_ptr<float>() : nullptr, reinterpret_cast<uint16_t*>(dxa.data_ptr()),
+                                       recomp ? nullptr : reinterpret_cast<const uint16_t*>(xa.data_ptr()), bx, bm, bmu,
+                                       bst ? part.data_ptr<float>() : nullptr, xcp, mout,
+                                       reinterpret_cast<uint16_t*>(dxa.data_ptr()),
                                        reinterpret_cast<uint16_t*>(dw.data_ptr()), ws.data_ptr<float>(), (int)M, (int)C4,
                                        (int)CW, stream());
   TORCH_CHECK(rc == 0, "pdt_conv1x1_bwd_fused failed: ", rc);
@@ -789,10 +806,13 @@ std::vector<Tensor> lenet_tail_bwd(Tensor dl, Tensor p1, std::vector<Tensor> w, 
 // bn_x / bn_mask / bn_mean: out is the gradient at the output of a BatchNorm with this input
 // (channels_last [M, N] bf16), ReLU bit-mask (or none) and batch mean: return that BatchNorm's
 // backward per-tile partials [2, T, N] fp32 (sum dz, sum dz (x - mean)) instead (not with stats).
+// a_coef [2, K] fp32 (optional): a is the INPUT of a BatchNorm + ReLU whose apply is deferred to here —
+// the GEMM uses relu(a_coef[0] * a + a_coef[1]) per channel (forward only; not with acc / bn_x).
 c10::optional<Tensor> conv1x1_gemm(Tensor a, Tensor b, Tensor out, bool acc, bool stats,
                                    c10::optional<Tensor> c_in, c10::optional<Tensor> c_mask,
                                    c10::optional<Tensor> bn_x, c10::optional<Tensor> bn_mask,
-                                   c10::optional<Tensor> bn_mean, int64_t c_stride, int64_t c_H, int64_t c_W) {
+                                   c10::optional<Tensor> bn_mean, int64_t c_stride, int64_t c_H, int64_t c_W,
+                                   c10::optional<Tensor> a_coef) {
   for (const Tensor* t : {&a, &b, &out}) {
     check_cuda(*t, "conv1x1_gemm operand");
     TORCH_CHECK(t->scalar_type() == at::kBFloat16 && t->dim() == 2 && t->is_contiguous(),
@@ -848,11 +868,18 @@ c10::optional<Tensor> conv1x1_gemm(Tensor a, Tensor b, Tensor out, bool acc, boo
     bmean = bn_mean->data_ptr<float>();
     part = at::empty({2, T, N}, a.options().dtype(at::kFloat));
   }
+  const float* acp = nullptr;
+  if (a_coef.has_value() && a_coef->defined()) {
+    TORCH_CHECK(!acc && !bstats, "conv1x1_gemm: a_coef is forward-only (no acc / bn_x)");
+    TORCH_CHECK(a_coef->scalar_type() == at::kFloat && a_coef->is_contiguous() && a_coef->numel() == 2 * K &&
+                a_coef->is_cuda(), "conv1x1_gemm: a_coef must be fp32 [2, K]");
+    acp = a_coef->data_ptr<float>();
+  }
   const int rc = pdt_conv1x1_gemm(reinterpret_cast<const uint16_t*>(a.data_ptr()),
                                   reinterpret_cast<const uint16_t*>(b.data_ptr()),
                                   reinterpret_cast<uint16_t*>(out.data_ptr()), cp, mp,
                                   stats ? part->data_ptr<float>() : nullptr, (int)M, (int)K, (int)N, bx, bm, bmean,
-                                  bstats ? part->data_ptr<float>() : nullptr, (int)c_stride, (int)c_H, (int)c_W,
+                                  bstats ? part->data_ptr<float>() : nullptr, (int)c_stride, (int)c_H, (int)c_W, acp,
                                   stream());
   TORCH_CHECK(rc == 0, "pdt_conv1x1_gemm failed: ", rc);
   return part;
@@ -1701,7 +1728,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv1x1_gemm", &conv1x1_gemm, py::arg("a"), py::arg("b"), py::arg("out"), py::arg("acc"), py::arg("stats"),
         py::arg("c_in") = py::none(), py::arg("c_mask") = py::none(), py::arg("bn_x") = py::none(),
         py::arg("bn_mask") = py::none(), py::arg("bn_mean") = py::none(), py::arg("c_stride") = 0,
-        py::arg("c_H") = 0, py::arg("c_W") = 0);
+        py::arg("c_H") = 0, py::arg("c_W") = 0, py::arg("a_coef") = py::none());
   m.def("bn_bwd_train_tiles", &bn_bwd_train_tiles);
   m.def("maxpool3s2_bwd_bn", &maxpool3s2_bwd_bn);
   m.def("maxpool3s2_bwd_bn_coef", &maxpool3s2_bwd_bn_coef);
@@ -1733,7 +1760,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv3x3_wgrad_tune", [](int target_wgs, int co_tile) { pdt_conv3x3_wgrad_tune(target_wgs, co_tile); });
   m.def("bn_bwd_train", &bn_bwd_train);
   m.def("bn_bwd_coef", &bn_bwd_coef);
-  m.def("conv1x1_bwd_fused", &conv1x1_bwd_fused);
+  m.def("conv1x1_bwd_fused", &conv1x1_bwd_fused, py::arg("dy"), py::arg("z"), py::arg("mz"), py::arg("mean"),
+        py::arg("coef"), py::arg("w"), py::arg("xa"), py::arg("bn_x") = py::none(), py::arg("bn_mask") = py::none(),
+        py::arg("bn_mean") = py::none(), py::arg("xcoef") = py::none());
   m.def("conv1x1_bwd_fused_tune", [](int grid) { pdt_conv1x1_bwd_fused_tune(grid); });
   m.def("ce_fwd", &ce_fwd);
   m.def("ce_bwd", &ce_bwd);

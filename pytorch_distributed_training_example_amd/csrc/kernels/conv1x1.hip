@@ -28,6 +28,11 @@
 //     (rounded) values, and the tile leaves as whole 16-B row pieces (C added there, fp32);
 //   * block -> tile map XCD-aware (xcd_remap): the N-tiles of one pixel tile share an L2.
 //
+//   ATR (forward only): A is a BatchNorm's INPUT whose apply was deferred to here: every A element is
+//                 replaced by relu(a[k] x + b[k]) (the coefficients of that BatchNorm + ReLU, fp32, same
+//                 fma and rounding as its apply pass) in registers after the fragment read, so the
+//                 BatchNorm's output is never written or read (ResNet bottleneck bn2 -> conv3).
+//
 //   BSTATS (data grad only): the output Y is the gradient dy at a BatchNorm's output, and that
 //                 BatchNorm's backward reduction is taken here instead of in a separate pass over
 //                 (dy, x): per 256-pixel tile, per channel, sum(dz) and sum(dz * (xb - mean)) with
@@ -99,11 +104,12 @@ struct CGeom {
   int s, H, W, Hs, Ws;
 };
 
-// NT: streaming (non-temporal) output stores
-template <class Cf, bool ACC, bool STATS, bool NT, bool BSTATS>
+// NT: streaming (non-temporal) output stores. ATR: acoef = [2][K] fp32 (a, then b), see the header.
+template <class Cf, bool ACC, bool STATS, bool NT, bool BSTATS, bool ATR = false>
 __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv1x1_kernel(
     const uint16_t* __restrict__ A, const uint16_t* __restrict__ B, uint16_t* Y, const uint16_t* Cin,
-    const uint8_t* __restrict__ Cmask, float* __restrict__ part, int M, int K, int N, BnSrc bs, CGeom cg) {
+    const uint8_t* __restrict__ Cmask, float* __restrict__ part, int M, int K, int N, BnSrc bs, CGeom cg,
+    const float* __restrict__ acoef) {
   constexpr int BM = Cf::BM, BN = Cf::BN;
   constexpr int WROWS = BM / Cf::WM, WCOLS = BN / Cf::WN;
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -147,6 +153,15 @@ __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv1x1_kernel(
 #pragma unroll
     for (int j = 0; j < Cf::kNB; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
 
+  // ATR: the [2][K] coefficient table in LDS past the ring / epilogue area (filled before any DMA)
+  float* const ctab = reinterpret_cast<float*>(lds + Cf::kLds);
+  if constexpr (ATR) {
+    for (int i = tid; i < 2 * K; i += Cf::kThreads) ctab[i] = acoef[i];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
+
   issue(0);
   if (S > 1) issue(1);
   const int lrow = lane & 15, lchk = lane >> 4;
@@ -163,6 +178,29 @@ __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv1x1_kernel(
     for (int i = 0; i < Cf::kMB; ++i) a[i] = *reinterpret_cast<const bf16x8*>(As + swz64(wm * WROWS + i * 16 + lrow, lchk));
 #pragma unroll
     for (int j = 0; j < Cf::kNB; ++j) b[j] = *reinterpret_cast<const bf16x8*>(Bs + swz64(wn * WCOLS + j * 16 + lrow, lchk));
+    if constexpr (ATR) {  // relu(a x + b) of the fragment's 8 channels, s * 32 + 8 lchk + 0..7
+      const int k0 = s * Cf::BK + 8 * lchk;
+      float ca[8], cb[8];
+      *reinterpret_cast<float4*>(ca) = *reinterpret_cast<const float4*>(ctab + k0);
+      *reinterpret_cast<float4*>(ca + 4) = *reinterpret_cast<const float4*>(ctab + k0 + 4);
+      *reinterpret_cast<float4*>(cb) = *reinterpret_cast<const float4*>(ctab + K + k0);
+      *reinterpret_cast<float4*>(cb + 4) = *reinterpret_cast<const float4*>(ctab + K + k0 + 4);
+#pragma unroll
+      for (int i = 0; i < Cf::kMB; ++i) {
+        typedef unsigned u4 __attribute__((ext_vector_type(4)));
+        const u4 w = __builtin_bit_cast(u4, a[i]);
+        float v[8];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) { v[2 * k] = __uint_as_float(w[k] << 16); v[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u); }
+        u4 o;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float t0 = v[2 * k] * ca[2 * k] + cb[2 * k], t1 = v[2 * k + 1] * ca[2 * k + 1] + cb[2 * k + 1];
+          o[k] = (uint32_t)f2bf(t0 > 0.f ? t0 : 0.f) | ((uint32_t)f2bf(t1 > 0.f ? t1 : 0.f) << 16);
+        }
+        a[i] = __builtin_bit_cast(bf16x8, o);
+      }
+    }
 #pragma unroll
     for (int i = 0; i < Cf::kMB; ++i)
 #pragma unroll
@@ -283,19 +321,24 @@ __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv1x1_kernel(
     bn_bwd_tile_store<BN, Cf::kWaves>(bs1, bs2, reinterpret_cast<float*>(lds), bs.part, (M + BM - 1) / BM, mt, N, n0);
 }
 
-template <class Cf, bool ACC, bool STATS, bool NT, bool BSTATS>
+constexpr int kMaxATRK = 512;  // ATR coefficient table: [2][K] floats past kLds
+
+template <class Cf, bool ACC, bool STATS, bool NT, bool BSTATS, bool ATR = false>
 int launch_nt(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t* c, const uint8_t* cm, float* part,
-              int M, int K, int N, const BnSrc& bs, const CGeom& cg, hipStream_t s) {
+              int M, int K, int N, const BnSrc& bs, const CGeom& cg, hipStream_t s, const float* acoef = nullptr) {
   static bool attr = false;
+  constexpr int kMaxLds = Cf::kLds + (ATR ? 2 * kMaxATRK * 4 : 0);
   if (!attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&conv1x1_kernel<Cf, ACC, STATS, NT, BSTATS>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, Cf::kLds) != hipSuccess)
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&conv1x1_kernel<Cf, ACC, STATS, NT, BSTATS, ATR>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, kMaxLds) != hipSuccess)
       return -3;
     attr = true;
   }
+  if (ATR && K > kMaxATRK) return -1;
+  const int lds = Cf::kLds + (ATR ? 2 * K * 4 : 0);
   const int64_t grid = (int64_t)(M + Cf::BM - 1) / Cf::BM * (N / Cf::BN);
-  hipLaunchKernelGGL((conv1x1_kernel<Cf, ACC, STATS, NT, BSTATS>), dim3((unsigned)grid), dim3(Cf::kThreads), Cf::kLds,
-                     s, a, b, y, c, cm, part, M, K, N, bs, cg);
+  hipLaunchKernelGGL((conv1x1_kernel<Cf, ACC, STATS, NT, BSTATS, ATR>), dim3((unsigned)grid), dim3(Cf::kThreads), lds,
+                     s, a, b, y, c, cm, part, M, K, N, bs, cg, acoef);
   return 0;
 }
 
@@ -312,8 +355,13 @@ using GNarrow = G1<64, 4, 1>;  // N == 64 (or odd multiples of 64): 4 waves of 6
 
 template <class Cf>
 int dispatch(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t* c, const uint8_t* cm, float* part,
-             int M, int K, int N, const BnSrc& bs, const CGeom& cg, hipStream_t s) {
+             int M, int K, int N, const BnSrc& bs, const CGeom& cg, hipStream_t s, const float* acoef = nullptr) {
   if ((c && part) || (cm && !c) || (part && bs.part) || (cg.s && (!c || cm))) return -1;  // not instantiated
+  if (acoef) {  // forward with the producing BatchNorm's apply deferred here (+ statistics epilogue)
+    if (c || bs.part) return -1;
+    if (part) return launch_nt<Cf, false, true, false, false, true>(a, b, y, c, cm, part, M, K, N, bs, cg, s, acoef);
+    return launch_nt<Cf, false, false, false, false, true>(a, b, y, c, cm, part, M, K, N, bs, cg, s, acoef);
+  }
   if (bs.part) {
     if (!bs.x || !bs.mean) return -1;
     if (c) return launch<Cf, true, false, true>(a, b, y, c, cm, part, M, K, N, bs, cg, s);
@@ -338,9 +386,11 @@ int pdt_conv1x1_tile_rows() { return 256; }
 // [2][T][N] receives that BatchNorm's backward per-tile sums (see the header). Not with part.
 // c_s, c_H, c_W (c_s > 0): c is the compact gradient of the stride-c_s subsampling of y's pixels
 // (y rows = [n][c_H][c_W]), see CGeom; needs c, no cm.
+// acoef ([2][K] fp32, or null): A is a BatchNorm input, relu(acoef[0][k] x + acoef[1][k]) is used (ATR).
 int pdt_conv1x1_gemm(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t* c, const uint8_t* cm,
                      float* part, int M, int K, int N, const uint16_t* bn_x, const uint8_t* bn_mask,
-                     const float* bn_mean, float* bn_part, int c_s, int c_H, int c_W, hipStream_t s) {
+                     const float* bn_mean, float* bn_part, int c_s, int c_H, int c_W, const float* acoef,
+                     hipStream_t s) {
   if (M < 1 || K < 32 || K % 32 != 0 || N < 64 || N % 64 != 0) return -1;
   if ((int64_t)M * (K > N ? K : N) >= ((int64_t)1 << 31) || (int64_t)N * K >= ((int64_t)1 << 31)) return -2;
   const BnSrc bs{bn_x, bn_mask, bn_mean, bn_part};
@@ -349,8 +399,8 @@ int pdt_conv1x1_gemm(const uint16_t* a, const uint16_t* b, uint16_t* y, const ui
     if (c_H < 1 || c_W < 1 || M % (c_H * c_W) != 0) return -1;
     cg = CGeom{c_s, c_H, c_W, (c_H - 1) / c_s + 1, (c_W - 1) / c_s + 1};
   }
-  if (N % 128 == 0) return dispatch<GWide>(a, b, y, c, cm, part, M, K, N, bs, cg, s);
-  return dispatch<GNarrow>(a, b, y, c, cm, part, M, K, N, bs, cg, s);
+  if (N % 128 == 0) return dispatch<GWide>(a, b, y, c, cm, part, M, K, N, bs, cg, s, acoef);
+  return dispatch<GNarrow>(a, b, y, c, cm, part, M, K, N, bs, cg, s, acoef);
 }
 
 }  // extern "C"

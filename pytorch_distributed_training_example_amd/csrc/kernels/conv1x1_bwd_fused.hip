@@ -13,21 +13,33 @@
 // (read dz, write dxa; its epilogue re-reads xb for the bn2 reduction) and the wgrad GEMM (read dz and
 // xa) — 22 "T" of traffic per layer-1 block (T = one 64-channel activation) against 10.3 T here.
 //
-// Structure (one persistent workgroup per CU, 4 waves, memory bound by design):
-//   * a stage = KP = 32 pixels. dy, z (512-B rows), the bn3 mask bits, xa and xb (128-B rows,
-//     XOR-swizzled by permuting each lane's DMA source chunk) and the bn2 mask bits are staged by
-//     LDS-DMA (global_load_lds, 16 / 4 / 1 bytes per lane) through a 3-slot ring, two stages in
-//     flight, counted vmcnt, raw s_barrier (cdna_hip_programming.md §5 "Pipelining across barriers");
+// Structure (one persistent workgroup per CU, memory bound by design):
+//   * a stage = KP pixels (32 at C4 = 256, 16 at C4 = 512). dy, z (C4-channel rows), the bn3 mask bits,
+//     xa and xb (one 128-B row per 64-channel slice, XOR-swizzled by permuting each lane's DMA source
+//     chunk) and the bn2 mask bits are staged by LDS-DMA (global_load_lds, 16 / 4 bytes per lane)
+//     through a 3-slot ring, two stages in flight, counted vmcnt, raw s_barrier
+//     (cdna_hip_programming.md §5 "Pipelining across barriers");
 //   * a transform pass turns (dy, z, mask) into dz in a separate LDS tile whose rows are swizzled
 //     with chunk ^ (((r & 3) << 2) | ((r >> 2) & 2)): conflict-free for BOTH readers, the dgrad's
 //     ds_read_b128 (16 pixel rows, one 16-B chunk) and the wgrad's ds_read_b64_tr_b16 (4 rows x 64 B);
+//   * a workgroup covers one 64-channel slice of CW ("role"; NR = CW / 64 roles per pixel group, placed
+//     on one XCD: blocks b, b + 8, ... — the second role's reads of dy / z can hit L2; speed only).
+//     At CW = 128 (layer 2) that pairing measured 904 us against a 434 us floor — the pairs drift
+//     apart and both read HBM — but one workgroup for both slices does not fit: W^T (128 KB) and the
+//     wgrad accumulators (256 KB) need 384 registers per lane at 4 waves, 8 waves spill at two per
+//     SIMD, and neither fits LDS beside the ring. NG (slices per workgroup) stays 1;
 //   * dgrad: v_mfma_f32_16x16x32_bf16 with W^T as the A operand held in VGPRs for the whole kernel
-//     (a wave owns 16 output channels x all C4 inputs = 32 VGPRs), dz as B;
-//   * wgrad: v_mfma_f32_32x32x16_bf16, dz^T and xa through transposed reads, a wave owns a 64 x CW
-//     block of dW in AGPR/VGPR accumulators for the whole kernel; fp32 partials per workgroup summed
-//     afterwards in a fixed order (deterministic);
+//     (a wave owns 16 output channels x all C4 inputs), dz as B;
+//   * wgrad: v_mfma_f32_32x32x16_bf16, dz^T and xa through transposed reads, a wave owns a C4/4 x 64
+//     block of dW in accumulators for the whole kernel; fp32 partials per workgroup summed afterwards
+//     in a fixed order (deterministic);
 //   * the dgrad tile leaves through an LDS staging tile as 16-B rows; the bn2 reduction is taken from
 //     the rounded bf16 values, exactly as conv1x1.hip's BSTATS epilogue does.
+//   * RECOMP: bn2's apply was deferred in the forward (conv3 read relu(a2 xb + b2) on load, conv1x1.hip
+//     ATR), so xa = relu(a2 xb + b2) is formed here from xb — in registers, on the wgrad's B fragments
+//     (one channel per lane: two coefficients) — with the same fma and rounding as the forward, and
+//     bn2's ReLU mask is computed from xb and WRITTEN here (bn2's backward apply reads it next): xa and
+//     the mask bits are never read.
 #include "../common.h"
 #include "../tile_stats.h"
 
@@ -42,51 +54,61 @@ typedef short s4v __attribute__((ext_vector_type(4)));
 #define PDT_LDS __attribute__((address_space(3)))
 
 __device__ __attribute__((aligned(256))) uint4 g_fb_zero[64];  // zero page for pixels past M (never written)
-__device__ uint4 g_fb_sink[256];  // epilogue stores of rows past M land here (keeps the vmcnt count exact)
+__device__ uint4 g_fb_sink[1024];  // epilogue stores of rows past M land here (keeps the vmcnt count exact)
 
-// C4: the BatchNorm's channels (conv output), CW: the conv's input channels. A workgroup owns a
-// 64-channel slice of CW ("role"; CW / 64 roles, each role's workgroup computes the full dz of its
-// pixels — the roles of one pixel group are placed on one XCD, so the second read of dy / z is an
-// L2 hit), the dgrad output of its slice and the wgrad columns of its slice.
-template <int C4_, int CW_, bool BSTATS_>
+// C4: the BatchNorm's channels (conv output), CW: the conv's input channels (NR = CW / 64 roles).
+template <int C4_, int CW_, bool BSTATS_, bool RECOMP_ = false>
 struct FB {
-  static constexpr int C4 = C4_, CW = CW_, NR = CW / 64, kSlots = 3, kWaves = 4, kThreads = 256;
+  static constexpr int C4 = C4_, CW = CW_, NG = 1, NR = CW / 64, kSlots = 3;
+  static constexpr int kWaves = 4, kThreads = 256;
   static constexpr int KP = C4 >= 512 ? 16 : 32;  // pixels per stage (LDS: 3 slots + the dz tile)
-  static constexpr bool BSTATS = BSTATS_;
-  static constexpr int kRowY = C4 * 2, kRowX = 128;  // LDS rows: dy / z / dz; the 64-channel slices
-  static constexpr int kY = KP * kRowY, kMZ = KP * C4 / 8, kXA = KP * kRowX, kMB = KP * 8;
-  // 16-B DMA pieces (1 KB per wave instruction): Y, Z, XA (, XB), padded to a multiple of the waves
+  static constexpr bool BSTATS = BSTATS_ || RECOMP_, RECOMP = RECOMP_;
+  // the transform coefficients: kernel-lifetime VGPRs, or an LDS table when the wgrad accumulators
+  // of all NG slices need the registers
+  static constexpr bool kCoefLds = NG > 1;
+  static constexpr int kRowY = C4 * 2, kRowX = 128;  // LDS rows: dy / z / dz; a 64-channel slice
+  static constexpr int kY = KP * kRowY, kMZ = KP * C4 / 8, kXA = KP * kRowX;
+  static constexpr int kMBRow = 8 * NG;              // bn2 mask bytes per pixel (this role's slices)
+  // 16-B DMA pieces (1 KB per wave instruction): Y, Z, XA (NG slices), XB (NG slices), dummies
   static constexpr int pY = kY / 1024, pX = kXA / 1024;
-  static constexpr int p16 = 2 * pY + pX * (BSTATS ? 2 : 1);
+  static constexpr int nXsrc = RECOMP ? 1 : (BSTATS ? 2 : 1);  // xa and / or xb staged
+  static constexpr int p16 = 2 * pY + pX * NG * nXsrc;
   static constexpr int n16 = (p16 + kWaves - 1) / kWaves;
-  // mask bits: bn3's by 4-B DMA (256 B per instruction), bn2's slice by 1-B DMA (64 B)
-  static constexpr int nMZ = kMZ / 256 / kWaves;
-  static constexpr int pMB = BSTATS ? kMB / 64 : 0;
-  static constexpr int nMB = (pMB + kWaves - 1) / kWaves;
-  static constexpr int oY = 0, oZ = kY, oMZ = 2 * kY, oXA = oMZ + kMZ, oXB = oXA + kXA;
-  static constexpr int oMB = oXB + (BSTATS ? kXA : 0);
-  static constexpr int oPad = oMB + nMB * kWaves * 64;        // dummy pieces land here
-  static constexpr int kSlot = (oPad + (n16 * kWaves > p16 ? 1024 : 0) + 255) / 256 * 256;
+  // 4-B DMA pieces (256 B per wave instruction; a sub-dword LDS-DMA does not land at lane x size —
+  // measured): bn3's mask rows, and bn2's mask bytes (one instruction: <= 64 / (2 NG) rows)
+  static constexpr int pMZ = kMZ / 256;
+  static constexpr int pMB = (BSTATS && !RECOMP) ? 1 : 0;
+  static constexpr int n4 = (pMZ + pMB + kWaves - 1) / kWaves;
+  static constexpr int oY = 0, oZ = kY, oMZ = 2 * kY, oXA = oMZ + kMZ;
+  static constexpr int oXB = RECOMP ? oXA : oXA + NG * kXA;  // RECOMP: only xb is staged (xa formed from it)
+  static constexpr int oMB = oXB + (BSTATS ? NG * kXA : 0);
+  static constexpr int oPad = oMB + (pMB ? 256 : 0);        // dummy pieces land here
+  static constexpr bool kPad = n16 * kWaves > p16 || n4 * kWaves > pMZ + pMB;
+  static constexpr int kSlot = (oPad + (kPad ? 1024 : 0) + 255) / 256 * 256;
   static constexpr int oDZ = kSlots * kSlot;
-  static constexpr int kLds = oDZ + kY;
-  static constexpr int kG = n16 + nMZ + nMB;  // DMA instructions per wave per stage
-  // epilogue: one 16-B chunk of the dgrad slice per thread per stage (threads past the tile store
-  // to a sink: every thread stores once, so the vmcnt counts are exact)
-  static constexpr int kStageOps = kG + 1;
+  static constexpr int oXC = oDZ + kY;                     // RECOMP: bn2's coefficients, [2][CW] fp32
+  static constexpr int oCT = oXC + (RECOMP ? 8 * CW : 0);  // kCoefLds: mean, A, B, D [4][C4] fp32
+  static constexpr int kLds = oCT + (kCoefLds ? 16 * C4 : 0);
+  static constexpr int kG = n16 + n4;  // DMA instructions per wave per stage
+  // epilogue: one 16-B chunk of the dgrad slice per thread per stage (threads past the tile store to
+  // a sink: every thread stores once, so the vmcnt counts are exact) + the bn2 mask byte (RECOMP)
+  static constexpr int kStageOps = kG + 1 + (RECOMP ? 1 : 0);
   static constexpr int kStgStride = kRowX + 16;  // staging rows padded: conflict-free 8-B writes
-  static constexpr int kKS = C4 / 32;   // 16x16x32 k-steps of the dgrad (W^T fragments in VGPRs)
-  static constexpr int kPB = KP / 16;   // pixel blocks of the dgrad tile
-  static constexpr int kWR = C4 / kWaves;  // dW rows per wave
-  static constexpr int kMI = kWR / 32, kNJ = 2;
-  static_assert(CW % 64 == 0 && C4 % 256 == 0, "shapes");
-  static_assert(nMZ * 256 * kWaves == kMZ, "DMA split (bn3 mask)");
-  static_assert(KP * 8 <= kThreads, "one epilogue chunk per thread at most");
+  static constexpr int kKS = C4 / 32;            // 16x16x32 k-steps of the dgrad (W^T fragments in VGPRs)
+  static constexpr int kPB = KP / 16;            // pixel blocks of the dgrad tile
+  static constexpr int kWR = C4 / 4;             // dW rows per wave (4 waves cover C4), all CW columns
+  static constexpr int kMI = kWR / 32, kNJ = 2 * NG;
+  static constexpr int kEpiPer = KP * 8;         // epilogue chunks per slice (one thread each)
+  static_assert(CW % 64 == 0 && C4 % 256 == 0 && NG <= 2, "shapes");
+  static_assert(NG * KP * 8 <= kThreads, "one epilogue chunk per thread at most");
+  static_assert(kEpiPer % 64 == 0, "an epilogue wave stays in one slice");
+  static_assert(KP * 2 * NG <= 64, "bn2 mask: one 4-B DMA instruction per stage");
   static_assert(KP * C4 / 8 % kThreads == 0, "transform chunks");
-  static_assert(KP * kStgStride <= kY, "staging fits the dead z region");
+  static_assert(NG * KP * kStgStride <= kY, "staging fits the dead z region");
   static_assert(kLds <= 160 * 1024, "LDS");
 };
 
-// dz tile swizzle (512-B rows; 16-B chunk index ^= g(row)), an involution within the row.
+// dz tile swizzle (16-B chunk index ^= g(row)), an involution within the row.
 __device__ __forceinline__ int swz_dz(int row, int ch) { return ch ^ (((row & 3) << 2) | ((row >> 2) & 2)); }
 // 128-B rows of the transposed-read operands (conv1x1_wgrad.hip): rows r, r+1 are the two halves of
 // a 256-B bank row, r+2, r+3 flip chunk bit 2.
@@ -111,12 +133,11 @@ __device__ __forceinline__ bf16x8 cat2(s4v a, s4v b) {
 template <int SZ>
 __device__ __forceinline__ void dma(const void* src, char* lds_wave_base) {
   const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(PDT_LDS const char*)lds_wave_base);
+  static_assert(SZ == 16 || SZ == 4, "16-B or 4-B pieces");
   if constexpr (SZ == 16)
     asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(m0) : "memory");
-  else if constexpr (SZ == 4)
-    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(src), "s"(m0) : "memory");
   else
-    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_ubyte %0, off" ::"v"(src), "s"(m0) : "memory");
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(src), "s"(m0) : "memory");
 }
 // s_waitcnt vmcnt(N) leaving expcnt / lgkmcnt unconstrained (gfx9 simm16 encoding)
 template <int N>
@@ -140,74 +161,116 @@ struct FBArgs {
   const float* D;
   const uint16_t* wt;   // [CW][C4] conv weight transposed (W^T)
   const uint16_t* xa;   // [M][CW] conv input
-  BnSrc bs;             // bn2: input xb [M][CW], mask, mean; part [2][Gp][CW]
+  BnSrc bs;             // bn2: input xb [M][CW], mask, mean; part [2][G][CW]
+  const float* xcoef;   // RECOMP: bn2's forward apply [2][CW] (a, b): xa = relu(a xb + b)
+  uint8_t* mask_out;    // RECOMP: bn2's ReLU bits [M*CW/8], written here
   uint16_t* dxa;        // [M][CW]
-  float* ws;            // [Gp][C4][CW] wgrad partials
-  int M, ntiles, Gp;    // Gp: pixel groups (workgroups per role)
+  float* ws;            // [G][C4][CW] wgrad partials
+  int M, ntiles, G;     // G: pixel groups (workgroups per role)
 };
 
 template <class Cf>
 __global__ __launch_bounds__(Cf::kThreads, 1) void conv1x1_bwd_fused_kernel(FBArgs a) {
-  constexpr int C4 = Cf::C4, CW = Cf::CW, KP = Cf::KP, RY = Cf::kRowY, RX = Cf::kRowX, NR = Cf::NR;
+  constexpr int C4 = Cf::C4, CW = Cf::CW, KP = Cf::KP, RY = Cf::kRowY, RX = Cf::kRowX, NT = Cf::kThreads;
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  // wid through readfirstlane: the compiler then keeps everything derived from it (the DMA pieces'
+  // bases, strides, LDS destinations) in SGPRs
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wq = wid;                      // dW rows / dgrad channels of this wave (in every slice)
   // block -> (pixel group, role): the NR roles of a pixel group are blocks b, b + 8, ... (one XCD
-  // under round-robin placement: the second read of dy / z hits L2 — speed only, never correctness)
+  // under round-robin placement — speed only, never correctness)
+  constexpr int NR = Cf::NR;
   const int b = blockIdx.x;
-  const int role = (b / 8) % NR, pg = (b % 8) + 8 * (b / (8 * NR));
-  const int Gp = a.Gp, cs = role * 64;  // this workgroup's slice of CW
-  if (pg >= Gp) return;  // the grid is rounded up to whole XCD pairings (uniform exit, no barrier yet)
-  const int S = (a.ntiles - pg + Gp - 1) / Gp;  // tiles pg, pg + Gp, ... (Gp <= ntiles: S >= 1)
+  const int role = (b / 8) % NR, g = (b % 8) + 8 * (b / (8 * NR));
+  const int G = a.G, cs = role * 64 * Cf::NG;  // pixel groups; this workgroup's first channel of CW
+  if (g >= G) return;  // the grid is rounded up to whole XCD pairings (uniform exit, no barrier yet)
+  const int S = (a.ntiles - g + G - 1) / G;  // tiles g, g + G, ... (G <= ntiles: S >= 1)
 
   // ---- kernel-lifetime registers: W^T fragments (dgrad A operand), the transform coefficients
-  bf16x8 wf[Cf::kKS];
+  bf16x8 wf[Cf::NG][Cf::kKS];
 #pragma unroll
-  for (int ks = 0; ks < Cf::kKS; ++ks)
-    wf[ks] = *reinterpret_cast<const bf16x8*>(a.wt + (int64_t)(cs + 16 * wid + (lane & 15)) * C4 + 32 * ks +
-                                              8 * (lane >> 4));
-  const int tc = tid % (C4 / 8);  // transform pass: this thread's 8-channel chunk
+  for (int sl = 0; sl < Cf::NG; ++sl)
+#pragma unroll
+    for (int ks = 0; ks < Cf::kKS; ++ks)
+      wf[sl][ks] = *reinterpret_cast<const bf16x8*>(a.wt + (int64_t)(cs + sl * 64 + 16 * wq + (lane & 15)) * C4 +
+                                                    32 * ks + 8 * (lane >> 4));
+  const int tc = tid % (C4 / 8);  // transform pass: this thread's 8-channel chunk (fixed)
   float cm[8], cA[8], cB[8], cD[8];
+  float* const ctab = reinterpret_cast<float*>(lds + Cf::oCT);
+  if constexpr (Cf::kCoefLds) {
+    for (int i = tid; i < C4; i += NT) {
+      ctab[i] = a.mean[i]; ctab[C4 + i] = a.A[i]; ctab[2 * C4 + i] = a.B[i]; ctab[3 * C4 + i] = a.D[i];
+    }
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    cm[k] = a.mean[tc * 8 + k]; cA[k] = a.A[tc * 8 + k]; cB[k] = a.B[tc * 8 + k]; cD[k] = a.D[tc * 8 + k];
+    for (int k = 0; k < 8; ++k) { cm[k] = 0.f; cA[k] = 0.f; cB[k] = 0.f; cD[k] = 0.f; }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      cm[k] = a.mean[tc * 8 + k]; cA[k] = a.A[tc * 8 + k]; cB[k] = a.B[tc * 8 + k]; cD[k] = a.D[tc * 8 + k];
+    }
   }
-  const int ec = tid % 8, er = tid / 8;  // epilogue: chunk / pixel row of the dgrad slice tile
+  const int eg = tid / Cf::kEpiPer, el = tid % Cf::kEpiPer;  // epilogue: slice, then chunk / pixel row
+  const int ec = el % 8, er = el / 8;
+  const int ecs = cs + eg * 64;               // the epilogue thread's slice
   float bmu[8], bs1[8], bs2[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) { bs1[k] = 0.f; bs2[k] = 0.f; bmu[k] = 0.f; }
   if constexpr (Cf::BSTATS) {
+    if (eg < Cf::NG) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) bmu[k] = a.bs.mean[cs + ec * 8 + k];
+      for (int k = 0; k < 8; ++k) bmu[k] = a.bs.mean[ecs + ec * 8 + k];
+    }
   }
-  // the loads above complete before any DMA is issued (no vmcnt(0) inside the ring)
+  // RECOMP: bn2's forward coefficients of this lane's wgrad B columns (32 j + lane % 32); the
+  // epilogue's 8-channel coefficients come from an LDS copy, filled here
+  float xca[Cf::kNJ], xcb[Cf::kNJ];
 #pragma unroll
-  for (int ks = 0; ks < Cf::kKS; ++ks) asm volatile("" : "+v"(wf[ks]));
+  for (int j = 0; j < Cf::kNJ; ++j) { xca[j] = 0.f; xcb[j] = 0.f; }
+  float* const xct = reinterpret_cast<float*>(lds + Cf::oXC);
+  if constexpr (Cf::RECOMP) {
+#pragma unroll
+    for (int j = 0; j < Cf::kNJ; ++j) {
+      xca[j] = a.xcoef[cs + 32 * j + (lane & 31)];
+      xcb[j] = a.xcoef[CW + cs + 32 * j + (lane & 31)];
+    }
+    for (int i = tid; i < 2 * CW; i += NT) xct[i] = a.xcoef[i];  // [a | b]
+  }
+  // the loads above complete before any DMA is issued (no vmcnt(0) inside the ring); the LDS tables
+  // are visible to every wave after the first stage's barrier
+#pragma unroll
+  for (int j = 0; j < Cf::kNJ; ++j) asm volatile("" : "+v"(xca[j]), "+v"(xcb[j]));
+#pragma unroll
+  for (int sl = 0; sl < Cf::NG; ++sl)
+#pragma unroll
+    for (int ks = 0; ks < Cf::kKS; ++ks) asm volatile("" : "+v"(wf[sl][ks]));
 #pragma unroll
   for (int k = 0; k < 8; ++k) asm volatile("" : "+v"(cm[k]), "+v"(cA[k]), "+v"(cB[k]), "+v"(cD[k]), "+v"(bmu[k]));
 
   // ---- per-lane 16-B DMA pieces (stage independent). Piece q = wid + kWaves * i of the stage's
-  // list [Y pieces][Z pieces][XA pieces][XB pieces][dummies]: source = base + p0 * stride + off,
-  // valid while the pixel row is < M (else the zero page), LDS destination = slot + dst.
+  // list [Y][Z][XA slices][XB slices][dummies]: source = base + p0 * stride + off, valid while the
+  // pixel row is < M (else the zero page), LDS destination = slot + dst.
   const uint16_t* pbase[Cf::n16];
   int pstride[Cf::n16], prow[Cf::n16], poff[Cf::n16], pdst[Cf::n16];
 #pragma unroll
   for (int i = 0; i < Cf::n16; ++i) {
     const int q = wid + Cf::kWaves * i;
-    if (q < 2 * Cf::pY) {  // dy / z: linear 512-B / 1-KB rows
+    if (q < 2 * Cf::pY) {  // dy / z: linear C4-channel rows
       const int o = (q % Cf::pY) * 1024 + lane * 16;
       pbase[i] = q < Cf::pY ? a.dy : a.z;
       pstride[i] = C4;
       prow[i] = o / RY;
       poff[i] = prow[i] * C4 + ((o % RY) >> 4) * 8;
       pdst[i] = (q < Cf::pY ? Cf::oY : Cf::oZ) + (q % Cf::pY) * 1024;
-    } else if (q < 2 * Cf::pY + (Cf::BSTATS ? 2 : 1) * Cf::pX) {  // xa / xb slices: swizzled 128-B rows
-      const int qq = q - 2 * Cf::pY, k = qq % Cf::pX;
+    } else if (q < 2 * Cf::pY + Cf::nXsrc * Cf::NG * Cf::pX) {  // xa / xb slices: swizzled 128-B rows
+      const int qq = q - 2 * Cf::pY;
+      const int src = qq / (Cf::NG * Cf::pX), sl = (qq / Cf::pX) % Cf::NG, k = qq % Cf::pX;
+      const bool is_xa = !Cf::RECOMP && src == 0;
       const int o = k * 1024 + lane * 16;
-      pbase[i] = (qq < Cf::pX ? a.xa : a.bs.x) + cs;
+      pbase[i] = (is_xa ? a.xa : a.bs.x) + cs + sl * 64;
       pstride[i] = CW;
       prow[i] = o / RX;
       poff[i] = prow[i] * CW + swz128(prow[i], (o % RX) >> 4) * 8;
-      pdst[i] = (qq < Cf::pX ? Cf::oXA : Cf::oXB) + k * 1024;
+      pdst[i] = (is_xa ? Cf::oXA : Cf::oXB) + sl * Cf::kXA + k * 1024;
     } else {  // dummy: zero page -> the slot's pad area (keeps every wave's DMA count equal)
       pbase[i] = reinterpret_cast<const uint16_t*>(g_fb_zero);
       pstride[i] = 0;
@@ -218,7 +281,7 @@ __global__ __launch_bounds__(Cf::kThreads, 1) void conv1x1_bwd_fused_kernel(FBAr
   }
   auto issue = [&](int s) {
     char* slot = lds + (s % Cf::kSlots) * Cf::kSlot;
-    const int p0 = (pg + s * Gp) * KP;
+    const int p0 = (g + s * G) * KP;
 #pragma unroll
     for (int i = 0; i < Cf::n16; ++i) {
       const bool ok = p0 + prow[i] < a.M;
@@ -226,33 +289,34 @@ __global__ __launch_bounds__(Cf::kThreads, 1) void conv1x1_bwd_fused_kernel(FBAr
               slot + pdst[i]);
     }
 #pragma unroll
-    for (int i = 0; i < Cf::nMZ; ++i) {
-      const int o = (wid * Cf::nMZ + i) * 256 + lane * 4;
-      const bool ok = p0 + o / (C4 / 8) < a.M;
-      dma<4>(ok ? (const void*)(a.mz + (int64_t)p0 * (C4 / 8) + o) : (const void*)g_fb_zero,
-             slot + Cf::oMZ + (wid * Cf::nMZ + i) * 256);
-    }
-#pragma unroll
-    for (int i = 0; i < Cf::nMB; ++i) {  // bn2's mask bytes of the slice: 8 per pixel
+    for (int i = 0; i < Cf::n4; ++i) {
       const int q = wid + Cf::kWaves * i;
-      const int o = q * 64 + lane, row = o / 8;
-      const bool real = q < Cf::pMB && a.bs.mask != nullptr;
-      const bool ok = real && p0 + row < a.M;
-      dma<1>(ok ? (const void*)(a.bs.mask + ((int64_t)(p0 + row) * CW + cs) / 8 + (o % 8)) : (const void*)g_fb_zero,
-             slot + (real ? Cf::oMB + q * 64 : Cf::oPad));
+      if (q < Cf::pMZ) {  // bn3's mask rows: 256 B = 256 / (C4/8) pixel rows
+        const int o = q * 256 + lane * 4;
+        const bool ok = p0 + o / (C4 / 8) < a.M;
+        dma<4>(ok ? (const void*)(a.mz + (int64_t)p0 * (C4 / 8) + o) : (const void*)g_fb_zero,
+               slot + Cf::oMZ + q * 256);
+      } else if (q < Cf::pMZ + Cf::pMB) {  // bn2's mask bytes of every slice: lane = 4 B of a row
+        const int row = lane / (2 * Cf::NG), wd = lane % (2 * Cf::NG);
+        const bool ok = a.bs.mask != nullptr && row < KP && p0 + row < a.M;
+        dma<4>(ok ? (const void*)(a.bs.mask + (int64_t)(p0 + row) * (CW / 8) + cs / 8 + wd * 4) : (const void*)g_fb_zero,
+               slot + (a.bs.mask != nullptr ? Cf::oMB : Cf::oPad));
+      } else {
+        dma<4>((const void*)g_fb_zero, slot + Cf::oPad);
+      }
     }
   };
 
   // ---- wgrad lane roles (transposed reads; conv1x1_wgrad.hip)
-  const int grp = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-  const int prw = 8 * (grp >> 1) + q, half8 = (p & 1) * 8;
+  const int grp = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
+  const int prw = 8 * (grp >> 1) + q4, half8 = (p4 & 1) * 8;
   int ya[Cf::kMI], xa[Cf::kNJ];
 #pragma unroll
   for (int i = 0; i < Cf::kMI; ++i)
-    ya[i] = prw * RY + (swz_dz(prw, (wid * Cf::kWR + 32 * i + 16 * (grp & 1) + 4 * p) >> 3) << 4) + half8;
+    ya[i] = prw * RY + (swz_dz(prw, (wq * Cf::kWR + 32 * i + 16 * (grp & 1) + 4 * p4) >> 3) << 4) + half8;
 #pragma unroll
-  for (int j = 0; j < Cf::kNJ; ++j)
-    xa[j] = prw * RX + (swz128(prw, (32 * j + 16 * (grp & 1) + 4 * p) >> 3) << 4) + half8;
+  for (int j = 0; j < Cf::kNJ; ++j)  // column block j: slice j / 2, its columns 32 (j % 2) ..
+    xa[j] = (j / 2) * Cf::kXA + prw * RX + (swz128(prw, (32 * (j % 2) + 16 * (grp & 1) + 4 * p4) >> 3) << 4) + half8;
   f16v acc[Cf::kMI][Cf::kNJ];
 #pragma unroll
   for (int i = 0; i < Cf::kMI; ++i)
@@ -266,7 +330,7 @@ __global__ __launch_bounds__(Cf::kThreads, 1) void conv1x1_bwd_fused_kernel(FBAr
   for (int s = 0; s < Cf::kSlots - 1; ++s)
     if (s < S) issue(s);
   for (int s = 0; s < S; ++s) {
-    // stage s's DMA is done once only the next stage's DMA (+ the previous stage's epilogue store,
+    // stage s's DMA is done once only the next stage's DMA (+ the previous stage's epilogue stores,
     // issued after it) is pending; every count is exact
     if (s + 1 >= S) wait_vm<0>();
     else if (s == 0) wait_vm<Cf::kG>();
@@ -274,12 +338,21 @@ __global__ __launch_bounds__(Cf::kThreads, 1) void conv1x1_bwd_fused_kernel(FBAr
     lds_barrier();  // B1: DMA(s) visible to all waves; every wave is past stage s-1
     if (s + Cf::kSlots - 1 < S) issue(s + Cf::kSlots - 1);  // its slot was last used in stage s-1
     const char* slot = lds + (s % Cf::kSlots) * Cf::kSlot;
-    const int p0 = (pg + s * Gp) * KP;
+    const int p0 = (g + s * G) * KP;
 
     // ---- transform: dz = A dy m + B (z - mean) + D -> swizzled dz tile (rows past M: zero)
 #pragma unroll
-    for (int i = 0; i < KP * C4 / 8 / Cf::kThreads; ++i) {
-      const int r = tid / (C4 / 8) + i * (Cf::kThreads / (C4 / 8));
+    for (int i = 0; i < KP * C4 / 8 / NT; ++i) {
+      const int r = tid / (C4 / 8) + i * (NT / (C4 / 8));
+      if constexpr (Cf::kCoefLds) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          *reinterpret_cast<float4*>(cm + 4 * h) = *reinterpret_cast<const float4*>(ctab + tc * 8 + 4 * h);
+          *reinterpret_cast<float4*>(cA + 4 * h) = *reinterpret_cast<const float4*>(ctab + C4 + tc * 8 + 4 * h);
+          *reinterpret_cast<float4*>(cB + 4 * h) = *reinterpret_cast<const float4*>(ctab + 2 * C4 + tc * 8 + 4 * h);
+          *reinterpret_cast<float4*>(cD + 4 * h) = *reinterpret_cast<const float4*>(ctab + 3 * C4 + tc * 8 + 4 * h);
+        }
+      }
       const uint4 gv = *reinterpret_cast<const uint4*>(slot + Cf::oY + r * RY + tc * 16);
       const uint4 zv = *reinterpret_cast<const uint4*>(slot + Cf::oZ + r * RY + tc * 16);
       const unsigned mk = *reinterpret_cast<const uint8_t*>(slot + Cf::oMZ + r * (C4 / 8) + tc);
@@ -306,20 +379,24 @@ __global__ __launch_bounds__(Cf::kThreads, 1) void conv1x1_bwd_fused_kernel(FBAr
     lds_barrier();  // B2: dz tile complete; z region of this slot is dead (reused as staging)
 
     // ---- dgrad: D[ci][px] = sum_c W^T[ci][c] dz[px][c]; lane holds 4 consecutive ci of one pixel
-    f4 dacc[Cf::kPB];
+    f4 dacc[Cf::NG][Cf::kPB];
 #pragma unroll
-    for (int pb = 0; pb < Cf::kPB; ++pb) dacc[pb] = f4{0.f, 0.f, 0.f, 0.f};
+    for (int sl = 0; sl < Cf::NG; ++sl)
+#pragma unroll
+      for (int pb = 0; pb < Cf::kPB; ++pb) dacc[sl][pb] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < Cf::kKS; ++ks) {
 #pragma unroll
       for (int pb = 0; pb < Cf::kPB; ++pb) {
         const int row = 16 * pb + (lane & 15), ch = 4 * ks + (lane >> 4);
         const bf16x8 bv = *reinterpret_cast<const bf16x8*>(dzs + row * RY + (swz_dz(row, ch) << 4));
-        dacc[pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ks], bv, dacc[pb], 0, 0, 0);
+#pragma unroll
+        for (int sl = 0; sl < Cf::NG; ++sl)
+          dacc[sl][pb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[sl][ks], bv, dacc[sl][pb], 0, 0, 0);
       }
     }
-    // ---- wgrad: dW[c][cs + k] += sum_px dz[px][c] xa[px][cs + k]
-    const char* xas = slot + Cf::oXA;
+    // ---- wgrad: dW[c][k] += sum_px dz[px][c] xa[px][k]
+    const char* xas = slot + (Cf::RECOMP ? Cf::oXB : Cf::oXA);
 #pragma unroll
     for (int kk = 0; kk < KP / 16; ++kk) {
       bf16x8 fa[Cf::kMI], fb[Cf::kNJ];
@@ -338,6 +415,21 @@ __global__ __launch_bounds__(Cf::kThreads, 1) void conv1x1_bwd_fused_kernel(FBAr
       for (int i = 0; i < Cf::kMI; ++i) asm volatile("" : "+v"(fa[i]));
 #pragma unroll
       for (int j = 0; j < Cf::kNJ; ++j) asm volatile("" : "+v"(fb[j]));
+      if constexpr (Cf::RECOMP) {  // xa = relu(a xb + b): 8 pixels of ONE channel per lane
+#pragma unroll
+        for (int j = 0; j < Cf::kNJ; ++j) {
+          typedef unsigned u4 __attribute__((ext_vector_type(4)));
+          const u4 w = __builtin_bit_cast(u4, fb[j]);
+          u4 o;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const float t0 = __uint_as_float(w[k] << 16) * xca[j] + xcb[j];
+            const float t1 = __uint_as_float(w[k] & 0xffff0000u) * xca[j] + xcb[j];
+            o[k] = (uint32_t)f2bf(t0 > 0.f ? t0 : 0.f) | ((uint32_t)f2bf(t1 > 0.f ? t1 : 0.f) << 16);
+          }
+          fb[j] = __builtin_bit_cast(bf16x8, o);
+        }
+      }
 #pragma unroll
       for (int i = 0; i < Cf::kMI; ++i)
 #pragma unroll
@@ -345,30 +437,50 @@ __global__ __launch_bounds__(Cf::kThreads, 1) void conv1x1_bwd_fused_kernel(FBAr
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
     }
 
-    // ---- epilogue: stage the bf16 dgrad slice [KP][64] in the dead z region, then 16-B rows out
+    // ---- epilogue: stage each slice's bf16 dgrad tile [KP][64] in the dead z region, 16-B rows out
     char* stg = const_cast<char*>(slot) + Cf::oZ;
 #pragma unroll
-    for (int pb = 0; pb < Cf::kPB; ++pb) {
-      const int px = 16 * pb + (lane & 15), ci = 16 * wid + 4 * (lane >> 4);
-      const f4 v = dacc[pb];
-      uint2 pk;
-      pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-      pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-      *reinterpret_cast<uint2*>(stg + px * Cf::kStgStride + ci * 2) = pk;
-    }
+    for (int sl = 0; sl < Cf::NG; ++sl)
+#pragma unroll
+      for (int pb = 0; pb < Cf::kPB; ++pb) {
+        const int px = 16 * pb + (lane & 15), ci = 16 * wq + 4 * (lane >> 4);
+        const f4 v = dacc[sl][pb];
+        uint2 pk;
+        pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+        pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+        *reinterpret_cast<uint2*>(stg + (sl * KP + px) * Cf::kStgStride + ci * 2) = pk;
+      }
     lds_barrier();  // B3
     {
-      const bool in_tile = er < KP;
-      const uint4 v = *reinterpret_cast<const uint4*>(stg + (in_tile ? er : 0) * Cf::kStgStride + ec * 16);
+      const bool in_tile = eg < Cf::NG && er < KP;  // (threads past the tile: the sink store only)
+      const uint4 v = *reinterpret_cast<const uint4*>(stg + (in_tile ? eg * KP + er : 0) * Cf::kStgStride + ec * 16);
       if (in_tile && p0 + er < a.M) {
-        if constexpr (Cf::BSTATS) {
-          const uint4 xb = *reinterpret_cast<const uint4*>(slot + Cf::oXB + er * RX + (swz128(er, ec) << 4));
-          const unsigned mk = *reinterpret_cast<const uint8_t*>(slot + Cf::oMB + er * 8 + ec);
+        const char* xbp = slot + Cf::oXB + eg * Cf::kXA + er * RX + (swz128(er, ec) << 4);
+        if constexpr (Cf::RECOMP) {  // bn2's mask from its input, same fma as its forward apply
+          const uint4 xb = *reinterpret_cast<const uint4*>(xbp);
+          const uint32_t xw[4] = {xb.x, xb.y, xb.z, xb.w};
+          float eca[8], ecb[8];
+          *reinterpret_cast<float4*>(eca) = *reinterpret_cast<const float4*>(xct + ecs + ec * 8);
+          *reinterpret_cast<float4*>(eca + 4) = *reinterpret_cast<const float4*>(xct + ecs + ec * 8 + 4);
+          *reinterpret_cast<float4*>(ecb) = *reinterpret_cast<const float4*>(xct + CW + ecs + ec * 8);
+          *reinterpret_cast<float4*>(ecb + 4) = *reinterpret_cast<const float4*>(xct + CW + ecs + ec * 8 + 4);
+          unsigned mk = 0;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const float xv = __uint_as_float(k & 1 ? (xw[k >> 1] & 0xffff0000u) : (xw[k >> 1] << 16));
+            mk |= (xv * eca[k] + ecb[k] > 0.f ? 1u : 0u) << k;
+          }
+          bn_bwd_accum8(v, xb, mk, bmu, bs1, bs2);
+          a.mask_out[((int64_t)(p0 + er) * CW + ecs) / 8 + ec] = (uint8_t)mk;
+        } else if constexpr (Cf::BSTATS) {
+          const uint4 xb = *reinterpret_cast<const uint4*>(xbp);
+          const unsigned mk = *reinterpret_cast<const uint8_t*>(slot + Cf::oMB + er * Cf::kMBRow + eg * 8 + ec);
           bn_bwd_accum8(v, xb, a.bs.mask ? mk : 0xffu, bmu, bs1, bs2);
         }
-        *reinterpret_cast<uint4*>(a.dxa + (int64_t)(p0 + er) * CW + cs + ec * 8) = v;
+        *reinterpret_cast<uint4*>(a.dxa + (int64_t)(p0 + er) * CW + ecs + ec * 8) = v;
       } else {
         g_fb_sink[tid] = v;  // one store per thread per stage, always (exact vmcnt counts)
+        if constexpr (Cf::RECOMP) reinterpret_cast<uint8_t*>(g_fb_sink)[8192 + tid] = 0;
       }
     }
   }
@@ -376,9 +488,9 @@ __global__ __launch_bounds__(Cf::kThreads, 1) void conv1x1_bwd_fused_kernel(FBAr
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
 
-  // ---- wgrad partials ws[pg][c][cs + k]; 32x32 accumulator: lane holds k = l % 32,
+  // ---- wgrad partials ws[g][c][k]; 32x32 accumulator: lane holds k = l % 32,
   // c = 8 (v / 4) + 4 (l / 32) + v % 4 for v = 0..15
-  float* wsp = a.ws + (int64_t)pg * C4 * CW + cs;
+  float* wsp = a.ws + (int64_t)g * C4 * CW + cs;
 #pragma unroll
   for (int i = 0; i < Cf::kMI; ++i)
 #pragma unroll
@@ -386,12 +498,39 @@ __global__ __launch_bounds__(Cf::kThreads, 1) void conv1x1_bwd_fused_kernel(FBAr
       const int k = 32 * j + (lane & 31);
 #pragma unroll
       for (int v = 0; v < 16; ++v) {
-        const int c = wid * Cf::kWR + 32 * i + 8 * (v >> 2) + 4 * (lane >> 5) + (v & 3);
+        const int c = wq * Cf::kWR + 32 * i + 8 * (v >> 2) + 4 * (lane >> 5) + (v & 3);
         wsp[(int64_t)c * CW + k] = acc[i][j][v];
       }
     }
-  if constexpr (Cf::BSTATS)
-    bn_bwd_tile_store<64, Cf::kWaves>(bs1, bs2, reinterpret_cast<float*>(lds), a.bs.part, Gp, pg, CW, cs);
+  if constexpr (Cf::BSTATS) {
+    // bn2 partials of this workgroup: lanes holding one chunk differ in lane bits 3..5 (a wave stays
+    // in one slice); then the waves of a slice in order (fixed-order: deterministic)
+#pragma unroll
+    for (int sh = 8; sh < 64; sh <<= 1)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        bs1[k] += __shfl_xor(bs1[k], sh, 64);
+        bs2[k] += __shfl_xor(bs2[k], sh, 64);
+      }
+    float* red = reinterpret_cast<float*>(lds);
+    __syncthreads();
+    if (lane < 8) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        red[wid * 128 + lane * 8 + k] = bs1[k];
+        red[wid * 128 + 64 + lane * 8 + k] = bs2[k];
+      }
+    }
+    __syncthreads();
+    constexpr int kWps = Cf::kEpiPer / 64;  // waves per slice in the epilogue
+    for (int t = tid; t < Cf::NG * 128; t += NT) {
+      const int sl = t / 128, st = (t / 64) % 2, ch = t % 64;
+      float sum = 0.f;
+#pragma unroll
+      for (int w = 0; w < kWps; ++w) sum += red[(sl * kWps + w) * 128 + st * 64 + ch];
+      a.bs.part[((int64_t)st * G + g) * CW + cs + sl * 64 + ch] = sum;
+    }
+  }
 }
 
 // dw[c][k] (bf16) = sum over the G workgroup partials in a fixed order (conv1x1_wgrad.hip's scheme:
@@ -423,7 +562,7 @@ __global__ __launch_bounds__(256) void fb_reduce_kernel(const float* __restrict_
   }
 }
 
-int g_grid = 0;  // 0: by shape (one workgroup per CU)
+int g_grid = 0;  // 0: one workgroup per CU
 
 // pixel groups: one workgroup per CU in all (NR roles each), a multiple of 8 (XCD pairing)
 inline int groups_of(int ntiles, int nr) {
@@ -442,13 +581,13 @@ int launch(const FBArgs& a0, uint16_t* dw, hipStream_t s) {
       return -3;
     attr = true;
   }
-  // every role of every pixel group: Gp groups x NR roles, with the pairing of the block map
-  // (groups past ntiles run zero stages; the grid stays a multiple of 8 * NR)
-  const int nblk = ((a0.Gp + 7) / 8) * 8 * Cf::NR;
+  // every role of every pixel group with the pairing of the block map (the grid is rounded up to a
+  // multiple of 8 * NR; groups past G exit at once)
+  const int nblk = ((a0.G + 7) / 8) * 8 * Cf::NR;
   hipLaunchKernelGGL(conv1x1_bwd_fused_kernel<Cf>, dim3(nblk), dim3(Cf::kThreads), Cf::kLds, s, a0);
   const int64_t n4 = (int64_t)Cf::C4 * Cf::CW / 4;
   hipLaunchKernelGGL(fb_reduce_kernel, dim3((unsigned)((n4 + kRedCols - 1) / kRedCols)), dim3(kRedCols * kRedGroups),
-                     0, s, a0.ws, dw, a0.Gp, n4);
+                     0, s, a0.ws, dw, a0.G, n4);
   return 0;
 }
 
@@ -461,8 +600,7 @@ extern "C" {
 // Shapes the fused kernel takes: (C4, CW) = (256, 64) and (512, 128) (ResNet-50 layers 1 and 2).
 int pdt_conv1x1_bwd_fused_ok(int C4, int CW) { return (C4 == 256 && CW == 64) || (C4 == 512 && CW == 128); }
 
-// Pixel groups of a call = wgrad partial slabs (workspace Gp*C4*CW floats) = bn2 partial rows
-// ([2][Gp][CW]).
+// Workgroups of a call = wgrad partial slabs (workspace G*C4*CW floats) = bn2 partial rows ([2][G][CW]).
 int pdt_conv1x1_bwd_fused_grid(int M, int C4, int CW) {
   const int kp = kp_of(C4);
   return groups_of((M + kp - 1) / kp, CW / 64);
@@ -470,26 +608,33 @@ int pdt_conv1x1_bwd_fused_grid(int M, int C4, int CW) {
 
 // See the header. dy, z: [M][C4]; mz: M*C4/8 bytes; mean/A/B/D: [C4]; wt: [CW][C4]; xa: [M][CW];
 // bx / bm / bmean / bpart (all null = no bn2 reduction; bm may be null = no ReLU): bn2's input
-// [M][CW], mask, mean [CW] and the [2][Gp][CW] partials out; dxa: [M][CW]; dw: [C4][CW] bf16;
-// ws: Gp*C4*CW floats. Returns 0, -1 for an unsupported shape.
+// [M][CW], mask, mean [CW] and the [2][G][CW] partials out; dxa: [M][CW]; dw: [C4][CW] bf16;
+// ws: G*C4*CW floats. xcoef / mask_out (RECOMP, both or neither): xa is NOT read — it is
+// relu(xcoef[0] bx + xcoef[1]) (bn2's deferred forward apply; xa may be null) — and bn2's ReLU bits are
+// computed and written to mask_out (bm unused); needs bx / bmean / bpart. Returns 0, -1 for an
+// unsupported shape.
 int pdt_conv1x1_bwd_fused(const uint16_t* dy, const uint16_t* z, const uint8_t* mz, const float* mean, const float* A,
                           const float* B, const float* D, const uint16_t* wt, const uint16_t* xa, const uint16_t* bx,
-                          const uint8_t* bm, const float* bmean, float* bpart, uint16_t* dxa, uint16_t* dw, float* ws,
-                          int M, int C4, int CW, hipStream_t s) {
+                          const uint8_t* bm, const float* bmean, float* bpart, const float* xcoef, uint8_t* mask_out,
+                          uint16_t* dxa, uint16_t* dw, float* ws, int M, int C4, int CW, hipStream_t s) {
   if (!pdt_conv1x1_bwd_fused_ok(C4, CW) || M < 1 || (int64_t)M * C4 >= ((int64_t)1 << 31)) return -1;
   if ((bx != nullptr) != (bpart != nullptr) || (bx && !bmean)) return -1;
+  const bool rc = xcoef != nullptr;
+  if (rc != (mask_out != nullptr) || (rc && !bx) || (!rc && !xa)) return -1;
   const int kp = kp_of(C4), ntiles = (M + kp - 1) / kp;
-  FBArgs a{dy, z, mz, mean, A, B, D, wt, xa, BnSrc{bx, bm, bmean, bpart}, dxa, ws, M, ntiles,
+  FBArgs a{dy, z, mz, mean, A, B, D, wt, xa, BnSrc{bx, bm, bmean, bpart}, xcoef, mask_out, dxa, ws, M, ntiles,
            pdt_conv1x1_bwd_fused_grid(M, C4, CW)};
   if (C4 == 256) {
+    if (rc) return launch<FB<256, 64, true, true>>(a, dw, s);
     if (bx) return launch<FB<256, 64, true>>(a, dw, s);
     return launch<FB<256, 64, false>>(a, dw, s);
   }
+  if (rc) return launch<FB<512, 128, true, true>>(a, dw, s);
   if (bx) return launch<FB<512, 128, true>>(a, dw, s);
   return launch<FB<512, 128, false>>(a, dw, s);
 }
 
-// Tuning hook: total workgroups per call (0 = one per CU).
+// Tuning hook: workgroups per call (0 = one per CU).
 void pdt_conv1x1_bwd_fused_tune(int grid) {
   if (grid >= 0) g_grid = grid;
 }

@@ -20,6 +20,7 @@ import torch
 from torch import nn
 
 from ..ops.batchnorm import BatchNorm2d, BNGradLink, ResidualGradLink
+from ..config import SW
 from ..ops.conv import Conv1x1, SplitConv2d, linked_conv, stem_block
 
 
@@ -108,17 +109,24 @@ class Bottleneck(nn.Module):
             # identity blocks: bn3's backward may hand the shortcut gradient over as (dy, mask)
             link = ResidualGradLink(lazy=self.downsample is None and self.conv1.masked_residual_ok(x))
             out = bn_act(self.bn1, self.conv1(x, res_link=link), relu=True)
-            out = bn_act(self.bn2, self.conv2(out), relu=True)
+            z2 = self.conv2(out)  # same shape / layout as bn2's output: decides conv3's paths
+            ds_bn = self.downsample[1] if self.downsample is not None else None
             # conv3 + bn3 backward as one kernel: bn3 hands its input gradient to conv3 in deferred form
-            blink = BNGradLink() if (self.conv3.fused_bwd_ok(out) and not self.bn3.has_hooks()
-                                     and (link.lazy or self.downsample is not None)) else None
+            blink = BNGradLink() if (self.conv3.fused_bwd_ok(z2) and not self.bn3.has_hooks()
+                                     and (link.lazy or (isinstance(ds_bn, BatchNorm2d) and DS_MASKED_GRAD[0]))) \
+                else None
+            if blink is not None and SW.bn2_defer and isinstance(self.bn2, BatchNorm2d) and not self.bn2.has_hooks():
+                # bn2 -> conv3: statistics only here; conv3's GEMM reads relu(a z2 + b) on load and its fused
+                # backward recomputes that operand (ops/batchnorm.py DeferredReLUBN): bn2's output never exists
+                out = self.bn2._forward_deferred_relu(z2)
+            else:
+                out = bn_act(self.bn2, z2, relu=True)
             out = self.conv3(out, bwd_link=blink)
             if self.downsample is None:  # identity: bn3's backward deposits the shortcut gradient
                 return self.bn3(out, residual=x, relu=True, res_link=link, out_link=blink)
             # shortcut built AFTER the main branch so its backward nodes run first (higher
             # autograd sequence numbers): the shortcut conv deposits, conv1 accumulates. Either
             # order is correct (whichever branch finishes second adds), this one saves a pass.
-            ds_bn = self.downsample[1]
             if isinstance(ds_bn, BatchNorm2d) and DS_MASKED_GRAD[0]:
                 # bn3's backward hands the shortcut gradient to the downsample BN as (dy, ReLU mask):
                 # the masked copy dres is never written

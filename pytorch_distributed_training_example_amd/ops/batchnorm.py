@@ -152,9 +152,21 @@ class BNGradLink:
 class _BNTrainFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, residual, weight, bias, running_mean, running_var, momentum, eps, relu, link=None,
-                part=None, gsrc=None, glink=None, res_ab=None, defer=None, out_link=None):
+                part=None, gsrc=None, glink=None, res_ab=None, defer=None, out_link=None, defer_relu=None):
         C = native()
-        if defer is not None:  # statistics only: the consumer applies y = a x + b itself (deferred apply)
+        ctx.defer_relu = defer_relu
+        if defer_relu is not None:  # stats only; the consumer conv applies relu(a x + b) (DeferredReLUBN)
+            if part is not None:
+                _, _, mean, invstd, ab = C.bn_fwd_train_tiles(x, part, None, weight, bias, running_mean,
+                                                              running_var, momentum, eps, False, apply=False)
+            else:
+                _, _, mean, invstd, ab = C.bn_fwd_train(x, None, weight, bias, running_mean, running_var,
+                                                        momentum, eps, False, apply=False)
+            M = x.numel() // x.shape[1]
+            dmask = torch.empty(M * x.shape[1] // 8, dtype=torch.uint8, device=x.device)  # filled in backward
+            defer_relu.extend([ab, dmask, mean])
+            y, mask = x.view_as(x), None
+        elif defer is not None:  # statistics only: the consumer applies y = a x + b itself (deferred apply)
             if part is not None:
                 _, _, mean, invstd, ab = C.bn_fwd_train_tiles(x, part, None, weight, bias, running_mean,
                                                               running_var, momentum, eps, False, apply=False)
@@ -170,6 +182,8 @@ class _BNTrainFn(torch.autograd.Function):
             y, mask, mean, invstd = C.bn_fwd_train(x, residual, weight, bias, running_mean, running_var,
                                                    momentum, eps, relu, res_ab=res_ab)
         ctx.relu = relu
+        if defer_relu is not None:
+            ctx.dmask = defer_relu[1]  # NOT saved_tensors: the consumer's backward writes it (raw pointer)
         ctx.has_res = residual is not None
         ctx.has_weight = weight is not None
         ctx.link = link
@@ -185,13 +199,15 @@ class _BNTrainFn(torch.autograd.Function):
         if gsrc is not None:  # what the consumer's dgrad GEMM needs for this BN's backward reduction
             gsrc.x, gsrc.mask, gsrc.mean = x, (mask if relu else None), mean
         # backward needs the BN input and a 1-bit ReLU mask, never the output y
-        ctx.save_for_backward(x, mask if relu else None, weight, mean, invstd)
+        ctx.save_for_backward(x, mask if (relu and defer_relu is None) else None, weight, mean, invstd)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, mask, weight, mean, invstd = ctx.saved_tensors
-        tail = (None,) * 12
+        if ctx.defer_relu is not None:  # the mask was written by the consumer's backward
+            mask = ctx.dmask
+        tail = (None,) * 13
         need_w = ctx.has_weight and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3])
         if dy is None:  # gradient handed over through glink as (dy, mask): a ReLU'd dy of the consumer
             g = ctx.glink.take() if ctx.glink is not None else None
@@ -295,6 +311,30 @@ class DeferredBNOutput:
         return _MaterializeFn.apply(self.raw, self.ab)
 
 
+class DeferredReLUBN:
+    """Internal handle for ``relu(bn(x))`` whose apply was deferred INTO THE CONSUMER CONV (ResNet
+    bottleneck bn2 -> conv3): statistics only in the forward; conv3's GEMM reads ``relu(a x + b)`` on
+    load (conv1x1.hip ATR) and its fused backward recomputes that operand and WRITES this BatchNorm's
+    ReLU bits into ``mask`` (conv1x1_bwd_fused.hip RECOMP), which the BatchNorm's backward then reads.
+    ``raw`` is the BatchNorm's autograd output (its storage holds the BN INPUT x); ``ab`` = [2, C]
+    fp32 (a, b); ``gsrc`` receives the BatchNorm's backward reduction from conv3's backward.
+    Only ``Bottleneck`` creates one, and only together with conv3's fused backward (``bwd_link``)."""
+
+    __slots__ = ("raw", "ab", "mask", "gsrc")
+
+    def __init__(self, raw, ab, mask, gsrc):
+        self.raw, self.ab, self.mask, self.gsrc = raw, ab, mask, gsrc
+
+    def materialize_parts(self):
+        """(relu(a x + b) as bf16, its ReLU bits) computed with PyTorch ops (fallback path)."""
+        sh = (1, -1, 1, 1)
+        t = self.raw.float() * self.ab[0].view(sh) + self.ab[1].view(sh)
+        y = t.clamp_min(0).to(self.raw.dtype).contiguous(memory_format=torch.channels_last)
+        pos = (t > 0).permute(0, 2, 3, 1).reshape(-1, 8).to(torch.int32)
+        bits = (pos << torch.arange(8, device=pos.device, dtype=torch.int32)).sum(1).to(torch.uint8)
+        return y, bits
+
+
 def materialize(t):
     """The value of a possibly apply-deferred BatchNorm output (a tensor passes through)."""
     return t.materialize() if isinstance(t, DeferredBNOutput) else t
@@ -302,7 +342,8 @@ def materialize(t):
 
 def batch_norm_act(x, residual, weight, bias, running_mean, running_var, training, momentum, eps, relu,
                    res_link: Optional[ResidualGradLink] = None, grad_link: Optional[ResidualGradLink] = None,
-                   defer_apply: bool = False, out_link: Optional[BNGradLink] = None):
+                   defer_apply: bool = False, out_link: Optional[BNGradLink] = None,
+                   defer_relu_apply: bool = False):
     """Functional fused BN(+add)(+ReLU). Native when x is a channels_last bf16 GPU tensor.
     ``res_link``: route the residual gradient through it instead of returning it (see
     ``ResidualGradLink``); only honoured on the native training path — callers check
@@ -334,11 +375,17 @@ def batch_norm_act(x, residual, weight, bias, running_mean, running_var, trainin
             defer = [] if (defer_apply and residual is None and not relu and x.dim() == 4) else None
             if defer is not None:
                 gsrc = None
+            dre = [] if (defer_relu_apply and residual is None and relu and x.dim() == 4 and gsrc is not None) else None
             y = _BNTrainFn.apply(x, residual, weight, bias, running_mean, running_var,
                                  float(momentum), float(eps), bool(relu), res_link, part, gsrc, grad_link, ab, defer,
-                                 out_link)
+                                 out_link, dre)
             if defer:
                 return DeferredBNOutput(y, defer[0])
+            if dre:
+                ab2, dmask, mean = dre
+                gsrc.x, gsrc.mask, gsrc.mean = x, dmask, mean
+                gsrc.out_version = y._version
+                return DeferredReLUBN(y, ab2, dmask, gsrc)
             if gsrc is not None:  # a consumer conv may take this BN's backward reduction (ops/conv.py)
                 gsrc.out_version = y._version
                 y._pdt_gsrc = gsrc
@@ -431,6 +478,13 @@ class BatchNorm2d(nn.BatchNorm2d):
         b = self.bias if self.affine else None
         return batch_norm_act(x, None, w, b, rm, rv, training, momentum if momentum is not None else 0.0,
                               self.eps, False, None, grad_link, defer_apply=True)
+
+    def _forward_deferred_relu(self, x: torch.Tensor):
+        """Internal (``Bottleneck``'s bn2 when conv3 runs the fused backward): ``relu(bn(x))`` as a
+        ``DeferredReLUBN`` (statistics only; conv3 applies it on load) on the native training path, a
+        normal output tensor otherwise. Bypasses the module call: callers check ``has_hooks()``."""
+        training, w, b, rm, rv, momentum, eps = self._step_args()
+        return batch_norm_act(x, None, w, b, rm, rv, training, momentum, eps, True, defer_relu_apply=True)
 
     def _step_args(self):
         """Per-call arguments of a training / eval forward (counts the batch, as ``forward`` does):

@@ -187,7 +187,9 @@ def _nhwc2d(t: torch.Tensor) -> torch.Tensor:
 
 class _Conv1x1Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, link=None, stats_out=None, gsrc=None, bwd_link=None):
+    def forward(ctx, x, weight, link=None, stats_out=None, gsrc=None, bwd_link=None, dre=None):
+        """``dre``: x is the INPUT of a BatchNorm + ReLU whose apply is deferred to here
+        (ops/batchnorm.py DeferredReLUBN): the GEMM reads relu(a x + b) (our kernel, ATR)."""
         N, Ci, H, W = x.shape
         Co = weight.shape[0]
         x2 = _nhwc2d(x)
@@ -201,6 +203,15 @@ class _Conv1x1Fn(torch.autograd.Function):
         if bwd_link is not None:
             ctx.set_materialize_grads(False)
         ctx.save_for_backward(x, weight)
+        ctx.dre = dre
+        if dre is not None:  # always our GEMM: no library takes the deferred operand
+            from ._native import native
+            y = torch.empty((N, Co, H, W), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+            part = native().conv1x1_gemm(x2, w2.contiguous(), _nhwc2d(y), False, stats_out is not None,
+                                         a_coef=dre.ab)
+            if stats_out is not None:
+                stats_out.append(part)
+            return y
         cands = {"miopen": lambda: F.conv2d(x, weight), "gemm": lambda: torch.mm(x2, w2.t())}
         if x.dtype == torch.bfloat16 and _ours_ok("fwd", M, Ci, Co):
             from ._native import native
@@ -226,14 +237,27 @@ class _Conv1x1Fn(torch.autograd.Function):
         x, weight = ctx.saved_tensors
         N, Ci, H, W = x.shape
         Co = weight.shape[0]
+        none7 = (None,) * 5
         if gy is None:  # the consuming BatchNorm handed its input gradient over (or there is none)
             d = ctx.bwd_link.take() if ctx.bwd_link is not None else None
             if d is None:
-                return None, None, None, None, None, None
+                return (None, None) + none7
             r = _bwd_fused(ctx, d, x, weight)
             if r is not None:
-                return r[0], r[1], None, None, None, None
+                return (r[0], r[1]) + none7
             gy = d.materialize()
+        if ctx.dre is not None:  # fallback: materialise the deferred operand and its ReLU bits
+            xa, bits = ctx.dre.materialize_parts()
+            ctx.dre.mask.copy_(bits)
+            r = _Conv1x1Fn._backward_dense(ctx, gy, xa, weight)
+            return r + (None,) * 5
+        return _Conv1x1Fn._backward_dense(ctx, gy, x, weight) + (None,) * 5
+
+    @staticmethod
+    def _backward_dense(ctx, gy, x, weight):
+        """(dx, dw) from a dense output gradient (the library / our GEMM paths)."""
+        N, Ci, H, W = x.shape
+        Co = weight.shape[0]
         gy = gy.contiguous(memory_format=torch.channels_last)
         x2, g2, w2 = _nhwc2d(x), _nhwc2d(gy), weight.reshape(Co, Ci)
         M = x2.shape[0]
@@ -331,7 +355,7 @@ class _Conv1x1Fn(torch.autograd.Function):
             else:
                 wfn = lambda: conv_bwd([False, True, False])[1]  # noqa: E731
             dw = wfn()
-        return dx, dw, None, None, None, None
+        return dx, dw
 
 
 def _bwd_fused(ctx, d, x, weight):
@@ -344,8 +368,12 @@ def _bwd_fused(ctx, d, x, weight):
         return None
     from ._native import native
     gs = ctx.gsrc if (ctx.gsrc is not None and ctx.gsrc.ready()) else None
+    dre = ctx.dre
+    if dre is not None and gs is None:
+        return None  # the recompute mode needs bn2's input / mean (its GradStatsSource)
     r = native().conv1x1_bwd_fused(d.dy.contiguous(memory_format=torch.channels_last), d.x, d.mask, d.mean, d.coef,
-                                   weight, x, gs.x if gs else None, gs.mask if gs else None, gs.mean if gs else None)
+                                   weight, x, gs.x if gs else None, gs.mask if gs else None, gs.mean if gs else None,
+                                   dre.ab if dre is not None else None)
     if not r:
         return None
     dx, dw, part = r
@@ -781,7 +809,17 @@ class Conv1x1(nn.Conv2d):
         """``res_link``: a ``ResidualGradLink`` whose gradient (the other branch's gradient of
         ``x``) meets this conv's input gradient; requires one of the GEMM paths. ``bwd_link``: a
         ``BNGradLink`` through which the BatchNorm consuming the output may hand over its input
-        gradient in deferred form (stride-1 GEMM path only; check ``fused_bwd_ok``)."""
+        gradient in deferred form (stride-1 GEMM path only; check ``fused_bwd_ok``). ``x`` may be a
+        ``DeferredReLUBN`` (bn2 -> conv3 with the fused backward): relu(a x + b) read on load."""
+        from .batchnorm import DeferredReLUBN
+        if isinstance(x, DeferredReLUBN):
+            assert bwd_link is not None and res_link is None and self.gemm_eligible(x.raw), \
+                "a deferred BatchNorm input needs the fused-backward GEMM path"
+            holder = [] if (self.emit_bn_stats and SW.conv_bn_stats) else None
+            y = _Conv1x1Fn.apply(x.raw, self.weight, None, holder, x.gsrc, bwd_link, x)
+            if holder:
+                y._pdt_bn_stats = BNStats(holder[0], y._version)
+            return y
         if self.gemm_eligible(x):
             holder = [] if (self.emit_bn_stats and self.training and torch.is_grad_enabled()
                             and SW.conv_bn_stats) else None

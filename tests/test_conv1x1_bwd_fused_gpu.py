@@ -141,9 +141,12 @@ def _grads(seed=0):
     return {n: p.grad.float().clone() for n, p in m.named_parameters()}
 
 
-def test_resnet50_grads_fused_vs_unfused(switch):
-    """The whole model's gradients with the fused conv3 + bn3 backward (layer 1) against the unfused
-    kernel chain: same math, different rounding points (dz is rounded once, in LDS)."""
+@pytest.mark.parametrize("defer", ["0", "1"])
+def test_resnet50_grads_fused_vs_unfused(switch, defer):
+    """The whole model's gradients with the fused conv3 + bn3 backward (layers 1-2) against the unfused
+    kernel chain: same math, different rounding points (dz is rounded once, in LDS). Through 50
+    random-init layers at batch 8 rounding differences grow toward the stem (the stem BN sees them
+    amplified most: ~8 % there), so this is a median / max check; the per-block check is below."""
     from pytorch_distributed_training_example_amd.ops import conv as conv_ops
     calls = []
     orig = conv_ops._bwd_fused
@@ -155,6 +158,7 @@ def test_resnet50_grads_fused_vs_unfused(switch):
     conv_ops._bwd_fused = spy
     try:
         switch("PDT_BWD_FUSED", "1")
+        switch("PDT_BN2_DEFER", defer)
         ga = _grads()
     finally:
         conv_ops._bwd_fused = orig
@@ -162,7 +166,105 @@ def test_resnet50_grads_fused_vs_unfused(switch):
     switch("PDT_BWD_FUSED", "0")
     gb = _grads()
     assert ga.keys() == gb.keys()
-    for n in ga:
-        a, b = ga[n], gb[n]
-        rel = (a - b).norm() / b.norm().clamp_min(1e-12)
-        assert rel < 2e-2, (n, float(rel))
+    rel = torch.tensor([float((ga[n] - gb[n]).norm() / gb[n].norm().clamp_min(1e-12)) for n in ga])
+    assert rel.median() < 1e-2 and rel.max() < 0.15, (float(rel.median()), float(rel.max()))
+
+
+@pytest.mark.parametrize("defer", ["0", "1"])
+@pytest.mark.parametrize("layer,block", [(1, 1), (1, 0), (2, 2)])
+def test_bottleneck_block_grads_fused_vs_unfused(switch, layer, block, defer):
+    """One bottleneck (identity or downsample) in isolation, the same upstream gradient: the output,
+    every parameter gradient and the input gradient with the fused conv3 + bn3 backward (and, defer=1,
+    bn2's apply deferred into conv3: ATR forward + RECOMP backward) against the unfused chain."""
+    from pytorch_distributed_training_example_amd.models import get_model
+    from pytorch_distributed_training_example_amd.models.precision import to_bf16_mixed
+    torch.manual_seed(0)
+    net = to_bf16_mixed(get_model("resnet50").cuda().to(memory_format=torch.channels_last))
+    blk = getattr(net, f"layer{layer}")[block]
+    cin = blk.conv1.in_channels
+    hw = 56 if layer == 1 else 28
+    if block == 0 and layer > 1:
+        hw *= 2
+    g = torch.Generator(device="cuda").manual_seed(layer * 10 + block)
+    x0 = torch.randn(4, cin, hw, hw, device="cuda", generator=g).relu().bfloat16()
+    x0 = x0.contiguous(memory_format=torch.channels_last)
+
+    from pytorch_distributed_training_example_amd.ops import batchnorm as bn_ops
+    seen = []
+    orig = bn_ops.DeferredReLUBN.__init__
+
+    def spy(self, *a):
+        seen.append(1)
+        orig(self, *a)
+
+    def run(flag):
+        switch("PDT_BWD_FUSED", flag)
+        switch("PDT_BN2_DEFER", defer)
+        blk.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_(True)
+        y = blk(x)
+        gy = torch.randn(y.shape, device="cuda", generator=torch.Generator(device="cuda").manual_seed(5)).bfloat16()
+        y.backward(gy.contiguous(memory_format=torch.channels_last))
+        return [y.detach().float(), x.grad.float()] + [p.grad.float().clone() for p in blk.parameters()]
+    bn_ops.DeferredReLUBN.__init__ = spy
+    try:
+        a = run("1")
+    finally:
+        bn_ops.DeferredReLUBN.__init__ = orig
+    assert len(seen) == int(defer)
+    b = run("0")
+    for i, (u, v) in enumerate(zip(a, b)):
+        rel = float((u - v).norm() / v.norm().clamp_min(1e-12))
+        assert rel < (1e-3 if i == 0 else 2e-2), (i, rel)
+
+
+@pytest.mark.parametrize("C4,CW", [(256, 64), (512, 128)])
+def test_fused_recompute_matches_fp32(C4, CW):
+    """RECOMP: bn2's apply deferred to the forward — xa = relu(a xb + b) is formed in the kernel (never
+    read) and bn2's ReLU bits are computed and written by it."""
+    N, H, W = 2, 17, 19
+    M = N * H * W
+    g = torch.Generator(device="cuda").manual_seed(7 + C4)
+    r = lambda *s: torch.randn(*s, device="cuda", generator=g)  # noqa: E731
+    dy, z = r(M, C4).bfloat16(), r(M, C4).bfloat16()
+    m3 = torch.rand(M * C4, device="cuda", generator=g) > 0.4
+    mean = r(C4) * 0.1
+    coef = torch.stack([r(C4).abs() + 0.5, r(C4) * 0.01, r(C4) * 0.01]).contiguous()
+    w = (r(C4, CW) / 16).bfloat16().view(C4, CW, 1, 1)
+    xb = r(M, CW).bfloat16()
+    xcoef = torch.stack([r(CW).abs() + 0.2, r(CW) * 0.3]).contiguous()
+    meanb = r(CW) * 0.1
+    mask_out = torch.full((M * CW // 8,), 0xAA, dtype=torch.uint8, device="cuda")
+    xa_shape = torch.empty(N, CW, H, W, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    dxa, dw, part = _native().conv1x1_bwd_fused(_nhwc(dy, N, H, W), _nhwc(z, N, H, W), _bits(m3), mean, coef, w,
+                                               xa_shape, _nhwc(xb, N, H, W), mask_out, meanb, xcoef)
+    t = xb.float() * xcoef[0] + xcoef[1]
+    xa = t.clamp_min(0).bfloat16().float()
+    mb = (t > 0).view(-1)
+    assert torch.equal(mask_out, _bits(mb))
+    gm = torch.where(m3.view(M, C4), dy.float(), 0.0)
+    dz = (coef[0] * gm + coef[1] * (z.float() - mean) + coef[2]).bfloat16().float()
+    d2 = dxa.permute(0, 2, 3, 1).reshape(M, CW).float()
+    torch.testing.assert_close(d2, dz @ w.view(C4, CW).float(), rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(dw.view(C4, CW).float(), dz.t() @ xa, rtol=2e-2, atol=5e-2)
+    gb = torch.where(mb.view(M, CW), d2, 0.0)
+    torch.testing.assert_close(part[0].sum(0), gb.sum(0), rtol=1e-3, atol=1e-2)
+    torch.testing.assert_close(part[1].sum(0), (gb * (xb.float() - meanb)).sum(0), rtol=1e-3, atol=1e-2)
+
+
+@pytest.mark.parametrize("K,N", [(64, 256), (128, 512), (64, 64)])
+def test_conv1x1_gemm_deferred_bn_input(K, N):
+    """conv1x1.hip ATR: the A operand is a BatchNorm input; relu(a x + b) is applied on load (with the
+    statistics epilogue on): same result as applying it first, rows past a 256-row tile included."""
+    M = 1000
+    g = torch.Generator(device="cuda").manual_seed(K + N)
+    x = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).bfloat16()
+    ac = torch.stack([torch.rand(K, device="cuda", generator=g) + 0.5, torch.randn(K, device="cuda", generator=g)])
+    y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    part = _native().conv1x1_gemm(x, w, y, False, True, a_coef=ac.contiguous())
+    xa = (x.float() * ac[0] + ac[1]).clamp_min(0).bfloat16()
+    y2 = torch.empty_like(y)
+    part2 = _native().conv1x1_gemm(xa, w, y2, False, True)
+    assert torch.equal(y, y2)
+    assert torch.equal(part, part2)

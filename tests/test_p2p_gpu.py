@@ -236,3 +236,47 @@ def test_pdt_p2p_backend_gpu():
     for t, a, c, calls in out:
         assert torch.equal(t, torch.full((4096,), 3.0)) and torch.equal(a, torch.full((1024,), 1.5))
         assert torch.equal(c, torch.full((16,), 1.0)) and calls == 2
+
+
+def _overlap_worker(rank, world):
+    """Backward/communication overlap, measured: the P2P all-reduce of the FIRST bucket (the last
+    layers' gradients) must complete on the GPU before backward's compute ends — i.e. it ran under
+    backward, not after it (the reference all-reduces only after backward, train.py:49-50)."""
+    from pytorch_distributed_training_example_amd.parallel import DistributedDataParallel
+    from pytorch_distributed_training_example_amd.parallel.p2p import (P2PAllReduce, P2PHookState,
+                                                                        p2p_allreduce_hook)
+    torch.manual_seed(0)
+    layers = []
+    for _ in range(12):
+        layers += [torch.nn.Linear(1024, 1024), torch.nn.ReLU()]
+    model = torch.nn.Sequential(*layers).cuda()
+    ddp = DistributedDataParallel(model, bucket_cap_mb=4, first_bucket_mb=4)
+    state = P2PHookState(P2PAllReduce(capacity_bytes=8 << 20))
+    done = []
+
+    def hook(st, bucket):
+        fut = p2p_allreduce_hook(st, bucket)
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(st.stream)  # completion of this bucket's P2P kernel
+        done.append(ev)
+        return fut
+    ddp.register_comm_hook(state, hook)
+    ddp.enable_comm_timing(True)
+    x = torch.randn(4096, 1024, device="cuda")
+    for _ in range(3):
+        done.clear()
+        ddp.zero_grad(set_to_none=True)
+        ddp(x).square().mean().backward()
+    torch.cuda.synchronize()
+    state.p2p.check()
+    end_of_compute = ddp._comm_events[-1][0]  # recorded when backward's compute was all issued
+    lead_ms = done[0].elapsed_time(end_of_compute)  # > 0: bucket 0 finished before compute ended
+    return len(done), lead_ms, ddp.comm_exposed_ms()
+
+
+def test_first_bucket_allreduce_overlaps_backward():
+    out = run_ranks(_overlap_worker, 2, use_gpu=True)
+    for nb, lead_ms, exposed in out:
+        assert nb >= 3, nb
+        assert lead_ms > 0.0, f"bucket 0's all-reduce ended {-lead_ms:.3f} ms AFTER backward's compute"
+        assert exposed is not None and exposed >= 0.0
