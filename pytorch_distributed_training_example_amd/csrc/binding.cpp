@@ -1029,8 +1029,8 @@ std::vector<Tensor> conv3x3s1_fwd_bnbwd(Tensor x, Tensor w, Tensor bn_x, c10::op
 
 // ----------------------------------------------------------------------------- 3x3 conv (stride 2, pad 1)
 // y = conv2d(x, w, stride=2, padding=1), channels_last bf16 (csrc/kernels/conv3x3_s2.hip); stats: also
-// the per-tile BatchNorm statistics of y -> {y, part [2, T, Co]}. Ci, Co % 128 == 0 (checked by caller:
-// returns {} for a shape the kernel does not take).
+// the per-tile BatchNorm statistics of y -> {y, part [2, T, Co]}. Ci % 64, Co % 128 == 0 (returns {} for
+// a shape the kernel does not take).
 std::vector<Tensor> conv3x3s2_fwd(Tensor x, Tensor w, bool stats) {
   check_nhwc_bf16(x, "x");
   TORCH_CHECK(w.dim() == 4 && w.size(2) == 3 && w.size(3) == 3 && w.size(1) == x.size(1) &&

@@ -235,9 +235,10 @@ int launch(const uint16_t* x, const uint16_t* w, uint16_t* y, float* part, const
 
 inline int tiles_of(int64_t M) { return (int)((M + kBM - 1) / kBM); }
 
-// shape limits shared by both directions: 32-bit element offsets, channel tiling
-inline int check_shape(int N, int H, int W, int Ci, int Co) {
-  if (N < 1 || H < 2 || W < 2 || Ci % kBN != 0 || Co % kBN != 0) return -1;
+// shape limits: 32-bit element offsets; the GEMM's N (output channels of this direction) tiles by kBN,
+// its K (gathered channels) by 64 (two kBK steps per tap)
+inline int check_shape(int N, int H, int W, int Ci, int Co, int kdim, int ndim) {
+  if (N < 1 || H < 2 || W < 2 || kdim % 64 != 0 || ndim % kBN != 0) return -1;
   if ((int64_t)N * H * W * (Ci > Co ? Ci : Co) >= (int64_t)1 << 31 || (int64_t)Co * 9 * Ci >= (int64_t)1 << 31)
     return -2;
   return 0;
@@ -257,10 +258,10 @@ int pdt_conv3x3s2_dgrad_tiles(int N, int H, int W) {
 
 // y[N,Ho,Wo,Co] = conv2d(x[N,H,W,Ci], w[Co,3,3,Ci], stride 2, padding 1), Ho = (H-1)/2+1 (NHWC bf16).
 // part (or null): per-256-pixel-tile BatchNorm statistics of y, [2][ceil(N*Ho*Wo/256)][Co] fp32.
-// Ci % 128 == 0, Co % 128 == 0. Returns 0, or < 0 for an unsupported shape (caller falls back).
+// Ci % 64 == 0, Co % 128 == 0. Returns 0, or < 0 for an unsupported shape (caller falls back).
 int pdt_conv3x3s2_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, float* part, int N, int H, int W, int Ci,
                       int Co, hipStream_t s) {
-  const int rc = check_shape(N, H, W, Ci, Co);
+  const int rc = check_shape(N, H, W, Ci, Co, Ci, Co);
   if (rc) return rc;
   Geo g{};
   g.N = N; g.Ho = (H - 1) / 2 + 1; g.Wo = (W - 1) / 2 + 1;
@@ -280,10 +281,11 @@ int pdt_conv3x3s2_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, float* 
 // wf[Ci,3,3,Co] (pdt_conv3x3_flip_weights). bn_x / bn_mask / bn_mean / bn_part (all null = off): dx is
 // the gradient at the output of a BatchNorm with input bn_x [N,H,W,Ci], ReLU mask bn_mask (or null)
 // and mean bn_mean; bn_part [2][pdt_conv3x3s2_dgrad_tiles()][Ci] receives its backward partials.
+// Ci % 128 == 0, Co % 64 == 0.
 int pdt_conv3x3s2_dgrad(const uint16_t* dy, const uint16_t* wf, uint16_t* dx, const uint16_t* bn_x,
                         const uint8_t* bn_mask, const float* bn_mean, float* bn_part, int N, int H, int W, int Ci,
                         int Co, hipStream_t s) {
-  const int rc = check_shape(N, H, W, Ci, Co);
+  const int rc = check_shape(N, H, W, Ci, Co, Co, Ci);
   if (rc) return rc;
   if (bn_part && (!bn_x || !bn_mean)) return -1;
   Geo g{};

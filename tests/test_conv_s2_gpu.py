@@ -13,7 +13,8 @@ def _rel(a, b):
 
 
 @pytest.mark.parametrize("N,C_in,C_out,H,W", [(2, 128, 128, 56, 56), (3, 256, 256, 28, 28), (4, 512, 512, 14, 14),
-                                              (2, 128, 256, 13, 11), (1, 256, 128, 2, 2), (2, 128, 128, 9, 30)])
+                                              (2, 128, 256, 13, 11), (1, 256, 128, 2, 2), (2, 128, 128, 9, 30),
+                                              (3, 64, 128, 24, 24)])
 def test_conv3x3s2_ours_matches_fp32(N, C_in, C_out, H, W, switch):
     from pytorch_distributed_training_example_amd.ops._native import native
     from pytorch_distributed_training_example_amd.ops.conv import SplitConv2d, conv3x3s2_eligible
@@ -39,7 +40,11 @@ def test_conv3x3s2_ours_matches_fp32(N, C_in, C_out, H, W, switch):
     # forward and data gradient came from our kernels, bit for bit
     gyc = gy.contiguous(memory_format=torch.channels_last)
     assert torch.equal(native().conv3x3s2_fwd(x.detach(), m.weight, False)[0], y)
-    assert torch.equal(native().conv3x3s2_dgrad(gyc, native().conv3x3_flip(m.weight), H, W)[0], x.grad)
+    r = native().conv3x3s2_dgrad(gyc, native().conv3x3_flip(m.weight), H, W)
+    if C_in % 128 == 0:
+        assert torch.equal(r[0], x.grad)
+    else:  # (ResNet-18 layer2) the data gradient's GEMM N = C_in does not tile: library fallback
+        assert not r
     dw = native().conv3x3s2_wgrad(x.detach(), gyc)
     if (H, W) != (13, 11) and (H, W) != (9, 30):  # shapes the S = 2 weight-gradient kernel is sized for
         assert dw is not None and torch.equal(dw, m.weight.grad), "stride-2 weight gradient not on our kernel"

@@ -52,12 +52,16 @@ def _worker(rank, world, model_name, reduce_dtype):
         return all(sa == sb for sa, sb, n in zip(a.stride(), b.stride(), a.shape) if n > 1)
     views_ok = all(p.grad.data_ptr() == v.data_ptr() and same_layout(p.grad, p)
                    for p, v in ddp.parameters_and_views())
-    # reference: the two ranks' half-batches one after the other, loss averaged
-    ref.zero_grad(set_to_none=True)
+    # reference: each rank's half-batch gradient computed on its own (the same kernels a rank runs),
+    # averaged in fp32
+    want = None
     for r in range(world):
+        ref.zero_grad(set_to_none=True)
         xr, yr = _data(r)
-        (cross_entropy(ref(xr), yr) / world).backward()
-    want = [p.grad.float().cpu() for p in ref.parameters()]
+        cross_entropy(ref(xr), yr).backward()
+        g = [p.grad.float().cpu() for p in ref.parameters()]
+        want = g if want is None else [a + b for a, b in zip(want, g)]
+    want = [a / world for a in want]
     return got, want, nbuckets, views_ok
 
 
@@ -72,10 +76,9 @@ def test_ddp_two_ranks_resnet_matches_half_batch_reference(model_name, reduce_dt
             assert torch.equal(a, b), "replicas must hold identical averaged gradients"
     rel = lambda a, b: ((a - b).norm() / (b.norm() + 1e-6)).item()  # noqa: E731
     errs = torch.tensor([rel(a, b) for a, b in zip(g0[1], want0)])
-    # bf16 compute through 50 layers (per-rank BN statistics over tiny late-stage maps amplify
-    # rounding) and a different summation order (bucketed averaging vs two accumulated backward
-    # passes): measured median 1-2 %. The wrong answers are far away: the SUM instead of the mean
-    # is 50 % off and a single rank's gradient 70 %.
-    assert errs.median() < 4e-2 and errs.max() < 0.2, (errs.median(), errs.max())
+    # each rank's local gradient is the reference half-batch gradient (deterministic kernels); the
+    # only difference is the bucket average's rounding to the gradient dtype (<= 1 bf16 ulp). The
+    # wrong answers are far away: the SUM instead of the mean is 50 % off, one rank's gradient ~70 %.
+    assert errs.max() < 1e-2, (errs.median(), errs.max(), int(errs.argmax()))
     sums = torch.tensor([rel(a, 2 * b) for a, b in zip(g0[1], want0)])
     assert sums.median() > 0.3, "averaging check has no power"
