@@ -32,8 +32,14 @@ PDT_FUSED_ADDLN             1            residual add fused into LayerNorm
 PDT_EMBEDDING_NATIVE        1            GPT-2 token/position embedding on our kernels
 PDT_BWD_FUSED               1            bottleneck conv3 + bn3 backward as one kernel (conv1x1_bwd_fused.hip):
                                          bn3's backward apply formed on load, conv3 dgrad + wgrad + bn2 reduction
-PDT_BN2_DEFER               1            with PDT_BWD_FUSED: bn2's apply + ReLU deferred into conv3 (read on load in
-                                         the forward GEMM, recomputed in the fused backward, which writes bn2's mask)
+PDT_BN2_DEFER               0            1: with PDT_BWD_FUSED, bn2's apply + ReLU deferred into conv3 (read on load
+                                         in the forward GEMM, recomputed in the fused backward, which writes bn2's
+                                         mask). Measured -0.2 % (profiles/r4/ab_bn2_defer.md): off
+PDT_BN_APPLY_GEMM_K         0            > 0: a BatchNorm(+residual)+ReLU apply after a 1x1 conv with <= this many
+                                         input channels runs as that conv's GEMM again with the apply epilogue
+                                         (reads the conv input, C/4 channels, instead of its output). 128 measured
+                                         -0.2 % (the GEMM epilogue streams at 3.3 TB/s, the apply pass at 4.5;
+                                         profiles/r4/ab_bn_apply_gemm.md): off
 PDT_LINEAR_EPILOGUE         0            1: Linear forward GEMMs (+bias, MLP fc1+bias+GELU) on our MFMA kernel
                                          (gemm.hip; 0.61-0.94x of tuned hipBLASLt, so off)
 """
@@ -47,7 +53,7 @@ class _Switches:
                  "conv1x1_table", "conv1x1_dump", "conv1x1_s2", "conv3x3", "conv3x3_wgrad", "conv3x3_s2", "conv_stem",
                  "conv_bn_stats", "bn_bwd_stats", "res_masked", "stem_bwd_fused", "stem_bn_wgrad", "wgrad_splitk", "slice_sum",
                  "subsample_native", "linear_splitk", "fused_addln", "embedding_native", "linear_epilogue",
-                 "bwd_fused", "bn2_defer")
+                 "bwd_fused", "bn2_defer", "bn_apply_gemm_k")
 
     def __init__(self):
         self.reload()
@@ -84,7 +90,8 @@ class _Switches:
         self.embedding_native = on("PDT_EMBEDDING_NATIVE")
         self.linear_epilogue = e("PDT_LINEAR_EPILOGUE", "0") == "1"
         self.bwd_fused = on("PDT_BWD_FUSED")
-        self.bn2_defer = on("PDT_BN2_DEFER")
+        self.bn2_defer = on("PDT_BN2_DEFER", "0")
+        self.bn_apply_gemm_k = int(e("PDT_BN_APPLY_GEMM_K", "0"))
         return self
 
 

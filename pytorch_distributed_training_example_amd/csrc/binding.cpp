@@ -132,6 +132,8 @@ int pdt_conv1x1_gemm(const uint16_t* a, const uint16_t* b, uint16_t* y, const ui
                      float* part, int M, int K, int N, const uint16_t* bn_x, const uint8_t* bn_mask,
                      const float* bn_mean, float* bn_part, int c_s, int c_H, int c_W, const float* acoef,
                      hipStream_t s);
+int pdt_conv1x1_gemm_apply(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t* res, const float* ab,
+                           const float* rab, uint8_t* mask, int M, int K, int N, const float* acoef, hipStream_t s);
 int pdt_maxpool_bn_parts(int N, int H);
 int pdt_maxpool3s2_bwd_bn(const uint16_t* dy, const uint8_t* code, uint16_t* dz, int N, int H, int W, int C,
                           const uint16_t* x, const float* gamma, const float* mean, const float* invstd, uint16_t* dx,
@@ -883,6 +885,44 @@ c10::optional<Tensor> conv1x1_gemm(Tensor a, Tensor b, Tensor out, bool acc, boo
                                   stream());
   TORCH_CHECK(rc == 0, "pdt_conv1x1_gemm failed: ", rc);
   return part;
+}
+
+// A BatchNorm (+ residual) + ReLU applied in the epilogue of the 1x1-conv GEMM that produced its input
+// (csrc/kernels/conv1x1.hip APPLY): y = relu(ab[0] * (a b^T) + ab[1] + r), r = res or rab[0] res + rab[1].
+// a [M, K], b [N, K] bf16 row-major; res: the residual (bf16, M * N elements, channels_last when 4-D; y gets
+// its shape / layout); ab, rab: fp32 [2, N]; a_coef: fp32 [2, K] (A is a deferred BatchNorm input, ATR).
+// Returns {y, mask uint8 [M * N / 8]}.
+std::vector<Tensor> conv1x1_gemm_apply(Tensor a, Tensor b, Tensor res, Tensor ab, c10::optional<Tensor> rab,
+                                       c10::optional<Tensor> a_coef) {
+  check_cuda(a, "a");
+  check_cuda(b, "b");
+  check_cuda(res, "res");
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.size(1) == b.size(1) && a.scalar_type() == at::kBFloat16 &&
+                  b.scalar_type() == at::kBFloat16 && a.is_contiguous() && b.is_contiguous(),
+              "conv1x1_gemm_apply: a [M, K], b [N, K] contiguous bf16");
+  const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
+  const auto fmt = res.dim() == 4 ? at::MemoryFormat::ChannelsLast : at::MemoryFormat::Contiguous;
+  TORCH_CHECK(res.scalar_type() == at::kBFloat16 && res.numel() == M * N && res.is_contiguous(fmt) &&
+                  (res.dim() != 4 || res.size(1) == N),
+              "conv1x1_gemm_apply: res must be [M, N] bf16 (channels_last when 4-D)");
+  auto f32 = [&](const Tensor& t, int64_t n, const char* what) {
+    check_cuda(t, what);
+    TORCH_CHECK(t.scalar_type() == at::kFloat && t.is_contiguous() && t.numel() == n, "conv1x1_gemm_apply: ", what,
+                " must be fp32 contiguous with ", n, " elements");
+    return t.data_ptr<float>();
+  };
+  const float* abp = f32(ab, 2 * N, "ab");
+  const float* rabp = (rab.has_value() && rab->defined()) ? f32(*rab, 2 * N, "rab") : nullptr;
+  const float* acp = (a_coef.has_value() && a_coef->defined()) ? f32(*a_coef, 2 * K, "a_coef") : nullptr;
+  auto y = at::empty_like(res, res.options(), fmt);
+  auto mask = at::empty({M * N / 8}, res.options().dtype(at::kByte));
+  const int rc = pdt_conv1x1_gemm_apply(reinterpret_cast<const uint16_t*>(a.data_ptr()),
+                                        reinterpret_cast<const uint16_t*>(b.data_ptr()),
+                                        reinterpret_cast<uint16_t*>(y.data_ptr()),
+                                        reinterpret_cast<const uint16_t*>(res.data_ptr()), abp, rabp,
+                                        mask.data_ptr<uint8_t>(), (int)M, (int)K, (int)N, acp, stream());
+  TORCH_CHECK(rc == 0, "pdt_conv1x1_gemm_apply failed: ", rc);
+  return {y, mask};
 }
 
 // Weight gradient of a stride-1 1x1 conv (csrc/kernels/conv1x1_wgrad.hip): dw [Co, Ci] bf16 =
@@ -1729,6 +1769,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("c_in") = py::none(), py::arg("c_mask") = py::none(), py::arg("bn_x") = py::none(),
         py::arg("bn_mask") = py::none(), py::arg("bn_mean") = py::none(), py::arg("c_stride") = 0,
         py::arg("c_H") = 0, py::arg("c_W") = 0, py::arg("a_coef") = py::none());
+  m.def("conv1x1_gemm_apply", &conv1x1_gemm_apply, py::arg("a"), py::arg("b"), py::arg("res"), py::arg("ab"),
+        py::arg("rab") = py::none(), py::arg("a_coef") = py::none());
   m.def("bn_bwd_train_tiles", &bn_bwd_train_tiles);
   m.def("maxpool3s2_bwd_bn", &maxpool3s2_bwd_bn);
   m.def("maxpool3s2_bwd_bn_coef", &maxpool3s2_bwd_bn_coef);

@@ -33,6 +33,13 @@
 //                 fma and rounding as its apply pass) in registers after the fragment read, so the
 //                 BatchNorm's output is never written or read (ResNet bottleneck bn2 -> conv3).
 //
+//   APPLY (forward only): the GEMM output z is the INPUT of a BatchNorm whose statistics are already
+//                 known (the same GEMM ran once before, with STATS, ops/conv.py): the epilogue writes that
+//                 BatchNorm's output relu(a z + b + r) and its ReLU bits instead of z, with r the residual
+//                 (or ra r + rb, a deferred shortcut BatchNorm). A ResNet bottleneck's bn3 apply pass then
+//                 reads conv3's input (C/4 channels) instead of z (C channels): 0.75 of a tensor less
+//                 traffic per block; z is still stored by the first run for the backward.
+//
 //   BSTATS (data grad only): the output Y is the gradient dy at a BatchNorm's output, and that
 //                 BatchNorm's backward reduction is taken here instead of in a separate pass over
 //                 (dy, x): per 256-pixel tile, per channel, sum(dz) and sum(dz * (xb - mean)) with
@@ -104,12 +111,21 @@ struct CGeom {
   int s, H, W, Hs, Ws;
 };
 
+// APPLY: the BatchNorm applied in the epilogue. ab = [2][N] (a, then b); rab = [2][N] (ra, rb) or null
+// (plain residual); the residual itself comes in Cin; mask [M * N / 8] receives the ReLU bits.
+struct ApArgs {
+  const float* ab;
+  const float* rab;
+  uint8_t* mask;
+};
+
 // NT: streaming (non-temporal) output stores. ATR: acoef = [2][K] fp32 (a, then b), see the header.
-template <class Cf, bool ACC, bool STATS, bool NT, bool BSTATS, bool ATR = false>
+template <class Cf, bool ACC, bool STATS, bool NT, bool BSTATS, bool ATR = false, bool APPLY = false>
 __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv1x1_kernel(
     const uint16_t* __restrict__ A, const uint16_t* __restrict__ B, uint16_t* Y, const uint16_t* Cin,
     const uint8_t* __restrict__ Cmask, float* __restrict__ part, int M, int K, int N, BnSrc bs, CGeom cg,
-    const float* __restrict__ acoef) {
+    const float* __restrict__ acoef, ApArgs ap) {
+  static_assert(!(APPLY && (ACC || STATS || BSTATS)), "APPLY is a forward epilogue of its own");
   constexpr int BM = Cf::BM, BN = Cf::BN;
   constexpr int WROWS = BM / Cf::WM, WCOLS = BN / Cf::WN;
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -235,6 +251,17 @@ __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv1x1_kernel(
   constexpr int kChunks = BN / 8;
   static_assert(Cf::kThreads % kChunks == 0, "a thread keeps one 8-channel chunk");
   float bs1[8], bs2[8], bmu[8];
+  float pa[8], pb[8], pra[8], prb[8];  // APPLY: this thread's 8 channels' coefficients
+  if constexpr (APPLY) {
+    const int c = tid % kChunks;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      pa[k] = ap.ab[n0 + c * 8 + k];
+      pb[k] = ap.ab[N + n0 + c * 8 + k];
+      pra[k] = ap.rab ? ap.rab[n0 + c * 8 + k] : 1.f;
+      prb[k] = ap.rab ? ap.rab[N + n0 + c * 8 + k] : 0.f;
+    }
+  }
   if constexpr (BSTATS) {
     const int c = tid % kChunks;
     *reinterpret_cast<float4*>(bmu) = *reinterpret_cast<const float4*>(bs.mean + n0 + c * 8);
@@ -268,6 +295,7 @@ __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv1x1_kernel(
       xbv[it] = *reinterpret_cast<const uint4*>(bs.x + off);
       if (bs.mask) bmkv[it] = bs.mask[off >> 3];
     }
+    if constexpr (APPLY) cv[it] = *reinterpret_cast<const uint4*>(Cin + off);  // the residual
     if constexpr (ACC) {
       cmk[it] = Cmask ? Cmask[off >> 3] : 0xffu;  // C = Cin * mask: a ReLU's masked gradient
       if (cg.s) {  // compact strided source
@@ -307,6 +335,28 @@ __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv1x1_kernel(
       v.z = (uint32_t)f2bf(a[4]) | ((uint32_t)f2bf(a[5]) << 16);
       v.w = (uint32_t)f2bf(a[6]) | ((uint32_t)f2bf(a[7]) << 16);
     }
+    if constexpr (APPLY) {  // relu(a z + b + r): the same fp32 operations as batchnorm.hip bn_apply_kernel
+      float z[8], r[8];
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w}, rw[4] = {cv[it].x, cv[it].y, cv[it].z, cv[it].w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        z[2 * k] = __uint_as_float(w[k] << 16); z[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+        r[2 * k] = __uint_as_float(rw[k] << 16); r[2 * k + 1] = __uint_as_float(rw[k] & 0xffff0000u);
+      }
+      unsigned mb = 0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float t = z[k] * pa[k] + pb[k];
+        t += ap.rab ? r[k] * pra[k] + prb[k] : r[k];
+        mb |= (t > 0.f ? 1u : 0u) << k;
+        z[k] = t > 0.f ? t : 0.f;
+      }
+      v.x = (uint32_t)f2bf(z[0]) | ((uint32_t)f2bf(z[1]) << 16);
+      v.y = (uint32_t)f2bf(z[2]) | ((uint32_t)f2bf(z[3]) << 16);
+      v.z = (uint32_t)f2bf(z[4]) | ((uint32_t)f2bf(z[5]) << 16);
+      v.w = (uint32_t)f2bf(z[6]) | ((uint32_t)f2bf(z[7]) << 16);
+      ap.mask[off >> 3] = (uint8_t)mb;
+    }
     if constexpr (BSTATS) bn_bwd_accum8(v, xbv[it], bmkv[it], bmu, bs1, bs2);
     if constexpr (NT) {
       const u32x4 t = {v.x, v.y, v.z, v.w};
@@ -323,13 +373,14 @@ __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv1x1_kernel(
 
 constexpr int kMaxATRK = 512;  // ATR coefficient table: [2][K] floats past kLds
 
-template <class Cf, bool ACC, bool STATS, bool NT, bool BSTATS, bool ATR = false>
+template <class Cf, bool ACC, bool STATS, bool NT, bool BSTATS, bool ATR = false, bool APPLY = false>
 int launch_nt(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t* c, const uint8_t* cm, float* part,
-              int M, int K, int N, const BnSrc& bs, const CGeom& cg, hipStream_t s, const float* acoef = nullptr) {
+              int M, int K, int N, const BnSrc& bs, const CGeom& cg, hipStream_t s, const float* acoef = nullptr,
+              const ApArgs& ap = ApArgs{}) {
   static bool attr = false;
   constexpr int kMaxLds = Cf::kLds + (ATR ? 2 * kMaxATRK * 4 : 0);
   if (!attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&conv1x1_kernel<Cf, ACC, STATS, NT, BSTATS, ATR>),
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&conv1x1_kernel<Cf, ACC, STATS, NT, BSTATS, ATR, APPLY>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, kMaxLds) != hipSuccess)
       return -3;
     attr = true;
@@ -337,8 +388,8 @@ int launch_nt(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t*
   if (ATR && K > kMaxATRK) return -1;
   const int lds = Cf::kLds + (ATR ? 2 * K * 4 : 0);
   const int64_t grid = (int64_t)(M + Cf::BM - 1) / Cf::BM * (N / Cf::BN);
-  hipLaunchKernelGGL((conv1x1_kernel<Cf, ACC, STATS, NT, BSTATS, ATR>), dim3((unsigned)grid), dim3(Cf::kThreads), lds,
-                     s, a, b, y, c, cm, part, M, K, N, bs, cg, acoef);
+  hipLaunchKernelGGL((conv1x1_kernel<Cf, ACC, STATS, NT, BSTATS, ATR, APPLY>), dim3((unsigned)grid),
+                     dim3(Cf::kThreads), lds, s, a, b, y, c, cm, part, M, K, N, bs, cg, acoef, ap);
   return 0;
 }
 
@@ -401,6 +452,24 @@ int pdt_conv1x1_gemm(const uint16_t* a, const uint16_t* b, uint16_t* y, const ui
   }
   if (N % 128 == 0) return dispatch<GWide>(a, b, y, c, cm, part, M, K, N, bs, cg, s, acoef);
   return dispatch<GNarrow>(a, b, y, c, cm, part, M, K, N, bs, cg, s, acoef);
+}
+
+// APPLY: y[M,N] = relu(ab[0] * (a b^T) + ab[1] + r) with r = res (rab null) or rab[0] res + rab[1], and its
+// ReLU bits -> mask [M * N / 8]; acoef as in pdt_conv1x1_gemm (ATR). The GEMM must be the one whose
+// statistics gave ab (same a, b, acoef: the z values are recomputed bit for bit).
+int pdt_conv1x1_gemm_apply(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t* res, const float* ab,
+                           const float* rab, uint8_t* mask, int M, int K, int N, const float* acoef, hipStream_t s) {
+  if (M < 1 || K < 32 || K % 32 != 0 || N < 64 || N % 64 != 0 || !res || !ab || !mask) return -1;
+  if ((int64_t)M * (K > N ? K : N) >= ((int64_t)1 << 31) || (int64_t)N * K >= ((int64_t)1 << 31)) return -2;
+  const BnSrc bs{};
+  const CGeom cg{0, 1, 1, 1, 1};
+  const ApArgs ap{ab, rab, mask};
+  if (N % 128 == 0) {
+    if (acoef) return launch_nt<GWide, false, false, false, false, true, true>(a, b, y, res, nullptr, nullptr, M, K, N, bs, cg, s, acoef, ap);
+    return launch_nt<GWide, false, false, false, false, false, true>(a, b, y, res, nullptr, nullptr, M, K, N, bs, cg, s, acoef, ap);
+  }
+  if (acoef) return launch_nt<GNarrow, false, false, false, false, true, true>(a, b, y, res, nullptr, nullptr, M, K, N, bs, cg, s, acoef, ap);
+  return launch_nt<GNarrow, false, false, false, false, false, true>(a, b, y, res, nullptr, nullptr, M, K, N, bs, cg, s, acoef, ap);
 }
 
 }  // extern "C"

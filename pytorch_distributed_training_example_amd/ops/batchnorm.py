@@ -152,7 +152,8 @@ class BNGradLink:
 class _BNTrainFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, residual, weight, bias, running_mean, running_var, momentum, eps, relu, link=None,
-                part=None, gsrc=None, glink=None, res_ab=None, defer=None, out_link=None, defer_relu=None):
+                part=None, gsrc=None, glink=None, res_ab=None, defer=None, out_link=None, defer_relu=None,
+                gemm=None):
         C = native()
         ctx.defer_relu = defer_relu
         if defer_relu is not None:  # stats only; the consumer conv applies relu(a x + b) (DeferredReLUBN)
@@ -175,6 +176,13 @@ class _BNTrainFn(torch.autograd.Function):
                                                         momentum, eps, False, apply=False)
             defer.append(ab)
             y, mask = x.view_as(x), None
+        elif gemm is not None and part is not None and residual is not None and relu:
+            # x came from our 1x1-conv GEMM (ops/conv.py GemmSource): the apply runs as that GEMM again with
+            # the apply epilogue, reading the conv's input instead of x (conv1x1.hip APPLY)
+            _, _, mean, invstd, ab = C.bn_fwd_train_tiles(x, part, None, weight, bias, running_mean, running_var,
+                                                          momentum, eps, False, apply=False)
+            a2, w2 = gemm.operands()
+            y, mask = C.conv1x1_gemm_apply(a2, w2, residual, ab, res_ab, gemm.acoef)
         elif part is not None:  # statistics from the producing conv's epilogue: no reduce pass over x
             y, mask, mean, invstd = C.bn_fwd_train_tiles(x, part, residual, weight, bias, running_mean,
                                                          running_var, momentum, eps, relu, res_ab=res_ab)
@@ -207,7 +215,7 @@ class _BNTrainFn(torch.autograd.Function):
         x, mask, weight, mean, invstd = ctx.saved_tensors
         if ctx.defer_relu is not None:  # the mask was written by the consumer's backward
             mask = ctx.dmask
-        tail = (None,) * 13
+        tail = (None,) * 14
         need_w = ctx.has_weight and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3])
         if dy is None:  # gradient handed over through glink as (dy, mask): a ReLU'd dy of the consumer
             g = ctx.glink.take() if ctx.glink is not None else None
@@ -376,9 +384,11 @@ def batch_norm_act(x, residual, weight, bias, running_mean, running_var, trainin
             if defer is not None:
                 gsrc = None
             dre = [] if (defer_relu_apply and residual is None and relu and x.dim() == 4 and gsrc is not None) else None
+            from .conv import gemm_source_of
+            gemm = gemm_source_of(x) if (relu and residual is not None and part is not None) else None
             y = _BNTrainFn.apply(x, residual, weight, bias, running_mean, running_var,
                                  float(momentum), float(eps), bool(relu), res_link, part, gsrc, grad_link, ab, defer,
-                                 out_link, dre)
+                                 out_link, dre, gemm)
             if defer:
                 return DeferredBNOutput(y, defer[0])
             if dre:

@@ -100,6 +100,31 @@ def _ours_ok(direction: str, M: int, K: int, N: int) -> bool:
             and M * max(K, N) < 2 ** 31 and SW.conv1x1 in ("auto", "ours"))
 
 
+class GemmSource:
+    """How a 1x1 conv output z was computed by our GEMM (input, weight, ATR coefficients): the consuming
+    BatchNorm's apply can run as that GEMM again with the apply epilogue (conv1x1.hip APPLY), reading the
+    conv input instead of z. Valid while z is unmodified (``version``)."""
+
+    __slots__ = ("x", "weight", "acoef", "version")
+
+    def __init__(self, x, weight, acoef, version):
+        self.x, self.weight, self.acoef, self.version = x, weight, acoef, version
+
+    def operands(self):
+        Co, Ci = self.weight.shape[:2]
+        return _nhwc2d(self.x), self.weight.reshape(Co, Ci).contiguous()
+
+
+def gemm_source_of(z: torch.Tensor):
+    g = getattr(z, "_pdt_gemm_src", None)
+    return g if (g is not None and g.version == z._version) else None
+
+
+def _attach_gemm_source(y, x, weight, acoef):
+    if 0 < weight.shape[1] <= SW.bn_apply_gemm_k:
+        y._pdt_gemm_src = GemmSource(x, weight, acoef, y._version)
+
+
 class BNStats:
     """Per-tile BatchNorm statistics of a conv output, computed in the conv's epilogue
     (conv1x1_gemm ``stats``), attached to the output tensor as ``_pdt_bn_stats``; the BatchNorm
@@ -820,6 +845,7 @@ class Conv1x1(nn.Conv2d):
             y = _Conv1x1Fn.apply(x.raw, self.weight, None, holder, x.gsrc, bwd_link, x)
             if holder:
                 y._pdt_bn_stats = BNStats(holder[0], y._version)
+                _attach_gemm_source(y, x.raw, self.weight, x.ab)
             return y
         if self.gemm_eligible(x):
             holder = [] if (self.emit_bn_stats and self.training and torch.is_grad_enabled()
@@ -828,8 +854,9 @@ class Conv1x1(nn.Conv2d):
             y = _Conv1x1Fn.apply(x, self.weight, res_link, holder,
                                  grad_stats_source_of(x) if self.training and torch.is_grad_enabled() else None,
                                  bwd_link)
-            if holder:
+            if holder:  # (our GEMM ran: the statistics came from its epilogue)
                 y._pdt_bn_stats = BNStats(holder[0], y._version)
+                _attach_gemm_source(y, x, self.weight, None)
             return y
         if self.strided_gemm_eligible(x):
             holder = [] if (self.emit_bn_stats and self.training and torch.is_grad_enabled()
