@@ -132,6 +132,7 @@ int pdt_conv1x1_gemm(const uint16_t* a, const uint16_t* b, uint16_t* y, const ui
                      float* part, int M, int K, int N, const uint16_t* bn_x, const uint8_t* bn_mask,
                      const float* bn_mean, float* bn_part, int c_s, int c_H, int c_W, const float* acoef,
                      hipStream_t s);
+void pdt_conv1x1_probe(int probe);
 int pdt_conv1x1_gemm_apply(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t* res, const float* ab,
                            const float* rab, uint8_t* mask, int M, int K, int N, const float* acoef, hipStream_t s);
 int pdt_maxpool_bn_parts(int N, int H);
@@ -1769,6 +1770,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("c_in") = py::none(), py::arg("c_mask") = py::none(), py::arg("bn_x") = py::none(),
         py::arg("bn_mask") = py::none(), py::arg("bn_mean") = py::none(), py::arg("c_stride") = 0,
         py::arg("c_H") = 0, py::arg("c_W") = 0, py::arg("a_coef") = py::none());
+  m.def("conv1x1_probe", [](int probe) { pdt_conv1x1_probe(probe); });
   m.def("conv1x1_gemm_apply", &conv1x1_gemm_apply, py::arg("a"), py::arg("b"), py::arg("res"), py::arg("ab"),
         py::arg("rab") = py::none(), py::arg("a_coef") = py::none());
   m.def("bn_bwd_train_tiles", &bn_bwd_train_tiles);

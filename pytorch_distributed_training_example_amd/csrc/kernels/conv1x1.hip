@@ -68,7 +68,7 @@ struct G1 {
   static constexpr int kABytes = BM * 64, kBBytes = BN * 64, kSlot = kABytes + kBBytes;
   static constexpr int kEpiStride = BN * 2 + 16;
   static constexpr int kEpi = BM * kEpiStride;
-  static constexpr int kRed = tile_bn_stats_lds<BM, BN, kThreads>();
+  static constexpr int kRed = rs8_tile_store_lds<BN, kWaves>();
   static constexpr int kLds = kSlots * kSlot > kEpi + kRed ? kSlots * kSlot : kEpi + kRed;
   static constexpr int kMB = BM / WM / 16, kNB = BN / WN / 16;
   static constexpr int kALd = BM / 16 / kWaves, kBLd = BN / 16 / kWaves, kG = kALd + kBLd;
@@ -117,7 +117,11 @@ struct ApArgs {
   const float* ab;
   const float* rab;
   uint8_t* mask;
+  int probe;  // diagnosis only (pdt_conv1x1_probe): 1 = no output stores, 2 = no MFMA, 4 = no operand DMA,
+             // 8 = 64-channel tiles (4 waves) for every N
 };
+
+int g_probe = 0;
 
 // NT: streaming (non-temporal) output stores. ATR: acoef = [2][K] fp32 (a, then b), see the header.
 template <class Cf, bool ACC, bool STATS, bool NT, bool BSTATS, bool ATR = false, bool APPLY = false>
@@ -162,6 +166,7 @@ __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv1x1_kernel(
 #pragma unroll
     for (int j = 0; j < Cf::kBLd; ++j) dma16(B + (boff[j] + ko), slot + Cf::kABytes + (wid * Cf::kBLd + j) * 1024);
   };
+  const int probe = ap.probe;
 
   f4 acc[Cf::kMB][Cf::kNB];
 #pragma unroll
@@ -178,15 +183,17 @@ __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv1x1_kernel(
     asm volatile("" ::: "memory");
   }
 
-  issue(0);
-  if (S > 1) issue(1);
+  if (!(probe & 4)) {
+    issue(0);
+    if (S > 1) issue(1);
+  }
   const int lrow = lane & 15, lchk = lane >> 4;
   for (int s = 0; s < S; ++s) {
     if (s + 1 < S) wait_vm<Cf::kG>();
     else wait_vm<0>();
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (s + 2 < S) issue(s + 2);  // slot (s+2)%3 was last read at step s-1: every wave is past it
+    if (s + 2 < S && !(probe & 4)) issue(s + 2);  // slot (s+2)%3 was last read at step s-1: every wave is past it
     const char* As = lds + (s % Cf::kSlots) * Cf::kSlot;
     const char* Bs = As + Cf::kABytes;
     bf16x8 a[Cf::kMB], b[Cf::kNB];
@@ -217,10 +224,12 @@ __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv1x1_kernel(
         a[i] = __builtin_bit_cast(bf16x8, o);
       }
     }
+    if (!(probe & 2)) {
 #pragma unroll
-    for (int i = 0; i < Cf::kMB; ++i)
+      for (int i = 0; i < Cf::kMB; ++i)
 #pragma unroll
-      for (int j = 0; j < Cf::kNB; ++j) acc[i][j] = mfma(b[j], a[i], acc[i][j]);  // D[n][m]
+        for (int j = 0; j < Cf::kNB; ++j) acc[i][j] = mfma(b[j], a[i], acc[i][j]);  // D[n][m]
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
 
@@ -244,9 +253,9 @@ __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv1x1_kernel(
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __syncthreads();
 
-  if constexpr (STATS)
-    tile_bn_stats<BM, BN, Cf::kThreads, Cf::kEpiStride>(lds, reinterpret_cast<float*>(lds + Cf::kEpi),
-                                                         min(BM, M - m0), part, mt, (M + BM - 1) / BM, N, n0);
+  // STATS: the tile's BatchNorm partials from the rows each thread stores (RowStats8), merged after the loop
+  RowStats8 rst;
+  if constexpr (STATS) rs8_init(rst, *reinterpret_cast<const uint4*>(lds + (tid % (BN / 8)) * 16));
 
   constexpr int kChunks = BN / 8;
   static_assert(Cf::kThreads % kChunks == 0, "a thread keeps one 8-channel chunk");
@@ -355,9 +364,11 @@ __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv1x1_kernel(
       v.y = (uint32_t)f2bf(z[2]) | ((uint32_t)f2bf(z[3]) << 16);
       v.z = (uint32_t)f2bf(z[4]) | ((uint32_t)f2bf(z[5]) << 16);
       v.w = (uint32_t)f2bf(z[6]) | ((uint32_t)f2bf(z[7]) << 16);
-      ap.mask[off >> 3] = (uint8_t)mb;
+      if (!(probe & 32)) ap.mask[off >> 3] = (uint8_t)mb;
     }
     if constexpr (BSTATS) bn_bwd_accum8(v, xbv[it], bmkv[it], bmu, bs1, bs2);
+    if constexpr (STATS) rs8_add(rst, v);
+    if (probe & 1) continue;
     if constexpr (NT) {
       const u32x4 t = {v.x, v.y, v.z, v.w};
       __builtin_nontemporal_store(t, reinterpret_cast<u32x4*>(Y + off));
@@ -369,6 +380,9 @@ __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv1x1_kernel(
 
   if constexpr (BSTATS)  // every wave is done reading the staged tile: its LDS holds the block sums
     bn_bwd_tile_store<BN, Cf::kWaves>(bs1, bs2, reinterpret_cast<float*>(lds), bs.part, (M + BM - 1) / BM, mt, N, n0);
+  if constexpr (STATS)
+    rs8_tile_store<BN, Cf::kWaves, Cf::kEpiStride>(rst, lds, reinterpret_cast<float*>(lds + Cf::kEpi), part,
+                                                    min(BM, M - m0), (M + BM - 1) / BM, mt, N, n0);
 }
 
 constexpr int kMaxATRK = 512;  // ATR coefficient table: [2][K] floats past kLds
@@ -388,8 +402,10 @@ int launch_nt(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t*
   if (ATR && K > kMaxATRK) return -1;
   const int lds = Cf::kLds + (ATR ? 2 * K * 4 : 0);
   const int64_t grid = (int64_t)(M + Cf::BM - 1) / Cf::BM * (N / Cf::BN);
+  ApArgs apx = ap;
+  apx.probe = g_probe;
   hipLaunchKernelGGL((conv1x1_kernel<Cf, ACC, STATS, NT, BSTATS, ATR, APPLY>), dim3((unsigned)grid),
-                     dim3(Cf::kThreads), lds, s, a, b, y, c, cm, part, M, K, N, bs, cg, acoef, ap);
+                     dim3(Cf::kThreads), lds, s, a, b, y, c, cm, part, M, K, N, bs, cg, acoef, apx);
   return 0;
 }
 
@@ -429,6 +445,9 @@ extern "C" {
 
 int pdt_conv1x1_tile_rows() { return 256; }
 
+// Diagnosis (tools/conv1x1_bw.py --probe): see ApArgs::probe. Results are wrong while set.
+void pdt_conv1x1_probe(int probe) { g_probe = probe; }
+
 // y[M,N] = a[M,K] * b[N,K]^T (+ c[M,N], masked by the bit-mask cm when given: bit j of byte
 // (m*N + n) / 8 — the BatchNorm ReLU mask layout); part: stats of y per 256-row tile (see above),
 // or null. All bf16 row-major, K % 32 == 0, N % 64 == 0, M * max(K, N) < 2^31. c may alias y.
@@ -450,7 +469,7 @@ int pdt_conv1x1_gemm(const uint16_t* a, const uint16_t* b, uint16_t* y, const ui
     if (c_H < 1 || c_W < 1 || M % (c_H * c_W) != 0) return -1;
     cg = CGeom{c_s, c_H, c_W, (c_H - 1) / c_s + 1, (c_W - 1) / c_s + 1};
   }
-  if (N % 128 == 0) return dispatch<GWide>(a, b, y, c, cm, part, M, K, N, bs, cg, s, acoef);
+  if (N % 128 == 0 && !(g_probe & 8)) return dispatch<GWide>(a, b, y, c, cm, part, M, K, N, bs, cg, s, acoef);
   return dispatch<GNarrow>(a, b, y, c, cm, part, M, K, N, bs, cg, s, acoef);
 }
 
@@ -464,7 +483,7 @@ int pdt_conv1x1_gemm_apply(const uint16_t* a, const uint16_t* b, uint16_t* y, co
   const BnSrc bs{};
   const CGeom cg{0, 1, 1, 1, 1};
   const ApArgs ap{ab, rab, mask};
-  if (N % 128 == 0) {
+  if (N % 128 == 0 && !(g_probe & 8)) {
     if (acoef) return launch_nt<GWide, false, false, false, false, true, true>(a, b, y, res, nullptr, nullptr, M, K, N, bs, cg, s, acoef, ap);
     return launch_nt<GWide, false, false, false, false, false, true>(a, b, y, res, nullptr, nullptr, M, K, N, bs, cg, s, acoef, ap);
   }

@@ -61,6 +61,83 @@ __device__ __forceinline__ void tile_bn_stats(const char* tile, float* red, int 
 template <int BM, int BN, int THREADS>
 constexpr int tile_bn_stats_lds() { return (THREADS / (BN / 2)) * BN * 4; }
 
+// ---- The same partials from the values an epilogue thread already holds (no extra pass over the
+// staged tile): every thread keeps sums of (y - K) and (y - K)^2 for one 8-channel chunk over its
+// rows, K = the tile's first row (the same shift for every thread of the block, read once from the
+// staged tile); the block sums them in a fixed order and stores S = n K + sum(y - K) and the centred
+// M2 = sum (y - K)^2 - sum(y - K)^2 / n. Packed fp32 math (v_pk_add / v_pk_fma): ~3 VALU per value.
+typedef float pdt_f2 __attribute__((ext_vector_type(2)));
+
+struct RowStats8 {
+  pdt_f2 k[4], s[4], q[4];
+};
+
+// K: the 8 channels' values in the tile's first row (as stored).
+__device__ __forceinline__ void rs8_init(RowStats8& t, const uint4& k) {
+  const uint32_t w[4] = {k.x, k.y, k.z, k.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    t.k[j] = pdt_f2{__uint_as_float(w[j] << 16), __uint_as_float(w[j] & 0xffff0000u)};
+    t.s[j] = pdt_f2{0.f, 0.f};
+    t.q[j] = pdt_f2{0.f, 0.f};
+  }
+}
+
+// One row's 8 bf16 values (as stored).
+__device__ __forceinline__ void rs8_add(RowStats8& t, const uint4& v) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const pdt_f2 d = pdt_f2{__uint_as_float(w[j] << 16), __uint_as_float(w[j] & 0xffff0000u)} - t.k[j];
+    t.s[j] += d;
+    t.q[j] = d * d + t.q[j];
+  }
+}
+
+// Tile partials of the chunk (tid % (BN/8)) every thread accumulated over its rows; tile = the staged
+// bf16 tile (row 0 = K, row stride STRIDE bytes), nvalid = its valid rows; `red`: WAVES * (BN/8) * 16 floats
+// of LDS outside the tile. Contains __syncthreads: every thread of the block must call it.
+template <int BN, int WAVES, int STRIDE>
+__device__ __forceinline__ void rs8_tile_store(RowStats8& t, const char* tile, float* red, float* __restrict__ part,
+                                               int nvalid, int T, int mt, int N, int n0) {
+  constexpr int kChunks = BN / 8;
+  static_assert(64 % kChunks == 0, "chunk lanes");
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+#pragma unroll
+  for (int sh = kChunks; sh < 64; sh <<= 1)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      t.s[j] += pdt_f2{__shfl_xor(t.s[j].x, sh, 64), __shfl_xor(t.s[j].y, sh, 64)};
+      t.q[j] += pdt_f2{__shfl_xor(t.q[j].x, sh, 64), __shfl_xor(t.q[j].y, sh, 64)};
+    }
+  if (lane < kChunks) {
+    float* r = red + (wid * kChunks + lane) * 16;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      r[2 * j] = t.s[j].x; r[2 * j + 1] = t.s[j].y;
+      r[8 + 2 * j] = t.q[j].x; r[8 + 2 * j + 1] = t.q[j].y;
+    }
+  }
+  __syncthreads();
+  if (tid < BN) {
+    const int c = tid >> 3, j = tid & 7;
+    float S = 0.f, Q = 0.f;
+#pragma unroll
+    for (int w = 0; w < WAVES; ++w) {
+      S += red[(w * kChunks + c) * 16 + j];
+      Q += red[(w * kChunks + c) * 16 + 8 + j];
+    }
+    (void)STRIDE;
+    const float K = __uint_as_float((uint32_t)*reinterpret_cast<const uint16_t*>(tile + tid * 2) << 16);
+    const float n = (float)nvalid;
+    part[(int64_t)mt * N + n0 + tid] = fmaf(n, K, S);
+    part[((int64_t)T + mt) * N + n0 + tid] = fmaxf(Q - S * S / n, 0.f);
+  }
+}
+
+template <int BN, int WAVES>
+constexpr int rs8_tile_store_lds() { return WAVES * (BN / 8) * 16 * 4; }
+
 // ---- BatchNorm BACKWARD reduction in the epilogue of the kernel that writes dy (the gradient at a
 // BatchNorm's output): per tile, per channel, sum(dz) and sum(dz * (x - mean)), dz = dy * ReLU mask.
 // part layout as above ([T][N] sums of dz, then [T][N] sums of dz (x - mean)); the finalize is
