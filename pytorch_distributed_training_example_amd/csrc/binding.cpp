@@ -133,6 +133,9 @@ int pdt_conv1x1_gemm(const uint16_t* a, const uint16_t* b, uint16_t* y, const ui
                      const float* bn_mean, float* bn_part, int c_s, int c_H, int c_W, const float* acoef,
                      hipStream_t s);
 void pdt_conv1x1_probe(int probe);
+int pdt_weight_prep_max_items();
+int pdt_weight_prep(const uint16_t* const* src, uint16_t* const* dst, const int* R, const int* C, const int* taps,
+                    int n, hipStream_t s);
 int pdt_conv1x1_gemm_apply(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t* res, const float* ab,
                            const float* rab, uint8_t* mask, int M, int K, int N, const float* acoef, hipStream_t s);
 int pdt_maxpool_bn_parts(int N, int H);
@@ -680,7 +683,8 @@ std::vector<Tensor> bn_bwd_coef(Tensor dy, Tensor x, c10::optional<Tensor> part,
 // computed and written into bn_mask (an output then, M*CW/8 bytes).
 std::vector<Tensor> conv1x1_bwd_fused(Tensor dy, Tensor z, Tensor mz, Tensor mean, Tensor coef, Tensor w, Tensor xa,
                                       c10::optional<Tensor> bn_x, c10::optional<Tensor> bn_mask,
-                                      c10::optional<Tensor> bn_mean, c10::optional<Tensor> xcoef) {
+                                      c10::optional<Tensor> bn_mean, c10::optional<Tensor> xcoef,
+                                      c10::optional<Tensor> wt_pre) {
   check_nhwc_bf16(dy, "dy");
   check_nhwc_bf16(z, "z");
   TORCH_CHECK(xa.dim() == 4 && xa.is_cuda() && xa.scalar_type() == at::kBFloat16, "conv1x1_bwd_fused: xa");
@@ -696,7 +700,15 @@ std::vector<Tensor> conv1x1_bwd_fused(Tensor dy, Tensor z, Tensor mz, Tensor mea
               coef.is_contiguous() && coef.numel() == 3 * C4, "conv1x1_bwd_fused: mean [C4], coef [3, C4] fp32");
   TORCH_CHECK(w.scalar_type() == at::kBFloat16 && w.numel() == C4 * CW && w.size(0) == C4,
               "conv1x1_bwd_fused: weight [C4, CW, 1, 1] bf16");
-  auto wt = w.reshape({C4, CW}).t().contiguous();
+  Tensor wt;
+  if (wt_pre.has_value() && wt_pre->defined()) {  // W^T from the step's batched weight prep
+    TORCH_CHECK(wt_pre->scalar_type() == at::kBFloat16 && wt_pre->is_contiguous() && wt_pre->dim() == 2 &&
+                    wt_pre->size(0) == CW && wt_pre->size(1) == C4,
+                "conv1x1_bwd_fused: wt [CW, C4] bf16");
+    wt = *wt_pre;
+  } else {
+    wt = w.reshape({C4, CW}).t().contiguous();
+  }
   auto dxa = at::empty({xa.size(0), CW, xa.size(2), xa.size(3)}, xa.options().memory_format(at::MemoryFormat::ChannelsLast));
   auto dw = at::empty({C4, CW}, w.options());
   const int G = pdt_conv1x1_bwd_fused_grid((int)M, (int)C4, (int)CW);
@@ -924,6 +936,49 @@ std::vector<Tensor> conv1x1_gemm_apply(Tensor a, Tensor b, Tensor res, Tensor ab
                                         mask.data_ptr<uint8_t>(), (int)M, (int)K, (int)N, acp, stream());
   TORCH_CHECK(rc == 0, "pdt_conv1x1_gemm_apply failed: ", rc);
   return {y, mask};
+}
+
+// Batched per-step weight transforms (csrc/kernels/weight_prep.hip): for each i, src[i] = a conv weight
+// [Co, Ci, k, k] bf16 (k = 1: any layout; k = 3: channels_last, storage [Co][3][3][Ci]) -> dst[i]: k = 1:
+// W^T [Ci, Co] contiguous; k = 3: the flipped transposed weights [Ci, Co, 3, 3] channels_last (= conv3x3_flip).
+void weight_prep(std::vector<Tensor> src, std::vector<Tensor> dst) {
+  TORCH_CHECK(src.size() == dst.size(), "weight_prep: src / dst lists differ");
+  const int cap = pdt_weight_prep_max_items();
+  std::vector<const uint16_t*> sp;
+  std::vector<uint16_t*> dp;
+  std::vector<int> R, C, T;
+  auto flush = [&]() {
+    if (sp.empty()) return;
+    TORCH_CHECK(pdt_weight_prep(sp.data(), dp.data(), R.data(), C.data(), T.data(), (int)sp.size(), stream()) == 0,
+                "pdt_weight_prep failed");
+    sp.clear(); dp.clear(); R.clear(); C.clear(); T.clear();
+  };
+  for (size_t i = 0; i < src.size(); ++i) {
+    const Tensor& w = src[i];
+    const Tensor& d = dst[i];
+    check_cuda(w, "src");
+    check_cuda(d, "dst");
+    TORCH_CHECK(w.dim() == 4 && w.scalar_type() == at::kBFloat16 && d.scalar_type() == at::kBFloat16 &&
+                    w.size(2) == w.size(3) && (w.size(2) == 1 || w.size(2) == 3),
+                "weight_prep: bf16 [Co, Ci, k, k] weights, k = 1 or 3");
+    const int64_t Co = w.size(0), Ci = w.size(1), k = w.size(2);
+    if (k == 1) {
+      TORCH_CHECK(w.is_contiguous() || w.is_contiguous(at::MemoryFormat::ChannelsLast), "weight_prep: 1x1 weight layout");
+      TORCH_CHECK(d.dim() == 2 && d.size(0) == Ci && d.size(1) == Co && d.is_contiguous(), "weight_prep: dst [Ci, Co]");
+    } else {
+      TORCH_CHECK(w.is_contiguous(at::MemoryFormat::ChannelsLast), "weight_prep: 3x3 weight must be channels_last");
+      TORCH_CHECK(d.dim() == 4 && d.size(0) == Ci && d.size(1) == Co && d.size(2) == 3 && d.size(3) == 3 &&
+                      d.is_contiguous(at::MemoryFormat::ChannelsLast),
+                  "weight_prep: dst [Ci, Co, 3, 3] channels_last");
+    }
+    sp.push_back(reinterpret_cast<const uint16_t*>(w.data_ptr()));
+    dp.push_back(reinterpret_cast<uint16_t*>(d.data_ptr()));
+    R.push_back((int)Co);
+    C.push_back((int)Ci);
+    T.push_back((int)(k * k));
+    if ((int)sp.size() == cap) flush();
+  }
+  flush();
 }
 
 // Weight gradient of a stride-1 1x1 conv (csrc/kernels/conv1x1_wgrad.hip): dw [Co, Ci] bf16 =
@@ -1771,6 +1826,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("bn_mask") = py::none(), py::arg("bn_mean") = py::none(), py::arg("c_stride") = 0,
         py::arg("c_H") = 0, py::arg("c_W") = 0, py::arg("a_coef") = py::none());
   m.def("conv1x1_probe", [](int probe) { pdt_conv1x1_probe(probe); });
+  m.def("weight_prep", &weight_prep);
   m.def("conv1x1_gemm_apply", &conv1x1_gemm_apply, py::arg("a"), py::arg("b"), py::arg("res"), py::arg("ab"),
         py::arg("rab") = py::none(), py::arg("a_coef") = py::none());
   m.def("bn_bwd_train_tiles", &bn_bwd_train_tiles);
@@ -1806,7 +1862,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_bwd_coef", &bn_bwd_coef);
   m.def("conv1x1_bwd_fused", &conv1x1_bwd_fused, py::arg("dy"), py::arg("z"), py::arg("mz"), py::arg("mean"),
         py::arg("coef"), py::arg("w"), py::arg("xa"), py::arg("bn_x") = py::none(), py::arg("bn_mask") = py::none(),
-        py::arg("bn_mean") = py::none(), py::arg("xcoef") = py::none());
+        py::arg("bn_mean") = py::none(), py::arg("xcoef") = py::none(), py::arg("wt") = py::none());
   m.def("conv1x1_bwd_fused_tune", [](int grid) { pdt_conv1x1_bwd_fused_tune(grid); });
   m.def("ce_fwd", &ce_fwd);
   m.def("ce_bwd", &ce_bwd);

@@ -21,7 +21,8 @@ from torch import nn
 
 from ..ops.batchnorm import BatchNorm2d, BNGradLink, ResidualGradLink
 from ..config import SW
-from ..ops.conv import Conv1x1, SplitConv2d, linked_conv, stem_block
+from ..ops._native import disabled as native_disabled
+from ..ops.conv import Conv1x1, SplitConv2d, linked_conv, prepare_weights, stem_block
 
 
 def conv3x3(inp: int, out: int, stride: int = 1, groups: int = 1, dilation: int = 1) -> nn.Conv2d:
@@ -47,6 +48,9 @@ DS_MASKED_GRAD = [True]  # downsample blocks: bn3 hands the shortcut gradient to
 # when the shortcut BN has forward hooks (they must see its real output)
 DS_DEFER_APPLY = [os.environ.get("PDT_DS_DEFER", "1") != "0"]
 _norm_kind = ["pdt"]
+# the backward weight transforms of all convs (1x1 W^T, 3x3 flips) made in one launch at the start of the
+# training forward (csrc/kernels/weight_prep.hip) instead of 53 per-conv launches in the backward
+PREP_WEIGHTS = [os.environ.get("PDT_PREP_WEIGHTS", "1") != "0"]
 
 
 def _bn(c: int, fused_relu: bool = False) -> nn.Module:
@@ -193,7 +197,20 @@ class ResNet(nn.Module):
             layers.append(block(self.inplanes, planes, groups=self.groups, base_width=self.base_width))
         return nn.Sequential(*layers)
 
+    def _prep_convs(self):
+        """The convs whose data gradients read transformed weights (1x1: W^T, 3x3: flipped)."""
+        convs = getattr(self, "_pdt_prep_convs", None)
+        if convs is None:
+            convs = [m for m in self.modules() if isinstance(m, (Conv1x1, SplitConv2d)) and m is not self.conv1
+                     and m.kernel_size in ((1, 1), (3, 3))]
+            self._pdt_prep_convs = convs
+        return convs
+
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if (PREP_WEIGHTS[0] and self.training and torch.is_grad_enabled() and x.is_cuda
+                and x.dtype == torch.bfloat16 and not native_disabled()):
+            # every conv's backward weight transform for this step, in one launch (ops/conv.py)
+            prepare_weights(self._prep_convs())
         y = stem_block(self.conv1, self.bn1, x)  # one node: the BN's backward apply goes into the wgrad
         if y is not None:
             x = y

@@ -100,6 +100,65 @@ def _ours_ok(direction: str, M: int, K: int, N: int) -> bool:
             and M * max(K, N) < 2 ** 31 and SW.conv1x1 in ("auto", "ours"))
 
 
+# ---- per-step weight transforms (csrc/kernels/weight_prep.hip): the data gradients of our 1x1 GEMM and 3x3
+# kernels read W^T [Ci, Co] / the flipped transposed 3x3 weights. ``prepare_weights`` (called by the model at
+# the start of a training forward) makes all of them in ONE launch; a backward takes its conv's copy only
+# if it was made by the latest prepare call (``prepared``), else transforms on its own as before.
+_PREP = {"stamp": 0, "map": {}}
+
+
+def prepare_weights(convs) -> None:
+    """W^T of every 1x1 and the flipped weights of every 3x3 conv in ``convs``, one kernel launch. The copies
+    are keyed by the weight OBJECT (a weakref, checked with ``is``) and its storage pointer, so a freed weight
+    whose address is reused by another never matches."""
+    import weakref
+    _PREP["stamp"] += 1
+    stamp, old = _PREP["stamp"], _PREP["map"]
+    mp = {}
+    srcs, dsts = [], []
+    for m in convs:
+        w = m.weight
+        k = w.shape[-1]
+        if not (w.is_cuda and w.dtype == torch.bfloat16 and w.dim() == 4 and k in (1, 3) and w.shape[-2] == k):
+            continue
+        if k == 3 and not w.is_contiguous(memory_format=torch.channels_last):
+            continue
+        Co, Ci = w.shape[:2]
+        e = old.get(id(w))
+        dst = e[3] if (e is not None and e[1]() is w) else None
+        want = (Ci, Co) if k == 1 else (Ci, Co, 3, 3)
+        if dst is None or tuple(dst.shape) != want or dst.device != w.device:
+            dst = (torch.empty(want, dtype=w.dtype, device=w.device) if k == 1 else
+                   torch.empty(want, dtype=w.dtype, device=w.device).contiguous(memory_format=torch.channels_last))
+        mp[id(w)] = (stamp, weakref.ref(w), w.data_ptr(), dst)
+        srcs.append(w.detach())
+        dsts.append(dst)
+    _PREP["map"] = mp
+    if srcs:
+        from ._native import native
+        native().weight_prep(srcs, dsts)
+
+
+def prepared(weight: torch.Tensor):
+    """This step's transformed copy of ``weight`` (see prepare_weights), or None."""
+    e = _PREP["map"].get(id(weight))
+    if e is None or e[0] != _PREP["stamp"] or e[1]() is not weight or e[2] != weight.data_ptr():
+        return None
+    return e[3]
+
+
+def _wt_of(weight: torch.Tensor, w2: torch.Tensor) -> torch.Tensor:
+    """W^T [Ci, Co] of a 1x1 conv weight (w2 = its [Co, Ci] view)."""
+    wt = prepared(weight)
+    return wt if wt is not None else w2.t().contiguous()
+
+
+def _flip_of(weight: torch.Tensor) -> torch.Tensor:
+    from ._native import native
+    wf = prepared(weight)
+    return wf if wf is not None else native().conv3x3_flip(weight)
+
+
 class GemmSource:
     """How a 1x1 conv output z was computed by our GEMM (input, weight, ATR coefficients): the consuming
     BatchNorm's apply can run as that GEMM again with the apply epilogue (conv1x1.hip APPLY), reading the
@@ -312,7 +371,7 @@ class _Conv1x1Fn(torch.autograd.Function):
             # dx = dy*mask + dY W: the shortcut's ReLU-masked gradient applied in the GEMM epilogue
             from ._native import native
             dx = torch.empty_like(x)
-            gpart = native().conv1x1_gemm(g2, w2.t().contiguous(), _nhwc2d(dx), True, False, acc.dy, acc.mask,
+            gpart = native().conv1x1_gemm(g2, _wt_of(weight, w2), _nhwc2d(dx), True, False, acc.dy, acc.mask,
                                           **bn_kw)
             acc = None
         elif isinstance(acc, MaskedGrad):
@@ -323,7 +382,7 @@ class _Conv1x1Fn(torch.autograd.Function):
             cands = {"miopen": lambda: conv_bwd([True, False, False]), "gemm": lambda: torch.mm(g2, w2)}
             if gy.dtype == torch.bfloat16 and _ours_ok("dgrad", M, Co, Ci):
                 from ._native import native
-                wt = w2.t().contiguous()  # [Ci, Co]: the B operand rows of dX = dY W
+                wt = _wt_of(weight, w2)  # [Ci, Co]: the B operand rows of dX = dY W
 
                 def ours_d():
                     d = torch.empty_like(x)
@@ -398,7 +457,7 @@ def _bwd_fused(ctx, d, x, weight):
         return None  # the recompute mode needs bn2's input / mean (its GradStatsSource)
     r = native().conv1x1_bwd_fused(d.dy.contiguous(memory_format=torch.channels_last), d.x, d.mask, d.mean, d.coef,
                                    weight, x, gs.x if gs else None, gs.mask if gs else None, gs.mean if gs else None,
-                                   dre.ab if dre is not None else None)
+                                   dre.ab if dre is not None else None, prepared(weight))
     if not r:
         return None
     dx, dw, part = r
@@ -484,7 +543,7 @@ class _Conv1x1StridedFn(torch.autograd.Function):
             if gy.dtype == torch.bfloat16 and _ours_ok("dgrad", M, Co, Ci):
                 from ._native import native
                 d = torch.empty((N, Ci, Hs, Ws), dtype=gy.dtype, device=gy.device, memory_format=torch.channels_last)
-                native().conv1x1_gemm(g2, w2.t().contiguous(), _nhwc2d(d), False, False)
+                native().conv1x1_gemm(g2, _wt_of(weight, w2), _nhwc2d(d), False, False)
             else:
                 d = torch.mm(g2, w2).view(N, Hs, Ws, Ci).permute(0, 3, 1, 2)
             compact = StridedGrad(d, ctx.s)
@@ -562,12 +621,12 @@ class _Conv3x3Fn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             gs = ctx.gsrc if ctx.gsrc is not None and ctx.gsrc.ready() else None
             if gs is not None:  # dx is the gradient at a BatchNorm's output: its reduction in the epilogue
-                r = native().conv3x3s1_fwd_bnbwd(gy, native().conv3x3_flip(weight), gs.x, gs.mask, gs.mean)
+                r = native().conv3x3s1_fwd_bnbwd(gy, _flip_of(weight), gs.x, gs.mask, gs.mean)
                 dx = r[0]
                 if len(r) == 2:
                     gs.deposit(r[1], dx)
             else:
-                dx = native().conv3x3s1_fwd(gy, native().conv3x3_flip(weight))
+                dx = native().conv3x3s1_fwd(gy, _flip_of(weight))
         if ctx.needs_input_grad[1]:
             if SW.conv3x3_wgrad == "ours":
                 dw = native().conv3x3s1_wgrad(x, gy)
@@ -608,7 +667,7 @@ class _Conv3x3S2Fn(torch.autograd.Function):
             H, W = x.shape[2], x.shape[3]
             gs = ctx.gsrc if ctx.gsrc is not None and ctx.gsrc.ready() else None
             kw = dict(bn_x=gs.x, bn_mask=gs.mask, bn_mean=gs.mean) if gs is not None else {}
-            r = native().conv3x3s2_dgrad(gy, native().conv3x3_flip(weight), H, W, **kw)
+            r = native().conv3x3s2_dgrad(gy, _flip_of(weight), H, W, **kw)
             if r:
                 dx = r[0]
                 if len(r) == 2:

@@ -108,6 +108,11 @@ def init_distributed(
         os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
     # dmabuf IPC is the only IPC mode the MI355X host driver supports; keep it for RCCL.
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    # ProcessGroupNCCL recycles its completion events through a cache: an event of a collective issued
+    # before a hipGraph capture can be re-recorded by one issued during capture while the watchdog thread
+    # still polls it -> hipErrorCapturedEvent, process abort (seen 1 in 2 graphed bench runs, round 4).
+    # Fresh events per collective cost nothing measurable at one bucket round per step.
+    os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
 
     device = torch.device("cpu")
     if use_gpu:
