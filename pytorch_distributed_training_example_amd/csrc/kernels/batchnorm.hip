@@ -411,6 +411,7 @@ __global__ __launch_bounds__(1024) void bn_fin_kernel(const float* __restrict__ 
 // between-tile term in double, so E[x^2] - mean^2 never cancels in fp32. Level 2 finalizes.
 // CENTRED = false (backward partials: sum dz, sum dz (x - mean)): plain double sums, Q = sum_t q_t.
 constexpr int kTilesPerBlock = 128;
+int g_tiles_fused = 1;  // pdt_bn_tiles_fused(0): the two-launch finalize (A/B)
 
 template <bool CENTRED>
 __global__ __launch_bounds__(1024) void bn_tiles_l1_kernel(const float* __restrict__ part, int T, int BMt, int64_t M,
@@ -438,6 +439,82 @@ __global__ __launch_bounds__(1024) void bn_tiles_l1_kernel(const float* __restri
     for (int u = 0; u < 16; ++u) { s += sm[0][u][cl]; q += sm[1][u][cl]; }
     out[((int64_t)blockIdx.y * C + c) * 2] = s;
     out[((int64_t)blockIdx.y * C + c) * 2 + 1] = q;
+  }
+}
+
+// Levels 1 + 2 in ONE launch (the finalize was a second ~5 us launch per BatchNorm, 94 per ResNet-50
+// step: 0.45 ms at 1024 images, 0.9 ms of a 12.8 ms step at 128): the block of tile range p writes its
+// level-1 sums, and the LAST block of its 64-channel column to arrive (release fence, ticket on a
+// self-resetting counter, acquire fence — the reduce kernels' pattern) sums the P entries in index
+// order and finalizes. P == 1: no ticket. Deterministic: fixed summation order either way.
+__device__ unsigned g_tiles_ctr[64];  // one per 64-channel column (C <= 4096), zero at load, self-resetting
+
+template <bool CENTRED>
+__global__ __launch_bounds__(1024) void bn_tiles_fin_kernel(const float* __restrict__ part, int T, int BMt, int64_t M,
+                                                            int C, double* __restrict__ lv, FinArgs fa) {
+  __shared__ double sm[2][16][64];
+  __shared__ int last;
+  const int tid = threadIdx.x, cl = tid & 63, j = tid >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  const int P = gridDim.y;
+  const int t0 = blockIdx.y * kTilesPerBlock, t1 = min(T, t0 + kTilesPerBlock);
+  double S = 0.0, Q = 0.0;
+#pragma unroll 4
+  for (int t = t0 + j; t < t1; t += 16) {
+    const float s = part[(int64_t)t * C + c];
+    const float q = part[((int64_t)T + t) * C + c];
+    const int64_t rem = M - (int64_t)t * BMt;
+    const double n = (double)(rem < BMt ? rem : BMt);
+    S += (double)s;
+    Q += CENTRED ? (double)q + (double)s * (double)s / n : (double)q;
+  }
+  sm[0][j][cl] = S;
+  sm[1][j][cl] = Q;
+  __syncthreads();
+  double s = 0.0, q = 0.0;
+  if (j == 0) {
+#pragma unroll
+    for (int u = 0; u < 16; ++u) { s += sm[0][u][cl]; q += sm[1][u][cl]; }
+  }
+  if (P > 1) {
+    if (j == 0) {
+      lv[((int64_t)blockIdx.y * C + c) * 2] = s;
+      lv[((int64_t)blockIdx.y * C + c) * 2 + 1] = q;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned tk = __hip_atomic_fetch_add(&g_tiles_ctr[blockIdx.x], 1u, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+      last = tk == (unsigned)(P - 1);
+    }
+    __syncthreads();
+    if (!last) return;
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      g_tiles_ctr[blockIdx.x] = 0u;
+    }
+    __syncthreads();
+    if (j != 0) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    s = 0.0;
+    q = 0.0;
+#pragma unroll 8
+    for (int p = 0; p < P; ++p) {
+      s += __builtin_nontemporal_load(&lv[((int64_t)p * C + c) * 2]);
+      q += __builtin_nontemporal_load(&lv[((int64_t)p * C + c) * 2 + 1]);
+    }
+  } else if (j != 0) {
+    return;
+  }
+  if (CENTRED) {
+    const double inv_m = 1.0 / (double)fa.M;
+    const double mu = s * inv_m;
+    bn_set_fwd(c, mu, q * inv_m - mu * mu, fa);
+  } else {
+    bn_finalize<1>(c, (float)s, (float)q, fa);
   }
 }
 
@@ -815,8 +892,12 @@ int bn_bwd_from_partials(const float* part, int T, int BMt, const uint16_t* dy, 
   FinArgs fa{};
   fa.gamma = gamma; fa.invstd = invstd; fa.dgamma = dgamma; fa.dbeta = dbeta; fa.A = A; fa.B = B; fa.D = D;
   fa.M = M;
-  hipLaunchKernelGGL(bn_tiles_l1_kernel<false>, dim3(C / 64, P), dim3(1024), 0, s, part, T, BMt, M, C, lv);
-  hipLaunchKernelGGL(bn_tiles_l2b_kernel, dim3((C + 255) / 256), dim3(256), 0, s, lv, P, C, fa);
+  if (g_tiles_fused && C / 64 <= 64) {
+    hipLaunchKernelGGL(bn_tiles_fin_kernel<false>, dim3(C / 64, P), dim3(1024), 0, s, part, T, BMt, M, C, lv, fa);
+  } else {
+    hipLaunchKernelGGL(bn_tiles_l1_kernel<false>, dim3(C / 64, P), dim3(1024), 0, s, part, T, BMt, M, C, lv);
+    hipLaunchKernelGGL(bn_tiles_l2b_kernel, dim3((C + 255) / 256), dim3(256), 0, s, lv, P, C, fa);
+  }
   if (!dx) return 0;  // coefficients only: the consumer applies them (pdt_stem_conv_wgrad_bn)
   const int64_t nvec = M * C / 8;
   const int fixed = (2048 % C) == 0;
@@ -840,6 +921,9 @@ extern "C" {
 int64_t pdt_bn_workspace_floats(int64_t M, int C) {
   return slab_floats3(reduce_geo3(M, C, 2), C) + 4 * (int64_t)C;  // U = 2 gives the most rows
 }
+
+// 1: one-launch tile finalize (bn_tiles_fin_kernel, default); 0: level-1 + level-2 launches.
+void pdt_bn_tiles_fused(int on) { g_tiles_fused = on; }
 
 // Select the reduce implementation / grid (benchmarking). Values <= 0 keep the current setting.
 void pdt_bn_tune(int variant, int target_blocks, int u_fwd, int u_bwd) {
@@ -909,8 +993,12 @@ int pdt_bn_fwd_train_tiles(const float* part, int T, int BMt, const uint16_t* x,
   fa.gamma = gamma; fa.beta = beta; fa.mean_out = mean; fa.invstd_out = invstd; fa.a_out = a;
   fa.b_out = b; fa.running_mean = running_mean; fa.running_var = running_var; fa.momentum = momentum;
   fa.eps = eps; fa.M = M;
-  hipLaunchKernelGGL(bn_tiles_l1_kernel<true>, dim3(C / 64, P), dim3(1024), 0, s, part, T, BMt, M, C, lv);
-  hipLaunchKernelGGL(bn_tiles_l2_kernel, dim3((C + 255) / 256), dim3(256), 0, s, lv, P, C, fa);
+  if (g_tiles_fused && C / 64 <= 64) {
+    hipLaunchKernelGGL(bn_tiles_fin_kernel<true>, dim3(C / 64, P), dim3(1024), 0, s, part, T, BMt, M, C, lv, fa);
+  } else {
+    hipLaunchKernelGGL(bn_tiles_l1_kernel<true>, dim3(C / 64, P), dim3(1024), 0, s, part, T, BMt, M, C, lv);
+    hipLaunchKernelGGL(bn_tiles_l2_kernel, dim3((C + 255) / 256), dim3(256), 0, s, lv, P, C, fa);
+  }
   if (!y) return 0;
   const int64_t nvec = M * C / 8;
   const int fixed = (2048 % C) == 0;

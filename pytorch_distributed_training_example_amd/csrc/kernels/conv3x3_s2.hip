@@ -38,15 +38,28 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 
 __device__ __attribute__((aligned(256))) uint4 g_s2_zero[16];  // zero page for padding rows (never written)
 
-constexpr int kBM = 256, kBN = 128, kBK = 32, kWM = 4, kWN = 2, kSlots = 3;
-constexpr int kWaves = kWM * kWN, kThreads = kWaves * 64;
-constexpr int kABytes = kBM * 64, kBBytes = kBN * 64, kSlot = kABytes + kBBytes;
-constexpr int kEpiStride = kBN * 2 + 16;
-constexpr int kEpi = kBM * kEpiStride + tile_bn_stats_lds<kBM, kBN, kThreads>();
-constexpr int kLds = kSlots * kSlot > kEpi ? kSlots * kSlot : kEpi;
-constexpr int kMB = kBM / kWM / 16, kNB = kBN / kWN / 16;
-constexpr int kALd = kBM / 16 / kWaves, kBLd = kBN / 16 / kWaves, kG = kALd + kBLd;
-static_assert(kALd * 16 * kWaves == kBM && kBLd * 16 * kWaves == kBN, "DMA split");
+// Tile 256 pixels x BN output channels: BN = 128 (8 waves, 4 x 2) or 64 (4 waves, 4 x 1, for a GEMM N
+// of 64 channels: the data gradient of a 64-input-channel conv, ResNet-18/34 layer2 block 0).
+template <int BN_>
+struct S2Cfg {
+  static constexpr int kBM = 256, kBN = BN_, kBK = 32, kWM = 4, kWN = BN_ / 64, kSlots = 3;
+  static constexpr int kWaves = kWM * kWN, kThreads = kWaves * 64;
+  static constexpr int kABytes = kBM * 64, kBBytes = kBN * 64, kSlot = kABytes + kBBytes;
+  static constexpr int kEpiStride = kBN * 2 + 16;
+  static constexpr int kEpi = kBM * kEpiStride + tile_bn_stats_lds<kBM, kBN, kThreads>();
+  static constexpr int kLds = kSlots * kSlot > kEpi ? kSlots * kSlot : kEpi;
+  static constexpr int kMB = kBM / kWM / 16, kNB = kBN / kWN / 16;
+  static constexpr int kALd = kBM / 16 / kWaves, kBLd = kBN / 16 / kWaves, kG = kALd + kBLd;
+  static_assert(kALd * 16 * kWaves == kBM && kBLd * 16 * kWaves == kBN, "DMA split");
+};
+constexpr int kBM = 256, kBK = 32;
+
+template <int G>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(G == 3 || G == 5, "vmcnt: DMA instructions per k-step");
+  if constexpr (G == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+}
 
 struct Taps {  // one phase: n taps, input-pixel offsets (dy, dx) and weight tap index w
   int n;
@@ -75,11 +88,14 @@ __device__ __forceinline__ void dma16(const void* src, char* lds_wave_base) {
   __builtin_amdgcn_global_load_lds(src, (PDT_LDS void*)lds_wave_base, 16, 0, 0);
 }
 
-template <bool STATS, bool BSTATS>
-__global__ __launch_bounds__(kThreads, 4) void conv3x3g_kernel(const uint16_t* __restrict__ X,
-                                                              const uint16_t* __restrict__ Wt,
-                                                              uint16_t* __restrict__ Y, float* __restrict__ part,
-                                                              BnSrc bs, Geo g) {
+template <class Cf, bool STATS, bool BSTATS>
+__global__ __launch_bounds__(Cf::kThreads, 4) void conv3x3g_kernel(const uint16_t* __restrict__ X,
+                                                                  const uint16_t* __restrict__ Wt,
+                                                                  uint16_t* __restrict__ Y, float* __restrict__ part,
+                                                                  BnSrc bs, Geo g) {
+  constexpr int kBN = Cf::kBN, kWM = Cf::kWM, kSlots = Cf::kSlots, kWaves = Cf::kWaves, kThreads = Cf::kThreads;
+  constexpr int kABytes = Cf::kABytes, kSlot = Cf::kSlot, kEpiStride = Cf::kEpiStride, kMB = Cf::kMB;
+  constexpr int kNB = Cf::kNB, kALd = Cf::kALd, kBLd = Cf::kBLd;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid % kWM, wn = wid / kWM;
@@ -147,8 +163,7 @@ __global__ __launch_bounds__(kThreads, 4) void conv3x3g_kernel(const uint16_t* _
   if (S > 1) issue(1);
   const int lrow = lane & 15, lchk = lane >> 4;
   for (int s = 0; s < S; ++s) {
-    static_assert(kG == 3, "vmcnt below counts 3 DMA instructions per k-step");
-    if (s + 1 < S) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    if (s + 1 < S) wait_vm<Cf::kG>();
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
@@ -217,28 +232,36 @@ __global__ __launch_bounds__(kThreads, 4) void conv3x3g_kernel(const uint16_t* _
     bn_bwd_tile_store<kBN, kWaves>(bs1, bs2, reinterpret_cast<float*>(lds), bs.part, g.T, ph * g.tpp + mt, g.Co, n0);
 }
 
-template <bool STATS, bool BSTATS>
-int launch(const uint16_t* x, const uint16_t* w, uint16_t* y, float* part, const BnSrc& bs, const Geo& g,
-           hipStream_t s) {
+template <class Cf, bool STATS, bool BSTATS>
+int launch_cf(const uint16_t* x, const uint16_t* w, uint16_t* y, float* part, const BnSrc& bs, const Geo& g,
+              hipStream_t s) {
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3g_kernel<STATS, BSTATS>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, kLds) != hipSuccess)
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3g_kernel<Cf, STATS, BSTATS>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, Cf::kLds) != hipSuccess)
       return -3;
     attr = true;
   }
-  const int64_t grid = (int64_t)g.nph * g.tpp * (g.Co / kBN);
-  hipLaunchKernelGGL((conv3x3g_kernel<STATS, BSTATS>), dim3((unsigned)grid), dim3(kThreads), kLds, s, x, w, y, part,
-                     bs, g);
+  const int64_t grid = (int64_t)g.nph * g.tpp * (g.Co / Cf::kBN);
+  hipLaunchKernelGGL((conv3x3g_kernel<Cf, STATS, BSTATS>), dim3((unsigned)grid), dim3(Cf::kThreads), Cf::kLds, s, x,
+                     w, y, part, bs, g);
   return 0;
+}
+
+// the GEMM N (g.Co) picks the tile: 128 channels when it divides, else 64
+template <bool STATS, bool BSTATS>
+int launch(const uint16_t* x, const uint16_t* w, uint16_t* y, float* part, const BnSrc& bs, const Geo& g,
+           hipStream_t s) {
+  if (g.Co % 128 == 0) return launch_cf<S2Cfg<128>, STATS, BSTATS>(x, w, y, part, bs, g, s);
+  return launch_cf<S2Cfg<64>, STATS, BSTATS>(x, w, y, part, bs, g, s);
 }
 
 inline int tiles_of(int64_t M) { return (int)((M + kBM - 1) / kBM); }
 
-// shape limits: 32-bit element offsets; the GEMM's N (output channels of this direction) tiles by kBN,
+// shape limits: 32-bit element offsets; the GEMM's N (output channels of this direction) tiles by 64 / 128,
 // its K (gathered channels) by 64 (two kBK steps per tap)
 inline int check_shape(int N, int H, int W, int Ci, int Co, int kdim, int ndim) {
-  if (N < 1 || H < 2 || W < 2 || kdim % 64 != 0 || ndim % kBN != 0) return -1;
+  if (N < 1 || H < 2 || W < 2 || kdim % 64 != 0 || ndim % 64 != 0) return -1;
   if ((int64_t)N * H * W * (Ci > Co ? Ci : Co) >= (int64_t)1 << 31 || (int64_t)Co * 9 * Ci >= (int64_t)1 << 31)
     return -2;
   return 0;
@@ -258,7 +281,7 @@ int pdt_conv3x3s2_dgrad_tiles(int N, int H, int W) {
 
 // y[N,Ho,Wo,Co] = conv2d(x[N,H,W,Ci], w[Co,3,3,Ci], stride 2, padding 1), Ho = (H-1)/2+1 (NHWC bf16).
 // part (or null): per-256-pixel-tile BatchNorm statistics of y, [2][ceil(N*Ho*Wo/256)][Co] fp32.
-// Ci % 64 == 0, Co % 128 == 0. Returns 0, or < 0 for an unsupported shape (caller falls back).
+// Ci % 64 == 0, Co % 64 == 0. Returns 0, or < 0 for an unsupported shape (caller falls back).
 int pdt_conv3x3s2_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, float* part, int N, int H, int W, int Ci,
                       int Co, hipStream_t s) {
   const int rc = check_shape(N, H, W, Ci, Co, Ci, Co);
@@ -281,7 +304,7 @@ int pdt_conv3x3s2_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, float* 
 // wf[Ci,3,3,Co] (pdt_conv3x3_flip_weights). bn_x / bn_mask / bn_mean / bn_part (all null = off): dx is
 // the gradient at the output of a BatchNorm with input bn_x [N,H,W,Ci], ReLU mask bn_mask (or null)
 // and mean bn_mean; bn_part [2][pdt_conv3x3s2_dgrad_tiles()][Ci] receives its backward partials.
-// Ci % 128 == 0, Co % 64 == 0.
+// Ci % 64 == 0, Co % 64 == 0.
 int pdt_conv3x3s2_dgrad(const uint16_t* dy, const uint16_t* wf, uint16_t* dx, const uint16_t* bn_x,
                         const uint8_t* bn_mask, const float* bn_mean, float* bn_part, int N, int H, int W, int Ci,
                         int Co, hipStream_t s) {

@@ -22,6 +22,9 @@ def _load():
     try:
         import torch  # noqa: F401  (libc10 / libtorch must be loaded first)
         _mod = importlib.import_module("pytorch_distributed_training_example_amd._C")
+        import os
+        if os.environ.get("PDT_BN_TILES_FUSED", "1") == "0":  # A/B: the two-launch BN tile finalize
+            _mod.bn_tiles_fused(0)
     except Exception as e:  # pragma: no cover - depends on build state
         _err = e
     return _mod

@@ -684,13 +684,13 @@ class _Conv3x3S2Fn(torch.autograd.Function):
 
 def conv3x3s2_eligible(conv: nn.Conv2d, x: torch.Tensor) -> bool:
     """Our stride-2 3x3 kernels apply: stride 2, padding 1, no bias/groups/dilation, channels_last
-    bf16 GPU input with Ci % 64 == 0 and Co % 128 == 0 (ResNet-50: layer2-4 block-0 conv2; ResNet-18/34:
-    layer2-4 block-0 conv1 — the data gradient of a Ci = 64 conv (ResNet-18 layer2) stays on MIOpen)."""
+    bf16 GPU input with Ci % 64 == 0 and Co % 64 == 0 (ResNet-50: layer2-4 block-0 conv2; ResNet-18/34:
+    layer2-4 block-0 conv1; 64-channel GEMM N dimensions take the kernel's 64-wide tile)."""
     return (conv.kernel_size == (3, 3) and conv.stride == (2, 2) and conv.padding == (1, 1)
             and conv.dilation == (1, 1) and conv.groups == 1 and conv.bias is None and conv.padding_mode == "zeros"
             and x.is_cuda and x.dim() == 4 and x.dtype == torch.bfloat16 and conv.weight.dtype == torch.bfloat16
             and x.is_contiguous(memory_format=torch.channels_last) and x.shape[1] % 64 == 0
-            and conv.out_channels % 128 == 0 and x.shape[2] >= 2 and x.shape[3] >= 2
+            and conv.out_channels % 64 == 0 and x.shape[2] >= 2 and x.shape[3] >= 2
             and SW.conv3x3_s2 == "ours" and not disabled())
 
 
