@@ -68,7 +68,7 @@ struct G1 {
   static constexpr int kABytes = BM * 64, kBBytes = BN * 64, kSlot = kABytes + kBBytes;
   static constexpr int kEpiStride = BN * 2 + 16;
   static constexpr int kEpi = BM * kEpiStride;
-  static constexpr int kRed = rs8_tile_store_lds<BN, kWaves>();
+  static constexpr int kRed = 0;  // (the statistics reduction reuses the released tile: rs8_tile_store)
   static constexpr int kLds = kSlots * kSlot > kEpi + kRed ? kSlots * kSlot : kEpi + kRed;
   static constexpr int kMB = BM / WM / 16, kNB = BN / WN / 16;
   static constexpr int kALd = BM / 16 / kWaves, kBLd = BN / 16 / kWaves, kG = kALd + kBLd;
@@ -118,7 +118,7 @@ struct ApArgs {
   const float* rab;
   uint8_t* mask;
   int probe;  // diagnosis only (pdt_conv1x1_probe): 1 = no output stores, 2 = no MFMA, 4 = no operand DMA,
-             // 8 = 64-channel tiles (4 waves) for every N
+             // 8 = 64-channel tiles (4 waves) for every N, 64 = no 256-channel tiles
 };
 
 int g_probe = 0;
@@ -255,7 +255,11 @@ __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv1x1_kernel(
 
   // STATS: the tile's BatchNorm partials from the rows each thread stores (RowStats8), merged after the loop
   RowStats8 rst;
-  if constexpr (STATS) rs8_init(rst, *reinterpret_cast<const uint4*>(lds + (tid % (BN / 8)) * 16));
+  float kst = 0.f;  // the tile's first-row value of channel tid (tid < BN), for rs8_tile_store
+  if constexpr (STATS) {
+    rs8_init(rst, *reinterpret_cast<const uint4*>(lds + (tid % (BN / 8)) * 16));
+    if (tid < BN) kst = __uint_as_float((uint32_t)*reinterpret_cast<const uint16_t*>(lds + tid * 2) << 16);
+  }
 
   constexpr int kChunks = BN / 8;
   static_assert(Cf::kThreads % kChunks == 0, "a thread keeps one 8-channel chunk");
@@ -380,9 +384,11 @@ __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv1x1_kernel(
 
   if constexpr (BSTATS)  // every wave is done reading the staged tile: its LDS holds the block sums
     bn_bwd_tile_store<BN, Cf::kWaves>(bs1, bs2, reinterpret_cast<float*>(lds), bs.part, (M + BM - 1) / BM, mt, N, n0);
-  if constexpr (STATS)
-    rs8_tile_store<BN, Cf::kWaves, Cf::kEpiStride>(rst, lds, reinterpret_cast<float*>(lds + Cf::kEpi), part,
-                                                    min(BM, M - m0), (M + BM - 1) / BM, mt, N, n0);
+  if constexpr (STATS) {
+    __syncthreads();  // every wave is done reading the staged tile: its LDS takes the reduction
+    rs8_tile_store<BN, Cf::kWaves>(rst, kst, reinterpret_cast<float*>(lds), part, min(BM, M - m0), (M + BM - 1) / BM,
+                                   mt, N, n0);
+  }
 }
 
 constexpr int kMaxATRK = 512;  // ATR coefficient table: [2][K] floats past kLds
@@ -417,6 +423,7 @@ int launch(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t* c,
   return launch_nt<Cf, ACC, STATS, false, BSTATS>(a, b, y, c, cm, part, M, K, N, bs, cg, s);
 }
 
+using GXWide = G1<256, 4, 4>;  // N % 256 == 0 (large M): 16 waves of 64x64, a block writes whole 512-B rows
 using GWide = G1<128, 4, 2>;   // N % 128 == 0: 8 waves of 64x64
 using GNarrow = G1<64, 4, 1>;  // N == 64 (or odd multiples of 64): 4 waves of 64x64
 
@@ -469,6 +476,11 @@ int pdt_conv1x1_gemm(const uint16_t* a, const uint16_t* b, uint16_t* y, const ui
     if (c_H < 1 || c_W < 1 || M % (c_H * c_W) != 0) return -1;
     cg = CGeom{c_s, c_H, c_W, (c_H - 1) / c_s + 1, (c_W - 1) / c_s + 1};
   }
+  // 256-wide tiles when the grid is deep (>= 8 blocks per CU): contiguous 512-B output rows, A read once
+  // (tools/conv1x1_probe.py, 1024 images: 128->512 @28 fwd+stats 293 vs 342 us, 64->256 @56 506-554 vs
+  // 553-571; at 512->2048 @7 — 1,568 blocks — 5 % slower, hence the threshold)
+  if (N % 256 == 0 && (int64_t)((M + 255) / 256) * (N / 256) >= 2048 && !(g_probe & 64))
+    return dispatch<GXWide>(a, b, y, c, cm, part, M, K, N, bs, cg, s, acoef);
   if (N % 128 == 0 && !(g_probe & 8)) return dispatch<GWide>(a, b, y, c, cm, part, M, K, N, bs, cg, s, acoef);
   return dispatch<GNarrow>(a, b, y, c, cm, part, M, K, N, bs, cg, s, acoef);
 }

@@ -94,11 +94,12 @@ __device__ __forceinline__ void rs8_add(RowStats8& t, const uint4& v) {
   }
 }
 
-// Tile partials of the chunk (tid % (BN/8)) every thread accumulated over its rows; tile = the staged
-// bf16 tile (row 0 = K, row stride STRIDE bytes), nvalid = its valid rows; `red`: WAVES * (BN/8) * 16 floats
-// of LDS outside the tile. Contains __syncthreads: every thread of the block must call it.
-template <int BN, int WAVES, int STRIDE>
-__device__ __forceinline__ void rs8_tile_store(RowStats8& t, const char* tile, float* red, float* __restrict__ part,
+// Tile partials of the chunk (tid % (BN/8)) every thread accumulated over its rows; K = the tile's first-row
+// value of channel tid (threads tid < BN; read before the tile's LDS was released), nvalid = the tile's valid
+// rows; `red`: WAVES * (BN/8) * 16 floats of LDS nobody reads any more. Contains __syncthreads: every thread of
+// the block must call it.
+template <int BN, int WAVES>
+__device__ __forceinline__ void rs8_tile_store(RowStats8& t, float K, float* red, float* __restrict__ part,
                                                int nvalid, int T, int mt, int N, int n0) {
   constexpr int kChunks = BN / 8;
   static_assert(64 % kChunks == 0, "chunk lanes");
@@ -127,8 +128,6 @@ __device__ __forceinline__ void rs8_tile_store(RowStats8& t, const char* tile, f
       S += red[(w * kChunks + c) * 16 + j];
       Q += red[(w * kChunks + c) * 16 + 8 + j];
     }
-    (void)STRIDE;
-    const float K = __uint_as_float((uint32_t)*reinterpret_cast<const uint16_t*>(tile + tid * 2) << 16);
     const float n = (float)nvalid;
     part[(int64_t)mt * N + n0 + tid] = fmaf(n, K, S);
     part[((int64_t)T + mt) * N + n0 + tid] = fmaxf(Q - S * S / n, 0.f);

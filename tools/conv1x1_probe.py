@@ -33,10 +33,10 @@ def main():
     a = ap.parse_args()
     from pytorch_distributed_training_example_amd.ops._native import native
     C = native()
-    probes = [0, 32, 1, 33, 7, 39]
-    print("probe: 1 = no stores, 2 = no MFMA, 4 = no operand DMA, 8 = 64-channel tiles, 16 = no statistics, 32 = no mask stores")
+    probes = [0, 64, 0, 64, 1, 65]
+    print("probe: 1 = no stores, 2 = no MFMA, 4 = no operand DMA, 8 = 64-channel tiles, 16 = no statistics, 32 = no mask stores, 64 = no 256-channel tiles")
     print(f"{'case':<34}" + "".join(f"{p:>9}" for p in probes) + "   GB  TB/s(p0)")
-    for h, ci, co in ((56, 64, 256), (28, 128, 512)):
+    for h, ci, co in ((56, 64, 256), (28, 128, 512), (14, 256, 1024), (7, 512, 2048)):
         M = a.batch * h * h
         x = torch.randn(M, ci, device="cuda").bfloat16()
         w = (torch.randn(co, ci, device="cuda") / ci ** 0.5).bfloat16()
