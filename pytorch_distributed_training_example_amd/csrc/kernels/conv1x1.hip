@@ -495,6 +495,10 @@ int pdt_conv1x1_gemm_apply(const uint16_t* a, const uint16_t* b, uint16_t* y, co
   const BnSrc bs{};
   const CGeom cg{0, 1, 1, 1, 1};
   const ApArgs ap{ab, rab, mask};
+  if (N % 256 == 0 && (int64_t)((M + 255) / 256) * (N / 256) >= 2048 && !(g_probe & 64)) {
+    if (acoef) return launch_nt<GXWide, false, false, false, false, true, true>(a, b, y, res, nullptr, nullptr, M, K, N, bs, cg, s, acoef, ap);
+    return launch_nt<GXWide, false, false, false, false, false, true>(a, b, y, res, nullptr, nullptr, M, K, N, bs, cg, s, acoef, ap);
+  }
   if (N % 128 == 0 && !(g_probe & 8)) {
     if (acoef) return launch_nt<GWide, false, false, false, false, true, true>(a, b, y, res, nullptr, nullptr, M, K, N, bs, cg, s, acoef, ap);
     return launch_nt<GWide, false, false, false, false, false, true>(a, b, y, res, nullptr, nullptr, M, K, N, bs, cg, s, acoef, ap);
