@@ -15,7 +15,20 @@
 
 #define PDT_WAVE 64
 
+#include <stdlib.h>
+
 namespace pdt {
+
+// Small grids (the reference's 128 images per rank at the 8-GPU point, ResNet layers 3-4): a conv whose
+// wide-tile grid gives fewer than one workgroup per CU takes the half-width tile instead (twice the
+// workgroups). PDT_SMALL_GRID_NARROW=0 turns it off (A/B), read once per process.
+inline bool small_grid_narrow(int64_t wide_blocks) {
+  static const int on = [] {
+    const char* e = getenv("PDT_SMALL_GRID_NARROW");
+    return e && e[0] == '0' ? 0 : 1;
+  }();
+  return on && wide_blocks < 256;
+}
 
 __device__ __forceinline__ float bf2f(uint16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
 __device__ __forceinline__ uint16_t f2bf(float f) {

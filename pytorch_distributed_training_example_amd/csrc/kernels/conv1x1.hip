@@ -481,7 +481,8 @@ int pdt_conv1x1_gemm(const uint16_t* a, const uint16_t* b, uint16_t* y, const ui
   // 553-571; at 512->2048 @7 — 1,568 blocks — 5 % slower, hence the threshold)
   if (N % 256 == 0 && (int64_t)((M + 255) / 256) * (N / 256) >= 2048 && !(g_probe & 64))
     return dispatch<GXWide>(a, b, y, c, cm, part, M, K, N, bs, cg, s, acoef);
-  if (N % 128 == 0 && !(g_probe & 8)) return dispatch<GWide>(a, b, y, c, cm, part, M, K, N, bs, cg, s, acoef);
+  if (N % 128 == 0 && !(g_probe & 8) && !small_grid_narrow((int64_t)((M + 255) / 256) * (N / 128)))
+    return dispatch<GWide>(a, b, y, c, cm, part, M, K, N, bs, cg, s, acoef);
   return dispatch<GNarrow>(a, b, y, c, cm, part, M, K, N, bs, cg, s, acoef);
 }
 

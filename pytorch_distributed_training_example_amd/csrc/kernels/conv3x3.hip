@@ -968,6 +968,9 @@ int launch(const uint16_t* x, const uint16_t* w, uint16_t* y, int N, int H, int 
   return 0;
 }
 
+// 128-channel tiles unless the grid would leave CUs idle (pdt::small_grid_narrow)
+inline bool h_wide(int64_t M, int Co) { return Co % 128 == 0 && !small_grid_narrow((M + 255) / 256 * (Co / 128)); }
+
 using CfWide = Cfg<256, 128, 4, 2, 32>;   // Co % 128 == 0: 8 waves of 64x64, 72 KB LDS -> 2 WG/CU
 using CfNarrow = Cfg<256, 64, 4, 1, 32>;  // Co == 64: 4 waves of 64x64, 60 KB LDS
 
@@ -987,7 +990,7 @@ int pdt_conv3x3s1_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int N, 
 #endif
   int rc = -1;
   if (Ci == 64 && Co == 64) rc = launch_wst<SCfg<64, 64>>(x, w, y, N, H, W, Ci, Co, s);
-  if (rc == -1) rc = Co % 128 == 0 ? launch_h<HWide>(x, w, y, N, H, W, Ci, Co, s) : launch_h<HNarrow>(x, w, y, N, H, W, Ci, Co, s);
+  if (rc == -1) rc = h_wide(M, Co) ? launch_h<HWide>(x, w, y, N, H, W, Ci, Co, s) : launch_h<HNarrow>(x, w, y, N, H, W, Ci, Co, s);
   if (rc != -4) return rc;
   // halo larger than the LDS buffer (tiny W): per-tap staging
   if (Co % 128 == 0) return launch<CfWide>(x, w, y, N, H, W, Ci, Co, s);
@@ -1007,7 +1010,7 @@ int pdt_conv3x3s1_fwd_stats(const uint16_t* x, const uint16_t* w, uint16_t* y, f
     return rc == -4 ? -5 : rc;
   }
   if (halo_rows_bound(H, W, 256) > 512) return -5;
-  return Co % 128 == 0 ? launch_h<HWide, true>(x, w, y, N, H, W, Ci, Co, s, part)
+  return h_wide(M, Co) ? launch_h<HWide, true>(x, w, y, N, H, W, Ci, Co, s, part)
                        : launch_h<HNarrow, true>(x, w, y, N, H, W, Ci, Co, s, part);
 }
 
@@ -1024,7 +1027,7 @@ int pdt_conv3x3s1_fwd_bnbwd(const uint16_t* x, const uint16_t* w, uint16_t* y, c
   if (Ci == 64 && Co == 64) return -5;  // weight-stationary kernel: its epilogue reduction did not pay
   if (halo_rows_bound(H, W, 256) > 512) return -5;
   const BnSrc bs{bn_x, bn_mask, bn_mean, bn_part};
-  return Co % 128 == 0 ? launch_h<HWide, false, true>(x, w, y, N, H, W, Ci, Co, s, nullptr, bs)
+  return h_wide(M, Co) ? launch_h<HWide, false, true>(x, w, y, N, H, W, Ci, Co, s, nullptr, bs)
                        : launch_h<HNarrow, false, true>(x, w, y, N, H, W, Ci, Co, s, nullptr, bs);
 }
 

@@ -252,7 +252,8 @@ int launch_cf(const uint16_t* x, const uint16_t* w, uint16_t* y, float* part, co
 template <bool STATS, bool BSTATS>
 int launch(const uint16_t* x, const uint16_t* w, uint16_t* y, float* part, const BnSrc& bs, const Geo& g,
            hipStream_t s) {
-  if (g.Co % 128 == 0) return launch_cf<S2Cfg<128>, STATS, BSTATS>(x, w, y, part, bs, g, s);
+  if (g.Co % 128 == 0 && !small_grid_narrow((int64_t)g.nph * g.tpp * (g.Co / 128)))
+    return launch_cf<S2Cfg<128>, STATS, BSTATS>(x, w, y, part, bs, g, s);
   return launch_cf<S2Cfg<64>, STATS, BSTATS>(x, w, y, part, bs, g, s);
 }
 

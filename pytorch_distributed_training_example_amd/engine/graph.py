@@ -67,7 +67,11 @@ class StaticStep:
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph, pool=self._pool):
+        # thread_local: the RCCL process group's watchdog thread polls completion events of collectives
+        # issued before the capture; under the default "global" mode HIP rejects those queries while any
+        # stream captures (hipErrorStreamCaptureUnsupported -> watchdog exception -> process abort, seen in
+        # graphed bench runs). Capture itself is per stream: the step's kernels are captured either way.
+        with torch.cuda.graph(self.graph, pool=self._pool, capture_error_mode="thread_local"):
             self.static_loss = self.fn(*self.static_inputs)
         torch.cuda.synchronize()
 
