@@ -28,11 +28,12 @@ struct PrepBatch {
 };
 
 __global__ __launch_bounds__(256) void weight_prep_kernel(PrepBatch b) {
-  __shared__ uint16_t tile[kT][kT + 2];
+  __shared__ uint16_t tile[kT][kT + 8];  // +8: 16-B aligned rows, 4-bank shift per row
   const PrepItem& p = b.it[blockIdx.y];
   const int tr = (p.R + kT - 1) / kT, tc = (p.C + kT - 1) / kT;
   const int ntiles = tr * tc * p.taps;
   const int tid = threadIdx.x;
+  const bool vec = (p.C % 8 == 0) && (p.R % 8 == 0);  // 16-B rows both ways (every ResNet conv)
   for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const int tap = t / (tr * tc), rc = t % (tr * tc);
     const int r0 = (rc / tc) * kT, c0 = (rc % tc) * kT;
@@ -40,17 +41,40 @@ __global__ __launch_bounds__(256) void weight_prep_kernel(PrepBatch b) {
     const uint16_t* src = p.src + (int64_t)stap * p.C;
     uint16_t* dst = p.dst + (int64_t)tap * p.R;
     const int64_t srs = (int64_t)p.taps * p.C, drs = (int64_t)p.taps * p.R;
-    // read 64 rows x 64 columns (a lane per column, 4 rows per pass)
-    for (int i = tid; i < kT * kT; i += 256) {
-      const int r = i / kT, c = i % kT;
-      const int gr = r0 + r, gc = c0 + c;
-      tile[r][c] = (gr < p.R && gc < p.C) ? src[gr * srs + gc] : (uint16_t)0;
-    }
-    __syncthreads();
-    for (int i = tid; i < kT * kT; i += 256) {
-      const int c = i / kT, r = i % kT;
-      const int gr = r0 + r, gc = c0 + c;
-      if (gr < p.R && gc < p.C) dst[gc * drs + gr] = tile[r][c];
+    if (vec) {
+      // read: 64 rows x 8 pieces of 8 columns (16 B), 2 pieces per thread
+      for (int i = tid; i < kT * 8; i += 256) {
+        const int r = i >> 3, pc = (i & 7) * 8;
+        const int gr = r0 + r, gc = c0 + pc;
+        uint4 v = make_uint4(0u, 0u, 0u, 0u);
+        if (gr < p.R && gc < p.C) v = *reinterpret_cast<const uint4*>(src + gr * srs + gc);
+        *reinterpret_cast<uint4*>(&tile[r][pc]) = v;
+      }
+      __syncthreads();
+      // write: 64 dst rows (columns c) x 8 pieces of 8 consecutive r, gathered from the tile
+      for (int i = tid; i < kT * 8; i += 256) {
+        const int c = i >> 3, pr = (i & 7) * 8;
+        const int gr = r0 + pr, gc = c0 + c;
+        if (gr < p.R && gc < p.C) {
+          uint32_t w[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            w[k] = (uint32_t)tile[pr + 2 * k][c] | ((uint32_t)tile[pr + 2 * k + 1][c] << 16);
+          *reinterpret_cast<uint4*>(dst + gc * drs + gr) = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+      }
+    } else {
+      for (int i = tid; i < kT * kT; i += 256) {
+        const int r = i / kT, c = i % kT;
+        const int gr = r0 + r, gc = c0 + c;
+        tile[r][c] = (gr < p.R && gc < p.C) ? src[gr * srs + gc] : (uint16_t)0;
+      }
+      __syncthreads();
+      for (int i = tid; i < kT * kT; i += 256) {
+        const int c = i / kT, r = i % kT;
+        const int gr = r0 + r, gc = c0 + c;
+        if (gr < p.R && gc < p.C) dst[gc * drs + gr] = tile[r][c];
+      }
     }
     __syncthreads();
   }
@@ -75,7 +99,7 @@ int pdt_weight_prep(const uint16_t* const* src, uint16_t* const* dst, const int*
     const int tiles = ((R[i] + kT - 1) / kT) * ((C[i] + kT - 1) / kT) * taps[i];
     most = tiles > most ? tiles : most;
   }
-  const int gx = most < 64 ? most : 64;  // tiles per item in flight; the grid strides over the rest
+  const int gx = most < 128 ? most : 128;  // tiles per item in flight; the grid strides over the rest
   hipLaunchKernelGGL(weight_prep_kernel, dim3(gx, n), dim3(256), 0, s, b);
   return 0;
 }

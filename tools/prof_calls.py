@@ -35,7 +35,7 @@ def main():
         wg = int(r.get("Workgroup_Size_X", r.get("Workgroup_Size", 1)) or 1)
         grid = int(r.get("Grid_Size_X", r.get("Grid_Size", 0)) or 0)
         if us >= min_us:
-            k = r["Kernel_Name"]
+            k = r["Kernel_Name"].replace("(anonymous namespace)::", "")
             k = k[:k.find("(")] if "(" in k else k
             print(f"| {i} | {us:.1f} | {grid // max(wg, 1)} | {wg} | `{k[:100]}` |")
     print(f"\n{len(last)} launches, {tot / 1e3:.2f} ms busy in the step")
