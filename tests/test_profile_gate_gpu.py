@@ -48,9 +48,11 @@ def test_resnet_step_runs_our_kernels():
     assert names, "no device kernels recorded"
     for ours in ("bn_reduce3_kernel", "bn_fin_kernel", "bn_apply_kernel", "bn_bwd_apply_kernel",
                  "bn_apply_pool_kernel", "maxpool_bwd_kernel", "ce_fwd_kernel", "ce_bwd_kernel", "mt_kernel",
-                 "conv3x3wst_kernel", "conv3x3h_kernel", "conv3x3_flip_kernel", "stem_conv_kernel",
+                 "conv3x3wst_kernel", "conv3x3h_kernel", "weight_prep_kernel", "stem_conv_kernel",
                  "stem_wgrad_kernel", "conv1x1_kernel", "conv3x3_wgrad_kernel", "conv3x3_wgrad_reduce_kernel"):
         assert _has(names, ours), (ours, sorted(set(names))[:40])
+    # the backward weight transforms run batched (weight_prep.hip), not per conv
+    assert not _has(names, "conv3x3_flip_kernel"), "per-conv 3x3 weight flips in the step"
     for stock in ("MIOpenBatchNorm", "batch_norm", "max_pool", "nll_loss", "log_softmax"):
         assert not _has(names, stock), (stock, [n for n in names if stock in n][:5])
     # residual gradients meet in conv1's dgrad GEMM: no per-block autograd add kernels (16 before).
