@@ -1,9 +1,19 @@
 """Group a prof_window.py *_kernels.csv by kernel family (ms per step)."""
 import csv
+import re
 import sys
 
 
 def family(n):
+    if "conv1x1_bwd_fused" in n or "fb_reduce" in n:
+        return "fused conv3 + BN3 backward (dgrad + wgrad + BN apply/reduction)"
+    m = re.search(r"conv1x1_kernel<(.*?)>\s*\(", n)
+    if m and m.group(1).rstrip().endswith("true"):
+        return "1x1 GEMM + BN(+res)+ReLU apply epilogue (recomputed conv3)"
+    if "conv1x1_wgrad" in n:
+        return "our 1x1 weight gradient (MFMA)"
+    if "weight_prep" in n:
+        return "batched weight transforms"
     if "bn_" in n or "maxpool" in n:
         return "our BN (+ReLU/residual/pool)"
     if "conv3x3" in n:
