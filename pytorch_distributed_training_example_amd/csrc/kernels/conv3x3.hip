@@ -403,11 +403,16 @@ __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv3x3h_kernel(
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
-  if constexpr (STATS)  // BatchNorm statistics of the staged bf16 tile (tile_stats.h)
-    tile_bn_stats<BM, BN, Cf::kThreads, Cf::kEpiStride>(lds, reinterpret_cast<float*>(lds + BM * Cf::kEpiStride),
-                                                         min(BM, M - m0), part, m0 / BM, (M + BM - 1) / BM, Co, n0);
   constexpr int kChunks = BN / 8;
   static_assert(Cf::kThreads % kChunks == 0, "a thread keeps one 8-channel chunk");
+  // STATS: BatchNorm statistics of the stored bf16 values from the epilogue's registers (tile_stats.h
+  // RowStats8: no extra passes over the staged tile)
+  RowStats8 rst;
+  float kst = 0.f;
+  if constexpr (STATS) {
+    rs8_init(rst, *reinterpret_cast<const uint4*>(lds + (tid % kChunks) * 16));
+    if (tid < BN) kst = __uint_as_float((uint32_t)*reinterpret_cast<const uint16_t*>(lds + tid * 2) << 16);
+  }
   float bs1[8], bs2[8], bmu[8];
   if constexpr (BSTATS) {
     const int c = tid % kChunks;
@@ -427,12 +432,18 @@ __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv3x3h_kernel(
         const unsigned mk = bs.mask ? bs.mask[off >> 3] : 0xffu;
         bn_bwd_accum8(v, xb, mk, bmu, bs1, bs2);
       }
+      if constexpr (STATS) rs8_add(rst, v);
       *reinterpret_cast<uint4*>(Y + off) = v;
     }
   }
   if constexpr (BSTATS)  // every wave is done reading the staged tile: its LDS holds the block sums
     bn_bwd_tile_store<BN, Cf::kWaves>(bs1, bs2, reinterpret_cast<float*>(lds), bs.part, (M + BM - 1) / BM, m0 / BM,
                                       Co, n0);
+  if constexpr (STATS) {
+    __syncthreads();  // (likewise)
+    rs8_tile_store<BN, Cf::kWaves>(rst, kst, reinterpret_cast<float*>(lds), part, min(BM, M - m0), (M + BM - 1) / BM,
+                                   m0 / BM, Co, n0);
+  }
 }
 
 // ---------------------------------------------------------------- warp-specialised halo variant

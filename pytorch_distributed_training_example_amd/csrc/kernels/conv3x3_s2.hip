@@ -199,10 +199,13 @@ __global__ __launch_bounds__(Cf::kThreads, 4) void conv3x3g_kernel(const uint16_
     }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __syncthreads();
-  if constexpr (STATS)  // forward only (one phase, output rows = GEMM rows)
-    tile_bn_stats<kBM, kBN, kThreads, kEpiStride>(lds, reinterpret_cast<float*>(lds + kBM * kEpiStride),
-                                                  min(kBM, M - m0), part, mt, g.T, g.Co, n0);
   constexpr int kChunks = kBN / 8;
+  RowStats8 rst;  // STATS (forward only: one phase, output rows = GEMM rows), tile_stats.h RowStats8
+  float kst = 0.f;
+  if constexpr (STATS) {
+    rs8_init(rst, *reinterpret_cast<const uint4*>(lds + (tid % kChunks) * 16));
+    if (tid < kBN) kst = __uint_as_float((uint32_t)*reinterpret_cast<const uint16_t*>(lds + tid * 2) << 16);
+  }
   float bs1[8], bs2[8], bmu[8];
   if constexpr (BSTATS) {
     const int c = tid % kChunks;
@@ -226,10 +229,15 @@ __global__ __launch_bounds__(Cf::kThreads, 4) void conv3x3g_kernel(const uint16_
       const unsigned mk = bs.mask ? bs.mask[off >> 3] : 0xffu;
       bn_bwd_accum8(v, xb, mk, bmu, bs1, bs2);
     }
+    if constexpr (STATS) rs8_add(rst, v);
     *reinterpret_cast<uint4*>(Y + off) = v;
   }
   if constexpr (BSTATS)  // every wave is done reading the staged tile: its LDS holds the block sums
     bn_bwd_tile_store<kBN, kWaves>(bs1, bs2, reinterpret_cast<float*>(lds), bs.part, g.T, ph * g.tpp + mt, g.Co, n0);
+  if constexpr (STATS) {
+    __syncthreads();
+    rs8_tile_store<kBN, kWaves>(rst, kst, reinterpret_cast<float*>(lds), part, min(kBM, M - m0), g.T, mt, g.Co, n0);
+  }
 }
 
 template <class Cf, bool STATS, bool BSTATS>
