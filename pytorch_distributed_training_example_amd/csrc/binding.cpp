@@ -186,6 +186,7 @@ int pdt_leaky_pool_bwd(const float* dy, const uint8_t* code, int64_t planes, int
                        hipStream_t s);
 int pdt_softmax_nll_small(const void* logits, int dtype, const int64_t* target, int64_t N, int V, int mode,
                           float smoothing, float* loss, void* dlogits, float dscale, double* acc, hipStream_t s);
+int pdt_mean_small(const float* v, int64_t n, float scale, float* out, hipStream_t s);
 }
 
 namespace {
@@ -1777,8 +1778,11 @@ Tensor leaky_pool_bwd(Tensor dy, Tensor code, int64_t H, int64_t W, double slope
 }
 
 // returns {loss[N] (if want_loss), dlogits (if want_grad)}; acc (fp64 [3]) accumulates eval metrics
+// mean_scale > 0 (with want_loss): also {.., mean_scale * sum(loss)} as a 0-d fp32 tensor (fixed-order
+// one-workgroup sum; the training loss without a torch reduction per step).
 std::vector<Tensor> softmax_nll_small(Tensor logits, Tensor target, int64_t mode, double smoothing, bool want_loss,
-                                      bool want_grad, double dscale, c10::optional<Tensor> acc) {
+                                      bool want_grad, double dscale, c10::optional<Tensor> acc,
+                                      double mean_scale) {
   check_cuda(logits, "logits");
   TORCH_CHECK(logits.dim() == 2 && logits.is_contiguous(), "softmax_nll_small: contiguous [N, V] logits");
   TORCH_CHECK(logits.size(1) <= 1024, "softmax_nll_small: V <= 1024");
@@ -1797,6 +1801,11 @@ std::vector<Tensor> softmax_nll_small(Tensor logits, Tensor target, int64_t mode
                                  want_loss ? loss.data_ptr<float>() : nullptr, want_grad ? dl.data_ptr() : nullptr,
                                  (float)dscale, ap, stream());
   TORCH_CHECK(rc == 0, "pdt_softmax_nll_small failed");
+  if (mean_scale > 0.0 && want_loss) {
+    auto mean = at::empty({}, logits.options().dtype(at::kFloat));
+    pdt_mean_small(loss.data_ptr<float>(), N, (float)mean_scale, mean.data_ptr<float>(), stream());
+    return {loss, dl, mean};
+  }
   return {loss, dl};
 }
 
@@ -1891,5 +1900,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("leaky_pool_bwd", &leaky_pool_bwd);
   m.def("lenet_tail_fwd", &lenet_tail_fwd);
   m.def("lenet_tail_bwd", &lenet_tail_bwd);
-  m.def("softmax_nll_small", &softmax_nll_small);
+  m.def("softmax_nll_small", &softmax_nll_small, py::arg("logits"), py::arg("target"), py::arg("mode"),
+        py::arg("smoothing"), py::arg("want_loss"), py::arg("want_grad"), py::arg("dscale"), py::arg("acc"),
+        py::arg("mean_scale") = 0.0);
 }

@@ -36,6 +36,19 @@ def available() -> bool:
     return _load() is not None
 
 
+_CUDA_OK: list = []
+
+
+def cuda_available() -> bool:
+    """``torch.cuda.is_available()``, asked once per process: it re-enumerates the devices on every call
+    (~130 us on the MI355X box), and the optimizer / DDP reducer asked it every step (cProfile of the
+    LeNet eager step, round 4)."""
+    if not _CUDA_OK:
+        import torch
+        _CUDA_OK.append(torch.cuda.is_available())
+    return _CUDA_OK[0]
+
+
 def disabled() -> bool:
     return SW.disable_native
 

@@ -118,10 +118,13 @@ class _SoftmaxNLLFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, logits, target, mode, smoothing):
         n = logits.shape[0]
-        loss, dl = native().softmax_nll_small(logits, target, _MODES[mode], smoothing, True, True,
-                                              1.0 / max(n, 1), None)
+        if n == 0:
+            ctx.save_for_backward(torch.empty_like(logits))
+            return logits.new_zeros((), dtype=torch.float32)
+        _, dl, mean = native().softmax_nll_small(logits, target, _MODES[mode], smoothing, True, True, 1.0 / n, None,
+                                                 mean_scale=1.0 / n)
         ctx.save_for_backward(dl)
-        return loss.sum() / max(n, 1)
+        return mean
 
     @staticmethod
     def backward(ctx, dloss):

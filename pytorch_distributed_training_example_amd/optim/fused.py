@@ -25,11 +25,11 @@ from typing import Dict, List, Optional, Tuple
 import torch
 from torch.optim import Optimizer
 
-from ..ops._native import native, use_native
+from ..ops._native import cuda_available, native, use_native
 
 
 def _capturing() -> bool:
-    return torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+    return cuda_available() and torch.cuda.is_current_stream_capturing()
 
 
 class _FusedOptimizer(Optimizer):

@@ -35,6 +35,7 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
+from ..ops._native import cuda_available
 from ..ops import multi_tensor
 from .buckets import (DEFAULT_BUCKET_CAP_MB, DEFAULT_FIRST_BUCKET_BYTES, BucketSpec,
                       compute_bucket_assignment)
@@ -343,7 +344,7 @@ class DistributedDataParallel(nn.Module):
                                       group=self.process_group, async_op=True)
 
     def _finalize_backward(self) -> None:
-        timing = self._comm_timing and torch.cuda.is_available() and not torch.cuda.is_current_stream_capturing()
+        timing = self._comm_timing and cuda_available() and not torch.cuda.is_current_stream_capturing()
         if timing:  # backward's compute is all queued: from here the compute stream waits on comm
             e0 = torch.cuda.Event(enable_timing=True)
             e0.record()
