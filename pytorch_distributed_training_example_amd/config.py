@@ -36,10 +36,11 @@ PDT_BN2_DEFER               0            1: with PDT_BWD_FUSED, bn2's apply + Re
                                          in the forward GEMM, recomputed in the fused backward, which writes bn2's
                                          mask). Measured -0.2 %, and -2 % with PDT_BN_APPLY_GEMM_K (the relu(a x + b)
                                          operand transform then runs in both GEMM passes): off
-PDT_BN_APPLY_GEMM_K         128          a BatchNorm(+residual)+ReLU apply after a 1x1 conv with <= this many input
+PDT_BN_APPLY_GEMM_K         64           a BatchNorm(+residual)+ReLU apply after a 1x1 conv with <= this many input
                                          channels runs as that conv's GEMM again with the apply epilogue (reads
                                          the conv input, C/4 channels, instead of its output; 0 = off). With the
-                                         256-channel GEMM tiles: +0.7 % (layers 1-2); 256 (adds layer 3): -0.6 %
+                                         256-channel GEMM tiles: 128 (layers 1-2) +0.7 % over off; 64 (layer 1
+                                         only) +0.2 % over 128 in two same-box A/Bs; 256 (adds layer 3) -0.6 %
                                          (profiles/r4/ab_bn_apply_gemm.md)
 PDT_LINEAR_EPILOGUE         0            1: Linear forward GEMMs (+bias, MLP fc1+bias+GELU) on our MFMA kernel
                                          (gemm.hip; 0.61-0.94x of tuned hipBLASLt, so off)
@@ -92,7 +93,7 @@ class _Switches:
         self.linear_epilogue = e("PDT_LINEAR_EPILOGUE", "0") == "1"
         self.bwd_fused = on("PDT_BWD_FUSED")
         self.bn2_defer = on("PDT_BN2_DEFER", "0")
-        self.bn_apply_gemm_k = int(e("PDT_BN_APPLY_GEMM_K", "128"))
+        self.bn_apply_gemm_k = int(e("PDT_BN_APPLY_GEMM_K", "64"))
         return self
 
 
