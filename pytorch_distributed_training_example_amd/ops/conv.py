@@ -467,8 +467,9 @@ def _bwd_fused(ctx, d, x, weight):
 
 
 def fused_bwd_shape_ok(weight: torch.Tensor) -> bool:
-    """(Co, Ci) of a 1x1 conv whose backward conv1x1_bwd_fused takes (ResNet-50 layer-1 / layer-2 conv3)."""
-    return weight.dim() == 4 and tuple(weight.shape[:2]) in ((256, 64), (512, 128)) and weight.dtype == torch.bfloat16
+    """(Co, Ci) of a 1x1 conv whose backward conv1x1_bwd_fused takes (ResNet-50 layer-1 / layer-2 conv3;
+    ``PDT_BWD_FUSED_SHAPES``, e.g. "256x64", restricts the set)."""
+    return weight.dim() == 4 and tuple(weight.shape[:2]) in SW.bwd_fused_shapes and weight.dtype == torch.bfloat16
 
 
 def _subsample_native(t: torch.Tensor) -> bool:
