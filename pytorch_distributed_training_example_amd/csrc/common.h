@@ -21,13 +21,16 @@ namespace pdt {
 
 // Small grids (the reference's 128 images per rank at the 8-GPU point, ResNet layers 3-4): a conv whose
 // wide-tile grid gives fewer than one workgroup per CU takes the half-width tile instead (twice the
-// workgroups). PDT_SMALL_GRID_NARROW=0 turns it off (A/B), read once per process.
+// workgroups). PDT_SMALL_GRID_NARROW = the workgroup threshold (default 256 = one per CU; 0 = off),
+// read once per process.
 inline bool small_grid_narrow(int64_t wide_blocks) {
-  static const int on = [] {
+  static const int64_t thr = [] {
     const char* e = getenv("PDT_SMALL_GRID_NARROW");
-    return e && e[0] == '0' ? 0 : 1;
+    if (!e || !e[0]) return (int64_t)256;
+    const long v = strtol(e, nullptr, 10);
+    return (int64_t)(v == 1 ? 256 : (v < 0 ? 0 : v));  // "1" kept as "on" (earlier A/B scripts)
   }();
-  return on && wide_blocks < 256;
+  return wide_blocks < thr;
 }
 
 __device__ __forceinline__ float bf2f(uint16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
