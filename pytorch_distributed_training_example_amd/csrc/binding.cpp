@@ -114,6 +114,14 @@ int pdt_conv3x3s2_wgrad(const uint16_t* x, const uint16_t* dy, uint16_t* dw, flo
 int pdt_conv3x3s1_fwd_stats(const uint16_t* x, const uint16_t* w, uint16_t* y, float* part, int N, int H, int W,
                             int Ci, int Co, hipStream_t s);
 int64_t pdt_stem_conv_wprep_elems();
+int64_t pdt_stem_stats_parts(int N, int H, int W);
+int pdt_stem_conv_fwd_stats(const uint16_t* x, const uint16_t* w, uint16_t* wp, uint16_t* y, float* part, int N, int H,
+                            int W, hipStream_t s);
+int64_t pdt_bn_parts_ws_floats(int P, int C);
+int pdt_bn_relu_maxpool_fwd_train_parts(const float* part, int P, const uint16_t* x, const float* gamma,
+                                        const float* beta, float* running_mean, float* running_var, float momentum,
+                                        float eps, int N, int H, int W, int C, uint16_t* y, uint8_t* code, float* mean,
+                                        float* invstd, float* ws, hipStream_t s);
 int pdt_stem_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* wp, uint16_t* y, int N, int H, int W,
                       hipStream_t s);
 int64_t pdt_stem_wgrad_ws_floats();
@@ -461,6 +469,35 @@ std::vector<Tensor> bn_relu_maxpool_fwd(Tensor x, c10::optional<Tensor> weight, 
                                          mean.data_ptr<float>(), invstd.data_ptr<float>(), ws.data_ptr<float>(),
                                          bn_counters(x), stream());
   TORCH_CHECK(rc == 0, "pdt_bn_relu_maxpool_fwd_train failed");
+  return {y, code, mean, invstd};
+}
+
+// The same with the statistics from stem_conv_fwd_stats's partials (no reduce pass over x).
+std::vector<Tensor> bn_relu_maxpool_fwd_parts(Tensor x, Tensor part, c10::optional<Tensor> weight,
+                                              c10::optional<Tensor> bias, c10::optional<Tensor> running_mean,
+                                              c10::optional<Tensor> running_var, double momentum, double eps) {
+  check_nhwc_bf16(x, "x");
+  TORCH_CHECK(x.dim() == 4, "bn_relu_maxpool: 4-D NHWC input");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(C == 64, "bn_relu_maxpool_fwd_parts: C == 64 (the stem)");
+  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.is_contiguous() && part.dim() == 1 &&
+                  part.numel() % (2 * C + 1) == 0, "bn_relu_maxpool_fwd_parts: part [P * (2 C + 1)] f32");
+  const int64_t P = part.numel() / (2 * C + 1);
+  const int64_t Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  auto y = at::empty({N, C, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  auto code = at::empty({N * Ho * Wo * C}, x.options().dtype(at::kByte));
+  auto fopt = x.options().dtype(at::kFloat);
+  auto mean = at::empty({C}, fopt), invstd = at::empty({C}, fopt);
+  auto ws = at::empty({pdt_bn_parts_ws_floats((int)P, (int)C)}, fopt);
+  float* rm = running_mean.has_value() && running_mean->defined() ? running_mean->data_ptr<float>() : nullptr;
+  float* rv = running_var.has_value() && running_var->defined() ? running_var->data_ptr<float>() : nullptr;
+  int rc = pdt_bn_relu_maxpool_fwd_train_parts(part.data_ptr<float>(), (int)P,
+                                               reinterpret_cast<const uint16_t*>(x.data_ptr()), opt_fptr(weight),
+                                               opt_fptr(bias), rm, rv, (float)momentum, (float)eps, (int)N, (int)H,
+                                               (int)W, (int)C, reinterpret_cast<uint16_t*>(y.data_ptr()),
+                                               code.data_ptr<uint8_t>(), mean.data_ptr<float>(),
+                                               invstd.data_ptr<float>(), ws.data_ptr<float>(), stream());
+  TORCH_CHECK(rc == 0, "pdt_bn_relu_maxpool_fwd_train_parts failed: ", rc);
   return {y, code, mean, invstd};
 }
 
@@ -1271,6 +1308,29 @@ Tensor stem_conv_fwd(Tensor x, Tensor w) {
   return y;
 }
 
+// stem_conv_fwd plus the output's BatchNorm statistics -> {y, part} (part: P (2 * 64 + 1) floats, the
+// input of bn_relu_maxpool_fwd_parts); {} when it does not apply (W != 224).
+std::vector<Tensor> stem_conv_fwd_stats(Tensor x, Tensor w) {
+  check_nhwc_bf16(x, "x");
+  TORCH_CHECK(x.size(1) == 3 && x.size(3) % 32 == 0, "stem_conv: x [N, 3, H, W] with W % 32 == 0");
+  TORCH_CHECK(w.dim() == 4 && w.size(0) == 64 && w.size(1) == 3 && w.size(2) == 7 && w.size(3) == 7 &&
+              w.scalar_type() == at::kBFloat16, "stem_conv: weight [64, 3, 7, 7] bf16");
+  const int64_t N = x.size(0), H = x.size(2), W = x.size(3), OH = (H - 1) / 2 + 1, OW = W / 2;
+  const int64_t P = pdt_stem_stats_parts((int)N, (int)H, (int)W);
+  if (P == 0) return {};
+  w = w.contiguous(at::MemoryFormat::ChannelsLast);
+  auto wp = at::empty({pdt_stem_conv_wprep_elems()}, w.options());
+  auto y = at::empty({N, 64, OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  auto part = at::empty({P * (2 * 64 + 1)}, x.options().dtype(at::kFloat));
+  const int rc = pdt_stem_conv_fwd_stats(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                                         reinterpret_cast<const uint16_t*>(w.data_ptr()),
+                                         reinterpret_cast<uint16_t*>(wp.data_ptr()),
+                                         reinterpret_cast<uint16_t*>(y.data_ptr()), part.data_ptr<float>(), (int)N,
+                                         (int)H, (int)W, stream());
+  TORCH_CHECK(rc == 0, "pdt_stem_conv_fwd_stats failed: ", rc);
+  return {y, part};
+}
+
 // Weight gradient of stem_conv_fwd: dw [64, 3, 7, 7] (channels_last) from x and dy [N, 64, OH, OW]
 // (channels_last); W % 32 == 0 and W <= 224.
 Tensor stem_conv_wgrad(Tensor x, Tensor dy) {
@@ -1830,6 +1890,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("res_ab") = py::none(), py::arg("apply") = true);
   m.def("bn_fwd_eval", &bn_fwd_eval);
   m.def("bn_relu_maxpool_fwd", &bn_relu_maxpool_fwd);
+  m.def("bn_relu_maxpool_fwd_parts", &bn_relu_maxpool_fwd_parts);
   m.def("maxpool3s2_bwd", &maxpool3s2_bwd);
   m.def("conv1x1_gemm", &conv1x1_gemm, py::arg("a"), py::arg("b"), py::arg("out"), py::arg("acc"), py::arg("stats"),
         py::arg("c_in") = py::none(), py::arg("c_mask") = py::none(), py::arg("bn_x") = py::none(),
@@ -1858,6 +1919,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv3x3s2_dgrad", &conv3x3s2_dgrad, py::arg("dy"), py::arg("wf"), py::arg("H"), py::arg("W"),
         py::arg("bn_x") = py::none(), py::arg("bn_mask") = py::none(), py::arg("bn_mean") = py::none());
   m.def("stem_conv_fwd", &stem_conv_fwd);
+  m.def("stem_conv_fwd_stats", &stem_conv_fwd_stats);
   m.def("stem_conv_wgrad", &stem_conv_wgrad);
   m.def("stem_conv_wgrad_bn", &stem_conv_wgrad_bn);
   m.def("conv3x3s1_wgrad", &conv3x3s1_wgrad);

@@ -410,10 +410,11 @@ __global__ __launch_bounds__(1024) void bn_fin_kernel(const float* __restrict__ 
 // block (64 channels, tile range) -> double (S, Q) with Q = sum_t (M2_t + S_t^2 / n_t) — the
 // between-tile term in double, so E[x^2] - mean^2 never cancels in fp32. Level 2 finalizes.
 // CENTRED = false (backward partials: sum dz, sum dz (x - mean)): plain double sums, Q = sum_t q_t.
+// NCNT: partial t covers part[2 T C + t] rows (float) instead of BMt (the stem conv's per-wave partials).
 constexpr int kTilesPerBlock = 128;
 int g_tiles_fused = 1;  // pdt_bn_tiles_fused(0): the two-launch finalize (A/B)
 
-template <bool CENTRED>
+template <bool CENTRED, bool NCNT = false>
 __global__ __launch_bounds__(1024) void bn_tiles_l1_kernel(const float* __restrict__ part, int T, int BMt, int64_t M,
                                                            int C, double* __restrict__ out) {
   __shared__ double sm[2][16][64];
@@ -426,9 +427,9 @@ __global__ __launch_bounds__(1024) void bn_tiles_l1_kernel(const float* __restri
     const float s = part[(int64_t)t * C + c];
     const float q = part[((int64_t)T + t) * C + c];
     const int64_t rem = M - (int64_t)t * BMt;
-    const double n = (double)(rem < BMt ? rem : BMt);
+    const double n = NCNT ? (double)part[2 * (int64_t)T * C + t] : (double)(rem < BMt ? rem : BMt);
     S += (double)s;
-    Q += CENTRED ? (double)q + (double)s * (double)s / n : (double)q;
+    Q += CENTRED ? (double)q + (n > 0.0 ? (double)s * (double)s / n : 0.0) : (double)q;
   }
   sm[0][j][cl] = S;
   sm[1][j][cl] = Q;
@@ -449,7 +450,7 @@ __global__ __launch_bounds__(1024) void bn_tiles_l1_kernel(const float* __restri
 // order and finalizes. P == 1: no ticket. Deterministic: fixed summation order either way.
 __device__ unsigned g_tiles_ctr[64];  // one per 64-channel column (C <= 4096), zero at load, self-resetting
 
-template <bool CENTRED>
+template <bool CENTRED, bool NCNT = false>
 __global__ __launch_bounds__(1024) void bn_tiles_fin_kernel(const float* __restrict__ part, int T, int BMt, int64_t M,
                                                             int C, double* __restrict__ lv, FinArgs fa) {
   __shared__ double sm[2][16][64];
@@ -464,9 +465,9 @@ __global__ __launch_bounds__(1024) void bn_tiles_fin_kernel(const float* __restr
     const float s = part[(int64_t)t * C + c];
     const float q = part[((int64_t)T + t) * C + c];
     const int64_t rem = M - (int64_t)t * BMt;
-    const double n = (double)(rem < BMt ? rem : BMt);
+    const double n = NCNT ? (double)part[2 * (int64_t)T * C + t] : (double)(rem < BMt ? rem : BMt);
     S += (double)s;
-    Q += CENTRED ? (double)q + (double)s * (double)s / n : (double)q;
+    Q += CENTRED ? (double)q + (n > 0.0 ? (double)s * (double)s / n : 0.0) : (double)q;
   }
   sm[0][j][cl] = S;
   sm[1][j][cl] = Q;
@@ -1031,6 +1032,33 @@ int pdt_bn_relu_maxpool_fwd_train(const uint16_t* x, const float* gamma, const f
   launch_reduce<0>(x, nullptr, nullptr, nullptr, M, C, ws, counters, fa, s);
   const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
   const int64_t nvec = (int64_t)N * Ho * Wo * (C / 8);
+  hipLaunchKernelGGL(bn_apply_pool_kernel, dim3(row_grid((int64_t)N * Ho)), dim3(256), 0, s, x, a, b, y, code, N, H, W, C,
+                     Ho, Wo);
+  return 0;
+}
+
+// pdt_bn_relu_maxpool_fwd_train with the statistics from the stem conv's partials (conv_stem.hip
+// pdt_stem_conv_fwd_stats: P partials with row counts, C == 64) instead of a reduce pass over x.
+// ws: pdt_bn_parts_ws_floats(P, C) floats.
+int64_t pdt_bn_parts_ws_floats(int P, int C) { return pdt_bn_tiles_ws_floats(P, C); }
+
+int pdt_bn_relu_maxpool_fwd_train_parts(const float* part, int P, const uint16_t* x, const float* gamma,
+                                        const float* beta, float* running_mean, float* running_var, float momentum,
+                                        float eps, int N, int H, int W, int C, uint16_t* y, uint8_t* code, float* mean,
+                                        float* invstd, float* ws, hipStream_t s) {
+  const int64_t M = (int64_t)N * H * W;
+  if (C % kCC != 0 || C / 64 > 64 || M < 1 || P < 1) return -1;
+  const int PB = (P + kTilesPerBlock - 1) / kTilesPerBlock;
+  double* lv = reinterpret_cast<double*>(ws);
+  float* a = ws + 4 * (int64_t)PB * C;
+  float* b = a + C;
+  FinArgs fa{};
+  fa.gamma = gamma; fa.beta = beta; fa.mean_out = mean; fa.invstd_out = invstd; fa.a_out = a;
+  fa.b_out = b; fa.running_mean = running_mean; fa.running_var = running_var; fa.momentum = momentum;
+  fa.eps = eps; fa.M = M;
+  // BMt = 1: unused (NCNT) but keeps the kernel's tail arithmetic in range
+  hipLaunchKernelGGL((bn_tiles_fin_kernel<true, true>), dim3(C / 64, PB), dim3(1024), 0, s, part, P, 1, M, C, lv, fa);
+  const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
   hipLaunchKernelGGL(bn_apply_pool_kernel, dim3(row_grid((int64_t)N * Ho)), dim3(256), 0, s, x, a, b, y, code, N, H, W, C,
                      Ho, Wo);
   return 0;

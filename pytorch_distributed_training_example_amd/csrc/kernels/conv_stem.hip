@@ -32,6 +32,7 @@
 //     non-persistent version (4-row tiles, 3 workgroups per CU, weights re-staged and the window
 //     loaded then waited on per tile) ran 384 us at batch 512 vs MIOpen's 860 us.
 #include "../common.h"
+#include "../tile_stats.h"
 
 #include <algorithm>
 
@@ -63,6 +64,7 @@ constexpr int kStPitch = kCo * 2 + 16;        // epilogue staging row (one pixel
 constexpr int kStage = 16 * kStPitch;         // per wave: one 16-pixel block
 constexpr int kLds = kLdsIn + kCo * kWPitch + kRowsOut * kStage;  // 64,496 B: window, weights, staging
 constexpr int kWPrepElems = kCo * 7 * 32;
+constexpr int kLdsStats = kLds + kRowsOut * 64 * 3 * 8;  // + per-lane (K, S, Q) pairs of the statistics variant
 
 __device__ __forceinline__ f4 mfma(bf16x8 a, bf16x8 b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
@@ -132,18 +134,20 @@ __device__ __forceinline__ void store_window(const Window& wv, char* lin, int ti
 #ifndef PDT_STEM_PROBE
 #define PDT_STEM_PROBE 0  // diagnostics only (tools/convbench/stem_bench.cpp): 1 = no Y stores, 2 = no MFMA, 3 = no window loads
 #endif
-template <bool FULL>  // FULL: every column tile is 112 wide (OW % 112 == 0): no per-block predicates
+// STATS (FULL and OW == 112 only): BatchNorm statistics of the stored output, per wave over all its
+// tiles — see the comment above pdt_stem_conv_fwd_stats.
+template <bool FULL, bool STATS = false>  // FULL: every column tile is 112 wide (OW % 112 == 0): no per-block predicates
 __global__ __launch_bounds__(kThreads, 2) void stem_conv_kernel(const uint16_t* __restrict__ X,
                                                           const uint16_t* __restrict__ Wp,
                                                           uint16_t* __restrict__ Y, int H, int W, int OH, int OW,
-                                                          int nrt, int nct, int ntiles) {
+                                                          int nrt, int nct, int ntiles, float* __restrict__ part) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   char* const lw = lds + kLdsIn;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int per = ntiles / gridDim.x, rem = ntiles % gridDim.x;
   const int t0 = blockIdx.x * per + min((int)blockIdx.x, rem);
   const int cnt = per + ((int)blockIdx.x < rem ? 1 : 0);
-  if (cnt == 0) return;
+  if (cnt == 0) return;  // never: grid <= ntiles
 
   auto coords = [&](int t, int& n, int& oh0, int& ow0) {
     const int ct = t % nct, rt = (t / nct) % nrt;
@@ -166,6 +170,14 @@ __global__ __launch_bounds__(kThreads, 2) void stem_conv_kernel(const uint16_t* 
   const int pl = lane & 15, g = lane >> 4;
   const char* wrow = lw + pl * kWPitch + g * 16;
   char* const stage = lw + kCo * kWPitch + wid * kStage;
+  // statistics: lane = channel pair (lane & 31) x 8 of the block's 16 pixels (lane >> 5); shifted
+  // sums about K = the wave's first stored value of the pair (packed fp32)
+  // (K, S, Q) live in a per-lane LDS slot between tiles, not in registers: this kernel sits at its
+  // 256-VGPR budget (carrying them spilled to scratch)
+  pdt_f2* const sst = reinterpret_cast<pdt_f2*>(lds + kLds) + (wid * 64 + lane) * 3;
+  bool kset = false;
+  int nrows = 0;
+  const char* const srd = stage + (lane >> 5) * 8 * kStPitch + (lane & 31) * 4;
   for (int k = 0; k < cnt; ++k) {
     const int t = t0 + k;
     coords(t, n, oh0, ow0);
@@ -223,6 +235,25 @@ __global__ __launch_bounds__(kThreads, 2) void stem_conv_kernel(const uint16_t* 
             *reinterpret_cast<uint2*>(stage + pl * kStPitch + j * 32 + g * 8) =
                 make_uint2(pk2(v[0], v[1]), pk2(v[2], v[3]));
           }
+          if constexpr (STATS) {  // the wave's own staging writes above complete in order first
+            pdt_f2 sk, ss, sq;
+            if (!kset) {
+              const uint32_t kw = *reinterpret_cast<const uint32_t*>(stage + (lane & 31) * 4);
+              sk = pdt_f2{__uint_as_float(kw << 16), __uint_as_float(kw & 0xffff0000u)};
+              ss = sq = pdt_f2{0.f, 0.f};
+              kset = true;
+            } else {
+              sk = sst[0]; ss = sst[1]; sq = sst[2];
+            }
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+              const uint32_t w = *reinterpret_cast<const uint32_t*>(srd + r * kStPitch);
+              const pdt_f2 d = pdt_f2{__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)} - sk;
+              ss += d;
+              sq = d * d + sq;
+            }
+            sst[0] = sk; sst[1] = ss; sst[2] = sq;
+          }
 #pragma unroll
           for (int h = 0; h < 2; ++h) {  // the wave's own LDS writes above complete in order first
             const int idx = lane + 64 * h, px = idx >> 3, c = idx & 7;
@@ -232,10 +263,26 @@ __global__ __launch_bounds__(kThreads, 2) void stem_conv_kernel(const uint16_t* 
           }
         }
       }
+      nrows += OW;
     }
     if (PDT_STEM_PROBE != 3 && k + 1 < cnt) {
       __syncthreads();  // every wave is done reading window k
       store_window(wv, lds, tid);
+    }
+  }
+  if constexpr (STATS) {  // partial p = (workgroup, wave): S = n K + sum (y - K), M2 = sum (y - K)^2 - sum (y - K)^2 / n
+    pdt_f2 sk = pdt_f2{0.f, 0.f}, ss = sk, sq = sk;
+    if (kset) { sk = sst[0]; ss = sst[1]; sq = sst[2]; }
+    ss += pdt_f2{__shfl_xor(ss.x, 32, 64), __shfl_xor(ss.y, 32, 64)};
+    sq += pdt_f2{__shfl_xor(sq.x, 32, 64), __shfl_xor(sq.y, 32, 64)};
+    if (lane < 32) {
+      const int P = gridDim.x * kRowsOut, p = blockIdx.x * kRowsOut + wid;
+      const float n = (float)nrows;
+      const float inv = nrows > 0 ? 1.f / n : 0.f;
+      *reinterpret_cast<float2*>(part + (int64_t)p * kCo + 2 * lane) = make_float2(fmaf(n, sk.x, ss.x), fmaf(n, sk.y, ss.y));
+      *reinterpret_cast<float2*>(part + (int64_t)(P + p) * kCo + 2 * lane) =
+          make_float2(fmaxf(sq.x - ss.x * ss.x * inv, 0.f), fmaxf(sq.y - ss.y * ss.y * inv, 0.f));
+      if (lane == 0) part[(int64_t)2 * P * kCo + p] = n;
     }
   }
 }
@@ -584,10 +631,44 @@ extern "C" int pdt_stem_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t*
   hipLaunchKernelGGL(stem_wprep_kernel, dim3((kWPrepElems + 255) / 256), dim3(256), 0, s, w, wp);
   if (OW % kTW == 0)
     hipLaunchKernelGGL(stem_conv_kernel<true>, dim3(grid), dim3(kThreads), kLds, s, x, wp, y, H, W, OH, OW, nrt, nct,
-                       (int)ntiles);
+                       (int)ntiles, nullptr);
   else
     hipLaunchKernelGGL(stem_conv_kernel<false>, dim3(grid), dim3(kThreads), kLds, s, x, wp, y, H, W, OH, OW, nrt, nct,
-                       (int)ntiles);
+                       (int)ntiles, nullptr);
+  return hipGetLastError() == hipSuccess ? 0 : -4;
+}
+
+// Partials written by pdt_stem_conv_fwd_stats for an [N, 3, H, W] input: 0 when it does not apply
+// (it needs OW == 112, i.e. W == 224 — the ImageNet stem).
+extern "C" int64_t pdt_stem_stats_parts(int N, int H, int W) {
+  if (N < 1 || H < 1 || W / 2 != kTW || W % 32 != 0) return 0;
+  const int OH = (H - 1) / 2 + 1;
+  const int64_t ntiles = (int64_t)N * ((OH + kRowsOut - 1) / kRowsOut);
+  return std::min<int64_t>(ntiles, 2 * stem_ncu()) * kRowsOut;
+}
+
+// pdt_stem_conv_fwd plus the BatchNorm statistics of y in the epilogue, so the stem's BatchNorm never
+// reads y for them (that reduce pass over the 1.6 GB stem output took 320 us of a 1024-image step):
+// each wave reads back the 16 x 64 block it just staged in LDS (the bf16 values stored) and keeps
+// shifted sums of its channel pair over every row it owns; at the end it writes one partial.
+// part (floats, P = pdt_stem_stats_parts): [P][64] sums S_p, [P][64] centred M2_p, [P] row counts n_p
+// — consumed by pdt_bn_relu_maxpool_fwd_train_parts. (A first statistics epilogue with Chan merges of
+// per-lane accumulators spilled; this one keeps 6 VGPRs across tiles.)
+extern "C" int pdt_stem_conv_fwd_stats(const uint16_t* x, const uint16_t* w, uint16_t* wp, uint16_t* y, float* part,
+                                       int N, int H, int W, hipStream_t s) {
+  const int64_t P = pdt_stem_stats_parts(N, H, W);
+  if (P == 0) return -1;
+  static const bool attr_ok = hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_conv_kernel<true, true>),
+                                                  hipFuncAttributeMaxDynamicSharedMemorySize, kLdsStats) == hipSuccess;
+  if (!attr_ok) return -2;
+  const int OH = (H - 1) / 2 + 1, OW = W / 2;
+  const int nrt = (OH + kRowsOut - 1) / kRowsOut, nct = 1;
+  const int64_t ntiles = (int64_t)N * nrt;
+  if (ntiles > 0x7fffffff || (int64_t)N * H > 0x7fffffff / 4) return -3;
+  const int grid = (int)(P / kRowsOut);
+  hipLaunchKernelGGL(stem_wprep_kernel, dim3((kWPrepElems + 255) / 256), dim3(256), 0, s, w, wp);
+  hipLaunchKernelGGL((stem_conv_kernel<true, true>), dim3(grid), dim3(kThreads), kLdsStats, s, x, wp, y, H, W, OH, OW, nrt,
+                     nct, (int)ntiles, part);
   return hipGetLastError() == hipSuccess ? 0 : -4;
 }
 

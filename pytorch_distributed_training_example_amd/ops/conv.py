@@ -749,15 +749,22 @@ class _StemBlockFn(torch.autograd.Function):
     node, so its backward can hand the BatchNorm's backward apply to the stem weight-gradient kernel:
     the pool-gradient kernel takes the BN reduction and yields dz (the gradient at the BN output) and
     the dx coefficients, and ``stem_conv_wgrad_bn`` forms dx = A dz + B (x - mean) + D while loading
-    its operand — the BN's dx (1.6 GB at batch 1024) is never written or read back. Forward is the
-    same two kernels as the unfused modules (stem conv, BN + ReLU + pool)."""
+    its operand — the BN's dx (1.6 GB at batch 1024) is never written or read back. Forward: the stem
+    conv with the BN statistics in its epilogue (``PDT_STEM_BN_STATS``, 224-wide images), then the BN
+    finalize + ReLU + pool kernel — or the unfused modules' kernels (stem conv; BN reduce, ReLU, pool)."""
 
     @staticmethod
     def forward(ctx, img, weight, gamma, beta, running_mean, running_var, momentum, eps):
         from ._native import native
         n = native()
-        xb = n.stem_conv_fwd(img, weight)
-        y, code, mean, invstd = n.bn_relu_maxpool_fwd(xb, gamma, beta, running_mean, running_var, momentum, eps)
+        r = n.stem_conv_fwd_stats(img, weight) if SW.stem_bn_stats else []
+        if r:  # the statistics come from the conv's epilogue partials: no reduce pass over xb
+            xb, part = r
+            y, code, mean, invstd = n.bn_relu_maxpool_fwd_parts(xb, part, gamma, beta, running_mean, running_var,
+                                                                momentum, eps)
+        else:
+            xb = n.stem_conv_fwd(img, weight)
+            y, code, mean, invstd = n.bn_relu_maxpool_fwd(xb, gamma, beta, running_mean, running_var, momentum, eps)
         ctx.save_for_backward(img, weight, xb, code, gamma, mean, invstd)
         return y
 

@@ -155,6 +155,40 @@ def test_stem_wgrad_with_fused_bn_apply(N, H, W):
     assert ((fused - ref).norm() / ref.norm()).item() < 1e-2
 
 
+@pytest.mark.parametrize("N,H", [(2, 224), (20, 224), (3, 30), (1, 8)])
+def test_stem_conv_bn_stats_epilogue(N, H):
+    """Stem conv with the BatchNorm statistics in its epilogue (stem_conv_fwd_stats, PDT_STEM_BN_STATS):
+    its output is the plain kernel's bit for bit, and the BN + ReLU + pool forward from its partials
+    (bn_relu_maxpool_fwd_parts) matches the reduce-pass path and an fp64 reference of the statistics.
+    (20, 224): more tiles than workgroups (several tiles per wave); (3, 30): waves with rows past OH."""
+    from pytorch_distributed_training_example_amd.ops._native import native
+    n = native()
+    cl = torch.channels_last
+    g = torch.Generator(device="cuda").manual_seed(N * H)
+    img = (torch.randn(N, 3, H, 224, device="cuda", generator=g) + 0.5).bfloat16().contiguous(memory_format=cl)
+    w = (torch.randn(64, 3, 7, 7, device="cuda", generator=g) * 0.1).bfloat16().contiguous(memory_format=cl)
+    gamma = torch.rand(64, device="cuda", generator=g) + 0.5
+    beta = torch.randn(64, device="cuda", generator=g) * 0.1
+    xb, part = n.stem_conv_fwd_stats(img, w)
+    assert torch.equal(xb, n.stem_conv_fwd(img, w))
+    assert n.stem_conv_fwd_stats(img[..., :192].contiguous(memory_format=cl), w) == []  # W != 224: not applicable
+    rm1, rv1 = torch.zeros(64, device="cuda"), torch.ones(64, device="cuda")
+    rm2, rv2 = rm1.clone(), rv1.clone()
+    y1, code1, mean1, inv1 = n.bn_relu_maxpool_fwd_parts(xb, part, gamma, beta, rm1, rv1, 0.1, 1e-5)
+    y2, code2, mean2, inv2 = n.bn_relu_maxpool_fwd(xb, gamma, beta, rm2, rv2, 0.1, 1e-5)
+    x64 = xb.double()
+    mu = x64.mean((0, 2, 3))
+    var = x64.var((0, 2, 3), unbiased=False)
+    torch.testing.assert_close(mean1.double(), mu, rtol=1e-5, atol=1e-5 * var.sqrt().max().item())
+    torch.testing.assert_close(inv1.double(), (var + 1e-5).rsqrt(), rtol=1e-4, atol=0)
+    torch.testing.assert_close(mean1, mean2, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(inv1, inv2, rtol=1e-5, atol=0)
+    torch.testing.assert_close(rm1, rm2, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(rv1, rv2, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(y1.float(), y2.float(), rtol=1e-2, atol=1e-2)
+    assert (code1 != code2).float().mean().item() < 1e-3  # argmax ties flip only where coefficients round apart
+
+
 def test_resnet_stem_block_node(switch):
     """ResNet-50's stem as one node (conv + BN + ReLU + pool, BN backward apply inside the weight-
     gradient kernel; PDT_STEM_BN_WGRAD=1) gives the forward output, running statistics and stem
