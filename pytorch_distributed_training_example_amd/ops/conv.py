@@ -345,7 +345,7 @@ class _Conv1x1Fn(torch.autograd.Function):
         gy = gy.contiguous(memory_format=torch.channels_last)
         x2, g2, w2 = _nhwc2d(x), _nhwc2d(gy), weight.reshape(Co, Ci)
         M = x2.shape[0]
-        dx = dw = None
+        dx = None
 
         def conv_bwd(mask):
             return torch.ops.aten.convolution_backward(gy, x, weight, None, [1, 1], [0, 0], [1, 1], False, [0, 0],
@@ -360,7 +360,20 @@ class _Conv1x1Fn(torch.autograd.Function):
         from .batchnorm import MaskedGrad
         # (the stride-2 shortcut's compact gradient added in our GEMM's epilogue instead of the
         # strided add pass below measured 0.4 % slower on ResNet-50 — hipBLASLt dgrad + add wins on
-        # those three shapes — and was removed; the kernel keeps the c_stride epilogue)
+        # those three shapes — so it is taken only where the same epilogue also takes the producing
+        # BatchNorm's backward reduction, which saves that BatchNorm a reduce pass: PDT_STRIDED_BSTATS)
+        if (strided is not None and SW.strided_bstats and not first and acc is None and ctx.needs_input_grad[0]
+                and ctx.gsrc is not None and ctx.gsrc.ready() and gy.dtype == torch.bfloat16
+                and _subsample_native(strided.t) and _ours_ok("dgrad", M, Co, Ci)):
+            from ._native import native
+            gs = ctx.gsrc
+            dx = torch.empty_like(x)
+            gpart = native().conv1x1_gemm(g2, _wt_of(weight, w2), _nhwc2d(dx), True, False, strided.t,
+                                          bn_x=gs.x, bn_mask=gs.mask, bn_mean=gs.mean, c_stride=strided.s, c_H=H,
+                                          c_W=W)
+            gs.deposit(gpart, dx)
+            strided = None
+            return dx, _Conv1x1Fn._wgrad(ctx, g2, x2, x, gy, weight, M, Ci, Co)
         # dx is final (nothing is added to it after the GEMM) unless this is the first of two linked
         # branches or a strided shortcut's gradient is added below: only then can the GEMM's epilogue
         # take the producing BatchNorm's backward reduction (GradStatsSource)
@@ -416,6 +429,17 @@ class _Conv1x1Fn(torch.autograd.Function):
             gs.deposit(gpart, dx)
         if first and dx is not None:  # first of the two branches: leave dx for the partner to add to
             ctx.link.grad, dx = dx, None
+        return dx, _Conv1x1Fn._wgrad(ctx, g2, x2, x, gy, weight, M, Ci, Co)
+
+    @staticmethod
+    def _wgrad(ctx, g2, x2, x, gy, weight, M, Ci, Co):
+        """dW of a 1x1 conv (None when not needed): the fastest of MIOpen / one GEMM / split-K GEMMs /
+        our one-pass kernel for the shape."""
+        dw = None
+
+        def conv_bwd(mask):
+            return torch.ops.aten.convolution_backward(gy, x, weight, None, [1, 1], [0, 0], [1, 1], False, [0, 0],
+                                                       1, mask)
         if ctx.needs_input_grad[1]:
             cands = {"miopen": lambda: conv_bwd([False, True, False]), "gemm": lambda: torch.mm(g2.t(), x2)}
             splitk_on = SW.wgrad_splitk
@@ -439,7 +463,7 @@ class _Conv1x1Fn(torch.autograd.Function):
             else:
                 wfn = lambda: conv_bwd([False, True, False])[1]  # noqa: E731
             dw = wfn()
-        return dx, dw
+        return dw
 
 
 def _bwd_fused(ctx, d, x, weight):

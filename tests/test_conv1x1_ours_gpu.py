@@ -442,6 +442,38 @@ def test_downsample_stride2_block_strided_grad(monkeypatch, switch):
         assert err < 2e-2, err
 
 
+def test_strided_shortcut_grad_with_bn_bwd_stats(monkeypatch, switch):
+    """A block followed by a stride-2 transition block: the transition conv1's data gradient adds the
+    shortcut's compact gradient AND takes the first block's bn3 backward reduction in one GEMM epilogue
+    (PDT_STRIDED_BSTATS=1) — gradients match the scatter-add + reduce-pass path (=0), and no
+    scatter-add ran."""
+    from pytorch_distributed_training_example_amd.models import resnet as R
+    from pytorch_distributed_training_example_amd.models.precision import to_bf16_mixed
+    from pytorch_distributed_training_example_amd.ops import conv as C
+    torch.manual_seed(0)
+    ds = R._Downsample(R.conv1x1(256, 512, 2), R._bn(512))
+    net = to_bf16_mixed(torch.nn.Sequential(R.Bottleneck(256, 64, 1, None), R.Bottleneck(256, 128, 2, ds))
+                        .cuda().to(memory_format=torch.channels_last))
+    x0 = torch.randn(8, 256, 28, 28, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    gy = torch.randn(8, 512, 14, 14, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    switch("PDT_CONV1X1", "ours")
+    adds = []
+    orig = C.StridedGrad.add_into
+    monkeypatch.setattr(C.StridedGrad, "add_into", lambda self, full: adds.append(1) or orig(self, full))
+    out = {}
+    for on in ("1", "0"):
+        switch("PDT_STRIDED_BSTATS", on)
+        adds.clear()
+        net.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_(True)
+        net(x).backward(gy)
+        out[on] = ([x.grad.float()] + [p.grad.float().clone() for p in net.parameters()], len(adds))
+    assert out["1"][1] == 0 and out["0"][1] == 1, (out["1"][1], out["0"][1])
+    for a, b in zip(out["1"][0], out["0"][0]):
+        err = ((a - b).norm() / (b.norm() + 1e-12)).item()
+        assert err < 2e-2, err
+
+
 def _ds_block_run(blk, x0, defer, bn3_eval=False):
     from pytorch_distributed_training_example_amd.models import resnet as R
     ds = blk.downsample
