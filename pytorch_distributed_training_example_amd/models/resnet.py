@@ -47,6 +47,8 @@ DS_MASKED_GRAD = [True]  # downsample blocks: bn3 hands the shortcut gradient to
 # its output is never written (+0.9 % ResNet-50, in-process A/B at 512/GPU). Skipped automatically
 # when the shortcut BN has forward hooks (they must see its real output)
 DS_DEFER_APPLY = [os.environ.get("PDT_DS_DEFER", "1") != "0"]
+# the shortcut BN's backward apply deferred into the shortcut conv's fused backward (where its shape allows)
+DS_FUSED_BWD = [os.environ.get("PDT_DS_FUSED_BWD", "1") != "0"]
 _norm_kind = ["pdt"]
 # the backward weight transforms of all convs (1x1 W^T, 3x3 flips) made in one launch at the start of the
 # training forward (csrc/kernels/weight_prep.hip) instead of 53 per-conv launches in the backward
@@ -135,11 +137,16 @@ class Bottleneck(nn.Module):
                 # bn3's backward hands the shortcut gradient to the downsample BN as (dy, ReLU mask):
                 # the masked copy dres is never written
                 glink = ResidualGradLink(lazy=True)
-                xs = linked_conv(self.downsample[0], x, link)
+                dconv = self.downsample[0]
+                # the shortcut conv's backward as one fused kernel too (layer 1's stride-1 256x64 shortcut):
+                # ds_bn hands it (dy, x, mask, coefficients) and never writes its input gradient
+                dlink = BNGradLink() if (DS_DEFER_APPLY[0] and DS_FUSED_BWD[0] and not ds_bn.has_hooks()
+                                         and isinstance(dconv, Conv1x1) and dconv.fused_bwd_ok(x)) else None
+                xs = linked_conv(dconv, x, link, bwd_link=dlink)
                 if DS_DEFER_APPLY[0] and not ds_bn.has_hooks():
                     # statistics only: an internal DeferredBNOutput handle that only bn3's fused
                     # apply consumes (a_ds x_ds + b_ds added there, the shortcut output never written)
-                    identity = ds_bn._forward_stats_only(xs, grad_link=glink)
+                    identity = ds_bn._forward_stats_only(xs, grad_link=glink, out_link=dlink)
                 else:
                     identity = ds_bn(xs, grad_link=glink)
                 return self.bn3(out, residual=identity, relu=True, res_link=glink, out_link=blink)

@@ -198,7 +198,9 @@ class _BNTrainFn(torch.autograd.Function):
         ctx.gsrc = gsrc
         # out_link: the conv that produced x takes this BatchNorm's input gradient in deferred form
         # (DeferredBNGrad) when the residual gradient needs no dense tensor either
-        ctx.out_link = out_link if (defer is None and (residual is None or (link is not None and link.lazy))) else None
+        # — or, for a statistics-only shortcut BN whose gradient arrives through glink as (dy, mask)
+        ctx.out_link = out_link if ((defer is None and (residual is None or (link is not None and link.lazy)))
+                                    or (defer is not None and glink is not None)) else None
         # glink: this output's only consumer (a residual BatchNorm) may hand its gradient over as
         # (dy, ReLU mask) and give autograd None — backward then runs with dy = None
         ctx.glink = glink
@@ -221,6 +223,11 @@ class _BNTrainFn(torch.autograd.Function):
             g = ctx.glink.take() if ctx.glink is not None else None
             if g is None:
                 return (None,) * 4 + tail
+            if isinstance(g, MaskedGrad) and ctx.out_link is not None:
+                # coefficients only: the shortcut conv's fused backward forms dx on load (DeferredBNGrad)
+                coef, dg, db = native().bn_bwd_coef(g.dy, x, None, g.mask, weight, mean, invstd, True, need_w)
+                ctx.out_link.grad = DeferredBNGrad(g.dy, x, g.mask, mean, coef)
+                return (None, None, dg if need_w else None, db if need_w else None) + tail
             if isinstance(g, MaskedGrad):
                 dx, _, dg, db = native().bn_bwd_train(g.dy, x, g.mask, weight, mean, invstd, True, False, need_w)
             else:
@@ -472,10 +479,12 @@ class BatchNorm2d(nn.BatchNorm2d):
         return bool(self._forward_hooks or self._forward_pre_hooks or _m._global_forward_hooks
                     or _m._global_forward_pre_hooks)
 
-    def _forward_stats_only(self, x: torch.Tensor, grad_link: Optional[ResidualGradLink] = None):
+    def _forward_stats_only(self, x: torch.Tensor, grad_link: Optional[ResidualGradLink] = None,
+                            out_link: Optional[BNGradLink] = None):
         """Internal (``Bottleneck``'s shortcut BN): statistics + running-stat update only, returned
         as a ``DeferredBNOutput`` on the native training path (a normal output tensor otherwise).
-        Bypasses the module call, so callers use it only when ``has_hooks()`` is False."""
+        ``out_link``: the shortcut conv (``fused_bwd_ok``) takes this BN's input gradient in deferred
+        form. Bypasses the module call, so callers use it only when ``has_hooks()`` is False."""
         training = self.training or not self.track_running_stats
         momentum = self.momentum
         if self.training and self.track_running_stats:
@@ -487,7 +496,7 @@ class BatchNorm2d(nn.BatchNorm2d):
         w = self.weight if self.affine else None
         b = self.bias if self.affine else None
         return batch_norm_act(x, None, w, b, rm, rv, training, momentum if momentum is not None else 0.0,
-                              self.eps, False, None, grad_link, defer_apply=True)
+                              self.eps, False, None, grad_link, defer_apply=True, out_link=out_link)
 
     def _forward_deferred_relu(self, x: torch.Tensor):
         """Internal (``Bottleneck``'s bn2 when conv3 runs the fused backward): ``relu(bn(x))`` as a

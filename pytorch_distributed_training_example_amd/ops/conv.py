@@ -324,6 +324,9 @@ class _Conv1x1Fn(torch.autograd.Function):
         none7 = (None,) * 5
         if gy is None:  # the consuming BatchNorm handed its input gradient over (or there is none)
             d = ctx.bwd_link.take() if ctx.bwd_link is not None else None
+            if d is None and ctx.link is not None:  # the partner branch still expects this one's gradient
+                gy = torch.zeros((N, Co, H, W), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+                return _Conv1x1Fn._backward_dense(ctx, gy, x, weight) + (None,) * 5
             if d is None:
                 return (None, None) + none7
             r = _bwd_fused(ctx, d, x, weight)
@@ -471,11 +474,14 @@ def _bwd_fused(ctx, d, x, weight):
     BatchNorm's deferred input gradient ``d`` (DeferredBNGrad) -> (dx, dw), with the producing BatchNorm's
     backward reduction deposited in its GradStatsSource. None when the kernel does not take the shape
     (the caller materialises d and runs the unfused path)."""
-    if not (SW.bwd_fused and ctx.link is None and ctx.needs_input_grad[0] and ctx.needs_input_grad[1]
-            and d.mask is not None and fused_bwd_shape_ok(weight)):
+    # linked (a downsample shortcut conv): only as the FIRST of the two branches — dx is deposited for
+    # conv1's dgrad GEMM to accumulate into, so it is not final and takes no BatchNorm reduction
+    linked = ctx.link is not None
+    if not (SW.bwd_fused and (not linked or ctx.link.grad is None) and ctx.needs_input_grad[0]
+            and ctx.needs_input_grad[1] and d.mask is not None and fused_bwd_shape_ok(weight)):
         return None
     from ._native import native
-    gs = ctx.gsrc if (ctx.gsrc is not None and ctx.gsrc.ready()) else None
+    gs = ctx.gsrc if (ctx.gsrc is not None and ctx.gsrc.ready() and not linked) else None
     dre = ctx.dre
     if dre is not None and gs is None:
         return None  # the recompute mode needs bn2's input / mean (its GradStatsSource)
@@ -487,6 +493,8 @@ def _bwd_fused(ctx, d, x, weight):
     dx, dw, part = r
     if gs is not None and part is not None:
         gs.deposit(part, dx)
+    if linked:
+        ctx.link.grad, dx = dx, None
     return dx, dw
 
 
@@ -887,10 +895,12 @@ class PatchConv2d(nn.Conv2d):
         return y.view(B, gh, gw, self.out_channels).permute(0, 3, 1, 2)
 
 
-def linked_conv(conv: nn.Conv2d, x: torch.Tensor, link) -> torch.Tensor:
-    """``conv(x)`` whose input gradient is summed with the partner branch's through ``link``."""
+def linked_conv(conv: nn.Conv2d, x: torch.Tensor, link, bwd_link=None) -> torch.Tensor:
+    """``conv(x)`` whose input gradient is summed with the partner branch's through ``link``
+    (``bwd_link``: see ``Conv1x1.forward``; the caller checked ``fused_bwd_ok``)."""
     if isinstance(conv, Conv1x1) and (conv.gemm_eligible(x) or conv.strided_gemm_eligible(x)):
-        return conv(x, res_link=link)
+        return conv(x, res_link=link, bwd_link=bwd_link)
+    assert bwd_link is None, "bwd_link needs the stride-1 GEMM path"
     return _LinkedConvFn.apply(x, conv.weight, conv.stride, conv.padding, link)
 
 

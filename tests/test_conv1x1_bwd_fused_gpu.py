@@ -162,7 +162,8 @@ def test_resnet50_grads_fused_vs_unfused(switch, defer):
         ga = _grads()
     finally:
         conv_ops._bwd_fused = orig
-    assert calls == [True] * 7, calls  # the three layer-1 and four layer-2 blocks, all on the fused kernel
+    # the three layer-1 and four layer-2 conv3s and layer 1's shortcut conv (DS_FUSED_BWD), all on the fused kernel
+    assert calls == [True] * 8, calls
     switch("PDT_BWD_FUSED", "0")
     gb = _grads()
     assert ga.keys() == gb.keys()

@@ -516,6 +516,34 @@ def test_downsample_bn_deferred_apply(stride):
         assert err < 1e-2, err
 
 
+def test_shortcut_conv_fused_backward(monkeypatch):
+    """Layer-1 style downsample block (stride 1, shortcut conv 64 -> 256): the shortcut BN's backward
+    apply is deferred into the shortcut conv's fused backward (DS_FUSED_BWD; dx deposited for conv1's
+    dgrad) — outputs, input / parameter gradients and running statistics match the unfused run, and
+    the fused kernel did run for the linked shortcut conv."""
+    from pytorch_distributed_training_example_amd.models import resnet as R
+    from pytorch_distributed_training_example_amd.ops import conv as C
+    blk = _make_ds_block(1, cin=64, planes=64)
+    x0 = torch.randn(8, 64, 14, 14, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    ran = []
+    orig = C._bwd_fused
+    monkeypatch.setattr(C, "_bwd_fused", lambda ctx, d, x, w: ran.append((ctx.link is not None, tuple(w.shape[:2])))
+                        or orig(ctx, d, x, w))
+    old = R.DS_FUSED_BWD[0]
+    try:
+        R.DS_FUSED_BWD[0] = True
+        a_all = _ds_block_run(blk, x0, True)
+        fused = list(ran)
+        R.DS_FUSED_BWD[0] = False
+        b_all = _ds_block_run(blk, x0, True)
+    finally:
+        R.DS_FUSED_BWD[0] = old
+    assert (True, (256, 64)) in fused, fused
+    for a, b in zip(a_all, b_all):
+        err = ((a - b).norm() / (b.norm() + 1e-12)).item()
+        assert err < 1e-2, err
+
+
 def test_deferred_shortcut_bn3_eval_gradients():
     """The deferred shortcut BN materialised for a non-fused consumer (bn3 frozen in eval while the
     block trains) must pass its gradient through unchanged: x / downsample grads equal the

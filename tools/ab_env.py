@@ -33,6 +33,7 @@ def apply_env(base: dict, env: dict) -> None:
     conv_ops._TABLE_LOADED[0] = False
     resnet.DS_DEFER_APPLY[0] = os.environ.get("PDT_DS_DEFER", "1") != "0"
     resnet.PREP_WEIGHTS[0] = os.environ.get("PDT_PREP_WEIGHTS", "1") != "0"
+    resnet.DS_FUSED_BWD[0] = os.environ.get("PDT_DS_FUSED_BWD", "1") != "0"
 
 
 def main():
