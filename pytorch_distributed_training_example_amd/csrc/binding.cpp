@@ -142,6 +142,7 @@ int pdt_conv1x1_gemm(const uint16_t* a, const uint16_t* b, uint16_t* y, const ui
                      hipStream_t s);
 void pdt_conv1x1_probe(int probe);
 void pdt_bn_tiles_fused(int on);
+void pdt_maxpool_bwd_v2(int on);
 int pdt_weight_prep_max_items();
 int pdt_weight_prep(const uint16_t* const* src, uint16_t* const* dst, const int* R, const int* C, const int* taps,
                     int n, hipStream_t s);
@@ -1899,6 +1900,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv1x1_probe", [](int probe) { pdt_conv1x1_probe(probe); });
   m.def("weight_prep", &weight_prep);
   m.def("bn_tiles_fused", [](int on) { pdt_bn_tiles_fused(on); });
+  m.def("maxpool_bwd_v2", [](int on) { pdt_maxpool_bwd_v2(on); });
   m.def("conv1x1_gemm_apply", &conv1x1_gemm_apply, py::arg("a"), py::arg("b"), py::arg("res"), py::arg("ab"),
         py::arg("rab") = py::none(), py::arg("a_coef") = py::none());
   m.def("bn_bwd_train_tiles", &bn_bwd_train_tiles);

@@ -795,6 +795,86 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const uint16_t* __rest
   }
 }
 
+// The same gradient, one thread per 2 x 2 block of input positions (2a + r, 2b + s) and 8 channels:
+// the block's positions lie only in the pooled windows (a .. a+1, b .. b+1), so the four (dy, code)
+// loads serve four outputs (maxpool_bwd_kernel loads them per position: 4x the load instructions and
+// L2 traffic, 980 us at batch 1024 = 4 TB/s). Each position sums its matching windows in the same
+// (a, b), (a, b+1), (a+1, b), (a+1, b+1) order, so dz is bit-identical to maxpool_bwd_kernel's.
+int g_pool_bwd_v2 = 1;  // pdt_maxpool_bwd_v2(0): maxpool_bwd_kernel (A/B)
+
+template <bool BNRED>
+__global__ __launch_bounds__(256) void maxpool_bwd2_kernel(const uint16_t* __restrict__ dy,
+                                                           const uint8_t* __restrict__ code, uint16_t* __restrict__ dz,
+                                                           int N, int H, int W, int C, int Ho, int Wo,
+                                                           const uint16_t* __restrict__ xb, const float* __restrict__ mean,
+                                                           float* __restrict__ part) {
+  const int C8 = C >> 3;
+  float s1[8], s2[8], mu[8];
+  if constexpr (BNRED) {  // C8 == 8 divides the thread stride: a thread's channel chunk never changes
+    ld8_f32(mean + (threadIdx.x % 8) * 8, mu);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { s1[j] = 0.f; s2[j] = 0.f; }
+  }
+  const int64_t total = (int64_t)N * Ho * Wo * C8;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int c8 = (int)(e % C8);
+    const int64_t pix = e / C8;  // pooled position (n, a, b)
+    const int b = (int)(pix % Wo);
+    const int64_t na = pix / Wo;
+    const int a = (int)(na % Ho), n = (int)(na / Ho);
+    const int a1 = min(Ho - 1, a + 1), b1 = min(Wo - 1, b + 1);
+    uint2 cw[4];
+    uint4 dv[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int oh = q < 2 ? a : a1, ow = (q & 1) ? b1 : b;
+      const int64_t o = (((int64_t)n * Ho + oh) * Wo + ow) * C + c8 * 8;
+      cw[q] = *reinterpret_cast<const uint2*>(code + o);
+      dv[q] = *reinterpret_cast<const uint4*>(dy + o);
+    }
+    uint4 xv[4];
+    if constexpr (BNRED) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int ih = 2 * a + (t >> 1), iw = 2 * b + (t & 1);
+        if (ih < H && iw < W) xv[t] = *reinterpret_cast<const uint4*>(xb + (((int64_t)n * H + ih) * W + iw) * C + c8 * 8);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {  // input position (2a + r, 2b + s)
+      const int r = t >> 1, sc = t & 1;
+      const int ih = 2 * a + r, iw = 2 * b + sc;
+      if (ih >= H || iw >= W) continue;
+      float g[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int dr = q >> 1, ds = q & 1;  // window (a + dr, b + ds)
+        if ((dr && !r) || (ds && !sc)) continue;  // (2a, .) lies in window row a only; likewise columns
+        if ((dr && a1 == a) || (ds && b1 == b)) continue;  // past the last window (clamped duplicate)
+        const uint32_t idx = (uint32_t)((dr ? 0 : r + 1) * 3 + (ds ? 0 : sc + 1));
+        float v[8];
+        unpack8(dv[q], v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const uint32_t cj = ((j < 4 ? cw[q].x : cw[q].y) >> (8 * (j & 3))) & 0xffu;
+          g[j] += cj == idx ? v[j] : 0.f;
+        }
+      }
+      uint4 st;
+      st.x = (uint32_t)f2bf(g[0]) | ((uint32_t)f2bf(g[1]) << 16);
+      st.y = (uint32_t)f2bf(g[2]) | ((uint32_t)f2bf(g[3]) << 16);
+      st.z = (uint32_t)f2bf(g[4]) | ((uint32_t)f2bf(g[5]) << 16);
+      st.w = (uint32_t)f2bf(g[6]) | ((uint32_t)f2bf(g[7]) << 16);
+      *reinterpret_cast<uint4*>(dz + (((int64_t)n * H + ih) * W + iw) * C + c8 * 8) = st;
+      if constexpr (BNRED) bn_bwd_accum8(st, xv[t], 0xffu, mu, s1, s2);
+    }
+  }
+  if constexpr (BNRED) {
+    __shared__ float red[4 * 2 * 64];
+    bn_bwd_tile_store<64, 4>(s1, s2, red, part, (int)gridDim.x, (int)blockIdx.x, 64, 0);
+  }
+}
+
 struct ReduceGeo {
   int nrow, nchunks;
   int64_t rows_per_block;
@@ -1168,6 +1248,20 @@ int pdt_bn_bwd_train_tiles(const float* part, int T, int BMt, const uint16_t* dy
                               dbeta, ws, s);
 }
 
+// A/B switch of the max-pool gradient kernel (maxpool_bwd2_kernel by default).
+void pdt_maxpool_bwd_v2(int on) { g_pool_bwd_v2 = on; }
+
+static void launch_pool_bwd_bn(const uint16_t* dy, const uint8_t* code, uint16_t* dz, int N, int H, int W, int C, int Ho,
+                               int Wo, const uint16_t* x, const float* mean, float* part, int T, hipStream_t s) {
+  // v2 covers input positions < (2 Ho, 2 Wo): every one when H <= 2 Ho and W <= 2 Wo (always, for 3x3/s2/p1)
+  if (g_pool_bwd_v2 && H <= 2 * Ho && W <= 2 * Wo)
+    hipLaunchKernelGGL(maxpool_bwd2_kernel<true>, dim3(T), dim3(256), 0, s, dy, code, dz, N, H, W, C, Ho, Wo, x, mean,
+                       part);
+  else
+    hipLaunchKernelGGL(maxpool_bwd_kernel<true>, dim3(T), dim3(256), 0, s, dy, code, dz, N, H, W, C, Ho, Wo, x, mean,
+                       part);
+}
+
 // Stem backward: max-pool gradient dz (written) with the stem BatchNorm's backward reduction fused,
 // then the BN finalize + apply -> dx. C == 64. ws: pdt_bn_tiles_ws_floats(pdt_maxpool_bn_parts(), C)
 // + 2C floats; part: 2 * pdt_maxpool_bn_parts() * C floats.
@@ -1181,8 +1275,7 @@ int pdt_maxpool3s2_bwd_bn(const uint16_t* dy, const uint8_t* code, uint16_t* dz,
   const int64_t M = (int64_t)N * H * W;
   if (M < 1) return -1;
   const int T = pdt_maxpool_bn_parts(N, H);
-  hipLaunchKernelGGL(maxpool_bwd_kernel<true>, dim3(T), dim3(256), 0, s, dy, code, dz, N, H, W, C, Ho, Wo, x, mean,
-                     part);
+  launch_pool_bwd_bn(dy, code, dz, N, H, W, C, Ho, Wo, x, mean, part, T, s);
   return bn_bwd_from_partials(part, T, 1, dz, x, nullptr, gamma, mean, invstd, M, C, 0, 0, dx, nullptr, dgamma, dbeta,
                               ws, s);
 }
@@ -1197,8 +1290,7 @@ int pdt_maxpool3s2_bwd_bn_coef(const uint16_t* dy, const uint8_t* code, uint16_t
   const int64_t M = (int64_t)N * H * W;
   if (M < 1) return -1;
   const int T = pdt_maxpool_bn_parts(N, H);
-  hipLaunchKernelGGL(maxpool_bwd_kernel<true>, dim3(T), dim3(256), 0, s, dy, code, dz, N, H, W, C, Ho, Wo, x, mean,
-                     part);
+  launch_pool_bwd_bn(dy, code, dz, N, H, W, C, Ho, Wo, x, mean, part, T, s);
   return bn_bwd_from_partials(part, T, 1, dz, x, nullptr, gamma, mean, invstd, M, C, 0, 0, nullptr, nullptr, dgamma,
                               dbeta, ws, s, coef);
 }

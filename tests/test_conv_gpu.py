@@ -155,6 +155,34 @@ def test_stem_wgrad_with_fused_bn_apply(N, H, W):
     assert ((fused - ref).norm() / ref.norm()).item() < 1e-2
 
 
+@pytest.mark.parametrize("N,H,W", [(2, 224, 224), (3, 17, 64), (1, 9, 32), (4, 30, 96)])
+def test_maxpool_bwd_2x2_block_kernel_bit_identical(N, H, W):
+    """The 2 x 2-block max-pool gradient kernel (maxpool_bwd2_kernel, default) writes the same dz bit for
+    bit as the per-position kernel (PDT_POOL_BWD_V2=0), odd pooled sizes included, and the BatchNorm
+    coefficients from its partials agree (the partial sums are taken in a different order)."""
+    from pytorch_distributed_training_example_amd.ops._native import native
+    n = native()
+    cl = torch.channels_last
+    g = torch.Generator(device="cuda").manual_seed(N * H + W)
+    img = (torch.randn(N, 3, H, W, device="cuda", generator=g) + 0.5).bfloat16().contiguous(memory_format=cl)
+    w = (torch.randn(64, 3, 7, 7, device="cuda", generator=g) * 0.1).bfloat16().contiguous(memory_format=cl)
+    gamma = torch.rand(64, device="cuda", generator=g) + 0.5
+    beta = torch.randn(64, device="cuda", generator=g) * 0.1
+    xb = n.stem_conv_fwd(img, w)
+    y, code, mean, invstd = n.bn_relu_maxpool_fwd(xb, gamma, beta, None, None, 0.1, 1e-5)
+    dy = torch.randn(y.shape, device="cuda", generator=g).bfloat16().contiguous(memory_format=cl)
+    out = {}
+    try:
+        for v2 in (1, 0):
+            n.maxpool_bwd_v2(v2)
+            out[v2] = n.maxpool3s2_bwd_bn_coef(dy, code, xb, gamma, mean, invstd, True)
+    finally:
+        n.maxpool_bwd_v2(1)
+    assert torch.equal(out[1][0], out[0][0])
+    for a, b in zip(out[1][1:], out[0][1:]):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5)
+
+
 @pytest.mark.parametrize("N,H", [(2, 224), (20, 224), (3, 30), (1, 8)])
 def test_stem_conv_bn_stats_epilogue(N, H):
     """Stem conv with the BatchNorm statistics in its epilogue (stem_conv_fwd_stats, PDT_STEM_BN_STATS):

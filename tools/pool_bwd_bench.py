@@ -1,18 +1,46 @@
-"""Stem max-pool backward (+ the stem BN backward reduction) at batch 1024: device time per call."""
-import os, sys, torch
-sys.path.insert(0, os.getcwd())
-from pytorch_distributed_training_example_amd.ops._native import native
-n = native(); cl = torch.channels_last
-def timeit(fn, it=10):
-    for _ in range(2): fn()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    torch.cuda.synchronize(); e0.record()
-    for _ in range(it): fn()
-    e1.record(); torch.cuda.synchronize(); return e0.elapsed_time(e1) * 1e3 / it
-xb = torch.randn(1024, 64, 112, 112, device="cuda").bfloat16().contiguous(memory_format=cl)
-g = torch.rand(64, device="cuda") + 0.5; b = torch.randn(64, device="cuda") * 0.1
-rm, rv = torch.zeros(64, device="cuda"), torch.ones(64, device="cuda")
-y, code, mean, invstd = n.bn_relu_maxpool_fwd(xb, g, b, rm, rv, 0.1, 1e-5)
-dy = torch.randn_like(y)
-print("pool bwd + BN reduce (coef only): %.1f us" % timeit(lambda: n.maxpool3s2_bwd_bn_coef(dy, code, xb, g, mean, invstd, True)))
-print("pool bwd plain: %.1f us" % timeit(lambda: n.maxpool3s2_bwd(dy, code, 112, 112)))
+"""Stem max-pool gradient (+ BN backward reduction) kernel time, 2 x 2-block kernel vs per-position kernel
+(batchnorm.hip maxpool_bwd2_kernel / maxpool_bwd_kernel), at the ResNet-50 bench shape.
+
+    python tools/pool_bwd_bench.py [--batch 1024]
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=1024)
+    a = ap.parse_args()
+    from pytorch_distributed_training_example_amd.ops._native import native
+    n = native()
+    cl = torch.channels_last
+    xb = torch.randn(a.batch, 64, 112, 112, device="cuda").bfloat16().contiguous(memory_format=cl)
+    gamma, beta = torch.rand(64, device="cuda") + 0.5, torch.randn(64, device="cuda") * 0.1
+    y, code, mean, invstd = n.bn_relu_maxpool_fwd(xb, gamma, beta, None, None, 0.1, 1e-5)
+    dy = torch.randn(y.shape, device="cuda").bfloat16().contiguous(memory_format=cl)
+    nbytes = dy.numel() * 2 + code.numel() + 2 * xb.numel() * 2
+    for v2 in (1, 0, 1, 0):
+        n.maxpool_bwd_v2(v2)
+        fn = lambda: n.maxpool3s2_bwd_bn_coef(dy, code, xb, gamma, mean, invstd, True)  # noqa: E731
+        fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(10):
+            fn()
+        e1.record()
+        e1.synchronize()
+        us = e0.elapsed_time(e1) / 10 * 1e3
+        print(f"v2={v2}: {us:8.1f} us per call (pool gradient + BN finalize), {nbytes / us / 1e6:5.2f} TB/s", flush=True)
+    n.maxpool_bwd_v2(1)
+
+
+if __name__ == "__main__":
+    main()
