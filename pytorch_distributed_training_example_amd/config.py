@@ -27,6 +27,8 @@ PDT_STEM_BN_WGRAD           1            stem weight gradient applies the stem B
 PDT_STRIDED_BSTATS          1            a transition block's conv1 data gradient adds the stride-2 shortcut's compact
                                          gradient AND takes the previous block's bn3 backward reduction in our
                                          GEMM's epilogue (vs hipBLASLt + scatter-add + a reduce pass)
+PDT_GAP_NATIVE              1            ResNet global-average-pool gradient on our kernel, with the last bn3's
+                                         backward reduction
 PDT_STEM_BN_STATS           1            stem conv emits its BatchNorm's statistics (no reduce pass; W == 224)
 PDT_WGRAD_SPLITK            1            split-K 1x1 weight gradients
 PDT_SLICE_SUM               1            split-K partial sums on our slice_sum kernel
@@ -60,7 +62,7 @@ class _Switches:
                  "conv1x1_table", "conv1x1_dump", "conv1x1_s2", "conv3x3", "conv3x3_wgrad", "conv3x3_s2", "conv_stem",
                  "conv_bn_stats", "bn_bwd_stats", "res_masked", "stem_bwd_fused", "stem_bn_wgrad", "stem_bn_stats", "wgrad_splitk", "slice_sum",
                  "subsample_native", "linear_splitk", "fused_addln", "embedding_native", "linear_epilogue",
-                 "bwd_fused", "bwd_fused_shapes", "bn2_defer", "bn_apply_gemm_k", "strided_bstats")
+                 "bwd_fused", "bwd_fused_shapes", "bn2_defer", "bn_apply_gemm_k", "strided_bstats", "gap_native")
 
     def __init__(self):
         self.reload()
@@ -103,6 +105,7 @@ class _Switches:
         self.bn2_defer = on("PDT_BN2_DEFER", "0")
         self.bn_apply_gemm_k = int(e("PDT_BN_APPLY_GEMM_K", "64"))
         self.strided_bstats = on("PDT_STRIDED_BSTATS")
+        self.gap_native = on("PDT_GAP_NATIVE")
         return self
 
 

@@ -143,6 +143,9 @@ int pdt_conv1x1_gemm(const uint16_t* a, const uint16_t* b, uint16_t* y, const ui
 void pdt_conv1x1_probe(int probe);
 void pdt_bn_tiles_fused(int on);
 void pdt_maxpool_bwd_v2(int on);
+int pdt_gap_bwd_parts(int64_t M, int C);
+int pdt_gap_bwd(const uint16_t* g, int N, int HW, int C, uint16_t* dy, const uint16_t* xb, const uint8_t* mask,
+                const float* mean, float* part, hipStream_t s);
 int pdt_weight_prep_max_items();
 int pdt_weight_prep(const uint16_t* const* src, uint16_t* const* dst, const int* R, const int* C, const int* taps,
                     int n, hipStream_t s);
@@ -500,6 +503,42 @@ std::vector<Tensor> bn_relu_maxpool_fwd_parts(Tensor x, Tensor part, c10::option
                                                invstd.data_ptr<float>(), ws.data_ptr<float>(), stream());
   TORCH_CHECK(rc == 0, "pdt_bn_relu_maxpool_fwd_train_parts failed: ", rc);
   return {y, code, mean, invstd};
+}
+
+// Global-average-pool gradient: g [N, C] bf16 -> dy [N, C, H, W] channels_last = g / (H W). With bn_x / bn_mask /
+// bn_mean (the pooled tensor is a BatchNorm(+ReLU) output): also that BatchNorm's backward partials [2, T, C]
+// (the input of bn_bwd_train_tiles); {dy} alone when the reduction does not apply to C.
+std::vector<Tensor> gap_bwd(Tensor g, int64_t H, int64_t W, c10::optional<Tensor> bn_x, c10::optional<Tensor> bn_mask,
+                            c10::optional<Tensor> bn_mean) {
+  check_cuda(g, "g");
+  TORCH_CHECK(g.dim() == 2 && g.scalar_type() == at::kBFloat16 && g.is_contiguous() && g.size(1) % 8 == 0,
+              "gap_bwd: g [N, C] contiguous bf16, C % 8 == 0");
+  const int64_t N = g.size(0), C = g.size(1), M = N * H * W;
+  auto dy = at::empty({N, C, H, W}, g.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const bool red = bn_x.has_value() && bn_x->defined() && pdt_gap_bwd_parts(M, (int)C) > 0;
+  Tensor part;
+  const uint16_t* xp = nullptr;
+  const uint8_t* mp = nullptr;
+  const float* mu = nullptr;
+  if (red) {
+    check_nhwc_bf16(*bn_x, "bn_x");
+    TORCH_CHECK(bn_x->sizes() == dy.sizes(), "gap_bwd: bn_x must be [N, C, H, W]");
+    TORCH_CHECK(bn_mean.has_value() && bn_mean->defined() && bn_mean->scalar_type() == at::kFloat &&
+                    bn_mean->numel() == C && bn_mean->is_cuda(), "gap_bwd: bn_mean fp32 [C]");
+    if (bn_mask.has_value() && bn_mask->defined()) {
+      TORCH_CHECK(bn_mask->scalar_type() == at::kByte && bn_mask->numel() == M * C / 8, "gap_bwd: bn_mask uint8 [M C / 8]");
+      mp = bn_mask->data_ptr<uint8_t>();
+    }
+    xp = reinterpret_cast<const uint16_t*>(bn_x->data_ptr());
+    mu = bn_mean->data_ptr<float>();
+    part = at::empty({2, pdt_gap_bwd_parts(M, (int)C), C}, g.options().dtype(at::kFloat));
+  }
+  const int rc = pdt_gap_bwd(reinterpret_cast<const uint16_t*>(g.data_ptr()), (int)N, (int)(H * W), (int)C,
+                             reinterpret_cast<uint16_t*>(dy.data_ptr()), xp, mp, mu,
+                             red ? part.data_ptr<float>() : nullptr, stream());
+  TORCH_CHECK(rc == 0, "pdt_gap_bwd failed: ", rc);
+  if (red) return {dy, part};
+  return {dy};
 }
 
 Tensor maxpool3s2_bwd(Tensor dy, Tensor code, int64_t H, int64_t W) {
@@ -1901,6 +1940,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("weight_prep", &weight_prep);
   m.def("bn_tiles_fused", [](int on) { pdt_bn_tiles_fused(on); });
   m.def("maxpool_bwd_v2", [](int on) { pdt_maxpool_bwd_v2(on); });
+  m.def("gap_bwd", &gap_bwd, py::arg("g"), py::arg("H"), py::arg("W"), py::arg("bn_x") = py::none(),
+        py::arg("bn_mask") = py::none(), py::arg("bn_mean") = py::none());
   m.def("conv1x1_gemm_apply", &conv1x1_gemm_apply, py::arg("a"), py::arg("b"), py::arg("res"), py::arg("ab"),
         py::arg("rab") = py::none(), py::arg("a_coef") = py::none());
   m.def("bn_bwd_train_tiles", &bn_bwd_train_tiles);

@@ -19,6 +19,7 @@
 //   reduce+finalize : Σdz, Σdz(x-mean) with dz = dy·mask → dgamma, dbeta, dx coefficients
 //   apply           : dx = A·dz + B·(x-mean) + D (and dres = dz for the residual branch)
 #include "../common.h"
+#include <algorithm>
 #include "../tile_stats.h"
 
 using namespace pdt;
@@ -875,6 +876,63 @@ __global__ __launch_bounds__(256) void maxpool_bwd2_kernel(const uint16_t* __res
   }
 }
 
+// ---- ResNet head: the global-average-pool gradient dy[n, h, w, c] = bf16(g[n, c] / (H W)) written
+// channels_last, with the backward reduction of the BatchNorm whose output was pooled (sum dz, sum dz
+// (x - mean), dz = dy * ReLU mask) from the values written: that BatchNorm (the last bn3) skips its
+// reduce pass, and the aten broadcast-copy kernel that wrote dy before is gone. Thread chunk c8 =
+// tid % C8 is fixed (C8 divides 256); part [2][gridDim.x][C], fixed-order sums (deterministic).
+template <bool BNRED>
+__global__ __launch_bounds__(256) void gap_bwd_kernel(const uint16_t* __restrict__ g, float scale, int HW, int C,
+                                                      int64_t M, uint16_t* __restrict__ dy,
+                                                      const uint16_t* __restrict__ xb, const uint8_t* __restrict__ mask,
+                                                      const float* __restrict__ mean, float* __restrict__ part) {
+  const int C8 = C >> 3, c8 = threadIdx.x % C8;
+  float s1[8], s2[8], mu[8];
+  if constexpr (BNRED) {
+    ld8_f32(mean + c8 * 8, mu);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { s1[j] = 0.f; s2[j] = 0.f; }
+  }
+  const int64_t total = M * C8;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t m = e / C8;
+    const int n = (int)(m / HW);
+    float v[8];
+    unpack8(*reinterpret_cast<const uint4*>(g + (int64_t)n * C + c8 * 8), v);
+    uint4 st;  // the same rounding as bf16 (gy * scale) in PyTorch
+    st.x = (uint32_t)f2bf(v[0] * scale) | ((uint32_t)f2bf(v[1] * scale) << 16);
+    st.y = (uint32_t)f2bf(v[2] * scale) | ((uint32_t)f2bf(v[3] * scale) << 16);
+    st.z = (uint32_t)f2bf(v[4] * scale) | ((uint32_t)f2bf(v[5] * scale) << 16);
+    st.w = (uint32_t)f2bf(v[6] * scale) | ((uint32_t)f2bf(v[7] * scale) << 16);
+    *reinterpret_cast<uint4*>(dy + e * 8) = st;
+    if constexpr (BNRED) {
+      const uint4 xv = *reinterpret_cast<const uint4*>(xb + e * 8);
+      const unsigned mk = mask ? mask[e] : 0xffu;
+      bn_bwd_accum8(st, xv, mk, mu, s1, s2);
+    }
+  }
+  if constexpr (BNRED) {
+    __shared__ float red[256 * 16];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { red[threadIdx.x * 16 + j] = s1[j]; red[threadIdx.x * 16 + 8 + j] = s2[j]; }
+    __syncthreads();
+    if ((int)threadIdx.x < C8) {
+      float t1[8], t2[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { t1[j] = 0.f; t2[j] = 0.f; }
+      for (int k = threadIdx.x; k < 256; k += C8)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { t1[j] += red[k * 16 + j]; t2[j] += red[k * 16 + 8 + j]; }
+      const int T = gridDim.x;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        part[(int64_t)blockIdx.x * C + c8 * 8 + j] = t1[j];
+        part[((int64_t)T + blockIdx.x) * C + c8 * 8 + j] = t2[j];
+      }
+    }
+  }
+}
+
 struct ReduceGeo {
   int nrow, nchunks;
   int64_t rows_per_block;
@@ -1246,6 +1304,32 @@ int pdt_bn_bwd_train_tiles(const float* part, int T, int BMt, const uint16_t* dy
   if (C % kCC != 0 || M < 1 || T < 1) return -1;
   return bn_bwd_from_partials(part, T, BMt, dy, x, mask, gamma, mean, invstd, M, C, relu, has_res, dx, dres, dgamma,
                               dbeta, ws, s);
+}
+
+// Workgroups (= BN partial tiles) of pdt_gap_bwd: 0 when the reduction does not apply (C / 8 must divide 256).
+int pdt_gap_bwd_parts(int64_t M, int C) {
+  if (C % 8 != 0 || C > 2048 || 256 % (C / 8) != 0 || M < 1) return 0;
+  return (int)std::min<int64_t>((M * (C / 8) + 255) / 256, 1024);
+}
+
+// dy [M = N H W, C] channels_last from g [N, C] (bf16) scaled by 1 / (H W); with xb (the pooled BatchNorm's
+// input), its ReLU mask (or null) and mean: that BatchNorm's backward partials into part [2][T][C],
+// T = pdt_gap_bwd_parts(M, C).
+int pdt_gap_bwd(const uint16_t* g, int N, int HW, int C, uint16_t* dy, const uint16_t* xb, const uint8_t* mask,
+                const float* mean, float* part, hipStream_t s) {
+  const int64_t M = (int64_t)N * HW;
+  if (C % 8 != 0 || M < 1) return -1;
+  const float scale = (float)(1.0 / (double)HW);
+  if (xb) {
+    const int T = pdt_gap_bwd_parts(M, C);
+    if (T == 0 || !mean || !part) return -2;
+    hipLaunchKernelGGL(gap_bwd_kernel<true>, dim3(T), dim3(256), 0, s, g, scale, HW, C, M, dy, xb, mask, mean, part);
+  } else {
+    const int grid = (int)std::min<int64_t>((M * (C / 8) + 255) / 256, 4096);
+    hipLaunchKernelGGL(gap_bwd_kernel<false>, dim3(grid), dim3(256), 0, s, g, scale, HW, C, M, dy, nullptr, nullptr,
+                       nullptr, nullptr);
+  }
+  return 0;
 }
 
 // A/B switch of the max-pool gradient kernel (maxpool_bwd2_kernel by default).

@@ -227,7 +227,8 @@ class ResNet(nn.Module):
             x = self.maxpool(bn_act(self.bn1, self.conv1(x), relu=True))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         if x.is_cuda and x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last) and x.shape[1] > 1:
-            x = _GlobalAvgPoolFn.apply(x)
+            from ..ops.batchnorm import grad_stats_source_of
+            x = _GlobalAvgPoolFn.apply(x, grad_stats_source_of(x) if self.training and torch.is_grad_enabled() else None)
         else:
             x = torch.flatten(self.avgpool(x), 1)
         return self.fc(x)
@@ -237,18 +238,30 @@ class _GlobalAvgPoolFn(torch.autograd.Function):
     """Global average pool of a channels_last [N, C, H, W] tensor -> [N, C]. Its backward writes the
     broadcast gradient straight into a channels_last tensor: nn.AdaptiveAvgPool2d's backward made
     an NCHW gradient that the channels_last BatchNorm backward then had to transpose (a 166 us
-    copy + 37 us scale of the [512, 2048, 7, 7] gradient per ResNet-50 step, profiles/r2)."""
+    copy + 37 us scale of the [512, 2048, 7, 7] gradient per ResNet-50 step, profiles/r2). On the GPU the
+    gradient is written by our kernel (batchnorm.hip gap_bwd_kernel, ``PDT_GAP_NATIVE``), which also takes the
+    pooled BatchNorm's backward reduction."""
 
     @staticmethod
-    def forward(ctx, x):
+    def forward(ctx, x, gsrc=None):
         ctx.shape = x.shape
+        ctx.gsrc = gsrc  # x is a BatchNorm output: our gradient kernel can take that BN's backward reduction
         return x.mean(dim=(2, 3))
 
     @staticmethod
     def backward(ctx, gy):
         n, c, h, w = ctx.shape
+        if (gy.dtype == torch.bfloat16 and gy.is_cuda and c % 8 == 0 and SW.gap_native
+                and not native_disabled()):
+            from ..ops._native import native
+            gs = ctx.gsrc if (ctx.gsrc is not None and ctx.gsrc.ready()) else None
+            r = native().gap_bwd(gy.contiguous(), h, w, gs.x if gs else None, gs.mask if gs else None,
+                                 gs.mean if gs else None)
+            if gs is not None and len(r) == 2:
+                gs.deposit(r[1], r[0])  # the last bn3's backward skips its reduce pass
+            return r[0], None
         g = (gy * (1.0 / (h * w))).view(n, c, 1, 1).expand(n, c, h, w)
-        return g.contiguous(memory_format=torch.channels_last)
+        return g.contiguous(memory_format=torch.channels_last), None
 
 
 def resnet18(**kw) -> ResNet:

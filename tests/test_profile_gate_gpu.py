@@ -47,7 +47,7 @@ def test_resnet_step_runs_our_kernels():
     names = _kernels(step)
     assert names, "no device kernels recorded"
     for ours in ("bn_reduce3_kernel", "bn_fin_kernel", "bn_apply_kernel", "bn_bwd_apply_kernel",
-                 "bn_apply_pool_kernel", "maxpool_bwd_kernel", "ce_fwd_kernel", "ce_bwd_kernel", "mt_kernel",
+                 "bn_apply_pool_kernel", "maxpool_bwd2_kernel", "gap_bwd_kernel", "ce_fwd_kernel", "ce_bwd_kernel", "mt_kernel",
                  "conv3x3wst_kernel", "conv3x3h_kernel", "weight_prep_kernel", "stem_conv_kernel",
                  "stem_wgrad_kernel", "conv1x1_kernel", "conv3x3_wgrad_kernel", "conv3x3_wgrad_reduce_kernel"):
         assert _has(names, ours), (ours, sorted(set(names))[:40])
