@@ -886,16 +886,17 @@ __global__ __launch_bounds__(256) void gap_bwd_kernel(const uint16_t* __restrict
                                                       int64_t M, uint16_t* __restrict__ dy,
                                                       const uint16_t* __restrict__ xb, const uint8_t* __restrict__ mask,
                                                       const float* __restrict__ mean, float* __restrict__ part) {
-  const int C8 = C >> 3, c8 = threadIdx.x % C8;
+  const int C8 = C >> 3;
   float s1[8], s2[8], mu[8];
-  if constexpr (BNRED) {
-    ld8_f32(mean + c8 * 8, mu);
+  if constexpr (BNRED) {  // C8 divides 256 and the stride: e % C8 == threadIdx.x % C8 throughout
+    ld8_f32(mean + (threadIdx.x % C8) * 8, mu);
 #pragma unroll
     for (int j = 0; j < 8; ++j) { s1[j] = 0.f; s2[j] = 0.f; }
   }
   const int64_t total = M * C8;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
     const int64_t m = e / C8;
+    const int c8 = (int)(e - m * C8);
     const int n = (int)(m / HW);
     float v[8];
     unpack8(*reinterpret_cast<const uint4*>(g + (int64_t)n * C + c8 * 8), v);
@@ -917,6 +918,7 @@ __global__ __launch_bounds__(256) void gap_bwd_kernel(const uint16_t* __restrict
     for (int j = 0; j < 8; ++j) { red[threadIdx.x * 16 + j] = s1[j]; red[threadIdx.x * 16 + 8 + j] = s2[j]; }
     __syncthreads();
     if ((int)threadIdx.x < C8) {
+      const int c8 = threadIdx.x;
       float t1[8], t2[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) { t1[j] = 0.f; t2[j] = 0.f; }
