@@ -671,11 +671,19 @@ __global__ __launch_bounds__(256) void bn_apply_pool_kernel(const uint16_t* __re
                                                             const float* __restrict__ a,
                                                             const float* __restrict__ b, uint16_t* __restrict__ y,
                                                             uint8_t* __restrict__ code, int N, int H, int W, int C,
-                                                            int Ho, int Wo) {
-  // one workgroup per output row (n, oh), threads over (ow, c8): 32-bit index math per element
+                                                            int Ho, int Wo, int contig) {
+  // one workgroup per output row (n, oh), threads over (ow, c8): 32-bit index math per element.
+  // contig: a workgroup walks a CONTIGUOUS run of output rows, so the input row two neighbouring
+  // windows share (2 oh + 1) is an L2 hit on the workgroup's own XCD (grid-stride rows land on
+  // different XCDs and fetch it from HBM twice)
   const int C8 = C >> 3;
   const int per_row = Wo * C8;
-  for (int64_t row = blockIdx.x; row < (int64_t)N * Ho; row += gridDim.x) {
+  const int64_t nrows = (int64_t)N * Ho;
+  const int64_t rper = contig ? (nrows + gridDim.x - 1) / gridDim.x : 1;
+  const int64_t rbeg = contig ? (int64_t)blockIdx.x * rper : blockIdx.x;
+  const int64_t rend = contig ? std::min<int64_t>(nrows, rbeg + rper) : nrows;
+  const int64_t rstep = contig ? 1 : gridDim.x;
+  for (int64_t row = rbeg; row < rend; row += rstep) {
    const int oh = (int)(row % Ho);
    const int n = (int)(row / Ho);
    for (int e = threadIdx.x; e < per_row; e += blockDim.x) {
@@ -802,13 +810,18 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const uint16_t* __rest
 // L2 traffic, 980 us at batch 1024 = 4 TB/s). Each position sums its matching windows in the same
 // (a, b), (a, b+1), (a+1, b), (a+1, b+1) order, so dz is bit-identical to maxpool_bwd_kernel's.
 int g_pool_bwd_v2 = 1;  // pdt_maxpool_bwd_v2(0): maxpool_bwd_kernel (A/B)
+// pdt_pool_fwd_contig(1): contiguous row / element runs per workgroup in the stem pool kernels. Measured
+// SLOWER than grid-stride (batch 1024: forward 836-850 vs 811 us, gradient 805-818 vs 748 us,
+// profiles/r4/pool_bwd_bench_b1024.txt): neighbouring workgroups in flight together share the rows in
+// MALL / L2 anyway, and one run per workgroup serialises its rows' latency. Off; kept for the A/B.
+int g_pool_contig = 0;
 
 template <bool BNRED>
 __global__ __launch_bounds__(256) void maxpool_bwd2_kernel(const uint16_t* __restrict__ dy,
                                                            const uint8_t* __restrict__ code, uint16_t* __restrict__ dz,
                                                            int N, int H, int W, int C, int Ho, int Wo,
                                                            const uint16_t* __restrict__ xb, const float* __restrict__ mean,
-                                                           float* __restrict__ part) {
+                                                           float* __restrict__ part, int contig) {
   const int C8 = C >> 3;
   float s1[8], s2[8], mu[8];
   if constexpr (BNRED) {  // C8 == 8 divides the thread stride: a thread's channel chunk never changes
@@ -817,7 +830,13 @@ __global__ __launch_bounds__(256) void maxpool_bwd2_kernel(const uint16_t* __res
     for (int j = 0; j < 8; ++j) { s1[j] = 0.f; s2[j] = 0.f; }
   }
   const int64_t total = (int64_t)N * Ho * Wo * C8;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+  // contig: a workgroup walks one contiguous run of (a multiple of 256) elements, so the dy / code rows that
+  // neighbouring pooled rows share stay in its XCD's L2 (as in bn_apply_pool_kernel)
+  const int64_t per = contig ? ((total + gridDim.x - 1) / gridDim.x + 255) / 256 * 256 : 0;
+  const int64_t ebeg = contig ? (int64_t)blockIdx.x * per + threadIdx.x : (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t eend = contig ? std::min<int64_t>(total, (int64_t)blockIdx.x * per + per) : total;
+  const int64_t estep = contig ? blockDim.x : (int64_t)gridDim.x * blockDim.x;
+  for (int64_t e = ebeg; e < eend; e += estep) {
     const int c8 = (int)(e % C8);
     const int64_t pix = e / C8;  // pooled position (n, a, b)
     const int b = (int)(pix % Wo);
@@ -1173,7 +1192,7 @@ int pdt_bn_relu_maxpool_fwd_train(const uint16_t* x, const float* gamma, const f
   const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
   const int64_t nvec = (int64_t)N * Ho * Wo * (C / 8);
   hipLaunchKernelGGL(bn_apply_pool_kernel, dim3(row_grid((int64_t)N * Ho)), dim3(256), 0, s, x, a, b, y, code, N, H, W, C,
-                     Ho, Wo);
+                     Ho, Wo, g_pool_contig);
   return 0;
 }
 
@@ -1200,7 +1219,7 @@ int pdt_bn_relu_maxpool_fwd_train_parts(const float* part, int P, const uint16_t
   hipLaunchKernelGGL((bn_tiles_fin_kernel<true, true>), dim3(C / 64, PB), dim3(1024), 0, s, part, P, 1, M, C, lv, fa);
   const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
   hipLaunchKernelGGL(bn_apply_pool_kernel, dim3(row_grid((int64_t)N * Ho)), dim3(256), 0, s, x, a, b, y, code, N, H, W, C,
-                     Ho, Wo);
+                     Ho, Wo, g_pool_contig);
   return 0;
 }
 
@@ -1336,13 +1355,14 @@ int pdt_gap_bwd(const uint16_t* g, int N, int HW, int C, uint16_t* dy, const uin
 
 // A/B switch of the max-pool gradient kernel (maxpool_bwd2_kernel by default).
 void pdt_maxpool_bwd_v2(int on) { g_pool_bwd_v2 = on; }
+void pdt_pool_fwd_contig(int on) { g_pool_contig = on; }
 
 static void launch_pool_bwd_bn(const uint16_t* dy, const uint8_t* code, uint16_t* dz, int N, int H, int W, int C, int Ho,
                                int Wo, const uint16_t* x, const float* mean, float* part, int T, hipStream_t s) {
   // v2 covers input positions < (2 Ho, 2 Wo): every one when H <= 2 Ho and W <= 2 Wo (always, for 3x3/s2/p1)
   if (g_pool_bwd_v2 && H <= 2 * Ho && W <= 2 * Wo)
     hipLaunchKernelGGL(maxpool_bwd2_kernel<true>, dim3(T), dim3(256), 0, s, dy, code, dz, N, H, W, C, Ho, Wo, x, mean,
-                       part);
+                       part, g_pool_contig);
   else
     hipLaunchKernelGGL(maxpool_bwd_kernel<true>, dim3(T), dim3(256), 0, s, dy, code, dz, N, H, W, C, Ho, Wo, x, mean,
                        part);

@@ -26,9 +26,7 @@ def main():
     y, code, mean, invstd = n.bn_relu_maxpool_fwd(xb, gamma, beta, None, None, 0.1, 1e-5)
     dy = torch.randn(y.shape, device="cuda").bfloat16().contiguous(memory_format=cl)
     nbytes = dy.numel() * 2 + code.numel() + 2 * xb.numel() * 2
-    for v2 in (1, 0, 1, 0):
-        n.maxpool_bwd_v2(v2)
-        fn = lambda: n.maxpool3s2_bwd_bn_coef(dy, code, xb, gamma, mean, invstd, True)  # noqa: E731
+    def timeit(fn):
         fn()
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -37,9 +35,19 @@ def main():
             fn()
         e1.record()
         e1.synchronize()
-        us = e0.elapsed_time(e1) / 10 * 1e3
-        print(f"v2={v2}: {us:8.1f} us per call (pool gradient + BN finalize), {nbytes / us / 1e6:5.2f} TB/s", flush=True)
+        return e0.elapsed_time(e1) / 10 * 1e3
+
+    fbytes = xb.numel() * 2 + y.numel() * 2 + code.numel()
+    for v2, contig in ((1, 1), (1, 0), (0, 0), (1, 1), (1, 0), (0, 0)):
+        n.maxpool_bwd_v2(v2)
+        n.pool_fwd_contig(contig)
+        us = timeit(lambda: n.maxpool3s2_bwd_bn_coef(dy, code, xb, gamma, mean, invstd, True))
+        fus = timeit(lambda: n.bn_relu_maxpool_fwd(xb, gamma, beta, None, None, 0.1, 1e-5))
+        print(f"v2={v2} contig={contig}: backward {us:8.1f} us (pool gradient + BN finalize, {nbytes / us / 1e6:5.2f} TB/s)"
+              f"  forward {fus:8.1f} us (BN reduce + apply + pool, {fbytes / fus / 1e6:5.2f} TB/s apply-pass bytes)",
+              flush=True)
     n.maxpool_bwd_v2(1)
+    n.pool_fwd_contig(0)
 
 
 if __name__ == "__main__":
