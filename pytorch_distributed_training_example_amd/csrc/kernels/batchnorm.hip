@@ -1032,9 +1032,16 @@ inline int row_grid(int64_t rows) {  // row-wise stem kernels: <= 16 workgroups 
   return (int)(rows < cap ? (rows < 1 ? 1 : rows) : cap);
 }
 
-inline int apply_grid(int64_t nvec) {
+// Workgroups per CU before the apply passes grid-stride (tools/bn_apply_grid_sweep.py, 1024 images, ResNet-50
+// shapes): the residual forward apply and the backward apply run fastest at 2 per CU, the plain forward apply
+// at 3-4 (8 before: 5-15 % slower, e.g. C = 512 at 28 x 28: residual 715 -> 611 us, backward 804 -> 748 us,
+// plain 520 -> 491 us, each with its reduce pass). pdt_bn_apply_wgs(n) forces n for all three (A/B).
+enum ApplyKind { kApplyPlain = 0, kApplyRes = 1, kApplyBwd = 2 };
+int g_apply_wgs[3] = {4, 2, 2};
+
+inline int apply_grid(int64_t nvec, ApplyKind kind) {
   int64_t g = (nvec + 255) / 256;
-  const int64_t cap = 256 * 8;  // 8 workgroups per CU, grid-stride the rest
+  const int64_t cap = 256 * (int64_t)g_apply_wgs[kind];
   return (int)(g < cap ? (g < 1 ? 1 : g) : cap);
 }
 
@@ -1061,7 +1068,7 @@ int bn_bwd_from_partials(const float* part, int T, int BMt, const uint16_t* dy, 
   if (!dx) return 0;  // coefficients only: the consumer applies them (pdt_stem_conv_wgrad_bn)
   const int64_t nvec = M * C / 8;
   const int fixed = (2048 % C) == 0;
-  const int grid = apply_grid(nvec);
+  const int grid = apply_grid(nvec, kApplyBwd);
 #define PDT_BAPPLY(RL, RS)                                                                                      \
   hipLaunchKernelGGL((bn_bwd_apply_kernel<RL, RS, 1>), dim3(grid), dim3(256), 0, s, dy, x, mask, mean, A, B, D, \
                      dx, dres, nvec, C, fixed)
@@ -1114,7 +1121,7 @@ int pdt_bn_fwd_train(const uint16_t* x, const uint16_t* res, const float* res_a,
   if (!y) return 0;
   const int64_t nvec = M * C / 8;
   const int fixed = (2048 % C) == 0;
-  const int grid = apply_grid(nvec);
+  const int grid = apply_grid(nvec, res ? kApplyRes : kApplyPlain);
 #define PDT_APPLY(RL, RS, MK)                                                                                 \
   hipLaunchKernelGGL((bn_apply_kernel<RL, RS, MK, 1>), dim3(grid), dim3(256), 0, s, x, res, a, b, y, mask, \
                      nvec, C, fixed, nullptr, nullptr)
@@ -1162,7 +1169,7 @@ int pdt_bn_fwd_train_tiles(const float* part, int T, int BMt, const uint16_t* x,
   if (!y) return 0;
   const int64_t nvec = M * C / 8;
   const int fixed = (2048 % C) == 0;
-  const int grid = apply_grid(nvec);
+  const int grid = apply_grid(nvec, res ? kApplyRes : kApplyPlain);
   const bool mk = mask != nullptr;
   if (res_a && !(relu && res && mk)) return -3;
   if (res_a) PDT_APPLY_RA();
@@ -1247,7 +1254,7 @@ int pdt_bn_fwd_eval(const uint16_t* x, const uint16_t* res, const float* gamma, 
                      running_var, eps, a, b);
   const int64_t nvec = M * C / 8;
   const int fixed = (2048 % C) == 0;
-  const int grid = apply_grid(nvec);
+  const int grid = apply_grid(nvec, res ? kApplyRes : kApplyPlain);
   if (relu && res) PDT_APPLY(true, true, false);
   else if (relu) PDT_APPLY(true, false, false);
   else if (res) PDT_APPLY(false, true, false);
@@ -1275,7 +1282,7 @@ int pdt_bn_bwd_train(const uint16_t* dy, const uint16_t* x, const uint8_t* mask,
   else launch_reduce<1>(x, dy, mask, mean, M, C, ws, counters, fa, s);
   const int64_t nvec = M * C / 8;
   const int fixed = (2048 % C) == 0;
-  const int grid = apply_grid(nvec);
+  const int grid = apply_grid(nvec, kApplyBwd);
 #define PDT_BAPPLY(RL, RS)                                                                                      \
   hipLaunchKernelGGL((bn_bwd_apply_kernel<RL, RS, 1>), dim3(grid), dim3(256), 0, s, dy, x, mask, mean, A, B, D, \
                      dx, dres, nvec, C, fixed)
@@ -1356,6 +1363,11 @@ int pdt_gap_bwd(const uint16_t* g, int N, int HW, int C, uint16_t* dy, const uin
 // A/B switch of the max-pool gradient kernel (maxpool_bwd2_kernel by default).
 void pdt_maxpool_bwd_v2(int on) { g_pool_bwd_v2 = on; }
 void pdt_pool_fwd_contig(int on) { g_pool_contig = on; }
+void pdt_bn_apply_wgs(int n) {  // n <= 0: the measured defaults
+  g_apply_wgs[kApplyPlain] = n > 0 ? n : 4;
+  g_apply_wgs[kApplyRes] = n > 0 ? n : 2;
+  g_apply_wgs[kApplyBwd] = n > 0 ? n : 2;
+}
 
 static void launch_pool_bwd_bn(const uint16_t* dy, const uint8_t* code, uint16_t* dz, int N, int H, int W, int C, int Ho,
                                int Wo, const uint16_t* x, const float* mean, float* part, int T, hipStream_t s) {

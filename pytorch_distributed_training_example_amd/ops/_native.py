@@ -27,6 +27,8 @@ def _load():
             _mod.bn_tiles_fused(0)
         if os.environ.get("PDT_POOL_BWD_V2", "1") == "0":  # A/B: the per-position max-pool gradient kernel
             _mod.maxpool_bwd_v2(0)
+        if os.environ.get("PDT_BN_APPLY_WGS"):  # A/B: one grid cap (workgroups per CU) for every BN apply pass
+            _mod.bn_apply_wgs(int(os.environ["PDT_BN_APPLY_WGS"]))
         if os.environ.get("PDT_CONV1X1_PROBE"):  # A/B / diagnosis only (conv1x1.hip ApArgs::probe)
             _mod.conv1x1_probe(int(os.environ["PDT_CONV1X1_PROBE"]))
     except Exception as e:  # pragma: no cover - depends on build state
