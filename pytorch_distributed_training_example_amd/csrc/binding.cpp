@@ -145,6 +145,7 @@ void pdt_bn_tiles_fused(int on);
 void pdt_maxpool_bwd_v2(int on);
 void pdt_pool_fwd_contig(int on);
 void pdt_bn_apply_wgs(int n);
+void pdt_bn_row_wgs(int n);
 int pdt_gap_bwd_parts(int64_t M, int C);
 int pdt_gap_bwd(const uint16_t* g, int N, int HW, int C, uint16_t* dy, const uint16_t* xb, const uint8_t* mask,
                 const float* mean, float* part, hipStream_t s);
@@ -1944,6 +1945,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("maxpool_bwd_v2", [](int on) { pdt_maxpool_bwd_v2(on); });
   m.def("pool_fwd_contig", [](int on) { pdt_pool_fwd_contig(on); });
   m.def("bn_apply_wgs", [](int n) { pdt_bn_apply_wgs(n); });
+  m.def("bn_row_wgs", [](int n) { pdt_bn_row_wgs(n); });
   m.def("gap_bwd", &gap_bwd, py::arg("g"), py::arg("H"), py::arg("W"), py::arg("bn_x") = py::none(),
         py::arg("bn_mask") = py::none(), py::arg("bn_mean") = py::none());
   m.def("conv1x1_gemm_apply", &conv1x1_gemm_apply, py::arg("a"), py::arg("b"), py::arg("res"), py::arg("ab"),

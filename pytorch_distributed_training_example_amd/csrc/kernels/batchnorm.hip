@@ -1027,8 +1027,10 @@ int64_t launch_reduce(const uint16_t* x, const uint16_t* dy, const uint8_t* mask
   }
 }
 
+int g_row_wgs = 16;  // pdt_bn_row_wgs(n): A/B of the stem pool kernels' grid cap (workgroups per CU)
+
 inline int row_grid(int64_t rows) {  // row-wise stem kernels: <= 16 workgroups per CU, grid-stride
-  const int64_t cap = 256 * 16;
+  const int64_t cap = 256 * (int64_t)g_row_wgs;
   return (int)(rows < cap ? (rows < 1 ? 1 : rows) : cap);
 }
 
@@ -1363,6 +1365,8 @@ int pdt_gap_bwd(const uint16_t* g, int N, int HW, int C, uint16_t* dy, const uin
 // A/B switch of the max-pool gradient kernel (maxpool_bwd2_kernel by default).
 void pdt_maxpool_bwd_v2(int on) { g_pool_bwd_v2 = on; }
 void pdt_pool_fwd_contig(int on) { g_pool_contig = on; }
+void pdt_bn_row_wgs(int n) { g_row_wgs = n > 0 ? n : 16; }
+
 void pdt_bn_apply_wgs(int n) {  // n <= 0: the measured defaults
   g_apply_wgs[kApplyPlain] = n > 0 ? n : 4;
   g_apply_wgs[kApplyRes] = n > 0 ? n : 2;

@@ -38,9 +38,11 @@ def main():
         return e0.elapsed_time(e1) / 10 * 1e3
 
     fbytes = xb.numel() * 2 + y.numel() * 2 + code.numel()
-    for v2, contig in ((1, 1), (1, 0), (0, 0), (1, 1), (1, 0), (0, 0)):
+    for v2, contig, wgs in ((1, 0, 16), (1, 0, 8), (1, 0, 4), (1, 0, 2), (1, 0, 16), (1, 1, 16), (0, 0, 16)):
         n.maxpool_bwd_v2(v2)
         n.pool_fwd_contig(contig)
+        n.bn_row_wgs(wgs)
+        print(f"row grid cap {wgs:2d} per CU:", end=" ")
         us = timeit(lambda: n.maxpool3s2_bwd_bn_coef(dy, code, xb, gamma, mean, invstd, True))
         fus = timeit(lambda: n.bn_relu_maxpool_fwd(xb, gamma, beta, None, None, 0.1, 1e-5))
         print(f"v2={v2} contig={contig}: backward {us:8.1f} us (pool gradient + BN finalize, {nbytes / us / 1e6:5.2f} TB/s)"
@@ -48,6 +50,7 @@ def main():
               flush=True)
     n.maxpool_bwd_v2(1)
     n.pool_fwd_contig(0)
+    n.bn_row_wgs(0)
 
 
 if __name__ == "__main__":
