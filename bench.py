@@ -270,8 +270,21 @@ def run(args, ctx):
     if dev.type == "cuda":
         torch.cuda.nvtx.range_pop()
     exposed = ddp.comm_exposed_ms() if timing else None
+    leads = ddp.bucket_ready_lead_ms() if timing else None
     if timing:
         ddp.enable_comm_timing(False)
+    # which device every rank bound, as RCCL saw it: one distinct GPU per rank (train.py:138,147 uses
+    # every visible GPU, one process each)
+    pg_size = dist.get_world_size() if dist.is_initialized() else 1
+    dev_idx = torch.tensor([dev.index if dev.type == "cuda" else -1], device=dev, dtype=torch.int64)
+    if world > 1:
+        gathered = [torch.zeros_like(dev_idx) for _ in range(world)]
+        dist.all_gather(gathered, dev_idx)
+        rank_devices = [int(t.item()) for t in gathered]
+    else:
+        rank_devices = [int(dev_idx.item())]
+    if dev.type == "cuda" and len(set(rank_devices)) != len(rank_devices):
+        raise RuntimeError(f"ranks share GPUs: rank->device {rank_devices}")
     if world > 1:
         t = torch.tensor([elapsed, exposed if exposed is not None else -1.0], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -295,6 +308,11 @@ def run(args, ctx):
                    "comm_exposed_ms": None if exposed is None else round(exposed, 3),
                    "bucket_mb": ([round(b / 2 ** 20, 2) for b in ddp.bucket_bytes()]
                                  if hasattr(ddp, "bucket_bytes") else None),
+                   # per bucket (launch order), rank 0: ms between the compute-stream point where the
+                   # bucket's all-reduce could start and the end of backward's compute (overlap window)
+                   "bucket_ready_lead_ms": None if leads is None else [round(v, 3) for v in leads],
+                   "pg_size": pg_size, "pg_backend": dist.get_backend() if dist.is_initialized() else None,
+                   "rank_devices": rank_devices,
                    "deterministic": bool(det), "final_loss": round(float(loss.float().item()), 4)},
     }
     return result

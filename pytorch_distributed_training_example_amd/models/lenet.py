@@ -63,7 +63,9 @@ class LeNet(nn.Module):
             return False  # submodule hooks must see their modules run
         slopes = {self.ConvNet[i].negative_slope for i in (2, 5, 8)} | {self.FC[1].negative_slope}
         from ..ops.lenet import stem_native_ok
-        return len(slopes) == 1 and stem_native_ok(img, self.ConvNet[1].weight)
+        # the fused tail max-pools the raw conv outputs and activates the winner: equal to the
+        # reference's MaxPool(LeakyReLU(z)) (cnn.py:14-15) only for a strictly increasing activation
+        return len(slopes) == 1 and next(iter(slopes)) > 0 and stem_native_ok(img, self.ConvNet[1].weight)
 
     def forward(self, img: torch.Tensor) -> torch.Tensor:
         if self._can_fuse(img):

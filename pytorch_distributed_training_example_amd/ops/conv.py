@@ -113,7 +113,7 @@ def prepare_weights(convs) -> None:
     whose address is reused by another never matches."""
     import weakref
     _PREP["stamp"] += 1
-    stamp, old = _PREP["stamp"], _PREP["map"]
+    stamp = _PREP["stamp"]
     mp = {}
     srcs, dsts = [], []
     for m in convs:
@@ -124,12 +124,15 @@ def prepare_weights(convs) -> None:
         if k == 3 and not w.is_contiguous(memory_format=torch.channels_last):
             continue
         Co, Ci = w.shape[:2]
-        e = old.get(id(w))
-        dst = e[3] if (e is not None and e[1]() is w) else None
+        # the copy is OWNED by the weight (attribute), not by this module-global map: a captured hipGraph
+        # holds its address, and another model's training forward replaces the map — the buffer must
+        # live as long as the weight, not until the next prepare call of any model
+        dst = getattr(w, "_pdt_wprep", None)
         want = (Ci, Co) if k == 1 else (Ci, Co, 3, 3)
         if dst is None or tuple(dst.shape) != want or dst.device != w.device:
             dst = (torch.empty(want, dtype=w.dtype, device=w.device) if k == 1 else
                    torch.empty(want, dtype=w.dtype, device=w.device).contiguous(memory_format=torch.channels_last))
+            w._pdt_wprep = dst
         mp[id(w)] = (stamp, weakref.ref(w), w.data_ptr(), dst)
         srcs.append(w.detach())
         dsts.append(dst)

@@ -13,7 +13,7 @@ take the PyTorch reference path (same math).
 Token ids are range-checked on the device: an id outside [0, V) reads nothing (zero output row, no
 gradient) and sets an error word. Without a host sync, that word is copied to pinned memory behind
 every forward and checked at the next call (``IndexError``, one step late, like an asynchronous
-device assert); ``check_ids()`` syncs and checks now. ``PDT_EMBEDDING_CHECK=1`` checks every call.
+device assert; raised once, then cleared); ``check_ids()`` syncs and checks now. ``PDT_EMBEDDING_CHECK=1`` checks every call.
 """
 from __future__ import annotations
 
@@ -35,10 +35,20 @@ def _raise_if_bad(err_value: int) -> None:
                          "(its rows were zeroed; the error word stays set: see check_ids)")
 
 
-def _poll_previous() -> None:
+def _poll_previous(device) -> None:
+    """Raise (once) for an out-of-range id seen by the PREVIOUS call. The error is cleared before
+    raising — the device word is zeroed stream-ordered, ahead of this call's kernel — so a caller
+    that catches the IndexError is not poisoned on every later step (nn.Embedding raises once)."""
     ev = _ERR["event"]
     if ev is not None and not torch.cuda.is_current_stream_capturing() and ev.query():
-        _raise_if_bad(int(_ERR["host"][0]))
+        bad = int(_ERR["host"][0])
+        if bad:
+            _ERR["event"] = None
+            _ERR["host"].zero_()
+            native().embedding_err(torch.empty(0, device=device)).zero_()
+            raise IndexError("token_position_embedding: a token id of the PREVIOUS call was outside "
+                             "[0, vocab size) (its rows were zeroed; set PDT_EMBEDDING_CHECK=1 to "
+                             "raise on the offending call itself)")
 
 
 def check_ids(device=None) -> None:
@@ -58,7 +68,7 @@ class _EmbeddingFn(torch.autograd.Function):
     def forward(ctx, idx, wte, wpe):
         ctx.save_for_backward(idx)
         ctx.V, ctx.P = wte.shape[0], wpe.shape[0]
-        _poll_previous()
+        _poll_previous(idx.device)
         out = native().embedding_fwd(idx, wte, wpe)
         if _SYNC_CHECK:
             check_ids(idx.device)

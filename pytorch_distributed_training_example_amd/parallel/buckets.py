@@ -12,7 +12,14 @@ Assignment rules (compatible with torch DDP's so bucket boundaries line up):
   * a bucket holds a single (dtype, device);
   * the first bucket is capped at ``first_bucket_bytes`` (small, so the first
     collective starts early), the rest at ``bucket_cap_bytes``;
-  * buckets are ordered by the earliest (reversed) position they contain.
+  * buckets are ordered by the position at which they FILL (their last member in the
+    ready order), i.e. the order the reducer can launch them. Sorting by the *first*
+    member instead lets a small bucket of another dtype that opens early but fills last
+    (the fp32 norm parameters of a bf16-mixed model: ResNet-50's BN bucket fills at
+    position 159 of 161, GPT-2's LayerNorm bucket at 289 of 292) sit in front of every
+    bf16 bucket; launches are strictly in bucket order (ranks must agree), so it would
+    hold all of them until the end of backward. torch's reducer likewise keeps buckets
+    in fill order after its rebuild.
 
 MI355X sizing note: ring all-reduce over xGMI is bound by one ≈153 GB/s link per ring;
 RCCL runs several rings to use the 7 links. A 25 MiB bucket costs ≈0.04–0.3 ms at n=8
@@ -85,7 +92,7 @@ def compute_bucket_assignment(
     for key, (members, _) in open_buckets.items():
         if members:
             done.append((members, key[0], key[1]))
-    done.sort(key=lambda b: min(pos[i] for i in b[0]))
+    done.sort(key=lambda b: (max(pos[i] for i in b[0]), min(pos[i] for i in b[0])))
     specs: List[BucketSpec] = []
     for members, dtype, device in done:
         spec = BucketSpec(indices=list(members), dtype=dtype, device=device)

@@ -196,6 +196,9 @@ class DistributedDataParallel(nn.Module):
         # stream at the start of _finalize_backward and after the last bucket's wait
         self._comm_timing = False
         self._comm_events: List[tuple] = []
+        # per backward: (bucket index, event on the compute stream when the bucket launched)
+        self._launch_events: List[tuple] = []
+        self._lead_samples: List[List[tuple]] = []
 
         ignore = getattr(module, "_ddp_params_and_buffers_to_ignore", set())
         seen = set()
@@ -333,6 +336,10 @@ class DistributedDataParallel(nn.Module):
     def _launch(self, bucket: _Bucket) -> None:
         bucket.launched = True
         self._pack(bucket)
+        if self._comm_timing and cuda_available() and not torch.cuda.is_current_stream_capturing():
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()  # the compute stream's position when this bucket's gradients are complete
+            self._launch_events.append((bucket.index, ev))
         if bucket.comm_buffer is not bucket.buffer:
             multi_tensor.copy_([bucket.buffer], [bucket.comm_buffer])
         if self._comm_hook is not None:
@@ -382,6 +389,8 @@ class DistributedDataParallel(nn.Module):
             e1 = torch.cuda.Event(enable_timing=True)
             e1.record()
             self._comm_events.append((e0, e1))
+            self._lead_samples.append([(i, ev, e0) for i, ev in self._launch_events])
+        self._launch_events = []
         self._next_bucket = 0
         self._callback_queued = False
         self._num_iterations += 1
@@ -427,6 +436,8 @@ class DistributedDataParallel(nn.Module):
         whole all-reduce time here. Events only, no host sync until ``comm_exposed_ms``."""
         self._comm_timing = bool(on)
         self._comm_events = []
+        self._launch_events = []
+        self._lead_samples = []
 
     def comm_exposed_ms(self, reset: bool = True) -> Optional[float]:
         """Mean exposed-communication ms per timed backward (synchronises); None if none timed."""
@@ -437,6 +448,24 @@ class DistributedDataParallel(nn.Module):
             return None
         torch.cuda.synchronize()
         return sum(a.elapsed_time(b) for a, b in ev) / len(ev)
+
+    def bucket_ready_lead_ms(self, reset: bool = True) -> Optional[List[float]]:
+        """Per bucket (launch order): mean GPU time between the point in the compute stream where the
+        bucket's collective could start (all of its gradients produced and packed) and the end of
+        backward's compute. > 0 means the all-reduce had that long to run under backward; the bucket
+        that fills last has ~0. Meaningful at N=1 too (the collective itself is not timed), so it
+        shows whether the bucket ORDER lets communication overlap. Synchronises."""
+        samples = self._lead_samples
+        if reset:
+            self._lead_samples = []
+        if not samples:
+            return None
+        torch.cuda.synchronize()
+        acc: Dict[int, List[float]] = {}
+        for per_bwd in samples:
+            for i, ev, e0 in per_bwd:
+                acc.setdefault(i, []).append(ev.elapsed_time(e0))
+        return [sum(v) / len(v) for _, v in sorted(acc.items())]
 
     def bucket_bytes(self) -> List[int]:
         """Bytes of each gradient bucket, in launch order."""

@@ -117,6 +117,12 @@ def init_distributed(
     device = torch.device("cpu")
     if use_gpu:
         n = torch.cuda.device_count()
+        if backend in ("nccl", "pdt_p2p") and (e_lws > n or local_rank >= n):
+            # RCCL needs one GPU per rank; wrapping local_rank % n would put two ranks on one GPU and
+            # report an N-GPU measurement taken on fewer GPUs
+            raise RuntimeError(f"{backend}: local rank {local_rank} of {e_lws} but only {n} visible "
+                               f"GPU(s); RCCL needs one GPU per rank")
+        # gloo rehearsals may share GPUs between ranks (tests/dist_utils.py use_gpu=True)
         dev_idx = local_rank % max(n, 1)
         if set_device:
             torch.cuda.set_device(dev_idx)

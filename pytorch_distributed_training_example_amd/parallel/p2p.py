@@ -271,19 +271,36 @@ class P2PProcessGroup(dist.ProcessGroup):
                 self.p2p_calls += 1
                 p2p.all_reduce(tensors[0], average=op == dist.ReduceOp.AVG)
                 return _DoneWork(tensors)
-        if op == dist.ReduceOp.AVG and self.inner_backend != "nccl":
-            # gloo has no AVG: SUM, then divide (this path: CPU tensors, or buckets the staging
-            # buffer cannot take, e.g. past its capacity or numel % 8 != 0)
-            sum_opts = dist.AllreduceOptions()
-            sum_opts.reduceOp = dist.ReduceOp.SUM
-            self.inner.allreduce(tensors, sum_opts).wait()
-            for t in tensors:
-                t.div_(self._world)
-            return _DoneWork(tensors)
+        if self._avg_needs_divide(op):
+            # gloo has no AVG (this path: CPU tensors, or buckets the staging buffer cannot take,
+            # e.g. past its capacity or numel % 8 != 0)
+            self.inner.allreduce(tensors, self._sum_opts(dist.AllreduceOptions())).wait()
+            return self._divided(tensors)
         return self.inner.allreduce(tensors, opts)
 
+    # gloo has no ReduceOp.AVG: every AVG reduction that goes to a gloo inner group runs as SUM and
+    # then one true division per output (floating tensors only: an integer average is not exact)
+    def _avg_needs_divide(self, op) -> bool:
+        return op == dist.ReduceOp.AVG and self.inner_backend != "nccl"
+
+    @staticmethod
+    def _sum_opts(opts):
+        opts.reduceOp = dist.ReduceOp.SUM
+        return opts
+
+    def _divided(self, tensors):
+        for t in tensors:
+            if not t.is_floating_point():
+                raise TypeError(f"pdt_p2p: ReduceOp.AVG of a {t.dtype} tensor (integer average is not exact)")
+            t.div_(self._world)
+        return _DoneWork(tensors)
+
     def allreduce_coalesced(self, tensors, opts=None):
-        return self.inner.allreduce_coalesced(tensors, opts or dist.AllreduceCoalescedOptions())
+        opts = opts or dist.AllreduceCoalescedOptions()
+        if self._avg_needs_divide(opts.reduceOp):
+            self.inner.allreduce_coalesced(tensors, self._sum_opts(dist.AllreduceCoalescedOptions())).wait()
+            return self._divided(tensors)
+        return self.inner.allreduce_coalesced(tensors, opts)
 
     def broadcast(self, tensors, opts=None):
         return self.inner.broadcast(tensors, opts or dist.BroadcastOptions())
@@ -301,7 +318,13 @@ class P2PProcessGroup(dist.ProcessGroup):
         return self.inner._reduce_scatter_base(output, input, opts or dist.ReduceScatterOptions())
 
     def reduce(self, tensors, opts=None):
-        return self.inner.reduce(tensors, opts or dist.ReduceOptions())
+        opts = opts or dist.ReduceOptions()
+        if self._avg_needs_divide(opts.reduceOp):
+            sum_opts = dist.ReduceOptions()
+            sum_opts.rootRank, sum_opts.rootTensor = opts.rootRank, opts.rootTensor
+            self.inner.reduce(tensors, self._sum_opts(sum_opts)).wait()
+            return self._divided(tensors) if self._rank == opts.rootRank else _DoneWork(tensors)
+        return self.inner.reduce(tensors, opts)
 
     def alltoall_base(self, output, input, output_split_sizes, input_split_sizes, opts=None):
         return self.inner.alltoall_base(output, input, output_split_sizes, input_split_sizes,

@@ -71,5 +71,10 @@ def test_out_of_range_ids_are_reported_not_read():
         E.check_ids()
     with pytest.raises(IndexError):  # the next call reports the earlier bad batch without a sync
         E.token_position_embedding(idx[:, :2], wte, wpe)
+    # raised once and cleared: a caller that caught it is not poisoned on later good calls
+    E.token_position_embedding(idx[:, :2], wte, wpe)
+    torch.cuda.synchronize()
+    E.token_position_embedding(idx[:, :2], wte, wpe)
+    E.check_ids()
     E.reset_id_errors()
     E.check_ids()

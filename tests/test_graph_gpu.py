@@ -14,7 +14,7 @@ def _setup(seed=0):
     return to_bf16_mixed(get_model("resnet18", num_classes=16).cuda().to(memory_format=torch.channels_last))
 
 
-def _run(base, mode, lr, xs, ys):
+def _run(base, mode, lr, xs, ys, other=None):
     from pytorch_distributed_training_example_amd.engine.graph import StaticStep
     from pytorch_distributed_training_example_amd.ops.cross_entropy import cross_entropy
     from pytorch_distributed_training_example_amd.optim import FusedSGD
@@ -40,6 +40,8 @@ def _run(base, mode, lr, xs, ys):
         runner = StaticStep(step, [xs[0], ys[0]], warmup=3)
         runner.capture()
         for x, y in zip(xs[1:], ys[1:]):
+            if other is not None:  # another model's eager training forward + backward between replays
+                cross_entropy(other(x), y).backward()
             out.append(float(runner(x, y)))
     grads = [p.grad.detach().float().clone() for p in m.parameters()]
     return torch.tensor(out), [p.detach().float().clone() for p in m.parameters()], grads
@@ -93,3 +95,18 @@ def test_graph_step_matches_eager_training():
     # and the updates really happened
     moved = [(a - p0.float()).norm().item() for a, p0 in zip(pg, base.parameters())]
     assert max(moved) > 0
+
+
+def test_graph_replay_survives_other_models_training_forward():
+    """The captured step holds the addresses of the per-step weight transforms (W^T / flipped 3x3,
+    ops/conv.py prepare_weights). Another model's training forward re-runs prepare_weights for ITS
+    convs; the captured model's buffers must stay alive and untouched (they are owned by the
+    weights, not by the module-global map), so the replay still equals eager bit for bit."""
+    base = _setup()
+    other = _setup(seed=7)
+    xs, ys = _data()
+    le, _, ge = _run(base, "eager", 0.0, xs, ys)
+    lg, _, gg = _run(base, "graph", 0.0, xs, ys, other=other)
+    assert torch.equal(lg, le), (lg, le)
+    bad = [i for i, (a, b) in enumerate(zip(gg, ge)) if not torch.equal(a, b)]
+    assert not bad, f"{len(bad)} of {len(ge)} gradients differ (first: {bad[:5]})"

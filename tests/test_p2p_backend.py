@@ -20,6 +20,16 @@ def _worker(rank, world):
     dist.all_reduce(t)
     avg = torch.arange(8, dtype=torch.float32) * (rank + 1)
     dist.all_reduce(avg, op=dist.ReduceOp.AVG)  # gloo has no AVG: the backend sums and divides
+    # every AVG that reaches the gloo inner group goes through SUM + divide (not just all_reduce)
+    co = [torch.full((4,), float(rank + 1)), torch.full((2,), 2.0 * (rank + 1))]
+    dist.all_reduce_coalesced(co, op=dist.ReduceOp.AVG)
+    red = torch.full((4,), float(rank + 1))
+    dist.reduce(red, dst=0, op=dist.ReduceOp.AVG)
+    iavg_err = None
+    try:
+        dist.all_reduce(torch.ones(4, dtype=torch.int32), op=dist.ReduceOp.AVG)
+    except Exception as e:  # integer average is not exact: refused, not truncated
+        iavg_err = type(e).__name__
     b = torch.full((3,), float(rank))
     dist.broadcast(b, src=1)
     outs = [torch.zeros(2) for _ in range(world)]
@@ -33,13 +43,18 @@ def _worker(rank, world):
     x = torch.ones(3, 4) * (rank + 1)
     ddp(x).sum().backward()
     pg = dist.distributed_c10d._get_default_group()
-    return t, b, torch.stack(outs), m.weight.grad.clone(), isinstance(pg, P2PProcessGroup) or "pdt_p2p", avg
+    return (t, b, torch.stack(outs), m.weight.grad.clone(), isinstance(pg, P2PProcessGroup) or "pdt_p2p", avg,
+            co, red, iavg_err)
 
 
 def test_pdt_p2p_backend_delegates_on_cpu():
     out = run_ranks(_worker, 2)
     for r in range(2):
-        t, b, g, wg, kind, avg = out[r]
+        t, b, g, wg, kind, avg, co, red, iavg_err = out[r]
+        assert torch.equal(co[0], torch.full((4,), 1.5)) and torch.equal(co[1], torch.full((2,), 3.0))
+        if r == 0:
+            assert torch.equal(red, torch.full((4,), 1.5))
+        assert iavg_err is not None
         assert torch.equal(t, torch.arange(8, dtype=torch.float32) * 3)
         assert torch.equal(avg, torch.arange(8, dtype=torch.float32) * 1.5)
         assert torch.equal(b, torch.ones(3))

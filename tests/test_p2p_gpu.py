@@ -280,3 +280,55 @@ def test_first_bucket_allreduce_overlaps_backward():
         assert nb >= 3, nb
         assert lead_ms > 0.0, f"bucket 0's all-reduce ended {-lead_ms:.3f} ms AFTER backward's compute"
         assert exposed is not None and exposed >= 0.0
+
+
+def _overlap_bf16_worker(rank, world):
+    """bf16-mixed ResNet-18 (fp32 BN parameters in their own bucket): with buckets in FILL order
+    (parallel/buckets.py) the fp32 norm bucket, which fills last, no longer gates the bf16 buckets —
+    each bf16 bucket's all-reduce is issued the moment it fills and completes under backward."""
+    from pytorch_distributed_training_example_amd.models import get_model
+    from pytorch_distributed_training_example_amd.models.precision import to_bf16_mixed
+    from pytorch_distributed_training_example_amd.ops.cross_entropy import cross_entropy
+    from pytorch_distributed_training_example_amd.parallel import DistributedDataParallel
+    from pytorch_distributed_training_example_amd.parallel.p2p import (P2PAllReduce, P2PHookState,
+                                                                        p2p_allreduce_hook)
+    torch.manual_seed(0)
+    model = to_bf16_mixed(get_model("resnet18", num_classes=16).cuda().to(memory_format=torch.channels_last))
+    ddp = DistributedDataParallel(model, bucket_cap_mb=4, first_bucket_mb=1)
+    state = P2PHookState(P2PAllReduce(capacity_bytes=8 << 20))
+    done = []
+
+    def hook(st, bucket):
+        fut = p2p_allreduce_hook(st, bucket)
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(st.stream)
+        done.append((bucket.index(), str(bucket.buffer().dtype), ev))
+        return fut
+    ddp.register_comm_hook(state, hook)
+    ddp.enable_comm_timing(True)
+    g = torch.Generator(device="cuda").manual_seed(1 + rank)
+    x = torch.randn(128, 3, 128, 128, device="cuda", generator=g).bfloat16().contiguous(
+        memory_format=torch.channels_last)
+    y = torch.randint(0, 16, (128,), device="cuda", generator=g)
+    for _ in range(3):
+        done.clear()
+        ddp.zero_grad(set_to_none=True)
+        cross_entropy(ddp(x), y).backward()
+    torch.cuda.synchronize()
+    state.p2p.check()
+    end_of_compute = ddp._comm_events[-1][0]
+    leads = [(i, dt, ev.elapsed_time(end_of_compute)) for i, dt, ev in done]
+    return leads, ddp.bucket_ready_lead_ms()
+
+
+def test_bf16_buckets_allreduce_under_backward():
+    out = run_ranks(_overlap_bf16_worker, 2, use_gpu=True)
+    for leads, ready in out:
+        bf16 = [(i, ms) for i, dt, ms in leads if dt == "torch.bfloat16"]
+        fp32 = [i for i, dt, _ in leads if dt == "torch.float32"]
+        assert len(bf16) >= 3 and fp32, leads
+        assert fp32 == [max(i for i, _, _ in leads)], f"the fp32 norm bucket must launch last: {leads}"
+        late = [(i, round(ms, 3)) for i, ms in bf16[:-1] if ms <= 0.0]
+        assert not late, f"bf16 buckets completed AFTER backward's compute: {late} (all: {leads})"
+        # launch lead (bench.py's bucket_ready_lead_ms): decreasing along the launch order
+        assert ready is not None and ready[0] > ready[-1]
