@@ -54,6 +54,7 @@ int pdt_conv1x1_bwd_fused(const uint16_t* dy, const uint16_t* z, const uint8_t* 
                           const uint8_t* bm, const float* bmean, float* bpart, const float* xcoef, uint8_t* mask_out,
                           uint16_t* dxa, uint16_t* dw, float* ws, int M, int C4, int CW, hipStream_t s);
 void pdt_conv1x1_bwd_fused_tune(int grid);
+int pdt_conv1x1_bwd_fused_slack(int slack);
 void pdt_bn_tune(int variant, int target_blocks, int u_fwd, int u_bwd);
 int pdt_bn_fwd_train(const uint16_t* x, const uint16_t* res, const float* res_a, const float* res_b,
                      const float* gamma, const float* beta,
@@ -141,6 +142,7 @@ int pdt_conv1x1_gemm(const uint16_t* a, const uint16_t* b, uint16_t* y, const ui
                      const float* bn_mean, float* bn_part, int c_s, int c_H, int c_W, const float* acoef,
                      hipStream_t s);
 void pdt_conv1x1_probe(int probe);
+int pdt_conv1x1_persist(int mode);
 void pdt_bn_tiles_fused(int on);
 void pdt_maxpool_bwd_v2(int on);
 void pdt_pool_fwd_contig(int on);
@@ -1940,6 +1942,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("bn_mask") = py::none(), py::arg("bn_mean") = py::none(), py::arg("c_stride") = 0,
         py::arg("c_H") = 0, py::arg("c_W") = 0, py::arg("a_coef") = py::none());
   m.def("conv1x1_probe", [](int probe) { pdt_conv1x1_probe(probe); });
+  m.def("conv1x1_persist", [](int mode) { return pdt_conv1x1_persist(mode); },
+        "1x1 GEMM persistence mode (0 off, 1 measured kinds, 2 all, -1 env default); returns the previous mode");
   m.def("weight_prep", &weight_prep);
   m.def("bn_tiles_fused", [](int on) { pdt_bn_tiles_fused(on); });
   m.def("maxpool_bwd_v2", [](int on) { pdt_maxpool_bwd_v2(on); });
@@ -1986,6 +1990,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("coef"), py::arg("w"), py::arg("xa"), py::arg("bn_x") = py::none(), py::arg("bn_mask") = py::none(),
         py::arg("bn_mean") = py::none(), py::arg("xcoef") = py::none(), py::arg("wt") = py::none());
   m.def("conv1x1_bwd_fused_tune", [](int grid) { pdt_conv1x1_bwd_fused_tune(grid); });
+  m.def("conv1x1_bwd_fused_slack", [](int slack) { return pdt_conv1x1_bwd_fused_slack(slack); },
+        "role lockstep slack of the fused conv3 + bn3 backward in stages (0 off, -1 query); returns the previous");
   m.def("ce_fwd", &ce_fwd);
   m.def("ce_bwd", &ce_bwd);
   m.def("ln_fwd", &ln_fwd, py::arg("x"), py::arg("w"), py::arg("b"), py::arg("eps"), py::arg("res") = py::none());

@@ -60,6 +60,9 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 #define PDT_LDS __attribute__((address_space(3)))
 
 __device__ __attribute__((aligned(256))) uint4 g_gemm_zero[16];  // zero page for rows past M (never written)
+__device__ uint8_t g_mask_ones[16] = {  // (non-const: global, not constant, address space)
+   0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff,
+                                            0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff};  // "no mask"
 
 template <int BN_, int WM_, int WN_>
 struct G1 {
@@ -124,12 +127,13 @@ struct ApArgs {
 int g_probe = 0;
 
 // NT: streaming (non-temporal) output stores. ATR: acoef = [2][K] fp32 (a, then b), see the header.
-template <class Cf, bool ACC, bool STATS, bool NT, bool BSTATS, bool ATR = false, bool APPLY = false>
+template <class Cf, bool ACC, bool STATS, bool NT, bool BSTATS, bool ATR = false, bool APPLY = false, bool STR = false>
 __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv1x1_kernel(
     const uint16_t* __restrict__ A, const uint16_t* __restrict__ B, uint16_t* Y, const uint16_t* Cin,
     const uint8_t* __restrict__ Cmask, float* __restrict__ part, int M, int K, int N, BnSrc bs, CGeom cg,
     const float* __restrict__ acoef, ApArgs ap) {
   static_assert(!(APPLY && (ACC || STATS || BSTATS)), "APPLY is a forward epilogue of its own");
+  static_assert(!STR || ACC, "STR: a strided accumulate source");
   constexpr int BM = Cf::BM, BN = Cf::BN;
   constexpr int WROWS = BM / Cf::WM, WCOLS = BN / Cf::WN;
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -290,36 +294,47 @@ __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv1x1_kernel(
   // (Both sources at 128 VGPRs — the 8-wave tile with ACC and BSTATS — go in two batches of rows:
   // all eight rows at once spilled there.)
   constexpr int kRowStep = Cf::kThreads / kChunks, kIt = BM / kRowStep;
-  constexpr int kB = (ACC && BSTATS && Cf::kWaves == 8) ? kIt / 2 : kIt;
+  constexpr int kB = (ACC && BSTATS && Cf::kWaves >= 8) ? kIt / 2 : kIt;
   static_assert(kRowStep * kIt == BM && kIt % kB == 0, "epilogue rows");
   const int r0 = tid / kChunks, c = tid % kChunks;
+  // The loads are BRANCH-FREE: a row past M reads the tile's last valid row (its results are dropped),
+  // a null mask reads a 0xff byte, and the strided source is a separate instantiation (STR). Written
+  // with per-row conditions, hipcc branched around every load and put an s_waitcnt vmcnt(1) / (0)
+  // into each row's branch (cdna_hip_programming.md §5, trap (c)): the rows' loads were serialised
+  // after all, one memory latency each.
+  const uint8_t* const cm_base = Cmask ? Cmask : g_mask_ones;
+  const int64_t cm_scale = Cmask ? 1 : 0;
+  const uint8_t* const bm_base = bs.mask ? bs.mask : g_mask_ones;
+  const int64_t bm_scale = bs.mask ? 1 : 0;
 #pragma unroll 1
   for (int h = 0; h < kIt; h += kB) {
   uint4 cv[kB], xbv[kB];
   unsigned cmk[kB], bmkv[kB];
+  bool okv[kB];
 #pragma unroll
   for (int it = 0; it < kB; ++it) {
     const int m = m0 + r0 + kRowStep * (h + it);
-    cmk[it] = 0u;
-    bmkv[it] = 0xffu;
-    if (m >= M) continue;
-    const int64_t off = (int64_t)m * N + n0 + c * 8;
+    const bool ok = m < M;
+    okv[it] = ok;
+    const int mc = ok ? m : M - 1;
+    const int64_t off = (int64_t)mc * N + n0 + c * 8;
     if constexpr (BSTATS) {
       xbv[it] = *reinterpret_cast<const uint4*>(bs.x + off);
-      if (bs.mask) bmkv[it] = bs.mask[off >> 3];
+      const unsigned b = bm_base[(off >> 3) * bm_scale];
+      bmkv[it] = ok ? b : 0u;  // a dropped row adds nothing to the reduction
     }
     if constexpr (APPLY) cv[it] = *reinterpret_cast<const uint4*>(Cin + off);  // the residual
     if constexpr (ACC) {
-      cmk[it] = Cmask ? Cmask[off >> 3] : 0xffu;  // C = Cin * mask: a ReLU's masked gradient
-      if (cg.s) {  // compact strided source
-        const int w = m % cg.W, t = m / cg.W, h = t % cg.H, n = t / cg.H;
-        if (h % cg.s == 0 && w % cg.s == 0)
-          cv[it] = *reinterpret_cast<const uint4*>(Cin + ((int64_t)(n * cg.Hs + h / cg.s) * cg.Ws + w / cg.s) * N +
-                                                   n0 + c * 8);
-        else
-          cmk[it] = 0u;
+      const unsigned mk = cm_base[(off >> 3) * cm_scale];  // C = Cin * mask: a ReLU's masked gradient
+      if constexpr (STR) {  // compact strided source: rows off the sampling grid add nothing
+        const int w = mc % cg.W, t = mc / cg.W, hh = t % cg.H, n = t / cg.H;
+        const bool on = hh % cg.s == 0 && w % cg.s == 0;
+        const int64_t co = on ? ((int64_t)(n * cg.Hs + hh / cg.s) * cg.Ws + w / cg.s) * N : 0;
+        cv[it] = *reinterpret_cast<const uint4*>(Cin + co + n0 + c * 8);
+        cmk[it] = on ? mk : 0u;
       } else {
         cv[it] = *reinterpret_cast<const uint4*>(Cin + off);
+        cmk[it] = mk;
       }
     }
   }
@@ -327,20 +342,18 @@ __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv1x1_kernel(
   for (int it = 0; it < kB; ++it) {
     const int r = r0 + kRowStep * (h + it);
     const int m = m0 + r;
-    if (m >= M) continue;
-    uint4 v = *reinterpret_cast<const uint4*>(lds + r * Cf::kEpiStride + c * 16);
-    const int64_t off = (int64_t)m * N + n0 + c * 8;
+    const bool ok = okv[it];
+    uint4 v = *reinterpret_cast<const uint4*>(lds + (ok ? r : 0) * Cf::kEpiStride + c * 16);
+    const int64_t off = (int64_t)(ok ? m : 0) * N + n0 + c * 8;
     if constexpr (ACC) {
-      float a[8], cc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+      float a[8], cc[8];
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w}, cw[4] = {cv[it].x, cv[it].y, cv[it].z, cv[it].w};
 #pragma unroll
-      for (int k = 0; k < 4; ++k) { a[2 * k] = __uint_as_float(w[k] << 16); a[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u); }
-      const unsigned mb = cmk[it];
-      if (mb) {
-        const uint32_t cw[4] = {cv[it].x, cv[it].y, cv[it].z, cv[it].w};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) { cc[2 * k] = __uint_as_float(cw[k] << 16); cc[2 * k + 1] = __uint_as_float(cw[k] & 0xffff0000u); }
+      for (int k = 0; k < 4; ++k) {
+        a[2 * k] = __uint_as_float(w[k] << 16); a[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+        cc[2 * k] = __uint_as_float(cw[k] << 16); cc[2 * k + 1] = __uint_as_float(cw[k] & 0xffff0000u);
       }
+      const unsigned mb = cmk[it];
 #pragma unroll
       for (int k = 0; k < 8; ++k) a[k] += (mb >> k) & 1u ? cc[k] : 0.f;
       v.x = (uint32_t)f2bf(a[0]) | ((uint32_t)f2bf(a[1]) << 16);
@@ -348,6 +361,7 @@ __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv1x1_kernel(
       v.z = (uint32_t)f2bf(a[4]) | ((uint32_t)f2bf(a[5]) << 16);
       v.w = (uint32_t)f2bf(a[6]) | ((uint32_t)f2bf(a[7]) << 16);
     }
+    unsigned amb = 0;
     if constexpr (APPLY) {  // relu(a z + b + r): the same fp32 operations as batchnorm.hip bn_apply_kernel
       float z[8], r[8];
       const uint32_t w[4] = {v.x, v.y, v.z, v.w}, rw[4] = {cv[it].x, cv[it].y, cv[it].z, cv[it].w};
@@ -356,22 +370,24 @@ __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv1x1_kernel(
         z[2 * k] = __uint_as_float(w[k] << 16); z[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
         r[2 * k] = __uint_as_float(rw[k] << 16); r[2 * k + 1] = __uint_as_float(rw[k] & 0xffff0000u);
       }
-      unsigned mb = 0;
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         float t = z[k] * pa[k] + pb[k];
         t += ap.rab ? r[k] * pra[k] + prb[k] : r[k];
-        mb |= (t > 0.f ? 1u : 0u) << k;
+        amb |= (t > 0.f ? 1u : 0u) << k;
         z[k] = t > 0.f ? t : 0.f;
       }
       v.x = (uint32_t)f2bf(z[0]) | ((uint32_t)f2bf(z[1]) << 16);
       v.y = (uint32_t)f2bf(z[2]) | ((uint32_t)f2bf(z[3]) << 16);
       v.z = (uint32_t)f2bf(z[4]) | ((uint32_t)f2bf(z[5]) << 16);
       v.w = (uint32_t)f2bf(z[6]) | ((uint32_t)f2bf(z[7]) << 16);
-      if (!(probe & 32)) ap.mask[off >> 3] = (uint8_t)mb;
     }
     if constexpr (BSTATS) bn_bwd_accum8(v, xbv[it], bmkv[it], bmu, bs1, bs2);
+    if (!ok) continue;
     if constexpr (STATS) rs8_add(rst, v);
+    if constexpr (APPLY) {
+      if (!(probe & 32)) ap.mask[off >> 3] = (uint8_t)amb;
+    }
     if (probe & 1) continue;
     if constexpr (NT) {
       const u32x4 t = {v.x, v.y, v.z, v.w};
@@ -391,16 +407,400 @@ __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv1x1_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------------------------------
+// PERSISTENT variant (PDT_CONV1X1_PERSIST; by default for the kinds where it measured faster, see g_persist): one
+// workgroup per CU (two for the 64-channel tile) walks its share of the tiles, and tile t+1's first
+// two operand k-steps are DMA'd into the ring WHILE tile t's epilogue runs (its staging area is placed
+// past those two slots), so its output stores drain under tile t+1's main loop. Measured reason
+// (profiles/r4/conv1x1_probe_b1024.txt): with nothing computed, loaded or stored the one-tile-per-
+// workgroup kernel still took ~245 us for 12,544 tiles of 1024 threads (~5 us per tile per CU of launch,
+// prologue and epilogue serialisation), and with one 135-KB workgroup per CU every tile ran its DMA
+// wait, MFMA and epilogue back to back.
+//
+// vmcnt accounting (hand-counted waits; the DMAs are inline asm, invisible to hipcc, so its own waits
+// for the epilogue's register loads can only over-wait): in issue order a tile's ops are D0, D1 (issued
+// by the previous tile's epilogue, or the prologue), that previous epilogue's kStores row stores, then
+// D2 (at step 0), D3 (step 1), ... Waiting for D_s leaves younger: D_{s+1} when it exists, plus the
+// previous epilogue's row stores while s < 2. Every row store is issued by every thread (rows past M
+// go to a sink) so the count is exact; the statistics stores come last and only make a wait stricter.
+template <class Cf>
+struct PL {
+  static constexpr int kStgOff = 2 * Cf::kSlot;              // slots 0 / 1 take tile t+1's D0 / D1
+  static constexpr int kFull = Cf::BM * Cf::kEpiStride;
+  static constexpr int kHalves = kStgOff + kFull <= 152 * 1024 ? 1 : 2;
+  static constexpr int kStg = kFull / kHalves;
+  static constexpr int kRed0 = Cf::kWaves * (Cf::BN / 8) * 16 * 4, kRed1 = Cf::kWaves * 2 * Cf::BN * 4;
+  static constexpr int kRed = kRed0 > kRed1 ? kRed0 : kRed1;
+  static constexpr int kArea = kStg > kRed ? kStg : kRed;
+  static constexpr int kLds = 3 * Cf::kSlot > kStgOff + kArea ? 3 * Cf::kSlot : kStgOff + kArea;
+  static constexpr int kOcc = (160 * 1024) / kLds;
+  static constexpr int kMinWaves = kOcc * Cf::kThreads / 256 > 0 ? kOcc * Cf::kThreads / 256 : 1;
+  static_assert(kLds <= 160 * 1024 && kFull % kHalves == 0, "LDS");
+};
+
+__device__ __attribute__((aligned(256))) uint4 g_gemm_sink[1024];  // row stores past M (exact vmcnt)
+__device__ uint8_t g_mask_sink[1024];
+
+__device__ __forceinline__ void dma16a(const void* src, char* lds_wave_base) {
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(PDT_LDS const char*)lds_wave_base);
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(m0) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void wait_vmn() {  // s_waitcnt vmcnt(N), expcnt / lgkmcnt unconstrained
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+
+template <class Cf, bool ACC, bool STATS, bool BSTATS, bool ATR, bool APPLY, bool STR>
+__global__ __launch_bounds__(Cf::kThreads, PL<Cf>::kMinWaves) void conv1x1p_kernel(
+    const uint16_t* __restrict__ A, const uint16_t* __restrict__ B, uint16_t* Y, const uint16_t* Cin,
+    const uint8_t* __restrict__ Cmask, float* __restrict__ part, int M, int K, int N, BnSrc bs, CGeom cg,
+    const float* __restrict__ acoef, ApArgs ap) {
+  static_assert(!(APPLY && (ACC || STATS || BSTATS)), "APPLY is a forward epilogue of its own");
+  static_assert(!STR || ACC, "STR: a strided accumulate source");
+  using L = PL<Cf>;
+  constexpr int BM = Cf::BM, BN = Cf::BN, kG = Cf::kG, kHalves = L::kHalves;
+  constexpr int WROWS = BM / Cf::WM, WCOLS = BN / Cf::WN;
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid % Cf::WM, wn = wid / Cf::WM;
+  const int ntn = N / BN, T = (M + BM - 1) / BM, total = T * ntn;
+  // tiles: 8 contiguous chunks, one per XCD (blocks b, b + 8, ... under round-robin placement — speed
+  // only): the N-tiles of a pixel tile run side by side on one L2
+  const int G = gridDim.x, xg = blockIdx.x % 8, jg = blockIdx.x / 8, gx = (G - xg + 7) / 8;
+  const int c_lo = (int)((int64_t)total * xg / 8), c_hi = (int)((int64_t)total * (xg + 1) / 8);
+  int tile = c_lo + jg;
+  if (tile >= c_hi) return;  // (uniform: before any barrier)
+  const int S = K / Cf::BK;
+  char* const stg = lds + L::kStgOff;
+
+  const int sub = lane >> 2, p = lane & 3;
+  auto aoff_of = [&](int m0, int i) {
+    const int r = (wid * Cf::kALd + i) * 16 + sub;
+    return m0 + r < M ? (m0 + r) * K + chk64(r, p) * 8 : -1;
+  };
+  auto boff_of = [&](int n0, int j) {
+    const int r = (wid * Cf::kBLd + j) * 16 + sub;
+    return (n0 + r) * K + chk64(r, p) * 8;
+  };
+  int aoff[Cf::kALd], boff[Cf::kBLd];
+  auto issue = [&](int s, int slot_i) {
+    char* slot = lds + slot_i * Cf::kSlot;
+    const int ko = s * Cf::BK;
+#pragma unroll
+    for (int i = 0; i < Cf::kALd; ++i)
+      dma16a(aoff[i] >= 0 ? (const void*)(A + (aoff[i] + ko)) : (const void*)g_gemm_zero, slot + (wid * Cf::kALd + i) * 1024);
+#pragma unroll
+    for (int j = 0; j < Cf::kBLd; ++j) dma16a(B + (boff[j] + ko), slot + Cf::kABytes + (wid * Cf::kBLd + j) * 1024);
+  };
+
+  float* const ctab = reinterpret_cast<float*>(lds + L::kLds);
+  if constexpr (ATR) {
+    for (int i = tid; i < 2 * K; i += Cf::kThreads) ctab[i] = acoef[i];
+    __syncthreads();  // (no DMA issued yet: a plain barrier)
+  }
+  // kernel-lifetime epilogue constants
+  constexpr int kChunks = BN / 8;
+  constexpr int kRowStep = Cf::kThreads / kChunks, kIt = BM / kRowStep;
+  constexpr int kItH = kIt / kHalves;
+  // rows per batch of loads (registers: 128 per lane at 16 waves, 256 below)
+  constexpr int kB = (ACC && BSTATS) ? (Cf::kWaves >= 16 ? 2 : (kItH >= 8 ? kItH / 2 : kItH)) : kItH;
+  constexpr int kStores = kIt * (APPLY ? 2 : 1);  // row stores per thread per tile (exact)
+  static_assert(kRowStep * kIt == BM && kIt % kHalves == 0 && kItH % kB == 0, "epilogue rows");
+  const int r0 = tid / kChunks, c = tid % kChunks;
+  const uint8_t* const cm_base = Cmask ? Cmask : g_mask_ones;
+  const int64_t cm_scale = Cmask ? 1 : 0;
+  const uint8_t* const bm_base = bs.mask ? bs.mask : g_mask_ones;
+  const int64_t bm_scale = bs.mask ? 1 : 0;
+
+  int mt = tile / ntn, n0 = (tile % ntn) * BN, m0 = mt * BM;
+#pragma unroll
+  for (int i = 0; i < Cf::kALd; ++i) aoff[i] = aoff_of(m0, i);
+#pragma unroll
+  for (int j = 0; j < Cf::kBLd; ++j) boff[j] = boff_of(n0, j);
+  issue(0, 0);
+  if (S > 1) issue(1, 1);
+  bool first = true;
+  const int lrow = lane & 15, lchk = lane >> 4;
+  for (;;) {
+    f4 acc[Cf::kMB][Cf::kNB];
+#pragma unroll
+    for (int i = 0; i < Cf::kMB; ++i)
+#pragma unroll
+      for (int j = 0; j < Cf::kNB; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; s < S; ++s) {
+      const bool nxt = s + 1 < S;
+      if (s >= 2 || first) {
+        if (nxt) wait_vmn<kG>(); else wait_vmn<0>();
+      } else {  // s < 2 after an epilogue: its row stores are younger than D_s
+        if (nxt) wait_vmn<kG + kStores>(); else wait_vmn<kStores>();
+      }
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (s + 2 < S) issue(s + 2, (s + 2) % 3);  // slot (s+2)%3 was last read at step s-1
+      const char* As = lds + (s % 3) * Cf::kSlot;
+      const char* Bs = As + Cf::kABytes;
+      bf16x8 a[Cf::kMB], b[Cf::kNB];
+#pragma unroll
+      for (int i = 0; i < Cf::kMB; ++i) a[i] = *reinterpret_cast<const bf16x8*>(As + swz64(wm * WROWS + i * 16 + lrow, lchk));
+#pragma unroll
+      for (int j = 0; j < Cf::kNB; ++j) b[j] = *reinterpret_cast<const bf16x8*>(Bs + swz64(wn * WCOLS + j * 16 + lrow, lchk));
+      if constexpr (ATR) {
+        const int k0 = s * Cf::BK + 8 * lchk;
+        float ca[8], cb[8];
+        *reinterpret_cast<float4*>(ca) = *reinterpret_cast<const float4*>(ctab + k0);
+        *reinterpret_cast<float4*>(ca + 4) = *reinterpret_cast<const float4*>(ctab + k0 + 4);
+        *reinterpret_cast<float4*>(cb) = *reinterpret_cast<const float4*>(ctab + K + k0);
+        *reinterpret_cast<float4*>(cb + 4) = *reinterpret_cast<const float4*>(ctab + K + k0 + 4);
+#pragma unroll
+        for (int i = 0; i < Cf::kMB; ++i) {
+          typedef unsigned u4 __attribute__((ext_vector_type(4)));
+          const u4 w = __builtin_bit_cast(u4, a[i]);
+          u4 o;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const float t0 = __uint_as_float(w[k] << 16) * ca[2 * k] + cb[2 * k];
+            const float t1 = __uint_as_float(w[k] & 0xffff0000u) * ca[2 * k + 1] + cb[2 * k + 1];
+            o[k] = (uint32_t)f2bf(t0 > 0.f ? t0 : 0.f) | ((uint32_t)f2bf(t1 > 0.f ? t1 : 0.f) << 16);
+          }
+          a[i] = __builtin_bit_cast(bf16x8, o);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < Cf::kMB; ++i)
+#pragma unroll
+        for (int j = 0; j < Cf::kNB; ++j) acc[i][j] = mfma(b[j], a[i], acc[i][j]);  // D[n][m]
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+
+    // the accumulators as the bf16 values the tile stores (half the registers to carry into the
+    // epilogue: a wave of the second half keeps them through the first half's rows)
+    uint2 pk[Cf::kMB][Cf::kNB];
+#pragma unroll
+    for (int i = 0; i < Cf::kMB; ++i)
+#pragma unroll
+      for (int j = 0; j < Cf::kNB; ++j) {
+        const f4 v = acc[i][j];
+        pk[i][j].x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+        pk[i][j].y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+      }
+    // ---- epilogue of this tile; the next tile's D0 / D1 go out first (slots 0 / 1: every wave is past
+    // its last fragment read after this barrier)
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const int cur_m0 = m0, cur_n0 = n0, cur_mt = mt;
+    const int next = tile + gx;
+    const bool has_next = next < c_hi;
+    if (has_next) {
+      mt = next / ntn; n0 = (next % ntn) * BN; m0 = mt * BM;
+#pragma unroll
+      for (int i = 0; i < Cf::kALd; ++i) aoff[i] = aoff_of(m0, i);
+#pragma unroll
+      for (int j = 0; j < Cf::kBLd; ++j) boff[j] = boff_of(n0, j);
+      issue(0, 0);
+      if (S > 1) issue(1, 1);
+    }
+
+    RowStats8 rst;
+    float kst = 0.f;
+    float bs1[8], bs2[8], bmu[8];
+    float pa[8], pb[8], pra[8], prb[8];
+    if constexpr (APPLY) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        pa[k] = ap.ab[cur_n0 + c * 8 + k];
+        pb[k] = ap.ab[N + cur_n0 + c * 8 + k];
+        pra[k] = ap.rab ? ap.rab[cur_n0 + c * 8 + k] : 1.f;
+        prb[k] = ap.rab ? ap.rab[N + cur_n0 + c * 8 + k] : 0.f;
+      }
+    }
+    if constexpr (BSTATS) {
+      *reinterpret_cast<float4*>(bmu) = *reinterpret_cast<const float4*>(bs.mean + cur_n0 + c * 8);
+      *reinterpret_cast<float4*>(bmu + 4) = *reinterpret_cast<const float4*>(bs.mean + cur_n0 + c * 8 + 4);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { bs1[k] = 0.f; bs2[k] = 0.f; }
+    }
+#pragma unroll
+    for (int hv = 0; hv < kHalves; ++hv) {
+      // this half's waves stage their accumulators (bf16) as rows [hv BM/H, (hv+1) BM/H) of the tile
+      constexpr int kWH = Cf::WM / kHalves;  // wave rows per half
+      if (wm / kWH == hv) {
+#pragma unroll
+        for (int i = 0; i < Cf::kMB; ++i)
+#pragma unroll
+          for (int j = 0; j < Cf::kNB; ++j) {
+            const int ml = (wm % kWH) * WROWS + i * 16 + lrow;
+            const int cl = wn * WCOLS + j * 16 + 4 * lchk;
+            *reinterpret_cast<uint2*>(stg + ml * Cf::kEpiStride + cl * 2) = pk[i][j];
+          }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if constexpr (STATS) {
+        if (hv == 0) {
+          rs8_init(rst, *reinterpret_cast<const uint4*>(stg + (tid % kChunks) * 16));
+          if (tid < BN) kst = __uint_as_float((uint32_t)*reinterpret_cast<const uint16_t*>(stg + tid * 2) << 16);
+        }
+      }
+#pragma unroll
+      for (int h = hv * kItH; h < (hv + 1) * kItH; h += kB) {
+        uint4 cv[kB], xbv[kB];
+        unsigned cmk[kB], bmkv[kB];
+        bool okv[kB];
+#pragma unroll
+        for (int it = 0; it < kB; ++it) {
+          const int m = cur_m0 + r0 + kRowStep * (h + it);
+          const bool ok = m < M;
+          okv[it] = ok;
+          const int mc = ok ? m : M - 1;
+          const int64_t off = (int64_t)mc * N + cur_n0 + c * 8;
+          if constexpr (BSTATS) {
+            xbv[it] = *reinterpret_cast<const uint4*>(bs.x + off);
+            const unsigned b8 = bm_base[(off >> 3) * bm_scale];
+            bmkv[it] = ok ? b8 : 0u;
+          }
+          if constexpr (APPLY) cv[it] = *reinterpret_cast<const uint4*>(Cin + off);
+          if constexpr (ACC) {
+            const unsigned mk = cm_base[(off >> 3) * cm_scale];
+            if constexpr (STR) {
+              const int w = mc % cg.W, t = mc / cg.W, hh = t % cg.H, n = t / cg.H;
+              const bool on = hh % cg.s == 0 && w % cg.s == 0;
+              const int64_t co = on ? ((int64_t)(n * cg.Hs + hh / cg.s) * cg.Ws + w / cg.s) * N : 0;
+              cv[it] = *reinterpret_cast<const uint4*>(Cin + co + cur_n0 + c * 8);
+              cmk[it] = on ? mk : 0u;
+            } else {
+              cv[it] = *reinterpret_cast<const uint4*>(Cin + off);
+              cmk[it] = mk;
+            }
+          }
+        }
+#pragma unroll
+        for (int it = 0; it < kB; ++it) {
+          const int r = r0 + kRowStep * (h + it);
+          const bool ok = okv[it];
+          uint4 v = *reinterpret_cast<const uint4*>(stg + (r - hv * (BM / kHalves)) * Cf::kEpiStride + c * 16);
+          const int64_t off = (int64_t)(cur_m0 + r) * N + cur_n0 + c * 8;
+          if constexpr (ACC) {
+            float a8[8], cc[8];
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w}, cw[4] = {cv[it].x, cv[it].y, cv[it].z, cv[it].w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              a8[2 * k] = __uint_as_float(w[k] << 16); a8[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+              cc[2 * k] = __uint_as_float(cw[k] << 16); cc[2 * k + 1] = __uint_as_float(cw[k] & 0xffff0000u);
+            }
+            const unsigned mb = cmk[it];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) a8[k] += (mb >> k) & 1u ? cc[k] : 0.f;
+            v.x = (uint32_t)f2bf(a8[0]) | ((uint32_t)f2bf(a8[1]) << 16);
+            v.y = (uint32_t)f2bf(a8[2]) | ((uint32_t)f2bf(a8[3]) << 16);
+            v.z = (uint32_t)f2bf(a8[4]) | ((uint32_t)f2bf(a8[5]) << 16);
+            v.w = (uint32_t)f2bf(a8[6]) | ((uint32_t)f2bf(a8[7]) << 16);
+          }
+          unsigned amb = 0;
+          if constexpr (APPLY) {
+            float z[8], rr[8];
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w}, rw[4] = {cv[it].x, cv[it].y, cv[it].z, cv[it].w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              z[2 * k] = __uint_as_float(w[k] << 16); z[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+              rr[2 * k] = __uint_as_float(rw[k] << 16); rr[2 * k + 1] = __uint_as_float(rw[k] & 0xffff0000u);
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+              float t = z[k] * pa[k] + pb[k];
+              t += ap.rab ? rr[k] * pra[k] + prb[k] : rr[k];
+              amb |= (t > 0.f ? 1u : 0u) << k;
+              z[k] = t > 0.f ? t : 0.f;
+            }
+            v.x = (uint32_t)f2bf(z[0]) | ((uint32_t)f2bf(z[1]) << 16);
+            v.y = (uint32_t)f2bf(z[2]) | ((uint32_t)f2bf(z[3]) << 16);
+            v.z = (uint32_t)f2bf(z[4]) | ((uint32_t)f2bf(z[5]) << 16);
+            v.w = (uint32_t)f2bf(z[6]) | ((uint32_t)f2bf(z[7]) << 16);
+          }
+          if constexpr (BSTATS) bn_bwd_accum8(v, xbv[it], bmkv[it], bmu, bs1, bs2);
+          if constexpr (STATS) {
+            if (ok) rs8_add(rst, v);
+          }
+          // every thread stores every row (past M: the sink) so the vmcnt counts above are exact
+          uint4* yp = ok ? reinterpret_cast<uint4*>(Y + off) : g_gemm_sink + tid;
+          *yp = v;
+          if constexpr (APPLY) {
+            uint8_t* mp = ok ? ap.mask + (off >> 3) : g_mask_sink + tid;
+            *mp = (uint8_t)amb;
+          }
+        }
+      }
+      __builtin_amdgcn_s_barrier();  // every wave is done reading this half's staged rows
+      asm volatile("" ::: "memory");
+    }
+    if constexpr (BSTATS)
+      bn_bwd_tile_store<BN, Cf::kWaves>(bs1, bs2, reinterpret_cast<float*>(stg), bs.part, T, cur_mt, N, cur_n0);
+    if constexpr (STATS)
+      rs8_tile_store<BN, Cf::kWaves>(rst, kst, reinterpret_cast<float*>(stg), part, min(BM, M - cur_m0), T, cur_mt, N,
+                                     cur_n0);
+    if constexpr (BSTATS || STATS) {  // the reduction area is the next epilogue's staging area
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+    if (!has_next) break;
+    tile = next;
+    first = false;
+  }
+  wait_vmn<0>();
+}
+
+// 0: one tile per workgroup everywhere; 1 (default): persistent where it measured faster — the 16-wave
+// 256-channel tile of the plain / statistics forward and of the data gradient without an accumulate source
+// (ResNet-50, 1024 images, tools/conv1x1_persist_bench.py, profiles/r5/conv1x1_persist_bench_b1024.txt:
+// forward + statistics 64->256 @56 526 -> 430 us, data gradient + BN reduction 64->256 @56 774 -> 725,
+// @28 458 -> 401, @14 290 -> 267); the ATR, APPLY and accumulate epilogues hold more registers and spill
+// at 128 per lane, and the 8- / 4-wave persistent tiles were slower: there the one-tile kernel stays;
+// 2: every kind and tile persistent (A/B). -1: PDT_CONV1X1_PERSIST, read once.
+int g_persist = -1;
+
+inline int persist_mode() {
+  if (g_persist < 0) {
+    const char* e = getenv("PDT_CONV1X1_PERSIST");
+    g_persist = (e && e[0]) ? (int)strtol(e, nullptr, 10) : 1;
+    if (g_persist < 0 || g_persist > 2) g_persist = 1;
+  }
+  return g_persist;
+}
+
+template <class Cf, bool ACC, bool STATS, bool BSTATS, bool ATR, bool APPLY, bool STR>
+int launch_p(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t* c, const uint8_t* cm, float* part, int M,
+             int K, int N, const BnSrc& bs, const CGeom& cg, hipStream_t s, const float* acoef, const ApArgs& ap) {
+  using L = PL<Cf>;
+  static bool attr = false;
+  constexpr int kMaxLds = L::kLds + (ATR ? 2 * 512 * 4 : 0);
+  if (!attr) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&conv1x1p_kernel<Cf, ACC, STATS, BSTATS, ATR, APPLY, STR>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, kMaxLds) != hipSuccess)
+      return -3;
+    attr = true;
+  }
+  const int lds = L::kLds + (ATR ? 2 * K * 4 : 0);
+  const int64_t total = (int64_t)(M + Cf::BM - 1) / Cf::BM * (N / Cf::BN);
+  const int occ = (160 * 1024) / lds > 0 ? (160 * 1024) / lds : 1;
+  int64_t grid = 256 * (int64_t)occ;
+  if (grid > total) grid = total;
+  hipLaunchKernelGGL((conv1x1p_kernel<Cf, ACC, STATS, BSTATS, ATR, APPLY, STR>), dim3((unsigned)grid),
+                     dim3(Cf::kThreads), lds, s, a, b, y, c, cm, part, M, K, N, bs, cg, acoef, ap);
+  return 0;
+}
+
 constexpr int kMaxATRK = 512;  // ATR coefficient table: [2][K] floats past kLds
 
-template <class Cf, bool ACC, bool STATS, bool NT, bool BSTATS, bool ATR = false, bool APPLY = false>
+template <class Cf, bool ACC, bool STATS, bool NT, bool BSTATS, bool ATR = false, bool APPLY = false, bool STR = false>
 int launch_nt(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t* c, const uint8_t* cm, float* part,
               int M, int K, int N, const BnSrc& bs, const CGeom& cg, hipStream_t s, const float* acoef = nullptr,
               const ApArgs& ap = ApArgs{}) {
   static bool attr = false;
   constexpr int kMaxLds = Cf::kLds + (ATR ? 2 * kMaxATRK * 4 : 0);
   if (!attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&conv1x1_kernel<Cf, ACC, STATS, NT, BSTATS, ATR, APPLY>),
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&conv1x1_kernel<Cf, ACC, STATS, NT, BSTATS, ATR, APPLY, STR>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, kMaxLds) != hipSuccess)
       return -3;
     attr = true;
@@ -410,7 +810,14 @@ int launch_nt(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t*
   const int64_t grid = (int64_t)(M + Cf::BM - 1) / Cf::BM * (N / Cf::BN);
   ApArgs apx = ap;
   apx.probe = g_probe;
-  hipLaunchKernelGGL((conv1x1_kernel<Cf, ACC, STATS, NT, BSTATS, ATR, APPLY>), dim3((unsigned)grid),
+  // persistent: from two tiles per workgroup up (probes run on the one-tile kernel)
+  if constexpr (!NT) {
+    constexpr bool kMeasured = Cf::kWaves >= 16 && !ACC && !ATR && !APPLY;  // see g_persist
+    const int pm = persist_mode();
+    if ((pm == 2 || (pm == 1 && kMeasured)) && g_probe == 0 && grid >= 2 * 256 * (int64_t)((160 * 1024) / PL<Cf>::kLds))
+      return launch_p<Cf, ACC, STATS, BSTATS, ATR, APPLY, STR>(a, b, y, c, cm, part, M, K, N, bs, cg, s, acoef, apx);
+  }
+  hipLaunchKernelGGL((conv1x1_kernel<Cf, ACC, STATS, NT, BSTATS, ATR, APPLY, STR>), dim3((unsigned)grid),
                      dim3(Cf::kThreads), lds, s, a, b, y, c, cm, part, M, K, N, bs, cg, acoef, apx);
   return 0;
 }
@@ -418,6 +825,8 @@ int launch_nt(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t*
 template <class Cf, bool ACC, bool STATS, bool BSTATS = false>
 int launch(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t* c, const uint8_t* cm, float* part, int M,
            int K, int N, const BnSrc& bs, const CGeom& cg, hipStream_t s) {
+  if constexpr (ACC)
+    if (cg.s) return launch_nt<Cf, ACC, STATS, false, BSTATS, false, false, true>(a, b, y, c, cm, part, M, K, N, bs, cg, s);
   // (non-temporal output stores, NT = true, measured no gain: default-policy stores keep the
   // output in L2 for the consuming BatchNorm)
   return launch_nt<Cf, ACC, STATS, false, BSTATS>(a, b, y, c, cm, part, M, K, N, bs, cg, s);
@@ -454,6 +863,14 @@ int pdt_conv1x1_tile_rows() { return 256; }
 
 // Diagnosis (tools/conv1x1_bw.py --probe): see ApArgs::probe. Results are wrong while set.
 void pdt_conv1x1_probe(int probe) { g_probe = probe; }
+
+// A/B hook (see g_persist): 0 = one tile per workgroup, 1 = persistent where measured faster (default),
+// 2 = every kind and tile persistent. Returns the previous mode.
+int pdt_conv1x1_persist(int mode) {
+  const int old = persist_mode();
+  g_persist = mode < 0 ? -1 : (mode > 2 ? 2 : mode);
+  return old;
+}
 
 // y[M,N] = a[M,K] * b[N,K]^T (+ c[M,N], masked by the bit-mask cm when given: bit j of byte
 // (m*N + n) / 8 — the BatchNorm ReLU mask layout); part: stats of y per 256-row tile (see above),

@@ -117,7 +117,8 @@ def init_distributed(
     device = torch.device("cpu")
     if use_gpu:
         n = torch.cuda.device_count()
-        if backend in ("nccl", "pdt_p2p") and (e_lws > n or local_rank >= n):
+        rccl = backend == "nccl" or (backend == "pdt_p2p" and (os.environ.get("PDT_P2P_INNER") or "nccl") == "nccl")
+        if rccl and (e_lws > n or local_rank >= n):
             # RCCL needs one GPU per rank; wrapping local_rank % n would put two ranks on one GPU and
             # report an N-GPU measurement taken on fewer GPUs
             raise RuntimeError(f"{backend}: local rank {local_rank} of {e_lws} but only {n} visible "
