@@ -38,7 +38,9 @@ PDT_FUSED_ADDLN             1            residual add fused into LayerNorm
 PDT_EMBEDDING_NATIVE        1            GPT-2 token/position embedding on our kernels
 PDT_BWD_FUSED               1            bottleneck conv3 + bn3 backward as one kernel (conv1x1_bwd_fused.hip):
                                          bn3's backward apply formed on load, conv3 dgrad + wgrad + bn2 reduction
-PDT_BWD_FUSED_SHAPES        256x64,512x128  (Co x Ci) of the conv3s that take the fused backward
+PDT_BWD_FUSED_SHAPES        256x64       (Co x Ci) of the conv3s that take the fused backward ("256x64,512x128" adds
+                                         layer 2: 0.9 % slower in-step since the branch-free conv1x1 epilogue,
+                                         profiles/r5/ab_layer2_unfused.txt)
 PDT_BN2_DEFER               0            1: with PDT_BWD_FUSED, bn2's apply + ReLU deferred into conv3 (read on load
                                          in the forward GEMM, recomputed in the fused backward, which writes bn2's
                                          mask). Measured -0.2 %, and -2 % with PDT_BN_APPLY_GEMM_K (the relu(a x + b)
@@ -101,7 +103,7 @@ class _Switches:
         self.linear_epilogue = e("PDT_LINEAR_EPILOGUE", "0") == "1"
         self.bwd_fused = on("PDT_BWD_FUSED")
         self.bwd_fused_shapes = tuple(tuple(int(v) for v in t.split("x")) for t in
-                                      e("PDT_BWD_FUSED_SHAPES", "256x64,512x128").split(",") if "x" in t)
+                                      e("PDT_BWD_FUSED_SHAPES", "256x64").split(",") if "x" in t)
         self.bn2_defer = on("PDT_BN2_DEFER", "0")
         self.bn_apply_gemm_k = int(e("PDT_BN_APPLY_GEMM_K", "64"))
         self.strided_bstats = on("PDT_STRIDED_BSTATS")

@@ -54,7 +54,6 @@ int pdt_conv1x1_bwd_fused(const uint16_t* dy, const uint16_t* z, const uint8_t* 
                           const uint8_t* bm, const float* bmean, float* bpart, const float* xcoef, uint8_t* mask_out,
                           uint16_t* dxa, uint16_t* dw, float* ws, int M, int C4, int CW, hipStream_t s);
 void pdt_conv1x1_bwd_fused_tune(int grid);
-int pdt_conv1x1_bwd_fused_slack(int slack);
 void pdt_bn_tune(int variant, int target_blocks, int u_fwd, int u_bwd);
 int pdt_bn_fwd_train(const uint16_t* x, const uint16_t* res, const float* res_a, const float* res_b,
                      const float* gamma, const float* beta,
@@ -180,7 +179,10 @@ int pdt_embedding_fwd(const int64_t* idx, const uint16_t* wte, const uint16_t* w
                       int D, int V, int* err, hipStream_t s);
 int64_t pdt_embedding_bwd_ws_ints(int64_t n, int V);
 int pdt_gemm_nt(const uint16_t* A, const uint16_t* B, uint16_t* C, uint16_t* G, const void* bias, int bias_f32,
-                int epi, int tanh_form, int M, int N, int K, hipStream_t s);
+                int epi, int tanh_form, int M, int N, int K, int nsplit, float* ws, int* cnt, hipStream_t s);
+int pdt_gemm_nt_splits(int M, int N, int K);
+int64_t pdt_gemm_nt_ws_floats(int M, int N, int nsplit);
+int64_t pdt_gemm_nt_tiles(int M, int N);
 int pdt_embedding_bwd(const int64_t* idx, const uint16_t* dout, uint16_t* dwte, uint16_t* dwpe, int* ws, int64_t n,
                       int B, int T, int V, int D, int* err, hipStream_t s);
 int64_t pdt_p2p_flags_bytes();
@@ -1803,7 +1805,8 @@ std::vector<Tensor> embedding_bwd(Tensor idx, Tensor dout, int64_t V, int64_t P)
 // ---- Linear GEMM with fused epilogues (csrc/kernels/gemm.hip) ----
 // a [M, K], b [N, K] contiguous bf16 -> {C [M, N]} (epi 0: a·bᵀ, 1: a·bᵀ + bias) or {C, G} (epi 2:
 // C = a·bᵀ, G = gelu(C + bias)). bias [N] fp32 or bf16. N % 256 == 0, K % 64 == 0 (gemm_nt_ok).
-std::vector<Tensor> gemm_nt(Tensor a, Tensor b, c10::optional<Tensor> bias, int64_t epi, bool tanh_form) {
+std::vector<Tensor> gemm_nt(Tensor a, Tensor b, c10::optional<Tensor> bias, int64_t epi, bool tanh_form,
+                            int64_t nsplit) {
   check_cuda(a, "a");
   check_cuda(b, "b");
   TORCH_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 && a.dim() == 2 && b.dim() == 2 &&
@@ -1821,10 +1824,18 @@ std::vector<Tensor> gemm_nt(Tensor a, Tensor b, c10::optional<Tensor> bias, int6
   }
   auto c = at::empty({M, N}, a.options());
   Tensor g = epi == 2 ? at::empty({M, N}, a.options()) : Tensor();
+  // nsplit: split-K slices (0 = the launcher's estimate, pdt_gemm_nt_splits)
+  const int sp = nsplit > 0 ? (int)nsplit : pdt_gemm_nt_splits((int)M, (int)N, (int)K);
+  Tensor ws, cnt;
+  if (sp > 1) {
+    ws = at::empty({pdt_gemm_nt_ws_floats((int)M, (int)N, sp)}, a.options().dtype(at::kFloat));
+    cnt = at::empty({pdt_gemm_nt_tiles((int)M, (int)N)}, a.options().dtype(at::kInt));
+  }
   const int rc = pdt_gemm_nt(reinterpret_cast<const uint16_t*>(a.data_ptr()), reinterpret_cast<const uint16_t*>(b.data_ptr()),
                              reinterpret_cast<uint16_t*>(c.data_ptr()),
                              epi == 2 ? reinterpret_cast<uint16_t*>(g.data_ptr()) : nullptr, bp, bf32, (int)epi,
-                             tanh_form ? 1 : 0, (int)M, (int)N, (int)K, stream());
+                             tanh_form ? 1 : 0, (int)M, (int)N, (int)K, sp,
+                             sp > 1 ? ws.data_ptr<float>() : nullptr, sp > 1 ? cnt.data_ptr<int>() : nullptr, stream());
   TORCH_CHECK(rc == 0, "pdt_gemm_nt failed (", rc, ") for M=", M, " N=", N, " K=", K);
   if (epi == 2) return {c, g};
   return {c};
@@ -1980,7 +1991,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv1x1_wgrad_tune", [](int target_wgs, int variant, int interleave) { pdt_conv1x1_wgrad_tune(target_wgs, variant, interleave); },
         py::arg("target_wgs"), py::arg("variant") = -2, py::arg("interleave") = -2);
   m.def("embedding_fwd", &embedding_fwd);
-  m.def("gemm_nt", &gemm_nt);
+  m.def("gemm_nt", &gemm_nt, py::arg("a"), py::arg("b"), py::arg("bias"), py::arg("epi"), py::arg("tanh_form"),
+        py::arg("nsplit") = 0);
+  m.def("gemm_nt_splits", [](int64_t M, int64_t N, int64_t K) { return pdt_gemm_nt_splits((int)M, (int)N, (int)K); });
   m.def("embedding_bwd", &embedding_bwd);
   m.def("embedding_err", &embedding_err);
   m.def("conv3x3_wgrad_tune", [](int target_wgs, int co_tile) { pdt_conv3x3_wgrad_tune(target_wgs, co_tile); });
@@ -1990,8 +2003,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("coef"), py::arg("w"), py::arg("xa"), py::arg("bn_x") = py::none(), py::arg("bn_mask") = py::none(),
         py::arg("bn_mean") = py::none(), py::arg("xcoef") = py::none(), py::arg("wt") = py::none());
   m.def("conv1x1_bwd_fused_tune", [](int grid) { pdt_conv1x1_bwd_fused_tune(grid); });
-  m.def("conv1x1_bwd_fused_slack", [](int slack) { return pdt_conv1x1_bwd_fused_slack(slack); },
-        "role lockstep slack of the fused conv3 + bn3 backward in stages (0 off, -1 query); returns the previous");
   m.def("ce_fwd", &ce_fwd);
   m.def("ce_bwd", &ce_bwd);
   m.def("ln_fwd", &ln_fwd, py::arg("x"), py::arg("w"), py::arg("b"), py::arg("eps"), py::arg("res") = py::none());

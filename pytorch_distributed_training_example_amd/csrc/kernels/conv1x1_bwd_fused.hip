@@ -55,16 +55,6 @@ typedef short s4v __attribute__((ext_vector_type(4)));
 
 __device__ __attribute__((aligned(256))) uint4 g_fb_zero[64];  // zero page for pixels past M (never written)
 __device__ uint4 g_fb_sink[1024];  // epilogue stores of rows past M land here (keeps the vmcnt count exact)
-// Role lockstep (NR > 1): the NR workgroups of a pixel group read the SAME dy / z rows (the whole C4 row
-// per pixel) for their own 64-channel slices. Free-running, they drift apart and each read comes from
-// HBM (layer 2: 914 us per call against a ~0.43 ms floor for ONE read). Each workgroup publishes the
-// stage it has started; before a workgroup issues the DMA of stage s + 2 it waits (s_sleep, bounded)
-// until its partners have started stage s + 2 - slack, so the rows one of them pulls into the XCD's L2
-// are still there for the others. A speed hint only: no data passes between the workgroups (every byte
-// read was written by earlier launches), so it needs no fences; the wait is bounded (a partner that is
-// not resident, e.g. CUs held by an RCCL kernel on another stream, only turns the throttle off) and a
-// timed-out workgroup stops throttling for the rest of the launch.
-__device__ int g_fb_prog[4096];
 
 // C4: the BatchNorm's channels (conv output), CW: the conv's input channels (NR = CW / 64 roles).
 template <int C4_, int CW_, bool BSTATS_, bool RECOMP_ = false>
@@ -176,9 +166,7 @@ struct FBArgs {
   uint8_t* mask_out;    // RECOMP: bn2's ReLU bits [M*CW/8], written here
   uint16_t* dxa;        // [M][CW]
   float* ws;            // [G][C4][CW] wgrad partials
-  int* prog;            // [grid] stages started per workgroup (zeroed before the launch), or null
   int M, ntiles, G;     // G: pixel groups (workgroups per role)
-  int slack;            // roles of a pixel group stay within this many stages of each other (0: off)
 };
 
 template <class Cf>
@@ -338,7 +326,6 @@ __global__ __launch_bounds__(Cf::kThreads, 1) void conv1x1_bwd_fused_kernel(FBAr
       for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
 
   char* const dzs = lds + Cf::oDZ;
-  bool throttle = NR > 1 && a.prog != nullptr && a.slack > 0;  // (wave-uniform)
 #pragma unroll
   for (int s = 0; s < Cf::kSlots - 1; ++s)
     if (s < S) issue(s);
@@ -349,28 +336,6 @@ __global__ __launch_bounds__(Cf::kThreads, 1) void conv1x1_bwd_fused_kernel(FBAr
     else if (s == 0) wait_vm<Cf::kG>();
     else wait_vm<Cf::kStageOps>();
     lds_barrier();  // B1: DMA(s) visible to all waves; every wave is past stage s-1
-    if constexpr (NR > 1) {
-      if (throttle) {
-        if (wid == 0 && lane == 0)  // vector store (agent scope: bypasses this CU's L1)
-          __hip_atomic_store(a.prog + b, s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int want = s + Cf::kSlots - a.slack;  // partners must have started this stage
-        if (want > 0 && s + Cf::kSlots - 1 < S) {
-#pragma unroll 1
-          for (int r = 0; r < NR && throttle; ++r) {
-            if (r == role) continue;
-            const int* pp = a.prog + (b % 8) + 8 * (r + NR * (b / (8 * NR)));
-            int v = 0, spins = 0;
-#pragma unroll 1
-            for (;;) {  // scalar poll (lgkmcnt, not vmcnt: the DMA ring keeps flowing)
-              asm volatile("s_load_dword %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(pp) : "memory");
-              if (v >= want) break;
-              if (++spins > 4096) { throttle = false; break; }
-              __builtin_amdgcn_s_sleep(2);
-            }
-          }
-        }
-      }
-    }
     if (s + Cf::kSlots - 1 < S) issue(s + Cf::kSlots - 1);  // its slot was last used in stage s-1
     const char* slot = lds + (s % Cf::kSlots) * Cf::kSlot;
     const int p0 = (g + s * G) * KP;
@@ -598,7 +563,6 @@ __global__ __launch_bounds__(256) void fb_reduce_kernel(const float* __restrict_
 }
 
 int g_grid = 0;  // 0: one workgroup per CU
-int g_slack = 2;  // role lockstep slack in stages (0 = off; pdt_conv1x1_bwd_fused_slack)
 
 // pixel groups: one workgroup per CU in all (NR roles each), a multiple of 8 (XCD pairing)
 inline int groups_of(int ntiles, int nr) {
@@ -620,16 +584,7 @@ int launch(const FBArgs& a0, uint16_t* dw, hipStream_t s) {
   // every role of every pixel group with the pairing of the block map (the grid is rounded up to a
   // multiple of 8 * NR; groups past G exit at once)
   const int nblk = ((a0.G + 7) / 8) * 8 * Cf::NR;
-  FBArgs a = a0;
-  a.prog = nullptr;
-  if (Cf::NR > 1 && g_slack > 0 && nblk <= 4096) {
-    static int* prog = nullptr;
-    if (!prog && hipGetSymbolAddress(reinterpret_cast<void**>(&prog), HIP_SYMBOL(g_fb_prog)) != hipSuccess) return -4;
-    if (hipMemsetAsync(prog, 0, sizeof(int) * nblk, s) != hipSuccess) return -4;
-    a.prog = prog;
-    a.slack = g_slack;
-  }
-  hipLaunchKernelGGL(conv1x1_bwd_fused_kernel<Cf>, dim3(nblk), dim3(Cf::kThreads), Cf::kLds, s, a);
+  hipLaunchKernelGGL(conv1x1_bwd_fused_kernel<Cf>, dim3(nblk), dim3(Cf::kThreads), Cf::kLds, s, a0);
   const int64_t n4 = (int64_t)Cf::C4 * Cf::CW / 4;
   hipLaunchKernelGGL(fb_reduce_kernel, dim3((unsigned)((n4 + kRedCols - 1) / kRedCols)), dim3(kRedCols * kRedGroups),
                      0, s, a0.ws, dw, a0.G, n4);
@@ -667,8 +622,8 @@ int pdt_conv1x1_bwd_fused(const uint16_t* dy, const uint16_t* z, const uint8_t* 
   const bool rc = xcoef != nullptr;
   if (rc != (mask_out != nullptr) || (rc && !bx) || (!rc && !xa)) return -1;
   const int kp = kp_of(C4), ntiles = (M + kp - 1) / kp;
-  FBArgs a{dy, z, mz, mean, A, B, D, wt, xa, BnSrc{bx, bm, bmean, bpart}, xcoef, mask_out, dxa, ws, nullptr, M,
-           ntiles, pdt_conv1x1_bwd_fused_grid(M, C4, CW), 0};
+  FBArgs a{dy, z, mz, mean, A, B, D, wt, xa, BnSrc{bx, bm, bmean, bpart}, xcoef, mask_out, dxa, ws, M, ntiles,
+           pdt_conv1x1_bwd_fused_grid(M, C4, CW)};
   if (C4 == 256) {
     if (rc) return launch<FB<256, 64, true, true>>(a, dw, s);
     if (bx) return launch<FB<256, 64, true>>(a, dw, s);
@@ -682,13 +637,6 @@ int pdt_conv1x1_bwd_fused(const uint16_t* dy, const uint16_t* z, const uint8_t* 
 // Tuning hook: workgroups per call (0 = one per CU).
 void pdt_conv1x1_bwd_fused_tune(int grid) {
   if (grid >= 0) g_grid = grid;
-}
-
-// Role lockstep slack in stages (0 = off); returns the previous value.
-int pdt_conv1x1_bwd_fused_slack(int slack) {
-  const int old = g_slack;
-  if (slack >= 0) g_slack = slack;
-  return old;
 }
 
 }  // extern "C"

@@ -34,6 +34,10 @@ def apply_env(base: dict, env: dict) -> None:
     resnet.DS_DEFER_APPLY[0] = os.environ.get("PDT_DS_DEFER", "1") != "0"
     resnet.PREP_WEIGHTS[0] = os.environ.get("PDT_PREP_WEIGHTS", "1") != "0"
     resnet.DS_FUSED_BWD[0] = os.environ.get("PDT_DS_FUSED_BWD", "1") != "0"
+    from pytorch_distributed_training_example_amd.ops._native import native
+    n = native()
+    if hasattr(n, "conv1x1_persist"):
+        n.conv1x1_persist(-1)  # re-read PDT_CONV1X1_PERSIST (the C side caches it)
 
 
 def main():

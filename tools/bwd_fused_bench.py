@@ -22,7 +22,6 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--grid", type=int, default=0)
-    ap.add_argument("--slacks", default="", help="A/B of the role lockstep slack, e.g. 0,1,2,4 (layer 2)")
     a = ap.parse_args()
     n = native()
     if a.grid:
@@ -66,16 +65,10 @@ def main():
         e1.synchronize()
         return e0.elapsed_time(e1) * 1e3 / a.reps
 
-    slacks = [int(v) for v in a.slacks.split(",")] if a.slacks else []
     res = {"fused": [], "unfused": []}
-    res.update({f"fused_slack{v}": [] for v in slacks})
     for _ in range(a.rounds):
         res["fused"].append(time(fused))
         res["unfused"].append(time(unfused))
-        for v in slacks:
-            old = n.conv1x1_bwd_fused_slack(v)
-            res[f"fused_slack{v}"].append(time(fused))
-            n.conv1x1_bwd_fused_slack(old)
     T = M * CW * 2
     floor_fused = (2 * 4 * T + 2 * 4 * T / 16 + 3 * T + T / 8) / 5.5e12 * 1e6
     for k, v in res.items():

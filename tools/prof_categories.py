@@ -7,8 +7,11 @@ import sys
 def family(n):
     if "conv1x1_bwd_fused" in n or "fb_reduce" in n:
         return "fused conv3 + BN3 backward (dgrad + wgrad + BN apply/reduction)"
-    m = re.search(r"conv1x1_kernel<(.*?)>\s*\(", n)
-    if m and m.group(1).rstrip().endswith("true"):
+    m = re.search(r"conv1x1_kernel<.*?G1<[^>]*>,(.*?)>\s*\(", n)  # <Cf, ACC, STATS, NT, BSTATS, ATR, APPLY[, STR]>
+    if m and [f.strip() for f in m.group(1).split(",")][5:6] == ["true"]:
+        return "1x1 GEMM + BN(+res)+ReLU apply epilogue (recomputed conv3)"
+    m = re.search(r"conv1x1p_kernel<.*?G1<[^>]*>,(.*?)>\s*\(", n)  # persistent: <Cf, ACC, STATS, BSTATS, ATR, APPLY, STR>
+    if m and [f.strip() for f in m.group(1).split(",")][4:5] == ["true"]:
         return "1x1 GEMM + BN(+res)+ReLU apply epilogue (recomputed conv3)"
     if "conv1x1_wgrad" in n:
         return "our 1x1 weight gradient (MFMA)"
@@ -18,7 +21,7 @@ def family(n):
         return "our BN (+ReLU/residual/pool)"
     if "conv3x3" in n:
         return "our 3x3 conv (MFMA)"
-    if "conv1x1_kernel" in n:
+    if "conv1x1_kernel" in n or "conv1x1p_kernel" in n:
         return "our 1x1 conv GEMM (MFMA, fused BN-stats epilogues)"
     if "stem_" in n:
         return "our 7x7 stem conv (MFMA)"
