@@ -179,10 +179,7 @@ int pdt_embedding_fwd(const int64_t* idx, const uint16_t* wte, const uint16_t* w
                       int D, int V, int* err, hipStream_t s);
 int64_t pdt_embedding_bwd_ws_ints(int64_t n, int V);
 int pdt_gemm_nt(const uint16_t* A, const uint16_t* B, uint16_t* C, uint16_t* G, const void* bias, int bias_f32,
-                int epi, int tanh_form, int M, int N, int K, int nsplit, float* ws, int* cnt, hipStream_t s);
-int pdt_gemm_nt_splits(int M, int N, int K);
-int64_t pdt_gemm_nt_ws_floats(int M, int N, int nsplit);
-int64_t pdt_gemm_nt_tiles(int M, int N);
+                int epi, int tanh_form, int M, int N, int K, hipStream_t s);
 int pdt_embedding_bwd(const int64_t* idx, const uint16_t* dout, uint16_t* dwte, uint16_t* dwpe, int* ws, int64_t n,
                       int B, int T, int V, int D, int* err, hipStream_t s);
 int64_t pdt_p2p_flags_bytes();
@@ -1805,8 +1802,7 @@ std::vector<Tensor> embedding_bwd(Tensor idx, Tensor dout, int64_t V, int64_t P)
 // ---- Linear GEMM with fused epilogues (csrc/kernels/gemm.hip) ----
 // a [M, K], b [N, K] contiguous bf16 -> {C [M, N]} (epi 0: a·bᵀ, 1: a·bᵀ + bias) or {C, G} (epi 2:
 // C = a·bᵀ, G = gelu(C + bias)). bias [N] fp32 or bf16. N % 256 == 0, K % 64 == 0 (gemm_nt_ok).
-std::vector<Tensor> gemm_nt(Tensor a, Tensor b, c10::optional<Tensor> bias, int64_t epi, bool tanh_form,
-                            int64_t nsplit) {
+std::vector<Tensor> gemm_nt(Tensor a, Tensor b, c10::optional<Tensor> bias, int64_t epi, bool tanh_form) {
   check_cuda(a, "a");
   check_cuda(b, "b");
   TORCH_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 && a.dim() == 2 && b.dim() == 2 &&
@@ -1824,18 +1820,10 @@ std::vector<Tensor> gemm_nt(Tensor a, Tensor b, c10::optional<Tensor> bias, int6
   }
   auto c = at::empty({M, N}, a.options());
   Tensor g = epi == 2 ? at::empty({M, N}, a.options()) : Tensor();
-  // nsplit: split-K slices (0 = the launcher's estimate, pdt_gemm_nt_splits)
-  const int sp = nsplit > 0 ? (int)nsplit : pdt_gemm_nt_splits((int)M, (int)N, (int)K);
-  Tensor ws, cnt;
-  if (sp > 1) {
-    ws = at::empty({pdt_gemm_nt_ws_floats((int)M, (int)N, sp)}, a.options().dtype(at::kFloat));
-    cnt = at::empty({pdt_gemm_nt_tiles((int)M, (int)N)}, a.options().dtype(at::kInt));
-  }
   const int rc = pdt_gemm_nt(reinterpret_cast<const uint16_t*>(a.data_ptr()), reinterpret_cast<const uint16_t*>(b.data_ptr()),
                              reinterpret_cast<uint16_t*>(c.data_ptr()),
                              epi == 2 ? reinterpret_cast<uint16_t*>(g.data_ptr()) : nullptr, bp, bf32, (int)epi,
-                             tanh_form ? 1 : 0, (int)M, (int)N, (int)K, sp,
-                             sp > 1 ? ws.data_ptr<float>() : nullptr, sp > 1 ? cnt.data_ptr<int>() : nullptr, stream());
+                             tanh_form ? 1 : 0, (int)M, (int)N, (int)K, stream());
   TORCH_CHECK(rc == 0, "pdt_gemm_nt failed (", rc, ") for M=", M, " N=", N, " K=", K);
   if (epi == 2) return {c, g};
   return {c};
@@ -1991,9 +1979,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv1x1_wgrad_tune", [](int target_wgs, int variant, int interleave) { pdt_conv1x1_wgrad_tune(target_wgs, variant, interleave); },
         py::arg("target_wgs"), py::arg("variant") = -2, py::arg("interleave") = -2);
   m.def("embedding_fwd", &embedding_fwd);
-  m.def("gemm_nt", &gemm_nt, py::arg("a"), py::arg("b"), py::arg("bias"), py::arg("epi"), py::arg("tanh_form"),
-        py::arg("nsplit") = 0);
-  m.def("gemm_nt_splits", [](int64_t M, int64_t N, int64_t K) { return pdt_gemm_nt_splits((int)M, (int)N, (int)K); });
+  m.def("gemm_nt", &gemm_nt);
   m.def("embedding_bwd", &embedding_bwd);
   m.def("embedding_err", &embedding_err);
   m.def("conv3x3_wgrad_tune", [](int target_wgs, int co_tile) { pdt_conv3x3_wgrad_tune(target_wgs, co_tile); });

@@ -499,15 +499,23 @@ __global__ __launch_bounds__(1024) void bn_tiles_fin_kernel(const float* __restr
       g_tiles_ctr[blockIdx.x] = 0u;
     }
     __syncthreads();
-    if (j != 0) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    // the P level-1 entries of the column, combined by all 16 row groups (group j takes p = j, j + 16, ...
+    // in order, then group sums in order: a fixed order, deterministic). One thread per channel walking all
+    // P entries serially made this tail ~10 us of dependent loads at layer 1 (P = 98).
     s = 0.0;
     q = 0.0;
-#pragma unroll 8
-    for (int p = 0; p < P; ++p) {
+    for (int p = j; p < P; p += 16) {
       s += __builtin_nontemporal_load(&lv[((int64_t)p * C + c) * 2]);
       q += __builtin_nontemporal_load(&lv[((int64_t)p * C + c) * 2 + 1]);
     }
+    sm[0][j][cl] = s;
+    sm[1][j][cl] = q;
+    __syncthreads();
+    if (j != 0) return;
+    s = 0.0;
+    q = 0.0;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) { s += sm[0][u][cl]; q += sm[1][u][cl]; }
   } else if (j != 0) {
     return;
   }
@@ -520,12 +528,24 @@ __global__ __launch_bounds__(1024) void bn_tiles_fin_kernel(const float* __restr
   }
 }
 
+// The P level-1 entries of channel c in the one-launch finalize's order (bn_tiles_fin_kernel): 16
+// strided groups (p = j, j + 16, ...), then the group sums in order — so both paths agree bit for bit.
+__device__ __forceinline__ void sum_level1(const double* __restrict__ in, int P, int C, int c, double& s, double& q) {
+  s = 0.0;
+  q = 0.0;
+  for (int j = 0; j < 16; ++j) {
+    double sj = 0.0, qj = 0.0;
+    for (int p = j; p < P; p += 16) { sj += in[((int64_t)p * C + c) * 2]; qj += in[((int64_t)p * C + c) * 2 + 1]; }
+    s += sj;
+    q += qj;
+  }
+}
+
 __global__ void bn_tiles_l2_kernel(const double* __restrict__ in, int P, int C, FinArgs fa) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
-  double s = 0.0, q = 0.0;
-#pragma unroll 8
-  for (int p = 0; p < P; ++p) { s += in[((int64_t)p * C + c) * 2]; q += in[((int64_t)p * C + c) * 2 + 1]; }
+  double s, q;
+  sum_level1(in, P, C, c, s, q);
   const double inv_m = 1.0 / (double)fa.M;
   const double mu = s * inv_m;
   bn_set_fwd(c, mu, q * inv_m - mu * mu, fa);
@@ -535,9 +555,8 @@ __global__ void bn_tiles_l2_kernel(const double* __restrict__ in, int P, int C, 
 __global__ void bn_tiles_l2b_kernel(const double* __restrict__ in, int P, int C, FinArgs fa) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
-  double s = 0.0, q = 0.0;
-#pragma unroll 8
-  for (int p = 0; p < P; ++p) { s += in[((int64_t)p * C + c) * 2]; q += in[((int64_t)p * C + c) * 2 + 1]; }
+  double s, q;
+  sum_level1(in, P, C, c, s, q);
   bn_finalize<1>(c, (float)s, (float)q, fa);
 }
 

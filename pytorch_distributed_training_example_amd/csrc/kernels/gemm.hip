@@ -94,35 +94,21 @@ __device__ __forceinline__ uint32_t pack2(float a, float b) {
   return (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)a) | ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)b) << 16);
 }
 
-// Split-K (nsplit > 1): the grid is tiles x nsplit workgroups; slice sl of a tile runs K-steps
-// [sl nk / nsplit, (sl + 1) nk / nsplit). Every slice writes its fp32 accumulators to a workspace slab in
-// register order (one 1-KB dwordx4 store per accumulator block and wave), then takes a ticket on the
-// tile's counter (zeroed by the launcher's memset node); the slice that draws nsplit - 1 reads the other
-// slabs and sums ALL slices in slice order (its own from registers: bit-identical for any arrival order)
-// and runs the epilogue. Publish / acquire as cdna_hip_programming.md §5 "Projection GEMM" item 2: every
-// wave's vmcnt(0) -> barrier -> lane 0 agent release fence -> vmcnt(0) -> relaxed agent fetch_add; the
-// reducer: agent acquire fence -> vmcnt(0) -> barrier -> plain loads. Valid for any placement of the
-// slices; they are consecutive block ids, i.e. one XCD under round-robin placement (speed only).
-// It turns the GPT-2 N = 1024 projections (128 tiles of 256 x 256 = half the CUs idle) into full waves.
 template <int EPI>
 __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __restrict__ A,
                                                                const uint16_t* __restrict__ B, uint16_t* __restrict__ C,
                                                                uint16_t* __restrict__ G, const void* __restrict__ bias,
-                                                               int bias_f32, int tanh_form, int M, int N, int K,
-                                                               int nsplit, float* __restrict__ ws, int* __restrict__ cnt) {
+                                                               int bias_f32, int tanh_form, int M, int N, int K) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 2, wc = wid & 3;
   const int ntn = N / kBN, ntm = (M + kBM - 1) / kBM;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  const int id = bid / nsplit, sl = bid % nsplit;
+  const int id = xcd_remap(blockIdx.x, gridDim.x);
   // groups of kGroup A bands: consecutive ids (one XCD) cover kGroup bands x a few N tiles, so the
   // tiles resident on an XCD at once share both operands in its L2
   const int gband = (id / (kGroup * ntn)) * kGroup, gsize = min(ntm - gband, kGroup), gi = id % (kGroup * ntn);
   const int m0 = (gband + gi % gsize) * kBM, n0 = (gi / gsize) * kBN;
-  const int nks = K / kBK / nsplit;  // K-steps of this slice (the launcher checks divisibility)
-  const int nk = nks;
-  const int kofs = sl * nks * kBK;   // first K column of this slice
+  const int nk = K / kBK;
 
   // DMA: waves 0-3 (wave row 0) stage the B rows of the image, waves 4-7 (row 1) the A rows — each
   // wave 64 rows as 8 instructions of 8 rows; lane -> (row + lane / 8, physical chunk lane % 8).
@@ -136,7 +122,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
     const int R = rbase + j * 8 + (lane >> 3);
     const int logical = (lane & 7) ^ ((R >> 1) & 7);
     const int grow = loads_b ? n0 + (R - kBM) : min(m0 + R, M - 1);
-    off[j] = grow * K + kofs + logical * 8;
+    off[j] = grow * K + logical * 8;
   }
   auto issue = [&](int t, int half) {  // half 0 / 1 of this wave's share of K-step t
     if (PDT_GEMM_PROBE == 2) return;
@@ -229,44 +215,6 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
   }
   if (wr == 0) bar();  // balance row 1's extra barrier
 
-  if (nsplit > 1) {
-    // ---- split-K: publish this slice's partial tile, the last arriver sums every slice in order
-    float* const slab = ws + ((int64_t)id * nsplit) * (kBM * kBN);
-    {
-      f4* mine = reinterpret_cast<f4*>(slab + (int64_t)sl * (kBM * kBN));
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) mine[(i * 4 + j) * kThreads + tid] = acc[i][j];
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    int* const flag = reinterpret_cast<int*>(lds);
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const int t = __hip_atomic_fetch_add(cnt + id, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      *flag = t == nsplit - 1;
-    }
-    __syncthreads();
-    if (!*flag) return;  // (uniform)
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-    const f4* all = reinterpret_cast<const f4*>(slab);
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int e = (i * 4 + j) * kThreads + tid;
-        f4 t = sl == 0 ? acc[i][j] : all[e];
-        for (int q = 1; q < nsplit; ++q) t += q == sl ? acc[i][j] : all[(int64_t)q * (kBM * kBN / 4) + e];
-        acc[i][j] = t;
-      }
-  }
-
   // ---- epilogue: lane holds C[m][n .. n+3] of every block (4 consecutive columns). The bf16 tile
   // is staged through LDS (free now: every read and DMA has retired) and written as whole 512-B
   // row segments — 8-B stores straight from the accumulators hit each 128-B line four times and
@@ -330,7 +278,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
 
 template <int EPI>
 int launch(const uint16_t* A, const uint16_t* B, uint16_t* C, uint16_t* G, const void* bias, int bias_f32,
-           int tanh_form, int M, int N, int K, int nsplit, float* ws, int* cnt, hipStream_t s) {
+           int tanh_form, int M, int N, int K, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_kernel<EPI>),
@@ -338,10 +286,9 @@ int launch(const uint16_t* A, const uint16_t* B, uint16_t* C, uint16_t* G, const
       return -3;
     attr = true;
   }
-  const int64_t tiles = (int64_t)((M + kBM - 1) / kBM) * (N / kBN);
-  if (nsplit > 1 && hipMemsetAsync(cnt, 0, sizeof(int) * tiles, s) != hipSuccess) return -4;
-  hipLaunchKernelGGL(gemm_nt_kernel<EPI>, dim3((unsigned)(tiles * nsplit)), dim3(kThreads), kLds, s, A, B, C, G, bias,
-                     bias_f32, tanh_form, M, N, K, nsplit, ws, cnt);
+  const int64_t grid = (int64_t)((M + kBM - 1) / kBM) * (N / kBN);
+  hipLaunchKernelGGL(gemm_nt_kernel<EPI>, dim3((unsigned)grid), dim3(kThreads), kLds, s, A, B, C, G, bias, bias_f32,
+                     tanh_form, M, N, K);
   return 0;
 }
 
@@ -349,43 +296,18 @@ int launch(const uint16_t* A, const uint16_t* B, uint16_t* C, uint16_t* G, const
 
 extern "C" {
 
-// Split-K slices for a shape (1 = none): the smallest estimated time ceil(tiles s / CUs) (nk / s + c), c = a
-// K-step-equivalent of per-workgroup prologue / epilogue / slab traffic, over s | nk with nk / s >= 4.
-int pdt_gemm_nt_splits(int M, int N, int K) {
-  if (M < 1 || N % kBN != 0 || K % kBK != 0) return 1;
-  const int64_t tiles = (int64_t)((M + kBM - 1) / kBM) * (N / kBN);
-  const int nk = K / kBK;
-  int best = 1;
-  double best_t = 1e30;
-  for (int sp = 1; sp <= 8; ++sp) {
-    if (nk % sp != 0 || (sp > 1 && nk / sp < 4)) continue;
-    const double waves = (double)((tiles * sp + 255) / 256);
-    const double t = waves * (nk / sp + (sp > 1 ? 5.0 : 3.0));
-    if (t < best_t - 1e-9) { best_t = t; best = sp; }
-  }
-  return best;
-}
-
-// Workspace floats / counter ints a split call needs.
-int64_t pdt_gemm_nt_ws_floats(int M, int N, int nsplit) {
-  return nsplit > 1 ? (int64_t)((M + kBM - 1) / kBM) * (N / kBN) * nsplit * kBM * kBN : 0;
-}
-int64_t pdt_gemm_nt_tiles(int M, int N) { return (int64_t)((M + kBM - 1) / kBM) * (N / kBN); }
-
 // C[M, N] (and G for epi 2) from A[M, K] and B[N, K], all row-major contiguous bf16.
 // epi: 0 none, 1 + bias, 2 C = A·Bᵀ and G = gelu(C + bias) (tanh_form: GPT-2's tanh GELU).
-// bias: [N] fp32 (bias_f32 = 1) or bf16, may be null. nsplit: split-K slices (1: none; > 1 needs ws with
-// pdt_gemm_nt_ws_floats floats and cnt with pdt_gemm_nt_tiles ints). Returns 0, or < 0 when not served.
+// bias: [N] fp32 (bias_f32 = 1) or bf16, may be null. Returns 0, or < 0 when the shape is not served.
 int pdt_gemm_nt(const uint16_t* A, const uint16_t* B, uint16_t* C, uint16_t* G, const void* bias, int bias_f32,
-                int epi, int tanh_form, int M, int N, int K, int nsplit, float* ws, int* cnt, hipStream_t s) {
+                int epi, int tanh_form, int M, int N, int K, hipStream_t s) {
   if (M < 1 || N % kBN != 0 || K % kBK != 0 || N < kBN || K < kBK) return -1;
   if ((int64_t)M * K >= (int64_t)1 << 31 || (int64_t)N * K >= (int64_t)1 << 31) return -2;
   if (epi == EPI_GELU && G == nullptr) return -1;
-  if (nsplit < 1 || (K / kBK) % nsplit != 0 || (nsplit > 1 && (!ws || !cnt))) return -1;
   switch (epi) {
-    case EPI_NONE: return launch<EPI_NONE>(A, B, C, G, bias, bias_f32, tanh_form, M, N, K, nsplit, ws, cnt, s);
-    case EPI_BIAS: return launch<EPI_BIAS>(A, B, C, G, bias, bias_f32, tanh_form, M, N, K, nsplit, ws, cnt, s);
-    case EPI_GELU: return launch<EPI_GELU>(A, B, C, G, bias, bias_f32, tanh_form, M, N, K, nsplit, ws, cnt, s);
+    case EPI_NONE: return launch<EPI_NONE>(A, B, C, G, bias, bias_f32, tanh_form, M, N, K, s);
+    case EPI_BIAS: return launch<EPI_BIAS>(A, B, C, G, bias, bias_f32, tanh_form, M, N, K, s);
+    case EPI_GELU: return launch<EPI_GELU>(A, B, C, G, bias, bias_f32, tanh_form, M, N, K, s);
     default: return -1;
   }
 }

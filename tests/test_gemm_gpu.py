@@ -65,37 +65,3 @@ def test_mlp_on_fused_epilogue_matches_default_path(switch, approximate):
     for a, b in zip(outs[0], outs[1]):
         assert _rel(b, a) < 1e-2, _rel(b, a)
 
-
-@pytest.mark.parametrize("M,K,N,sp", [(8192, 1024, 1024, 2), (8192, 4096, 1024, 2), (8192, 4096, 1024, 4),
-                                      (1000, 768, 768, 3), (25216, 3072, 768, 6)])
-@pytest.mark.parametrize("epi", [0, 1, 2])
-def test_gemm_nt_split_k(M, K, N, sp, epi):
-    """Split-K: slices publish fp32 slabs, the last arriver sums every slice in order and runs the
-    epilogue. Against fp32, and run-to-run bit-identical (the sum order does not depend on which
-    slice arrives last)."""
-    g = torch.Generator(device="cuda").manual_seed(M + K + N + sp)
-    a = (torch.rand(M, K, device="cuda", generator=g) * 2 - 1).bfloat16()
-    b = ((torch.rand(N, K, device="cuda", generator=g) * 2 - 1) / K ** 0.5).bfloat16()
-    bias = torch.rand(N, device="cuda", generator=g) - 0.5
-    bias = bias.bfloat16() if epi == 1 else bias
-    out = _C().gemm_nt(a, b, bias if epi else None, epi, True, sp)
-    out2 = _C().gemm_nt(a, b, bias if epi else None, epi, True, sp)
-    for x, y in zip(out, out2):
-        assert torch.equal(x, y)
-    ref = a.float() @ b.float().t()
-    if epi == 1:
-        ref = ref + bias.float()
-    assert _rel(out[0], ref) < 4e-3
-    if epi == 2:
-        gref = F.gelu(out[0].float() + bias, approximate="tanh")
-        assert _rel(out[1], gref) < 4e-3
-    one = _C().gemm_nt(a, b, bias if epi else None, epi, True, 1)
-    assert _rel(out[0], one[0]) < 2e-3  # differs from one K chain by rounding only
-
-
-def test_gemm_nt_auto_split_choices():
-    """The launcher's split estimate: the N = 1024 GPT-2 projections (128 tiles) split, fc1 (512 tiles) not."""
-    C = _C()
-    assert C.gemm_nt_splits(8192, 1024, 1024) > 1
-    assert C.gemm_nt_splits(8192, 1024, 4096) == 1
-    assert C.gemm_nt_splits(8192, 4096, 1024) > 1

@@ -35,7 +35,7 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&a, (int64_t)s.M * s.K * 2)); CK(hipMalloc(&b, (int64_t)s.N * s.K * 2)); CK(hipMalloc(&c, (int64_t)s.M * s.N * 2));
     hipLaunchKernelGGL(fill_kernel, dim3(1024), dim3(256), 0, 0, a, (int64_t)s.M * s.K, 1u, 1.f);
     hipLaunchKernelGGL(fill_kernel, dim3(1024), dim3(256), 0, 0, b, (int64_t)s.N * s.K, 7u, 1.f);
-    CK(pdt_gemm_nt(a, b, c, nullptr, nullptr, 0, 0, 0, s.M, s.N, s.K, 1, nullptr, nullptr, 0) == 0 ? hipSuccess : hipErrorInvalidValue);
+    CK(pdt_gemm_nt(a, b, c, nullptr, nullptr, 0, 0, 0, s.M, s.N, s.K, 0) == 0 ? hipSuccess : hipErrorInvalidValue);
     CK(hipDeviceSynchronize());
     double err = 0;
     if (PDT_GEMM_PROBE == 0) {  // 64 sampled outputs against an fp64 host dot product
@@ -54,7 +54,7 @@ int main(int argc, char** argv) {
     float best = 1e30f;
     for (int r = 0; r < 5; ++r) {
       CK(hipEventRecord(e0));
-      for (int i = 0; i < iters; ++i) pdt_gemm_nt(a, b, c, nullptr, nullptr, 0, 0, 0, s.M, s.N, s.K, 1, nullptr, nullptr, 0);
+      for (int i = 0; i < iters; ++i) pdt_gemm_nt(a, b, c, nullptr, nullptr, 0, 0, 0, s.M, s.N, s.K, 0);
       CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
       float ms; CK(hipEventElapsedTime(&ms, e0, e1)); best = fminf(best, ms / iters);
     }

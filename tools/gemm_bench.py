@@ -29,7 +29,6 @@ def main() -> None:
     ap.add_argument("--epi", default="bias", choices=["none", "bias", "gelu"])
     ap.add_argument("--rounds", type=int, default=10)
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--splits", default="0", help="our kernel's split-K slices to time, e.g. 0,1,2,4 (0 = auto)")
     args = ap.parse_args()
     from pytorch_distributed_training_example_amd.engine.gemm_tuning import use_repo_gemm_tuning
     use_repo_gemm_tuning()
@@ -45,19 +44,15 @@ def main() -> None:
         b = (torch.rand(N, device="cuda") * 0.2 - 0.1).bfloat16()
         bf = b.float()
         tanh = name.startswith("gpt2")
-        splits = [int(v) for v in args.splits.split(",")]
-        nk = K // 64
-        splits = [sp for sp in splits if sp == 0 or nk % sp == 0]
         if args.epi == "none":
-            mk = lambda sp: (lambda: C.gemm_nt(x, w, None, 0, False, sp))  # noqa: E731
+            ours = lambda: C.gemm_nt(x, w, None, 0, False)  # noqa: E731
             lib = lambda: F.linear(x, w)  # noqa: E731
         elif args.epi == "bias":
-            mk = lambda sp: (lambda: C.gemm_nt(x, w, b, 1, False, sp))  # noqa: E731
+            ours = lambda: C.gemm_nt(x, w, b, 1, False)  # noqa: E731
             lib = lambda: F.linear(x, w, b)  # noqa: E731
         else:
-            mk = lambda sp: (lambda: C.gemm_nt(x, w, bf, 2, tanh, sp))  # noqa: E731
+            ours = lambda: C.gemm_nt(x, w, bf, 2, tanh)  # noqa: E731
             lib = lambda: C.bias_gelu_fwd(F.linear(x, w), bf, tanh)  # noqa: E731
-        ours = mk(splits[0])
         # numerics against fp32
         ref = x.float() @ w.float().t()
         if args.epi == "bias":
@@ -68,10 +63,9 @@ def main() -> None:
             gref = F.gelu(got[0].float() + bf, approximate="tanh" if tanh else "none")
             gerr = ((got[1].float() - gref).norm() / gref.norm()).item()
             err = max(err, gerr)
-        arms = [("lib", lib)] + [(f"ours_s{sp}", mk(sp)) for sp in splits]
-        times = {a: [] for a, _ in arms}
+        times = {"ours": [], "lib": []}
         for _ in range(args.rounds):
-            for arm, fn in arms:
+            for arm, fn in (("ours", ours), ("lib", lib)):
                 for _ in range(3):
                     fn()
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -82,16 +76,13 @@ def main() -> None:
                 e.synchronize()
                 times[arm].append(s.elapsed_time(e) * 1000 / args.iters)
         flop = 2.0 * M * N * K
-        out = {"shape": name, "M": M, "K": K, "N": N, "epi": args.epi, "rel_err": round(err, 6),
-               "auto_split": C.gemm_nt_splits(M, N, K)}
+        out = {"shape": name, "M": M, "K": K, "N": N, "epi": args.epi, "rel_err": round(err, 6)}
         for arm, t in times.items():
             t.sort()
             med = t[len(t) // 2]
             out[f"{arm}_us"] = round(med, 1)
             out[f"{arm}_tflops"] = round(flop / med / 1e6, 1)
-        best = min((a for a, _ in arms if a != "lib"), key=lambda a: out[f"{a}_us"])
-        out["best"] = best
-        out["speedup"] = round(out["lib_us"] / out[f"{best}_us"], 3)
+        out["speedup"] = round(out["lib_us"] / out["ours_us"], 3)
         print(json.dumps(out), flush=True)
 
 
