@@ -10,7 +10,7 @@ Switch                      default      meaning
 PDT_DISABLE_NATIVE          0            1: every op on its PyTorch reference path (stock baseline)
 PDT_CONV1X1                 auto         1x1 conv backend: auto (measured table) | ours | gemm | miopen | off
 PDT_CONV1X1_OURS            fwd,dgrad,wgrad  directions allowed on our MFMA kernels (conv1x1.hip, conv1x1_wgrad.hip)
-PDT_CONV1X1_PREFER          ""           directions that take our GEMM regardless of the table
+PDT_CONV1X1_PREFER          fwd,bwd_data directions that take our GEMM regardless of the table ("none": table only)
 PDT_CONV1X1_OVERRIDE        ""           per-shape decisions "dir,dtype,M,Ci,Co=algo;..." (A/B tools)
 PDT_CONV1X1_TABLE           1            0: ignore tuning/conv1x1_gfx950.json
 PDT_CONV1X1_DUMP            ""           write the decisions to this path at exit
@@ -78,7 +78,9 @@ class _Switches:
         self.disable_native = e("PDT_DISABLE_NATIVE", "0") == "1"
         self.conv1x1 = e("PDT_CONV1X1", "auto")
         self.conv1x1_ours = tuple(e("PDT_CONV1X1_OURS", "fwd,dgrad,wgrad").split(","))
-        self.conv1x1_prefer = tuple(p for p in e("PDT_CONV1X1_PREFER", "").split(",") if p)
+        # our GEMM for the 1x1 forward and data gradients of every shape (layers 3-4 included): on par
+        # with hipBLASLt in-step (profiles/r5/ab_conv1x1_prefer.txt), and its epilogues take the BN work
+        self.conv1x1_prefer = tuple(p for p in e("PDT_CONV1X1_PREFER", "fwd,bwd_data").split(",") if p)
         ov = e("PDT_CONV1X1_OVERRIDE", "")
         self.conv1x1_override = dict(p.split("=", 1) for p in ov.replace("+", ";").split(";") if "=" in p)
         self.conv1x1_table = on("PDT_CONV1X1_TABLE")

@@ -84,7 +84,11 @@ __device__ __forceinline__ void accum_row(const uint16_t* __restrict__ x, const 
 
 // Forward outputs of one channel from its batch mean and (biased) variance: mean / invstd,
 // the apply coefficients y = a*x + b, and the running statistics (unbiased variance).
+// (fp contraction off here and in fin_fwd_sums: every finalize kernel that inlines these must round
+// identically — with contraction the compiler picked different fma pairings in the one- and two-launch
+// tile finalizes, and running_var differed in the last bit)
 __device__ __forceinline__ void bn_set_fwd(int ch, double mu_d, double var, const FinArgs& fa) {
+#pragma clang fp contract(off)
   const int64_t Mt = fa.M;
   var = var < 0.0 ? 0.0 : var;
   const float mu = (float)mu_d;
@@ -444,6 +448,27 @@ __global__ __launch_bounds__(1024) void bn_tiles_l1_kernel(const float* __restri
   }
 }
 
+// Forward finalize from the double sums S = sum x, Q = sum x^2 (about the tile means, recombined).
+__device__ __forceinline__ void fin_fwd_sums(int c, double s, double q, const FinArgs& fa) {
+#pragma clang fp contract(off)
+  const double inv_m = 1.0 / (double)fa.M;
+  const double mu = s * inv_m;
+  bn_set_fwd(c, mu, q * inv_m - mu * mu, fa);
+}
+
+// The P level-1 entries of channel c in the one-launch finalize's order (bn_tiles_fin_kernel): 16
+// strided groups (p = j, j + 16, ...), then the group sums in order — so both paths agree bit for bit.
+__device__ __forceinline__ void sum_level1(const double* __restrict__ in, int P, int C, int c, double& s, double& q) {
+  s = 0.0;
+  q = 0.0;
+  for (int j = 0; j < 16; ++j) {
+    double sj = 0.0, qj = 0.0;
+    for (int p = j; p < P; p += 16) { sj += in[((int64_t)p * C + c) * 2]; qj += in[((int64_t)p * C + c) * 2 + 1]; }
+    s += sj;
+    q += qj;
+  }
+}
+
 // Levels 1 + 2 in ONE launch (the finalize was a second ~5 us launch per BatchNorm, 94 per ResNet-50
 // step: 0.45 ms at 1024 images, 0.9 ms of a 12.8 ms step at 128): the block of tile range p writes its
 // level-1 sums, and the LAST block of its 64-channel column to arrive (release fence, ticket on a
@@ -520,24 +545,9 @@ __global__ __launch_bounds__(1024) void bn_tiles_fin_kernel(const float* __restr
     return;
   }
   if (CENTRED) {
-    const double inv_m = 1.0 / (double)fa.M;
-    const double mu = s * inv_m;
-    bn_set_fwd(c, mu, q * inv_m - mu * mu, fa);
+    fin_fwd_sums(c, s, q, fa);
   } else {
     bn_finalize<1>(c, (float)s, (float)q, fa);
-  }
-}
-
-// The P level-1 entries of channel c in the one-launch finalize's order (bn_tiles_fin_kernel): 16
-// strided groups (p = j, j + 16, ...), then the group sums in order — so both paths agree bit for bit.
-__device__ __forceinline__ void sum_level1(const double* __restrict__ in, int P, int C, int c, double& s, double& q) {
-  s = 0.0;
-  q = 0.0;
-  for (int j = 0; j < 16; ++j) {
-    double sj = 0.0, qj = 0.0;
-    for (int p = j; p < P; p += 16) { sj += in[((int64_t)p * C + c) * 2]; qj += in[((int64_t)p * C + c) * 2 + 1]; }
-    s += sj;
-    q += qj;
   }
 }
 
@@ -546,9 +556,7 @@ __global__ void bn_tiles_l2_kernel(const double* __restrict__ in, int P, int C, 
   if (c >= C) return;
   double s, q;
   sum_level1(in, P, C, c, s, q);
-  const double inv_m = 1.0 / (double)fa.M;
-  const double mu = s * inv_m;
-  bn_set_fwd(c, mu, q * inv_m - mu * mu, fa);
+  fin_fwd_sums(c, s, q, fa);
 }
 
 // Backward finalize from the level-1 sums: S = sum dz, Q = sum dz (x - mean) -> dgamma / dbeta / A, B, D.

@@ -896,7 +896,10 @@ int pdt_conv1x1_gemm(const uint16_t* a, const uint16_t* b, uint16_t* y, const ui
   // 256-wide tiles when the grid is deep (>= 8 blocks per CU): contiguous 512-B output rows, A read once
   // (tools/conv1x1_probe.py, 1024 images: 128->512 @28 fwd+stats 293 vs 342 us, 64->256 @56 506-554 vs
   // 553-571; at 512->2048 @7 — 1,568 blocks — 5 % slower, hence the threshold)
-  if (N % 256 == 0 && (int64_t)((M + 255) / 256) * (N / 256) >= 2048 && !(g_probe & 64))
+  // (the 16-wave tile only for the plain / statistics forward and the data gradient without an accumulate
+  // source — with the ATR operand transform or an accumulate source the 8-wave tile, two workgroups per
+  // CU, ran 5-10 % faster at every ResNet-50 depth: profiles/r5/conv1x1_tiles_bench_b1024.txt)
+  if (N % 256 == 0 && (int64_t)((M + 255) / 256) * (N / 256) >= 2048 && !(g_probe & 64) && !c && !acoef)
     return dispatch<GXWide>(a, b, y, c, cm, part, M, K, N, bs, cg, s, acoef);
   if (N % 128 == 0 && !(g_probe & 8) && !small_grid_narrow((int64_t)((M + 255) / 256) * (N / 128)))
     return dispatch<GWide>(a, b, y, c, cm, part, M, K, N, bs, cg, s, acoef);
@@ -913,10 +916,8 @@ int pdt_conv1x1_gemm_apply(const uint16_t* a, const uint16_t* b, uint16_t* y, co
   const BnSrc bs{};
   const CGeom cg{0, 1, 1, 1, 1};
   const ApArgs ap{ab, rab, mask};
-  if (N % 256 == 0 && (int64_t)((M + 255) / 256) * (N / 256) >= 2048 && !(g_probe & 64)) {
-    if (acoef) return launch_nt<GXWide, false, false, false, false, true, true>(a, b, y, res, nullptr, nullptr, M, K, N, bs, cg, s, acoef, ap);
-    return launch_nt<GXWide, false, false, false, false, false, true>(a, b, y, res, nullptr, nullptr, M, K, N, bs, cg, s, acoef, ap);
-  }
+  // (APPLY on the 8-wave tile at every size: 892 vs 943 us at 64->256 @56, 505 vs 540 @28, 307 vs 333 @14 on
+  // the 16-wave one, profiles/r5/conv1x1_tiles_bench_b1024.txt)
   if (N % 128 == 0 && !(g_probe & 8)) {
     if (acoef) return launch_nt<GWide, false, false, false, false, true, true>(a, b, y, res, nullptr, nullptr, M, K, N, bs, cg, s, acoef, ap);
     return launch_nt<GWide, false, false, false, false, false, true>(a, b, y, res, nullptr, nullptr, M, K, N, bs, cg, s, acoef, ap);
