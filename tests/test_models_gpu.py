@@ -21,8 +21,7 @@ def _grads(model, x, y, loss_fn):
 def _compare(name, make_input, loss_fn, slack=1.3, **kw):
     """Native bf16 path must be as accurate as the stock bf16 path, both measured against an fp32
     oracle. (A direct native-vs-stock comparison is meaningless for deep random-init nets: two
-    bf16 runs differing by 1e-3 in the input already disagree by >100% in early-layer grads,
-    see tools/diag_e2e.py.)"""
+    bf16 runs differing by 1e-3 in the input already disagree by >100% in early-layer grads.)"""
     from pytorch_distributed_training_example_amd.models import get_model
     from pytorch_distributed_training_example_amd.models.precision import to_bf16_mixed
     torch.manual_seed(0)
