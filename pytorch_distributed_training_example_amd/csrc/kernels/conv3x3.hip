@@ -39,6 +39,8 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 #define PDT_LDS __attribute__((address_space(3)))
 
 __device__ __attribute__((aligned(256))) uint4 g_conv_zero[16];  // zero page for padding rows (never written)
+__device__ uint8_t g_conv_ones[16] = {0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff,
+                                      0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff};  // "no ReLU mask"
 
 constexpr int kSlots = 3;
 
@@ -421,19 +423,40 @@ __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv3x3h_kernel(
 #pragma unroll
     for (int k = 0; k < 8; ++k) { bs1[k] = 0.f; bs2[k] = 0.f; }
   }
-  for (int idx = tid; idx < BM * kChunks; idx += Cf::kThreads) {
-    const int r = idx / kChunks, cc = idx % kChunks;
-    const int m = m0 + r;
-    if (m < M) {
-      const int64_t off = (int64_t)m * Co + n0 + cc * 8;
-      const uint4 v = *reinterpret_cast<const uint4*>(lds + r * Cf::kEpiStride + cc * 16);
+  // Rows in batches whose BN-input loads are all issued before the first use, branch-free (a row past
+  // M reads the last valid row and adds nothing; a null mask reads a 0xff byte). Written per row with
+  // conditions, every row's loads waited a full memory latency (hipcc branches around a conditional
+  // load and waits inside the branch, cdna_hip_programming.md §5 trap (c)): the BN-reduction data
+  // gradient ran ~30 us per call slower than the forward (profiles/r5).
+  constexpr int kRowIt = BM * kChunks / Cf::kThreads;
+  constexpr int kBt = BSTATS && kRowIt > 4 ? 4 : kRowIt;
+  static_assert(kRowIt * Cf::kThreads == BM * kChunks && kRowIt % kBt == 0, "epilogue rows");
+  const uint8_t* const bm_base = bs.mask ? bs.mask : g_conv_ones;
+  const int64_t bm_scale = bs.mask ? 1 : 0;
+#pragma unroll 1
+  for (int h = 0; h < kRowIt; h += kBt) {
+    uint4 xbv[kBt];
+    unsigned mkv[kBt];
+#pragma unroll
+    for (int it = 0; it < kBt; ++it) {
       if constexpr (BSTATS) {
-        const uint4 xb = *reinterpret_cast<const uint4*>(bs.x + off);
-        const unsigned mk = bs.mask ? bs.mask[off >> 3] : 0xffu;
-        bn_bwd_accum8(v, xb, mk, bmu, bs1, bs2);
+        const int idx = tid + (h + it) * Cf::kThreads, r = idx / kChunks, cc = idx % kChunks;
+        const int m = m0 + r, mc = m < M ? m : M - 1;
+        const int64_t off = (int64_t)mc * Co + n0 + cc * 8;
+        xbv[it] = *reinterpret_cast<const uint4*>(bs.x + off);
+        const unsigned mk = bm_base[(off >> 3) * bm_scale];
+        mkv[it] = m < M ? mk : 0u;
       }
+    }
+#pragma unroll
+    for (int it = 0; it < kBt; ++it) {
+      const int idx = tid + (h + it) * Cf::kThreads, r = idx / kChunks, cc = idx % kChunks;
+      const int m = m0 + r;
+      const uint4 v = *reinterpret_cast<const uint4*>(lds + r * Cf::kEpiStride + cc * 16);
+      if constexpr (BSTATS) bn_bwd_accum8(v, xbv[it], mkv[it], bmu, bs1, bs2);
+      if (m >= M) continue;
       if constexpr (STATS) rs8_add(rst, v);
-      *reinterpret_cast<uint4*>(Y + off) = v;
+      *reinterpret_cast<uint4*>(Y + (int64_t)m * Co + n0 + cc * 8) = v;
     }
   }
   if constexpr (BSTATS)  // every wave is done reading the staged tile: its LDS holds the block sums

@@ -32,6 +32,10 @@ using namespace pdt;
 
 namespace {
 
+__device__ uint8_t g_s2_ones[16] = {0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff,
+                                    0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff};  // "no ReLU mask"
+
+
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f4 __attribute__((ext_vector_type(4)));
 #define PDT_LDS __attribute__((address_space(3)))
@@ -215,22 +219,44 @@ __global__ __launch_bounds__(Cf::kThreads, 4) void conv3x3g_kernel(const uint16_
     for (int k = 0; k < 8; ++k) { bs1[k] = 0.f; bs2[k] = 0.f; }
   }
   const int py = g.py[ph], px = g.px[ph];
-  for (int idx = tid; idx < kBM * kChunks; idx += kThreads) {
-    const int r = idx / kChunks, c = idx % kChunks;
-    const int m = m0 + r;
-    if (m >= M) continue;
-    const int n = m / HW, rem = m % HW, y = rem / g.Wo, x = rem % g.Wo;
-    const int oy = y * g.sy + py, ox = x * g.sy + px;
-    if (oy >= g.Hy || ox >= g.Wy) continue;  // odd input size: the last phase row/column is outside
-    const int64_t off = ((int64_t)(n * g.Hy + oy) * g.Wy + ox) * g.Co + n0 + c * 8;
-    const uint4 v = *reinterpret_cast<const uint4*>(lds + r * kEpiStride + c * 16);
-    if constexpr (BSTATS) {
-      const uint4 xb = *reinterpret_cast<const uint4*>(bs.x + off);
-      const unsigned mk = bs.mask ? bs.mask[off >> 3] : 0xffu;
-      bn_bwd_accum8(v, xb, mk, bmu, bs1, bs2);
+  // rows in batches, their BN-input loads issued before the first use and branch-free (invalid rows read
+  // row 0 and add nothing): per-row conditional loads waited a memory latency each (conv3x3.hip, halo
+  // kernel epilogue, has the same note)
+  constexpr int kRowIt = kBM * kChunks / kThreads;
+  constexpr int kBt = BSTATS && kRowIt > 4 ? 4 : kRowIt;
+  static_assert(kRowIt * kThreads == kBM * kChunks && kRowIt % kBt == 0, "epilogue rows");
+  const uint8_t* const bm_base = bs.mask ? bs.mask : g_s2_ones;
+  const int64_t bm_scale = bs.mask ? 1 : 0;
+#pragma unroll 1
+  for (int h = 0; h < kRowIt; h += kBt) {
+    int64_t offv[kBt];
+    bool okv[kBt];
+    uint4 xbv[kBt];
+    unsigned mkv[kBt];
+#pragma unroll
+    for (int it = 0; it < kBt; ++it) {
+      const int idx = tid + (h + it) * kThreads, r = idx / kChunks, c = idx % kChunks;
+      const int m = m0 + r, mc = m < M ? m : M - 1;
+      const int n = mc / HW, rem = mc % HW, y = rem / g.Wo, x = rem % g.Wo;
+      const int oy = y * g.sy + py, ox = x * g.sy + px;
+      // (odd input size: the last phase row / column is outside)
+      okv[it] = m < M && oy < g.Hy && ox < g.Wy;
+      offv[it] = okv[it] ? ((int64_t)(n * g.Hy + oy) * g.Wy + ox) * g.Co + n0 + c * 8 : (int64_t)n0 + c * 8;
+      if constexpr (BSTATS) {
+        xbv[it] = *reinterpret_cast<const uint4*>(bs.x + offv[it]);
+        const unsigned mk = bm_base[(offv[it] >> 3) * bm_scale];
+        mkv[it] = okv[it] ? mk : 0u;
+      }
     }
-    if constexpr (STATS) rs8_add(rst, v);
-    *reinterpret_cast<uint4*>(Y + off) = v;
+#pragma unroll
+    for (int it = 0; it < kBt; ++it) {
+      const int idx = tid + (h + it) * kThreads, r = idx / kChunks, c = idx % kChunks;
+      const uint4 v = *reinterpret_cast<const uint4*>(lds + r * kEpiStride + c * 16);
+      if constexpr (BSTATS) bn_bwd_accum8(v, xbv[it], mkv[it], bmu, bs1, bs2);
+      if (!okv[it]) continue;
+      if constexpr (STATS) rs8_add(rst, v);
+      *reinterpret_cast<uint4*>(Y + offv[it]) = v;
+    }
   }
   if constexpr (BSTATS)  // every wave is done reading the staged tile: its LDS holds the block sums
     bn_bwd_tile_store<kBN, kWaves>(bs1, bs2, reinterpret_cast<float*>(lds), bs.part, g.T, ph * g.tpp + mt, g.Co, n0);

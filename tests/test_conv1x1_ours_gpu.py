@@ -148,7 +148,8 @@ def test_conv3x3_stats_epilogue(shape):
     torch.testing.assert_close(part[1], m2, rtol=1e-4, atol=1e-3)
 
 
-@pytest.mark.parametrize("shape", [(4, 128, 128, 28, 28), (3, 64, 64, 13, 11), (32, 64, 64, 56, 56)])
+@pytest.mark.parametrize("shape", [(4, 128, 128, 28, 28), (3, 64, 64, 13, 11), (32, 64, 64, 56, 56),
+                                   (1024, 256, 256, 14, 14), (3, 128, 128, 13, 11)])
 @pytest.mark.parametrize("with_mask", [True, False])
 def test_conv3x3_bn_backward_epilogue(shape, with_mask):
     """The 3x3 data-gradient launch that also takes the BatchNorm backward reduction (halo kernel):
