@@ -142,6 +142,8 @@ int pdt_conv1x1_gemm(const uint16_t* a, const uint16_t* b, uint16_t* y, const ui
                      hipStream_t s);
 void pdt_conv1x1_probe(int probe);
 int pdt_conv1x1_persist(int mode);
+int pdt_conv3x3_opt(int v);
+int pdt_conv3x3s1_stats_tile_rows(int N, int H, int W, int Ci, int Co);
 void pdt_bn_tiles_fused(int on);
 void pdt_maxpool_bwd_v2(int on);
 void pdt_pool_fwd_contig(int on);
@@ -1098,11 +1100,14 @@ std::vector<Tensor> bn_fwd_train_tiles(Tensor x, Tensor part, c10::optional<Tens
   check_nhwc_bf16(x, "x");
   const int64_t C = x.size(1);
   const int64_t M = x.numel() / C;
-  const int BMt = pdt_conv1x1_tile_rows();
-  const int64_t T = (M + BMt - 1) / BMt;
   TORCH_CHECK(C % 64 == 0, "pdt bn: C must be a multiple of 64");
   TORCH_CHECK(part.scalar_type() == at::kFloat && part.is_contiguous() && part.dim() == 3 && part.size(0) == 2 &&
-              part.size(1) == T && part.size(2) == C, "bn_fwd_train_tiles: partials [2, T, C] fp32 expected");
+              part.size(2) == C, "bn_fwd_train_tiles: partials [2, T, C] fp32 expected");
+  // tile height from the partials' row count: 256 (every producer) or 224 (the layer-1 row-tile 3x3,
+  // used only where M / 224 >= 256, so the two never give the same T)
+  const int64_t T = part.size(1);
+  const int BMt = T == (M + 255) / 256 ? 256 : (M % 224 == 0 && T == M / 224 ? 224 : 0);
+  TORCH_CHECK(BMt > 0, "bn_fwd_train_tiles: partials row count ", T, " matches no tile height for M = ", M);
   const auto rab = res_ab_ptrs(res_ab, C);
   Tensor y;
   if (apply) y = at::empty_like(x);
@@ -1160,7 +1165,8 @@ std::vector<Tensor> conv3x3s1_fwd_stats(Tensor x, Tensor w) {
   w = w.contiguous(at::MemoryFormat::ChannelsLast);
   const int64_t N = x.size(0), Ci = x.size(1), H = x.size(2), W = x.size(3), Co = w.size(0);
   auto y = at::empty({N, Co, H, W}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
-  const int64_t T = (N * H * W + pdt_conv1x1_tile_rows() - 1) / pdt_conv1x1_tile_rows();
+  const int64_t rows = pdt_conv3x3s1_stats_tile_rows((int)N, (int)H, (int)W, (int)Ci, (int)Co);
+  const int64_t T = (N * H * W + rows - 1) / rows;
   auto part = at::empty({2, T, Co}, x.options().dtype(at::kFloat));
   const int rc = pdt_conv3x3s1_fwd_stats(reinterpret_cast<const uint16_t*>(x.data_ptr()),
                                          reinterpret_cast<const uint16_t*>(w.data_ptr()),
@@ -1943,6 +1949,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv1x1_probe", [](int probe) { pdt_conv1x1_probe(probe); });
   m.def("conv1x1_persist", [](int mode) { return pdt_conv1x1_persist(mode); },
         "1x1 GEMM persistence mode (0 off, 1 measured kinds, 2 all, -1 env default); returns the previous mode");
+  m.def("conv3x3_opt", [](int v) { return pdt_conv3x3_opt(v); },
+        "3x3 conv variant bits (csrc/kernels/conv3x3.hip conv3x3_opt; -1 env default); returns the previous value");
   m.def("weight_prep", &weight_prep);
   m.def("bn_tiles_fused", [](int on) { pdt_bn_tiles_fused(on); });
   m.def("maxpool_bwd_v2", [](int on) { pdt_maxpool_bwd_v2(on); });

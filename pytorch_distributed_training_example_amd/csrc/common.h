@@ -105,6 +105,40 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// Cross-lane adds in the VALU (DPP row permutes, gfx950 v_permlane16/32_swap) instead of ds_bpermute
+// (__shfl_xor goes through the LDS crossbar: ~100-cycle latency per step, serialised in a reduction
+// chain). Each pairs the same lanes as v + __shfl_xor(v, SH), so results are bit-identical to the
+// shuffle forms. SH = 8 has no exact VALU form and stays a shuffle.
+template <int SH>
+__device__ __forceinline__ float xor_add(float v) {
+  static_assert(SH == 1 || SH == 2 || SH == 8 || SH == 16 || SH == 32, "xor_add: lane distance");
+  if constexpr (SH == 1) {
+    return v + __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, true));
+  } else if constexpr (SH == 2) {
+    return v + __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, true));
+  } else if constexpr (SH == 8) {
+    return v + __shfl_xor(v, 8, 64);
+  } else if constexpr (SH == 16) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  } else {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  }
+}
+
+// Sum over the 16 lanes of each DPP row (lanes 16r .. 16r+15), in every lane of the row: the pairs of
+// v += __shfl_xor(v, 1, 2, 4, 8) in that order (after the xor-1/2 steps a quad is uniform, so the
+// half-row mirror pairs quad 0 with 1 as xor 4 does; after it a half-row is uniform, so the row mirror
+// pairs the halves as xor 8 does): bit-identical to the shuffle chain, four VALU ops.
+__device__ __forceinline__ float row16_sum(float v) {
+  v = xor_add<1>(v);
+  v = xor_add<2>(v);
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x141, 0xF, 0xF, true));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x140, 0xF, 0xF, true));
+  return v;
+}
+
 // Block-wide sum; `red` needs blockDim.x/64 floats of LDS. Result valid in all threads.
 __device__ __forceinline__ float block_sum(float v, float* red) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;

@@ -506,12 +506,10 @@ __global__ __launch_bounds__(Cf::kThreads, 1) void conv1x1_bwd_fused_kernel(FBAr
     // bn2 partials of this workgroup: lanes holding one chunk differ in lane bits 3..5 (a wave stays
     // in one slice); then the waves of a slice in order (fixed-order: deterministic)
 #pragma unroll
-    for (int sh = 8; sh < 64; sh <<= 1)
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        bs1[k] += __shfl_xor(bs1[k], sh, 64);
-        bs2[k] += __shfl_xor(bs2[k], sh, 64);
-      }
+    for (int k = 0; k < 8; ++k) {  // v += v[lane ^ 8], [lane ^ 16], [lane ^ 32] (common.h xor_add)
+      bs1[k] = xor_add<32>(xor_add<16>(xor_add<8>(bs1[k])));
+      bs2[k] = xor_add<32>(xor_add<16>(xor_add<8>(bs2[k])));
+    }
     float* red = reinterpret_cast<float*>(lds);
     __syncthreads();
     if (lane < 8) {

@@ -42,6 +42,26 @@ __device__ __attribute__((aligned(256))) uint4 g_conv_zero[16];  // zero page fo
 __device__ uint8_t g_conv_ones[16] = {0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff,
                                       0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff};  // "no ReLU mask"
 
+// Runtime variant bits for A/B (pdt_conv3x3_opt; env PDT_CONV3X3_OPT read once, default kOptDefault):
+//   bit 0: the weight-stationary kernel skips the DMA of halo rows past its tile's extent;
+//   bits 1 / 2 (timing probes only, WRONG results): that kernel without its halo DMA after the first
+//   chunk / without its MFMA loop — the compute-only and load-only times of its pipeline;
+//   bit 3: its fragment-read / MFMA software pipeline pinned with scheduling barriers;
+//   bit 4 (probe, WRONG results): its loader waves do not wait for a chunk's DMA before the barrier;
+//   bit 5: 64 -> 64 channels at W = 56 on the row-tile kernel (conv3x3wsr_kernel) instead (bits 1 / 2
+//   are its timing probes too);
+//   bit 6: the halo kernel (conv3x3h, layers 2-4) issues its LDS DMA through inline asm (dma16a).
+constexpr int kOptDefault = 41;
+int g_c3opt = -1;
+inline int conv3x3_opt() {
+  if (g_c3opt < 0) {
+    const char* e = getenv("PDT_CONV3X3_OPT");
+    g_c3opt = (e && e[0]) ? (int)strtol(e, nullptr, 10) : kOptDefault;
+    if (g_c3opt < 0) g_c3opt = kOptDefault;
+  }
+  return g_c3opt;
+}
+
 constexpr int kSlots = 3;
 
 // Tile BM pixels x BN channels, WM x WN waves (each (BM/WM) x (BN/WN)), BK input channels per
@@ -84,6 +104,20 @@ __device__ __forceinline__ f4 mfma(bf16x8 a, bf16x8 b, f4 c) {
 
 __device__ __forceinline__ void dma16(const void* src, char* lds_wave_base) {
   __builtin_amdgcn_global_load_lds(src, (PDT_LDS void*)lds_wave_base, 16, 0, 0);
+}
+
+// LDS DMA through inline asm: with the builtin form anywhere in a loop, the compiler's waitcnt pass
+// treats the LGKM counter as out of order and turns every fragment-read wait into lgkmcnt(0); hidden
+// from it, the DMA is counted by this kernel's own vmcnt waits and the ds_read waits stay exact.
+__device__ __forceinline__ void dma16a(const void* src, char* lds_wave_base) {
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(PDT_LDS const char*)lds_wave_base);
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(m0) : "memory");
+}
+
+template <bool ASM>
+__device__ __forceinline__ void dma16x(const void* src, char* lds_wave_base) {
+  if constexpr (ASM) dma16a(src, lds_wave_base);
+  else dma16(src, lds_wave_base);
 }
 
 template <int G>
@@ -267,7 +301,7 @@ __device__ __forceinline__ int chk64(int row, int p) { return p ^ (((row >> 2) &
 
 // BSTATS: Y is the gradient at a BatchNorm's output (this launch is a data gradient): its backward
 // reduction is taken in the epilogue (tile_stats.h bn_bwd_accum8 / bn_bwd_tile_store).
-template <class Cf, bool STATS = false, bool BSTATS = false>
+template <class Cf, bool STATS = false, bool BSTATS = false, bool AD = false>
 __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv3x3h_kernel(
     const uint16_t* __restrict__ X, const uint16_t* __restrict__ Wt, uint16_t* __restrict__ Y, int N, int H, int W,
     int Ci, int Co, float* __restrict__ part, BnSrc bs) {
@@ -322,7 +356,7 @@ __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv3x3h_kernel(
 #pragma unroll
     for (int i = 0; i < Cf::kHLd; ++i) {
       const uint16_t* src = hoff[i] >= 0 ? X + (hoff[i] + c * BK) : reinterpret_cast<const uint16_t*>(g_conv_zero);
-      dma16(src, hb + (wid * Cf::kHLd + i) * 1024);
+      dma16x<AD>(src, hb + (wid * Cf::kHLd + i) * 1024);
     }
   };
   auto issue_b = [&](int s) {
@@ -330,7 +364,7 @@ __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv3x3h_kernel(
     char* bs = bslot0 + (s & 1) * Cf::kBBytes;
 #pragma unroll
     for (int j = 0; j < Cf::kBLd; ++j)
-      dma16(Wt + (boff[j] + g * Cf::TPS * Ci + c * BK), bs + (wid * Cf::kBLd + j) * 1024);
+      dma16x<AD>(Wt + (boff[j] + g * Cf::TPS * Ci + c * BK), bs + (wid * Cf::kBLd + j) * 1024);
   };
 
   f4 acc[Cf::kMB][Cf::kNB];
@@ -668,12 +702,13 @@ struct SCfg {
 // 437 us per call vs 390 us + a 97 us reduce pass (layer 1, batch 1024). (The backward reduction
 // the same way — the BatchNorm input read with 8-B per-lane loads in the epilogue, or prefetched
 // under the last chunk's MFMAs — ran 688-771 us vs 385 us + a 140 us reduce pass: not kept.)
-template <class Cf, bool STATS = false>
+template <class Cf, bool STATS = false, bool PIPE = true>
 __global__ __launch_bounds__(Cf::kThreads, 1) void conv3x3wst_kernel(const uint16_t* __restrict__ X,
                                                                    const uint16_t* __restrict__ Wt,
                                                                    uint16_t* __restrict__ Y, int N, int H, int W,
-                                                                   float* __restrict__ part) {
+                                                                   float* __restrict__ part, int opt) {
   constexpr int BM = Cf::BM, BK = Cf::BK, CI = Cf::CI, CO = Cf::CO, NCH = Cf::kNch;
+  const bool kSkipDead = opt & 1;
   constexpr bool kRed = STATS;
   static_assert(!kRed || NCH >= 2, "a parked chunk is merged before the next tile's end overwrites it");
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -714,6 +749,8 @@ __global__ __launch_bounds__(Cf::kThreads, 1) void conv3x3wst_kernel(const uint1
     char* hb = halo0 + (k & 1) * Cf::kHaloBytes;
 #pragma unroll
     for (int i = 0; i < Cf::kHIns; ++i) {
+      // rows past the tile's halo are never read: skip whole 16-row DMA instructions (wave-uniform)
+      if (kSkipDead && (l * Cf::kHIns + i) * 16 >= Q) break;
       const int q = (l * Cf::kHIns + i) * 16 + sub;
       const uint16_t* src = reinterpret_cast<const uint16_t*>(g_conv_zero);
       if (q < Q) {
@@ -768,9 +805,9 @@ __global__ __launch_bounds__(Cf::kThreads, 1) void conv3x3wst_kernel(const uint1
   asm volatile("" ::: "memory");
   for (int k = 0; k < K; ++k) {
     if (loader) {
-      if (k + 1 < K) {
+      if (k + 1 < K && !(opt & 2)) {
         dma_halo(k + 1);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (!(opt & 16)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
     } else {
       const int tl = t_begin + k / NCH, c = k % NCH;
@@ -805,7 +842,24 @@ __global__ __launch_bounds__(Cf::kThreads, 1) void conv3x3wst_kernel(const uint1
         }
       };
       (void)wb;
+      if (!(opt & 4)) {
       rd(0, 0);
+      if constexpr (PIPE) {
+        // One consumer wave per SIMD: nothing hides a fragment read's latency but this wave's own
+        // MFMAs, so pin the software pipeline (tap t+1's reads issued, then tap t's 16 MFMAs) against
+        // the scheduler, which otherwise interleaves reads and MFMAs with a full lgkmcnt(0) wait
+        // every 4 MFMAs.
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+          if (t < 8) rd(t + 1, (t + 1) & 1);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = mfma(bq[t & 1][j], a[t & 1][i], acc[i][j]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      } else {
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
         if (t < 8) rd(t + 1, (t + 1) & 1);
@@ -813,6 +867,8 @@ __global__ __launch_bounds__(Cf::kThreads, 1) void conv3x3wst_kernel(const uint1
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 4; ++j) acc[i][j] = mfma(bq[t & 1][j], a[t & 1][i], acc[i][j]);
+      }
+      }
       }
       if (c == NCH - 1) {  // tile done: accumulators straight to HBM (4 channels = 8 B per lane)
         float s1[4][4], s2[4][4];
@@ -850,8 +906,7 @@ __global__ __launch_bounds__(Cf::kThreads, 1) void conv3x3wst_kernel(const uint1
           for (int j = 0; j < 4; ++j)
 #pragma unroll
             for (int e = 0; e < 4; ++e)
-#pragma unroll
-              for (int sh = 1; sh < 16; sh <<= 1) s1[j][e] += __shfl_xor(s1[j][e], sh, 64);
+              s1[j][e] = row16_sum(s1[j][e]);  // over the 16 pixel lanes (DPP, no LDS)
           {  // centred sum of squares about this wave's 64-row mean
             const int nw = max(0, min(64, cur_mlast - (cur_m0 + wid * 64) + 1));
             const float inv = nw > 0 ? 1.f / (float)nw : 0.f;
@@ -871,8 +926,7 @@ __global__ __launch_bounds__(Cf::kThreads, 1) void conv3x3wst_kernel(const uint1
           for (int j = 0; j < 4; ++j)
 #pragma unroll
             for (int e = 0; e < 4; ++e)
-#pragma unroll
-              for (int sh = 1; sh < 16; sh <<= 1) s2[j][e] += __shfl_xor(s2[j][e], sh, 64);
+              s2[j][e] = row16_sum(s2[j][e]);
           if (lrow == 0) {
 #pragma unroll
             for (int j = 0; j < 4; ++j)
@@ -897,6 +951,274 @@ __global__ __launch_bounds__(Cf::kThreads, 1) void conv3x3wst_kernel(const uint1
   if constexpr (kRed) {  // the last tile's chunks (parked before the loop's final barrier)
     if (!loader && wid == 0 && pending >= 0) merge(pending);
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (probe bit 4 leaves DMA in flight to here)
+}
+
+// ---------------------------------------------------------------- weight-stationary row-tile variant
+// Layer 1 of ResNet-50 at 224 x 224 (64 -> 64 channels, 56 x 56). The persistent kernel above ran
+// 385-436 us per call at 1024 images against a 94 us MFMA floor, and rocprofv3 counters
+// (profiles/r5/pmc_conv3x3wst_layer1.md) put it at 24 % MFMA-busy with ~4 VALU instructions per MFMA:
+// its 256-pixel tiles cross image rows and images, so every fragment row, halo row and DMA source is
+// a runtime-divisor function of the tile (consumer and loader waves alike), and each chunk's halo DMA
+// was drained before the next barrier (one chunk of lookahead). Here a tile is R = 224 / W WHOLE rows of
+// one image (W = 56: 4 rows = 224 pixels), so
+//   * every consumer lane's fragment rows are the same in every tile (computed once per launch) and a
+//     halo row's (padded row, column) is a compile-time-divisor split of its index;
+//   * the halo of a 32-channel chunk is (R + 2) padded rows with ONE pad column shared by consecutive
+//     rows — (R + 2)(W + 1) + 1 = 343 rows of 64 B (21.4 KB) — so FOUR buffers fit next to the 72 KB of
+//     stationary weights and loader waves keep three chunks in flight (counted vmcnt);
+//   * 4 consumer waves as 2 (pixels) x 2 (channels), 112 x 32 each (7 x 2 v_mfma_f32_16x16x32_bf16),
+//     results straight from the accumulators to HBM; BatchNorm statistics per 224-row tile (tile_stats.h
+//     layout with BMt = 224: bn_fwd_train_tiles reads the tile height off the partials' row count).
+// Requires H % R == 0 (tiles never cross images) and M % 224 == 0 follows.
+template <int W_>
+struct RCfg {
+  static constexpr int W = W_, BM = 224, R = BM / W, CI = 64, CO = 64, BK = 32, NCH = 2, NL = 4, NBUF = 4;
+  static constexpr int kThreads = (4 + NL) * 64;
+  static constexpr int kStride = W + 1;                    // halo row pitch: one pad column between rows
+  static constexpr int kHaloRows = (R + 2) * kStride + 1;  // 343 at W = 56
+  static constexpr int kHaloBytes = kHaloRows * 64;
+  static constexpr int kHIns = (kHaloRows + 15) / 16;      // 16-row DMA instructions per chunk (4 loaders)
+  static constexpr int kWRows = NCH * 9 * CO, kWBytes = kWRows * 64;
+  static constexpr int kStatBytes = 2 * 2 * CO * 4;        // [pixel half][sum, M2][co]
+  static constexpr int kLds = kWBytes + NBUF * kHaloBytes + kStatBytes;
+  static constexpr int kMB = BM / 2 / 16;                  // 16-pixel blocks per consumer wave
+  static_assert(R * W == BM && BM % 32 == 0, "whole image rows, two 16-row-block halves");
+  static_assert(kWRows % (16 * (4 + NL)) == 0, "weight DMA split");
+  static_assert(kLds <= 160 * 1024, "LDS");
+};
+
+template <int N>
+__device__ __forceinline__ void wait_vm_n() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if constexpr (N == 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+  else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else static_assert(N < 0, "vmcnt value");
+}
+
+template <class Cf, bool STATS = false>
+__global__ __launch_bounds__(Cf::kThreads, 1) void conv3x3wsr_kernel(const uint16_t* __restrict__ X,
+                                                                   const uint16_t* __restrict__ Wt,
+                                                                   uint16_t* __restrict__ Y, int N, int H,
+                                                                   float* __restrict__ part, int opt) {
+  constexpr int W = Cf::W, R = Cf::R, BM = Cf::BM, BK = Cf::BK, CI = Cf::CI, CO = Cf::CO, NB = Cf::NBUF;
+  constexpr int S = Cf::kStride, MB = Cf::kMB, HR = Cf::kHaloRows, HI = Cf::kHIns;
+  constexpr int kSplit = 3;  // A blocks in the first read group of a tap
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  char* const wlds = lds;
+  char* const halo0 = lds + Cf::kWBytes;
+  float* const statb = reinterpret_cast<float*>(lds + Cf::kWBytes + NB * Cf::kHaloBytes);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const bool loader = wid >= 4;
+  const int tpi = H / R, ntile = N * tpi;
+  const int g = gridDim.x, b = blockIdx.x;
+  const int t_begin = (int)((int64_t)ntile * b / g), t_end = (int)((int64_t)ntile * (b + 1) / g);
+  const int K = (t_end - t_begin) * 2;  // (tile, chunk) steps of this workgroup
+  const int sub = lane >> 2, p = lane & 3;
+
+  {  // weights [chunk][tap][co] rows of 64 B: every wave DMAs its share once
+    constexpr int kIns = Cf::kWRows / 16 / (4 + Cf::NL);
+#pragma unroll
+    for (int i = 0; i < kIns; ++i) {
+      const int r = (wid * kIns + i) * 16 + sub;
+      const int c = r / (9 * CO), t = (r / CO) % 9, co = r % CO;
+      dma16a(Wt + (co * 9 + t) * CI + c * BK + chk64(r, p) * 8, wlds + (wid * kIns + i) * 1024);
+    }
+  }
+  // loader wave l issues the chunk's DMA instructions l, l + 4, ... (HI in all): nl of them
+  const int l = wid - 4;
+  const int nl = (HI - l + 3) / 4;
+  // the zero page's address once (SGPRs), not a GOT load per DMA instruction inside the loop
+  uint64_t zpa = reinterpret_cast<uint64_t>(g_conv_zero);
+  asm volatile("" : "+s"(zpa));
+  const uint16_t* const zpage = reinterpret_cast<const uint16_t*>(zpa);
+  auto dma_halo = [&](int k) {
+    const int tl = t_begin + (k >> 1), c = k & 1;
+    const int n = tl / tpi, r0 = (tl - n * tpi) * R;
+    char* hb = halo0 + (k % NB) * Cf::kHaloBytes;
+    // loader and consumer roles share one register allocation: keep the loader's per-lane row math in
+    // the loop (not hoisted and held live across the consumers' MFMA code)
+    int lsub = sub;
+    asm volatile("" : "+v"(lsub));
+#pragma unroll
+    for (int i = 0; i < (HI + 3) / 4; ++i) {
+      const int gi = l + 4 * i;
+      if (gi >= HI) break;  // wave-uniform
+      const int q = gi * 16 + lsub;
+      const int pr = q / S, pc = q - pr * S - 1, ih = r0 - 1 + pr;
+      const uint16_t* src = zpage;
+      if (pc >= 0 && pc < W && ih >= 0 && ih < H) src = X + (((n * H + ih) * W + pc) * CI + c * BK + chk64(q, p) * 8);
+      if (q < HR) dma16a(src, hb + gi * 1024);  // the last instruction's rows past HR stay off
+    }
+  };
+  auto wait_next = [&](int k) {  // chunk k + 1 landed: allow the DMAs of chunks k + 2 .. k + 3 in flight
+    const int after = min(K - 1, k + 3) - (k + 1);
+    if (after <= 0) wait_vm_n<0>();
+    else if (after == 1) { if (nl == 6) wait_vm_n<6>(); else wait_vm_n<5>(); }
+    else { if (nl == 6) wait_vm_n<12>(); else wait_vm_n<10>(); }
+  };
+
+  // consumer geometry: identical in every tile
+  const int lrow = lane & 15, lchk = lane >> 4;
+  const int wm = wid & 1, wn = (wid >> 1) & 1;
+  // swizzled LDS offsets of every (block, tap) fragment row, relative to the halo buffer: the same in
+  // every tile and chunk, so computed once (63 VGPRs; recomputing them costs ~5 VALU per fragment read,
+  // 3 VALU per MFMA in all)
+  int aoff[MB][9];
+#pragma unroll
+  for (int i = 0; i < MB; ++i) {
+    const int mm = wm * (BM / 2) + i * 16 + lrow;
+    const int ab = (mm / W) * S + mm % W;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int q = ab + (t / 3) * S + (t % 3);
+      aoff[i][t] = q * 64 + (chk64(q, lchk) << 4);
+      asm volatile("" : "+v"(aoff[i][t]));
+    }
+  }
+  const int bbase = lrow * 64 + (chk64(lrow, lchk) << 4) + (wn * 32) * 64;  // + (c*9*CO + t*CO + j*16) * 64
+  f4 acc[MB][2];
+  int pending = -1;
+  auto merge = [&](int tl) {  // consumer wave 0: one channel per lane, Chan's formula over the two halves
+    const float S0 = statb[0 * CO + lane], Q0 = statb[1 * CO + lane];
+    const float S1 = statb[2 * CO + lane], Q1 = statb[3 * CO + lane];
+    const float d = (S1 - S0) * (1.f / (BM / 2));
+    part[(int64_t)tl * CO + lane] = S0 + S1;
+    part[((int64_t)ntile + tl) * CO + lane] = Q0 + Q1 + d * d * (float)(BM / 4);
+  };
+
+  if (loader) {
+    for (int j = 0; j < 3 && j < K; ++j) dma_halo(j);
+    const int after = min(K - 1, 2);  // chunks issued after chunk 0
+    if (after <= 0) wait_vm_n<0>();
+    else if (after == 1) { if (nl == 6) wait_vm_n<6>(); else wait_vm_n<5>(); }
+    else { if (nl == 6) wait_vm_n<12>(); else wait_vm_n<10>(); }
+  } else {
+    wait_vm_n<0>();
+  }
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+  for (int tl = t_begin; tl < t_end; ++tl) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int k = (tl - t_begin) * 2 + c;
+      if (loader) {
+        if (k + 3 < K && !(opt & 2)) dma_halo(k + 3);
+        wait_next(k);
+      } else {
+        if constexpr (STATS) {
+          if (pending >= 0 && wid == 0) merge(pending);
+          pending = -1;
+        }
+        const char* hb = halo0 + (k % NB) * Cf::kHaloBytes;
+        const char* wb = wlds + bbase + (c * 9 * CO) * 64;
+        bf16x8 a[2][MB], bq[2][2];
+        // fragment reads of tap t in two groups: B + A blocks 0..2, then A blocks 3..6
+        auto rd = [&](int t, int set, int part) {
+          if (part == 0) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) bq[set][j] = *reinterpret_cast<const bf16x8*>(wb + (t * CO + j * 16) * 64);
+          }
+#pragma unroll
+          for (int i = part == 0 ? 0 : kSplit; i < (part == 0 ? kSplit : MB); ++i)
+            a[set][i] = *reinterpret_cast<const bf16x8*>(hb + aoff[i][t]);
+        };
+        auto mm = [&](int t, int i0, int i1) {
+#pragma unroll
+          for (int i = i0; i < i1; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+              acc[i][j] = (c == 0 && t == 0) ? mfma(bq[0][j], a[0][i], f4{0.f, 0.f, 0.f, 0.f})
+                                             : mfma(bq[t & 1][j], a[t & 1][i], acc[i][j]);
+        };
+        // One consumer wave per SIMD: only this wave's own MFMAs can hide its fragment reads, so the
+        // software pipeline is pinned against the scheduler (which otherwise interleaves reads and
+        // MFMAs with a full lgkmcnt(0) wait every 2 MFMAs): tap t+1's reads go out in two groups, each
+        // ahead of half of tap t's MFMAs, so at most 14 LDS reads are ever outstanding — within the
+        // 4-bit lgkmcnt, which lets the compiler wait for exactly the reads an MFMA group consumes
+        // (9 per tap in one group would put 18 in flight and force lgkmcnt(0)).
+        if (!(opt & 4)) {
+        rd(0, 0, 0);
+        rd(0, 0, 1);
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+          if (t < 8) rd(t + 1, (t + 1) & 1, 0);
+          __builtin_amdgcn_sched_barrier(0);
+          mm(t, 0, kSplit + 1);
+          __builtin_amdgcn_sched_barrier(0);
+          if (t < 8) rd(t + 1, (t + 1) & 1, 1);
+          __builtin_amdgcn_sched_barrier(0);
+          mm(t, kSplit + 1, MB);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        }
+        if (c == 1) {  // tile done: bf16 results straight to HBM (4 channels = 8 B per lane)
+          const int m0 = tl * BM + wm * (BM / 2);
+          float s1[2][4];
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) s1[j][e] = 0.f;
+#pragma unroll
+          for (int i = 0; i < MB; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              const f4 v = acc[i][j];
+              uint2 pk;
+              pk.x = (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)v[0]) |
+                     ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)v[1]) << 16);
+              pk.y = (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)v[2]) |
+                     ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)v[3]) << 16);
+              *reinterpret_cast<uint2*>(Y + (int64_t)(m0 + i * 16 + lrow) * CO + wn * 32 + j * 16 + 4 * lchk) = pk;
+              if constexpr (STATS) {  // statistics of the values written (bf16-rounded)
+                acc[i][j] = f4{__uint_as_float(pk.x << 16), __uint_as_float(pk.x & 0xffff0000u),
+                               __uint_as_float(pk.y << 16), __uint_as_float(pk.y & 0xffff0000u)};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) s1[j][e] += acc[i][j][e];
+              }
+            }
+          if constexpr (STATS) {
+            float s2[2][4];
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                s1[j][e] = row16_sum(s1[j][e]);
+                const float mu = s1[j][e] * (1.f / (BM / 2));
+                float q2 = 0.f;
+#pragma unroll
+                for (int i = 0; i < MB; ++i) {
+                  const float d = acc[i][j][e] - mu;
+                  q2 += d * d;
+                }
+                s2[j][e] = row16_sum(q2);
+              }
+            if (lrow == 0) {
+#pragma unroll
+              for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                  const int co = wn * 32 + j * 16 + 4 * lchk + e;
+                  statb[(wm * 2) * CO + co] = s1[j][e];
+                  statb[(wm * 2 + 1) * CO + co] = s2[j][e];
+                }
+            }
+            pending = tl;
+          }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+  }
+  if constexpr (STATS) {
+    if (!loader && wid == 0 && pending >= 0) merge(pending);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // (The weight gradient lives in conv3x3_wgrad.hip: a first version here, register-staged with
@@ -914,7 +1236,9 @@ int launch_h(const uint16_t* x, const uint16_t* w, uint16_t* y, int N, int H, in
              float* part = nullptr, const BnSrc& bs = BnSrc{}) {
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3h_kernel<Cf, STATS, BSTATS>),
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3h_kernel<Cf, STATS, BSTATS, false>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, Cf::kLds) != hipSuccess ||
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3h_kernel<Cf, STATS, BSTATS, true>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, Cf::kLds) != hipSuccess)
       return -3;
     attr = true;
@@ -923,8 +1247,12 @@ int launch_h(const uint16_t* x, const uint16_t* w, uint16_t* y, int N, int H, in
   if (halo_rows_bound(H, W, Cf::BM) > Cf::kHaloRows) return -4;
   const int64_t M = (int64_t)N * H * W;
   const int64_t grid = (M + Cf::BM - 1) / Cf::BM * (Co / Cf::BN);
-  hipLaunchKernelGGL((conv3x3h_kernel<Cf, STATS, BSTATS>), dim3((unsigned)grid), dim3(Cf::kThreads), Cf::kLds, s, x, w,
-                     y, N, H, W, Ci, Co, part, bs);
+  if (conv3x3_opt() & 64)
+    hipLaunchKernelGGL((conv3x3h_kernel<Cf, STATS, BSTATS, true>), dim3((unsigned)grid), dim3(Cf::kThreads), Cf::kLds,
+                       s, x, w, y, N, H, W, Ci, Co, part, bs);
+  else
+    hipLaunchKernelGGL((conv3x3h_kernel<Cf, STATS, BSTATS, false>), dim3((unsigned)grid), dim3(Cf::kThreads), Cf::kLds,
+                       s, x, w, y, N, H, W, Ci, Co, part, bs);
   return 0;
 }
 
@@ -952,12 +1280,14 @@ int launch_wst(const uint16_t* x, const uint16_t* w, uint16_t* y, int N, int H, 
   static bool attr = false;
   static int ncu = 0;
   if (!attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3wst_kernel<Cf, STATS>),
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3wst_kernel<Cf, STATS, true>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, Cf::kLds) != hipSuccess ||
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3wst_kernel<Cf, STATS, false>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, Cf::kLds) != hipSuccess)
       return -3;
     int dev = 0;
-    hipGetDevice(&dev);
-    hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
     attr = true;
   }
   if (Ci != Cf::CI || Co != Cf::CO) return -1;
@@ -965,8 +1295,42 @@ int launch_wst(const uint16_t* x, const uint16_t* w, uint16_t* y, int N, int H, 
   const int64_t M = (int64_t)N * H * W;
   const int64_t ntile = (M + Cf::BM - 1) / Cf::BM;
   const int grid = (int)(ntile < ncu ? ntile : ncu);
-  hipLaunchKernelGGL((conv3x3wst_kernel<Cf, STATS>), dim3(grid), dim3(Cf::kThreads), Cf::kLds, s, x, w, y, N, H, W,
-                     part);
+  const int opt = conv3x3_opt();
+  if (opt & 8)
+    hipLaunchKernelGGL((conv3x3wst_kernel<Cf, STATS, true>), dim3(grid), dim3(Cf::kThreads), Cf::kLds, s, x, w, y, N, H,
+                       W, part, opt);
+  else
+    hipLaunchKernelGGL((conv3x3wst_kernel<Cf, STATS, false>), dim3(grid), dim3(Cf::kThreads), Cf::kLds, s, x, w, y, N,
+                       H, W, part, opt);
+  return 0;
+}
+
+// The row-tile weight-stationary kernel (conv3x3wsr_kernel): opt bit 5, W = 56 (ResNet-50 layer 1 at
+// 224 x 224; other widths keep conv3x3wst), whole-row tiles inside one image, at least one tile per CU.
+using RCfg56 = RCfg<56>;
+inline bool wsr_applies(int N, int H, int W, int Ci, int Co) {
+  return (conv3x3_opt() & 32) && Ci == 64 && Co == 64 && W == RCfg56::W && H % RCfg56::R == 0 &&
+         (int64_t)N * (H / RCfg56::R) >= 256;
+}
+
+template <bool STATS>
+int launch_wsr(const uint16_t* x, const uint16_t* w, uint16_t* y, int N, int H, hipStream_t s, float* part = nullptr) {
+  using Cf = RCfg56;
+  static bool attr = false;
+  static int ncu = 0;
+  if (!attr) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3wsr_kernel<Cf, STATS>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, Cf::kLds) != hipSuccess)
+      return -3;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    attr = true;
+  }
+  const int64_t ntile = (int64_t)N * (H / Cf::R);
+  const int grid = (int)(ntile < ncu ? ntile : ncu);
+  hipLaunchKernelGGL((conv3x3wsr_kernel<Cf, STATS>), dim3(grid), dim3(Cf::kThreads), Cf::kLds, s, x, w, y, N, H, part,
+                     conv3x3_opt());
   return 0;
 }
 
@@ -1023,6 +1387,7 @@ int pdt_conv3x3s1_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int N, 
   return PDT_CONV_LAUNCH<PDT_CONV_CFG_OVERRIDE>(x, w, y, N, H, W, Ci, Co, s);
 #endif
   int rc = -1;
+  if (wsr_applies(N, H, W, Ci, Co)) return launch_wsr<false>(x, w, y, N, H, s);
   if (Ci == 64 && Co == 64) rc = launch_wst<SCfg<64, 64>>(x, w, y, N, H, W, Ci, Co, s);
   if (rc == -1) rc = h_wide(M, Co) ? launch_h<HWide>(x, w, y, N, H, W, Ci, Co, s) : launch_h<HNarrow>(x, w, y, N, H, W, Ci, Co, s);
   if (rc != -4) return rc;
@@ -1031,7 +1396,14 @@ int pdt_conv3x3s1_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int N, 
   return launch<CfNarrow>(x, w, y, N, H, W, Ci, Co, s);
 }
 
-// Forward + per-256-pixel-tile BatchNorm statistics of y into part ([2][T][Co] fp32, tile_stats.h).
+// Rows per statistics tile of pdt_conv3x3s1_fwd_stats at this shape: 224 where the row-tile kernel runs
+// (part then has M / 224 tiles), else 256.
+int pdt_conv3x3s1_stats_tile_rows(int N, int H, int W, int Ci, int Co) {
+  return wsr_applies(N, H, W, Ci, Co) ? RCfg56::BM : 256;
+}
+
+// Forward + per-tile BatchNorm statistics of y into part ([2][T][Co] fp32, tile_stats.h; tiles of
+// pdt_conv3x3s1_stats_tile_rows rows).
 // The halo and weight-stationary (64 -> 64) kernels have the statistics epilogue: returns -5 where
 // another kernel would run (tiny W: per-tap staging) — caller falls back.
 int pdt_conv3x3s1_fwd_stats(const uint16_t* x, const uint16_t* w, uint16_t* y, float* part, int N, int H, int W,
@@ -1039,6 +1411,7 @@ int pdt_conv3x3s1_fwd_stats(const uint16_t* x, const uint16_t* w, uint16_t* y, f
   if (Ci % 32 != 0 || Co % 64 != 0 || N < 1 || H < 1 || W < 1) return -1;
   const int64_t M = (int64_t)N * H * W;
   if (M * (Ci > Co ? Ci : Co) >= (int64_t)1 << 31 || (int64_t)Co * 9 * Ci >= (int64_t)1 << 31) return -2;
+  if (wsr_applies(N, H, W, Ci, Co)) return launch_wsr<true>(x, w, y, N, H, s, part);  // 224-row tiles
   if (Ci == 64 && Co == 64) {
     const int rc = launch_wst<SCfg<64, 64>, true>(x, w, y, N, H, W, Ci, Co, s, part);
     return rc == -4 ? -5 : rc;
@@ -1063,6 +1436,14 @@ int pdt_conv3x3s1_fwd_bnbwd(const uint16_t* x, const uint16_t* w, uint16_t* y, c
   const BnSrc bs{bn_x, bn_mask, bn_mean, bn_part};
   return h_wide(M, Co) ? launch_h<HWide, false, true>(x, w, y, N, H, W, Ci, Co, s, nullptr, bs)
                        : launch_h<HNarrow, false, true>(x, w, y, N, H, W, Ci, Co, s, nullptr, bs);
+}
+
+// Set the 3x3 variant bits (conv3x3_opt); -1 re-reads PDT_CONV3X3_OPT. Returns the previous value.
+int pdt_conv3x3_opt(int v) {
+  const int old = conv3x3_opt();
+  g_c3opt = v;
+  (void)conv3x3_opt();
+  return old;
 }
 
 // wf[Ci,3,3,Co] (the data-gradient weights) from w[Co,3,3,Ci].

@@ -273,8 +273,8 @@ __global__ __launch_bounds__(kThreads, 2) void stem_conv_kernel(const uint16_t* 
   if constexpr (STATS) {  // partial p = (workgroup, wave): S = n K + sum (y - K), M2 = sum (y - K)^2 - sum (y - K)^2 / n
     pdt_f2 sk = pdt_f2{0.f, 0.f}, ss = sk, sq = sk;
     if (kset) { sk = sst[0]; ss = sst[1]; sq = sst[2]; }
-    ss += pdt_f2{__shfl_xor(ss.x, 32, 64), __shfl_xor(ss.y, 32, 64)};
-    sq += pdt_f2{__shfl_xor(sq.x, 32, 64), __shfl_xor(sq.y, 32, 64)};
+    ss = pdt_f2{xor_add<32>(ss.x), xor_add<32>(ss.y)};
+    sq = pdt_f2{xor_add<32>(sq.x), xor_add<32>(sq.y)};
     if (lane < 32) {
       const int P = gridDim.x * kRowsOut, p = blockIdx.x * kRowsOut + wid;
       const float n = (float)nrows;

@@ -104,13 +104,17 @@ __device__ __forceinline__ void rs8_tile_store(RowStats8& t, float K, float* red
   constexpr int kChunks = BN / 8;
   static_assert(64 % kChunks == 0, "chunk lanes");
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  auto xr = [](float v) {  // v + v[lane ^ sh] for sh = kChunks .. 32 (VALU cross-lane forms)
+    if constexpr (kChunks <= 8) v = xor_add<8>(v);
+    if constexpr (kChunks <= 16) v = xor_add<16>(v);
+    return xor_add<32>(v);
+  };
+  static_assert(kChunks >= 8, "xor_add distances");
 #pragma unroll
-  for (int sh = kChunks; sh < 64; sh <<= 1)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      t.s[j] += pdt_f2{__shfl_xor(t.s[j].x, sh, 64), __shfl_xor(t.s[j].y, sh, 64)};
-      t.q[j] += pdt_f2{__shfl_xor(t.q[j].x, sh, 64), __shfl_xor(t.q[j].y, sh, 64)};
-    }
+  for (int j = 0; j < 4; ++j) {
+    t.s[j] = pdt_f2{xr(t.s[j].x), xr(t.s[j].y)};
+    t.q[j] = pdt_f2{xr(t.q[j].x), xr(t.q[j].y)};
+  }
   if (lane < kChunks) {
     float* r = red + (wid * kChunks + lane) * 16;
 #pragma unroll
@@ -173,13 +177,14 @@ __device__ __forceinline__ void bn_bwd_tile_store(float (&s1)[8], float (&s2)[8]
   static_assert(64 % kChunks == 0, "chunk lanes");
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   // lanes of one wave holding the same chunk differ in the lane bits >= log2(kChunks)
+  static_assert(kChunks >= 8, "xor_add distances");
 #pragma unroll
-  for (int sh = kChunks; sh < 64; sh <<= 1)
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      s1[k] += __shfl_xor(s1[k], sh, 64);
-      s2[k] += __shfl_xor(s2[k], sh, 64);
-    }
+  for (int k = 0; k < 8; ++k) {
+    if constexpr (kChunks <= 8) { s1[k] = xor_add<8>(s1[k]); s2[k] = xor_add<8>(s2[k]); }
+    if constexpr (kChunks <= 16) { s1[k] = xor_add<16>(s1[k]); s2[k] = xor_add<16>(s2[k]); }
+    s1[k] = xor_add<32>(s1[k]);
+    s2[k] = xor_add<32>(s2[k]);
+  }
   __syncthreads();
   if (lane < kChunks) {
 #pragma unroll

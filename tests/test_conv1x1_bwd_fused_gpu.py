@@ -2,6 +2,8 @@
 PyTorch references of the same math: the BatchNorm backward apply formed on load, the 1x1 conv's data
 and weight gradients, and the producing BatchNorm's backward partial sums; plus the coefficient-only
 BatchNorm backward (bn_bwd_coef) against the full native backward."""
+import os
+
 import pytest
 import torch
 
@@ -129,24 +131,45 @@ def test_bn_bwd_coef_matches_full_backward(relu, with_part):
     torch.testing.assert_close(db2, db, rtol=1e-3, atol=1e-3)
 
 
-def _grads(seed=0):
+def _grads(seed=0, fp32=False):
+    """ResNet-50 parameter gradients of one step at batch 8 (96 x 96): bf16-mixed on our kernels, or
+    (fp32=True) the same weights, input and labels in fp32 on stock PyTorch ops (PDT_DISABLE_NATIVE) —
+    the oracle, as in tests/test_models_gpu.py."""
+    from pytorch_distributed_training_example_amd.config import SW
     from pytorch_distributed_training_example_amd.models import get_model
     from pytorch_distributed_training_example_amd.models.precision import to_bf16_mixed
-    torch.manual_seed(seed)
-    m = to_bf16_mixed(get_model("resnet50").cuda().to(memory_format=torch.channels_last))
-    x = torch.randn(8, 3, 96, 96, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
-    y = torch.randint(0, 1000, (8,), device="cuda")
-    loss = torch.nn.functional.cross_entropy(m(x).float(), y)
-    loss.backward()
-    return {n: p.grad.float().clone() for n, p in m.named_parameters()}
+    if fp32:
+        os.environ["PDT_DISABLE_NATIVE"] = "1"
+        SW.reload()
+    try:
+        torch.manual_seed(seed)
+        m = get_model("resnet50").cuda().to(memory_format=torch.channels_last)
+        if not fp32:
+            m = to_bf16_mixed(m)
+        x = torch.randn(8, 3, 96, 96, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+        y = torch.randint(0, 1000, (8,), device="cuda")
+        if fp32:
+            x = x.float()
+        loss = torch.nn.functional.cross_entropy(m(x).float(), y)
+        loss.backward()
+        return {n: p.grad.float().clone() for n, p in m.named_parameters()}
+    finally:
+        if fp32:
+            os.environ.pop("PDT_DISABLE_NATIVE", None)
+            SW.reload()
+
+
+def _rel(ga, gref):
+    return torch.tensor([float((ga[n] - gref[n]).norm() / gref[n].norm().clamp_min(1e-12)) for n in gref])
 
 
 @pytest.mark.parametrize("defer", ["0", "1"])
 def test_resnet50_grads_fused_vs_unfused(switch, defer):
-    """The whole model's gradients with the fused conv3 + bn3 backward (layers 1-2) against the unfused
-    kernel chain: same math, different rounding points (dz is rounded once, in LDS). Through 50
-    random-init layers at batch 8 rounding differences grow toward the stem (the stem BN sees them
-    amplified most: ~8 % there), so this is a median / max check; the per-block check is below."""
+    """The whole model's gradients with the fused conv3 + bn3 backward (layers 1-2) and with the unfused
+    kernel chain, each against an fp32 oracle (the same weights, input and labels on PyTorch's fp32 ops):
+    the fused path must be as accurate as the unfused one, tensor by tensor. (Both are deterministic,
+    tests/test_determinism_gpu.py, so the bound is a fixed comparison, not a tolerance for noise.) The
+    per-block check is below."""
     from pytorch_distributed_training_example_amd.ops import conv as conv_ops
     calls = []
     orig = conv_ops._bwd_fused
@@ -167,9 +190,14 @@ def test_resnet50_grads_fused_vs_unfused(switch, defer):
     assert calls == [True] * 8, calls
     switch("PDT_BWD_FUSED", "0")
     gb = _grads()
-    assert ga.keys() == gb.keys()
-    rel = torch.tensor([float((ga[n] - gb[n]).norm() / gb[n].norm().clamp_min(1e-12)) for n in ga])
-    assert rel.median() < 1e-2 and rel.max() < 0.15, (float(rel.median()), float(rel.max()))
+    g32 = _grads(fp32=True)
+    assert ga.keys() == gb.keys() == g32.keys()
+    ea, eb = _rel(ga, g32), _rel(gb, g32)
+    print(f"fused vs fp32: median {float(ea.median()):.4f} max {float(ea.max()):.4f}; "
+          f"unfused vs fp32: median {float(eb.median()):.4f} max {float(eb.max()):.4f}")
+    assert float(ea.median()) <= 1.1 * float(eb.median()) + 1e-3, (float(ea.median()), float(eb.median()))
+    worse = [(n, float(a), float(b)) for n, a, b in zip(g32, ea, eb) if a > 1.5 * b + 5e-3]
+    assert not worse, worse[:8]
 
 
 @pytest.mark.parametrize("defer", ["0", "1"])

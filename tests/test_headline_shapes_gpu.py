@@ -121,3 +121,40 @@ def test_multi_tensor_copy_bucket_pack(src_dtype, dst_dtype):
     multi_tensor.copy_(src, dst)
     for s, d in zip(src, dst):
         assert torch.equal(s.to(dst_dtype), d)
+
+
+@pytest.mark.parametrize("opt", [41])
+def test_conv3x3_layer1_row_tiles(opt):
+    """conv3x3wsr_kernel (layer 1, 64 -> 64 at 56 x 56, whole-row 224-pixel tiles, four-deep halo DMA
+    pipeline): forward + statistics against an fp32 oracle, the BN forward finalize from its 224-row
+    partials against torch's batch statistics, and the data gradient (same kernel, flipped weights)."""
+    C = _n()
+    old = C.conv3x3_opt(opt)
+    try:
+        N, c, H = 24, 64, 56  # 336 tiles: at least one per CU, so the row-tile kernel runs
+        g = torch.Generator(device="cuda").manual_seed(3)
+        x = _cl(torch.randn(N, c, H, H, device="cuda", generator=g).bfloat16())
+        w = _cl((torch.randn(c, c, 3, 3, device="cuda", generator=g) / 24).bfloat16())
+        y, part = C.conv3x3s1_fwd_stats(x, w)
+        M = N * H * H
+        assert part.shape == (2, M // 224, c)
+        ref = torch.nn.functional.conv2d(x.float(), w.float(), padding=1)
+        torch.testing.assert_close(y.float(), ref, rtol=2e-2, atol=2e-2)
+        yf = y.float().permute(0, 2, 3, 1).reshape(-1, 224, c)
+        torch.testing.assert_close(part[0], yf.sum(1), rtol=1e-4, atol=1e-3)
+        torch.testing.assert_close(part[1], ((yf - yf.mean(1, keepdim=True)) ** 2).sum(1), rtol=1e-3, atol=1e-3)
+        gamma = torch.rand(c, device="cuda") + 0.5
+        beta = torch.randn(c, device="cuda")
+        _, _, mean, invstd = C.bn_fwd_train_tiles(y, part, None, gamma, beta, None, None, 0.1, 1e-5, True, None, True)
+        yv = y.float().permute(0, 2, 3, 1).reshape(-1, c)
+        torch.testing.assert_close(mean, yv.mean(0), rtol=1e-4, atol=1e-4)
+        torch.testing.assert_close(invstd, (yv.var(0, unbiased=False) + 1e-5).rsqrt(), rtol=1e-3, atol=1e-3)
+        wf = C.conv3x3_flip(w)
+        dx = C.conv3x3s1_fwd(y, wf)
+        gref = torch.nn.grad.conv2d_input(x.shape, w.float(), y.float(), padding=1)
+        torch.testing.assert_close(dx.float(), gref, rtol=2e-2, atol=5e-2)
+        C.conv3x3_opt(9)  # the 256-pixel weight-stationary kernel on the same input: same convolution
+        y2 = C.conv3x3s1_fwd(x, w)
+        torch.testing.assert_close(y.float(), y2.float(), rtol=1e-2, atol=1e-2)
+    finally:
+        C.conv3x3_opt(old)
