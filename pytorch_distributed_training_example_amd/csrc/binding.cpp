@@ -144,6 +144,7 @@ void pdt_conv1x1_probe(int probe);
 int pdt_conv1x1_persist(int mode);
 int pdt_conv3x3_opt(int v);
 int pdt_conv3x3s1_stats_tile_rows(int N, int H, int W, int Ci, int Co);
+int pdt_conv3x3s1_bnbwd_tile_rows(int N, int H, int W, int Ci, int Co);
 void pdt_bn_tiles_fused(int on);
 void pdt_maxpool_bwd_v2(int on);
 void pdt_pool_fwd_contig(int on);
@@ -1199,7 +1200,8 @@ std::vector<Tensor> conv3x3s1_fwd_bnbwd(Tensor x, Tensor w, Tensor bn_x, c10::op
     mp = bn_mask->data_ptr<uint8_t>();
   }
   auto y = at::empty({N, Co, H, W}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
-  const int64_t T = (N * H * W + pdt_conv1x1_tile_rows() - 1) / pdt_conv1x1_tile_rows();
+  const int64_t rows = pdt_conv3x3s1_bnbwd_tile_rows((int)N, (int)H, (int)W, (int)Ci, (int)Co);
+  const int64_t T = (N * H * W + rows - 1) / rows;
   auto part = at::empty({2, T, Co}, x.options().dtype(at::kFloat));
   const int rc = pdt_conv3x3s1_fwd_bnbwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
                                          reinterpret_cast<const uint16_t*>(w.data_ptr()),

@@ -39,7 +39,7 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 #define PDT_LDS __attribute__((address_space(3)))
 
 __device__ __attribute__((aligned(256))) uint4 g_conv_zero[16];  // zero page for padding rows (never written)
-__device__ uint8_t g_conv_ones[16] = {0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff,
+__device__ __attribute__((aligned(16))) uint8_t g_conv_ones[16] = {0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff,
                                       0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff};  // "no ReLU mask"
 
 // Runtime variant bits for A/B (pdt_conv3x3_opt; env PDT_CONV3X3_OPT read once, default kOptDefault):
@@ -50,7 +50,8 @@ __device__ uint8_t g_conv_ones[16] = {0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 
 //   bit 4 (probe, WRONG results): its loader waves do not wait for a chunk's DMA before the barrier;
 //   bit 5: 64 -> 64 channels at W = 56 on the row-tile kernel (conv3x3wsr_kernel) instead (bits 1 / 2
 //   are its timing probes too);
-//   bit 6: the halo kernel (conv3x3h, layers 2-4) issues its LDS DMA through inline asm (dma16a).
+//   bit 6: the halo kernel (conv3x3h, layers 2-4) issues its LDS DMA through inline asm (dma16a);
+//   bit 7: the row-tile kernel takes the data gradient's BatchNorm backward reduction (BSTATS).
 constexpr int kOptDefault = 41;
 int g_c3opt = -1;
 inline int conv3x3_opt() {
@@ -998,11 +999,16 @@ __device__ __forceinline__ void wait_vm_n() {
   else static_assert(N < 0, "vmcnt value");
 }
 
-template <class Cf, bool STATS = false>
+// BSTATS: Y is the gradient at a BatchNorm's output (a data gradient): that BatchNorm's backward
+// reduction (sum dz, sum dz (x - mean), dz = Y * ReLU mask) per 224-row tile into bs.part; the BN input
+// and mask of the tile's pixels are loaded into registers at the start of its second chunk, under the
+// MFMAs (28 + 7 VGPRs), and reduced from the accumulators like the forward statistics.
+template <class Cf, bool STATS = false, bool BSTATS = false>
 __global__ __launch_bounds__(Cf::kThreads, 1) void conv3x3wsr_kernel(const uint16_t* __restrict__ X,
                                                                    const uint16_t* __restrict__ Wt,
                                                                    uint16_t* __restrict__ Y, int N, int H,
-                                                                   float* __restrict__ part, int opt) {
+                                                                   float* __restrict__ part, int opt, BnSrc bs) {
+  static_assert(!(STATS && BSTATS), "one epilogue reduction");
   constexpr int W = Cf::W, R = Cf::R, BM = Cf::BM, BK = Cf::BK, CI = Cf::CI, CO = Cf::CO, NB = Cf::NBUF;
   constexpr int S = Cf::kStride, MB = Cf::kMB, HR = Cf::kHaloRows, HI = Cf::kHIns;
   constexpr int kSplit = 3;  // A blocks in the first read group of a tap
@@ -1064,30 +1070,54 @@ __global__ __launch_bounds__(Cf::kThreads, 1) void conv3x3wsr_kernel(const uint1
   const int lrow = lane & 15, lchk = lane >> 4;
   const int wm = wid & 1, wn = (wid >> 1) & 1;
   // swizzled LDS offsets of every (block, tap) fragment row, relative to the halo buffer: the same in
-  // every tile and chunk, so computed once (63 VGPRs; recomputing them costs ~5 VALU per fragment read,
-  // 3 VALU per MFMA in all)
-  int aoff[MB][9];
+  // every tile and chunk, so computed once (recomputing them costs ~5 VALU per fragment read, 3 VALU per
+  // MFMA in all)
+  // two 16-bit offsets per VGPR (offsets < 22 KB): 35 VGPRs instead of 63, unpacked by the address add
+  // (BSTATS needs 35 more VGPRs in its epilogue than 256 allow with these held: it recomputes them)
+  static_assert(Cf::kHaloBytes <= 65536, "16-bit fragment offsets");
+  constexpr bool kHold = !BSTATS;
+  uint32_t aoff[MB][5];
+  int abase[MB];
 #pragma unroll
   for (int i = 0; i < MB; ++i) {
     const int mm = wm * (BM / 2) + i * 16 + lrow;
     const int ab = (mm / W) * S + mm % W;
+    abase[i] = ab;
+    if constexpr (kHold) {
 #pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      const int q = ab + (t / 3) * S + (t % 3);
-      aoff[i][t] = q * 64 + (chk64(q, lchk) << 4);
-      asm volatile("" : "+v"(aoff[i][t]));
+      for (int u = 0; u < 5; ++u) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int h = 0; h < 2 && 2 * u + h < 9; ++h) {
+          const int t = 2 * u + h;
+          const int q = ab + (t / 3) * S + (t % 3);
+          v |= (uint32_t)(q * 64 + (chk64(q, lchk) << 4)) << (16 * h);
+        }
+        aoff[i][u] = v;
+        asm volatile("" : "+v"(aoff[i][u]));
+      }
     }
   }
   const int bbase = lrow * 64 + (chk64(lrow, lchk) << 4) + (wn * 32) * 64;  // + (c*9*CO + t*CO + j*16) * 64
   f4 acc[MB][2];
   int pending = -1;
-  auto merge = [&](int tl) {  // consumer wave 0: one channel per lane, Chan's formula over the two halves
+  float* const opart = BSTATS ? bs.part : part;
+  auto merge = [&](int tl) {  // consumer wave 0: one channel per lane, over the two pixel halves
     const float S0 = statb[0 * CO + lane], Q0 = statb[1 * CO + lane];
     const float S1 = statb[2 * CO + lane], Q1 = statb[3 * CO + lane];
-    const float d = (S1 - S0) * (1.f / (BM / 2));
-    part[(int64_t)tl * CO + lane] = S0 + S1;
-    part[((int64_t)ntile + tl) * CO + lane] = Q0 + Q1 + d * d * (float)(BM / 4);
+    opart[(int64_t)tl * CO + lane] = S0 + S1;
+    if constexpr (BSTATS) {  // plain sums
+      opart[((int64_t)ntile + tl) * CO + lane] = Q0 + Q1;
+    } else {  // Chan's formula: centred sums of squares of two 112-row halves
+      const float d = (S1 - S0) * (1.f / (BM / 2));
+      opart[((int64_t)ntile + tl) * CO + lane] = Q0 + Q1 + d * d * (float)(BM / 4);
+    }
   };
+  // BSTATS: the mask base (all-ones page when there is no ReLU)
+  const uint8_t* const bm_base = BSTATS && bs.mask ? bs.mask : g_conv_ones;
+  const int64_t bm_scale = BSTATS && bs.mask ? 1 : 0;
+  uint2 bxv[MB][2];
+  uint32_t bmk[MB];
 
   if (loader) {
     for (int j = 0; j < 3 && j < K; ++j) dma_halo(j);
@@ -1109,12 +1139,42 @@ __global__ __launch_bounds__(Cf::kThreads, 1) void conv3x3wsr_kernel(const uint1
         if (k + 3 < K && !(opt & 2)) dma_halo(k + 3);
         wait_next(k);
       } else {
-        if constexpr (STATS) {
+        if constexpr (STATS || BSTATS) {
           if (pending >= 0 && wid == 0) merge(pending);
           pending = -1;
         }
+        // BSTATS: the tile's BN input and mask bits, loaded at the epilogue (held across the MFMAs, the 35
+        // VGPRs spill: 256 per wave at two waves per SIMD)
+        auto prefetch_bn = [&]() {
+          int m0 = tl * BM + wm * (BM / 2) + lrow;
+          asm volatile("" : "+v"(m0));  // per-lane address math stays here (hoisted, it would spill)
+#pragma unroll
+          for (int i = 0; i < MB; ++i) {
+            const int64_t m = m0 + i * 16;
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+              bxv[i][j] = *reinterpret_cast<const uint2*>(bs.x + m * CO + wn * 32 + j * 16 + 4 * lchk);
+            bmk[i] = *reinterpret_cast<const uint32_t*>(bm_base + (m * (CO / 8) + wn * 4) * bm_scale);
+          }
+        };
         const char* hb = halo0 + (k % NB) * Cf::kHaloBytes;
         const char* wb = wlds + bbase + (c * 9 * CO) * 64;
+        int ab[MB];
+        if constexpr (!kHold) {
+#pragma unroll
+          for (int i = 0; i < MB; ++i) {
+            ab[i] = abase[i];
+            asm volatile("" : "+v"(ab[i]));
+          }
+        }
+        auto frag_off = [&](int i, int t) -> uint32_t {
+          if constexpr (kHold) {
+            return (t & 1) ? (aoff[i][t >> 1] >> 16) : (aoff[i][t >> 1] & 0xffffu);
+          } else {
+            const int q = ab[i] + (t / 3) * S + (t % 3);
+            return (uint32_t)(q * 64 + (chk64(q, lchk) << 4));
+          }
+        };
         bf16x8 a[2][MB], bq[2][2];
         // fragment reads of tap t in two groups: B + A blocks 0..2, then A blocks 3..6
         auto rd = [&](int t, int set, int part) {
@@ -1124,7 +1184,7 @@ __global__ __launch_bounds__(Cf::kThreads, 1) void conv3x3wsr_kernel(const uint1
           }
 #pragma unroll
           for (int i = part == 0 ? 0 : kSplit; i < (part == 0 ? kSplit : MB); ++i)
-            a[set][i] = *reinterpret_cast<const bf16x8*>(hb + aoff[i][t]);
+            a[set][i] = *reinterpret_cast<const bf16x8*>(hb + frag_off(i, t));
         };
         auto mm = [&](int t, int i0, int i1) {
 #pragma unroll
@@ -1157,11 +1217,21 @@ __global__ __launch_bounds__(Cf::kThreads, 1) void conv3x3wsr_kernel(const uint1
         }
         if (c == 1) {  // tile done: bf16 results straight to HBM (4 channels = 8 B per lane)
           const int m0 = tl * BM + wm * (BM / 2);
-          float s1[2][4];
+          float s1[2][4], s2b[2][4];
 #pragma unroll
           for (int j = 0; j < 2; ++j)
 #pragma unroll
-            for (int e = 0; e < 4; ++e) s1[j][e] = 0.f;
+            for (int e = 0; e < 4; ++e) s1[j][e] = s2b[j][e] = 0.f;
+          float bmu[2][4];  // this lane's 8 channels' batch means (cache-resident; loaded here, not held)
+          if constexpr (BSTATS) {
+            prefetch_bn();
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              const float4 mv = *reinterpret_cast<const float4*>(bs.mean + wn * 32 + j * 16 + 4 * lchk);
+              bmu[j][0] = mv.x; bmu[j][1] = mv.y; bmu[j][2] = mv.z; bmu[j][3] = mv.w;
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the prefetched BN inputs and the means
+          }
 #pragma unroll
           for (int i = 0; i < MB; ++i)
 #pragma unroll
@@ -1173,6 +1243,18 @@ __global__ __launch_bounds__(Cf::kThreads, 1) void conv3x3wsr_kernel(const uint1
               pk.y = (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)v[2]) |
                      ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)v[3]) << 16);
               *reinterpret_cast<uint2*>(Y + (int64_t)(m0 + i * 16 + lrow) * CO + wn * 32 + j * 16 + 4 * lchk) = pk;
+              if constexpr (BSTATS) {  // dz = written value x mask; sums of dz and dz (x - mean)
+                const float gv[4] = {__uint_as_float(pk.x << 16), __uint_as_float(pk.x & 0xffff0000u),
+                                     __uint_as_float(pk.y << 16), __uint_as_float(pk.y & 0xffff0000u)};
+                const float xv[4] = {__uint_as_float(bxv[i][j].x << 16), __uint_as_float(bxv[i][j].x & 0xffff0000u),
+                                     __uint_as_float(bxv[i][j].y << 16), __uint_as_float(bxv[i][j].y & 0xffff0000u)};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                  const float dz = (bmk[i] >> (j * 16 + 4 * lchk + e)) & 1u ? gv[e] : 0.f;
+                  s1[j][e] += dz;
+                  s2b[j][e] += dz * (xv[e] - bmu[j][e]);
+                }
+              }
               if constexpr (STATS) {  // statistics of the values written (bf16-rounded)
                 acc[i][j] = f4{__uint_as_float(pk.x << 16), __uint_as_float(pk.x & 0xffff0000u),
                                __uint_as_float(pk.y << 16), __uint_as_float(pk.y & 0xffff0000u)};
@@ -1180,6 +1262,26 @@ __global__ __launch_bounds__(Cf::kThreads, 1) void conv3x3wsr_kernel(const uint1
                 for (int e = 0; e < 4; ++e) s1[j][e] += acc[i][j][e];
               }
             }
+          if constexpr (BSTATS) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {  // every lane takes part in the DPP row sums
+                s1[j][e] = row16_sum(s1[j][e]);
+                s2b[j][e] = row16_sum(s2b[j][e]);
+              }
+            if (lrow == 0) {
+#pragma unroll
+              for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                  const int co = wn * 32 + j * 16 + 4 * lchk + e;
+                  statb[(wm * 2) * CO + co] = s1[j][e];
+                  statb[(wm * 2 + 1) * CO + co] = s2b[j][e];
+                }
+            }
+            pending = tl;
+          }
           if constexpr (STATS) {
             float s2[2][4];
 #pragma unroll
@@ -1215,7 +1317,7 @@ __global__ __launch_bounds__(Cf::kThreads, 1) void conv3x3wsr_kernel(const uint1
       asm volatile("" ::: "memory");
     }
   }
-  if constexpr (STATS) {
+  if constexpr (STATS || BSTATS) {
     if (!loader && wid == 0 && pending >= 0) merge(pending);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1313,13 +1415,14 @@ inline bool wsr_applies(int N, int H, int W, int Ci, int Co) {
          (int64_t)N * (H / RCfg56::R) >= 256;
 }
 
-template <bool STATS>
-int launch_wsr(const uint16_t* x, const uint16_t* w, uint16_t* y, int N, int H, hipStream_t s, float* part = nullptr) {
+template <bool STATS, bool BSTATS = false>
+int launch_wsr(const uint16_t* x, const uint16_t* w, uint16_t* y, int N, int H, hipStream_t s, float* part = nullptr,
+               const BnSrc& bs = BnSrc{}) {
   using Cf = RCfg56;
   static bool attr = false;
   static int ncu = 0;
   if (!attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3wsr_kernel<Cf, STATS>),
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3wsr_kernel<Cf, STATS, BSTATS>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, Cf::kLds) != hipSuccess)
       return -3;
     int dev = 0;
@@ -1329,8 +1432,8 @@ int launch_wsr(const uint16_t* x, const uint16_t* w, uint16_t* y, int N, int H, 
   }
   const int64_t ntile = (int64_t)N * (H / Cf::R);
   const int grid = (int)(ntile < ncu ? ntile : ncu);
-  hipLaunchKernelGGL((conv3x3wsr_kernel<Cf, STATS>), dim3(grid), dim3(Cf::kThreads), Cf::kLds, s, x, w, y, N, H, part,
-                     conv3x3_opt());
+  hipLaunchKernelGGL((conv3x3wsr_kernel<Cf, STATS, BSTATS>), dim3(grid), dim3(Cf::kThreads), Cf::kLds, s, x, w, y, N,
+                     H, part, conv3x3_opt(), bs);
   return 0;
 }
 
@@ -1402,6 +1505,11 @@ int pdt_conv3x3s1_stats_tile_rows(int N, int H, int W, int Ci, int Co) {
   return wsr_applies(N, H, W, Ci, Co) ? RCfg56::BM : 256;
 }
 
+// Same for the backward reduction of pdt_conv3x3s1_fwd_bnbwd.
+int pdt_conv3x3s1_bnbwd_tile_rows(int N, int H, int W, int Ci, int Co) {
+  return wsr_applies(N, H, W, Ci, Co) && (conv3x3_opt() & 128) ? RCfg56::BM : 256;
+}
+
 // Forward + per-tile BatchNorm statistics of y into part ([2][T][Co] fp32, tile_stats.h; tiles of
 // pdt_conv3x3s1_stats_tile_rows rows).
 // The halo and weight-stationary (64 -> 64) kernels have the statistics epilogue: returns -5 where
@@ -1431,9 +1539,11 @@ int pdt_conv3x3s1_fwd_bnbwd(const uint16_t* x, const uint16_t* w, uint16_t* y, c
   if (Ci % 32 != 0 || Co % 64 != 0 || N < 1 || H < 1 || W < 1 || !bn_x || !bn_mean || !bn_part) return -1;
   const int64_t M = (int64_t)N * H * W;
   if (M * (Ci > Co ? Ci : Co) >= (int64_t)1 << 31 || (int64_t)Co * 9 * Ci >= (int64_t)1 << 31) return -2;
-  if (Ci == 64 && Co == 64) return -5;  // weight-stationary kernel: its epilogue reduction did not pay
-  if (halo_rows_bound(H, W, 256) > 512) return -5;
   const BnSrc bs{bn_x, bn_mask, bn_mean, bn_part};
+  // the row-tile kernel takes it (224-row tiles); the 256-pixel weight-stationary one's reduction did not pay
+  if (wsr_applies(N, H, W, Ci, Co) && (conv3x3_opt() & 128)) return launch_wsr<false, true>(x, w, y, N, H, s, nullptr, bs);
+  if (Ci == 64 && Co == 64) return -5;
+  if (halo_rows_bound(H, W, 256) > 512) return -5;
   return h_wide(M, Co) ? launch_h<HWide, false, true>(x, w, y, N, H, W, Ci, Co, s, nullptr, bs)
                        : launch_h<HNarrow, false, true>(x, w, y, N, H, W, Ci, Co, s, nullptr, bs);
 }

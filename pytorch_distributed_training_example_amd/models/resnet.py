@@ -107,7 +107,12 @@ class Bottleneck(nn.Module):
         self.stride = stride
 
     def forward(self, x):
+        # The linked path needs bn3 on its native kernel (bf16): only that path deposits the shortcut
+        # gradient into the link. With any other BatchNorm path conv1's backward would find the link
+        # empty, park its dx there for a partner that never comes, and the conv1 branch's gradient
+        # would be lost (fp32 ResNet-50 on the GPU lost it in every block until round 5).
         if (RESIDUAL_GRAD_LINK[0] and self.training and x.requires_grad and torch.is_grad_enabled()
+                and x.dtype == torch.bfloat16 and not native_disabled()
                 and isinstance(self.conv1, Conv1x1) and isinstance(self.bn3, BatchNorm2d)
                 and self.conv1.gemm_eligible(x) and x.shape[1] % 64 == 0):
             # the two gradients of x (conv1 branch, shortcut) meet in conv1's data-gradient GEMM

@@ -123,7 +123,7 @@ def test_multi_tensor_copy_bucket_pack(src_dtype, dst_dtype):
         assert torch.equal(s.to(dst_dtype), d)
 
 
-@pytest.mark.parametrize("opt", [41])
+@pytest.mark.parametrize("opt", [41, 41 + 128])
 def test_conv3x3_layer1_row_tiles(opt):
     """conv3x3wsr_kernel (layer 1, 64 -> 64 at 56 x 56, whole-row 224-pixel tiles, four-deep halo DMA
     pipeline): forward + statistics against an fp32 oracle, the BN forward finalize from its 224-row
@@ -153,6 +153,21 @@ def test_conv3x3_layer1_row_tiles(opt):
         dx = C.conv3x3s1_fwd(y, wf)
         gref = torch.nn.grad.conv2d_input(x.shape, w.float(), y.float(), padding=1)
         torch.testing.assert_close(dx.float(), gref, rtol=2e-2, atol=5e-2)
+        if opt & 128:  # the data gradient with the producing BatchNorm's backward reduction (BSTATS)
+            bx = _cl(torch.randn(N, c, H, H, device="cuda", generator=g).bfloat16())
+            bits, mask = _bits(M, c, g)
+            mean = bx.float().permute(0, 2, 3, 1).reshape(M, c).mean(0).contiguous()
+            dx2, bpart = C.conv3x3s1_fwd_bnbwd(y, wf, bx, mask, mean)
+            assert torch.equal(dx2, dx)
+            assert bpart.shape == (2, M // 224, c)
+            dz = torch.where(bits, dx.float().permute(0, 2, 3, 1).reshape(M, c), 0.0)
+            xc = bx.float().permute(0, 2, 3, 1).reshape(M, c) - mean
+            torch.testing.assert_close(bpart[0].sum(0), dz.sum(0), rtol=1e-3, atol=1e-1)
+            torch.testing.assert_close(bpart[1].sum(0), (dz * xc).sum(0), rtol=1e-3, atol=1e-1)
+            torch.testing.assert_close(bpart[0], dz.view(-1, 224, c).sum(1), rtol=1e-3, atol=1e-2)
+            dx3, bpart3 = C.conv3x3s1_fwd_bnbwd(y, wf, bx, None, mean)  # no ReLU mask
+            torch.testing.assert_close(bpart3[0].sum(0), dx.float().permute(0, 2, 3, 1).reshape(M, c).sum(0),
+                                       rtol=1e-3, atol=1e-1)
         C.conv3x3_opt(9)  # the 256-pixel weight-stationary kernel on the same input: same convolution
         y2 = C.conv3x3s1_fwd(x, w)
         torch.testing.assert_close(y.float(), y2.float(), rtol=1e-2, atol=1e-2)

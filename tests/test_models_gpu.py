@@ -118,3 +118,33 @@ def test_global_avgpool_channels_last_grad():
     torch.testing.assert_close(y.float(), yr, rtol=1e-2, atol=1e-2)
     torch.testing.assert_close(x.grad.float(), xr.grad, rtol=1e-2, atol=1e-3)
     assert x.grad.is_contiguous(memory_format=torch.channels_last)
+
+
+def test_resnet50_fp32_native_matches_stock():
+    """fp32 ResNet-50 with native ops enabled against stock PyTorch (PDT_DISABLE_NATIVE): the same model.
+    Round 5 found the bottleneck's residual-gradient link taken in fp32, where only the bf16 BatchNorm
+    kernel deposits the shortcut gradient: conv1's branch gradient was dropped in every block and the
+    stem gradient came out 360x too small (tools/diag_oracle.py)."""
+    from pytorch_distributed_training_example_amd.config import SW
+    from pytorch_distributed_training_example_amd.models import get_model
+
+    def grads(disable):
+        if disable:
+            os.environ["PDT_DISABLE_NATIVE"] = "1"
+        SW.reload()
+        try:
+            torch.manual_seed(0)
+            m = get_model("resnet50").cuda().to(memory_format=torch.channels_last)
+            x = torch.randn(8, 3, 96, 96, device="cuda").contiguous(memory_format=torch.channels_last)
+            y = torch.randint(0, 1000, (8,), device="cuda")
+            torch.nn.functional.cross_entropy(m(x), y).backward()
+            return {k: p.grad.clone() for k, p in m.named_parameters()}
+        finally:
+            os.environ.pop("PDT_DISABLE_NATIVE", None)
+            SW.reload()
+
+    ga, gb = grads(False), grads(True)
+    e = torch.tensor([float((ga[k] - gb[k]).norm() / gb[k].norm().clamp_min(1e-12)) for k in gb])
+    ratio = float(ga["conv1.weight"].norm() / gb["conv1.weight"].norm())
+    assert 0.8 < ratio < 1.25, ratio
+    assert float(e.median()) < 0.05 and float(e.max()) < 0.5, (float(e.median()), float(e.max()))

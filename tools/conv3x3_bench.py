@@ -63,8 +63,10 @@ def main():
         mean = torch.randn(w, device="cuda")
         fl = 2.0 * M * w * w * 9
         cases = [(f"s1 fwd+stats {w}@{h}", n_s1 + (0 if s2 else 0), lambda: C.conv3x3s1_fwd_stats(x, wt), fl)]
-        if w == 64:
+        if w == 64:  # plain, and with the BN reduction where the kernel takes it (opt bit 7)
             cases.append((f"s1 dgrad {w}@{h}", n_s1, lambda: C.conv3x3s1_fwd(gy, wf), fl))
+            cases.append((f"s1 dgrad+bnred {w}@{h} (if taken)", 0,
+                          lambda: C.conv3x3s1_fwd_bnbwd(gy, wf, bx, mask, mean), fl))
         else:
             cases.append((f"s1 dgrad+bnred {w}@{h}", n_s1, lambda: C.conv3x3s1_fwd_bnbwd(gy, wf, bx, mask, mean), fl))
         cases.append((f"s1 wgrad {w}@{h}", n_s1, lambda: C.conv3x3s1_wgrad(x, gy), fl))
