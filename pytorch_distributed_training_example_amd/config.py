@@ -24,6 +24,7 @@ PDT_BN_BWD_STATS            1            BatchNorm backward reduction in dgrad e
 PDT_RES_MASKED              1            ReLU'd residual gradient handed over as (dy, mask)
 PDT_STEM_BWD_FUSED          1            stem pool backward takes the BN backward reduction
 PDT_STEM_BN_WGRAD           1            stem weight gradient applies the stem BN backward on load
+PDT_STEM_POOL_WGRAD         1            ... and forms the max-pool gradient itself (pooled dy + codes): dz never in HBM
 PDT_STRIDED_BSTATS          1            a transition block's conv1 data gradient adds the stride-2 shortcut's compact
                                          gradient AND takes the previous block's bn3 backward reduction in our
                                          GEMM's epilogue (vs hipBLASLt + scatter-add + a reduce pass)
@@ -62,7 +63,7 @@ import os
 class _Switches:
     __slots__ = ("disable_native", "conv1x1", "conv1x1_ours", "conv1x1_prefer", "conv1x1_override",
                  "conv1x1_table", "conv1x1_dump", "conv1x1_s2", "conv3x3", "conv3x3_wgrad", "conv3x3_s2", "conv_stem",
-                 "conv_bn_stats", "bn_bwd_stats", "res_masked", "stem_bwd_fused", "stem_bn_wgrad", "stem_bn_stats", "wgrad_splitk", "slice_sum",
+                 "conv_bn_stats", "bn_bwd_stats", "res_masked", "stem_bwd_fused", "stem_bn_wgrad", "stem_bn_stats", "stem_pool_wgrad", "wgrad_splitk", "slice_sum",
                  "subsample_native", "linear_splitk", "fused_addln", "embedding_native", "linear_epilogue",
                  "bwd_fused", "bwd_fused_shapes", "bn2_defer", "bn_apply_gemm_k", "strided_bstats", "gap_native")
 
@@ -96,6 +97,9 @@ class _Switches:
         self.stem_bwd_fused = on("PDT_STEM_BWD_FUSED")
         self.stem_bn_wgrad = on("PDT_STEM_BN_WGRAD")
         self.stem_bn_stats = on("PDT_STEM_BN_STATS")
+        # the stem weight gradient forms the max-pool gradient itself from (pooled dy, winner codes):
+        # the 1.6 GB pool-input gradient is neither written nor read back (conv_stem.hip POOL)
+        self.stem_pool_wgrad = on("PDT_STEM_POOL_WGRAD")
         self.wgrad_splitk = on("PDT_WGRAD_SPLITK")
         self.slice_sum = on("PDT_SLICE_SUM")
         self.subsample_native = on("PDT_SUBSAMPLE_NATIVE")

@@ -127,6 +127,9 @@ int pdt_stem_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* wp, uint16
 int64_t pdt_stem_wgrad_ws_floats();
 int pdt_stem_conv_wgrad(const uint16_t* x, const uint16_t* dy, uint16_t* dw, float* ws, int N, int H, int W,
                         hipStream_t s);
+int pdt_stem_conv_wgrad_bn_pool(const uint16_t* x, const uint16_t* dyp, const uint8_t* code, const uint16_t* xb,
+                                const float* coef, const float* mean, uint16_t* dw, float* ws, int N, int H, int W,
+                                hipStream_t s);
 int pdt_stem_conv_wgrad_bn(const uint16_t* x, const uint16_t* dz, const uint16_t* xb, const float* coef,
                            const float* mean, uint16_t* dw, float* ws, int N, int H, int W, hipStream_t s);
 int pdt_maxpool3s2_bwd(const uint16_t* dy, const uint8_t* code, uint16_t* dz, int N, int H, int W, int C,
@@ -646,7 +649,7 @@ std::vector<Tensor> maxpool3s2_bwd_bn(Tensor dy, Tensor code, Tensor x, c10::opt
 // Same without the BN apply: returns {dz (the max-pool gradient = dy at the BN output), coef [3, 64]
 // (A, B, D: dx = A dz + B (x - mean) + D), dgamma, dbeta} for stem_conv_wgrad_bn.
 std::vector<Tensor> maxpool3s2_bwd_bn_coef(Tensor dy, Tensor code, Tensor x, c10::optional<Tensor> weight,
-                                           Tensor mean, Tensor invstd, bool need_dgamma) {
+                                           Tensor mean, Tensor invstd, bool need_dgamma, bool write_dz) {
   check_nhwc_bf16(dy, "dy");
   check_nhwc_bf16(x, "x");
   const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
@@ -654,7 +657,8 @@ std::vector<Tensor> maxpool3s2_bwd_bn_coef(Tensor dy, Tensor code, Tensor x, c10
   TORCH_CHECK(dy.size(0) == N && dy.size(1) == C && dy.size(2) == (H - 1) / 2 + 1 && dy.size(3) == (W - 1) / 2 + 1,
               "maxpool3s2_bwd_bn_coef: dy shape");
   TORCH_CHECK(code.scalar_type() == at::kByte && code.numel() == dy.numel(), "maxpool3s2_bwd_bn_coef: code");
-  auto dz = at::empty_like(x);
+  Tensor dz;
+  if (write_dz) dz = at::empty_like(x);
   auto fopt = x.options().dtype(at::kFloat);
   auto coef = at::empty({3, C}, fopt);
   Tensor dg, db;
@@ -667,7 +671,7 @@ std::vector<Tensor> maxpool3s2_bwd_bn_coef(Tensor dy, Tensor code, Tensor x, c10
   auto ws = at::empty({pdt_bn_tiles_ws_floats(T, (int)C) + 2 * C}, fopt);
   const int rc = pdt_maxpool3s2_bwd_bn_coef(
       reinterpret_cast<const uint16_t*>(dy.data_ptr()), code.data_ptr<uint8_t>(),
-      reinterpret_cast<uint16_t*>(dz.data_ptr()), (int)N, (int)H, (int)W, (int)C,
+      write_dz ? reinterpret_cast<uint16_t*>(dz.data_ptr()) : nullptr, (int)N, (int)H, (int)W, (int)C,
       reinterpret_cast<const uint16_t*>(x.data_ptr()), opt_fptr(weight), mean.data_ptr<float>(),
       invstd.data_ptr<float>(), coef.data_ptr<float>(), need_dgamma ? dg.data_ptr<float>() : nullptr,
       need_dgamma ? db.data_ptr<float>() : nullptr, part.data_ptr<float>(), ws.data_ptr<float>(), stream());
@@ -1428,6 +1432,36 @@ Tensor stem_conv_wgrad_bn(Tensor x, Tensor dz, Tensor xb, Tensor coef, Tensor me
   return dw;
 }
 
+// The same weight gradient from the gradient at the max-pool OUTPUT (dyp [N, 64, PH, PW]) and the pool's
+// winner codes: the pool's input gradient dz is formed per tile inside the kernel, never in HBM.
+Tensor stem_conv_wgrad_bn_pool(Tensor x, Tensor dyp, Tensor code, Tensor xb, Tensor coef, Tensor mean) {
+  check_nhwc_bf16(x, "x");
+  check_nhwc_bf16(dyp, "dyp");
+  check_nhwc_bf16(xb, "xb");
+  const int64_t N = x.size(0), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(x.size(1) == 3 && W % 32 == 0 && W <= 224, "stem_conv_wgrad_bn_pool: x [N, 3, H, W], W % 32 == 0, W <= 224");
+  const int64_t OH = (H - 1) / 2 + 1, OW = W / 2;
+  TORCH_CHECK(xb.size(0) == N && xb.size(1) == 64 && xb.size(2) == OH && xb.size(3) == OW,
+              "stem_conv_wgrad_bn_pool: xb [N, 64, OH, OW]");
+  TORCH_CHECK(dyp.size(0) == N && dyp.size(1) == 64 && dyp.size(2) == (OH - 1) / 2 + 1 && dyp.size(3) == (OW - 1) / 2 + 1,
+              "stem_conv_wgrad_bn_pool: dyp [N, 64, PH, PW]");
+  TORCH_CHECK(code.is_cuda() && code.scalar_type() == at::kByte && code.numel() == dyp.numel() && code.is_contiguous(),
+              "stem_conv_wgrad_bn_pool: code uint8, one per dyp element");
+  TORCH_CHECK(coef.is_cuda() && coef.scalar_type() == at::kFloat && coef.is_contiguous() && coef.numel() == 3 * 64,
+              "stem_conv_wgrad_bn_pool: coef [3, 64] f32");
+  TORCH_CHECK(mean.is_cuda() && mean.scalar_type() == at::kFloat && mean.is_contiguous() && mean.numel() == 64,
+              "stem_conv_wgrad_bn_pool: mean [64] f32");
+  auto ws = at::empty({pdt_stem_wgrad_ws_floats()}, x.options().dtype(at::kFloat));
+  auto dw = at::empty({64, 3, 7, 7}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const int rc = pdt_stem_conv_wgrad_bn_pool(
+      reinterpret_cast<const uint16_t*>(x.data_ptr()), reinterpret_cast<const uint16_t*>(dyp.data_ptr()),
+      code.data_ptr<uint8_t>(), reinterpret_cast<const uint16_t*>(xb.data_ptr()), coef.data_ptr<float>(),
+      mean.data_ptr<float>(), reinterpret_cast<uint16_t*>(dw.data_ptr()), ws.data_ptr<float>(), (int)N, (int)H, (int)W,
+      stream());
+  TORCH_CHECK(rc == 0, "pdt_stem_conv_wgrad_bn_pool failed: ", rc);
+  return dw;
+}
+
 // ----------------------------------------------------------------------------- cross entropy
 std::vector<Tensor> ce_fwd(Tensor logits, Tensor target, double smoothing, int64_t ignore_index) {
   check_cuda(logits, "logits");
@@ -1965,7 +1999,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("rab") = py::none(), py::arg("a_coef") = py::none());
   m.def("bn_bwd_train_tiles", &bn_bwd_train_tiles);
   m.def("maxpool3s2_bwd_bn", &maxpool3s2_bwd_bn);
-  m.def("maxpool3s2_bwd_bn_coef", &maxpool3s2_bwd_bn_coef);
+  m.def("maxpool3s2_bwd_bn_coef", &maxpool3s2_bwd_bn_coef, py::arg("dy"), py::arg("code"), py::arg("x"),
+        py::arg("weight"), py::arg("mean"), py::arg("invstd"), py::arg("need_dgamma"), py::arg("write_dz") = true);
   m.def("slice_sum", &slice_sum);
   m.def("subsample_gather", &subsample_gather);
   m.def("subsample_scatter_add", &subsample_scatter_add);
@@ -1984,6 +2019,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("stem_conv_fwd_stats", &stem_conv_fwd_stats);
   m.def("stem_conv_wgrad", &stem_conv_wgrad);
   m.def("stem_conv_wgrad_bn", &stem_conv_wgrad_bn);
+  m.def("stem_conv_wgrad_bn_pool", &stem_conv_wgrad_bn_pool);
   m.def("conv3x3s1_wgrad", &conv3x3s1_wgrad);
   m.def("conv1x1_wgrad", &conv1x1_wgrad);
   m.def("conv1x1_wgrad_tune", [](int target_wgs, int variant, int interleave) { pdt_conv1x1_wgrad_tune(target_wgs, variant, interleave); },

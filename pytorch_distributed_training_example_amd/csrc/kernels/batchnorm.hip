@@ -821,7 +821,7 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const uint16_t* __rest
     st.y = (uint32_t)f2bf(g[2]) | ((uint32_t)f2bf(g[3]) << 16);
     st.z = (uint32_t)f2bf(g[4]) | ((uint32_t)f2bf(g[5]) << 16);
     st.w = (uint32_t)f2bf(g[6]) | ((uint32_t)f2bf(g[7]) << 16);
-    *reinterpret_cast<uint4*>(dz + i * 8) = st;
+    if (dz) *reinterpret_cast<uint4*>(dz + i * 8) = st;  // null: the reduction only (its consumer re-forms dz)
     if constexpr (BNRED) bn_bwd_accum8(st, xv, 0xffu, mu, s1, s2);
    }
   }
@@ -912,7 +912,7 @@ __global__ __launch_bounds__(256) void maxpool_bwd2_kernel(const uint16_t* __res
       st.y = (uint32_t)f2bf(g[2]) | ((uint32_t)f2bf(g[3]) << 16);
       st.z = (uint32_t)f2bf(g[4]) | ((uint32_t)f2bf(g[5]) << 16);
       st.w = (uint32_t)f2bf(g[6]) | ((uint32_t)f2bf(g[7]) << 16);
-      *reinterpret_cast<uint4*>(dz + (((int64_t)n * H + ih) * W + iw) * C + c8 * 8) = st;
+      if (dz) *reinterpret_cast<uint4*>(dz + (((int64_t)n * H + ih) * W + iw) * C + c8 * 8) = st;  // null: sums only
       if constexpr (BNRED) bn_bwd_accum8(st, xv[t], 0xffu, mu, s1, s2);
     }
   }
@@ -1430,7 +1430,8 @@ int pdt_maxpool3s2_bwd_bn(const uint16_t* dy, const uint8_t* code, uint16_t* dz,
 }
 
 // Same, without the apply: dz and the dx coefficients coef [3][C] = A, B, D (dx = A dz + B (x - mean)
-// + D) for a consumer that applies them on load (the stem weight gradient).
+// + D) for a consumer that applies them on load (the stem weight gradient). dz = null: not written
+// (pdt_stem_conv_wgrad_bn_pool forms it again from dy and the codes).
 int pdt_maxpool3s2_bwd_bn_coef(const uint16_t* dy, const uint8_t* code, uint16_t* dz, int N, int H, int W, int C,
                                const uint16_t* x, const float* gamma, const float* mean, const float* invstd,
                                float* coef, float* dgamma, float* dbeta, float* part, float* ws, hipStream_t s) {

@@ -58,9 +58,11 @@ constexpr int halo_max(int S) { return S == 1 ? 256 : 320; }
 // (An LDS-DMA staging variant — global_load_lds into 1 or 2 LDS buffers, source-swizzled — measured
 // 5-11 % SLOWER than the register staging below on every ResNet-50 shape, e.g. 336 vs 302 us at
 // 28x28x128, 493 vs 445 us at 56x56x64: the loop is bound by LDS-read latency, not by staging VGPRs.)
-template <int CO_T_, bool PF_, int S_ = 1>
+// W2T: the halo row pitch W2 (padded pixels per image row) as a compile-time constant (0: runtime), so
+// the tap offsets kh * W2 * 128 are ds_read immediates instead of a VALU add per fragment read.
+template <int CO_T_, bool PF_, int S_ = 1, int W2T_ = 0>
 struct WCfg {
-  static constexpr int CO_T = CO_T_, CI_T = 64, S = S_;
+  static constexpr int CO_T = CO_T_, CI_T = 64, S = S_, W2T = W2T_;
   static constexpr int kHaloMax = halo_max(S), kKpMax = kp_max(S);
   static constexpr bool PF = PF_;      // register staging: next tile's loads under this tile's MFMAs
   static constexpr int kWaves = (CO_T / 32) * (CI_T / 32);
@@ -69,7 +71,7 @@ struct WCfg {
   static constexpr int kChY = CO_T / 8;                  // 16-B chunks per dY row
   static constexpr int kDyBytes = kKpMax * kRowY;
   static constexpr int kHaloBytes = kHaloMax * 128;
-  static constexpr int kLds = kDyBytes + kHaloBytes + kKpMax * 4;
+  static constexpr int kLds = kDyBytes + kHaloBytes + kKpMax * 16;  // table: int4 per pixel
   // prefetch registers (16-B pieces per thread), sized for the worst tile
   static constexpr int kPfY = kKpMax * kChY / kThreads;  // exact: writes never leave the buffers
   static constexpr int kPfX = kHaloMax * 8 / kThreads;
@@ -106,7 +108,7 @@ __global__ __launch_bounds__(Cf::kThreads, 2) void conv3x3_wgrad_kernel(const ui
   extern __shared__ __attribute__((aligned(16))) char lds[];
   char* const dys = lds;
   char* const hal = lds + Cf::kDyBytes;
-  int* const table = reinterpret_cast<int*>(lds + Cf::kDyBytes + Cf::kHaloBytes);
+  int4* const table = reinterpret_cast<int4*>(lds + Cf::kDyBytes + Cf::kHaloBytes);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   // halo rows of one padded image row: W + 2 rounded up to a multiple of 4, so the tap offset kh*W2
   // never changes a row's chunk swizzle (it depends on row bit 1); stride 2: two de-interleaved
@@ -114,7 +116,8 @@ __global__ __launch_bounds__(Cf::kThreads, 2) void conv3x3_wgrad_kernel(const ui
   constexpr int S = Cf::S;
   const int H = g.H, W = g.W, Hi = g.Hi, Wi = g.Wi;
   const int HALF = S == 1 ? 0 : ((Wi + 3) / 2 + 3) & ~3;
-  const int W2 = S == 1 ? (W + 2 + 3) & ~3 : 2 * HALF, H2 = Hi + 2;
+  const int W2r = S == 1 ? (W + 2 + 3) & ~3 : 2 * HALF, H2 = Hi + 2;
+  const int W2 = Cf::W2T ? Cf::W2T : W2r;  // launch checks W2T == W2r
   const int kwo1 = S == 1 ? 1 : HALF, kwo2 = S == 1 ? 2 : 1;  // row shift of taps kw = 1, 2
   const int nblk_ci = g.Ci / 64;
   // XCD-aware: consecutive logical ids (one split's channel blocks) on one XCD
@@ -162,6 +165,10 @@ __global__ __launch_bounds__(Cf::kThreads, 2) void conv3x3_wgrad_kernel(const ui
       pfx[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
     }
   };
+  // table[j]: for pixel j the halo byte offsets of its tap (0, kw) rows, kw = 0, 1, 2, with the row's
+  // XOR swizzle folded in (T(row) = row * 128 | (row & 2) << 5; a lane's read address is T ^ its chunk
+  // and half offset): 3 XORs per pixel set and k-step instead of ~5 VALU per swizzled row address
+  auto trow = [](int row) { return (row << 7) | ((row & 2) << 5); };
   auto write_table = [&]() {  // into `table` (the current buffer)
     for (int j = tid; j < KP; j += Cf::kThreads) {
       int hr = 0;  // pad pixels (dY rows are zero): any finite halo row
@@ -169,7 +176,7 @@ __global__ __launch_bounds__(Cf::kThreads, 2) void conv3x3_wgrad_kernel(const ui
         const int gg = pf_g0 + j / W, w = j % W;
         hr = ((gg / H) * H2 + S * (gg % H) - pf_prs) * W2 + w;  // tap (0, 0) of pixel j
       }
-      table[j] = hr;
+      table[j] = make_int4(trow(hr), trow(hr + kwo1), trow(hr + kwo2), 0);
     }
   };
   auto write_tile = [&]() {
@@ -224,31 +231,31 @@ __global__ __launch_bounds__(Cf::kThreads, 2) void conv3x3_wgrad_kernel(const ui
     // offset; B rows of tap (kh, kw) = (h + kw) + kh*W2 with W2 % 4 == 0: 3 swizzled bases per
     // pixel set and per k-step, the kh taps by adding kh*W2*128.
     auto addrY = [&](int row) { return chunk_off<Cf::kRowY>(row, ychunk) + half8; };
-    auto addrX = [&](int row) { return chunk_off<128>(row, xchunk) + half8; };
+    const int xl = (xchunk << 4) | half8;  // this lane's piece of a 128-B halo row, before the row swizzle
     const int khs = W2 * 128;
     auto rdA = [&](int r) {
       const char* p = dys + addrY(r);
       return cat2(tr_read(p), tr_read(p + 4 * Cf::kRowY));
     };
     int bx0[3], bx1[3];
-    auto bases = [&](int h0_, int h1_) {
-      bx0[0] = addrX(h0_);
-      bx1[0] = addrX(h1_);
-      bx0[1] = addrX(h0_ + kwo1);
-      bx1[1] = addrX(h1_ + kwo1);
-      bx0[2] = addrX(h0_ + kwo2);
-      bx1[2] = addrX(h1_ + kwo2);
+    auto bases = [&](int4 e0, int4 e1) {
+      bx0[0] = e0.x ^ xl;
+      bx1[0] = e1.x ^ xl;
+      bx0[1] = e0.y ^ xl;
+      bx1[1] = e1.y ^ xl;
+      bx0[2] = e0.z ^ xl;
+      bx1[2] = e1.z ^ xl;
     };
     auto rdB = [&](int, int, int t) {
       const int kh = t / 3, kw = t % 3;
-      return cat2(tr_read(hal + bx0[kw] + kh * khs), tr_read(hal + bx1[kw] + kh * khs));
+      const int ko = Cf::W2T ? kh * Cf::W2T * 128 : kh * khs;  // immediate when the pitch is compile-time
+      return cat2(tr_read(hal + bx0[kw] + ko), tr_read(hal + bx1[kw] + ko));
     };
     // cross-step pipelining: the next k-step's A fragment, table entries, swizzled bases and its
     // first three B fragments are read while this step's last MFMAs run
     int r0 = prow;
     bf16x8 a = rdA(r0);
-    int h0 = table[r0], h1 = table[r0 + 4];
-    bases(h0, h1);
+    bases(table[r0], table[r0 + 4]);
     bf16x8 bq0 = rdB(0, 0, 0), bq1 = rdB(0, 0, 1), bq2 = rdB(0, 0, 2);
     // (sched_barrier(0) pins the written order: LLVM's scheduler otherwise sinks each read to just
     // before its MFMA, which then waits out the whole LDS latency.)
@@ -265,7 +272,7 @@ __global__ __launch_bounds__(Cf::kThreads, 2) void conv3x3_wgrad_kernel(const ui
       PDT_PIN();
       PDT_MF(2, bq2);
       bq2 = rdB(0, 0, 5);
-      const int h0n = table[rn], h1n = table[rn + 4];
+      const int4 h0n = table[rn], h1n = table[rn + 4];
       PDT_PIN();
       PDT_MF(3, bq0);
       bq0 = rdB(0, 0, 6);
@@ -434,6 +441,23 @@ int launch(const uint16_t* x, const uint16_t* dy, uint16_t* dw, float* ws, const
   return 0;
 }
 
+// The halo row pitch of the shape as a compile-time constant where ResNet-50 / ResNet-18 at 224 x 224
+// need one (stride 1: W + 2 rounded up to 4 -> 60, 32, 16, 12; stride 2: 2 HALF -> 64, 32, 16); any other
+// pitch takes the runtime-pitch instantiation.
+template <int CO_T, bool PF, int S>
+int launch_pitch(const uint16_t* x, const uint16_t* dy, uint16_t* dw, float* ws, const Geo& g, hipStream_t s) {
+  const int half = ((g.Wi + 3) / 2 + 3) & ~3;
+  const int w2 = S == 1 ? (g.W + 2 + 3) & ~3 : 2 * half;
+  switch (w2) {
+    case 12: return launch<WCfg<CO_T, PF, S, 12>>(x, dy, dw, ws, g, s);
+    case 16: return launch<WCfg<CO_T, PF, S, 16>>(x, dy, dw, ws, g, s);
+    case 32: return launch<WCfg<CO_T, PF, S, 32>>(x, dy, dw, ws, g, s);
+    case 60: return launch<WCfg<CO_T, PF, S, 60>>(x, dy, dw, ws, g, s);
+    case 64: return launch<WCfg<CO_T, PF, S, 64>>(x, dy, dw, ws, g, s);
+    default: return launch<WCfg<CO_T, PF, S, 0>>(x, dy, dw, ws, g, s);
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -457,7 +481,7 @@ int pdt_conv3x3s1_wgrad(const uint16_t* x, const uint16_t* dy, uint16_t* dw, flo
   Geo g;
   const int co_t = co_tile_of(Co);
   if (!geo_of(N, H, W, Ci, Co, co_t, target_wgs(co_t), g)) return -4;
-  return co_t == 128 ? launch<WCfg<128, true>>(x, dy, dw, ws, g, s) : launch<WCfg<64, false>>(x, dy, dw, ws, g, s);
+  return co_t == 128 ? launch_pitch<128, true, 1>(x, dy, dw, ws, g, s) : launch_pitch<64, false, 1>(x, dy, dw, ws, g, s);
 }
 
 // Stride 2 / pad 1 (input x [N,H,W,Ci], dy [N,Ho,Wo,Co], Ho = (H-1)/2+1), Ci % 64 == 0, Co % 64 == 0.
@@ -481,7 +505,7 @@ int pdt_conv3x3s2_wgrad(const uint16_t* x, const uint16_t* dy, uint16_t* dw, flo
   Geo g;
   const int co_t = s2_co_tile(Co);
   if (!geo_of(N, (H - 1) / 2 + 1, (W - 1) / 2 + 1, Ci, Co, co_t, target_wgs(co_t), g, 2, H, W)) return -4;
-  return co_t == 128 ? launch<WCfg<128, true, 2>>(x, dy, dw, ws, g, s) : launch<WCfg<64, false, 2>>(x, dy, dw, ws, g, s);
+  return co_t == 128 ? launch_pitch<128, true, 2>(x, dy, dw, ws, g, s) : launch_pitch<64, false, 2>(x, dy, dw, ws, g, s);
 }
 
 void pdt_conv3x3_wgrad_probe(int probe) { g_probe = probe; }

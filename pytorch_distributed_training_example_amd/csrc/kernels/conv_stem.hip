@@ -340,6 +340,13 @@ __device__ __forceinline__ void dma16_opaque(const void* src, const char* lds_ds
   asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(m0) : "memory");
 }
 
+// The stem BatchNorm's backward apply dx = A dz + B (x - mean) + D, unfused (no contraction): the
+// dz-tile and pooled-gradient forms of the weight gradient evaluate it identically, bit for bit.
+__device__ __forceinline__ float bn_apply_dx(float a, float g, float b, float x, float m, float d) {
+#pragma clang fp contract(off)
+  return a * g + b * (x - m) + d;
+}
+
 typedef short s4v __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ bf16x8 tr8(const char* p0, const char* p1) {
   const s4v a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4v*)p0);
@@ -352,14 +359,21 @@ __device__ __forceinline__ bf16x8 tr8(const char* p0, const char* p1) {
 #ifndef PDT_STEM_WG_PROBE
 #define PDT_STEM_WG_PROBE 0  // diagnostics only: 1 = staging without compute, 2 = compute without staging
 #endif
-template <bool BNA>
+// POOL (with BNA): dY is the gradient at the MAX-POOL output [N, PH, PW, 64] with its winner codes
+// `pcode` (bn_apply_pool_kernel), not the pool's input gradient: each tile DMAs the two pooled rows its
+// two stem rows fall in (dy + codes, 21 KB in place of the 28 KB dz tile) and forms dz per position in
+// the apply pass with maxpool_bwd2_kernel's window order and bf16 rounding — so the stem's dz (1.6 GB
+// at 1024 images) is neither written by the pool gradient nor read back here.
+template <bool BNA, bool POOL = false>
 __global__ __launch_bounds__(kGThreads, 1) void stem_wgrad_kernel(const uint16_t* __restrict__ X,
                                                                   const uint16_t* __restrict__ dY,
                                                                   float* __restrict__ ws, int H, int W, int OH,
                                                                   int OW, int nrt, int ntiles,
                                                                   const uint16_t* __restrict__ Xb = nullptr,
                                                                   const float* __restrict__ coef = nullptr,
-                                                                  const float* __restrict__ mean = nullptr) {
+                                                                  const float* __restrict__ mean = nullptr,
+                                                                  const uint8_t* __restrict__ pcode = nullptr) {
+  static_assert(!POOL || BNA, "the pooled form is the fused BN apply's");
   extern __shared__ __attribute__((aligned(16))) char lds[];
   constexpr int kBuf = BNA ? kGBufB : kGBuf;
   float* const ctab = reinterpret_cast<float*>(lds + 2 * kGBufB);  // BNA: [A | B | D | mean][64]
@@ -389,16 +403,114 @@ __global__ __launch_bounds__(kGThreads, 1) void stem_wgrad_kernel(const uint16_t
       dma16_opaque(src, buf + q * 1024);
     }
   };
+  const int PH = (OH - 1) / 2 + 1, PW = (OW - 1) / 2 + 1;
+  // POOL: pooled rows a = oh0 / 2 and min(a + 1, PH - 1): dy at [0, 2 PW * 128), codes after it
+  auto dma_pooled = [&](int t, char* buf) {
+    const int n = t / nrt, a = (t - n * nrt) * kGRowsOut / 2;
+    const int a1 = min(a + 1, PH - 1);
+    const int npx = 2 * PW;
+    for (int q = wid; q < (npx + 7) / 8; q += 8) {  // dy: 8 pooled pixels (128 B each) per instruction
+      const int px = q * 8 + (lane >> 3), pos = lane & 7;
+      const int pr = px >= PW, pc = px - pr * PW;
+      const void* src = px < npx ? (const void*)(dY + ((int64_t)(n * PH + (pr ? a1 : a)) * PW + pc) * 64 + pos * 8)
+                                 : (const void*)g_stem_zero;
+      dma16_opaque(src, buf + q * 1024);
+    }
+    char* cbuf = buf + npx * 128;
+    for (int q = wid; q < (npx + 15) / 16; q += 8) {  // codes: 16 pooled pixels (64 B each) per instruction
+      const int px = q * 16 + (lane >> 2), pos = lane & 3;
+      const int pr = px >= PW, pc = px - pr * PW;
+      const void* src = px < npx ? (const void*)(pcode + ((int64_t)(n * PH + (pr ? a1 : a)) * PW + pc) * 64 + pos * 16)
+                                 : (const void*)g_stem_zero;
+      dma16_opaque(src, cbuf + q * 1024);
+    }
+  };
   auto dma_dy = [&](int t, char* buf) {
-    dma_tile(dY, t, buf);
+    if constexpr (POOL) dma_pooled(t, buf);
+    else dma_tile(dY, t, buf);
     if (BNA) dma_tile(Xb, t, buf + kGBuf);
   };
   // BNA: dz tile (buf) and BN input tile (buf + kGBuf), same swizzled layout -> dx in place of dz.
   // Thread: channel chunk tid % 8 (its 8 coefficients), rows tid / 8 + 64 u; LDS position of its
   // chunk in row r = chunk ^ swizzle(r). Rows past the tile's valid pixels stay zero.
+  // POOL: dz of tile pixel r (stem row oh0 + r / OW, column r % OW), channels cc*8 .. +7, from the pooled
+  // rows in LDS: windows (A + dr, B + ds) in maxpool_bwd2_kernel's order, rounded to bf16 as it writes dz
+  auto pooled_dz = [&](const char* buf, int oh0, int r, int cc, float (&g)[8]) {
+    const int ih = oh0 + r / OW, iw = r % OW;
+    const int A = ih >> 1, rr = ih & 1, B = iw >> 1, sc = iw & 1;
+    const int A1 = min(PH - 1, A + 1), B1 = min(PW - 1, B + 1);
+    const int a = oh0 >> 1;  // pooled row of LDS row 0
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int dr = q >> 1, ds = q & 1;
+      if ((dr && !rr) || (ds && !sc)) continue;
+      if ((dr && A1 == A) || (ds && B1 == B)) continue;
+      const int po = (dr ? A1 : A) - a, pc = ds ? B1 : B;
+      const uint32_t idx = (uint32_t)((dr ? 0 : rr + 1) * 3 + (ds ? 0 : sc + 1));
+      const uint4 dv = *reinterpret_cast<const uint4*>(buf + (po * PW + pc) * 128 + cc * 16);
+      const uint2 cw = *reinterpret_cast<const uint2*>(buf + 2 * PW * 128 + (po * PW + pc) * 64 + cc * 8);
+      const uint32_t w[4] = {dv.x, dv.y, dv.z, dv.w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float v = __uint_as_float(j & 1 ? (w[j >> 1] & 0xffff0000u) : (w[j >> 1] << 16));
+        const uint32_t cj = ((j < 4 ? cw.x : cw.y) >> (8 * (j & 3))) & 0xffu;
+        g[j] += cj == idx ? v : 0.f;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] = bf2f(f2bf(g[j]));
+  };
   auto bn_apply_tile = [&](int t, char* buf) {
     const int n = t / nrt, oh0 = (t - n * nrt) * kGRowsOut;
     const int vrows = min(kGRowsOut, OH - oh0) * OW;
+    if constexpr (POOL) {
+      // every thread's rows first (the pooled data lies where the results go), then one barrier
+      int tix;
+      asm volatile("v_mov_b32 %0, %1" : "=v"(tix) : "v"((int)threadIdx.x));
+      const int cc = tix & 7;
+      constexpr int kU = (kGMaxPx + 63) / 64;
+      uint4 res[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int r = (tix >> 3) + 64 * u;
+        float o[8];
+        if (r < vrows) {
+          float g[8], xf[8];
+          pooled_dz(buf, oh0, r, cc, g);
+          const char* px = buf + kGBuf + r * 128 + ((cc ^ (((r >> 1) & 3) << 1)) * 16);
+          ld8_bf16(reinterpret_cast<const uint16_t*>(px), xf);
+          // the dz-tile path's coefficient loads and formula (bn_apply_dx: bit-identical)
+          float av[8], bv[8], dv[8], mv[8];
+          const float4* ct = reinterpret_cast<const float4*>(ctab + cc * 8);
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const float4 a4 = ct[h], b4 = ct[16 + h], d4 = ct[32 + h], m4 = ct[48 + h];
+            av[4 * h] = a4.x; av[4 * h + 1] = a4.y; av[4 * h + 2] = a4.z; av[4 * h + 3] = a4.w;
+            bv[4 * h] = b4.x; bv[4 * h + 1] = b4.y; bv[4 * h + 2] = b4.z; bv[4 * h + 3] = b4.w;
+            dv[4 * h] = d4.x; dv[4 * h + 1] = d4.y; dv[4 * h + 2] = d4.z; dv[4 * h + 3] = d4.w;
+            mv[4 * h] = m4.x; mv[4 * h + 1] = m4.y; mv[4 * h + 2] = m4.z; mv[4 * h + 3] = m4.w;
+          }
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = bn_apply_dx(av[j], g[j], bv[j], xf[j], mv[j], dv[j]);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = 0.f;
+        }
+        res[u].x = (uint32_t)f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16);
+        res[u].y = (uint32_t)f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16);
+        res[u].z = (uint32_t)f2bf(o[4]) | ((uint32_t)f2bf(o[5]) << 16);
+        res[u].w = (uint32_t)f2bf(o[6]) | ((uint32_t)f2bf(o[7]) << 16);
+      }
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int r = (tix >> 3) + 64 * u;
+        if (r < P) *reinterpret_cast<uint4*>(buf + r * 128 + ((cc ^ (((r >> 1) & 3) << 1)) * 16)) = res[u];
+      }
+      return;
+    }
     // one row at a time, coefficients re-read from LDS per row, and the thread index passed through
     // an opaque move so its derived addresses are not hoisted out of the tile loop: this kernel's
     // compute phase already holds 256 VGPRs, so nothing of the apply may stay live across it
@@ -425,7 +537,7 @@ __global__ __launch_bounds__(kGThreads, 1) void stem_wgrad_kernel(const uint16_t
           mv[4 * h] = m4.x; mv[4 * h + 1] = m4.y; mv[4 * h + 2] = m4.z; mv[4 * h + 3] = m4.w;
         }
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = av[j] * g[j] + bv[j] * (xf[j] - mv[j]) + dv[j];
+        for (int j = 0; j < 8; ++j) o[j] = bn_apply_dx(av[j], g[j], bv[j], xf[j], mv[j], dv[j]);
       } else {
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] = 0.f;
@@ -686,20 +798,27 @@ extern "C" int64_t pdt_stem_wgrad_ws_floats() { return (int64_t)stem_ncu() * 64 
 
 namespace {
 int stem_wgrad_launch(const uint16_t* x, const uint16_t* dy, const uint16_t* xb, const float* coef, const float* mean,
-                      uint16_t* dw, float* ws, int N, int H, int W, hipStream_t s) {
+                      uint16_t* dw, float* ws, int N, int H, int W, hipStream_t s, const uint8_t* pcode = nullptr) {
   if (N < 1 || H < 1 || W < 32 || W % 32 != 0 || W > 2 * kTW) return -1;
   const int OH = (H - 1) / 2 + 1, OW = W / 2;
   static const bool attr_ok =
       hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_wgrad_kernel<false>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, kGLds) == hipSuccess &&
       hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_wgrad_kernel<true>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, kGLdsB) == hipSuccess &&
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_wgrad_kernel<true, true>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, kGLdsB) == hipSuccess;
   if (!attr_ok) return -2;
   const int nrt = (OH + kGRowsOut - 1) / kGRowsOut;
   const int64_t ntiles = (int64_t)N * nrt;
   if (ntiles > 0x7fffffff || (int64_t)N * OH * OW * 64 > 0x7fffffffLL * 4) return -3;
   const int grid = (int)std::min<int64_t>(ntiles, stem_ncu());
-  if (xb)
+  // (POOL: the two pooled rows of a tile, dy + codes = 2 PW x 192 B, fit the 28 KB dz-tile space)
+  static_assert(2 * ((kTW + 1) / 2) * 192 <= kGDy, "pooled rows in the dz tile's space");
+  if (xb && pcode)
+    hipLaunchKernelGGL((stem_wgrad_kernel<true, true>), dim3(grid), dim3(kGThreads), kGLdsB, s, x, dy, ws, H, W, OH,
+                       OW, nrt, (int)ntiles, xb, coef, mean, pcode);
+  else if (xb)
     hipLaunchKernelGGL(stem_wgrad_kernel<true>, dim3(grid), dim3(kGThreads), kGLdsB, s, x, dy, ws, H, W, OH, OW, nrt,
                        (int)ntiles, xb, coef, mean);
   else
@@ -724,4 +843,14 @@ extern "C" int pdt_stem_conv_wgrad_bn(const uint16_t* x, const uint16_t* dz, con
                                       const float* mean, uint16_t* dw, float* ws, int N, int H, int W, hipStream_t s) {
   if (!xb || !coef || !mean) return -1;
   return stem_wgrad_launch(x, dz, xb, coef, mean, dw, ws, N, H, W, s);
+}
+
+// Same from the gradient at the MAX-POOL output: dyp [N, 64, PH, PW] and the pool's winner codes
+// (bn_apply_pool_kernel, 1 byte per (pooled position, channel)); the pool's input gradient dz is formed
+// per tile in LDS (pdt_maxpool3s2_bwd_bn_coef with dz = null gives coef without writing it).
+extern "C" int pdt_stem_conv_wgrad_bn_pool(const uint16_t* x, const uint16_t* dyp, const uint8_t* code,
+                                           const uint16_t* xb, const float* coef, const float* mean, uint16_t* dw,
+                                           float* ws, int N, int H, int W, hipStream_t s) {
+  if (!xb || !coef || !mean || !code) return -1;
+  return stem_wgrad_launch(x, dyp, xb, coef, mean, dw, ws, N, H, W, s, code);
 }

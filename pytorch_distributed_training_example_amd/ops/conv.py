@@ -817,6 +817,10 @@ class _StemBlockFn(torch.autograd.Function):
             dimg = torch.ops.aten.convolution_backward(*args, [True, False, False])[0]
             if ctx.needs_input_grad[1]:
                 dw = n.stem_conv_wgrad(img, dx)
+        elif SW.stem_pool_wgrad and ctx.needs_input_grad[1]:
+            # the pool gradient's BN reduction only (no dz written); the weight gradient re-forms dz per tile
+            _, coef, dg, db = n.maxpool3s2_bwd_bn_coef(dy, code, xb, gamma, mean, invstd, need_bn, False)
+            dw = n.stem_conv_wgrad_bn_pool(img, dy, code, xb, coef, mean)
         else:
             dz, coef, dg, db = n.maxpool3s2_bwd_bn_coef(dy, code, xb, gamma, mean, invstd, need_bn)
             if ctx.needs_input_grad[1]:

@@ -125,8 +125,9 @@ def test_resnet_bottleneck_uses_fused_stats(monkeypatch, switch):
                                    (4, 64, 64, 14, 14), (3, 64, 64, 13, 11), (32, 64, 64, 56, 56)])
 def test_conv3x3_stats_epilogue(shape):
     """The 3x3 statistics epilogue (halo kernel; 64 -> 64: the weight-stationary kernel, whose waves
-    merge four 64-row chunks per tile — ragged last tile, and > 1 tile per persistent workgroup at
-    32 x 56 x 56): same y as the plain launch, per-tile partials match an fp32 recomputation from y."""
+    merge four 64-row chunks per tile — ragged last tile; at 32 x 56 x 56 the row-tile kernel with
+    224-row tiles, > 1 tile per persistent workgroup): same y as the plain launch, per-tile partials
+    match an fp32 recomputation from y."""
     N, Ci, Co, H, W = shape
     torch.manual_seed(0)
     x = torch.randn(N, Ci, H, W, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
@@ -137,9 +138,11 @@ def test_conv3x3_stats_epilogue(shape):
     assert len(r) == 2
     part = r[1]
     M = N * H * W
-    T = (M + 255) // 256
+    T = part.shape[1]
+    BMt = 224 if (M % 224 == 0 and T == M // 224 and T != (M + 255) // 256) else 256  # row tiles: 224
+    assert T == (M + BMt - 1) // BMt
     y2 = r[0].permute(0, 2, 3, 1).reshape(M, Co).float()
-    yf = torch.cat([y2, torch.full((T * 256 - M, Co), float("nan"), device="cuda")]).view(T, 256, Co)
+    yf = torch.cat([y2, torch.full((T * BMt - M, Co), float("nan"), device="cuda")]).view(T, BMt, Co)
     valid = ~torch.isnan(yf)
     s = torch.where(valid, yf, 0).sum(1)
     mu = s / valid.sum(1).float()
