@@ -54,6 +54,9 @@ PDT_BN_APPLY_GEMM_K         64           a BatchNorm(+residual)+ReLU apply after
                                          (profiles/r4/ab_bn_apply_gemm.md)
 PDT_LINEAR_EPILOGUE         0            1: Linear forward GEMMs (+bias, MLP fc1+bias+GELU) on our MFMA kernel
                                          (gemm.hip; 0.61-0.94x of tuned hipBLASLt, so off)
+PDT_FP8_FUSED_GELU          1            fp8 MLPs: bias+GELU (and its backward) emit e4m3 + transpose directly
+                                         (fp8.hip fp8_gelu_cast_kernel): no bf16 activation, no cast pass
+PDT_FP8_WEIGHT_MULTI        1            fp8: every Linear weight cast in one launch per forward (fp8_cast_multi)
 """
 from __future__ import annotations
 
@@ -65,7 +68,8 @@ class _Switches:
                  "conv1x1_table", "conv1x1_dump", "conv1x1_s2", "conv3x3", "conv3x3_wgrad", "conv3x3_s2", "conv_stem",
                  "conv_bn_stats", "bn_bwd_stats", "res_masked", "stem_bwd_fused", "stem_bn_wgrad", "stem_bn_stats", "stem_pool_wgrad", "wgrad_splitk", "slice_sum",
                  "subsample_native", "linear_splitk", "fused_addln", "embedding_native", "linear_epilogue",
-                 "bwd_fused", "bwd_fused_shapes", "bn2_defer", "bn_apply_gemm_k", "strided_bstats", "gap_native")
+                 "bwd_fused", "bwd_fused_shapes", "bn2_defer", "bn_apply_gemm_k", "strided_bstats", "gap_native",
+                 "fp8_fused_gelu", "fp8_weight_multi")
 
     def __init__(self):
         self.reload()
@@ -114,6 +118,8 @@ class _Switches:
         self.bn_apply_gemm_k = int(e("PDT_BN_APPLY_GEMM_K", "64"))
         self.strided_bstats = on("PDT_STRIDED_BSTATS")
         self.gap_native = on("PDT_GAP_NATIVE")
+        self.fp8_fused_gelu = on("PDT_FP8_FUSED_GELU")
+        self.fp8_weight_multi = on("PDT_FP8_WEIGHT_MULTI")
         return self
 
 

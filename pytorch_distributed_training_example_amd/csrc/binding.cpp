@@ -181,6 +181,12 @@ int pdt_bn_fwd_train_tiles(const float* part, int T, int BMt, const uint16_t* x,
 int pdt_fp8_cast_transpose(const uint16_t* x, int64_t M, int64_t K, const float* scale, uint8_t* out,
                            uint8_t* out_t, float* amax, hipStream_t s);
 int pdt_fp8_update_scales(float* state, int n, int L, float margin_scale, hipStream_t s);
+int64_t pdt_fp8_gelu_cast_workspace_floats(int64_t M, int D);
+int pdt_fp8_gelu_cast(const uint16_t* h, const uint16_t* dg, const float* bias, int64_t M, int D, int tanh_form,
+                      const float* scale, uint8_t* out, uint8_t* out_t, float* amax, float* part, hipStream_t s);
+int pdt_fp8_cast_multi(int n, const uint16_t* const* x, const int* M, const int* K, float* const* st,
+                       uint8_t* const* out, uint8_t* const* out_t, hipStream_t s);
+int pdt_colsum_finalize(const float* part, int nblk, int D, void* out, int odtype, hipStream_t s);
 int pdt_embedding_fwd(const int64_t* idx, const uint16_t* wte, const uint16_t* wpe, uint16_t* out, int64_t n, int T,
                       int D, int V, int* err, hipStream_t s);
 int64_t pdt_embedding_bwd_ws_ints(int64_t n, int V);
@@ -1679,6 +1685,83 @@ std::vector<Tensor> fp8_cast_transpose(Tensor x, Tensor state_row, bool transpos
   return {out, out_t};
 }
 
+// The MLP activation straight to fp8 (fp8.hip fp8_gelu_cast_kernel). h: bf16 [M, D] (fc1 output
+// without bias), bias: fp32 [D] or none. Forward (dg undefined): {fp8(gelu(h + bias)), its
+// transpose}. Backward: {fp8(dg * gelu'(h + bias)), its transpose, bias gradient in db_dtype (or
+// undefined without bias)}. state_row as fp8_cast_transpose.
+std::vector<Tensor> fp8_gelu_cast(Tensor h, c10::optional<Tensor> dg, c10::optional<Tensor> bias, Tensor state_row,
+                                  bool tanh_form, at::ScalarType db_dtype) {
+  check_cuda(h, "h");
+  TORCH_CHECK(h.scalar_type() == at::kBFloat16 && h.dim() == 2 && h.is_contiguous(), "fp8_gelu_cast: bf16 [M, D] h");
+  TORCH_CHECK(state_row.scalar_type() == at::kFloat && state_row.numel() >= 3 && state_row.is_contiguous(),
+              "fp8_gelu_cast: fp32 state row");
+  const int64_t M = h.size(0), D = h.size(1);
+  TORCH_CHECK(M % 16 == 0 && D % 64 == 0 && M > 0, "fp8_gelu_cast: M % 16 == 0 and D % 64 == 0");
+  const bool bwd = dg.has_value() && dg->defined();
+  if (bwd)
+    TORCH_CHECK(dg->scalar_type() == at::kBFloat16 && dg->sizes() == h.sizes() && dg->is_contiguous(),
+                "fp8_gelu_cast: dg like h");
+  const bool hb = bias.has_value() && bias->defined();
+  if (hb)
+    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->is_contiguous() && bias->numel() == D,
+                "fp8_gelu_cast: fp32 bias [D]");
+  auto o8 = h.options().dtype(at::kFloat8_e4m3fn);
+  auto out = at::empty({M, D}, o8), out_t = at::empty({D, M}, o8);
+  Tensor part, db;
+  if (bwd) part = at::empty({pdt_fp8_gelu_cast_workspace_floats(M, (int)D)}, h.options().dtype(at::kFloat));
+  float* st = state_row.data_ptr<float>();
+  const int nchunk = pdt_fp8_gelu_cast(reinterpret_cast<const uint16_t*>(h.data_ptr()),
+                                       bwd ? reinterpret_cast<const uint16_t*>(dg->data_ptr()) : nullptr,
+                                       hb ? bias->data_ptr<float>() : nullptr, M, (int)D, tanh_form, st + 1,
+                                       reinterpret_cast<uint8_t*>(out.data_ptr()),
+                                       reinterpret_cast<uint8_t*>(out_t.data_ptr()), st,
+                                       bwd ? part.data_ptr<float>() : nullptr, stream());
+  TORCH_CHECK(nchunk > 0, "pdt_fp8_gelu_cast failed: ", nchunk);
+  if (bwd && hb) {
+    TORCH_CHECK(db_dtype == at::kFloat || db_dtype == at::kBFloat16, "fp8_gelu_cast: db dtype fp32 / bf16");
+    db = at::empty({D}, h.options().dtype(db_dtype));
+    pdt_colsum_finalize(part.data_ptr<float>(), nchunk, (int)D, db.data_ptr(), db_dtype == at::kFloat ? 0 : 1,
+                        stream());
+  }
+  return {out, out_t, db};
+}
+
+// Every tensor of xs (bf16 [M_i, K_i] contiguous) cast with its state row in one launch (<= 64 per
+// launch): returns [q_0, qt_0, q_1, qt_1, ...].
+std::vector<Tensor> fp8_cast_multi(std::vector<Tensor> xs, std::vector<Tensor> rows) {
+  TORCH_CHECK(xs.size() == rows.size(), "fp8_cast_multi: one state row per tensor");
+  std::vector<Tensor> res;
+  res.reserve(2 * xs.size());
+  for (size_t base = 0; base < xs.size(); base += 64) {
+    const int n = (int)std::min<size_t>(64, xs.size() - base);
+    std::vector<const uint16_t*> px(n);
+    std::vector<int> pm(n), pk(n);
+    std::vector<float*> ps(n);
+    std::vector<uint8_t*> po(n), pt(n);
+    for (int i = 0; i < n; ++i) {
+      const Tensor& x = xs[base + i];
+      const Tensor& r = rows[base + i];
+      check_cuda(x, "x");
+      TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.dim() == 2 && x.is_contiguous(), "fp8_cast_multi: bf16 [M, K]");
+      TORCH_CHECK(r.scalar_type() == at::kFloat && r.numel() >= 3 && r.is_contiguous(), "fp8_cast_multi: state row");
+      const int64_t M = x.size(0), K = x.size(1);
+      TORCH_CHECK(M % 16 == 0 && K % 16 == 0 && M > 0 && M * K < ((int64_t)1 << 31), "fp8_cast_multi: shape");
+      auto o8 = x.options().dtype(at::kFloat8_e4m3fn);
+      res.push_back(at::empty({M, K}, o8));
+      res.push_back(at::empty({K, M}, o8));
+      px[i] = reinterpret_cast<const uint16_t*>(x.data_ptr());
+      pm[i] = (int)M;
+      pk[i] = (int)K;
+      ps[i] = r.data_ptr<float>();
+      po[i] = reinterpret_cast<uint8_t*>(res[res.size() - 2].data_ptr());
+      pt[i] = reinterpret_cast<uint8_t*>(res.back().data_ptr());
+    }
+    const int rc = pdt_fp8_cast_multi(n, px.data(), pm.data(), pk.data(), ps.data(), po.data(), pt.data(), stream());
+    TORCH_CHECK(rc == 0, "pdt_fp8_cast_multi failed: ", rc);
+  }
+  return res;
+}
+
 void fp8_update_scales(Tensor state, int64_t history, double margin) {
   check_cuda(state, "state");
   TORCH_CHECK(state.scalar_type() == at::kFloat && state.is_contiguous() && state.dim() == 2 &&
@@ -2054,6 +2137,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("capacity", &P2PComm::capacity);
   m.def("fp8_cast_transpose", &fp8_cast_transpose);
   m.def("fp8_update_scales", &fp8_update_scales);
+  m.def("fp8_gelu_cast", &fp8_gelu_cast, py::arg("h"), py::arg("dg") = py::none(), py::arg("bias") = py::none(),
+        py::arg("state_row"), py::arg("tanh_form") = false, py::arg("db_dtype") = at::kFloat);
+  m.def("fp8_cast_multi", &fp8_cast_multi);
   m.def("lenet_stem_fwd", &lenet_stem_fwd);
   m.def("lenet_stem_bwd", &lenet_stem_bwd);
   m.def("leaky_pool_fwd", &leaky_pool_fwd);

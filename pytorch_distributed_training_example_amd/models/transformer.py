@@ -20,6 +20,7 @@ from torch import nn
 
 from ..config import SW
 from ..ops.attention import attention_qkv
+from ..ops.fp8 import fp8_mlp
 from ..ops.gelu import bias_gelu
 from ..ops.layernorm import LayerNorm, add_layer_norm
 from ..ops.linear import linear as _linear
@@ -60,7 +61,11 @@ class MLP(nn.Module):
         self.approximate = approximate
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        if getattr(self.c_fc, "_fp8", None) is None:
+        if getattr(self.c_fc, "_fp8", None) is not None:
+            y = fp8_mlp(x, self.c_fc, self.c_proj, self.approximate)
+            if y is not None:
+                return y
+        else:
             g = linear_gelu(x, self.c_fc.weight, self.c_fc.bias, self.approximate)  # PDT_LINEAR_EPILOGUE=1
             if g is not None:
                 return linear(g, self.c_proj)

@@ -25,6 +25,7 @@ from typing import Optional
 import torch
 from torch import nn
 
+from ..config import SW
 from ._native import native, use_native
 
 
@@ -51,17 +52,37 @@ class Fp8State(nn.Module):
         if self.state.is_cuda:
             native().fp8_update_scales(self.state, self.history, self.margin)
 
+    @torch.no_grad()
+    def cast_weights(self, lins) -> None:
+        """fp8 copies (row-major + transposed) of every tagged Linear's weight in ONE launch
+        (``fp8_cast_multi``), cached for this forward: the per-Linear cast launches are gone."""
+        self.wcache = {}
+        ws = [m.weight for m in lins if fp8_ok_weight(m.weight)]
+        if not ws or not ws[0].is_cuda:
+            return
+        rows = [self.state[m._fp8[1] + 1] for m in lins if fp8_ok_weight(m.weight)]
+        out = native().fp8_cast_multi(ws, rows)
+        for i, w in enumerate(ws):
+            self.wcache[id(w)] = (w, out[2 * i], out[2 * i + 1])
+
+    def weight_fp8(self, w: torch.Tensor, slot: int):
+        """(wq, wqt) of ``w``: this forward's cached cast, or a cast now (eval / untagged calls)."""
+        e = self.wcache.get(id(w)) if getattr(self, "wcache", None) else None
+        if e is not None and e[0] is w:
+            return e[1], e[2]
+        return native().fp8_cast_transpose(w, self.state[slot + 1], True)
+
 
 class _Fp8LinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, state, slot):
+    def forward(ctx, x, w, b, state, slot, st=None):
         C = native()
         K = x.shape[-1]
         x2 = x.reshape(-1, K)
         if not x2.is_contiguous():
             x2 = x2.contiguous()
         xq, xqt = C.fp8_cast_transpose(x2, state[slot], True)
-        wq, wqt = C.fp8_cast_transpose(w, state[slot + 1], True)
+        wq, wqt = st.weight_fp8(w, slot) if st is not None else C.fp8_cast_transpose(w, state[slot + 1], True)
         y = torch._scaled_mm(xq, wq.t(), scale_a=state[slot, 2], scale_b=state[slot + 1, 2], bias=b,
                              out_dtype=torch.bfloat16)
         ctx.save_for_backward(xqt, wqt, state)
@@ -87,7 +108,12 @@ class _Fp8LinearFn(torch.autograd.Function):
                                   out_dtype=torch.bfloat16)
         if ctx.has_b and ctx.needs_input_grad[2]:
             db = C.colsum(dy2, torch.bfloat16)
-        return dx, dw, db, None, None
+        return dx, dw, db, None, None, None
+
+
+def fp8_ok_weight(w: torch.Tensor) -> bool:
+    return (w.dim() == 2 and w.dtype == torch.bfloat16 and w.is_contiguous() and w.shape[0] % 16 == 0
+            and w.shape[1] % 16 == 0)
 
 
 def fp8_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
@@ -99,8 +125,75 @@ def fp8_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
 def fp8_linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor], state: Fp8State,
                slot: int) -> torch.Tensor:
     if fp8_ok(x, weight):
-        return _Fp8LinearFn.apply(x, weight, bias, state.state, slot)
+        return _Fp8LinearFn.apply(x, weight, bias, state.state, slot, state)
     return torch.nn.functional.linear(x, weight, bias)
+
+
+class _Fp8MlpFn(torch.autograd.Function):
+    """fc1 -> bias + GELU -> fc2 with the activation produced in fp8 where it is computed:
+    ``fp8_gelu_cast`` turns fc1's bf16 output h into gelu(h + b1) as e4m3 (+ transpose) in one
+    pass, and its backward form turns (dg, h) into dh = dg gelu'(h + b1) as e4m3 (+ transpose,
+    + the b1 gradient). The bf16 activation and its gradient are never written (unfused: a strip
+    kernel writing them + a cast-transpose reading them back, twice per block)."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, state, s1, s2, st, tanh_form):
+        C = native()
+        D = x.shape[-1]
+        x2 = x.reshape(-1, D)
+        if not x2.is_contiguous():
+            x2 = x2.contiguous()
+        xq, xqt = C.fp8_cast_transpose(x2, state[s1], True)
+        w1q, w1qt = st.weight_fp8(w1, s1)
+        h = torch._scaled_mm(xq, w1q.t(), scale_a=state[s1, 2], scale_b=state[s1 + 1, 2], out_dtype=torch.bfloat16)
+        b1f = None if b1 is None else b1.float()
+        gq, gqt, _ = C.fp8_gelu_cast(h, None, b1f, state[s2], tanh_form)
+        w2q, w2qt = st.weight_fp8(w2, s2)
+        y = torch._scaled_mm(gq, w2q.t(), scale_a=state[s2, 2], scale_b=state[s2 + 1, 2], bias=b2,
+                             out_dtype=torch.bfloat16)
+        ctx.save_for_backward(xqt, w1qt, h, gqt, w2qt, b1f, state)
+        ctx.s1, ctx.s2, ctx.tanh_form, ctx.xshape = s1, s2, tanh_form, x.shape
+        ctx.b1_dtype = None if b1 is None else b1.dtype
+        ctx.has_b2 = b2 is not None
+        return y.reshape(*x.shape[:-1], w2.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        xqt, w1qt, h, gqt, w2qt, b1f, state = ctx.saved_tensors
+        s1, s2 = ctx.s1, ctx.s2
+        C = native()
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        if not dy2.is_contiguous():
+            dy2 = dy2.contiguous()
+        dyq, dyqt = C.fp8_cast_transpose(dy2, state[s2 + 2], True)
+        dg = torch._scaled_mm(dyq, w2qt.t(), scale_a=state[s2 + 2, 2], scale_b=state[s2 + 1, 2],
+                              out_dtype=torch.bfloat16)
+        dw2 = torch._scaled_mm(dyqt, gqt.t(), scale_a=state[s2 + 2, 2], scale_b=state[s2, 2], out_dtype=torch.bfloat16)
+        db2 = C.colsum(dy2, torch.bfloat16) if ctx.has_b2 else None
+        dbt = ctx.b1_dtype if ctx.b1_dtype in (torch.float32, torch.bfloat16) else torch.float32
+        dhq, dhqt, db1 = C.fp8_gelu_cast(h, dg, b1f, state[s1 + 2], ctx.tanh_form, dbt)
+        dx = torch._scaled_mm(dhq, w1qt.t(), scale_a=state[s1 + 2, 2], scale_b=state[s1 + 1, 2],
+                              out_dtype=torch.bfloat16).reshape(ctx.xshape)
+        dw1 = torch._scaled_mm(dhqt, xqt.t(), scale_a=state[s1 + 2, 2], scale_b=state[s1, 2], out_dtype=torch.bfloat16)
+        if db1 is not None and ctx.b1_dtype is not None and db1.dtype != ctx.b1_dtype:
+            db1 = db1.to(ctx.b1_dtype)
+        return dx, dw1, db1, dw2, db2, None, None, None, None, None
+
+
+def fp8_mlp(x: torch.Tensor, fc1: nn.Linear, fc2: nn.Linear, approximate: str) -> Optional[torch.Tensor]:
+    """The MLP on fp8 with the fused GELU casts, or None when a shape / dtype is not served (the
+    caller then runs the per-Linear path)."""
+    a, b = getattr(fc1, "_fp8", None), getattr(fc2, "_fp8", None)
+    if a is None or b is None or a[0] is not b[0] or not SW.fp8_fused_gelu:
+        return None
+    m = x.numel() // max(x.shape[-1], 1)
+    if not (fp8_ok(x, fc1.weight) and fc2.weight.dtype == torch.bfloat16 and fc1.weight.shape[0] % 64 == 0
+            and fc2.weight.shape[0] % 16 == 0 and fc1.weight.is_contiguous() and fc2.weight.is_contiguous()
+            and m % 16 == 0 and (fc1.bias is None or fc1.bias.dtype in (torch.float32, torch.bfloat16))):
+        return None
+    st = a[0]
+    return _Fp8MlpFn.apply(x, fc1.weight, fc1.bias, fc2.weight, fc2.bias, st.state, a[1], b[1], st,
+                           approximate == "tanh")
 
 
 def enable_fp8(model: nn.Module, history: int = 16, margin: float = 0.0, blocks_only: bool = True) -> Fp8State:
@@ -122,5 +215,9 @@ def enable_fp8(model: nn.Module, history: int = 16, margin: float = 0.0, blocks_
     def _refresh(mod, args):
         if mod.training:
             state.update()
+            if SW.fp8_weight_multi:
+                state.cast_weights(lins)
+        else:
+            state.wcache = {}
     model._fp8_hook = model.register_forward_pre_hook(_refresh)
     return state

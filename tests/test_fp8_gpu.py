@@ -77,3 +77,110 @@ def test_vit_tiny_fp8_trains():
         losses.append(float(loss))
     assert all(torch.isfinite(torch.tensor(losses)))
     assert losses[-1] < 0.5 * losses[0], losses
+
+
+def _st(scale):
+    st = torch.zeros(3 + 4, device="cuda")
+    st[1], st[2] = scale, 1.0 / scale
+    return st
+
+
+@pytest.mark.parametrize("m,d,tanh_form", [(25216, 3072, False), (8192, 4096, True), (48, 192, False)])
+def test_gelu_cast_fwd_bit_identical_to_unfused(m, d, tanh_form):
+    """fp8(gelu(h + b)) and its transpose in one pass == bias+GELU strip kernel then cast-transpose."""
+    from pytorch_distributed_training_example_amd.ops._native import native
+    C = native()
+    torch.manual_seed(1)
+    h = (torch.randn(m, d, device="cuda") * 2).bfloat16()
+    b = torch.randn(d, device="cuda") * 0.5
+    st_ref, st = _st(64.0), _st(64.0)
+    g = C.bias_gelu_fwd(h, b, tanh_form)
+    q_ref, qt_ref = C.fp8_cast_transpose(g, st_ref, True)
+    q, qt, db = C.fp8_gelu_cast(h, None, b, st, tanh_form)
+    assert db is None
+    assert torch.equal(q.view(torch.uint8), q_ref.view(torch.uint8))
+    assert torch.equal(qt.view(torch.uint8), qt_ref.view(torch.uint8))
+    assert st[0].item() == st_ref[0].item() == g.float().abs().max().item()
+
+
+@pytest.mark.parametrize("m,d,tanh_form", [(25216, 3072, False), (8192, 4096, True), (48, 192, False)])
+def test_gelu_cast_bwd_bit_identical_to_unfused(m, d, tanh_form):
+    """fp8(dg * gelu'(h + b)) (+ transpose) == GELU-backward strip kernel then cast-transpose; the
+    bias gradient against the strip kernel's and an fp32 reference."""
+    from pytorch_distributed_training_example_amd.ops._native import native
+    C = native()
+    torch.manual_seed(2)
+    h = (torch.randn(m, d, device="cuda") * 2).bfloat16()
+    dg = torch.randn(m, d, device="cuda").bfloat16()
+    b = torch.randn(d, device="cuda") * 0.5
+    st_ref, st = _st(32.0), _st(32.0)
+    dh, db_ref = C.bias_gelu_bwd(dg, h, b, tanh_form)
+    q_ref, qt_ref = C.fp8_cast_transpose(dh, st_ref, True)
+    q, qt, db = C.fp8_gelu_cast(h, dg, b, st, tanh_form, torch.float32)
+    assert torch.equal(q.view(torch.uint8), q_ref.view(torch.uint8))
+    assert torch.equal(qt.view(torch.uint8), qt_ref.view(torch.uint8))
+    assert st[0].item() == st_ref[0].item()
+    torch.testing.assert_close(db, db_ref, rtol=1e-4, atol=1e-3)
+    hf = (h.float() + b).requires_grad_(True)
+    torch.nn.functional.gelu(hf, approximate="tanh" if tanh_form else "none").backward(dg.float())
+    ref = hf.grad.sum(0)
+    assert ((db - ref).norm() / ref.norm()).item() < 1e-4
+
+
+def test_cast_multi_matches_per_tensor():
+    from pytorch_distributed_training_example_amd.ops._native import native
+    C = native()
+    torch.manual_seed(3)
+    shapes = [(2304, 768), (768, 768), (3072, 768), (768, 3072), (16, 48), (4096, 1024)] * 12  # > 64: two launches
+    xs = [(torch.randn(*s, device="cuda") * 0.05).bfloat16() for s in shapes]
+    rows = [_st(1024.0 + i) for i in range(len(xs))]
+    rows_ref = [_st(1024.0 + i) for i in range(len(xs))]
+    out = C.fp8_cast_multi(xs, rows)
+    for i, x in enumerate(xs):
+        q, qt = C.fp8_cast_transpose(x, rows_ref[i], True)
+        assert torch.equal(out[2 * i].view(torch.uint8), q.view(torch.uint8)), i
+        assert torch.equal(out[2 * i + 1].view(torch.uint8), qt.view(torch.uint8)), i
+        assert rows[i][0].item() == rows_ref[i][0].item(), i
+
+
+@pytest.mark.parametrize("approximate", ["none", "tanh"])
+def test_fp8_mlp_fused_matches_per_linear_path(approximate):
+    """The fused fp8 MLP (GELU casts + one-launch weight casts) against the per-Linear fp8 path: the
+    same fp8 operands, so every output and gradient is bit-identical except fc1's bias gradient
+    (summation order)."""
+    from pytorch_distributed_training_example_amd.config import SW
+    from pytorch_distributed_training_example_amd.models.transformer import MLP
+    from pytorch_distributed_training_example_amd.ops.fp8 import enable_fp8
+    torch.manual_seed(4)
+    mlp = MLP(768, 3072, approximate).cuda().bfloat16()
+
+    class Wrap(torch.nn.Module):  # enable_fp8 tags Linears inside transformer Blocks; tag all here
+        def __init__(self):
+            super().__init__()
+            self.mlp = mlp
+
+        def forward(self, x):
+            return self.mlp(x)
+    wrap = Wrap()
+    x0 = torch.randn(16, 197, 768, device="cuda").bfloat16()
+    g = torch.randn(16, 197, 768, device="cuda").bfloat16()
+    res = {}
+    saved = (SW.fp8_fused_gelu, SW.fp8_weight_multi)
+    try:
+        for fused in (False, True):
+            SW.fp8_fused_gelu = SW.fp8_weight_multi = fused
+            st = enable_fp8(wrap, history=4, blocks_only=False)
+            for _ in range(2):  # calibrate the delayed scales, then measure
+                mlp.zero_grad(set_to_none=True)
+                x = x0.clone().requires_grad_(True)
+                y = wrap(x)
+                y.backward(g)
+            res[fused] = [y, x.grad, mlp.c_fc.weight.grad, mlp.c_fc.bias.grad, mlp.c_proj.weight.grad,
+                          mlp.c_proj.bias.grad, st.state.clone()]
+            wrap._fp8_hook.remove()
+    finally:
+        SW.fp8_fused_gelu, SW.fp8_weight_multi = saved
+    a, b = res[False], res[True]
+    for i in (0, 1, 2, 4, 5, 6):
+        assert torch.equal(a[i], b[i]), i
+    torch.testing.assert_close(a[3].float(), b[3].float(), rtol=2e-2, atol=1e-2)
