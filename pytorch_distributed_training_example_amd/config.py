@@ -57,6 +57,9 @@ PDT_LINEAR_EPILOGUE         0            1: Linear forward GEMMs (+bias, MLP fc1
 PDT_FP8_FUSED_GELU          1            fp8 MLPs: bias+GELU (and its backward) emit e4m3 + transpose directly
                                          (fp8.hip fp8_gelu_cast_kernel): no bf16 activation, no cast pass
 PDT_FP8_WEIGHT_MULTI        1            fp8: every Linear weight cast in one launch per forward (fp8_cast_multi)
+PDT_FP8_CAST_COLSUM         1            fp8: a Linear's output-gradient cast also yields its bias gradient
+PDT_FP8_LN                  1            fp8: the add+LayerNorm in front of qkv / fc1 writes its output as e4m3 +
+                                         transpose for that GEMM (layernorm.hip ln_fwd_fp8_kernel): no bf16 y
 """
 from __future__ import annotations
 
@@ -69,7 +72,7 @@ class _Switches:
                  "conv_bn_stats", "bn_bwd_stats", "res_masked", "stem_bwd_fused", "stem_bn_wgrad", "stem_bn_stats", "stem_pool_wgrad", "wgrad_splitk", "slice_sum",
                  "subsample_native", "linear_splitk", "fused_addln", "embedding_native", "linear_epilogue",
                  "bwd_fused", "bwd_fused_shapes", "bn2_defer", "bn_apply_gemm_k", "strided_bstats", "gap_native",
-                 "fp8_fused_gelu", "fp8_weight_multi")
+                 "fp8_fused_gelu", "fp8_weight_multi", "fp8_cast_colsum", "fp8_ln")
 
     def __init__(self):
         self.reload()
@@ -120,6 +123,8 @@ class _Switches:
         self.gap_native = on("PDT_GAP_NATIVE")
         self.fp8_fused_gelu = on("PDT_FP8_FUSED_GELU")
         self.fp8_weight_multi = on("PDT_FP8_WEIGHT_MULTI")
+        self.fp8_cast_colsum = on("PDT_FP8_CAST_COLSUM")
+        self.fp8_ln = on("PDT_FP8_LN")
         return self
 
 

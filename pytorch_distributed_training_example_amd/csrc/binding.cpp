@@ -74,6 +74,9 @@ int pdt_ce_bwd(const void* logits, int dtype, const int64_t* target, const float
 int64_t pdt_ln_workspace_floats(int64_t N, int D);
 int pdt_ln_fwd(const void* x, const void* res, int dtype, const float* w, const float* b, void* y, void* sum_out,
                float* mean, float* rstd, int64_t N, int D, float eps, hipStream_t s);
+int pdt_ln_fwd_fp8(const uint16_t* x, const uint16_t* res, const float* w, const float* b, uint16_t* sum_out,
+                   uint8_t* yq, uint8_t* yqt, float* mean, float* rstd, int64_t N, int D, float eps,
+                   const float* scale, float* amax, hipStream_t s);
 int pdt_ln_bwd(const void* dy, const void* x, const void* dres, int dtype, const float* w, const float* mean,
                const float* rstd, void* dx, float* dw, float* db, int64_t N, int D, float* ws, hipStream_t s);
 int pdt_attn_fwd(const uint16_t* q, const int64_t* qs, const uint16_t* k, const int64_t* ks, const uint16_t* v,
@@ -187,6 +190,8 @@ int pdt_fp8_gelu_cast(const uint16_t* h, const uint16_t* dg, const float* bias, 
 int pdt_fp8_cast_multi(int n, const uint16_t* const* x, const int* M, const int* K, float* const* st,
                        uint8_t* const* out, uint8_t* const* out_t, hipStream_t s);
 int pdt_colsum_finalize(const float* part, int nblk, int D, void* out, int odtype, hipStream_t s);
+int pdt_fp8_cast_colsum(const uint16_t* x, int64_t M, int D, const float* scale, uint8_t* out, uint8_t* out_t,
+                        float* amax, float* part, hipStream_t s);
 int pdt_embedding_fwd(const int64_t* idx, const uint16_t* wte, const uint16_t* wpe, uint16_t* out, int64_t n, int T,
                       int D, int V, int* err, hipStream_t s);
 int64_t pdt_embedding_bwd_ws_ints(int64_t n, int V);
@@ -1520,6 +1525,36 @@ std::vector<Tensor> ln_fwd(Tensor x, Tensor w, Tensor b, double eps, c10::option
   return {y, mean, rstd, sum};
 }
 
+// LayerNorm straight to fp8 for an fp8 GEMM (layernorm.hip ln_fwd_fp8_kernel): x bf16 [N, D]
+// (+ res: s = x + res stored). Returns {yq [N, D], yq^T [D, N], mean, rstd, s}; state_row is the
+// consuming GEMM's input-operand row (amax, scale, ...).
+std::vector<Tensor> ln_fwd_fp8(Tensor x, Tensor w, Tensor b, double eps, c10::optional<Tensor> res, Tensor state_row) {
+  check_cuda(x, "x");
+  TORCH_CHECK(x.is_contiguous() && x.scalar_type() == at::kBFloat16, "ln_fp8: x must be contiguous bf16");
+  const int64_t D = x.size(-1), N = x.numel() / D;
+  TORCH_CHECK(w.scalar_type() == at::kFloat && b.scalar_type() == at::kFloat, "ln_fp8: weight/bias must be fp32");
+  TORCH_CHECK(state_row.scalar_type() == at::kFloat && state_row.numel() >= 3 && state_row.is_contiguous(),
+              "ln_fp8: fp32 state row");
+  const bool hr = res.has_value() && res->defined();
+  if (hr)
+    TORCH_CHECK(res->is_contiguous() && res->sizes() == x.sizes() && res->scalar_type() == x.scalar_type(),
+                "ln_fp8: residual must match x (contiguous, same shape/dtype)");
+  auto o8 = x.options().dtype(at::kFloat8_e4m3fn);
+  auto yq = at::empty({N, D}, o8), yqt = at::empty({D, N}, o8);
+  Tensor sum;
+  if (hr) sum = at::empty_like(x);
+  auto fopt = x.options().dtype(at::kFloat);
+  auto mean = at::empty({N}, fopt), rstd = at::empty({N}, fopt);
+  float* st = state_row.data_ptr<float>();
+  int rc = pdt_ln_fwd_fp8(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                          hr ? reinterpret_cast<const uint16_t*>(res->data_ptr()) : nullptr, w.data_ptr<float>(),
+                          b.data_ptr<float>(), hr ? reinterpret_cast<uint16_t*>(sum.data_ptr()) : nullptr,
+                          reinterpret_cast<uint8_t*>(yq.data_ptr()), reinterpret_cast<uint8_t*>(yqt.data_ptr()),
+                          mean.data_ptr<float>(), rstd.data_ptr<float>(), N, (int)D, (float)eps, st + 1, st, stream());
+  TORCH_CHECK(rc == 0, "pdt_ln_fwd_fp8: unsupported N=", N, " D=", D);
+  return {yq, yqt, mean, rstd, sum};
+}
+
 // dres: optional gradient added into dx (the residual stream's own gradient).
 std::vector<Tensor> ln_bwd(Tensor dy, Tensor x, Tensor w, Tensor mean, Tensor rstd, c10::optional<Tensor> dres) {
   TORCH_CHECK(dy.is_contiguous() && x.is_contiguous(), "ln bwd: contiguous inputs required");
@@ -1723,6 +1758,30 @@ std::vector<Tensor> fp8_gelu_cast(Tensor h, c10::optional<Tensor> dg, c10::optio
     pdt_colsum_finalize(part.data_ptr<float>(), nchunk, (int)D, db.data_ptr(), db_dtype == at::kFloat ? 0 : 1,
                         stream());
   }
+  return {out, out_t, db};
+}
+
+// A Linear's output gradient dy (bf16 [M, D], D % 64 == 0): {fp8(dy), its transpose, sum_m dy in
+// db_dtype} in one pass (fp8.hip M_CAST_SUM) — the cast and the bias gradient.
+std::vector<Tensor> fp8_cast_colsum(Tensor x, Tensor state_row, at::ScalarType db_dtype) {
+  check_cuda(x, "x");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.dim() == 2 && x.is_contiguous(), "fp8_cast_colsum: bf16 [M, D]");
+  TORCH_CHECK(state_row.scalar_type() == at::kFloat && state_row.numel() >= 3 && state_row.is_contiguous(),
+              "fp8_cast_colsum: fp32 state row");
+  TORCH_CHECK(db_dtype == at::kFloat || db_dtype == at::kBFloat16, "fp8_cast_colsum: db dtype fp32 / bf16");
+  const int64_t M = x.size(0), D = x.size(1);
+  TORCH_CHECK(M % 16 == 0 && D % 64 == 0 && M > 0, "fp8_cast_colsum: M % 16 == 0 and D % 64 == 0");
+  auto o8 = x.options().dtype(at::kFloat8_e4m3fn);
+  auto out = at::empty({M, D}, o8), out_t = at::empty({D, M}, o8);
+  auto part = at::empty({pdt_fp8_gelu_cast_workspace_floats(M, (int)D)}, x.options().dtype(at::kFloat));
+  auto db = at::empty({D}, x.options().dtype(db_dtype));
+  float* st = state_row.data_ptr<float>();
+  const int nchunk = pdt_fp8_cast_colsum(reinterpret_cast<const uint16_t*>(x.data_ptr()), M, (int)D, st + 1,
+                                         reinterpret_cast<uint8_t*>(out.data_ptr()),
+                                         reinterpret_cast<uint8_t*>(out_t.data_ptr()), st, part.data_ptr<float>(),
+                                         stream());
+  TORCH_CHECK(nchunk > 0, "pdt_fp8_cast_colsum failed: ", nchunk);
+  pdt_colsum_finalize(part.data_ptr<float>(), nchunk, (int)D, db.data_ptr(), db_dtype == at::kFloat ? 0 : 1, stream());
   return {out, out_t, db};
 }
 
@@ -2121,6 +2180,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ce_fwd", &ce_fwd);
   m.def("ce_bwd", &ce_bwd);
   m.def("ln_fwd", &ln_fwd, py::arg("x"), py::arg("w"), py::arg("b"), py::arg("eps"), py::arg("res") = py::none());
+  m.def("ln_fwd_fp8", &ln_fwd_fp8, py::arg("x"), py::arg("w"), py::arg("b"), py::arg("eps"), py::arg("res"),
+        py::arg("state_row"));
   m.def("ln_bwd", &ln_bwd, py::arg("dy"), py::arg("x"), py::arg("w"), py::arg("mean"), py::arg("rstd"),
         py::arg("dres") = py::none());
   m.def("bias_gelu_fwd", &bias_gelu_fwd);
@@ -2140,6 +2201,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("fp8_gelu_cast", &fp8_gelu_cast, py::arg("h"), py::arg("dg") = py::none(), py::arg("bias") = py::none(),
         py::arg("state_row"), py::arg("tanh_form") = false, py::arg("db_dtype") = at::kFloat);
   m.def("fp8_cast_multi", &fp8_cast_multi);
+  m.def("fp8_cast_colsum", &fp8_cast_colsum);
   m.def("lenet_stem_fwd", &lenet_stem_fwd);
   m.def("lenet_stem_bwd", &lenet_stem_bwd);
   m.def("leaky_pool_fwd", &leaky_pool_fwd);

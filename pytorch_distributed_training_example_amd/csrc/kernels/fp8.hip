@@ -10,103 +10,167 @@
 //     and its transpose (the operand layouts hipBLASLt needs for the fwd / dgrad / wgrad GEMMs),
 //     scales by the tensor's current scale (read from device memory: capture-safe, no host sync)
 //     and folds |x|max into the tensor's amax slot (atomicMax on the float bits — the values are
-//     non-negative so integer order == float order), one atomic per workgroup. 64x64 tiles
+//     non-negative so integer order == float order), one atomic per workgroup. 128x64 tiles
 //     staged through LDS, persistent grid.
 //   fp8_update_scales: one launch per step for ALL fp8 tensors of a model: push amax into the
 //     history (shift register), scale = 448 / (max(history) * 2^margin), scale_inv = 1/scale, reset amax.
 #include "../common.h"
+#include "../fp8_pack.h"
 #include "../gelu_math.h"
 
 using namespace pdt;
 
 namespace {
 
-constexpr float kE4M3Max = 448.f;
 constexpr int kTile = 64;
 
-__device__ __forceinline__ uint32_t pack4_fp8(float a, float b, float c, float d) {
-  a = __builtin_amdgcn_fmed3f(a, kE4M3Max, -kE4M3Max);
-  b = __builtin_amdgcn_fmed3f(b, kE4M3Max, -kE4M3Max);
-  c = __builtin_amdgcn_fmed3f(c, kE4M3Max, -kE4M3Max);
-  d = __builtin_amdgcn_fmed3f(d, kE4M3Max, -kE4M3Max);
-  int w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);  // bytes 0,1
-  w = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);        // bytes 2,3
-  return (uint32_t)w;
+// ---- the tile engine shared by every cast kernel ----
+// A tile is 128 rows x 64 columns. Row-major phase: thread t converts 16 columns (cc = 16 (t & 3))
+// of rows t / 4 and t / 4 + 64 (two 32-B loads per row in flight per thread, prefetched one tile
+// ahead) and stores the 16 fp8 bytes; the bytes also go to an LDS image of the tile. Transposed
+// phase: thread t reads one 4-column word from each row of an 8-row block (rb = t & 15, word
+// gq = t / 16), transposes the 8 x 4 bytes in registers and stores 8 B into each of 4 rows of the
+// transposed output: the 16 lanes of a word column write 128 contiguous bytes of one out_t row
+// (the 64-row version wrote 64-B halves of lines with 16-B stores and ran at 3.4-4.1 TB/s).
+// LDS: word g of row r at r * 16 + (g ^ ((r >> 3) & 15)) — the transposed reads then see 2-way
+// bank conflicts instead of 16-way.
+constexpr int kTM = 128;
+__device__ __forceinline__ int t8(int r, int g) { return r * 16 + (g ^ ((r >> 3) & 15)); }
+
+struct Pre {
+  uint4 x[2][2], g[2][2];  // [row half][16-B piece]: the operand and (GELU backward) its gradient
+};
+
+enum { M_CAST = 0, M_GELU = 1, M_GELU_BWD = 2, M_CAST_SUM = 3 };  // M_CAST_SUM: cast + column sums
+
+template <int MODE>
+__device__ __forceinline__ void tile_load(Pre& p, const uint16_t* __restrict__ x, const uint16_t* __restrict__ dg,
+                                          int64_t rows, int64_t K, int64_t m0, int64_t k0, int ra, int cc) {
+  if (k0 + cc >= K) return;
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh) {
+    const int64_t row = m0 + ra + 64 * hh;
+    if (row < rows) {
+      const int64_t off = row * K + k0 + cc;
+      p.x[hh][0] = *reinterpret_cast<const uint4*>(x + off);
+      p.x[hh][1] = *reinterpret_cast<const uint4*>(x + off + 8);
+      if (MODE == M_GELU_BWD) {
+        p.g[hh][0] = *reinterpret_cast<const uint4*>(dg + off);
+        p.g[hh][1] = *reinterpret_cast<const uint4*>(dg + off + 8);
+      }
+    }
+  }
 }
 
-// Persistent grid over 64x64 tiles (grid-stride); 256 threads; thread t handles row t/4 of a tile,
-// 16 columns. amax is kept in registers across tiles and reduced once per workgroup: one atomic
-// per workgroup (a per-wave atomic on the single amax word serialises in L2 — 19k atomics on a
-// ViT activation cost ~250 us). Requires M % 16 == 0 and K % 16 == 0.
+// rows: rows of this tile's range that exist (M, or the end of a row chunk); M: out_t's row length.
+template <int MODE>
+__device__ __forceinline__ void tile_emit(const Pre& p, const float (&b)[16], float s, int tanh_form, int64_t rows,
+                                          int64_t M, int64_t K, int64_t m0, int64_t k0, int ra, int cc,
+                                          uint8_t* __restrict__ out, uint8_t* __restrict__ out_t, uint32_t* lds,
+                                          float& am, float (&cs)[16]) {
+  const bool colok = k0 + cc < K;
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh) {
+    const int64_t row = m0 + ra + 64 * hh;
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+    if (row < rows && colok) {
+      float v[16], g[16];
+      ld8_bf16(reinterpret_cast<const uint16_t*>(&p.x[hh][0]), *reinterpret_cast<float(*)[8]>(v));
+      ld8_bf16(reinterpret_cast<const uint16_t*>(&p.x[hh][1]), *reinterpret_cast<float(*)[8]>(v + 8));
+      if (MODE == M_GELU_BWD) {
+        ld8_bf16(reinterpret_cast<const uint16_t*>(&p.g[hh][0]), *reinterpret_cast<float(*)[8]>(g));
+        ld8_bf16(reinterpret_cast<const uint16_t*>(&p.g[hh][1]), *reinterpret_cast<float(*)[8]>(g + 8));
+      }
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        if (MODE == M_GELU) {
+          v[j] = bf2f(f2bf(gelu_f(v[j] + b[j], tanh_form)));
+        } else if (MODE == M_GELU_BWD) {
+          const float a = g[j] * gelu_grad(v[j] + b[j], tanh_form);
+          cs[j] += a;
+          v[j] = bf2f(f2bf(a));
+        } else if (MODE == M_CAST_SUM) {
+          cs[j] += v[j];
+        }
+        am = fmaxf(am, fabsf(v[j]));
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        w[q] = pack4_fp8(v[4 * q] * s, v[4 * q + 1] * s, v[4 * q + 2] * s, v[4 * q + 3] * s);
+      *reinterpret_cast<uint4*>(out + row * K + k0 + cc) = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) lds[t8(ra + 64 * hh, (cc >> 2) + q)] = w[q];
+  }
+  __syncthreads();
+  const int rb = threadIdx.x & 15, gq = threadIdx.x >> 4;
+  if (m0 + rb * 8 < rows && k0 + 4 * gq < K) {  // rows and K are multiples of 8 / 16: whole blocks
+    uint32_t wv[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) wv[i] = lds[t8(rb * 8 + i, gq)];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t lo = byte_col(wv[0], wv[1], wv[2], wv[3], j), hi = byte_col(wv[4], wv[5], wv[6], wv[7], j);
+      *reinterpret_cast<uint2*>(out_t + (k0 + 4 * gq + j) * M + m0 + rb * 8) = make_uint2(lo, hi);
+    }
+  }
+  __syncthreads();  // the LDS image is rewritten by the next tile
+}
+
+__device__ __forceinline__ void amax_commit(float am, float* red, float* amax) {
+  am = wave_max(am);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = am;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float bm = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    if (bm > 0.f) atomicMax(reinterpret_cast<int*>(amax), __float_as_int(bm));
+  }
+}
+
+// Plain cast over tiles tb, tb + step, ... of a bf16 [M, K] tensor (k tiles fastest).
+__device__ __forceinline__ void cast_tiles(const uint16_t* __restrict__ x, int64_t M, int64_t K, float s,
+                                           uint8_t* __restrict__ out, uint8_t* __restrict__ out_t, float* amax,
+                                           int64_t tb, int64_t step, uint32_t* lds, float* red) {
+  const int64_t ntk = (K + kTile - 1) / kTile, ntiles = ntk * ((M + kTM - 1) / kTM);
+  const int ra = threadIdx.x >> 2, cc = (threadIdx.x & 3) * 16;
+  float am = 0.f, cs[16], b[16];
+  Pre p;
+  if (tb < ntiles) tile_load<M_CAST>(p, x, nullptr, M, K, (tb / ntk) * kTM, (tb % ntk) * kTile, ra, cc);
+  for (int64_t t = tb; t < ntiles; t += step) {
+    const int64_t m0 = (t / ntk) * kTM, k0 = (t % ntk) * kTile;
+    const Pre cur = p;
+    if (t + step < ntiles)
+      tile_load<M_CAST>(p, x, nullptr, M, K, ((t + step) / ntk) * kTM, ((t + step) % ntk) * kTile, ra, cc);
+    tile_emit<M_CAST>(cur, b, s, 0, M, M, K, m0, k0, ra, cc, out, out_t, lds, am, cs);
+  }
+  amax_commit(am, red, amax);
+}
+
+// Persistent grid over 128x64 tiles (grid-stride); amax kept in registers and committed with one
+// atomic per workgroup (a per-wave atomic on the single amax word serialises in L2 — 19k atomics on
+// a ViT activation cost ~250 us). Requires M % 16 == 0 and K % 16 == 0.
 __global__ __launch_bounds__(256) void fp8_cast_transpose_kernel(const uint16_t* __restrict__ x, int64_t M, int64_t K,
                                                                  const float* __restrict__ scale,
                                                                  uint8_t* __restrict__ out,
                                                                  uint8_t* __restrict__ out_t,
                                                                  float* __restrict__ amax) {
-  __shared__ uint32_t tile[kTile][kTile / 4 + 1];  // fp8 bytes, 4 per word, padded rows
+  __shared__ uint32_t lds[kTM * 16];
   __shared__ float red[4];
-  const int64_t ntk = (K + kTile - 1) / kTile, ntiles = ntk * ((M + kTile - 1) / kTile);
-  const int r = threadIdx.x >> 2, cc = (threadIdx.x & 3) * 16;
-  const int c = threadIdx.x >> 2, rr = (threadIdx.x & 3) * 16;
-  const float s = *scale;
-  float am = 0.f;
-  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-    const int64_t m0 = (t / ntk) * kTile, k0 = (t % ntk) * kTile;
-    uint32_t w[4] = {0u, 0u, 0u, 0u};
-    if ((m0 + r < M) && (k0 + cc < K)) {
-      const uint16_t* src = x + (m0 + r) * K + k0 + cc;
-      float v[16];
-      ld8_bf16(src, *reinterpret_cast<float(*)[8]>(v));
-      ld8_bf16(src + 8, *reinterpret_cast<float(*)[8]>(v + 8));
-#pragma unroll
-      for (int j = 0; j < 16; ++j) am = fmaxf(am, fabsf(v[j]));
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        w[q] = pack4_fp8(v[4 * q] * s, v[4 * q + 1] * s, v[4 * q + 2] * s, v[4 * q + 3] * s);
-      *reinterpret_cast<uint4*>(out + (m0 + r) * K + k0 + cc) = make_uint4(w[0], w[1], w[2], w[3]);
-    }
-    if (out_t) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) tile[r][(cc >> 2) + q] = w[q];
-      __syncthreads();
-      // transposed: thread t writes 16 bytes of row (k0 + t/4) of out_t, i.e. column t/4 of the tile
-      if (k0 + c < K && m0 + rr < M) {
-        const int wsel = c >> 2, sh = (c & 3) * 8;
-        uint32_t o[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          uint32_t v = 0;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) v |= ((tile[rr + 4 * q + j][wsel] >> sh) & 0xffu) << (8 * j);
-          o[q] = v;
-        }
-        *reinterpret_cast<uint4*>(out_t + (k0 + c) * M + m0 + rr) = make_uint4(o[0], o[1], o[2], o[3]);
-      }
-      __syncthreads();  // tile is reused by the next iteration
-    }
-  }
-  am = wave_max(am);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = am;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const float b = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-    if (b > 0.f) atomicMax(reinterpret_cast<int*>(amax), __float_as_int(b));
-  }
+  cast_tiles(x, M, K, *scale, out, out_t, amax, blockIdx.x, gridDim.x, lds, red);
 }
 
 // The MLP's activation in fp8, produced where it is computed (fp8.py _Fp8MlpFn):
-//   forward  (BWD = false): g  = gelu(h + bias)            -> g  as e4m3 [M, D] + its transpose
-//   backward (BWD = true):  dh = dg * gelu'(h + bias)      -> dh as e4m3 [M, D] + its transpose,
-//                                                             and sum_m dh (bias gradient partials)
+//   forward  (MODE = M_GELU):     g  = gelu(h + bias)        -> g  as e4m3 [M, D] + its transpose
+//   backward (MODE = M_GELU_BWD): dh = dg * gelu'(h + bias)  -> dh as e4m3 [M, D] + its transpose,
+//                                                               and sum_m dh (bias gradient partials)
 // Unfused, each was a bias+GELU strip kernel writing a bf16 [M, D] tensor and a cast-transpose pass
 // reading it back: 2 x 2 B of traffic per element less here (ViT-B/16: [25216, 3072] per block).
 // The value quantized is the bf16-rounded activation, exactly what the unfused chain quantized
 // (same gelu_math.h functions, same scale product), so gq / dhq are bit-identical to it; the bias
 // gradient sums the unrounded fp32 dh, as the strip kernel does (different summation order).
-// A workgroup owns one 64-column strip and a chunk of 64-row tiles: the bias and the column sums
-// stay in registers; the next tile's operands are loaded before the current tile's transposed write.
-// D % 64 == 0, M % 16 == 0.
-template <bool BWD>
+// A workgroup owns one 64-column strip and a chunk of 128-row tiles: the bias and the column sums
+// stay in registers. D % 64 == 0, M % 16 == 0.
+template <int MODE>
 __global__ __launch_bounds__(256) void fp8_gelu_cast_kernel(const uint16_t* __restrict__ h,
                                                             const uint16_t* __restrict__ dg,
                                                             const float* __restrict__ bias, int64_t M, int D,
@@ -114,82 +178,29 @@ __global__ __launch_bounds__(256) void fp8_gelu_cast_kernel(const uint16_t* __re
                                                             const float* __restrict__ scale,
                                                             uint8_t* __restrict__ out, uint8_t* __restrict__ out_t,
                                                             float* __restrict__ amax, float* __restrict__ part) {
-  __shared__ uint32_t tile[kTile][kTile / 4 + 1];
+  constexpr bool BWD = MODE == M_GELU_BWD || MODE == M_CAST_SUM;  // column partial sums
+  __shared__ uint32_t lds[kTM * 16];
   __shared__ float red[4];
   __shared__ float cred[4][BWD ? kTile : 1];
-  const int r = threadIdx.x >> 2, cc = (threadIdx.x & 3) * 16;
-  const int c = threadIdx.x >> 2, rr = (threadIdx.x & 3) * 16;
-  const int k0 = blockIdx.x * kTile;
+  const int ra = threadIdx.x >> 2, cc = (threadIdx.x & 3) * 16;
+  const int64_t k0 = (int64_t)blockIdx.x * kTile;
   const int64_t mbeg = (int64_t)blockIdx.y * rows_per_chunk;
   const int64_t mend = min(M, mbeg + rows_per_chunk);
   const float s = *scale;
-  float b[16];
+  float b[16], cs[16], am = 0.f;
 #pragma unroll
-  for (int j = 0; j < 16; ++j) b[j] = bias ? bias[k0 + cc + j] : 0.f;
-  float am = 0.f, cs[16];
-#pragma unroll
-  for (int j = 0; j < 16; ++j) cs[j] = 0.f;
-  uint4 hv[2], gv[2];
-  auto load = [&](int64_t m0) {
-    if (m0 + r < mend) {
-      const int64_t off = (m0 + r) * D + k0 + cc;
-      hv[0] = *reinterpret_cast<const uint4*>(h + off);
-      hv[1] = *reinterpret_cast<const uint4*>(h + off + 8);
-      if (BWD) {
-        gv[0] = *reinterpret_cast<const uint4*>(dg + off);
-        gv[1] = *reinterpret_cast<const uint4*>(dg + off + 8);
-      }
-    }
-  };
-  load(mbeg);
-  for (int64_t m0 = mbeg; m0 < mend; m0 += kTile) {
-    uint32_t w[4] = {0u, 0u, 0u, 0u};
-    if (m0 + r < mend) {
-      float v[16], g[16];
-      ld8_bf16(reinterpret_cast<const uint16_t*>(&hv[0]), *reinterpret_cast<float(*)[8]>(v));
-      ld8_bf16(reinterpret_cast<const uint16_t*>(&hv[1]), *reinterpret_cast<float(*)[8]>(v + 8));
-      if (BWD) {
-        ld8_bf16(reinterpret_cast<const uint16_t*>(&gv[0]), *reinterpret_cast<float(*)[8]>(g));
-        ld8_bf16(reinterpret_cast<const uint16_t*>(&gv[1]), *reinterpret_cast<float(*)[8]>(g + 8));
-      }
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        float a;
-        if (BWD) {
-          a = g[j] * gelu_grad(v[j] + b[j], tanh_form);
-          cs[j] += a;
-        } else {
-          a = gelu_f(v[j] + b[j], tanh_form);
-        }
-        v[j] = bf2f(f2bf(a));
-        am = fmaxf(am, fabsf(v[j]));
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        w[q] = pack4_fp8(v[4 * q] * s, v[4 * q + 1] * s, v[4 * q + 2] * s, v[4 * q + 3] * s);
-      *reinterpret_cast<uint4*>(out + (m0 + r) * D + k0 + cc) = make_uint4(w[0], w[1], w[2], w[3]);
-    }
-    if (m0 + kTile < mend) load(m0 + kTile);  // in flight during the transposed write
-#pragma unroll
-    for (int q = 0; q < 4; ++q) tile[r][(cc >> 2) + q] = w[q];
-    __syncthreads();
-    if (m0 + rr < mend) {
-      const int wsel = c >> 2, sh = (c & 3) * 8;
-      uint32_t o[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        uint32_t t = 0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) t |= ((tile[rr + 4 * q + j][wsel] >> sh) & 0xffu) << (8 * j);
-        o[q] = t;
-      }
-      *reinterpret_cast<uint4*>(out_t + (int64_t)(k0 + c) * M + m0 + rr) = make_uint4(o[0], o[1], o[2], o[3]);
-    }
-    __syncthreads();
+  for (int j = 0; j < 16; ++j) {
+    b[j] = (MODE != M_CAST_SUM && bias) ? bias[k0 + cc + j] : 0.f;
+    cs[j] = 0.f;
   }
-  am = wave_max(am);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = am;
-  if (BWD) {  // column sums: lanes with equal (lane & 3) share the columns; fixed butterfly order
+  Pre p;
+  tile_load<MODE>(p, h, dg, mend, D, mbeg, k0, ra, cc);
+  for (int64_t m0 = mbeg; m0 < mend; m0 += kTM) {
+    const Pre cur = p;
+    if (m0 + kTM < mend) tile_load<MODE>(p, h, dg, mend, D, m0 + kTM, k0, ra, cc);
+    tile_emit<MODE>(cur, b, s, tanh_form, mend, M, D, m0, k0, ra, cc, out, out_t, lds, am, cs);
+  }
+  if constexpr (BWD) {  // column sums: lanes with equal (lane & 3) share the columns; fixed butterfly order
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
 #pragma unroll
@@ -199,30 +210,32 @@ __global__ __launch_bounds__(256) void fp8_gelu_cast_kernel(const uint16_t* __re
 #pragma unroll
       for (int j = 0; j < 16; ++j) cred[threadIdx.x >> 6][cc + j] = cs[j];
     }
+    __syncthreads();
+    if (threadIdx.x < kTile)
+      part[(int64_t)blockIdx.y * D + k0 + threadIdx.x] =
+          (cred[0][threadIdx.x] + cred[1][threadIdx.x]) + (cred[2][threadIdx.x] + cred[3][threadIdx.x]);
   }
-  __syncthreads();
-  if constexpr (BWD)
-    if (threadIdx.x < kTile) part[(int64_t)blockIdx.y * D + k0 + threadIdx.x] =
-        (cred[0][threadIdx.x] + cred[1][threadIdx.x]) + (cred[2][threadIdx.x] + cred[3][threadIdx.x]);
-  if (threadIdx.x == 0) {
-    const float bm = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-    if (bm > 0.f) atomicMax(reinterpret_cast<int*>(amax), __float_as_int(bm));
-  }
+  amax_commit(am, red, amax);
 }
 
-// Row chunks of whole 64-row tiles so that strips x chunks ~ 1024 workgroups.
-inline int gelu_cast_chunks(int64_t M, int D, int& rpc) {
-  const int64_t tiles = (M + kTile - 1) / kTile, strips = D / kTile;
-  int64_t n = 1024 / strips;
+// Row chunks of whole 128-row tiles so that strips x chunks ~ one resident wave of workgroups: 1024
+// for the forward (4 per CU), 768 for the backward (162 VGPRs: 3 per CU) — a second partial round
+// of workgroups would run at a fraction of the occupancy.
+inline int gelu_cast_chunks(int64_t M, int D, bool bwd, int& rpc) {
+  const int64_t tiles = (M + kTM - 1) / kTM, strips = D / kTile;
+  int64_t n = (bwd ? 768 : 1024) / strips;
   if (n > tiles) n = tiles;
   if (n < 1) n = 1;
-  rpc = (int)(((tiles + n - 1) / n) * kTile);
+  rpc = (int)(((tiles + n - 1) / n) * kTM);
   return (int)((M + rpc - 1) / rpc);
 }
 
-// Weight casts of a whole model in one launch: a table of tensors, one workgroup-range per tensor
-// (each runs fp8_cast_transpose's tile loop over its own tiles). A step casts every fp8 Linear's
-// weight once (48 tensors on ViT-B/16): one launch instead of 48 launches of a few microseconds.
+// (the same kernel with MODE = M_CAST_SUM is the cast of a Linear's output gradient dy that also
+// yields the bias gradient sum_m dy: the separate column-strip pass over dy is gone.)
+
+// Weight casts of a whole model in one launch: a table of tensors, one workgroup range per tensor
+// (each runs the cast tile loop over its own tiles). A step casts every fp8 Linear's weight once
+// (48 tensors on ViT-B/16): one launch instead of 48 launches of a few microseconds.
 struct CastJob {
   const uint16_t* x;
   uint8_t* out;
@@ -238,59 +251,14 @@ struct CastTable {
 };
 
 __global__ __launch_bounds__(256) void fp8_cast_multi_kernel(CastTable tab) {
-  __shared__ uint32_t tile[kTile][kTile / 4 + 1];
+  __shared__ uint32_t lds[kTM * 16];
   __shared__ float red[4];
   int ji = 0;
   for (int q = 1; q < tab.n; ++q)
     if ((int)blockIdx.x >= tab.j[q].blk0) ji = q;
   const CastJob& J = tab.j[ji];
   const int nb = (ji + 1 < tab.n ? tab.j[ji + 1].blk0 : (int)gridDim.x) - J.blk0;
-  const int bid = blockIdx.x - J.blk0;
-  const int64_t M = J.M, K = J.K;
-  const int64_t ntk = (K + kTile - 1) / kTile, ntiles = ntk * ((M + kTile - 1) / kTile);
-  const int r = threadIdx.x >> 2, cc = (threadIdx.x & 3) * 16;
-  const int c = threadIdx.x >> 2, rr = (threadIdx.x & 3) * 16;
-  const float s = J.st[1];
-  float am = 0.f;
-  for (int64_t t = bid; t < ntiles; t += nb) {
-    const int64_t m0 = (t / ntk) * kTile, k0 = (t % ntk) * kTile;
-    uint32_t w[4] = {0u, 0u, 0u, 0u};
-    if ((m0 + r < M) && (k0 + cc < K)) {
-      const uint16_t* src = J.x + (m0 + r) * K + k0 + cc;
-      float v[16];
-      ld8_bf16(src, *reinterpret_cast<float(*)[8]>(v));
-      ld8_bf16(src + 8, *reinterpret_cast<float(*)[8]>(v + 8));
-#pragma unroll
-      for (int j = 0; j < 16; ++j) am = fmaxf(am, fabsf(v[j]));
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        w[q] = pack4_fp8(v[4 * q] * s, v[4 * q + 1] * s, v[4 * q + 2] * s, v[4 * q + 3] * s);
-      *reinterpret_cast<uint4*>(J.out + (m0 + r) * K + k0 + cc) = make_uint4(w[0], w[1], w[2], w[3]);
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) tile[r][(cc >> 2) + q] = w[q];
-    __syncthreads();
-    if (k0 + c < K && m0 + rr < M) {
-      const int wsel = c >> 2, sh = (c & 3) * 8;
-      uint32_t o[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        uint32_t v = 0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v |= ((tile[rr + 4 * q + j][wsel] >> sh) & 0xffu) << (8 * j);
-        o[q] = v;
-      }
-      *reinterpret_cast<uint4*>(J.out_t + (k0 + c) * M + m0 + rr) = make_uint4(o[0], o[1], o[2], o[3]);
-    }
-    __syncthreads();
-  }
-  am = wave_max(am);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = am;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const float bm = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-    if (bm > 0.f) atomicMax(reinterpret_cast<int*>(J.st), __float_as_int(bm));
-  }
+  cast_tiles(J.x, J.M, J.K, J.st[1], J.out, J.out_t, J.st, blockIdx.x - J.blk0, nb, lds, red);
 }
 
 // state rows: [amax_cur, scale, scale_inv, hist_0 .. hist_{L-1}] per tensor (stride 3 + L floats).
@@ -322,8 +290,10 @@ int pdt_fp8_cast_transpose(const uint16_t* x, int64_t M, int64_t K, const float*
                            uint8_t* out_t, float* amax, hipStream_t s) {
   if (M % 16 != 0 || K % 16 != 0) return -1;
   if (M == 0 || K == 0) return 0;
-  const int64_t ntiles = ((K + kTile - 1) / kTile) * ((M + kTile - 1) / kTile);
-  const unsigned grid = (unsigned)(ntiles < 1024 ? ntiles : 1024);  // 4 workgroups per CU
+  const int64_t ntiles = ((K + kTile - 1) / kTile) * ((M + kTM - 1) / kTM);
+  // every workgroup resident at once (74 VGPRs: 6 per CU) with an equal tile count each
+  const int64_t per = (ntiles + 1535) / 1536;
+  const unsigned grid = (unsigned)((ntiles + per - 1) / per);
   hipLaunchKernelGGL(fp8_cast_transpose_kernel, dim3(grid), dim3(256), 0, s, x, M, K, scale, out, out_t, amax);
   return 0;
 }
@@ -331,7 +301,7 @@ int pdt_fp8_cast_transpose(const uint16_t* x, int64_t M, int64_t K, const float*
 int64_t pdt_fp8_gelu_cast_workspace_floats(int64_t M, int D) {
   if (D % kTile != 0 || M <= 0) return 0;
   int rpc;
-  return (int64_t)gelu_cast_chunks(M, D, rpc) * D;
+  return (int64_t)gelu_cast_chunks(M, D, true, rpc) * D;
 }
 
 // bwd = 0: out = fp8(gelu(h + bias)); bwd = 1: out = fp8(dg * gelu'(h + bias)) and part[nchunk][D]
@@ -342,14 +312,26 @@ int pdt_fp8_gelu_cast(const uint16_t* h, const uint16_t* dg, const float* bias, 
   if (D % kTile != 0 || M % 16 != 0 || M <= 0 || D <= 0) return -1;
   if (dg && !part) return -1;
   int rpc;
-  const int nchunk = gelu_cast_chunks(M, D, rpc);
+  const int nchunk = gelu_cast_chunks(M, D, dg != nullptr, rpc);
   const dim3 grid(D / kTile, nchunk);
   if (dg)
-    hipLaunchKernelGGL(fp8_gelu_cast_kernel<true>, grid, dim3(256), 0, s, h, dg, bias, M, D, rpc, tanh_form, scale,
+    hipLaunchKernelGGL(fp8_gelu_cast_kernel<M_GELU_BWD>, grid, dim3(256), 0, s, h, dg, bias, M, D, rpc, tanh_form, scale,
                        out, out_t, amax, part);
   else
-    hipLaunchKernelGGL(fp8_gelu_cast_kernel<false>, grid, dim3(256), 0, s, h, dg, bias, M, D, rpc, tanh_form, scale,
+    hipLaunchKernelGGL(fp8_gelu_cast_kernel<M_GELU>, grid, dim3(256), 0, s, h, dg, bias, M, D, rpc, tanh_form, scale,
                        out, out_t, amax, part);
+  return nchunk;
+}
+
+// x bf16 [M, D] -> fp8 + transpose (scale, amax as pdt_fp8_cast_transpose) and part[nchunk][D] =
+// per-chunk column sums of x (fp32). Returns the chunk count, or < 0 (D % 64, M % 16).
+int pdt_fp8_cast_colsum(const uint16_t* x, int64_t M, int D, const float* scale, uint8_t* out, uint8_t* out_t,
+                        float* amax, float* part, hipStream_t s) {
+  if (D % kTile != 0 || M % 16 != 0 || M <= 0 || D <= 0 || !part) return -1;
+  int rpc;
+  const int nchunk = gelu_cast_chunks(M, D, true, rpc);
+  hipLaunchKernelGGL(fp8_gelu_cast_kernel<M_CAST_SUM>, dim3(D / kTile, nchunk), dim3(256), 0, s, x, nullptr, nullptr,
+                     M, D, rpc, 0, scale, out, out_t, amax, part);
   return nchunk;
 }
 
@@ -364,7 +346,7 @@ int pdt_fp8_cast_multi(int n, const uint16_t* const* x, const int* M, const int*
   int blk = 0;
   for (int i = 0; i < n; ++i) {
     if (M[i] % 16 != 0 || K[i] % 16 != 0 || M[i] <= 0 || K[i] <= 0) return -1;
-    const int64_t tiles = (int64_t)((K[i] + kTile - 1) / kTile) * ((M[i] + kTile - 1) / kTile);
+    const int64_t tiles = (int64_t)((K[i] + kTile - 1) / kTile) * ((M[i] + kTM - 1) / kTM);
     tab.j[i] = CastJob{x[i], out[i], out_t[i], st[i], M[i], K[i], blk};
     blk += (int)(tiles < 64 ? tiles : 64);  // <= 64 workgroups per tensor, tiles grid-strided
   }

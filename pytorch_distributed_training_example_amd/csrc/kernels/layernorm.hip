@@ -12,6 +12,7 @@
 // residual stream's own gradient, dx = LN'(dy) + ds. That removes the separate add kernels
 // (2 per block forward, 2 per block backward) and one full read of s.
 #include "../common.h"
+#include "../fp8_pack.h"
 
 using namespace pdt;
 
@@ -21,6 +22,31 @@ constexpr int kRowsPerBlock = 4;  // 4 waves, one row each
 
 template <typename T> __device__ __forceinline__ float round_to(float v) { return v; }
 template <> __device__ __forceinline__ float round_to<uint16_t>(float v) { return bf2f(f2bf(v)); }
+
+// Row statistics and the normalised value, shared by ln_fwd_kernel and ln_fwd_fp8_kernel with FP
+// contraction off, so both produce the same bits (the fp8 form quantizes exactly the bf16 y).
+template <int K>
+__device__ __forceinline__ void ln_stats(const float (&v)[K][4], float eps, float& mean, float& rstd) {
+#pragma clang fp contract(off)
+  constexpr int D = 256 * K;
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < K; ++k) s += v[k][0] + v[k][1] + v[k][2] + v[k][3];
+  mean = wave_sum(s) * (1.f / D);
+  float q = 0.f;
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float d = v[k][j] - mean;
+      q += d * d;
+    }
+  rstd = rsqrtf(wave_sum(q) * (1.f / D) + eps);
+}
+__device__ __forceinline__ float ln_val(float v, float mean, float rstd, float w, float b) {
+#pragma clang fp contract(off)
+  return (v - mean) * rstd * w + b;
+}
 
 // K = D / 256: 4-element groups per lane (D = 256*K)
 template <typename T, int K>
@@ -35,7 +61,6 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, co
   if (row >= N) return;
   const T* xr = x + row * D;
   float v[K][4];
-  float s = 0.f;
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     Vec4<T>::ld(xr, (int64_t)(k * 256 + lane * 4), v[k]);
@@ -46,15 +71,9 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, co
       for (int j = 0; j < 4; ++j) v[k][j] = round_to<T>(v[k][j] + hv[j]);
       Vec4<T>::st(sum_out + row * D, (int64_t)(k * 256 + lane * 4), v[k]);
     }
-    s += v[k][0] + v[k][1] + v[k][2] + v[k][3];
   }
-  const float mean = wave_sum(s) * (1.f / D);
-  float q = 0.f;
-#pragma unroll
-  for (int k = 0; k < K; ++k)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) { const float d = v[k][j] - mean; q += d * d; }
-  const float rstd = rsqrtf(wave_sum(q) * (1.f / D) + eps);
+  float mean, rstd;
+  ln_stats<K>(v, eps, mean, rstd);
   T* yr = y + row * D;
 #pragma unroll
   for (int k = 0; k < K; ++k) {
@@ -63,10 +82,115 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, co
     Vec4<float>::ld(w, c, wv);
     Vec4<float>::ld(b, c, bv);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) o[j] = (v[k][j] - mean) * rstd * wv[j] + bv[j];
+    for (int j = 0; j < 4; ++j) o[j] = ln_val(v[k][j], mean, rstd, wv[j], bv[j]);
     Vec4<T>::st(yr, (int64_t)c, o);
   }
   if (lane == 0) { mean_out[row] = mean; rstd_out[row] = rstd; }
+}
+
+// LayerNorm (+ residual add) whose output goes straight to e4m3 for the fp8 GEMM that consumes it
+// (ops/fp8.py Fp8Act: a transformer block's qkv and fc1 inputs). Unfused, the bf16 y was written
+// here and read back by a cast-transpose pass; now the kernel writes y as fp8 row-major AND
+// transposed (the layouts the forward and the weight-gradient GEMMs take), scaled by the consumer's
+// delayed scale, with |y|max folded into its amax slot. y is rounded to bf16 before quantizing, so
+// the bytes equal the unfused chain's. A workgroup owns 64 rows (8 waves x 8 rows, 4 rows' loads
+// issued at a time); the fp8 rows also go to an LDS image (row pitch D + 4 bytes: the transposed
+// readers' 8-row blocks hit distinct banks) from which the transposed 64-B row segments are written.
+// Tiles are placed XCD-aware so the two tiles sharing a 128-B line of y^T write it through one L2.
+template <int K>
+__global__ __launch_bounds__(512) void ln_fwd_fp8_kernel(const uint16_t* __restrict__ x,
+                                                         const uint16_t* __restrict__ res,
+                                                         const float* __restrict__ w, const float* __restrict__ b,
+                                                         uint16_t* __restrict__ sum_out, uint8_t* __restrict__ yq,
+                                                         uint8_t* __restrict__ yqt, float* __restrict__ mean_out,
+                                                         float* __restrict__ rstd_out, int64_t N, float eps,
+                                                         const float* __restrict__ scale, float* __restrict__ amax) {
+  constexpr int D = 256 * K, kRows = 64, kPitch = D + 4;
+  __shared__ __attribute__((aligned(16))) uint8_t tile[kRows * kPitch];
+  __shared__ float red[8];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t m0 = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * kRows;
+  const float s8 = *scale;
+  float wr[K][4], br[K][4];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    Vec4<float>::ld(w, k * 256 + lane * 4, wr[k]);
+    Vec4<float>::ld(b, k * 256 + lane * 4, br[k]);
+  }
+  float am = 0.f;
+#pragma unroll 1
+  for (int r0 = 0; r0 < 8; r0 += 4) {
+    uint2 xv[4][K], hv[4][K];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int64_t row = m0 + wv * 8 + r0 + q;
+      if (row < N) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          xv[q][k] = *reinterpret_cast<const uint2*>(x + row * D + k * 256 + lane * 4);
+          if (res != nullptr) hv[q][k] = *reinterpret_cast<const uint2*>(res + row * D + k * 256 + lane * 4);
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int tr = wv * 8 + r0 + q;
+      const int64_t row = m0 + tr;
+      if (row >= N) continue;  // wave-uniform
+      float v[K][4];
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        v[k][0] = __uint_as_float(xv[q][k].x << 16); v[k][1] = __uint_as_float(xv[q][k].x & 0xffff0000u);
+        v[k][2] = __uint_as_float(xv[q][k].y << 16); v[k][3] = __uint_as_float(xv[q][k].y & 0xffff0000u);
+        if (res != nullptr) {  // s = x + h, stored and normalised at storage precision (as ln_fwd_kernel)
+          const float hh[4] = {__uint_as_float(hv[q][k].x << 16), __uint_as_float(hv[q][k].x & 0xffff0000u),
+                               __uint_as_float(hv[q][k].y << 16), __uint_as_float(hv[q][k].y & 0xffff0000u)};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[k][j] = round_to<uint16_t>(v[k][j] + hh[j]);
+          Vec4<uint16_t>::st(sum_out + row * D, (int64_t)(k * 256 + lane * 4), v[k]);
+        }
+      }
+      float mean, rstd;
+      ln_stats<K>(v, eps, mean, rstd);
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        float o[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          o[j] = round_to<uint16_t>(ln_val(v[k][j], mean, rstd, wr[k][j], br[k][j]));
+          am = fmaxf(am, fabsf(o[j]));
+        }
+        const uint32_t pk = pack4_fp8(o[0] * s8, o[1] * s8, o[2] * s8, o[3] * s8);
+        *reinterpret_cast<uint32_t*>(yq + row * D + k * 256 + lane * 4) = pk;
+        *reinterpret_cast<uint32_t*>(tile + tr * kPitch + k * 256 + lane * 4) = pk;
+      }
+      if (lane == 0) { mean_out[row] = mean; rstd_out[row] = rstd; }
+    }
+  }
+  __syncthreads();
+  // y^T: item (word column g, 8-row block rb) -> 4 rows of y^T, 8 bytes each; N % 16 == 0 keeps
+  // 8-row blocks whole
+  for (int it = threadIdx.x; it < (D / 4) * 8; it += 512) {
+    const int rb = it & 7, g = it >> 3;
+    if (m0 + rb * 8 < N) {
+      uint32_t t8[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) t8[i] = *reinterpret_cast<const uint32_t*>(tile + (rb * 8 + i) * kPitch + g * 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        *reinterpret_cast<uint2*>(yqt + (int64_t)(g * 4 + j) * N + m0 + rb * 8) =
+            make_uint2(byte_col(t8[0], t8[1], t8[2], t8[3], j), byte_col(t8[4], t8[5], t8[6], t8[7], j));
+    }
+  }
+  am = wave_max(am);
+  if (lane == 0) red[wv] = am;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float bm = red[0];
+#pragma unroll
+    for (int i = 1; i < 8; ++i) bm = fmaxf(bm, red[i]);
+    if (bm > 0.f) atomicMax(reinterpret_cast<int*>(amax), __float_as_int(bm));
+  }
 }
 
 // Backward: dx per row; per-block partial dgamma/dbeta written to part[blk][2][D].
@@ -228,6 +352,30 @@ int pdt_ln_fwd(const void* x, const void* res, int dtype, const float* w, const 
                        (const uint16_t*)res, w, b, (uint16_t*)y, (uint16_t*)sum_out, mean, rstd, N, eps);
   PDT_LN_SWITCH(PDT_LNF)
 #undef PDT_LNF
+  return 0;
+}
+
+// bf16 x (+ res -> sum_out) -> LayerNorm -> e4m3 yq [N, D] and yq^T [D, N] (scale / amax: the
+// consumer's fp8 state row). N % 16 == 0; D = 256 K, K in {2, .., 6} (K = 8 would spill).
+int pdt_ln_fwd_fp8(const uint16_t* x, const uint16_t* res, const float* w, const float* b, uint16_t* sum_out,
+                   uint8_t* yq, uint8_t* yqt, float* mean, float* rstd, int64_t N, int D, float eps,
+                   const float* scale, float* amax, hipStream_t s) {
+  if ((res == nullptr) != (sum_out == nullptr)) return -2;
+  if (D % 256 != 0 || N % 16 != 0) return -1;
+  if (N == 0) return 0;
+  const dim3 grid((unsigned)((N + 63) / 64));
+#define PDT_LNF8(K)                                                                                          \
+  hipLaunchKernelGGL((ln_fwd_fp8_kernel<K>), grid, dim3(512), 0, s, x, res, w, b, sum_out, yq, yqt, mean, rstd, N, \
+                     eps, scale, amax);
+  switch (D / 256) {
+    case 2: PDT_LNF8(2); break;
+    case 3: PDT_LNF8(3); break;
+    case 4: PDT_LNF8(4); break;
+    case 5: PDT_LNF8(5); break;
+    case 6: PDT_LNF8(6); break;
+    default: return -1;
+  }
+#undef PDT_LNF8
   return 0;
 }
 

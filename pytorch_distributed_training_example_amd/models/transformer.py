@@ -20,7 +20,7 @@ from torch import nn
 
 from ..config import SW
 from ..ops.attention import attention_qkv
-from ..ops.fp8 import fp8_mlp
+from ..ops.fp8 import add_layer_norm_fp8, fp8_input_slot, fp8_linear, fp8_mlp
 from ..ops.gelu import bias_gelu
 from ..ops.layernorm import LayerNorm, add_layer_norm
 from ..ops.linear import linear as _linear
@@ -28,11 +28,11 @@ from ..ops.linear import linear_gelu
 
 
 def linear(x, mod: nn.Linear, bias=True):
-    """``mod``'s GEMM: fp8 when ``enable_fp8`` tagged it (ops/fp8.py), else bf16 (ops/linear.py)."""
+    """``mod``'s GEMM: fp8 when ``enable_fp8`` tagged it (ops/fp8.py), else bf16 (ops/linear.py).
+    ``x`` may be an ``Fp8Act`` (already e4m3, from ``add_layer_norm_fp8``) for a tagged ``mod``."""
     b = mod.bias if bias else None
     fp8 = getattr(mod, "_fp8", None)
     if fp8 is not None:
-        from ..ops.fp8 import fp8_linear
         return fp8_linear(x, mod.weight, b, fp8[0], fp8[1])
     return _linear(x, mod.weight, b)
 
@@ -104,10 +104,22 @@ def run_blocks(blocks, x: torch.Tensor, final_ln: nn.Module) -> torch.Tensor:
         return final_ln(x)
     y = blocks[0].ln_1(x)
     for i, blk in enumerate(blocks):
-        x, y = add_layer_norm(x, blk.attn(y), blk.ln_2)
-        nxt = blocks[i + 1].ln_1 if i + 1 < len(blocks) else final_ln
-        x, y = add_layer_norm(x, blk.mlp(y), nxt)
+        x, y = _add_ln(x, blk.attn(y), blk.ln_2, blk.mlp)
+        nxt, cons = (blocks[i + 1].ln_1, blocks[i + 1].attn.c_attn) if i + 1 < len(blocks) else (final_ln, None)
+        x, y = _add_ln(x, blk.mlp(y), nxt, cons)
     return y
+
+
+def _add_ln(x, h, ln, consumer):
+    """add_layer_norm, or its fp8-emitting form when ``consumer`` (the module the normalised output
+    feeds) runs an fp8 GEMM on it (ops/fp8.py fp8_input_slot)."""
+    if consumer is not None and getattr(ln, "weight", None) is not None and h.shape == x.shape:
+        t = fp8_input_slot(consumer, x)
+        if (t is not None and x.dtype == torch.bfloat16 and h.dtype == x.dtype and x.shape[-1] % 256 == 0
+                and 2 <= x.shape[-1] // 256 <= 6 and ln.weight.dtype == torch.float32
+                and ln.bias is not None and ln.bias.dtype == torch.float32 and len(ln.normalized_shape) == 1):
+            return add_layer_norm_fp8(x, h, ln, t[0], t[1])
+    return add_layer_norm(x, h, ln)
 
 
 def init_weights(module: nn.Module, std: float = 0.02, n_layer: Optional[int] = None) -> None:

@@ -75,13 +75,14 @@ class Fp8State(nn.Module):
 
 class _Fp8LinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, state, slot, st=None):
+    def forward(ctx, x, w, b, state, slot, st=None, xq=None, xqt=None):
         C = native()
         K = x.shape[-1]
-        x2 = x.reshape(-1, K)
-        if not x2.is_contiguous():
-            x2 = x2.contiguous()
-        xq, xqt = C.fp8_cast_transpose(x2, state[slot], True)
+        if xq is None:
+            x2 = x.reshape(-1, K)
+            if not x2.is_contiguous():
+                x2 = x2.contiguous()
+            xq, xqt = C.fp8_cast_transpose(x2, state[slot], True)
         wq, wqt = st.weight_fp8(w, slot) if st is not None else C.fp8_cast_transpose(w, state[slot + 1], True)
         y = torch._scaled_mm(xq, wq.t(), scale_a=state[slot, 2], scale_b=state[slot + 1, 2], bias=b,
                              out_dtype=torch.bfloat16)
@@ -98,17 +99,24 @@ class _Fp8LinearFn(torch.autograd.Function):
         dy2 = dy.reshape(-1, n)
         if not dy2.is_contiguous():
             dy2 = dy2.contiguous()
-        dyq, dyqt = C.fp8_cast_transpose(dy2, state[s + 2], True)
         dx = dw = db = None
+        if ctx.has_b and ctx.needs_input_grad[2] and _colsum_ok(dy2):
+            dyq, dyqt, db = C.fp8_cast_colsum(dy2, state[s + 2], torch.bfloat16)  # cast + bias grad, one pass
+        else:
+            dyq, dyqt = C.fp8_cast_transpose(dy2, state[s + 2], True)
         if ctx.needs_input_grad[0]:
             dx = torch._scaled_mm(dyq, wqt.t(), scale_a=state[s + 2, 2], scale_b=state[s + 1, 2],
                                   out_dtype=torch.bfloat16).reshape(ctx.xshape)
         if ctx.needs_input_grad[1]:
             dw = torch._scaled_mm(dyqt, xqt.t(), scale_a=state[s + 2, 2], scale_b=state[s, 2],
                                   out_dtype=torch.bfloat16)
-        if ctx.has_b and ctx.needs_input_grad[2]:
+        if ctx.has_b and ctx.needs_input_grad[2] and db is None:
             db = C.colsum(dy2, torch.bfloat16)
-        return dx, dw, db, None, None, None
+        return dx, dw, db, None, None, None, None, None
+
+
+def _colsum_ok(dy2: torch.Tensor) -> bool:
+    return SW.fp8_cast_colsum and dy2.shape[1] % 64 == 0
 
 
 def fp8_ok_weight(w: torch.Tensor) -> bool:
@@ -122,8 +130,25 @@ def fp8_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
             and x.shape[-1] % 16 == 0 and w.shape[0] % 16 == 0 and m % 16 == 0 and m > 0)
 
 
-def fp8_linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor], state: Fp8State,
+class Fp8Act:
+    """An activation its producer already wrote in e4m3 for the fp8 GEMM that consumes it
+    (``add_layer_norm_fp8``): the row-major and transposed copies, plus ``token`` — a
+    zero-storage bf16 tensor of the activation's shape that carries the autograd edge (the
+    consumer returns the bf16 gradient of the activation as the token's gradient)."""
+    __slots__ = ("token", "q", "qt")
+
+    def __init__(self, token, q, qt):
+        self.token, self.q, self.qt = token, q, qt
+
+    @property
+    def shape(self):
+        return self.token.shape
+
+
+def fp8_linear(x, weight: torch.Tensor, bias: Optional[torch.Tensor], state: Fp8State,
                slot: int) -> torch.Tensor:
+    if isinstance(x, Fp8Act):  # the producer emitted fp8 for exactly this GEMM (fp8_input_slot)
+        return _Fp8LinearFn.apply(x.token, weight, bias, state.state, slot, state, x.q, x.qt)
     if fp8_ok(x, weight):
         return _Fp8LinearFn.apply(x, weight, bias, state.state, slot, state)
     return torch.nn.functional.linear(x, weight, bias)
@@ -137,13 +162,14 @@ class _Fp8MlpFn(torch.autograd.Function):
     kernel writing them + a cast-transpose reading them back, twice per block)."""
 
     @staticmethod
-    def forward(ctx, x, w1, b1, w2, b2, state, s1, s2, st, tanh_form):
+    def forward(ctx, x, w1, b1, w2, b2, state, s1, s2, st, tanh_form, xq=None, xqt=None):
         C = native()
         D = x.shape[-1]
-        x2 = x.reshape(-1, D)
-        if not x2.is_contiguous():
-            x2 = x2.contiguous()
-        xq, xqt = C.fp8_cast_transpose(x2, state[s1], True)
+        if xq is None:
+            x2 = x.reshape(-1, D)
+            if not x2.is_contiguous():
+                x2 = x2.contiguous()
+            xq, xqt = C.fp8_cast_transpose(x2, state[s1], True)
         w1q, w1qt = st.weight_fp8(w1, s1)
         h = torch._scaled_mm(xq, w1q.t(), scale_a=state[s1, 2], scale_b=state[s1 + 1, 2], out_dtype=torch.bfloat16)
         b1f = None if b1 is None else b1.float()
@@ -165,11 +191,16 @@ class _Fp8MlpFn(torch.autograd.Function):
         dy2 = dy.reshape(-1, dy.shape[-1])
         if not dy2.is_contiguous():
             dy2 = dy2.contiguous()
-        dyq, dyqt = C.fp8_cast_transpose(dy2, state[s2 + 2], True)
+        db2 = None
+        if ctx.has_b2 and _colsum_ok(dy2):
+            dyq, dyqt, db2 = C.fp8_cast_colsum(dy2, state[s2 + 2], torch.bfloat16)
+        else:
+            dyq, dyqt = C.fp8_cast_transpose(dy2, state[s2 + 2], True)
         dg = torch._scaled_mm(dyq, w2qt.t(), scale_a=state[s2 + 2, 2], scale_b=state[s2 + 1, 2],
                               out_dtype=torch.bfloat16)
         dw2 = torch._scaled_mm(dyqt, gqt.t(), scale_a=state[s2 + 2, 2], scale_b=state[s2, 2], out_dtype=torch.bfloat16)
-        db2 = C.colsum(dy2, torch.bfloat16) if ctx.has_b2 else None
+        if ctx.has_b2 and db2 is None:
+            db2 = C.colsum(dy2, torch.bfloat16)
         dbt = ctx.b1_dtype if ctx.b1_dtype in (torch.float32, torch.bfloat16) else torch.float32
         dhq, dhqt, db1 = C.fp8_gelu_cast(h, dg, b1f, state[s1 + 2], ctx.tanh_form, dbt)
         dx = torch._scaled_mm(dhq, w1qt.t(), scale_a=state[s1 + 2, 2], scale_b=state[s1 + 1, 2],
@@ -177,23 +208,78 @@ class _Fp8MlpFn(torch.autograd.Function):
         dw1 = torch._scaled_mm(dhqt, xqt.t(), scale_a=state[s1 + 2, 2], scale_b=state[s1, 2], out_dtype=torch.bfloat16)
         if db1 is not None and ctx.b1_dtype is not None and db1.dtype != ctx.b1_dtype:
             db1 = db1.to(ctx.b1_dtype)
-        return dx, dw1, db1, dw2, db2, None, None, None, None, None
+        return dx, dw1, db1, dw2, db2, None, None, None, None, None, None, None
 
 
-def fp8_mlp(x: torch.Tensor, fc1: nn.Linear, fc2: nn.Linear, approximate: str) -> Optional[torch.Tensor]:
-    """The MLP on fp8 with the fused GELU casts, or None when a shape / dtype is not served (the
-    caller then runs the per-Linear path)."""
+def _mlp_ok(x: torch.Tensor, fc1: nn.Linear, fc2: nn.Linear) -> bool:
     a, b = getattr(fc1, "_fp8", None), getattr(fc2, "_fp8", None)
     if a is None or b is None or a[0] is not b[0] or not SW.fp8_fused_gelu:
-        return None
+        return False
     m = x.numel() // max(x.shape[-1], 1)
-    if not (fp8_ok(x, fc1.weight) and fc2.weight.dtype == torch.bfloat16 and fc1.weight.shape[0] % 64 == 0
+    return (fp8_ok(x, fc1.weight) and fc2.weight.dtype == torch.bfloat16 and fc1.weight.shape[0] % 64 == 0
             and fc2.weight.shape[0] % 16 == 0 and fc1.weight.is_contiguous() and fc2.weight.is_contiguous()
-            and m % 16 == 0 and (fc1.bias is None or fc1.bias.dtype in (torch.float32, torch.bfloat16))):
+            and m % 16 == 0 and (fc1.bias is None or fc1.bias.dtype in (torch.float32, torch.bfloat16)))
+
+
+def fp8_mlp(x, fc1: nn.Linear, fc2: nn.Linear, approximate: str) -> Optional[torch.Tensor]:
+    """The MLP on fp8 with the fused GELU casts, or None when a shape / dtype is not served (the
+    caller then runs the per-Linear path). ``x`` may be an ``Fp8Act`` (then it is always served)."""
+    a, b = getattr(fc1, "_fp8", None), getattr(fc2, "_fp8", None)
+    pre = isinstance(x, Fp8Act)
+    xt = x.token if pre else x
+    if not pre and not _mlp_ok(x, fc1, fc2):
         return None
     st = a[0]
-    return _Fp8MlpFn.apply(x, fc1.weight, fc1.bias, fc2.weight, fc2.bias, st.state, a[1], b[1], st,
-                           approximate == "tanh")
+    return _Fp8MlpFn.apply(xt, fc1.weight, fc1.bias, fc2.weight, fc2.bias, st.state, a[1], b[1], st,
+                           approximate == "tanh", x.q if pre else None, x.qt if pre else None)
+
+
+def fp8_input_slot(consumer: nn.Module, x: torch.Tensor):
+    """(state, slot) when ``consumer`` — an fp8-tagged Linear, or an MLP whose fused fp8 path
+    will run — takes ``x`` as an fp8 GEMM operand and can be handed an ``Fp8Act``; else None."""
+    if not SW.fp8_ln:
+        return None
+    if isinstance(consumer, nn.Linear):
+        t = getattr(consumer, "_fp8", None)
+        return (t[0], t[1]) if t is not None and fp8_ok(x, consumer.weight) else None
+    fc1, fc2 = getattr(consumer, "c_fc", None), getattr(consumer, "c_proj", None)
+    if isinstance(fc1, nn.Linear) and isinstance(fc2, nn.Linear) and _mlp_ok(x, fc1, fc2):
+        return fc1._fp8[0], fc1._fp8[1]
+    return None
+
+
+class _AddLNFp8Fn(torch.autograd.Function):
+    """(s, y) = (x + h, LayerNorm(x + h)) with y emitted as e4m3 (+ transpose) for the consumer's
+    fp8 GEMM (layernorm.hip ln_fwd_fp8_kernel): returns s, the zero-storage token standing for
+    y, and the fp8 copies. Backward: the token's gradient is dy; dx = dh = LN'(dy) + ds, as the
+    bf16 add+LayerNorm Function."""
+
+    @staticmethod
+    def forward(ctx, x, h, weight, bias, eps, state_row):
+        D = x.shape[-1]
+        yq, yqt, mean, rstd, s = native().ln_fwd_fp8(x.reshape(-1, D), weight, bias, eps, h.reshape(-1, D), state_row)
+        s = s.view(x.shape)
+        token = torch.empty((), dtype=x.dtype, device=x.device).expand(x.shape)  # never read
+        ctx.mark_non_differentiable(yq, yqt)
+        ctx.set_materialize_grads(False)  # no zero-filled gradients for the fp8 copies
+        ctx.save_for_backward(s, weight, mean, rstd)
+        return s, token, yq, yqt
+
+    @staticmethod
+    def backward(ctx, ds, dy, _dq, _dqt):
+        s, weight, mean, rstd = ctx.saved_tensors
+        if dy is None:
+            dy = torch.zeros_like(s)
+        dres = ds.contiguous() if ds is not None else None
+        dx, dw, db = native().ln_bwd(dy.contiguous(), s, weight, mean, rstd, dres)
+        return dx, dx, dw, db, None, None
+
+
+def add_layer_norm_fp8(x: torch.Tensor, h: torch.Tensor, ln: nn.Module, state: "Fp8State", slot: int):
+    """``(s, Fp8Act(ln(s)))`` with ``s = x + h``; the caller checked ``fp8_input_slot``."""
+    s, token, q, qt = _AddLNFp8Fn.apply(x.contiguous(), h.contiguous(), ln.weight, ln.bias, float(ln.eps),
+                                        state.state[slot])
+    return s, Fp8Act(token, q, qt)
 
 
 def enable_fp8(model: nn.Module, history: int = 16, margin: float = 0.0, blocks_only: bool = True) -> Fp8State:

@@ -146,7 +146,7 @@ def test_cast_multi_matches_per_tensor():
 @pytest.mark.parametrize("approximate", ["none", "tanh"])
 def test_fp8_mlp_fused_matches_per_linear_path(approximate):
     """The fused fp8 MLP (GELU casts + one-launch weight casts) against the per-Linear fp8 path: the
-    same fp8 operands, so every output and gradient is bit-identical except fc1's bias gradient
+    same fp8 operands, so every output and gradient is bit-identical except the bias gradients
     (summation order)."""
     from pytorch_distributed_training_example_amd.config import SW
     from pytorch_distributed_training_example_amd.models.transformer import MLP
@@ -165,10 +165,10 @@ def test_fp8_mlp_fused_matches_per_linear_path(approximate):
     x0 = torch.randn(16, 197, 768, device="cuda").bfloat16()
     g = torch.randn(16, 197, 768, device="cuda").bfloat16()
     res = {}
-    saved = (SW.fp8_fused_gelu, SW.fp8_weight_multi)
+    saved = (SW.fp8_fused_gelu, SW.fp8_weight_multi, SW.fp8_cast_colsum)
     try:
         for fused in (False, True):
-            SW.fp8_fused_gelu = SW.fp8_weight_multi = fused
+            SW.fp8_fused_gelu = SW.fp8_weight_multi = SW.fp8_cast_colsum = fused
             st = enable_fp8(wrap, history=4, blocks_only=False)
             for _ in range(2):  # calibrate the delayed scales, then measure
                 mlp.zero_grad(set_to_none=True)
@@ -179,8 +179,91 @@ def test_fp8_mlp_fused_matches_per_linear_path(approximate):
                           mlp.c_proj.bias.grad, st.state.clone()]
             wrap._fp8_hook.remove()
     finally:
-        SW.fp8_fused_gelu, SW.fp8_weight_multi = saved
+        SW.fp8_fused_gelu, SW.fp8_weight_multi, SW.fp8_cast_colsum = saved
     a, b = res[False], res[True]
-    for i in (0, 1, 2, 4, 5, 6):
+    for i in (0, 1, 2, 4, 6):
         assert torch.equal(a[i], b[i]), i
-    torch.testing.assert_close(a[3].float(), b[3].float(), rtol=2e-2, atol=1e-2)
+    for i in (3, 5):  # bias gradients: fused column sums, another summation order
+        torch.testing.assert_close(a[i].float(), b[i].float(), rtol=2e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("m,d", [(25216, 768), (25216, 2304), (8192, 1024), (48, 192)])
+def test_cast_colsum_matches_cast_and_colsum(m, d):
+    """dy -> (fp8, transpose) bit-identical to fp8_cast_transpose, and the bias gradient against the
+    column-strip kernel and fp32."""
+    from pytorch_distributed_training_example_amd.ops._native import native
+    C = native()
+    torch.manual_seed(5)
+    x = torch.randn(m, d, device="cuda").bfloat16()
+    st_ref, st = _st(100.0), _st(100.0)
+    q_ref, qt_ref = C.fp8_cast_transpose(x, st_ref, True)
+    q, qt, db = C.fp8_cast_colsum(x, st, torch.float32)
+    assert torch.equal(q.view(torch.uint8), q_ref.view(torch.uint8))
+    assert torch.equal(qt.view(torch.uint8), qt_ref.view(torch.uint8))
+    assert st[0].item() == st_ref[0].item()
+    ref = x.double().sum(0)
+    assert ((db.double() - ref).norm() / ref.norm()).item() < 1e-5
+    torch.testing.assert_close(db, C.colsum(x, torch.float32), rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("n,d", [(25216, 768), (8192, 1024), (48, 512)])
+def test_ln_fwd_fp8_bit_identical_to_ln_then_cast(n, d):
+    """add + LayerNorm emitting e4m3 (+ transpose) == the bf16 add + LayerNorm kernel followed by the
+    cast-transpose pass: the same bytes, statistics, residual sum and amax."""
+    from pytorch_distributed_training_example_amd.ops._native import native
+    C = native()
+    torch.manual_seed(6)
+    x = torch.randn(n, d, device="cuda").bfloat16()
+    h = torch.randn(n, d, device="cuda").bfloat16()
+    w = torch.rand(d, device="cuda") + 0.5
+    b = torch.randn(d, device="cuda") * 0.1
+    st_ref, st = _st(80.0), _st(80.0)
+    y, mean_r, rstd_r, s_r = C.ln_fwd(x, w, b, 1e-6, h)
+    q_ref, qt_ref = C.fp8_cast_transpose(y, st_ref, True)
+    q, qt, mean, rstd, s = C.ln_fwd_fp8(x, w, b, 1e-6, h, st)
+    assert torch.equal(s, s_r) and torch.equal(mean, mean_r) and torch.equal(rstd, rstd_r)
+    assert torch.equal(q.view(torch.uint8), q_ref.view(torch.uint8))
+    assert torch.equal(qt.view(torch.uint8), qt_ref.view(torch.uint8))
+    assert st[0].item() == st_ref[0].item()
+
+
+def test_vit_blocks_fp8_ln_matches_cast_path():
+    """Two ViT-B/16-width blocks + final LayerNorm, fp8: the add+LayerNorm emitting e4m3 for qkv / fc1
+    (PDT_FP8_LN) against the bf16 LayerNorm + cast path — bit-identical outputs and gradients."""
+    from pytorch_distributed_training_example_amd.config import SW
+    from pytorch_distributed_training_example_amd.models.transformer import Block, run_blocks
+    from pytorch_distributed_training_example_amd.ops.fp8 import enable_fp8
+    from pytorch_distributed_training_example_amd.ops.layernorm import LayerNorm
+    torch.manual_seed(7)
+
+    class Net(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.blocks = torch.nn.ModuleList([Block(768, 12, eps=1e-6) for _ in range(2)])
+            self.ln_f = LayerNorm(768, eps=1e-6)
+
+        def forward(self, x):
+            return run_blocks(self.blocks, x, self.ln_f)
+    net = Net().cuda()
+    for m in net.modules():  # bf16 weights, fp32 LayerNorm parameters (models/precision.py)
+        if isinstance(m, torch.nn.Linear):
+            m.to(torch.bfloat16)
+    x0 = torch.randn(16, 197, 768, device="cuda").bfloat16()
+    g = torch.randn(16, 197, 768, device="cuda").bfloat16()
+    res = {}
+    saved = SW.fp8_ln
+    try:
+        for on in (False, True):
+            SW.fp8_ln = on
+            st = enable_fp8(net, history=4)
+            for _ in range(2):
+                net.zero_grad(set_to_none=True)
+                x = x0.clone().requires_grad_(True)
+                y = net(x)
+                y.backward(g)
+            res[on] = [y, x.grad, st.state.clone()] + [p.grad.clone() for p in net.parameters()]
+            net._fp8_hook.remove()
+    finally:
+        SW.fp8_ln = saved
+    for i, (a, b) in enumerate(zip(res[False], res[True])):
+        assert torch.equal(a, b), i
