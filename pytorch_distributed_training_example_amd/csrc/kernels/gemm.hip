@@ -58,7 +58,8 @@ enum { EPI_NONE = 0, EPI_BIAS = 1, EPI_GELU = 2 };
 constexpr int kGroup = PDT_GEMM_GROUP;  // A bands per tile group (tile order)
 
 #ifndef PDT_GEMM_PROBE
-#define PDT_GEMM_PROBE 0  // diagnostics only (tools/convbench/gemm_bench.cpp): 1 = no MFMA, 2 = no DMA
+#define PDT_GEMM_PROBE 0  // diagnostics only (tools/convbench/gemm_bench.cpp): 1 = no MFMA, 2 = no DMA,
+                          // 3 = no epilogue (accumulators kept alive, nothing staged or stored)
 #endif
 
 __device__ __forceinline__ int swz(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
@@ -215,6 +216,15 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
   }
   if (wr == 0) bar();  // balance row 1's extra barrier
 
+  if (PDT_GEMM_PROBE == 3) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) t += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+    if (t == 1234.5f) C[tid] = 1;
+    return;
+  }
   // ---- epilogue: lane holds C[m][n .. n+3] of every block (4 consecutive columns). The bf16 tile
   // is staged through LDS (free now: every read and DMA has retired) and written as whole 512-B
   // row segments — 8-B stores straight from the accumulators hit each 128-B line four times and
@@ -289,7 +299,7 @@ int launch(const uint16_t* A, const uint16_t* B, uint16_t* C, uint16_t* G, const
   const int64_t grid = (int64_t)((M + kBM - 1) / kBM) * (N / kBN);
   hipLaunchKernelGGL(gemm_nt_kernel<EPI>, dim3((unsigned)grid), dim3(kThreads), kLds, s, A, B, C, G, bias, bias_f32,
                      tanh_form, M, N, K);
-  return 0;
+  return hipPeekAtLastError() == hipSuccess ? 0 : -4;  // a refused launch fails loudly, not as garbage
 }
 
 }  // namespace
