@@ -76,7 +76,7 @@ int pdt_ln_fwd(const void* x, const void* res, int dtype, const float* w, const 
                float* mean, float* rstd, int64_t N, int D, float eps, hipStream_t s);
 int pdt_ln_fwd_fp8(const uint16_t* x, const uint16_t* res, const float* w, const float* b, uint16_t* sum_out,
                    uint8_t* yq, uint8_t* yqt, float* mean, float* rstd, int64_t N, int D, float eps,
-                   const float* scale, float* amax, hipStream_t s);
+                   const float* scale, float* amax, int striped, hipStream_t s);
 int pdt_ln_bwd(const void* dy, const void* x, const void* dres, int dtype, const float* w, const float* mean,
                const float* rstd, void* dx, float* dw, float* db, int64_t N, int D, float* ws, hipStream_t s);
 int pdt_attn_fwd(const uint16_t* q, const int64_t* qs, const uint16_t* k, const int64_t* ks, const uint16_t* v,
@@ -182,16 +182,20 @@ int pdt_bn_fwd_train_tiles(const float* part, int T, int BMt, const uint16_t* x,
                            float momentum, float eps, int64_t M, int C, int relu, uint16_t* y, uint8_t* mask,
                            float* mean, float* invstd, float* ws, hipStream_t s);
 int pdt_fp8_cast_transpose(const uint16_t* x, int64_t M, int64_t K, const float* scale, uint8_t* out,
-                           uint8_t* out_t, float* amax, hipStream_t s);
-int pdt_fp8_update_scales(float* state, int n, int L, float margin_scale, hipStream_t s);
+                           uint8_t* out_t, float* amax, int striped, hipStream_t s);
+int pdt_fp8_update_scales(float* state, int n, int L, float margin_scale, int striped, hipStream_t s);
+// fp8 state rows of at least this many floats carry 16 amax stripes (csrc/fp8_pack.h kAmaxRowMin)
+constexpr int64_t kFp8StripedRow = 261;
+inline int fp8_striped(const at::Tensor& row) { return row.numel() >= kFp8StripedRow ? 1 : 0; }
 int64_t pdt_fp8_gelu_cast_workspace_floats(int64_t M, int D);
 int pdt_fp8_gelu_cast(const uint16_t* h, const uint16_t* dg, const float* bias, int64_t M, int D, int tanh_form,
-                      const float* scale, uint8_t* out, uint8_t* out_t, float* amax, float* part, hipStream_t s);
+                      const float* scale, uint8_t* out, uint8_t* out_t, float* amax, float* part, int striped,
+                      hipStream_t s);
 int pdt_fp8_cast_multi(int n, const uint16_t* const* x, const int* M, const int* K, float* const* st,
-                       uint8_t* const* out, uint8_t* const* out_t, hipStream_t s);
+                       const int* striped, uint8_t* const* out, uint8_t* const* out_t, hipStream_t s);
 int pdt_colsum_finalize(const float* part, int nblk, int D, void* out, int odtype, hipStream_t s);
 int pdt_fp8_cast_colsum(const uint16_t* x, int64_t M, int D, const float* scale, uint8_t* out, uint8_t* out_t,
-                        float* amax, float* part, hipStream_t s);
+                        float* amax, float* part, int striped, hipStream_t s);
 int pdt_embedding_fwd(const int64_t* idx, const uint16_t* wte, const uint16_t* wpe, uint16_t* out, int64_t n, int T,
                       int D, int V, int* err, hipStream_t s);
 int64_t pdt_embedding_bwd_ws_ints(int64_t n, int V);
@@ -1550,7 +1554,8 @@ std::vector<Tensor> ln_fwd_fp8(Tensor x, Tensor w, Tensor b, double eps, c10::op
                           hr ? reinterpret_cast<const uint16_t*>(res->data_ptr()) : nullptr, w.data_ptr<float>(),
                           b.data_ptr<float>(), hr ? reinterpret_cast<uint16_t*>(sum.data_ptr()) : nullptr,
                           reinterpret_cast<uint8_t*>(yq.data_ptr()), reinterpret_cast<uint8_t*>(yqt.data_ptr()),
-                          mean.data_ptr<float>(), rstd.data_ptr<float>(), N, (int)D, (float)eps, st + 1, st, stream());
+                          mean.data_ptr<float>(), rstd.data_ptr<float>(), N, (int)D, (float)eps, st + 1, st,
+                          fp8_striped(state_row), stream());
   TORCH_CHECK(rc == 0, "pdt_ln_fwd_fp8: unsupported N=", N, " D=", D);
   return {yq, yqt, mean, rstd, sum};
 }
@@ -1715,7 +1720,8 @@ std::vector<Tensor> fp8_cast_transpose(Tensor x, Tensor state_row, bool transpos
   float* st = state_row.data_ptr<float>();
   int rc = pdt_fp8_cast_transpose(reinterpret_cast<const uint16_t*>(x.data_ptr()), M, K, st + 1,
                                   reinterpret_cast<uint8_t*>(out.data_ptr()),
-                                  transpose ? reinterpret_cast<uint8_t*>(out_t.data_ptr()) : nullptr, st, stream());
+                                  transpose ? reinterpret_cast<uint8_t*>(out_t.data_ptr()) : nullptr, st,
+                                  fp8_striped(state_row), stream());
   TORCH_CHECK(rc == 0, "pdt_fp8_cast_transpose failed");
   return {out, out_t};
 }
@@ -1750,7 +1756,7 @@ std::vector<Tensor> fp8_gelu_cast(Tensor h, c10::optional<Tensor> dg, c10::optio
                                        hb ? bias->data_ptr<float>() : nullptr, M, (int)D, tanh_form, st + 1,
                                        reinterpret_cast<uint8_t*>(out.data_ptr()),
                                        reinterpret_cast<uint8_t*>(out_t.data_ptr()), st,
-                                       bwd ? part.data_ptr<float>() : nullptr, stream());
+                                       bwd ? part.data_ptr<float>() : nullptr, fp8_striped(state_row), stream());
   TORCH_CHECK(nchunk > 0, "pdt_fp8_gelu_cast failed: ", nchunk);
   if (bwd && hb) {
     TORCH_CHECK(db_dtype == at::kFloat || db_dtype == at::kBFloat16, "fp8_gelu_cast: db dtype fp32 / bf16");
@@ -1779,7 +1785,7 @@ std::vector<Tensor> fp8_cast_colsum(Tensor x, Tensor state_row, at::ScalarType d
   const int nchunk = pdt_fp8_cast_colsum(reinterpret_cast<const uint16_t*>(x.data_ptr()), M, (int)D, st + 1,
                                          reinterpret_cast<uint8_t*>(out.data_ptr()),
                                          reinterpret_cast<uint8_t*>(out_t.data_ptr()), st, part.data_ptr<float>(),
-                                         stream());
+                                         fp8_striped(state_row), stream());
   TORCH_CHECK(nchunk > 0, "pdt_fp8_cast_colsum failed: ", nchunk);
   pdt_colsum_finalize(part.data_ptr<float>(), nchunk, (int)D, db.data_ptr(), db_dtype == at::kFloat ? 0 : 1, stream());
   return {out, out_t, db};
@@ -1794,7 +1800,7 @@ std::vector<Tensor> fp8_cast_multi(std::vector<Tensor> xs, std::vector<Tensor> r
   for (size_t base = 0; base < xs.size(); base += 64) {
     const int n = (int)std::min<size_t>(64, xs.size() - base);
     std::vector<const uint16_t*> px(n);
-    std::vector<int> pm(n), pk(n);
+    std::vector<int> pm(n), pk(n), pst(n);
     std::vector<float*> ps(n);
     std::vector<uint8_t*> po(n), pt(n);
     for (int i = 0; i < n; ++i) {
@@ -1812,10 +1818,12 @@ std::vector<Tensor> fp8_cast_multi(std::vector<Tensor> xs, std::vector<Tensor> r
       pm[i] = (int)M;
       pk[i] = (int)K;
       ps[i] = r.data_ptr<float>();
+      pst[i] = fp8_striped(r);
       po[i] = reinterpret_cast<uint8_t*>(res[res.size() - 2].data_ptr());
       pt[i] = reinterpret_cast<uint8_t*>(res.back().data_ptr());
     }
-    const int rc = pdt_fp8_cast_multi(n, px.data(), pm.data(), pk.data(), ps.data(), po.data(), pt.data(), stream());
+    const int rc = pdt_fp8_cast_multi(n, px.data(), pm.data(), pk.data(), ps.data(), pst.data(), po.data(), pt.data(),
+                                      stream());
     TORCH_CHECK(rc == 0, "pdt_fp8_cast_multi failed: ", rc);
   }
   return res;
@@ -1823,10 +1831,12 @@ std::vector<Tensor> fp8_cast_multi(std::vector<Tensor> xs, std::vector<Tensor> r
 
 void fp8_update_scales(Tensor state, int64_t history, double margin) {
   check_cuda(state, "state");
+  const bool striped = state.dim() == 2 && state.size(1) == kFp8StripedRow - 1 + history;
   TORCH_CHECK(state.scalar_type() == at::kFloat && state.is_contiguous() && state.dim() == 2 &&
-                  state.size(1) == 3 + history, "fp8_update_scales: state [n, 3 + L] fp32");
+                  (state.size(1) == 3 + history || striped),
+              "fp8_update_scales: state [n, 3 + L] or striped [n, 260 + L] fp32");
   pdt_fp8_update_scales(state.data_ptr<float>(), (int)state.size(0), (int)history, (float)std::pow(2.0, margin),
-                        stream());
+                        striped ? 1 : 0, stream());
 }
 
 // ---- intra-node P2P all-reduce (csrc/kernels/p2p.hip) ----

@@ -6,6 +6,15 @@ namespace pdt {
 
 constexpr float kE4M3Max = 448.f;
 
+// Striped fp8 state rows (ops/fp8.py Fp8State): [amax, scale, scale_inv, pad, 16 amax stripes 16 floats
+// (64 B) apart, history...]. A row of at least kAmaxRowMin floats is striped (the C API takes the flag).
+constexpr int kAmaxStripes = 16, kAmaxStripe0 = 4, kAmaxStripeStride = 16;
+constexpr int kAmaxHist = kAmaxStripe0 + kAmaxStripes * kAmaxStripeStride;  // 260: history offset
+constexpr int kAmaxRowMin = kAmaxHist + 1;
+__device__ __forceinline__ float* amax_slot(float* row, int striped, int wg) {
+  return striped ? row + kAmaxStripe0 + (wg & (kAmaxStripes - 1)) * kAmaxStripeStride : row;
+}
+
 // 4 floats -> 4 saturated e4m3 bytes (byte i = value i), round to nearest even.
 __device__ __forceinline__ uint32_t pack4_fp8(float a, float b, float c, float d) {
   a = __builtin_amdgcn_fmed3f(a, kE4M3Max, -kE4M3Max);

@@ -64,7 +64,7 @@ __device__ __forceinline__ void tile_load(Pre& p, const uint16_t* __restrict__ x
 
 // rows: rows of this tile's range that exist (M, or the end of a row chunk); M: out_t's row length.
 template <int MODE>
-__device__ __forceinline__ void tile_emit(const Pre& p, const float (&b)[16], float s, int tanh_form, int64_t rows,
+__device__ __forceinline__ void tile_emit(const Pre& p, const float* bl, float s, int tanh_form, int64_t rows,
                                           int64_t M, int64_t K, int64_t m0, int64_t k0, int ra, int cc,
                                           uint8_t* __restrict__ out, uint8_t* __restrict__ out_t, uint32_t* lds,
                                           float& am, float (&cs)[16]) {
@@ -80,6 +80,11 @@ __device__ __forceinline__ void tile_emit(const Pre& p, const float (&b)[16], fl
       if (MODE == M_GELU_BWD) {
         ld8_bf16(reinterpret_cast<const uint16_t*>(&p.g[hh][0]), *reinterpret_cast<float(*)[8]>(g));
         ld8_bf16(reinterpret_cast<const uint16_t*>(&p.g[hh][1]), *reinterpret_cast<float(*)[8]>(g + 8));
+      }
+      float b[16];  // the strip's bias (GELU modes), from LDS: 16 VGPRs fewer through the tile loop
+      if (MODE == M_GELU || MODE == M_GELU_BWD) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) *reinterpret_cast<float4*>(b + 4 * q) = reinterpret_cast<const float4*>(bl + cc)[q];
       }
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
@@ -117,23 +122,26 @@ __device__ __forceinline__ void tile_emit(const Pre& p, const float (&b)[16], fl
   __syncthreads();  // the LDS image is rewritten by the next tile
 }
 
-__device__ __forceinline__ void amax_commit(float am, float* red, float* amax) {
+// amax: the state row. Striped rows (Fp8State, fp8_pack.h kAmaxStripes) take workgroup b's maximum
+// in stripe b % 16 (64-B apart, 16 L2 lines): one amax word took every workgroup's atomic in turn,
+// ~7 ns each — 8.6 us of a 23 us cast over 1,182 workgroups (profiles/r5/fp8_amax_atomics.txt).
+__device__ __forceinline__ void amax_commit(float am, float* red, float* amax, int striped, int wg) {
   am = wave_max(am);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = am;
   __syncthreads();
   if (threadIdx.x == 0) {
     const float bm = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-    if (bm > 0.f) atomicMax(reinterpret_cast<int*>(amax), __float_as_int(bm));
+    if (bm > 0.f && amax) atomicMax(reinterpret_cast<int*>(amax_slot(amax, striped, wg)), __float_as_int(bm));
   }
 }
 
 // Plain cast over tiles tb, tb + step, ... of a bf16 [M, K] tensor (k tiles fastest).
 __device__ __forceinline__ void cast_tiles(const uint16_t* __restrict__ x, int64_t M, int64_t K, float s,
                                            uint8_t* __restrict__ out, uint8_t* __restrict__ out_t, float* amax,
-                                           int64_t tb, int64_t step, uint32_t* lds, float* red) {
+                                           int striped, int64_t tb, int64_t step, uint32_t* lds, float* red) {
   const int64_t ntk = (K + kTile - 1) / kTile, ntiles = ntk * ((M + kTM - 1) / kTM);
   const int ra = threadIdx.x >> 2, cc = (threadIdx.x & 3) * 16;
-  float am = 0.f, cs[16], b[16];
+  float am = 0.f, cs[16];
   Pre p;
   if (tb < ntiles) tile_load<M_CAST>(p, x, nullptr, M, K, (tb / ntk) * kTM, (tb % ntk) * kTile, ra, cc);
   for (int64_t t = tb; t < ntiles; t += step) {
@@ -141,9 +149,9 @@ __device__ __forceinline__ void cast_tiles(const uint16_t* __restrict__ x, int64
     const Pre cur = p;
     if (t + step < ntiles)
       tile_load<M_CAST>(p, x, nullptr, M, K, ((t + step) / ntk) * kTM, ((t + step) % ntk) * kTile, ra, cc);
-    tile_emit<M_CAST>(cur, b, s, 0, M, M, K, m0, k0, ra, cc, out, out_t, lds, am, cs);
+    tile_emit<M_CAST>(cur, nullptr, s, 0, M, M, K, m0, k0, ra, cc, out, out_t, lds, am, cs);
   }
-  amax_commit(am, red, amax);
+  amax_commit(am, red, amax, striped, (int)tb);
 }
 
 // Persistent grid over 128x64 tiles (grid-stride); amax kept in registers and committed with one
@@ -153,10 +161,10 @@ __global__ __launch_bounds__(256) void fp8_cast_transpose_kernel(const uint16_t*
                                                                  const float* __restrict__ scale,
                                                                  uint8_t* __restrict__ out,
                                                                  uint8_t* __restrict__ out_t,
-                                                                 float* __restrict__ amax) {
+                                                                 float* __restrict__ amax, int striped) {
   __shared__ uint32_t lds[kTM * 16];
   __shared__ float red[4];
-  cast_tiles(x, M, K, *scale, out, out_t, amax, blockIdx.x, gridDim.x, lds, red);
+  cast_tiles(x, M, K, *scale, out, out_t, amax, striped, blockIdx.x, gridDim.x, lds, red);
 }
 
 // The MLP's activation in fp8, produced where it is computed (fp8.py _Fp8MlpFn):
@@ -177,28 +185,29 @@ __global__ __launch_bounds__(256) void fp8_gelu_cast_kernel(const uint16_t* __re
                                                             int rows_per_chunk, int tanh_form,
                                                             const float* __restrict__ scale,
                                                             uint8_t* __restrict__ out, uint8_t* __restrict__ out_t,
-                                                            float* __restrict__ amax, float* __restrict__ part) {
+                                                            float* __restrict__ amax, float* __restrict__ part,
+                                                            int striped) {
   constexpr bool BWD = MODE == M_GELU_BWD || MODE == M_CAST_SUM;  // column partial sums
   __shared__ uint32_t lds[kTM * 16];
   __shared__ float red[4];
   __shared__ float cred[4][BWD ? kTile : 1];
+  __shared__ __attribute__((aligned(16))) float bl[kTile];
   const int ra = threadIdx.x >> 2, cc = (threadIdx.x & 3) * 16;
   const int64_t k0 = (int64_t)blockIdx.x * kTile;
   const int64_t mbeg = (int64_t)blockIdx.y * rows_per_chunk;
   const int64_t mend = min(M, mbeg + rows_per_chunk);
   const float s = *scale;
-  float b[16], cs[16], am = 0.f;
+  float cs[16], am = 0.f;
 #pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    b[j] = (MODE != M_CAST_SUM && bias) ? bias[k0 + cc + j] : 0.f;
-    cs[j] = 0.f;
-  }
+  for (int j = 0; j < 16; ++j) cs[j] = 0.f;
+  if (threadIdx.x < kTile) bl[threadIdx.x] = (MODE != M_CAST_SUM && bias) ? bias[k0 + threadIdx.x] : 0.f;
+  __syncthreads();
   Pre p;
   tile_load<MODE>(p, h, dg, mend, D, mbeg, k0, ra, cc);
   for (int64_t m0 = mbeg; m0 < mend; m0 += kTM) {
     const Pre cur = p;
     if (m0 + kTM < mend) tile_load<MODE>(p, h, dg, mend, D, m0 + kTM, k0, ra, cc);
-    tile_emit<MODE>(cur, b, s, tanh_form, mend, M, D, m0, k0, ra, cc, out, out_t, lds, am, cs);
+    tile_emit<MODE>(cur, bl, s, tanh_form, mend, M, D, m0, k0, ra, cc, out, out_t, lds, am, cs);
   }
   if constexpr (BWD) {  // column sums: lanes with equal (lane & 3) share the columns; fixed butterfly order
 #pragma unroll
@@ -215,7 +224,7 @@ __global__ __launch_bounds__(256) void fp8_gelu_cast_kernel(const uint16_t* __re
       part[(int64_t)blockIdx.y * D + k0 + threadIdx.x] =
           (cred[0][threadIdx.x] + cred[1][threadIdx.x]) + (cred[2][threadIdx.x] + cred[3][threadIdx.x]);
   }
-  amax_commit(am, red, amax);
+  amax_commit(am, red, amax, striped, blockIdx.y * gridDim.x + blockIdx.x);
 }
 
 // Row chunks of whole 128-row tiles so that strips x chunks ~ one resident wave of workgroups: 1024
@@ -241,7 +250,7 @@ struct CastJob {
   uint8_t* out;
   uint8_t* out_t;
   float* st;  // state row: amax, scale, ...
-  int M, K;
+  int M, K, striped;
   int blk0;   // first workgroup of this job
 };
 constexpr int kMaxJobs = 64;
@@ -258,22 +267,32 @@ __global__ __launch_bounds__(256) void fp8_cast_multi_kernel(CastTable tab) {
     if ((int)blockIdx.x >= tab.j[q].blk0) ji = q;
   const CastJob& J = tab.j[ji];
   const int nb = (ji + 1 < tab.n ? tab.j[ji + 1].blk0 : (int)gridDim.x) - J.blk0;
-  cast_tiles(J.x, J.M, J.K, J.st[1], J.out, J.out_t, J.st, blockIdx.x - J.blk0, nb, lds, red);
+  cast_tiles(J.x, J.M, J.K, J.st[1], J.out, J.out_t, J.st, J.striped, blockIdx.x - J.blk0, nb, lds, red);
 }
 
-// state rows: [amax_cur, scale, scale_inv, hist_0 .. hist_{L-1}] per tensor (stride 3 + L floats).
-// The history is a shift register (newest first), so no ring position has to live on the host —
-// the update is identical on every replay of a captured step.
-__global__ void fp8_update_scales_kernel(float* __restrict__ state, int n, int L, float margin_scale) {
+// state rows: [amax_cur, scale, scale_inv, hist_0 .. hist_{L-1}] per tensor (stride 3 + L floats), or
+// striped (fp8_pack.h): [amax_cur, scale, scale_inv, pad, 16 amax stripes 16 floats apart, hist...]
+// (stride kAmaxHist + L). The history is a shift register (newest first), so no ring position has to
+// live on the host — the update is identical on every replay of a captured step.
+__global__ void fp8_update_scales_kernel(float* __restrict__ state, int n, int L, float margin_scale, int striped) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  float* st = state + (int64_t)i * (3 + L);
-  float m = st[0];
-  for (int j = L - 1; j > 0; --j) {
-    st[3 + j] = st[3 + j - 1];
-    m = fmaxf(m, st[3 + j]);
+  const int h0 = striped ? kAmaxHist : 3;
+  float* st = state + (int64_t)i * (h0 + L);
+  float cur = st[0];
+  if (striped) {
+#pragma unroll
+    for (int j = 0; j < kAmaxStripes; ++j) {
+      cur = fmaxf(cur, st[kAmaxStripe0 + j * kAmaxStripeStride]);
+      st[kAmaxStripe0 + j * kAmaxStripeStride] = 0.f;
+    }
   }
-  st[3] = st[0];
+  float m = cur;
+  for (int j = L - 1; j > 0; --j) {
+    st[h0 + j] = st[h0 + j - 1];
+    m = fmaxf(m, st[h0 + j]);
+  }
+  st[h0] = cur;
   if (m > 0.f && isfinite(m)) {
     const float sc = kE4M3Max / (m * margin_scale);
     st[1] = sc;
@@ -284,17 +303,28 @@ __global__ void fp8_update_scales_kernel(float* __restrict__ state, int n, int L
 
 }  // namespace
 
+// diagnosis only: PDT_FP8_AMAX_PROBE=1 drops the amax atomics (times their cost; scales go stale)
+inline bool amax_probe() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("PDT_FP8_AMAX_PROBE");
+    v = (e && e[0] == '1') ? 1 : 0;
+  }
+  return v == 1;
+}
+
 extern "C" {
 
 int pdt_fp8_cast_transpose(const uint16_t* x, int64_t M, int64_t K, const float* scale, uint8_t* out,
-                           uint8_t* out_t, float* amax, hipStream_t s) {
+                           uint8_t* out_t, float* amax, int striped, hipStream_t s) {
   if (M % 16 != 0 || K % 16 != 0) return -1;
   if (M == 0 || K == 0) return 0;
   const int64_t ntiles = ((K + kTile - 1) / kTile) * ((M + kTM - 1) / kTM);
   // every workgroup resident at once (74 VGPRs: 6 per CU) with an equal tile count each
   const int64_t per = (ntiles + 1535) / 1536;
   const unsigned grid = (unsigned)((ntiles + per - 1) / per);
-  hipLaunchKernelGGL(fp8_cast_transpose_kernel, dim3(grid), dim3(256), 0, s, x, M, K, scale, out, out_t, amax);
+  hipLaunchKernelGGL(fp8_cast_transpose_kernel, dim3(grid), dim3(256), 0, s, x, M, K, scale, out, out_t,
+                     amax_probe() ? nullptr : amax, striped);
   return 0;
 }
 
@@ -308,7 +338,8 @@ int64_t pdt_fp8_gelu_cast_workspace_floats(int64_t M, int D) {
 // = per-chunk column sums of it (fp32, unrounded). out_t = the transpose. Returns the chunk count
 // (>= 1), or < 0 when the shape is not served (D % 64, M % 16).
 int pdt_fp8_gelu_cast(const uint16_t* h, const uint16_t* dg, const float* bias, int64_t M, int D, int tanh_form,
-                      const float* scale, uint8_t* out, uint8_t* out_t, float* amax, float* part, hipStream_t s) {
+                      const float* scale, uint8_t* out, uint8_t* out_t, float* amax, float* part, int striped,
+                      hipStream_t s) {
   if (D % kTile != 0 || M % 16 != 0 || M <= 0 || D <= 0) return -1;
   if (dg && !part) return -1;
   int rpc;
@@ -316,29 +347,29 @@ int pdt_fp8_gelu_cast(const uint16_t* h, const uint16_t* dg, const float* bias, 
   const dim3 grid(D / kTile, nchunk);
   if (dg)
     hipLaunchKernelGGL(fp8_gelu_cast_kernel<M_GELU_BWD>, grid, dim3(256), 0, s, h, dg, bias, M, D, rpc, tanh_form, scale,
-                       out, out_t, amax, part);
+                       out, out_t, amax_probe() ? nullptr : amax, part, striped);
   else
     hipLaunchKernelGGL(fp8_gelu_cast_kernel<M_GELU>, grid, dim3(256), 0, s, h, dg, bias, M, D, rpc, tanh_form, scale,
-                       out, out_t, amax, part);
+                       out, out_t, amax_probe() ? nullptr : amax, part, striped);
   return nchunk;
 }
 
 // x bf16 [M, D] -> fp8 + transpose (scale, amax as pdt_fp8_cast_transpose) and part[nchunk][D] =
 // per-chunk column sums of x (fp32). Returns the chunk count, or < 0 (D % 64, M % 16).
 int pdt_fp8_cast_colsum(const uint16_t* x, int64_t M, int D, const float* scale, uint8_t* out, uint8_t* out_t,
-                        float* amax, float* part, hipStream_t s) {
+                        float* amax, float* part, int striped, hipStream_t s) {
   if (D % kTile != 0 || M % 16 != 0 || M <= 0 || D <= 0 || !part) return -1;
   int rpc;
   const int nchunk = gelu_cast_chunks(M, D, true, rpc);
   hipLaunchKernelGGL(fp8_gelu_cast_kernel<M_CAST_SUM>, dim3(D / kTile, nchunk), dim3(256), 0, s, x, nullptr, nullptr,
-                     M, D, rpc, 0, scale, out, out_t, amax, part);
+                     M, D, rpc, 0, scale, out, out_t, amax_probe() ? nullptr : amax, part, striped);
   return nchunk;
 }
 
 // n bf16 [M_i, K_i] tensors -> fp8 row-major + transposed copies, scaled by their state rows, amax
 // folded in; one launch. Returns 0, or < 0 when a shape is not served.
 int pdt_fp8_cast_multi(int n, const uint16_t* const* x, const int* M, const int* K, float* const* st,
-                       uint8_t* const* out, uint8_t* const* out_t, hipStream_t s) {
+                       const int* striped, uint8_t* const* out, uint8_t* const* out_t, hipStream_t s) {
   if (n <= 0) return 0;
   if (n > kMaxJobs) return -2;
   CastTable tab;
@@ -347,16 +378,17 @@ int pdt_fp8_cast_multi(int n, const uint16_t* const* x, const int* M, const int*
   for (int i = 0; i < n; ++i) {
     if (M[i] % 16 != 0 || K[i] % 16 != 0 || M[i] <= 0 || K[i] <= 0) return -1;
     const int64_t tiles = (int64_t)((K[i] + kTile - 1) / kTile) * ((M[i] + kTM - 1) / kTM);
-    tab.j[i] = CastJob{x[i], out[i], out_t[i], st[i], M[i], K[i], blk};
+    tab.j[i] = CastJob{x[i], out[i], out_t[i], st[i], M[i], K[i], striped[i], blk};
     blk += (int)(tiles < 64 ? tiles : 64);  // <= 64 workgroups per tensor, tiles grid-strided
   }
   hipLaunchKernelGGL(fp8_cast_multi_kernel, dim3(blk), dim3(256), 0, s, tab);
   return 0;
 }
 
-int pdt_fp8_update_scales(float* state, int n, int L, float margin_scale, hipStream_t s) {
+int pdt_fp8_update_scales(float* state, int n, int L, float margin_scale, int striped, hipStream_t s) {
   if (n == 0) return 0;
-  hipLaunchKernelGGL(fp8_update_scales_kernel, dim3((n + 255) / 256), dim3(256), 0, s, state, n, L, margin_scale);
+  hipLaunchKernelGGL(fp8_update_scales_kernel, dim3((n + 255) / 256), dim3(256), 0, s, state, n, L, margin_scale,
+                     striped);
   return 0;
 }
 

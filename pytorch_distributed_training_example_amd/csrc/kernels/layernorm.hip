@@ -93,10 +93,10 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, co
 // here and read back by a cast-transpose pass; now the kernel writes y as fp8 row-major AND
 // transposed (the layouts the forward and the weight-gradient GEMMs take), scaled by the consumer's
 // delayed scale, with |y|max folded into its amax slot. y is rounded to bf16 before quantizing, so
-// the bytes equal the unfused chain's. A workgroup owns 64 rows (8 waves x 8 rows, 4 rows' loads
-// issued at a time); the fp8 rows also go to an LDS image (row pitch D + 4 bytes: the transposed
-// readers' 8-row blocks hit distinct banks) from which the transposed 64-B row segments are written.
-// Tiles are placed XCD-aware so the two tiles sharing a 128-B line of y^T write it through one L2.
+// the bytes equal the unfused chain's. A workgroup owns 32 rows (8 waves x 4 rows, every row's loads
+// issued before any row's math: one exposed latency per wave); the fp8 rows also go to an LDS image (row pitch D + 4 bytes: the transposed
+// readers' 8-row blocks hit distinct banks) from which the transposed 32-B row segments are written.
+// Tiles are placed XCD-aware so the four tiles sharing a 128-B line of y^T write it through one L2.
 template <int K>
 __global__ __launch_bounds__(512) void ln_fwd_fp8_kernel(const uint16_t* __restrict__ x,
                                                          const uint16_t* __restrict__ res,
@@ -104,8 +104,9 @@ __global__ __launch_bounds__(512) void ln_fwd_fp8_kernel(const uint16_t* __restr
                                                          uint16_t* __restrict__ sum_out, uint8_t* __restrict__ yq,
                                                          uint8_t* __restrict__ yqt, float* __restrict__ mean_out,
                                                          float* __restrict__ rstd_out, int64_t N, float eps,
-                                                         const float* __restrict__ scale, float* __restrict__ amax) {
-  constexpr int D = 256 * K, kRows = 64, kPitch = D + 4;
+                                                         const float* __restrict__ scale, float* __restrict__ amax,
+                                                         int striped) {
+  constexpr int D = 256 * K, kRows = 32, kPitch = D + 4;
   __shared__ __attribute__((aligned(16))) uint8_t tile[kRows * kPitch];
   __shared__ float red[8];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -118,12 +119,12 @@ __global__ __launch_bounds__(512) void ln_fwd_fp8_kernel(const uint16_t* __restr
     Vec4<float>::ld(b, k * 256 + lane * 4, br[k]);
   }
   float am = 0.f;
-#pragma unroll 1
-  for (int r0 = 0; r0 < 8; r0 += 4) {
+  {
+    constexpr int r0 = 0;
     uint2 xv[4][K], hv[4][K];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int64_t row = m0 + wv * 8 + r0 + q;
+      const int64_t row = m0 + wv * 4 + r0 + q;
       if (row < N) {
 #pragma unroll
         for (int k = 0; k < K; ++k) {
@@ -134,7 +135,7 @@ __global__ __launch_bounds__(512) void ln_fwd_fp8_kernel(const uint16_t* __restr
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int tr = wv * 8 + r0 + q;
+      const int tr = wv * 4 + r0 + q;
       const int64_t row = m0 + tr;
       if (row >= N) continue;  // wave-uniform
       float v[K][4];
@@ -170,8 +171,8 @@ __global__ __launch_bounds__(512) void ln_fwd_fp8_kernel(const uint16_t* __restr
   __syncthreads();
   // y^T: item (word column g, 8-row block rb) -> 4 rows of y^T, 8 bytes each; N % 16 == 0 keeps
   // 8-row blocks whole
-  for (int it = threadIdx.x; it < (D / 4) * 8; it += 512) {
-    const int rb = it & 7, g = it >> 3;
+  for (int it = threadIdx.x; it < (D / 4) * 4; it += 512) {
+    const int rb = it & 3, g = it >> 2;
     if (m0 + rb * 8 < N) {
       uint32_t t8[8];
 #pragma unroll
@@ -189,7 +190,7 @@ __global__ __launch_bounds__(512) void ln_fwd_fp8_kernel(const uint16_t* __restr
     float bm = red[0];
 #pragma unroll
     for (int i = 1; i < 8; ++i) bm = fmaxf(bm, red[i]);
-    if (bm > 0.f) atomicMax(reinterpret_cast<int*>(amax), __float_as_int(bm));
+    if (bm > 0.f) atomicMax(reinterpret_cast<int*>(amax_slot(amax, striped, blockIdx.x)), __float_as_int(bm));
   }
 }
 
@@ -359,14 +360,14 @@ int pdt_ln_fwd(const void* x, const void* res, int dtype, const float* w, const 
 // consumer's fp8 state row). N % 16 == 0; D = 256 K, K in {2, .., 6} (K = 8 would spill).
 int pdt_ln_fwd_fp8(const uint16_t* x, const uint16_t* res, const float* w, const float* b, uint16_t* sum_out,
                    uint8_t* yq, uint8_t* yqt, float* mean, float* rstd, int64_t N, int D, float eps,
-                   const float* scale, float* amax, hipStream_t s) {
+                   const float* scale, float* amax, int striped, hipStream_t s) {
   if ((res == nullptr) != (sum_out == nullptr)) return -2;
   if (D % 256 != 0 || N % 16 != 0) return -1;
   if (N == 0) return 0;
-  const dim3 grid((unsigned)((N + 63) / 64));
+  const dim3 grid((unsigned)((N + 31) / 32));
 #define PDT_LNF8(K)                                                                                          \
   hipLaunchKernelGGL((ln_fwd_fp8_kernel<K>), grid, dim3(512), 0, s, x, res, w, b, sum_out, yq, yqt, mean, rstd, N, \
-                     eps, scale, amax);
+                     eps, scale, amax, striped);
   switch (D / 256) {
     case 2: PDT_LNF8(2); break;
     case 3: PDT_LNF8(3); break;

@@ -175,6 +175,7 @@ def test_fp8_mlp_fused_matches_per_linear_path(approximate):
                 x = x0.clone().requires_grad_(True)
                 y = wrap(x)
                 y.backward(g)
+            st.update()  # folds the amax stripes (which workgroup wrote which stripe differs by path)
             res[fused] = [y, x.grad, mlp.c_fc.weight.grad, mlp.c_fc.bias.grad, mlp.c_proj.weight.grad,
                           mlp.c_proj.bias.grad, st.state.clone()]
             wrap._fp8_hook.remove()
@@ -261,9 +262,44 @@ def test_vit_blocks_fp8_ln_matches_cast_path():
                 x = x0.clone().requires_grad_(True)
                 y = net(x)
                 y.backward(g)
+            st.update()  # folds the amax stripes (which workgroup wrote which stripe differs by path)
             res[on] = [y, x.grad, st.state.clone()] + [p.grad.clone() for p in net.parameters()]
             net._fp8_hook.remove()
     finally:
         SW.fp8_ln = saved
     for i, (a, b) in enumerate(zip(res[False], res[True])):
         assert torch.equal(a, b), i
+
+
+@pytest.mark.parametrize("kind", ["cast", "colsum", "gelu", "ln"])
+def test_striped_amax_rows(kind):
+    """Producers writing into a striped state row (Fp8State): after update() the newest history
+    entry is the tensor's |x|max, the stripes are cleared, and the bytes equal the unstriped cast."""
+    from pytorch_distributed_training_example_amd.ops._native import native
+    from pytorch_distributed_training_example_amd.ops.fp8 import Fp8State
+    C = native()
+    torch.manual_seed(9)
+    st = Fp8State(1, history=4).cuda()
+    st.state[0, 1], st.state[0, 2] = 8.0, 0.125
+    ref = _st(8.0)
+    x = torch.randn(25216, 768, device="cuda").bfloat16()
+    if kind == "cast":
+        q, _ = C.fp8_cast_transpose(x, st.state[0], True)
+        q_ref, _ = C.fp8_cast_transpose(x, ref, True)
+    elif kind == "colsum":
+        q, _, _ = C.fp8_cast_colsum(x, st.state[0], torch.float32)
+        q_ref, _, _ = C.fp8_cast_colsum(x, ref, torch.float32)
+    elif kind == "gelu":
+        b = torch.randn(768, device="cuda")
+        q, _, _ = C.fp8_gelu_cast(x, None, b, st.state[0], False)
+        q_ref, _, _ = C.fp8_gelu_cast(x, None, b, ref, False)
+    else:
+        h = torch.randn_like(x)
+        w, lb = torch.rand(768, device="cuda") + 0.5, torch.randn(768, device="cuda")
+        q = C.ln_fwd_fp8(x, w, lb, 1e-6, h, st.state[0])[0]
+        q_ref = C.ln_fwd_fp8(x, w, lb, 1e-6, h, ref)[0]
+    assert torch.equal(q.view(torch.uint8), q_ref.view(torch.uint8))
+    assert st.state[0, 0].item() == 0.0  # the stripes took every workgroup's maximum
+    st.update()
+    assert st.state[0, Fp8State.STRIPED].item() == ref[0].item() > 0
+    assert (st.state[0, 4:Fp8State.STRIPED] == 0).all()
