@@ -67,7 +67,7 @@ template <int MODE>
 __device__ __forceinline__ void tile_emit(const Pre& p, const float* bl, float s, int tanh_form, int64_t rows,
                                           int64_t M, int64_t K, int64_t m0, int64_t k0, int ra, int cc,
                                           uint8_t* __restrict__ out, uint8_t* __restrict__ out_t, uint32_t* lds,
-                                          float& am, float (&cs)[16]) {
+                                          float& am, float (&cs)[16], int probe) {
   const bool colok = k0 + cc < K;
 #pragma unroll
   for (int hh = 0; hh < 2; ++hh) {
@@ -102,14 +102,14 @@ __device__ __forceinline__ void tile_emit(const Pre& p, const float* bl, float s
 #pragma unroll
       for (int q = 0; q < 4; ++q)
         w[q] = pack4_fp8(v[4 * q] * s, v[4 * q + 1] * s, v[4 * q + 2] * s, v[4 * q + 3] * s);
-      *reinterpret_cast<uint4*>(out + row * K + k0 + cc) = make_uint4(w[0], w[1], w[2], w[3]);
+      if (!(probe & 2)) *reinterpret_cast<uint4*>(out + row * K + k0 + cc) = make_uint4(w[0], w[1], w[2], w[3]);
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) lds[t8(ra + 64 * hh, (cc >> 2) + q)] = w[q];
   }
   __syncthreads();
   const int rb = threadIdx.x & 15, gq = threadIdx.x >> 4;
-  if (m0 + rb * 8 < rows && k0 + 4 * gq < K) {  // rows and K are multiples of 8 / 16: whole blocks
+  if (!(probe & 1) && m0 + rb * 8 < rows && k0 + 4 * gq < K) {  // rows and K are multiples of 8 / 16: whole blocks
     uint32_t wv[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) wv[i] = lds[t8(rb * 8 + i, gq)];
@@ -149,9 +149,9 @@ __device__ __forceinline__ void cast_tiles(const uint16_t* __restrict__ x, int64
     const Pre cur = p;
     if (t + step < ntiles)
       tile_load<M_CAST>(p, x, nullptr, M, K, ((t + step) / ntk) * kTM, ((t + step) % ntk) * kTile, ra, cc);
-    tile_emit<M_CAST>(cur, nullptr, s, 0, M, M, K, m0, k0, ra, cc, out, out_t, lds, am, cs);
+    tile_emit<M_CAST>(cur, nullptr, s, 0, M, M, K, m0, k0, ra, cc, out, out_t, lds, am, cs, striped >> 1);
   }
-  amax_commit(am, red, amax, striped, (int)tb);
+  amax_commit(am, red, amax, striped & 1, (int)tb);
 }
 
 // Persistent grid over 128x64 tiles (grid-stride); amax kept in registers and committed with one
@@ -207,7 +207,7 @@ __global__ __launch_bounds__(256) void fp8_gelu_cast_kernel(const uint16_t* __re
   for (int64_t m0 = mbeg; m0 < mend; m0 += kTM) {
     const Pre cur = p;
     if (m0 + kTM < mend) tile_load<MODE>(p, h, dg, mend, D, m0 + kTM, k0, ra, cc);
-    tile_emit<MODE>(cur, bl, s, tanh_form, mend, M, D, m0, k0, ra, cc, out, out_t, lds, am, cs);
+    tile_emit<MODE>(cur, bl, s, tanh_form, mend, M, D, m0, k0, ra, cc, out, out_t, lds, am, cs, striped >> 1);
   }
   if constexpr (BWD) {  // column sums: lanes with equal (lane & 3) share the columns; fixed butterfly order
 #pragma unroll
@@ -224,7 +224,7 @@ __global__ __launch_bounds__(256) void fp8_gelu_cast_kernel(const uint16_t* __re
       part[(int64_t)blockIdx.y * D + k0 + threadIdx.x] =
           (cred[0][threadIdx.x] + cred[1][threadIdx.x]) + (cred[2][threadIdx.x] + cred[3][threadIdx.x]);
   }
-  amax_commit(am, red, amax, striped, blockIdx.y * gridDim.x + blockIdx.x);
+  amax_commit(am, red, amax, striped & 1, blockIdx.y * gridDim.x + blockIdx.x);
 }
 
 // Row chunks of whole 128-row tiles so that strips x chunks ~ one resident wave of workgroups: 1024
@@ -312,6 +312,16 @@ inline bool amax_probe() {
   }
   return v == 1;
 }
+// diagnosis only: PDT_FP8_STORE_PROBE = 1 skips the transposed stores, 2 the row-major ones (bits of the
+// kernels' flags argument above the stripe bit)
+inline int store_probe() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("PDT_FP8_STORE_PROBE");
+    v = (e && e[0]) ? (int)strtol(e, nullptr, 10) & 3 : 0;
+  }
+  return v << 1;
+}
 
 extern "C" {
 
@@ -324,7 +334,7 @@ int pdt_fp8_cast_transpose(const uint16_t* x, int64_t M, int64_t K, const float*
   const int64_t per = (ntiles + 1535) / 1536;
   const unsigned grid = (unsigned)((ntiles + per - 1) / per);
   hipLaunchKernelGGL(fp8_cast_transpose_kernel, dim3(grid), dim3(256), 0, s, x, M, K, scale, out, out_t,
-                     amax_probe() ? nullptr : amax, striped);
+                     amax_probe() ? nullptr : amax, striped | store_probe());
   return 0;
 }
 
@@ -347,10 +357,10 @@ int pdt_fp8_gelu_cast(const uint16_t* h, const uint16_t* dg, const float* bias, 
   const dim3 grid(D / kTile, nchunk);
   if (dg)
     hipLaunchKernelGGL(fp8_gelu_cast_kernel<M_GELU_BWD>, grid, dim3(256), 0, s, h, dg, bias, M, D, rpc, tanh_form, scale,
-                       out, out_t, amax_probe() ? nullptr : amax, part, striped);
+                       out, out_t, amax_probe() ? nullptr : amax, part, striped | store_probe());
   else
     hipLaunchKernelGGL(fp8_gelu_cast_kernel<M_GELU>, grid, dim3(256), 0, s, h, dg, bias, M, D, rpc, tanh_form, scale,
-                       out, out_t, amax_probe() ? nullptr : amax, part, striped);
+                       out, out_t, amax_probe() ? nullptr : amax, part, striped | store_probe());
   return nchunk;
 }
 
@@ -362,7 +372,7 @@ int pdt_fp8_cast_colsum(const uint16_t* x, int64_t M, int D, const float* scale,
   int rpc;
   const int nchunk = gelu_cast_chunks(M, D, true, rpc);
   hipLaunchKernelGGL(fp8_gelu_cast_kernel<M_CAST_SUM>, dim3(D / kTile, nchunk), dim3(256), 0, s, x, nullptr, nullptr,
-                     M, D, rpc, 0, scale, out, out_t, amax_probe() ? nullptr : amax, part, striped);
+                     M, D, rpc, 0, scale, out, out_t, amax_probe() ? nullptr : amax, part, striped | store_probe());
   return nchunk;
 }
 
