@@ -87,17 +87,23 @@ __device__ __forceinline__ void tile_emit(const Pre& p, const float* bl, float s
         for (int q = 0; q < 4; ++q) *reinterpret_cast<float4*>(b + 4 * q) = reinterpret_cast<const float4*>(bl + cc)[q];
       }
 #pragma unroll
-      for (int j = 0; j < 16; ++j) {
+      for (int j = 0; j < 16; j += 2) {
         if (MODE == M_GELU) {
-          v[j] = bf2f(f2bf(gelu_f(v[j] + b[j], tanh_form)));
+          const gf2 r = gelu2(gf2{v[j] + b[j], v[j + 1] + b[j + 1]}, tanh_form);
+          v[j] = bf2f(f2bf(r.x));
+          v[j + 1] = bf2f(f2bf(r.y));
         } else if (MODE == M_GELU_BWD) {
-          const float a = g[j] * gelu_grad(v[j] + b[j], tanh_form);
-          cs[j] += a;
-          v[j] = bf2f(f2bf(a));
+          const gf2 a = gf2{g[j], g[j + 1]} * gelu_grad2(gf2{v[j] + b[j], v[j + 1] + b[j + 1]}, tanh_form);
+          cs[j] += a.x;
+          cs[j + 1] += a.y;
+          v[j] = bf2f(f2bf(a.x));
+          v[j + 1] = bf2f(f2bf(a.y));
         } else if (MODE == M_CAST_SUM) {
           cs[j] += v[j];
+          cs[j + 1] += v[j + 1];
         }
         am = fmaxf(am, fabsf(v[j]));
+        am = fmaxf(am, fabsf(v[j + 1]));
       }
 #pragma unroll
       for (int q = 0; q < 4; ++q)

@@ -23,7 +23,11 @@ __global__ __launch_bounds__(256) void bias_gelu_fwd_kernel(const T* __restrict_
     if (bias) Vec4<float>::ld(bias, c, b);
     else b[0] = b[1] = b[2] = b[3] = 0.f;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = gelu_f(v[j] + b[j], tanh_form);
+    for (int j = 0; j < 4; j += 2) {
+      const gf2 r = gelu2(gf2{v[j] + b[j], v[j + 1] + b[j + 1]}, tanh_form);
+      v[j] = r.x;
+      v[j + 1] = r.y;
+    }
     Vec4<T>::st(y, i * 4, v);
   }
 }
@@ -82,9 +86,11 @@ __global__ __launch_bounds__(256) void strip_kernel(const T* __restrict__ dy, co
         Vec8<T>::ld(x + r * D + c, v0);
         Vec8<T>::ld(x + (r + 4) * D + c, v1);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          g0[j] *= gelu_grad(v0[j] + b[j], tanh_form);
-          g1[j] *= gelu_grad(v1[j] + b[j], tanh_form);
+        for (int j = 0; j < 8; j += 2) {
+          const gf2 d0 = gf2{g0[j], g0[j + 1]} * gelu_grad2(gf2{v0[j] + b[j], v0[j + 1] + b[j + 1]}, tanh_form);
+          const gf2 d1 = gf2{g1[j], g1[j + 1]} * gelu_grad2(gf2{v1[j] + b[j], v1[j + 1] + b[j + 1]}, tanh_form);
+          g0[j] = d0.x; g0[j + 1] = d0.y;
+          g1[j] = d1.x; g1[j + 1] = d1.y;
         }
         Vec8<T>::st(dx + r * D + c, g0);
         Vec8<T>::st(dx + (r + 4) * D + c, g1);
@@ -99,7 +105,10 @@ __global__ __launch_bounds__(256) void strip_kernel(const T* __restrict__ dy, co
         float v0[8];
         Vec8<T>::ld(x + r * D + c, v0);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) g0[j] *= gelu_grad(v0[j] + b[j], tanh_form);
+        for (int j = 0; j < 8; j += 2) {
+          const gf2 d0 = gf2{g0[j], g0[j + 1]} * gelu_grad2(gf2{v0[j] + b[j], v0[j + 1] + b[j + 1]}, tanh_form);
+          g0[j] = d0.x; g0[j + 1] = d0.y;
+        }
         Vec8<T>::st(dx + r * D + c, g0);
       }
 #pragma unroll
@@ -138,9 +147,11 @@ __global__ __launch_bounds__(256) void gelu_fwd_strip_kernel(const T* __restrict
     Vec8<T>::ld(x + r * D + c, v0);
     Vec8<T>::ld(x + (r + 4) * D + c, v1);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      v0[j] = gelu_f(v0[j] + b[j], tanh_form);
-      v1[j] = gelu_f(v1[j] + b[j], tanh_form);
+    for (int j = 0; j < 8; j += 2) {
+      const gf2 q0 = gelu2(gf2{v0[j] + b[j], v0[j + 1] + b[j + 1]}, tanh_form);
+      const gf2 q1 = gelu2(gf2{v1[j] + b[j], v1[j + 1] + b[j + 1]}, tanh_form);
+      v0[j] = q0.x; v0[j + 1] = q0.y;
+      v1[j] = q1.x; v1[j + 1] = q1.y;
     }
     Vec8<T>::st(y + r * D + c, v0);
     Vec8<T>::st(y + (r + 4) * D + c, v1);
@@ -149,7 +160,10 @@ __global__ __launch_bounds__(256) void gelu_fwd_strip_kernel(const T* __restrict
     float v0[8];
     Vec8<T>::ld(x + r * D + c, v0);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v0[j] = gelu_f(v0[j] + b[j], tanh_form);
+    for (int j = 0; j < 8; j += 2) {
+      const gf2 q0 = gelu2(gf2{v0[j] + b[j], v0[j + 1] + b[j + 1]}, tanh_form);
+      v0[j] = q0.x; v0[j + 1] = q0.y;
+    }
     Vec8<T>::st(y + r * D + c, v0);
   }
 }
