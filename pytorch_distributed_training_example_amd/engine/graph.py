@@ -39,6 +39,21 @@ def make_miopen_capture_safe() -> None:
     torch.backends.cudnn.benchmark = True
 
 
+def _drain_pg_watchdog(wait_s: float = 0.25) -> None:
+    """Let the RCCL process group's watchdog retire the (completed) collectives of the warm-up
+    iterations before a capture starts: its thread polls each pending work's completion event every
+    ~100 ms, and a poll that lands while the capture is in progress has been seen to fail with
+    hipErrorCapturedEvent and abort the process (1 of ~8 graphed runs in round 5, none with the
+    list empty). The device is already synchronized, so one sweep retires everything; one-time cost."""
+    import time
+    try:
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized() and dist.get_backend() == "nccl":
+            time.sleep(wait_s)
+    except Exception:  # pragma: no cover - no process group / CPU-only build
+        pass
+
+
 class StaticStep:
     """Capture ``fn(*static_inputs) -> loss`` into a hipGraph and replay it.
 
@@ -66,6 +81,7 @@ class StaticStep:
                 self.static_loss = self.fn(*self.static_inputs)
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
+        _drain_pg_watchdog()
         self.graph = torch.cuda.CUDAGraph()
         # thread_local: the RCCL process group's watchdog thread polls completion events of collectives
         # issued before the capture; under the default "global" mode HIP rejects those queries while any
