@@ -45,10 +45,18 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f4 __attribute__((ext_vector_type(4)));
 #define PDT_LDS __attribute__((address_space(3)))
 
-constexpr int kBM = 256, kBN = 256, kBK = 64, kThreads = 512;
-constexpr int kStage = (kBM + kBN) * kBK * 2;  // 64 KB
-constexpr int kEpiStride = kBN * 2 + 16;       // staged bf16 output rows (padded)
-constexpr int kLds = 2 * kStage > kBM * kEpiStride ? 2 * kStage : kBM * kEpiStride;
+constexpr int kBM = 256, kBK = 64, kThreads = 512;
+// Tile 256 x BN: BN = 256, or 128 for shapes with fewer 256 x 256 tiles than ~1.5 waves of CUs
+// (gpt2_proj / gpt2_fc2: 128 tiles on 256 CUs; vit_proj: 297) — twice the tiles, wave tiles
+// 128 x 32, half the MFMAs per phase.
+template <int BN>
+struct GT {
+  static constexpr int kStage = (kBM + BN) * kBK * 2;  // 64 / 48 KB
+  static constexpr int kEpiStride = BN * 2 + 16;       // staged bf16 output rows (padded)
+  static constexpr int kLds = 2 * kStage > kBM * kEpiStride ? 2 * kStage : kBM * kEpiStride;
+  static constexpr int WC = BN / 4, NJ = WC / 16, NH = NJ / 2;  // wave columns, 16-col blocks, per phase
+  static constexpr int kBI = BN / 32;                          // DMA instructions of a B-loading wave
+};
 
 enum { EPI_NONE = 0, EPI_BIAS = 1, EPI_GELU = 2 };
 
@@ -95,7 +103,7 @@ __device__ __forceinline__ uint32_t pack2(float a, float b) {
   return (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)a) | ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)b) << 16);
 }
 
-template <int EPI>
+template <int EPI, int BN>
 __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __restrict__ A,
                                                                const uint16_t* __restrict__ B, uint16_t* __restrict__ C,
                                                                uint16_t* __restrict__ G, const void* __restrict__ bias,
@@ -103,20 +111,24 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 2, wc = wid & 3;
-  const int ntn = N / kBN, ntm = (M + kBM - 1) / kBM;
+  using T = GT<BN>;
+  constexpr int kStage = T::kStage, kEpiStride = T::kEpiStride, WC = T::WC, NJ = T::NJ, NH = T::NH;
+  const int ntn = N / BN, ntm = (M + kBM - 1) / kBM;
   const int id = xcd_remap(blockIdx.x, gridDim.x);
   // groups of kGroup A bands: consecutive ids (one XCD) cover kGroup bands x a few N tiles, so the
   // tiles resident on an XCD at once share both operands in its L2
   const int gband = (id / (kGroup * ntn)) * kGroup, gsize = min(ntm - gband, kGroup), gi = id % (kGroup * ntn);
-  const int m0 = (gband + gi % gsize) * kBM, n0 = (gi / gsize) * kBN;
+  const int m0 = (gband + gi % gsize) * kBM, n0 = (gi / gsize) * BN;
   const int nk = K / kBK;
 
   // DMA: waves 0-3 (wave row 0) stage the B rows of the image, waves 4-7 (row 1) the A rows — each
-  // wave 64 rows as 8 instructions of 8 rows; lane -> (row + lane / 8, physical chunk lane % 8).
-  // Instructions 0-3 are half 0 of the wave's share, 4-7 half 1.
+  // A wave 64 rows as 8 instructions of 8 rows, each B wave BN / 4 rows (8 or 4 instructions); lane ->
+  // (row + lane / 8, physical chunk lane % 8). The first half of a wave's instructions is half 0 of
+  // its share, the rest half 1.
   const bool loads_b = wid < 4;
   const uint16_t* const src = loads_b ? B : A;
-  const int rbase = loads_b ? kBM + wid * 64 : (wid - 4) * 64;  // first LDS row of this wave's share
+  const int rbase = loads_b ? kBM + wid * WC : (wid - 4) * 64;  // first LDS row of this wave's share
+  const int nI = loads_b ? T::kBI : 8;                         // (wave-uniform)
   int off[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -129,17 +141,18 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
     if (PDT_GEMM_PROBE == 2) return;
     char* st = lds + (t & 1) * kStage + rbase * 128;
 #pragma unroll
-    for (int j = half * 4; j < half * 4 + 4; ++j)
-      __builtin_amdgcn_global_load_lds(src + (off[j] + t * kBK), (PDT_LDS void*)(st + j * 1024), 16, 0, 0);
+    for (int j = 0; j < 8; ++j)
+      if (j >= half * (nI / 2) && j < (half + 1) * (nI / 2))  // (wave-uniform)
+        __builtin_amdgcn_global_load_lds(src + (off[j] + t * kBK), (PDT_LDS void*)(st + j * 1024), 16, 0, 0);
   };
 
   const int lrow = lane & 15, lchk = lane >> 4;
-  f4 acc[8][4];
+  f4 acc[8][NJ];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 a[4][2], b0[2][2], b1[2][2];
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 a[4][2], b0[NH][2], b1[NH][2];
 
   auto read_a = [&](const char* SA, int aq) {
 #pragma unroll
@@ -148,27 +161,29 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
       for (int kk = 0; kk < 2; ++kk)
         a[i][kk] = *reinterpret_cast<const bf16x8*>(SA + swz(wr * 128 + aq * 64 + i * 16 + lrow, kk * 4 + lchk));
   };
-  auto read_b = [&](const char* SB, int bq, bf16x8 (&b)[2][2]) {
+  auto read_b = [&](const char* SB, int bq, bf16x8 (&b)[NH][2]) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < NH; ++j)
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
-        b[j][kk] = *reinterpret_cast<const bf16x8*>(SB + swz(kBM + wc * 64 + bq * 32 + j * 16 + lrow, kk * 4 + lchk));
+        b[j][kk] = *reinterpret_cast<const bf16x8*>(SB + swz(kBM + wc * WC + bq * (WC / 2) + j * 16 + lrow,
+                                                             kk * 4 + lchk));
   };
-  auto quad = [&](int aq, int bq, const bf16x8 (&b)[2][2]) {
+  auto quad = [&](int aq, int bq, const bf16x8 (&b)[NH][2]) {
     if (PDT_GEMM_PROBE == 1) {  // keep the fragment reads alive without the MFMAs
 #pragma unroll
       for (int i = 0; i < 4; ++i) asm volatile("" ::"v"(a[i][0]), "v"(a[i][1]));
-      asm volatile("" ::"v"(b[0][0]), "v"(b[0][1]), "v"(b[1][0]), "v"(b[1][1]));
+#pragma unroll
+      for (int j = 0; j < NH; ++j) asm volatile("" ::"v"(b[j][0]), "v"(b[j][1]));
       return;
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < NH; ++j)
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk)
-          acc[aq * 4 + i][bq * 2 + j] = mfma(b[j][kk], a[i][kk], acc[aq * 4 + i][bq * 2 + j]);  // D[n][m]
+          acc[aq * 4 + i][bq * NH + j] = mfma(b[j][kk], a[i][kk], acc[aq * 4 + i][bq * NH + j]);  // D[n][m]
   };
 
   // Pipeline (intervals = barrier-delimited; row 0 loads in even ones, row 1 in odd ones): the B
@@ -179,8 +194,12 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
   issue(0, 0);
   issue(0, 1);
   if (nk > 1) issue(1, 0);
-  if (nk > 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (nk > 1) {  // step 0's share landed: younger are step 1's half 0 (nI / 2 instructions)
+    if (nI == 8) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   bar();
   if (wr == 1) bar();  // row 1 runs one barrier behind row 0
 
@@ -221,7 +240,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) t += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+      for (int j = 0; j < NJ; ++j) t += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
     if (t == 1234.5f) C[tid] = 1;
     return;
   }
@@ -229,10 +248,10 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
   // is staged through LDS (free now: every read and DMA has retired) and written as whole 512-B
   // row segments — 8-B stores straight from the accumulators hit each 128-B line four times and
   // ran the write-out at ~1 TB/s. EPI_GELU stages H, then G.
-  float bv[4][4];
+  float bv[NJ][4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int n = n0 + wc * 64 + j * 16 + 4 * lchk;
+  for (int j = 0; j < NJ; ++j) {
+    const int n = n0 + wc * WC + j * 16 + 4 * lchk;
 #pragma unroll
     for (int e = 0; e < 4; ++e) bv[j][e] = 0.f;
     if constexpr (EPI != EPI_NONE) {
@@ -253,7 +272,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < NJ; ++j) {
         f4 v = acc[i][j];
         uint2 pk;
         if constexpr (EPI == EPI_GELU) {
@@ -267,12 +286,12 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
         } else {
           pk = make_uint2(pack2(v[0] + bv[j][0], v[1] + bv[j][1]), pack2(v[2] + bv[j][2], v[3] + bv[j][3]));
         }
-        *reinterpret_cast<uint2*>(lds + (wr * 128 + i * 16 + lrow) * kEpiStride + (wc * 64 + j * 16 + 4 * lchk) * 2) = pk;
+        *reinterpret_cast<uint2*>(lds + (wr * 128 + i * 16 + lrow) * kEpiStride + (wc * WC + j * 16 + 4 * lchk) * 2) = pk;
       }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     bar();
-    for (int idx = tid; idx < kBM * (kBN / 8); idx += kThreads) {
-      const int r = idx / (kBN / 8), c = idx % (kBN / 8);
+    for (int idx = tid; idx < kBM * (BN / 8); idx += kThreads) {
+      const int r = idx / (BN / 8), c = idx % (BN / 8);
       const int m = m0 + r;
       if (m < M)
         *reinterpret_cast<uint4*>(out + (int64_t)m * N + n0 + c * 8) =
@@ -286,32 +305,55 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
   }
 }
 
-template <int EPI>
-int launch(const uint16_t* A, const uint16_t* B, uint16_t* C, uint16_t* G, const void* bias, int bias_f32,
-           int tanh_form, int M, int N, int K, hipStream_t s) {
+template <int EPI, int BN>
+int launch_bn(const uint16_t* A, const uint16_t* B, uint16_t* C, uint16_t* G, const void* bias, int bias_f32,
+              int tanh_form, int M, int N, int K, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_kernel<EPI>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, kLds) != hipSuccess)
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_kernel<EPI, BN>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, GT<BN>::kLds) != hipSuccess)
       return -3;
     attr = true;
   }
-  const int64_t grid = (int64_t)((M + kBM - 1) / kBM) * (N / kBN);
-  hipLaunchKernelGGL(gemm_nt_kernel<EPI>, dim3((unsigned)grid), dim3(kThreads), kLds, s, A, B, C, G, bias, bias_f32,
-                     tanh_form, M, N, K);
+  const int64_t grid = (int64_t)((M + kBM - 1) / kBM) * (N / BN);
+  hipLaunchKernelGGL((gemm_nt_kernel<EPI, BN>), dim3((unsigned)grid), dim3(kThreads), GT<BN>::kLds, s, A, B, C, G, bias,
+                     bias_f32, tanh_form, M, N, K);
   return hipPeekAtLastError() == hipSuccess ? 0 : -4;  // a refused launch fails loudly, not as garbage
+}
+
+// 256 x 256 tiles unless they fill at most one wave of the 256 CUs (then 256 x 128: twice the tiles).
+// Measured (profiles/r5/gemm_bn128.txt): 128 tiles of 256 x 256 (GPT-2 proj / fc2) run 18% / 13% faster
+// as 256 x 128; 297 tiles (ViT proj / fc2) run 6% / 9% slower. PDT_GEMM_BN=128 / 256 forces one (A/B).
+inline int pick_bn(int M, int N) {
+  static int forced = -1;
+  if (forced < 0) {
+    const char* e = getenv("PDT_GEMM_BN");
+    forced = (e && e[0]) ? (int)strtol(e, nullptr, 10) : 0;
+  }
+  if (forced == 128 && N % 128 == 0) return 128;
+  if (forced == 256 && N % 256 == 0) return 256;
+  if (N % 256 != 0) return 128;
+  const int64_t tiles = (int64_t)((M + kBM - 1) / kBM) * (N / 256);
+  return tiles <= 256 ? 128 : 256;
+}
+
+template <int EPI>
+int launch(const uint16_t* A, const uint16_t* B, uint16_t* C, uint16_t* G, const void* bias, int bias_f32,
+           int tanh_form, int M, int N, int K, hipStream_t s) {
+  return pick_bn(M, N) == 128 ? launch_bn<EPI, 128>(A, B, C, G, bias, bias_f32, tanh_form, M, N, K, s)
+                              : launch_bn<EPI, 256>(A, B, C, G, bias, bias_f32, tanh_form, M, N, K, s);
 }
 
 }  // namespace
 
 extern "C" {
 
-// C[M, N] (and G for epi 2) from A[M, K] and B[N, K], all row-major contiguous bf16.
+// C[M, N] (and G for epi 2) from A[M, K] and B[N, K], all row-major contiguous bf16; N % 128 == 0.
 // epi: 0 none, 1 + bias, 2 C = A·Bᵀ and G = gelu(C + bias) (tanh_form: GPT-2's tanh GELU).
 // bias: [N] fp32 (bias_f32 = 1) or bf16, may be null. Returns 0, or < 0 when the shape is not served.
 int pdt_gemm_nt(const uint16_t* A, const uint16_t* B, uint16_t* C, uint16_t* G, const void* bias, int bias_f32,
                 int epi, int tanh_form, int M, int N, int K, hipStream_t s) {
-  if (M < 1 || N % kBN != 0 || K % kBK != 0 || N < kBN || K < kBK) return -1;
+  if (M < 1 || N % 128 != 0 || K % kBK != 0 || N < 128 || K < kBK) return -1;
   if ((int64_t)M * K >= (int64_t)1 << 31 || (int64_t)N * K >= (int64_t)1 << 31) return -2;
   if (epi == EPI_GELU && G == nullptr) return -1;
   switch (epi) {

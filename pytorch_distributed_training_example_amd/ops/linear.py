@@ -49,9 +49,9 @@ def _wgrad(dy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
 
 
 def gemm_nt_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
-    """Shapes our GEMM kernel serves: bf16, out features % 256, in features % 64."""
+    """Shapes our GEMM kernel serves: bf16, out features % 128, in features % 64."""
     return (x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and w.dim() == 2
-            and w.shape[0] % 256 == 0 and w.shape[1] % 64 == 0 and x.shape[-1] == w.shape[1] and x.numel() > 0)
+            and w.shape[0] % 128 == 0 and w.shape[1] % 64 == 0 and x.shape[-1] == w.shape[1] and x.numel() > 0)
 
 
 def _ours(x: torch.Tensor, w: torch.Tensor) -> bool:

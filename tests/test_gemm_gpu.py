@@ -19,7 +19,7 @@ def _rel(a, b):
 
 
 @pytest.mark.parametrize("M,K,N", [(256, 64, 256), (300, 128, 512), (1000, 768, 768), (4096, 1024, 3072),
-                                   (25216 // 8, 3072, 768)])
+                                   (25216 // 8, 3072, 768), (8192, 256, 3072), (1000, 128, 384)])
 @pytest.mark.parametrize("epi", [0, 1, 2])
 def test_gemm_nt_matches_fp32(M, K, N, epi):
     g = torch.Generator(device="cuda").manual_seed(M + K + N + epi)
