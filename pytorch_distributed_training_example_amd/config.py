@@ -60,6 +60,8 @@ PDT_FP8_WEIGHT_MULTI        1            fp8: every Linear weight cast in one la
 PDT_FP8_CAST_COLSUM         1            fp8: a Linear's output-gradient cast also yields its bias gradient
 PDT_FP8_LN                  1            fp8: the add+LayerNorm in front of qkv / fc1 writes its output as e4m3 +
                                          transpose for that GEMM (layernorm.hip ln_fwd_fp8_kernel): no bf16 y
+PDT_WGRAD_STREAM_M          0            conv weight gradients with <= this many output pixels run on a side
+                                         stream, concurrent with their data gradient (0 = in-stream)
 """
 from __future__ import annotations
 
@@ -72,7 +74,7 @@ class _Switches:
                  "conv_bn_stats", "bn_bwd_stats", "res_masked", "stem_bwd_fused", "stem_bn_wgrad", "stem_bn_stats", "stem_pool_wgrad", "wgrad_splitk", "slice_sum",
                  "subsample_native", "linear_splitk", "fused_addln", "embedding_native", "linear_epilogue",
                  "bwd_fused", "bwd_fused_shapes", "bn2_defer", "bn_apply_gemm_k", "strided_bstats", "gap_native",
-                 "fp8_fused_gelu", "fp8_weight_multi", "fp8_cast_colsum", "fp8_ln")
+                 "fp8_fused_gelu", "fp8_weight_multi", "fp8_cast_colsum", "fp8_ln", "wgrad_stream_m")
 
     def __init__(self):
         self.reload()
@@ -125,6 +127,9 @@ class _Switches:
         self.fp8_weight_multi = on("PDT_FP8_WEIGHT_MULTI")
         self.fp8_cast_colsum = on("PDT_FP8_CAST_COLSUM")
         self.fp8_ln = on("PDT_FP8_LN")
+        # conv weight gradients of at most this many output pixels run on a side stream, concurrent
+        # with their data gradient (0 = off): small-batch grids leave CUs idle (ops/conv.py _WgradFork)
+        self.wgrad_stream_m = int(e("PDT_WGRAD_STREAM_M", "0"))
         return self
 
 

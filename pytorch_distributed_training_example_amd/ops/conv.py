@@ -87,8 +87,44 @@ def _ensure_table() -> None:
     if SW.conv1x1_dump:
         atexit.register(dump_table, SW.conv1x1_dump)
 
-# Weight gradients run in-stream: a side stream for them measured 4 % SLOWER on ResNet-50 (10,212
-# vs 10,617 img/s, round 2) — both streams' kernels already fill the chip — and was removed.
+# Weight gradients run in-stream by default: a side stream for them measured 4 % SLOWER on ResNet-50 at
+# 1024 images (10,212 vs 10,617 img/s, round 2) — both streams' kernels already fill the chip. At small
+# per-GPU batches (128 / rank: layer 3-4 grids of 200-400 workgroups on 256 CUs) the data and weight
+# gradient of one conv can share the chip: PDT_WGRAD_STREAM_M (SW.wgrad_stream_m) sends the weight
+# gradients of convs with at most that many output pixels to a side stream.
+_SIDE = {}
+
+
+class _WgradFork:
+    """Fork point of one conv backward: created BEFORE the data gradient is queued (an event on the current
+    stream), ``run(fn)`` launches the weight gradient on the side stream after that event — so it overlaps
+    the data gradient — and joins the current stream to it before returning (the gradient is consumed on
+    the current stream right after the backward returns). Inside hipGraph capture the event fork / join
+    become graph edges. Off (plain call) unless SW.wgrad_stream_m >= M."""
+
+    __slots__ = ("cur", "ev")
+
+    def __init__(self, t: torch.Tensor, M: int):
+        self.cur = self.ev = None
+        if SW.wgrad_stream_m and M <= SW.wgrad_stream_m and t.is_cuda:
+            self.cur = torch.cuda.current_stream(t.device)
+            self.ev = torch.cuda.Event()
+            self.ev.record(self.cur)
+
+    def run(self, fn):
+        if self.cur is None:
+            return fn()
+        dev = self.cur.device
+        s = _SIDE.get(dev)
+        if s is None:
+            s = _SIDE[dev] = torch.cuda.Stream(device=dev)
+        s.wait_event(self.ev)
+        with torch.cuda.stream(s):
+            dw = fn()
+        if dw is not None:
+            dw.record_stream(self.cur)  # allocated on the side stream, read on the current one
+        self.cur.wait_stream(s)
+        return dw
 
 
 def _ours_ok(direction: str, M: int, K: int, N: int) -> bool:
@@ -351,6 +387,7 @@ class _Conv1x1Fn(torch.autograd.Function):
         gy = gy.contiguous(memory_format=torch.channels_last)
         x2, g2, w2 = _nhwc2d(x), _nhwc2d(gy), weight.reshape(Co, Ci)
         M = x2.shape[0]
+        fork = _WgradFork(gy, M)
         dx = None
 
         def conv_bwd(mask):
@@ -379,7 +416,7 @@ class _Conv1x1Fn(torch.autograd.Function):
                                           c_W=W)
             gs.deposit(gpart, dx)
             strided = None
-            return dx, _Conv1x1Fn._wgrad(ctx, g2, x2, x, gy, weight, M, Ci, Co)
+            return dx, _Conv1x1Fn._wgrad(ctx, g2, x2, x, gy, weight, M, Ci, Co, fork)
         # dx is final (nothing is added to it after the GEMM) unless this is the first of two linked
         # branches or a strided shortcut's gradient is added below: only then can the GEMM's epilogue
         # take the producing BatchNorm's backward reduction (GradStatsSource)
@@ -435,12 +472,12 @@ class _Conv1x1Fn(torch.autograd.Function):
             gs.deposit(gpart, dx)
         if first and dx is not None:  # first of the two branches: leave dx for the partner to add to
             ctx.link.grad, dx = dx, None
-        return dx, _Conv1x1Fn._wgrad(ctx, g2, x2, x, gy, weight, M, Ci, Co)
+        return dx, _Conv1x1Fn._wgrad(ctx, g2, x2, x, gy, weight, M, Ci, Co, fork)
 
     @staticmethod
-    def _wgrad(ctx, g2, x2, x, gy, weight, M, Ci, Co):
+    def _wgrad(ctx, g2, x2, x, gy, weight, M, Ci, Co, fork=None):
         """dW of a 1x1 conv (None when not needed): the fastest of MIOpen / one GEMM / split-K GEMMs /
-        our one-pass kernel for the shape."""
+        our one-pass kernel for the shape (on the side stream when ``fork`` is active, see _WgradFork)."""
         dw = None
 
         def conv_bwd(mask):
@@ -468,7 +505,7 @@ class _Conv1x1Fn(torch.autograd.Function):
                 wfn = lambda: _wgrad_splitk(g2, x2, sk).as_strided(weight.shape, weight.stride())  # noqa: E731
             else:
                 wfn = lambda: conv_bwd([False, True, False])[1]  # noqa: E731
-            dw = wfn()
+            dw = fork.run(wfn) if fork is not None else wfn()
         return dw
 
 
@@ -653,6 +690,7 @@ class _Conv3x3Fn(torch.autograd.Function):
         from ._native import native
         x, weight = ctx.saved_tensors
         gy = gy.contiguous(memory_format=torch.channels_last)
+        fork = _WgradFork(gy, gy.shape[0] * gy.shape[2] * gy.shape[3])
         dx = dw = None
         if ctx.needs_input_grad[0]:
             gs = ctx.gsrc if ctx.gsrc is not None and ctx.gsrc.ready() else None
@@ -665,7 +703,7 @@ class _Conv3x3Fn(torch.autograd.Function):
                 dx = native().conv3x3s1_fwd(gy, _flip_of(weight))
         if ctx.needs_input_grad[1]:
             if SW.conv3x3_wgrad == "ours":
-                dw = native().conv3x3s1_wgrad(x, gy)
+                dw = fork.run(lambda: native().conv3x3s1_wgrad(x, gy))
             if dw is None:
                 args = (gy, x, weight, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1)
                 dw = torch.ops.aten.convolution_backward(*args, [False, True, False])[1]
@@ -697,6 +735,7 @@ class _Conv3x3S2Fn(torch.autograd.Function):
         from ._native import native
         x, weight = ctx.saved_tensors
         gy = gy.contiguous(memory_format=torch.channels_last)
+        fork = _WgradFork(gy, gy.shape[0] * gy.shape[2] * gy.shape[3])
         args = (gy, x, weight, None, [2, 2], [1, 1], [1, 1], False, [0, 0], 1)
         dx = dw = None
         if ctx.needs_input_grad[0]:
@@ -712,7 +751,7 @@ class _Conv3x3S2Fn(torch.autograd.Function):
                 dx = torch.ops.aten.convolution_backward(*args, [True, False, False])[0]
         if ctx.needs_input_grad[1]:
             if SW.conv3x3_wgrad == "ours":
-                dw = native().conv3x3s2_wgrad(x, gy)
+                dw = fork.run(lambda: native().conv3x3s2_wgrad(x, gy))
             if dw is None:
                 dw = torch.ops.aten.convolution_backward(*args, [False, True, False])[1]
         return dx, dw, None, None

@@ -110,3 +110,29 @@ def test_graph_replay_survives_other_models_training_forward():
     assert torch.equal(lg, le), (lg, le)
     bad = [i for i, (a, b) in enumerate(zip(gg, ge)) if not torch.equal(a, b)]
     assert not bad, f"{len(bad)} of {len(ge)} gradients differ (first: {bad[:5]})"
+
+
+@pytest.mark.parametrize("arch", ["resnet18", "resnet50"])
+def test_side_stream_wgrad_matches_in_stream(arch):
+    """Weight gradients on the side stream (ops/conv.py _WgradFork, PDT_WGRAD_STREAM_M): the same kernels
+    on other streams, joined before the gradient is consumed — eager AND the captured graph (fork / join
+    as graph edges) must equal the in-stream eager step bit for bit (lr = 0: gradients compared)."""
+    from pytorch_distributed_training_example_amd.config import SW
+    from pytorch_distributed_training_example_amd.models import get_model
+    from pytorch_distributed_training_example_amd.models.precision import to_bf16_mixed
+    torch.manual_seed(0)
+    base = to_bf16_mixed(get_model(arch, num_classes=16).cuda().to(memory_format=torch.channels_last))
+    xs, ys = _data()
+    old = SW.wgrad_stream_m
+    try:
+        SW.wgrad_stream_m = 0
+        le, _, ge = _run(base, "eager", 0.0, xs, ys)
+        SW.wgrad_stream_m = 1 << 30
+        ls, _, gs = _run(base, "eager", 0.0, xs, ys)
+        lg, _, gg = _run(base, "graph", 0.0, xs, ys)
+    finally:
+        SW.wgrad_stream_m = old
+    for tag, l2, g2 in (("eager", ls, gs), ("graph", lg, gg)):
+        assert torch.equal(l2, le), (tag, l2, le)
+        bad = [i for i, (a, b) in enumerate(zip(g2, ge)) if not torch.equal(a, b)]
+        assert not bad, f"{tag}: {len(bad)} of {len(ge)} gradients differ (first: {bad[:5]})"
