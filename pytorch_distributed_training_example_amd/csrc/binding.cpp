@@ -1151,10 +1151,8 @@ std::vector<Tensor> bn_fwd_train_tiles(Tensor x, Tensor part, c10::optional<Tens
                                         (relu && apply) ? mask.data_ptr<uint8_t>() : nullptr, mean.data_ptr<float>(),
                                         invstd.data_ptr<float>(), ws.data_ptr<float>(), stream());
   TORCH_CHECK(rc == 0, "pdt_bn_fwd_train_tiles failed: ", rc);
-  if (!apply) {
-    const int64_t P = (T + 127) / 128;
-    return {Tensor(), Tensor(), mean, invstd, ws.narrow(0, 4 * P * C, 2 * C).view({2, C})};
-  }
+  if (!apply)  // the apply coefficients (a, b) are the workspace's last 2C floats (past the level-1 sums)
+    return {Tensor(), Tensor(), mean, invstd, ws.narrow(0, ws.numel() - 2 * C, 2 * C).view({2, C})};
   return {y, mask, mean, invstd};
 }
 

@@ -416,16 +416,28 @@ __global__ __launch_bounds__(1024) void bn_fin_kernel(const float* __restrict__ 
 // between-tile term in double, so E[x^2] - mean^2 never cancels in fp32. Level 2 finalizes.
 // CENTRED = false (backward partials: sum dz, sum dz (x - mean)): plain double sums, Q = sum_t q_t.
 // NCNT: partial t covers part[2 T C + t] rows (float) instead of BMt (the stem conv's per-wave partials).
-constexpr int kTilesPerBlock = 128;
+// Tiles per level-1 block (PDT_BN_TILES_PER_BLOCK, read once; a multiple of 16): 128. 32 (each of a block's
+// 16 row groups sums two tiles, one round of loads, 4x the blocks) measured no faster — 10,874-10,914 vs
+// 10,909-10,925 img/s at 128 / GPU graphed, 15,309 vs 15,387 at 1024 (profiles/r5/bn_tiles_per_block.txt):
+// the ~5-12 us of these launches is launch / tail latency, not their loads.
+int g_tiles_per_block = 0;
+inline int tiles_per_block() {
+  if (g_tiles_per_block == 0) {
+    const char* e = getenv("PDT_BN_TILES_PER_BLOCK");
+    const int v = (e && e[0]) ? (int)strtol(e, nullptr, 10) : 128;
+    g_tiles_per_block = (v >= 16 && v % 16 == 0) ? v : 128;
+  }
+  return g_tiles_per_block;
+}
 int g_tiles_fused = 1;  // pdt_bn_tiles_fused(0): the two-launch finalize (A/B)
 
 template <bool CENTRED, bool NCNT = false>
 __global__ __launch_bounds__(1024) void bn_tiles_l1_kernel(const float* __restrict__ part, int T, int BMt, int64_t M,
-                                                           int C, double* __restrict__ out) {
+                                                           int C, double* __restrict__ out, int tpb) {
   __shared__ double sm[2][16][64];
   const int tid = threadIdx.x, cl = tid & 63, j = tid >> 6;
   const int c = blockIdx.x * 64 + cl;
-  const int t0 = blockIdx.y * kTilesPerBlock, t1 = min(T, t0 + kTilesPerBlock);
+  const int t0 = blockIdx.y * tpb, t1 = min(T, t0 + tpb);
   double S = 0.0, Q = 0.0;
 #pragma unroll 4
   for (int t = t0 + j; t < t1; t += 16) {
@@ -478,13 +490,13 @@ __device__ unsigned g_tiles_ctr[64];  // one per 64-channel column (C <= 4096), 
 
 template <bool CENTRED, bool NCNT = false>
 __global__ __launch_bounds__(1024) void bn_tiles_fin_kernel(const float* __restrict__ part, int T, int BMt, int64_t M,
-                                                            int C, double* __restrict__ lv, FinArgs fa) {
+                                                            int C, double* __restrict__ lv, FinArgs fa, int tpb) {
   __shared__ double sm[2][16][64];
   __shared__ int last;
   const int tid = threadIdx.x, cl = tid & 63, j = tid >> 6;
   const int c = blockIdx.x * 64 + cl;
   const int P = gridDim.y;
-  const int t0 = blockIdx.y * kTilesPerBlock, t1 = min(T, t0 + kTilesPerBlock);
+  const int t0 = blockIdx.y * tpb, t1 = min(T, t0 + tpb);
   double S = 0.0, Q = 0.0;
 #pragma unroll 4
   for (int t = t0 + j; t < t1; t += 16) {
@@ -527,11 +539,23 @@ __global__ __launch_bounds__(1024) void bn_tiles_fin_kernel(const float* __restr
     // the P level-1 entries of the column, combined by all 16 row groups (group j takes p = j, j + 16, ...
     // in order, then group sums in order: a fixed order, deterministic). One thread per channel walking all
     // P entries serially made this tail ~10 us of dependent loads at layer 1 (P = 98).
+    // Loads 8 entries at a time (clamped indices, no branch around a load), added in the same p order.
     s = 0.0;
     q = 0.0;
-    for (int p = j; p < P; p += 16) {
-      s += __builtin_nontemporal_load(&lv[((int64_t)p * C + c) * 2]);
-      q += __builtin_nontemporal_load(&lv[((int64_t)p * C + c) * 2 + 1]);
+    for (int p0 = j; p0 < P; p0 += 16 * 8) {
+      double ts[8], tq[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int p = min(p0 + 16 * u, P - 1);
+        ts[u] = __builtin_nontemporal_load(&lv[((int64_t)p * C + c) * 2]);
+        tq[u] = __builtin_nontemporal_load(&lv[((int64_t)p * C + c) * 2 + 1]);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (p0 + 16 * u < P) {
+          s += ts[u];
+          q += tq[u];
+        }
     }
     sm[0][j][cl] = s;
     sm[1][j][cl] = q;
@@ -1080,7 +1104,7 @@ int bn_bwd_from_partials(const float* part, int T, int BMt, const uint16_t* dy, 
                          int C, int relu, int has_res, uint16_t* dx, uint16_t* dres, float* dgamma, float* dbeta,
                          float* ws, hipStream_t s, float* coef = nullptr) {
   if (relu && !mask) return -2;
-  const int P = (T + kTilesPerBlock - 1) / kTilesPerBlock;
+  const int P = (T + tiles_per_block() - 1) / tiles_per_block();
   double* lv = reinterpret_cast<double*>(ws);
   float* A = coef ? coef : ws + 4 * (int64_t)P * C;  // coef: the caller's [3][C] (A, B, D)
   float* B = A + C;
@@ -1089,9 +1113,9 @@ int bn_bwd_from_partials(const float* part, int T, int BMt, const uint16_t* dy, 
   fa.gamma = gamma; fa.invstd = invstd; fa.dgamma = dgamma; fa.dbeta = dbeta; fa.A = A; fa.B = B; fa.D = D;
   fa.M = M;
   if (g_tiles_fused && C / 64 <= 64) {
-    hipLaunchKernelGGL(bn_tiles_fin_kernel<false>, dim3(C / 64, P), dim3(1024), 0, s, part, T, BMt, M, C, lv, fa);
+    hipLaunchKernelGGL(bn_tiles_fin_kernel<false>, dim3(C / 64, P), dim3(1024), 0, s, part, T, BMt, M, C, lv, fa, tiles_per_block());
   } else {
-    hipLaunchKernelGGL(bn_tiles_l1_kernel<false>, dim3(C / 64, P), dim3(1024), 0, s, part, T, BMt, M, C, lv);
+    hipLaunchKernelGGL(bn_tiles_l1_kernel<false>, dim3(C / 64, P), dim3(1024), 0, s, part, T, BMt, M, C, lv, tiles_per_block());
     hipLaunchKernelGGL(bn_tiles_l2b_kernel, dim3((C + 255) / 256), dim3(256), 0, s, lv, P, C, fa);
   }
   if (!dx) return 0;  // coefficients only: the consumer applies them (pdt_stem_conv_wgrad_bn)
@@ -1169,7 +1193,7 @@ int pdt_bn_fwd_train(const uint16_t* x, const uint16_t* res, const float* res_a,
 
 // Workspace floats of pdt_bn_fwd_train_tiles.
 int64_t pdt_bn_tiles_ws_floats(int T, int C) {
-  const int64_t P = (T + kTilesPerBlock - 1) / kTilesPerBlock;
+  const int64_t P = (T + tiles_per_block() - 1) / tiles_per_block();
   return 4 * P * C + 2 * (int64_t)C;
 }
 
@@ -1181,7 +1205,7 @@ int pdt_bn_fwd_train_tiles(const float* part, int T, int BMt, const uint16_t* x,
                            float momentum, float eps, int64_t M, int C, int relu, uint16_t* y, uint8_t* mask,
                            float* mean, float* invstd, float* ws, hipStream_t s) {
   if (C % kCC != 0 || M < 1 || T != (int)((M + BMt - 1) / BMt)) return -1;
-  const int P = (T + kTilesPerBlock - 1) / kTilesPerBlock;
+  const int P = (T + tiles_per_block() - 1) / tiles_per_block();
   double* lv = reinterpret_cast<double*>(ws);
   float* a = ws + 4 * (int64_t)P * C;
   float* b = a + C;
@@ -1190,9 +1214,9 @@ int pdt_bn_fwd_train_tiles(const float* part, int T, int BMt, const uint16_t* x,
   fa.b_out = b; fa.running_mean = running_mean; fa.running_var = running_var; fa.momentum = momentum;
   fa.eps = eps; fa.M = M;
   if (g_tiles_fused && C / 64 <= 64) {
-    hipLaunchKernelGGL(bn_tiles_fin_kernel<true>, dim3(C / 64, P), dim3(1024), 0, s, part, T, BMt, M, C, lv, fa);
+    hipLaunchKernelGGL(bn_tiles_fin_kernel<true>, dim3(C / 64, P), dim3(1024), 0, s, part, T, BMt, M, C, lv, fa, tiles_per_block());
   } else {
-    hipLaunchKernelGGL(bn_tiles_l1_kernel<true>, dim3(C / 64, P), dim3(1024), 0, s, part, T, BMt, M, C, lv);
+    hipLaunchKernelGGL(bn_tiles_l1_kernel<true>, dim3(C / 64, P), dim3(1024), 0, s, part, T, BMt, M, C, lv, tiles_per_block());
     hipLaunchKernelGGL(bn_tiles_l2_kernel, dim3((C + 255) / 256), dim3(256), 0, s, lv, P, C, fa);
   }
   if (!y) return 0;
@@ -1243,7 +1267,7 @@ int pdt_bn_relu_maxpool_fwd_train_parts(const float* part, int P, const uint16_t
                                         float* invstd, float* ws, hipStream_t s) {
   const int64_t M = (int64_t)N * H * W;
   if (C % kCC != 0 || C / 64 > 64 || M < 1 || P < 1) return -1;
-  const int PB = (P + kTilesPerBlock - 1) / kTilesPerBlock;
+  const int PB = (P + tiles_per_block() - 1) / tiles_per_block();
   double* lv = reinterpret_cast<double*>(ws);
   float* a = ws + 4 * (int64_t)PB * C;
   float* b = a + C;
@@ -1252,7 +1276,7 @@ int pdt_bn_relu_maxpool_fwd_train_parts(const float* part, int P, const uint16_t
   fa.b_out = b; fa.running_mean = running_mean; fa.running_var = running_var; fa.momentum = momentum;
   fa.eps = eps; fa.M = M;
   // BMt = 1: unused (NCNT) but keeps the kernel's tail arithmetic in range
-  hipLaunchKernelGGL((bn_tiles_fin_kernel<true, true>), dim3(C / 64, PB), dim3(1024), 0, s, part, P, 1, M, C, lv, fa);
+  hipLaunchKernelGGL((bn_tiles_fin_kernel<true, true>), dim3(C / 64, PB), dim3(1024), 0, s, part, P, 1, M, C, lv, fa, tiles_per_block());
   const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
   hipLaunchKernelGGL(bn_apply_pool_kernel, dim3(row_grid((int64_t)N * Ho)), dim3(256), 0, s, x, a, b, y, code, N, H, W, C,
                      Ho, Wo, g_pool_contig);
