@@ -201,6 +201,8 @@ int pdt_embedding_fwd(const int64_t* idx, const uint16_t* wte, const uint16_t* w
 int64_t pdt_embedding_bwd_ws_ints(int64_t n, int V);
 int pdt_gemm_nt(const uint16_t* A, const uint16_t* B, uint16_t* C, uint16_t* G, const void* bias, int bias_f32,
                 int epi, int tanh_form, int M, int N, int K, hipStream_t s);
+int pdt_gemm_nt_fp8(const uint8_t* A, const uint8_t* B, uint16_t* C, const float* sa, const float* sb,
+                    const void* bias, int bias_f32, int epi, int M, int N, int K, hipStream_t s);
 int pdt_embedding_bwd(const int64_t* idx, const uint16_t* dout, uint16_t* dwte, uint16_t* dwpe, int* ws, int64_t n,
                       int B, int T, int V, int D, int* err, hipStream_t s);
 int64_t pdt_p2p_flags_bytes();
@@ -2021,6 +2023,35 @@ std::vector<Tensor> gemm_nt(Tensor a, Tensor b, c10::optional<Tensor> bias, int6
   return {c};
 }
 
+// fp8 e4m3 operands (csrc/kernels/gemm.hip F8): C [M, N] bf16 = (a sa)(b sb)^T (+ bias) from a [M, K], b [N, K]
+// contiguous float8_e4m3fn and one-element fp32 dequantisation scales (torch._scaled_mm's scale_a / scale_b).
+// N % 128 == 0, K % 128 == 0 (gemm_nt_fp8_ok).
+Tensor gemm_nt_fp8(Tensor a, Tensor b, Tensor sa, Tensor sb, c10::optional<Tensor> bias) {
+  check_cuda(a, "a");
+  check_cuda(b, "b");
+  TORCH_CHECK(a.scalar_type() == at::kFloat8_e4m3fn && b.scalar_type() == at::kFloat8_e4m3fn && a.dim() == 2 &&
+                  b.dim() == 2 && a.is_contiguous() && b.is_contiguous() && a.size(1) == b.size(1),
+              "gemm_nt_fp8: a [M, K], b [N, K] contiguous float8_e4m3fn");
+  TORCH_CHECK(sa.scalar_type() == at::kFloat && sb.scalar_type() == at::kFloat && sa.numel() == 1 && sb.numel() == 1 &&
+                  sa.is_cuda() && sb.is_cuda(), "gemm_nt_fp8: one-element fp32 device scales");
+  const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
+  const void* bp = nullptr;
+  int bf32 = 0;
+  if (bias.has_value() && bias->defined()) {
+    TORCH_CHECK(bias->is_contiguous() && bias->numel() == N &&
+                    (bias->scalar_type() == at::kFloat || bias->scalar_type() == at::kBFloat16),
+                "gemm_nt_fp8: bias [N] fp32 or bf16");
+    bp = bias->data_ptr();
+    bf32 = bias->scalar_type() == at::kFloat;
+  }
+  auto c = at::empty({M, N}, a.options().dtype(at::kBFloat16));
+  const int rc = pdt_gemm_nt_fp8(reinterpret_cast<const uint8_t*>(a.data_ptr()), reinterpret_cast<const uint8_t*>(b.data_ptr()),
+                                 reinterpret_cast<uint16_t*>(c.data_ptr()), sa.data_ptr<float>(), sb.data_ptr<float>(), bp,
+                                 bf32, bp ? 1 : 0, (int)M, (int)N, (int)K, stream());
+  TORCH_CHECK(rc == 0, "pdt_gemm_nt_fp8 failed (", rc, ") for M=", M, " N=", N, " K=", K);
+  return c;
+}
+
 // ---- LeNet (reference model) ops: csrc/kernels/lenet.hip ----
 constexpr int kStemIpb = 4;  // images per workgroup in the conv1 weight-gradient reduction
 
@@ -2176,6 +2207,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("target_wgs"), py::arg("variant") = -2, py::arg("interleave") = -2);
   m.def("embedding_fwd", &embedding_fwd);
   m.def("gemm_nt", &gemm_nt);
+  m.def("gemm_nt_fp8", &gemm_nt_fp8, py::arg("a"), py::arg("b"), py::arg("sa"), py::arg("sb"), py::arg("bias") = py::none());
   m.def("embedding_bwd", &embedding_bwd);
   m.def("embedding_err", &embedding_err);
   m.def("conv3x3_wgrad_tune", [](int target_wgs, int co_tile) { pdt_conv3x3_wgrad_tune(target_wgs, co_tile); });

@@ -76,6 +76,26 @@ __device__ __forceinline__ f4 mfma(bf16x8 a, bf16x8 b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
+// fp8 (F8): the same LDS images hold 128 e4m3 values per 128-B row, so one K-step is ONE block-scaled
+// v_mfma_scale_f32_16x16x128_f8f6f4 per 16 x 16 block (unit scales, e8m0 127) instead of two bf16 MFMAs:
+// twice the cycles of one bf16 16x16x32, so the same matrix-pipe time and the same fragment bytes per
+// K-step for twice the K — the bf16 kernel's LDS-read bound (header) halved per FLOP. A lane's 32 operand
+// bytes are its two bf16 fragments' 16-B chunks (chunks lchk and 4 + lchk of the row): any fixed byte ->
+// k placement shared by A and B gives the same dot product, so the hardware's k order within a lane's
+// 32 bytes never matters. The per-tensor dequantisation scales multiply the fp32 accumulators in the
+// epilogue (torch._scaled_mm semantics: C = (A sa)(B sb)^T + bias).
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f4 mfma8(i32x8 a, i32x8 b, f4 c) {
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 127, 0, 127);  // e4m3 x e4m3
+}
+// a lane's 32-B fp8 fragment: the 16-B chunks lchk and 4 + lchk of an LDS row (loaded straight into the
+// two halves of the operand's 8 consecutive VGPRs — no register copies)
+__device__ __forceinline__ i32x8 ld_frag8(const char* p0, const char* p1) {
+  const i32x4 x = *reinterpret_cast<const i32x4*>(p0), y = *reinterpret_cast<const i32x4*>(p1);
+  return __builtin_shufflevector(x, y, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
 __device__ __forceinline__ void bar() {
   __builtin_amdgcn_sched_barrier(0);
   __builtin_amdgcn_s_barrier();
@@ -103,11 +123,14 @@ __device__ __forceinline__ uint32_t pack2(float a, float b) {
   return (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)a) | ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)b) << 16);
 }
 
-template <int EPI, int BN>
+// F8: A / B are e4m3 [M, 2K] / [N, 2K] bytes passed as uint16 rows of K (so every address below is the
+// bf16 kernel's), sa / sb their device-side dequantisation scales.
+template <int EPI, int BN, bool F8 = false>
 __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __restrict__ A,
                                                                const uint16_t* __restrict__ B, uint16_t* __restrict__ C,
                                                                uint16_t* __restrict__ G, const void* __restrict__ bias,
-                                                               int bias_f32, int tanh_form, int M, int N, int K) {
+                                                               int bias_f32, int tanh_form, int M, int N, int K,
+                                                               const float* __restrict__ sa, const float* __restrict__ sb) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 2, wc = wid & 3;
@@ -153,23 +176,33 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
   bf16x8 a[4][2], b0[NH][2], b1[NH][2];
+  i32x8 a8[4], b08[NH], b18[NH];  // F8 fragments
 
   auto read_a = [&](const char* SA, int aq) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 4; ++i) {
+      const int r = wr * 128 + aq * 64 + i * 16 + lrow;
+      if constexpr (F8) {
+        a8[i] = ld_frag8(SA + swz(r, lchk), SA + swz(r, 4 + lchk));
+      } else {
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-        a[i][kk] = *reinterpret_cast<const bf16x8*>(SA + swz(wr * 128 + aq * 64 + i * 16 + lrow, kk * 4 + lchk));
+        for (int kk = 0; kk < 2; ++kk) a[i][kk] = *reinterpret_cast<const bf16x8*>(SA + swz(r, kk * 4 + lchk));
+      }
+    }
   };
-  auto read_b = [&](const char* SB, int bq, bf16x8 (&b)[NH][2]) {
+  auto read_b = [&](const char* SB, int bq, bf16x8 (&b)[NH][2], i32x8 (&b8)[NH]) {
 #pragma unroll
-    for (int j = 0; j < NH; ++j)
+    for (int j = 0; j < NH; ++j) {
+      const int r = kBM + wc * WC + bq * (WC / 2) + j * 16 + lrow;
+      if constexpr (F8) {
+        b8[j] = ld_frag8(SB + swz(r, lchk), SB + swz(r, 4 + lchk));
+      } else {
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-        b[j][kk] = *reinterpret_cast<const bf16x8*>(SB + swz(kBM + wc * WC + bq * (WC / 2) + j * 16 + lrow,
-                                                             kk * 4 + lchk));
+        for (int kk = 0; kk < 2; ++kk) b[j][kk] = *reinterpret_cast<const bf16x8*>(SB + swz(r, kk * 4 + lchk));
+      }
+    }
   };
-  auto quad = [&](int aq, int bq, const bf16x8 (&b)[NH][2]) {
+  auto quad = [&](int aq, int bq, const bf16x8 (&b)[NH][2], const i32x8 (&b8)[NH]) {
     if (PDT_GEMM_PROBE == 1) {  // keep the fragment reads alive without the MFMAs
 #pragma unroll
       for (int i = 0; i < 4; ++i) asm volatile("" ::"v"(a[i][0]), "v"(a[i][1]));
@@ -180,10 +213,15 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < NH; ++j)
+      for (int j = 0; j < NH; ++j) {
+        if constexpr (F8) {
+          acc[aq * 4 + i][bq * NH + j] = mfma8(b8[j], a8[i], acc[aq * 4 + i][bq * NH + j]);
+        } else {
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-          acc[aq * 4 + i][bq * NH + j] = mfma(b[j][kk], a[i][kk], acc[aq * 4 + i][bq * NH + j]);  // D[n][m]
+          for (int kk = 0; kk < 2; ++kk)
+            acc[aq * 4 + i][bq * NH + j] = mfma(b[j][kk], a[i][kk], acc[aq * 4 + i][bq * NH + j]);  // D[n][m]
+        }
+      }
   };
 
   // Pipeline (intervals = barrier-delimited; row 0 loads in even ones, row 1 in odd ones): the B
@@ -210,10 +248,10 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
       // ---- load section
       if (q == 0) {
         if (k + 1 < nk) issue(k + 1, 1);
-        read_b(S, 0, b0);
+        read_b(S, 0, b0, b08);
         read_a(S, 0);
       } else if (q == 1) {
-        read_b(S, 1, b1);
+        read_b(S, 1, b1, b18);
       } else if (q == 2) {
         read_a(S, 1);
       } else {
@@ -225,10 +263,10 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_setprio(1);
-      if (q == 0) quad(0, 0, b0);
-      else if (q == 1) quad(0, 1, b1);
-      else if (q == 2) quad(1, 1, b1);
-      else quad(1, 0, b0);
+      if (q == 0) quad(0, 0, b0, b08);
+      else if (q == 1) quad(0, 1, b1, b18);
+      else if (q == 2) quad(1, 1, b1, b18);
+      else quad(1, 0, b0, b08);
       __builtin_amdgcn_s_setprio(0);
       bar();
     }
@@ -266,6 +304,13 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
         }
       }
     }
+  }
+  if constexpr (F8) {
+    const float sc = *sa * *sb;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[i][j] *= sc;
   }
   bar();
   auto stage_out = [&](uint16_t* __restrict__ out, bool gelu_pass) {
@@ -305,19 +350,19 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
   }
 }
 
-template <int EPI, int BN>
+template <int EPI, int BN, bool F8 = false>
 int launch_bn(const uint16_t* A, const uint16_t* B, uint16_t* C, uint16_t* G, const void* bias, int bias_f32,
-              int tanh_form, int M, int N, int K, hipStream_t s) {
+              int tanh_form, int M, int N, int K, hipStream_t s, const float* sa = nullptr, const float* sb = nullptr) {
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_kernel<EPI, BN>),
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_kernel<EPI, BN, F8>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, GT<BN>::kLds) != hipSuccess)
       return -3;
     attr = true;
   }
   const int64_t grid = (int64_t)((M + kBM - 1) / kBM) * (N / BN);
-  hipLaunchKernelGGL((gemm_nt_kernel<EPI, BN>), dim3((unsigned)grid), dim3(kThreads), GT<BN>::kLds, s, A, B, C, G, bias,
-                     bias_f32, tanh_form, M, N, K);
+  hipLaunchKernelGGL((gemm_nt_kernel<EPI, BN, F8>), dim3((unsigned)grid), dim3(kThreads), GT<BN>::kLds, s, A, B, C, G,
+                     bias, bias_f32, tanh_form, M, N, K, sa, sb);
   return hipPeekAtLastError() == hipSuccess ? 0 : -4;  // a refused launch fails loudly, not as garbage
 }
 
@@ -337,11 +382,11 @@ inline int pick_bn(int M, int N) {
   return tiles <= 256 ? 128 : 256;
 }
 
-template <int EPI>
+template <int EPI, bool F8 = false>
 int launch(const uint16_t* A, const uint16_t* B, uint16_t* C, uint16_t* G, const void* bias, int bias_f32,
-           int tanh_form, int M, int N, int K, hipStream_t s) {
-  return pick_bn(M, N) == 128 ? launch_bn<EPI, 128>(A, B, C, G, bias, bias_f32, tanh_form, M, N, K, s)
-                              : launch_bn<EPI, 256>(A, B, C, G, bias, bias_f32, tanh_form, M, N, K, s);
+           int tanh_form, int M, int N, int K, hipStream_t s, const float* sa = nullptr, const float* sb = nullptr) {
+  return pick_bn(M, N) == 128 ? launch_bn<EPI, 128, F8>(A, B, C, G, bias, bias_f32, tanh_form, M, N, K, s, sa, sb)
+                              : launch_bn<EPI, 256, F8>(A, B, C, G, bias, bias_f32, tanh_form, M, N, K, s, sa, sb);
 }
 
 }  // namespace
@@ -360,6 +405,21 @@ int pdt_gemm_nt(const uint16_t* A, const uint16_t* B, uint16_t* C, uint16_t* G, 
     case EPI_NONE: return launch<EPI_NONE>(A, B, C, G, bias, bias_f32, tanh_form, M, N, K, s);
     case EPI_BIAS: return launch<EPI_BIAS>(A, B, C, G, bias, bias_f32, tanh_form, M, N, K, s);
     case EPI_GELU: return launch<EPI_GELU>(A, B, C, G, bias, bias_f32, tanh_form, M, N, K, s);
+    default: return -1;
+  }
+}
+
+// fp8 e4m3 operands: C[M, N] bf16 = (A sa)(B sb)^T (+ bias, epi 1) from A [M, K] and B [N, K] row-major e4m3
+// bytes and device-side fp32 dequantisation scales sa / sb (torch._scaled_mm's); N % 128 == 0, K % 128 == 0.
+int pdt_gemm_nt_fp8(const uint8_t* A, const uint8_t* B, uint16_t* C, const float* sa, const float* sb,
+                    const void* bias, int bias_f32, int epi, int M, int N, int K, hipStream_t s) {
+  if (M < 1 || N % 128 != 0 || K % (2 * kBK) != 0 || N < 128 || K < 2 * kBK || !sa || !sb) return -1;
+  if ((int64_t)M * K >= (int64_t)1 << 31 || (int64_t)N * K >= (int64_t)1 << 31) return -2;
+  const uint16_t* a = reinterpret_cast<const uint16_t*>(A);
+  const uint16_t* b = reinterpret_cast<const uint16_t*>(B);
+  switch (epi) {  // the kernel addresses 128-B rows of K / 2 uint16
+    case EPI_NONE: return launch<EPI_NONE, true>(a, b, C, nullptr, bias, bias_f32, 0, M, N, K / 2, s, sa, sb);
+    case EPI_BIAS: return launch<EPI_BIAS, true>(a, b, C, nullptr, bias, bias_f32, 0, M, N, K / 2, s, sa, sb);
     default: return -1;
   }
 }
