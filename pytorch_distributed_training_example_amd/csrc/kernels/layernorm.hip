@@ -305,9 +305,20 @@ __global__ __launch_bounds__(256) void ln_bwd_finalize_kernel(const float* __res
   }
 }
 
+// Workgroup cap (PDT_LN_BWD_BLOCKS, read once; A/B): 512 = 2 workgroups per CU.
+inline int64_t ln_bwd_cap() {
+  static int64_t cap = 0;
+  if (cap == 0) {
+    const char* e = getenv("PDT_LN_BWD_BLOCKS");
+    const int64_t v = (e && e[0]) ? strtol(e, nullptr, 10) : 512;
+    cap = v >= 64 && v <= 4096 ? v : 512;
+  }
+  return cap;
+}
+
 inline int ln_bwd_blocks(int64_t N, int& rows_per_block) {
   int64_t nblk = (N + 31) / 32;  // >= 8 rows per wave
-  if (nblk > 512) nblk = 512;     // 2 workgroups per CU; the dgamma/dbeta slab is nblk x 2 x D floats
+  if (nblk > ln_bwd_cap()) nblk = ln_bwd_cap();  // the dgamma/dbeta slab is nblk x 2 x D floats
   if (nblk < 1) nblk = 1;
   rows_per_block = (int)((N + nblk - 1) / nblk);
   return (int)((N + rows_per_block - 1) / rows_per_block);
