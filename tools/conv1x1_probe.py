@@ -33,7 +33,7 @@ def main():
     a = ap.parse_args()
     from pytorch_distributed_training_example_amd.ops._native import native
     C = native()
-    probes = [0, 64, 0, 64, 1, 65]
+    probes = [int(v) for v in os.environ.get("PDT_PROBES", "0,64,0,64,1,65").split(",")]
     print("probe: 1 = no stores, 2 = no MFMA, 4 = no operand DMA, 8 = 64-channel tiles, 16 = no statistics, 32 = no mask stores, 64 = no 256-channel tiles")
     print(f"{'case':<34}" + "".join(f"{p:>9}" for p in probes) + "   GB  TB/s(p0)")
     for h, ci, co in ((56, 64, 256), (28, 128, 512), (14, 256, 1024), (7, 512, 2048)):
