@@ -201,8 +201,9 @@ int pdt_embedding_fwd(const int64_t* idx, const uint16_t* wte, const uint16_t* w
 int64_t pdt_embedding_bwd_ws_ints(int64_t n, int V);
 int pdt_gemm_nt(const uint16_t* A, const uint16_t* B, uint16_t* C, uint16_t* G, const void* bias, int bias_f32,
                 int epi, int tanh_form, int M, int N, int K, hipStream_t s);
+int pdt_gemm_nt_fp8_ksplit(int M, int N, int K);
 int pdt_gemm_nt_fp8(const uint8_t* A, const uint8_t* B, uint16_t* C, const float* sa, const float* sb,
-                    const void* bias, int bias_f32, int epi, int M, int N, int K, hipStream_t s);
+                    const void* bias, int bias_f32, int epi, int M, int N, int K, float* ws, int ksplit, hipStream_t s);
 int pdt_embedding_bwd(const int64_t* idx, const uint16_t* dout, uint16_t* dwte, uint16_t* dwpe, int* ws, int64_t n,
                       int B, int T, int V, int D, int* err, hipStream_t s);
 int64_t pdt_p2p_flags_bytes();
@@ -2045,9 +2046,14 @@ Tensor gemm_nt_fp8(Tensor a, Tensor b, Tensor sa, Tensor sb, c10::optional<Tenso
     bf32 = bias->scalar_type() == at::kFloat;
   }
   auto c = at::empty({M, N}, a.options().dtype(at::kBFloat16));
+  // few output tiles and no bias (the weight gradients): split K, fp32 partials + one reduce pass
+  const int ks = bp ? 1 : pdt_gemm_nt_fp8_ksplit((int)M, (int)N, (int)K);
+  Tensor ws;
+  if (ks > 1) ws = at::empty({(int64_t)ks * M * N}, a.options().dtype(at::kFloat));
   const int rc = pdt_gemm_nt_fp8(reinterpret_cast<const uint8_t*>(a.data_ptr()), reinterpret_cast<const uint8_t*>(b.data_ptr()),
                                  reinterpret_cast<uint16_t*>(c.data_ptr()), sa.data_ptr<float>(), sb.data_ptr<float>(), bp,
-                                 bf32, bp ? 1 : 0, (int)M, (int)N, (int)K, stream());
+                                 bf32, bp ? 1 : 0, (int)M, (int)N, (int)K, ks > 1 ? ws.data_ptr<float>() : nullptr, ks,
+                                 stream());
   TORCH_CHECK(rc == 0, "pdt_gemm_nt_fp8 failed (", rc, ") for M=", M, " N=", N, " K=", K);
   return c;
 }

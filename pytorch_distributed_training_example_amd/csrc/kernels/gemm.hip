@@ -37,6 +37,8 @@
 //     and share both in its L2 (8k^3: 1421 vs 1309 TF for plain N-first order).
 #include "../common.h"
 
+#include <algorithm>
+
 using namespace pdt;
 
 namespace {
@@ -130,19 +132,24 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
                                                                const uint16_t* __restrict__ B, uint16_t* __restrict__ C,
                                                                uint16_t* __restrict__ G, const void* __restrict__ bias,
                                                                int bias_f32, int tanh_form, int M, int N, int K,
-                                                               const float* __restrict__ sa, const float* __restrict__ sb) {
+                                                               const float* __restrict__ sa, const float* __restrict__ sb,
+                                                               float* __restrict__ part, int ksplit) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid >> 2, wc = wid & 3;
   using T = GT<BN>;
   constexpr int kStage = T::kStage, kEpiStride = T::kEpiStride, WC = T::WC, NJ = T::NJ, NH = T::NH;
   const int ntn = N / BN, ntm = (M + kBM - 1) / kBM;
-  const int id = xcd_remap(blockIdx.x, gridDim.x);
+  const int id0 = xcd_remap(blockIdx.x, gridDim.x);
+  // split-K (F8, ksplit > 1): block id = split * tiles + tile; split s takes K-steps [s nkt / ksplit,
+  // (s + 1) nkt / ksplit) and writes its fp32 tile to part[s] (summed by splitk_reduce_kernel)
+  const int split = id0 / (ntn * ntm), id = id0 - split * (ntn * ntm);
   // groups of kGroup A bands: consecutive ids (one XCD) cover kGroup bands x a few N tiles, so the
   // tiles resident on an XCD at once share both operands in its L2
   const int gband = (id / (kGroup * ntn)) * kGroup, gsize = min(ntm - gband, kGroup), gi = id % (kGroup * ntn);
   const int m0 = (gband + gi % gsize) * kBM, n0 = (gi / gsize) * BN;
-  const int nk = K / kBK;
+  const int nkt = K / kBK, kb = split * nkt / ksplit;
+  const int nk = (split + 1) * nkt / ksplit - kb;
 
   // DMA: waves 0-3 (wave row 0) stage the B rows of the image, waves 4-7 (row 1) the A rows — each
   // A wave 64 rows as 8 instructions of 8 rows, each B wave BN / 4 rows (8 or 4 instructions); lane ->
@@ -158,7 +165,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
     const int R = rbase + j * 8 + (lane >> 3);
     const int logical = (lane & 7) ^ ((R >> 1) & 7);
     const int grow = loads_b ? n0 + (R - kBM) : min(m0 + R, M - 1);
-    off[j] = grow * K + logical * 8;
+    off[j] = grow * K + logical * 8 + kb * kBK;
   }
   auto issue = [&](int t, int half) {  // half 0 / 1 of this wave's share of K-step t
     if (PDT_GEMM_PROBE == 2) return;
@@ -313,6 +320,33 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
       for (int j = 0; j < NJ; ++j) acc[i][j] *= sc;
   }
   bar();
+  if constexpr (F8) {
+    if (ksplit > 1) {  // fp32 partial tile, staged through LDS one wave row (128 rows) at a time
+      constexpr int kPS = BN * 4 + 16;
+      float* const pb = part + (int64_t)split * M * N;
+#pragma unroll 1
+      for (int ph = 0; ph < 2; ++ph) {
+        if (wr == ph) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j)
+              *reinterpret_cast<f4*>(lds + (i * 16 + lrow) * kPS + (wc * WC + j * 16 + 4 * lchk) * 4) = acc[i][j];
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        bar();
+        for (int idx = tid; idx < 128 * (BN / 4); idx += kThreads) {
+          const int r = idx / (BN / 4), c = idx % (BN / 4);
+          const int m = m0 + ph * 128 + r;
+          if (m < M)
+            *reinterpret_cast<float4*>(pb + (int64_t)m * N + n0 + c * 4) =
+                *reinterpret_cast<const float4*>(lds + r * kPS + c * 16);
+        }
+        bar();
+      }
+      return;
+    }
+  }
   auto stage_out = [&](uint16_t* __restrict__ out, bool gelu_pass) {
 #pragma unroll
     for (int i = 0; i < 8; ++i)
@@ -352,7 +386,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
 
 template <int EPI, int BN, bool F8 = false>
 int launch_bn(const uint16_t* A, const uint16_t* B, uint16_t* C, uint16_t* G, const void* bias, int bias_f32,
-              int tanh_form, int M, int N, int K, hipStream_t s, const float* sa = nullptr, const float* sb = nullptr) {
+              int tanh_form, int M, int N, int K, hipStream_t s, const float* sa = nullptr, const float* sb = nullptr,
+              float* part = nullptr, int ksplit = 1) {
   static bool attr = false;
   if (!attr) {
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_nt_kernel<EPI, BN, F8>),
@@ -360,9 +395,9 @@ int launch_bn(const uint16_t* A, const uint16_t* B, uint16_t* C, uint16_t* G, co
       return -3;
     attr = true;
   }
-  const int64_t grid = (int64_t)((M + kBM - 1) / kBM) * (N / BN);
+  const int64_t grid = (int64_t)((M + kBM - 1) / kBM) * (N / BN) * ksplit;
   hipLaunchKernelGGL((gemm_nt_kernel<EPI, BN, F8>), dim3((unsigned)grid), dim3(kThreads), GT<BN>::kLds, s, A, B, C, G,
-                     bias, bias_f32, tanh_form, M, N, K, sa, sb);
+                     bias, bias_f32, tanh_form, M, N, K, sa, sb, part, ksplit);
   return hipPeekAtLastError() == hipSuccess ? 0 : -4;  // a refused launch fails loudly, not as garbage
 }
 
@@ -384,9 +419,40 @@ inline int pick_bn(int M, int N) {
 
 template <int EPI, bool F8 = false>
 int launch(const uint16_t* A, const uint16_t* B, uint16_t* C, uint16_t* G, const void* bias, int bias_f32,
-           int tanh_form, int M, int N, int K, hipStream_t s, const float* sa = nullptr, const float* sb = nullptr) {
-  return pick_bn(M, N) == 128 ? launch_bn<EPI, 128, F8>(A, B, C, G, bias, bias_f32, tanh_form, M, N, K, s, sa, sb)
-                              : launch_bn<EPI, 256, F8>(A, B, C, G, bias, bias_f32, tanh_form, M, N, K, s, sa, sb);
+           int tanh_form, int M, int N, int K, hipStream_t s, const float* sa = nullptr, const float* sb = nullptr,
+           float* part = nullptr, int ksplit = 1) {
+  return pick_bn(M, N) == 128
+             ? launch_bn<EPI, 128, F8>(A, B, C, G, bias, bias_f32, tanh_form, M, N, K, s, sa, sb, part, ksplit)
+             : launch_bn<EPI, 256, F8>(A, B, C, G, bias, bias_f32, tanh_form, M, N, K, s, sa, sb, part, ksplit);
+}
+
+// C = bf16(sum over the ksplit fp32 partial tiles), fixed order (deterministic); 4 elements per thread.
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ part, uint16_t* __restrict__ C,
+                                                            int64_t n4, int64_t MN, int ksplit) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 a = reinterpret_cast<const float4*>(part)[i];
+    for (int sp = 1; sp < ksplit; ++sp) {
+      const float4 b = reinterpret_cast<const float4*>(part + sp * MN)[i];
+      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    }
+    reinterpret_cast<uint2*>(C)[i] = make_uint2(pack2(a.x, a.y), pack2(a.z, a.w));
+  }
+}
+
+// K splits for an fp8 GEMM with few output tiles (PDT_GEMM_KSPLIT forces a count, 1 = off): about 384
+// workgroups, at least 8 K-steps of 128 per split, at most 16 splits.
+int fp8_ksplit(int M, int N, int K) {
+  static int forced = -1;
+  if (forced < 0) {
+    const char* e = getenv("PDT_GEMM_KSPLIT");
+    forced = (e && e[0]) ? (int)strtol(e, nullptr, 10) : 0;
+  }
+  const int nkt = K / (2 * kBK);
+  const int64_t tiles = (int64_t)((M + kBM - 1) / kBM) * (N / pick_bn(M, N));
+  int ks = forced > 0 ? forced : (tiles >= 192 ? 1 : (int)((384 + tiles - 1) / tiles));
+  ks = std::min(ks, std::min(16, nkt / 8));
+  return ks < 1 ? 1 : ks;
 }
 
 }  // namespace
@@ -411,12 +477,27 @@ int pdt_gemm_nt(const uint16_t* A, const uint16_t* B, uint16_t* C, uint16_t* G, 
 
 // fp8 e4m3 operands: C[M, N] bf16 = (A sa)(B sb)^T (+ bias, epi 1) from A [M, K] and B [N, K] row-major e4m3
 // bytes and device-side fp32 dequantisation scales sa / sb (torch._scaled_mm's); N % 128 == 0, K % 128 == 0.
+// ws / ksplit (epi 0 only): pdt_gemm_nt_fp8_ksplit() splits of K, ws = ksplit * M * N floats (ksplit 1: unused).
+int pdt_gemm_nt_fp8_ksplit(int M, int N, int K) {
+  if (M < 1 || N % 128 != 0 || K % (2 * kBK) != 0 || N < 128 || K < 2 * kBK) return 1;
+  return fp8_ksplit(M, N, K);
+}
+
 int pdt_gemm_nt_fp8(const uint8_t* A, const uint8_t* B, uint16_t* C, const float* sa, const float* sb,
-                    const void* bias, int bias_f32, int epi, int M, int N, int K, hipStream_t s) {
+                    const void* bias, int bias_f32, int epi, int M, int N, int K, float* ws, int ksplit, hipStream_t s) {
   if (M < 1 || N % 128 != 0 || K % (2 * kBK) != 0 || N < 128 || K < 2 * kBK || !sa || !sb) return -1;
   if ((int64_t)M * K >= (int64_t)1 << 31 || (int64_t)N * K >= (int64_t)1 << 31) return -2;
+  if (ksplit < 1 || ksplit > K / (2 * kBK) || (ksplit > 1 && (!ws || epi != EPI_NONE))) return -1;
   const uint16_t* a = reinterpret_cast<const uint16_t*>(A);
   const uint16_t* b = reinterpret_cast<const uint16_t*>(B);
+  if (ksplit > 1) {
+    const int rc = launch<EPI_NONE, true>(a, b, C, nullptr, nullptr, 0, 0, M, N, K / 2, s, sa, sb, ws, ksplit);
+    if (rc) return rc;
+    const int64_t MN = (int64_t)M * N, n4 = MN / 4;
+    const int64_t g = std::min<int64_t>((n4 + 255) / 256, 2048);
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)g), dim3(256), 0, s, ws, C, n4, MN, ksplit);
+    return hipPeekAtLastError() == hipSuccess ? 0 : -4;
+  }
   switch (epi) {  // the kernel addresses 128-B rows of K / 2 uint16
     case EPI_NONE: return launch<EPI_NONE, true>(a, b, C, nullptr, bias, bias_f32, 0, M, N, K / 2, s, sa, sb);
     case EPI_BIAS: return launch<EPI_BIAS, true>(a, b, C, nullptr, bias, bias_f32, 0, M, N, K / 2, s, sa, sb);

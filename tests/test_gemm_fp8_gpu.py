@@ -13,7 +13,9 @@ def _q(shape, g, scale):
 
 
 @pytest.mark.parametrize("M,N,K", [(256, 128, 128), (300, 256, 256), (1000, 384, 768), (4096, 3072, 1024),
-                                   (25216, 768, 768), (2048, 256, 4096)])
+                                   (25216, 768, 768), (2048, 256, 4096),
+                                   # weight-gradient shapes (few output tiles, long K): split-K + reduce pass
+                                   (2304, 768, 25216), (768, 768, 25216), (1024, 4096, 8192), (200, 128, 2048)])
 @pytest.mark.parametrize("bias", [None, "f32", "bf16"])
 def test_gemm_nt_fp8_matches_fp32_reference(M, N, K, bias):
     from pytorch_distributed_training_example_amd.ops._native import native

@@ -2,6 +2,7 @@
 is active) on the ViT-B/16 and GPT-2-medium Linear shapes (forward and data gradient: M = tokens).
 One JSON line per shape: {"shape", "M", "N", "K", "ours_us", "lib_us", "speedup", "ours_tflops"}."""
 import json
+import os
 import sys
 
 import torch
@@ -29,7 +30,14 @@ def main():
         "vit_fc2": (25216, 768, 3072), "vit_qkv_dgrad": (25216, 768, 2304), "vit_fc1_dgrad": (25216, 768, 3072),
         "vit_fc2_dgrad": (25216, 3072, 768),
         "gpt2_qkv": (8192, 3072, 1024), "gpt2_proj": (8192, 1024, 1024), "gpt2_fc1": (8192, 4096, 1024),
-        "gpt2_fc2": (8192, 1024, 4096), "sq8k": (8192, 8192, 8192)}
+        "gpt2_fc2": (8192, 1024, 4096), "sq8k": (8192, 8192, 8192),
+        # weight gradients dW [out, in] = dY^T X over the tokens (split-K path)
+        "vit_qkv_wgrad": (2304, 768, 25216), "vit_proj_wgrad": (768, 768, 25216), "vit_fc1_wgrad": (3072, 768, 25216),
+        "vit_fc2_wgrad": (768, 3072, 25216), "gpt2_qkv_wgrad": (3072, 1024, 8192), "gpt2_proj_wgrad": (1024, 1024, 8192),
+        "gpt2_fc1_wgrad": (4096, 1024, 8192), "gpt2_fc2_wgrad": (1024, 4096, 8192)}
+    only = os.environ.get("SHAPES")
+    if only:
+        shapes = {k: v for k, v in shapes.items() if k in only.split(",")}
     g = torch.Generator(device="cuda").manual_seed(0)
     for name, (M, N, K) in shapes.items():
         a = (torch.randn(M, K, device="cuda", generator=g) * 4).to(torch.float8_e4m3fn)
