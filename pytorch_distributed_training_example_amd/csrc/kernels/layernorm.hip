@@ -316,8 +316,19 @@ inline int64_t ln_bwd_cap() {
   return cap;
 }
 
+// Minimum rows per workgroup (PDT_LN_BWD_ROWS, read once; A/B): 32 = 8 rows per wave.
+inline int64_t ln_bwd_min_rows() {
+  static int64_t r = 0;
+  if (r == 0) {
+    const char* e = getenv("PDT_LN_BWD_ROWS");
+    const int64_t v = (e && e[0]) ? strtol(e, nullptr, 10) : 32;
+    r = v >= 4 && v <= 256 ? v : 32;
+  }
+  return r;
+}
+
 inline int ln_bwd_blocks(int64_t N, int& rows_per_block) {
-  int64_t nblk = (N + 31) / 32;  // >= 8 rows per wave
+  int64_t nblk = (N + ln_bwd_min_rows() - 1) / ln_bwd_min_rows();
   if (nblk > ln_bwd_cap()) nblk = ln_bwd_cap();  // the dgamma/dbeta slab is nblk x 2 x D floats
   if (nblk < 1) nblk = 1;
   rows_per_block = (int)((N + nblk - 1) / nblk);
