@@ -38,7 +38,10 @@ import torch.distributed as dist
 
 from ..ops._native import native
 
-ONESHOT_MAX_BYTES = 256 << 10  # one-shot below, two-shot above (latency vs bytes moved per GPU)
+# one-shot below, two-shot above (latency vs bytes moved per GPU). An estimate, not a measurement: the crossover
+# needs >= 2 GPUs of one node (tools/p2p_crossover.py measures it, and the hook's RCCL crossover, under torchrun);
+# the P2P hook stays opt-in (--comm-hook p2p) until it is measured.
+ONESHOT_MAX_BYTES = 256 << 10
 DEFAULT_TIMEOUT_S = 300.0  # a peer may be this late (wall clock) before the call poisons its output
 MAX_TIMEOUT_S = 1800.0
 
