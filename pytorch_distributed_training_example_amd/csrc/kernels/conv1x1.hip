@@ -835,6 +835,16 @@ int launch(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t* c,
 using GXWide = G1<256, 4, 4>;  // N % 256 == 0 (large M): 16 waves of 64x64, a block writes whole 512-B rows
 using GWide = G1<128, 4, 2>;   // N % 128 == 0: 8 waves of 64x64
 using GNarrow = G1<64, 4, 1>;  // N == 64 (or odd multiples of 64): 4 waves of 64x64
+// 8 waves of 128 x 64 (PDT_CONV1X1_W2=1, A/B): the deep-K forward shapes (layers 3-4) are MFMA-fed, not HBM-bound,
+// and a 64 x 64 wave tile reads 2.7x the LDS bytes per MFMA of a 128 x 64 one
+using GXWide2 = G1<256, 2, 4>;
+inline bool w2_on() {
+  static const int v = [] {
+    const char* e = getenv("PDT_CONV1X1_W2");
+    return (e && e[0]) ? (int)strtol(e, nullptr, 10) : 0;
+  }();
+  return v != 0;
+}
 
 template <class Cf>
 int dispatch(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t* c, const uint8_t* cm, float* part,
@@ -899,6 +909,8 @@ int pdt_conv1x1_gemm(const uint16_t* a, const uint16_t* b, uint16_t* y, const ui
   // (the 16-wave tile only for the plain / statistics forward and the data gradient without an accumulate
   // source — with the ATR operand transform or an accumulate source the 8-wave tile, two workgroups per
   // CU, ran 5-10 % faster at every ResNet-50 depth: profiles/r5/conv1x1_tiles_bench_b1024.txt)
+  if (w2_on() && N % 256 == 0 && K >= 256 && !c && !acoef && !bs.part && !(g_probe & 64))
+    return dispatch<GXWide2>(a, b, y, c, cm, part, M, K, N, bs, cg, s, acoef);
   if (N % 256 == 0 && (int64_t)((M + 255) / 256) * (N / 256) >= 2048 && !(g_probe & 64) && !c && !acoef)
     return dispatch<GXWide>(a, b, y, c, cm, part, M, K, N, bs, cg, s, acoef);
   if (N % 128 == 0 && !(g_probe & 8) && !small_grid_narrow((int64_t)((M + 255) / 256) * (N / 128)))
