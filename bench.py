@@ -72,7 +72,9 @@ def parse(argv=None):
     ap.add_argument("--impl", default="ours", choices=["ours", "torch_ddp", "reference"])
     ap.add_argument("--graph", type=int, default=0,
                     help="hipGraph-capture the step (ours; excludes the capture-unsafe MIOpen solvers)")
-    ap.add_argument("--bucket-cap-mb", type=float, default=25.0)
+    ap.add_argument("--bucket-cap-mb", default="auto",
+                    help="MiB cap per gradient bucket, or 'auto' (ours): the comm-model plan whose last-filling "
+                         "bucket is <= 2 MiB (parallel/buckets.py plan_auto); torch_ddp uses 25 for 'auto'")
     ap.add_argument("--reduce-single-rank", type=int, default=1,
                     help="ours at N=1: still pack buckets and issue the (1-rank RCCL) all-reduce, as torch "
                          "DDP does, so N=1 carries the same per-step reducer work as N>1")
@@ -130,7 +132,8 @@ def build(args, ctx):
     else:
         if args.impl == "torch_ddp" and world > 1:
             ddp = torch.nn.parallel.DistributedDataParallel(model, device_ids=[dev.index],
-                                                            bucket_cap_mb=args.bucket_cap_mb,
+                                                            bucket_cap_mb=(25.0 if args.bucket_cap_mb == "auto"
+                                                                           else float(args.bucket_cap_mb)),
                                                             broadcast_buffers=False, gradient_as_bucket_view=True)
         else:
             ddp = model

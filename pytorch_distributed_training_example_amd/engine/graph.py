@@ -39,19 +39,47 @@ def make_miopen_capture_safe() -> None:
     torch.backends.cudnn.benchmark = True
 
 
-def _drain_pg_watchdog(wait_s: float = 0.25) -> None:
-    """Let the RCCL process group's watchdog retire the (completed) collectives of the warm-up
-    iterations before a capture starts: its thread polls each pending work's completion event every
-    ~100 ms, and a poll that lands while the capture is in progress has been seen to fail with
-    hipErrorCapturedEvent and abort the process (1 of ~8 graphed runs in round 5, none with the
-    list empty). The device is already synchronized, so one sweep retires everything; one-time cost."""
+def wait_pg_watchdog_idle(timeout_s: float = 30.0) -> bool:
+    """Block until the RCCL process group's watchdog has RETIRED every collective issued so far, so
+    it issues no event query while a capture runs. Returns True when verified, False when it cannot
+    be checked (no RCCL group, or the flight recorder is off).
+
+    Cause of the round-4/5 capture aborts (1 in 2 graphed runs in global capture mode, 1 in ~8 in
+    thread_local mode): ProcessGroupNCCL's watchdog thread keeps every non-captured collective in its
+    work list and calls ``work.isCompleted()`` on it every ~100 ms — an ``hipEventQuery`` of the
+    collective's end event from a second thread. A query that overlaps the capture of the step fails
+    (hipErrorStreamCaptureUnsupported in global mode; hipErrorCapturedEvent in thread_local mode)
+    and the watchdog aborts the process. Collectives issued DURING capture are never put in that
+    list (ProcessGroupNCCL enqueues work to the watchdog only when the stream is not capturing), so
+    once the list is empty the watchdog queries nothing until the capture has ended.
+
+    The list is not exposed, but the flight recorder mirrors it: the watchdog calls ``retire_id``
+    on a work's trace entry exactly when it erases that work from the list (``retired`` in the
+    dump). The launcher turns the recorder on (``TORCH_FR_BUFFER_SIZE``, parallel/launcher.py);
+    this polls its dump until every entry is retired. The caller has synchronized the device, so
+    every collective is complete and the next watchdog sweep retires them all."""
+    import pickle
     import time
     try:
         import torch.distributed as dist
-        if dist.is_available() and dist.is_initialized() and dist.get_backend() == "nccl":
-            time.sleep(wait_s)
-    except Exception:  # pragma: no cover - no process group / CPU-only build
-        pass
+        if not (dist.is_available() and dist.is_initialized() and dist.get_backend() == "nccl"):
+            return False
+        dump = torch._C._distributed_c10d._dump_nccl_trace
+    except Exception:  # pragma: no cover - CPU-only build
+        return False
+    if int(os.environ.get("TORCH_FR_BUFFER_SIZE", os.environ.get("TORCH_NCCL_TRACE_BUFFER_SIZE", "0")) or 0) <= 0:
+        return False
+    deadline = time.monotonic() + timeout_s
+    while True:
+        # our own process's trace (includeCollectives, no stack traces, all entries)
+        entries = pickle.loads(dump(True, False, False)).get("entries", [])
+        pending = [e for e in entries if not e.get("retired", True)]
+        if not pending:
+            return True
+        if time.monotonic() > deadline:
+            raise RuntimeError(f"hipGraph capture: the RCCL watchdog has not retired {len(pending)} collective(s) "
+                               f"after {timeout_s:.0f} s (first: {pending[0].get('profiling_name')})")
+        time.sleep(0.005)
 
 
 class StaticStep:
@@ -70,6 +98,7 @@ class StaticStep:
         self.static_loss: Optional[torch.Tensor] = None
         self._warmup = warmup
         self._pool = pool
+        self.watchdog_idle: Optional[bool] = None
 
     def capture(self) -> None:
         if not self.enabled:
@@ -81,12 +110,10 @@ class StaticStep:
                 self.static_loss = self.fn(*self.static_inputs)
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
-        _drain_pg_watchdog()
+        self.watchdog_idle = wait_pg_watchdog_idle()  # no watchdog event query can overlap the capture
         self.graph = torch.cuda.CUDAGraph()
-        # thread_local: the RCCL process group's watchdog thread polls completion events of collectives
-        # issued before the capture; under the default "global" mode HIP rejects those queries while any
-        # stream captures (hipErrorStreamCaptureUnsupported -> watchdog exception -> process abort, seen in
-        # graphed bench runs). Capture itself is per stream: the step's kernels are captured either way.
+        # thread_local: other threads' HIP calls (the allocator's, the profiler's) stay legal during the
+        # capture; the RCCL watchdog's queries are excluded above. Capture itself is per stream.
         with torch.cuda.graph(self.graph, pool=self._pool, capture_error_mode="thread_local"):
             self.static_loss = self.fn(*self.static_inputs)
         torch.cuda.synchronize()

@@ -61,6 +61,11 @@ def _bn(c: int, fused_relu: bool = False) -> nn.Module:
     return nn.BatchNorm2d(c)
 
 
+def _bn_trains(bn: nn.Module) -> bool:
+    """``bn`` is our BatchNorm and will take batch_norm_act's training (batch-statistics) path."""
+    return isinstance(bn, BatchNorm2d) and (bn.training or not bn.track_running_stats)
+
+
 def bn_act(bn: nn.Module, x, residual=None, relu: bool = False):
     """relu?(bn(x) + residual?) — one fused kernel for our BN, three ops for torch's."""
     if isinstance(bn, BatchNorm2d):
@@ -111,14 +116,20 @@ class Bottleneck(nn.Module):
         # gradient into the link. With any other BatchNorm path conv1's backward would find the link
         # empty, park its dx there for a partner that never comes, and the conv1 branch's gradient
         # would be lost (fp32 ResNet-50 on the GPU lost it in every block until round 5).
+        # The BatchNorms that deposit into the links must run batch_norm_act's training path (a frozen /
+        # eval-mode BN runs _BNEvalFn, which returns the shortcut gradient through autograd instead).
+        ds_bn0 = self.downsample[1] if self.downsample is not None else None
         if (RESIDUAL_GRAD_LINK[0] and self.training and x.requires_grad and torch.is_grad_enabled()
                 and x.dtype == torch.bfloat16 and not native_disabled()
-                and isinstance(self.conv1, Conv1x1) and isinstance(self.bn3, BatchNorm2d)
+                and isinstance(self.conv1, Conv1x1) and _bn_trains(self.bn3)
+                and (ds_bn0 is None or not isinstance(ds_bn0, BatchNorm2d) or _bn_trains(ds_bn0))
                 and self.conv1.gemm_eligible(x) and x.shape[1] % 64 == 0):
             # the two gradients of x (conv1 branch, shortcut) meet in conv1's data-gradient GEMM
             # (beta = 1) instead of an autograd add kernel (ops/batchnorm.py ResidualGradLink)
-            # identity blocks: bn3's backward may hand the shortcut gradient over as (dy, mask)
-            link = ResidualGradLink(lazy=self.downsample is None and self.conv1.masked_residual_ok(x))
+            # identity blocks: bn3's backward may hand the shortcut gradient over as (dy, mask); conv1's
+            # backward always runs after bn3's there (consumer_last: never parks its dx)
+            link = ResidualGradLink(lazy=self.downsample is None and self.conv1.masked_residual_ok(x),
+                                    consumer_last=self.downsample is None)
             out = bn_act(self.bn1, self.conv1(x, res_link=link), relu=True)
             z2 = self.conv2(out)  # same shape / layout as bn2's output: decides conv3's paths
             ds_bn = self.downsample[1] if self.downsample is not None else None

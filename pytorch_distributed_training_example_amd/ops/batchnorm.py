@@ -41,13 +41,18 @@ class ResidualGradLink:
     ``relu(bn3(x) + identity)`` backward deposits (it always runs first: the main branch is
     upstream of it); downsample blocks: the shortcut conv deposits (ops/conv.py linked_conv)."""
 
-    __slots__ = ("grad", "lazy")
+    __slots__ = ("grad", "lazy", "consumer_last")
 
-    def __init__(self, lazy: bool = False):
+    def __init__(self, lazy: bool = False, consumer_last: bool = False):
         self.grad = None
         # lazy: the depositing BatchNorm hands over (dy, relu mask) instead of writing dres = dy*mask;
         # the consumer (our 1x1 dgrad GEMM) applies the mask in its accumulate epilogue
         self.lazy = lazy
+        # consumer_last: the accumulating conv's backward always runs after the depositor's (identity
+        # blocks: bn3 is downstream of conv1). Finding the link empty then means the depositor took a
+        # path that returned its gradient through autograd (e.g. a BatchNorm in eval mode): the consumer
+        # must return its own dx instead of parking it for a partner that never comes.
+        self.consumer_last = consumer_last
 
     def take(self):
         g, self.grad = self.grad, None

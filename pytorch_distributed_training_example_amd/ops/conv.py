@@ -396,7 +396,7 @@ class _Conv1x1Fn(torch.autograd.Function):
 
         # the other branch's gradient of x, if it already arrived (ResidualGradLink)
         acc = ctx.link.take() if ctx.link is not None else None
-        first = ctx.link is not None and acc is None
+        first = ctx.link is not None and acc is None and not ctx.link.consumer_last
         strided = None
         if isinstance(acc, StridedGrad):  # a stride-2 shortcut's compact gradient: added below
             strided, acc = acc, None

@@ -23,9 +23,14 @@ Assignment rules (compatible with torch DDP's so bucket boundaries line up):
 
 MI355X sizing note: ring all-reduce over xGMI is bound by one ≈153 GB/s link per ring;
 RCCL runs several rings to use the 7 links. A 25 MiB bucket costs ≈0.04–0.3 ms at n=8
-(SURVEY.md §5.1), i.e. well under one layer's backward for ResNet-50 at batch 256, so the
-torch defaults (1 MiB first bucket, 25 MiB cap) are kept and the sweep tool
-(tools/bucket_sweep.py) tunes them per model.
+(SURVEY.md §5.1), i.e. well under one layer's backward for ResNet-50 at batch 256, so
+mid-backward buckets can be large. What is NOT hidden is the bucket that fills last: its
+collective starts when backward's compute ends. ``plan_auto`` (``bucket_cap_mb="auto"``) is
+a comm-model plan built backwards from the end of backward: the last-filling bucket is capped at
+``tail_bytes`` (2 MiB: α-dominated, ≈15 µs of wire time on one xGMI link at n = 8), the one
+before at ``growth`` × that, and so on up to the 25 MiB cap, so each bucket's all-reduce is
+no longer than the (growing) stretch of backward compute still ahead of it. The sweep tool
+(tools/bucket_sweep.py) tunes the fixed caps per model.
 """
 from __future__ import annotations
 
@@ -36,6 +41,8 @@ import torch
 
 DEFAULT_FIRST_BUCKET_BYTES = 1 * 1024 * 1024
 DEFAULT_BUCKET_CAP_MB = 25.0
+AUTO_TAIL_BYTES = 2 * 1024 * 1024
+AUTO_GROWTH = 4
 
 
 @dataclass
@@ -96,6 +103,55 @@ def compute_bucket_assignment(
     specs: List[BucketSpec] = []
     for members, dtype, device in done:
         spec = BucketSpec(indices=list(members), dtype=dtype, device=device)
+        off = 0
+        for i in members:
+            spec.offsets.append(off)
+            spec.numels.append(params[i].numel())
+            off = _align(off + params[i].numel(), align_elems)
+        spec.total = max(off, 1)
+        specs.append(spec)
+    return specs
+
+
+def plan_auto(
+    params: Sequence[torch.Tensor],
+    bucket_cap_bytes: int = int(DEFAULT_BUCKET_CAP_MB * 1024 * 1024),
+    tail_bytes: int = AUTO_TAIL_BYTES,
+    growth: int = AUTO_GROWTH,
+    order: Sequence[int] | None = None,
+    align_elems: int = 8,
+) -> List[BucketSpec]:
+    """The comm-model bucket plan (module docstring): walk the ready order BACKWARDS per
+    (dtype, device); the first bucket met (the one that fills last) is capped at ``tail_bytes``,
+    each earlier one at ``growth`` × the previous cap, up to ``bucket_cap_bytes``. A single
+    parameter larger than its cap gets a bucket of its own. Buckets are returned in fill order."""
+    n = len(params)
+    if order is None:
+        order = list(range(n - 1, -1, -1))
+    pos = {idx: i for i, idx in enumerate(order)}
+    cur: Dict[Tuple[torch.dtype, torch.device], Tuple[List[int], int]] = {}
+    cap: Dict[Tuple[torch.dtype, torch.device], int] = {}
+    done: List[Tuple[List[int], torch.dtype, torch.device]] = []
+    for idx in reversed(list(order)):
+        p = params[idx]
+        key = (p.dtype, p.device)
+        nb = p.numel() * p.element_size()
+        members, size = cur.get(key, ([], 0))
+        limit = cap.setdefault(key, min(tail_bytes, bucket_cap_bytes))
+        if members and size + nb > limit:  # close it: the next (earlier-filling) bucket may be larger
+            done.append((members, key[0], key[1]))
+            cap[key] = min(limit * growth, bucket_cap_bytes)
+            members, size = [], 0
+        members.append(idx)
+        cur[key] = (members, size + nb)
+    for key, (members, _) in cur.items():
+        if members:
+            done.append((members, key[0], key[1]))
+    specs: List[BucketSpec] = []
+    for members, dtype, device in sorted(done, key=lambda b: (max(pos[i] for i in b[0]),
+                                                              min(pos[i] for i in b[0]))):
+        members = sorted(members, key=lambda i: pos[i])  # slots in ready order, as the greedy plan
+        spec = BucketSpec(indices=members, dtype=dtype, device=device)
         off = 0
         for i in members:
             spec.offsets.append(off)

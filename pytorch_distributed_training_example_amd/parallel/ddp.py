@@ -28,6 +28,7 @@ from __future__ import annotations
 
 import contextlib
 import logging
+import os
 import warnings
 from typing import Any, Callable, Dict, List, Optional, Sequence
 
@@ -37,8 +38,9 @@ import torch.nn as nn
 
 from ..ops._native import cuda_available
 from ..ops import multi_tensor
-from .buckets import (DEFAULT_BUCKET_CAP_MB, DEFAULT_FIRST_BUCKET_BYTES, BucketSpec,
-                      compute_bucket_assignment)
+from .debug import ReducerDebug
+from .buckets import (AUTO_TAIL_BYTES, DEFAULT_BUCKET_CAP_MB, DEFAULT_FIRST_BUCKET_BYTES, BucketSpec,
+                      compute_bucket_assignment, plan_auto)
 
 log = logging.getLogger(__name__)
 
@@ -150,7 +152,7 @@ class DistributedDataParallel(nn.Module):
         broadcast_buffers: bool = True,
         init_sync: bool = True,
         process_group=None,
-        bucket_cap_mb: Optional[float] = None,
+        bucket_cap_mb: Optional[float | str] = None,
         find_unused_parameters: bool = False,
         check_reduction: bool = False,
         gradient_as_bucket_view: bool = True,
@@ -159,6 +161,7 @@ class DistributedDataParallel(nn.Module):
         reduce_dtype: Optional[torch.dtype] = None,
         rebuild_buckets: bool = True,
         reduce_single_rank: bool = False,
+        debug: Optional[bool] = None,
     ):
         super().__init__()
         self.module = module
@@ -173,7 +176,13 @@ class DistributedDataParallel(nn.Module):
         self.gradient_as_bucket_view = gradient_as_bucket_view
         self.static_graph = static_graph
         self.reduce_dtype = reduce_dtype
-        self.bucket_bytes_cap = int((bucket_cap_mb if bucket_cap_mb is not None
+        # "auto": the comm-model plan (buckets.plan_auto) — the bucket that fills last is capped at
+        # PDT_TAIL_BUCKET_MB (2 MiB) so the collective left after backward is short, earlier ones grow
+        self._auto_plan = isinstance(bucket_cap_mb, str) and bucket_cap_mb.lower() == "auto"
+        if isinstance(bucket_cap_mb, str) and not self._auto_plan:
+            bucket_cap_mb = float(bucket_cap_mb)
+        self._tail_bytes = int(float(os.environ.get("PDT_TAIL_BUCKET_MB", AUTO_TAIL_BYTES / 2 ** 20)) * 2 ** 20)
+        self.bucket_bytes_cap = int((bucket_cap_mb if bucket_cap_mb is not None and not self._auto_plan
                                      else DEFAULT_BUCKET_CAP_MB) * 1024 * 1024)
         self.first_bucket_bytes = int(first_bucket_mb * 1024 * 1024) if first_bucket_mb is not None \
             else min(DEFAULT_FIRST_BUCKET_BYTES, self.bucket_bytes_cap)
@@ -199,6 +208,11 @@ class DistributedDataParallel(nn.Module):
         # per backward: (bucket index, event on the compute stream when the bucket launched)
         self._launch_events: List[tuple] = []
         self._lead_samples: List[List[tuple]] = []
+        # debug mode (parallel/debug.py ReducerDebug): collective log + stream-safety assert + per-bucket
+        # checksum across ranks after every backward; ``PDT_DDP_DEBUG=1`` turns it on without code changes
+        if debug is None:
+            debug = os.environ.get("PDT_DDP_DEBUG", "0") not in ("", "0")
+        self._debug = ReducerDebug(self.process_group) if debug else None
 
         ignore = getattr(module, "_ddp_params_and_buffers_to_ignore", set())
         seen = set()
@@ -257,8 +271,11 @@ class DistributedDataParallel(nn.Module):
                     chunk, size = [], 0
 
     def _build_buckets(self, order: Optional[List[int]]) -> None:
-        specs = compute_bucket_assignment(self._params, self.bucket_bytes_cap,
-                                          self.first_bucket_bytes, order=order)
+        if self._auto_plan:
+            specs = plan_auto(self._params, self.bucket_bytes_cap, self._tail_bytes, order=order)
+        else:
+            specs = compute_bucket_assignment(self._params, self.bucket_bytes_cap,
+                                              self.first_bucket_bytes, order=order)
         old_grads = {i: p.grad for i, p in enumerate(self._params)}
         self._buckets: List[_Bucket] = []
         self._param_loc: Dict[int, tuple[int, int]] = {}
@@ -342,6 +359,9 @@ class DistributedDataParallel(nn.Module):
             self._launch_events.append((bucket.index, ev))
         if bucket.comm_buffer is not bucket.buffer:
             multi_tensor.copy_([bucket.buffer], [bucket.comm_buffer])
+        if self._debug is not None:
+            self._debug.on_launch(bucket.index, bucket.comm_buffer,
+                                  "comm_hook" if self._comm_hook is not None else "all_reduce")
         if self._comm_hook is not None:
             gb = GradBucket(bucket.index, bucket.comm_buffer, bucket.params, bucket.views,
                             bucket.index == len(self._buckets) - 1)
@@ -365,6 +385,8 @@ class DistributedDataParallel(nn.Module):
                         bucket.arrived[j] = True
                 bucket.pending = 0
         self._launch_ready_buckets()
+        works = [(b.index, b.future if b.future is not None else b.work) for b in self._buckets] \
+            if self._debug is not None else None
         for bucket in self._buckets:
             if bucket.future is not None:
                 out = bucket.future.wait()
@@ -385,6 +407,9 @@ class DistributedDataParallel(nn.Module):
                     elif p.grad.data_ptr() != v.data_ptr():
                         p.grad.copy_(v)
             bucket.reset()
+        if works is not None:  # every bucket reduced and unpacked: the optimizer reads them next
+            self._debug.after_backward(works, [b.buffer for b in self._buckets],
+                                       [[self._param_names[i] for i in b.spec.indices] for b in self._buckets])
         if timing:
             e1 = torch.cuda.Event(enable_timing=True)
             e1.record()

@@ -113,18 +113,23 @@ def init_distributed(
     # still polls it -> hipErrorCapturedEvent, process abort (seen 1 in 2 graphed bench runs, round 4).
     # Fresh events per collective cost nothing measurable at one bucket round per step.
     os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
+    # the flight recorder mirrors the RCCL watchdog's pending-work list (an entry is retired when the
+    # watchdog drops the work): engine/graph.py gates a hipGraph capture on it being empty
+    os.environ.setdefault("TORCH_FR_BUFFER_SIZE", "256")
 
     device = torch.device("cpu")
     if use_gpu:
         n = torch.cuda.device_count()
         rccl = backend == "nccl" or (backend == "pdt_p2p" and (os.environ.get("PDT_P2P_INNER") or "nccl") == "nccl")
-        if rccl and (e_lws > n or local_rank >= n):
-            # RCCL needs one GPU per rank; wrapping local_rank % n would put two ranks on one GPU and
-            # report an N-GPU measurement taken on fewer GPUs
-            raise RuntimeError(f"{backend}: local rank {local_rank} of {e_lws} but only {n} visible "
+        if rccl and n > 1 and local_rank >= n:
+            # RCCL needs one GPU per rank; wrapping local_rank % n would put two local ranks on one GPU
+            # and report an N-GPU measurement taken on fewer GPUs. n == 1 is the launcher that exposes
+            # one GPU per rank (ROCR/HIP_VISIBLE_DEVICES): device 0 is then this rank's own GPU. A missing
+            # LOCAL_WORLD_SIZE (mpirun/srun-style launches) is not compared against the device count.
+            raise RuntimeError(f"{backend}: local rank {local_rank} but only {n} visible "
                                f"GPU(s); RCCL needs one GPU per rank")
         # gloo rehearsals may share GPUs between ranks (tests/dist_utils.py use_gpu=True)
-        dev_idx = local_rank % max(n, 1)
+        dev_idx = 0 if n <= 1 else local_rank % n
         if set_device:
             torch.cuda.set_device(dev_idx)
         device = torch.device("cuda", dev_idx)

@@ -1,0 +1,237 @@
+"""AMP fp16 dynamic loss scaling on the GPU (SURVEY.md §2.3 "AMP: non-finite check + unscale, and
+loss-scale update"; BASELINE.json:5 "AMP loss scaling" as hand-written HIP). The reference trains in
+fp32 only (/root/reference/train.py:42-57); these tests pin our device-resident scaler
+(engine/amp.py: csrc/kernels/amp.hip ``amp_unscale`` + ``amp_update_kernel``) to
+``torch.amp.GradScaler`` semantics:
+
+  * a scripted sequence of finite / inf / nan / -inf steps: scale, growth tracker and parameters
+    equal torch's scaler + ``torch.optim.SGD`` after every step (growth and backoff both hit);
+  * every fused optimizer skips its update ON DEVICE when ``found_inf`` is set: a skipped step
+    followed by a clean scaled step equals one clean unscaled step (Adam's step counter included);
+  * one amp_fp16 DDP training step (1-rank RCCL reducer) of ViT-tiny / ResNet-18 against an fp32 oracle;
+  * one hipGraph-captured amp_fp16 step — capture fails on any host synchronisation — replayed
+    against eager, including a replay whose gradients overflow (skip + backoff on device).
+"""
+import copy
+import math
+
+import pytest
+import torch
+
+from dist_utils import run_ranks
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [(1000,), (37, 3), (64, 65)]
+
+
+def _grads(base, k, kind):
+    g = torch.Generator(device="cuda").manual_seed(100 + k)
+    gs = [torch.randn(p.shape, device="cuda", generator=g) for p in base]
+    if kind == "inf":
+        gs[1].view(-1)[5] = math.inf
+    elif kind == "nan":
+        gs[2].view(-1)[-1] = math.nan
+    elif kind == "ninf":
+        gs[0].view(-1)[0] = -math.inf
+    return gs
+
+
+def test_grad_scaler_matches_torch_over_scripted_sequence():
+    from pytorch_distributed_training_example_amd.engine.amp import GradScaler
+    from pytorch_distributed_training_example_amd.ops._native import native
+    from pytorch_distributed_training_example_amd.optim import FusedSGD
+    assert native() is not None  # the HIP path, not the CPU fallback
+    torch.manual_seed(0)
+    base = [torch.randn(s, device="cuda") for s in SHAPES]
+    ours_p = [b.clone().requires_grad_() for b in base]
+    ref_p = [b.clone().requires_grad_() for b in base]
+    kw = dict(init_scale=2.0 ** 10, growth_factor=2.0, backoff_factor=0.5, growth_interval=3)
+    ours, ref = GradScaler(**kw, device="cuda"), torch.amp.GradScaler("cuda", **kw)
+    opt_o = FusedSGD(ours_p, lr=0.1, momentum=0.9)
+    opt_r = torch.optim.SGD(ref_p, lr=0.1, momentum=0.9)
+    seq = ["ok", "ok", "inf", "ok", "ok", "ok", "ok", "nan", "ninf", "ok", "ok", "ok", "ok"]
+    scales = []
+    for k, kind in enumerate(seq):
+        s = ours.get_scale()
+        assert s == ref.get_scale()
+        gs = _grads(base, k, kind)
+        for p, g in zip(ours_p, gs):
+            p.grad = g * s
+        for p, g in zip(ref_p, gs):
+            p.grad = g * s
+        ours.step(opt_o)
+        ours.update()
+        ref.step(opt_r)
+        ref.update()
+        scales.append(ours.get_scale())
+        assert ours.get_scale() == ref.get_scale(), (k, kind, ours.get_scale(), ref.get_scale())
+        assert int(ours._growth_tracker.item()) == int(ref._growth_tracker.item()), k
+        assert float(ours.found_inf().item()) == 0.0  # reset for the next step
+        for a, b in zip(ours_p, ref_p):
+            torch.testing.assert_close(a, b, rtol=1e-6, atol=1e-6)
+    assert any(b > a for a, b in zip([1024.0] + scales, scales)), scales  # grew
+    assert any(b < a for a, b in zip([1024.0] + scales, scales)), scales  # backed off
+    # state_dict keys / values as torch's
+    sd, rsd = ours.state_dict(), ref.state_dict()
+    assert sd["scale"] == rsd["scale"] and sd["_growth_tracker"] == rsd["_growth_tracker"]
+
+
+def test_scale_update_does_not_grow_to_inf():
+    from pytorch_distributed_training_example_amd.engine.amp import GradScaler
+    sc = GradScaler(init_scale=3.0e38, growth_interval=1, device="cuda")
+    sc.update()  # growth would overflow fp32: the scale keeps its value (torch: isfinite check)
+    assert sc.get_scale() == pytest.approx(3.0e38) and math.isfinite(sc.get_scale())
+    assert int(sc._growth_tracker.item()) == 0
+
+
+def _opt(name, params):
+    from pytorch_distributed_training_example_amd.optim import FusedAdadelta, FusedAdamW, FusedSGD
+    if name == "sgd":
+        return FusedSGD(params, lr=1e-2, momentum=0.9, weight_decay=1e-4)
+    if name == "adamw":
+        return FusedAdamW(params, lr=1e-2, weight_decay=0.1)
+    return FusedAdadelta(params, lr=1.0, weight_decay=1e-4)
+
+
+def _state_tensors(opt, params):
+    out = []
+    for p in params:
+        for k, v in sorted(opt.state[p].items()):
+            if torch.is_tensor(v) and k != "step" or (k == "step" and torch.is_tensor(v) and v.is_cuda):
+                out.append((k, v.detach().clone()))
+    return out
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("name", ["sgd", "adamw", "adadelta"])
+def test_fused_optimizer_skips_on_found_inf(name, dtype):
+    """A: clean step, then an overflowed (skipped) step, then a clean SCALED step (inv_scale in-kernel).
+    B: the same two clean steps unscaled. A == B: the skip left params, master weights and every
+    state tensor (momentum, exp_avg/exp_avg_sq, Adam's device step counter, square_avg/acc_delta)
+    untouched, and the in-kernel unscale equals unscaled gradients."""
+    torch.manual_seed(1)
+    base = [torch.randn(s, device="cuda").to(dtype) for s in SHAPES]
+    pa = [b.clone().requires_grad_() for b in base]
+    pb = [b.clone().requires_grad_() for b in base]
+    oa, ob = _opt(name, pa), _opt(name, pb)
+    g1 = [torch.randn_like(b, dtype=torch.float32).to(dtype) for b in base]
+    g2 = [torch.randn_like(b, dtype=torch.float32).to(dtype) for b in base]
+    for ps, o in ((pa, oa), (pb, ob)):
+        for p, g in zip(ps, g1):
+            p.grad = g.clone()
+        o.step()
+    snap = [p.detach().clone() for p in pa], _state_tensors(oa, pa)
+    scale = 1024.0  # power of two: scaled then unscaled gradients are exact in bf16 too
+    inv = torch.full((1,), 1.0 / scale, device="cuda")
+    # overflowed step: garbage gradients, found_inf set -> no change at all
+    for p in pa:
+        p.grad = torch.full_like(p, math.inf)
+    oa.step(inv_scale=inv, found_inf=torch.ones(1, device="cuda"))
+    for a, b in zip(pa, snap[0]):
+        assert torch.equal(a.detach(), b), f"{name}: a skipped step changed a parameter"
+    for (k, a), (_, b) in zip(_state_tensors(oa, pa), snap[1]):
+        assert torch.equal(a, b), f"{name}: a skipped step changed state {k}"
+    # clean scaled step vs clean unscaled step
+    for p, g in zip(pa, g2):
+        p.grad = (g.float() * scale).to(dtype)
+    oa.step(inv_scale=inv, found_inf=torch.zeros(1, device="cuda"))
+    for p, g in zip(pb, g2):
+        p.grad = g.clone()
+    ob.step()
+    for a, b in zip(pa, pb):
+        torch.testing.assert_close(a.detach().float(), b.detach().float(), rtol=1e-6, atol=1e-6)
+    for (k, a), (_, b) in zip(_state_tensors(oa, pa), _state_tensors(ob, pb)):
+        torch.testing.assert_close(a.float(), b.float(), rtol=1e-6, atol=1e-7, msg=f"{name}: state {k}")
+
+
+def _amp_ddp_worker(rank, world, model_name):
+    from pytorch_distributed_training_example_amd.engine.amp import GradScaler
+    from pytorch_distributed_training_example_amd.engine.trainer import StepConfig, TrainStep, make_loss_fn
+    from pytorch_distributed_training_example_amd.models import get_model
+    from pytorch_distributed_training_example_amd.optim import FusedSGD
+    from pytorch_distributed_training_example_amd.parallel import DistributedDataParallel
+    torch.manual_seed(0)
+    if model_name == "vit_tiny":
+        model = get_model("vit_tiny", image_size=32, num_classes=10).cuda()
+        x = torch.randn(8, 3, 32, 32, device="cuda")
+    else:
+        model = get_model("resnet18", num_classes=10).cuda().to(memory_format=torch.channels_last)
+        x = torch.randn(8, 3, 64, 64, device="cuda").contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (8,), device="cuda", generator=torch.Generator(device="cuda").manual_seed(3))
+    if model_name == "vit_tiny":  # ViT zero-inits its head (no gradient would reach the body)
+        torch.nn.init.normal_(model.heads.head.weight, std=0.02)
+    oracle = copy.deepcopy(model)
+    ddp = DistributedDataParallel(model, broadcast_buffers=False, reduce_single_rank=True)
+    scaler = GradScaler(init_scale=2.0 ** 12, growth_interval=2000, device="cuda")
+    opt = FusedSGD(model.parameters(), lr=0.0)
+    loss_fn = make_loss_fn("cross_entropy")
+    step = TrainStep(ddp, opt, loss_fn, StepConfig(precision="amp_fp16", reducer="ddp"), scaler=scaler,
+                     raw_model=model)
+    loss = float(step(x, y))
+    torch.cuda.synchronize()
+    got = [p.grad.detach().float().cpu() for p in model.parameters()]
+    oracle.zero_grad(set_to_none=True)
+    ref_loss = loss_fn(oracle(x), y)
+    ref_loss.backward()
+    want = [p.grad.detach().float().cpu() for p in oracle.parameters()]
+    return loss, float(ref_loss), got, want, scaler.get_scale(), int(scaler._growth_tracker.item())
+
+
+@pytest.mark.parametrize("model_name", ["vit_tiny", "resnet18"])
+def test_amp_fp16_ddp_step_matches_fp32_oracle(model_name):
+    (loss, ref_loss, got, want, scale, tracker), = run_ranks(_amp_ddp_worker, 1, (model_name,), use_gpu=True,
+                                                             backend="nccl")
+    # a clean step: no overflow at 2^12, the tracker counted it, the unscaled gradients are the fp32 ones
+    assert scale == 2.0 ** 12 and tracker == 1
+    assert abs(loss - ref_loss) < 1e-2 * max(1.0, abs(ref_loss)), (loss, ref_loss)
+    rel = torch.tensor([((a - b).norm() / (b.norm() + 1e-12)).item() for a, b in zip(got, want)
+                        if b.norm() > 1e-6 * max(w.norm() for w in want)])
+    # fp16 autocast: 11-bit significands through the forward and backward GEMMs. Per-tensor errors are
+    # ~1e-3; a missing unscale would be 4096x off, a skipped update of the scale would show above
+    assert rel.median() < 1e-2 and rel.max() < 6e-2, (float(rel.median()), float(rel.max()), int(rel.argmax()))
+
+
+def test_amp_fp16_graph_captured_step():
+    """The whole amp_fp16 step (autocast forward, scaled backward, unscale + inf-check, fused SGD with
+    on-device skip, scale update) captured once and replayed: equals eager step for step, and a replay
+    on an input that overflows skips the update and halves the scale on device."""
+    from pytorch_distributed_training_example_amd.engine.amp import GradScaler
+    from pytorch_distributed_training_example_amd.engine.trainer import StepConfig, TrainStep, make_loss_fn
+    from pytorch_distributed_training_example_amd.models import get_model
+    from pytorch_distributed_training_example_amd.optim import FusedSGD
+
+    def build():
+        torch.manual_seed(0)
+        m = get_model("vit_tiny", image_size=32, num_classes=10).cuda()
+        torch.nn.init.normal_(m.heads.head.weight, std=0.02)
+        sc = GradScaler(init_scale=2.0 ** 12, growth_interval=2, device="cuda")
+        opt = FusedSGD(m.parameters(), lr=1e-2, momentum=0.9)
+        return m, sc, TrainStep(m, opt, make_loss_fn("cross_entropy"), StepConfig(precision="amp_fp16", reducer="none"),
+                                scaler=sc, raw_model=m)
+
+    g = torch.Generator(device="cuda").manual_seed(5)
+    xs = [torch.randn(8, 3, 32, 32, device="cuda", generator=g) for _ in range(8)]
+    ys = [torch.randint(0, 10, (8,), device="cuda", generator=g) for _ in range(8)]
+    bad = 3  # this replay's input overflows fp16 in the forward -> non-finite gradients
+    xs[bad] = xs[bad] * 1e6
+    me, se, te = build()
+    mg, sg, tg = build()
+    tg.enable_graph(warmup=2)
+    # the graphed runner's first call runs 2 eager warm-up steps on xs[0] (StaticStep.capture), captures,
+    # then replays xs[0]: eager does the same 2 extra steps first
+    for _ in range(2):
+        te(xs[0], ys[0])
+    le, lg, scales = [], [], []
+    for i in range(len(xs)):
+        le.append(float(te(xs[i], ys[i])))
+        lg.append(float(tg(xs[i], ys[i])))
+        scales.append(se.get_scale())
+        assert se.get_scale() == sg.get_scale(), (i, se.get_scale(), sg.get_scale())
+        for a, b in zip(me.parameters(), mg.parameters()):
+            torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6, msg=f"replay {i}")
+    assert tg._graphs and all(r.graph is not None for r in tg._graphs.values())
+    # the overflow replay backed off on device; the clean replays grew the scale (interval 2)
+    assert scales[bad] == scales[bad - 1] / 2, scales
+    assert max(scales[bad + 1:]) > scales[bad], scales
+    assert all(math.isfinite(v) for i, v in enumerate(le) if i != bad)

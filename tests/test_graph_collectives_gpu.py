@@ -57,6 +57,11 @@ def _train(rank, mode, hook):
     else:
         runner = StaticStep(step, [xs[0], ys[0]], warmup=3)
         runner.capture()
+        import torch.distributed as dist
+        if dist.get_backend() == "nccl":
+            # the capture was gated on the RCCL watchdog having retired every warm-up collective
+            # (engine/graph.py wait_pg_watchdog_idle, flight recorder on): verified, not slept on
+            assert runner.watchdog_idle is True
         for x, y in zip(xs[1:], ys[1:]):
             out.append(float(runner(x, y)))
     torch.cuda.synchronize()

@@ -148,3 +148,37 @@ def test_resnet50_fp32_native_matches_stock():
     ratio = float(ga["conv1.weight"].norm() / gb["conv1.weight"].norm())
     assert 0.8 < ratio < 1.25, ratio
     assert float(e.median()) < 0.05 and float(e.max()) < 0.5, (float(e.median()), float(e.max()))
+
+
+def test_resnet50_frozen_bn3_keeps_conv1_branch_gradient():
+    """A training bottleneck whose bn3 is frozen (eval mode, running statistics) must not take the
+    residual-gradient link: the eval BatchNorm returns the shortcut gradient through autograd, so the
+    link stays empty and conv1's backward would park its branch gradient for a partner that never
+    comes (models/resnet.py). Linked path on vs off: same gradients to bf16 noise."""
+    from pytorch_distributed_training_example_amd.models import get_model
+    from pytorch_distributed_training_example_amd.models import resnet as R
+    from pytorch_distributed_training_example_amd.models.precision import to_bf16_mixed
+
+    def grads(link):
+        R.RESIDUAL_GRAD_LINK[0] = link
+        try:
+            torch.manual_seed(0)
+            m = to_bf16_mixed(get_model("resnet50", num_classes=16).cuda().to(memory_format=torch.channels_last))
+            for mod in m.modules():
+                if isinstance(mod, R.Bottleneck):
+                    mod.bn3.eval()
+            g = torch.Generator(device="cuda").manual_seed(2)
+            x = torch.randn(4, 3, 96, 96, device="cuda", generator=g).bfloat16().contiguous(
+                memory_format=torch.channels_last)
+            y = torch.randint(0, 16, (4,), device="cuda", generator=g)
+            torch.nn.functional.cross_entropy(m(x).float(), y).backward()
+            return {k: p.grad.float().clone() for k, p in m.named_parameters()}
+        finally:
+            R.RESIDUAL_GRAD_LINK[0] = True
+
+    ga, gb = grads(True), grads(False)
+    ratio = float(ga["conv1.weight"].norm() / gb["conv1.weight"].norm())
+    assert 0.9 < ratio < 1.1, ratio
+    e = torch.tensor([float((ga[k] - gb[k]).norm() / gb[k].norm().clamp_min(1e-12)) for k in gb
+                      if gb[k].norm() > 0])
+    assert float(e.median()) < 2e-2, float(e.median())
