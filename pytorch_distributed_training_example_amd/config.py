@@ -42,6 +42,9 @@ PDT_BWD_FUSED               1            bottleneck conv3 + bn3 backward as one 
 PDT_BWD_FUSED_SHAPES        256x64       (Co x Ci) of the conv3s that take the fused backward ("256x64,512x128" adds
                                          layer 2: 0.9 % slower in-step since the branch-free conv1x1 epilogue,
                                          profiles/r5/ab_layer2_unfused.txt)
+PDT_BWD_ALG                 1            bottleneck conv3 + bn3 backward (the shapes PDT_BWD_FUSED does not take) without
+                                         bn3's apply pass: z = a W^T substituted into bn3's backward (ops/conv.py
+                                         _bwd_alg, csrc/kernels/bn_alg.hip): one wgrad pass + one data-gradient GEMM
 PDT_BN2_DEFER               0            1: with PDT_BWD_FUSED, bn2's apply + ReLU deferred into conv3 (read on load
                                          in the forward GEMM, recomputed in the fused backward, which writes bn2's
                                          mask). Measured -0.2 %, and -2 % with PDT_BN_APPLY_GEMM_K (the relu(a x + b)
@@ -73,7 +76,7 @@ class _Switches:
                  "conv1x1_table", "conv1x1_dump", "conv1x1_s2", "conv3x3", "conv3x3_wgrad", "conv3x3_s2", "conv_stem",
                  "conv_bn_stats", "bn_bwd_stats", "res_masked", "stem_bwd_fused", "stem_bn_wgrad", "stem_bn_stats", "stem_pool_wgrad", "wgrad_splitk", "slice_sum",
                  "subsample_native", "linear_splitk", "fused_addln", "embedding_native", "linear_epilogue",
-                 "bwd_fused", "bwd_fused_shapes", "bn2_defer", "bn_apply_gemm_k", "strided_bstats", "gap_native",
+                 "bwd_fused", "bwd_fused_shapes", "bwd_alg", "bn2_defer", "bn_apply_gemm_k", "strided_bstats", "gap_native",
                  "fp8_fused_gelu", "fp8_weight_multi", "fp8_cast_colsum", "fp8_ln", "wgrad_stream_m")
 
     def __init__(self):
@@ -119,6 +122,7 @@ class _Switches:
         self.bwd_fused = on("PDT_BWD_FUSED")
         self.bwd_fused_shapes = tuple(tuple(int(v) for v in t.split("x")) for t in
                                       e("PDT_BWD_FUSED_SHAPES", "256x64").split(",") if "x" in t)
+        self.bwd_alg = on("PDT_BWD_ALG")
         self.bn2_defer = on("PDT_BN2_DEFER", "0")
         self.bn_apply_gemm_k = int(e("PDT_BN_APPLY_GEMM_K", "64"))
         self.strided_bstats = on("PDT_STRIDED_BSTATS")

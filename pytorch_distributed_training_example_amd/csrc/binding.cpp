@@ -139,6 +139,14 @@ int pdt_maxpool3s2_bwd(const uint16_t* dy, const uint8_t* code, uint16_t* dz, in
                        hipStream_t s);
 int pdt_conv1x1_tile_rows();
 int64_t pdt_conv1x1_wgrad_ws_floats(int M, int Ci, int Co, int* nsplit_out);
+int64_t pdt_conv1x1_wgrad_seg_ws_floats(int M, int Ci, int co1, int co2, int* rows_out);
+int pdt_conv1x1_wgrad_seg(const uint16_t* x, const uint16_t* dy1, int co1, const uint16_t* dy2, int co2, float* out,
+                          float* ws, int M, int Ci, hipStream_t s);
+int pdt_conv1x1_gemm_seg(const uint16_t* a1, int k1, const uint16_t* a2, int k2, int rep2, const uint16_t* b,
+                         uint16_t* y, int M, int N, const uint16_t* bn_x, const uint8_t* bn_mask, const float* bn_mean,
+                         float* bn_part, hipStream_t s);
+int pdt_bn_alg_assemble(const uint16_t* W, const float* coef, const float* mean, const float* G, const float* wg,
+                        const float* BWG, uint16_t* bcat, uint16_t* dW, int C4, int CW, hipStream_t s);
 int pdt_conv1x1_wgrad(const uint16_t* x, const uint16_t* dy, uint16_t* dw, float* ws, int M, int Ci, int Co,
                       hipStream_t s);
 void pdt_conv1x1_wgrad_tune(int target_wgs, int variant, int interleave);
@@ -1113,6 +1121,99 @@ Tensor conv1x1_wgrad(Tensor x, Tensor dy) {
   if (rc == -1 || rc == -2) return Tensor();
   TORCH_CHECK(rc == 0, "pdt_conv1x1_wgrad failed: ", rc);
   return dw;
+}
+
+// ALG backward of conv3 + bn3 (csrc/kernels/bn_alg.hip, ops/conv.py _bwd_alg): [dy1 | dy2 | 1]^T x in fp32,
+// rows co1 + co2 (+ the ones block: column sums of x). x [M, Ci], dy1 [M, co1], dy2 [M, co2] contiguous bf16.
+// Returns an empty tensor for an unsupported shape.
+Tensor conv1x1_wgrad_seg(Tensor x, Tensor dy1, Tensor dy2) {
+  for (const Tensor* t : {&x, &dy1, &dy2}) {
+    check_cuda(*t, "conv1x1_wgrad_seg operand");
+    TORCH_CHECK(t->dim() == 2 && t->scalar_type() == at::kBFloat16 && t->is_contiguous() && t->size(0) == x.size(0),
+                "conv1x1_wgrad_seg: contiguous bf16 [M, *] operands");
+  }
+  const int64_t M = x.size(0), Ci = x.size(1), co1 = dy1.size(1), co2 = dy2.size(1);
+  if (M * std::max(std::max(Ci, co1), co2) >= ((int64_t)1 << 31)) return Tensor();
+  int rows = 0;
+  const int64_t wsf = pdt_conv1x1_wgrad_seg_ws_floats((int)M, (int)Ci, (int)co1, (int)co2, &rows);
+  if (wsf == 0) return Tensor();
+  auto ws = at::empty({wsf}, x.options().dtype(at::kFloat));
+  auto out = at::empty({rows, Ci}, x.options().dtype(at::kFloat));
+  const int rc = pdt_conv1x1_wgrad_seg(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                                       reinterpret_cast<const uint16_t*>(dy1.data_ptr()), (int)co1,
+                                       reinterpret_cast<const uint16_t*>(dy2.data_ptr()), (int)co2, out.data_ptr<float>(),
+                                       ws.data_ptr<float>(), (int)M, (int)Ci, stream());
+  if (rc == -1 || rc == -2) return Tensor();
+  TORCH_CHECK(rc == 0, "pdt_conv1x1_wgrad_seg failed: ", rc);
+  return out;
+}
+
+// out[M, N] = [a1 | a2 x rep2 | 1] b^T (b [N, k1 + rep2 k2 + 32]) with the BSTATS epilogue when bn_x is given
+// (then returns the backward partials [2, T, N], as conv1x1_gemm).
+c10::optional<Tensor> conv1x1_gemm_seg(Tensor a1, Tensor a2, int64_t rep2, Tensor b, Tensor out,
+                                       c10::optional<Tensor> bn_x, c10::optional<Tensor> bn_mask,
+                                       c10::optional<Tensor> bn_mean) {
+  for (const Tensor* t : {&a1, &a2, &b, &out}) {
+    check_cuda(*t, "conv1x1_gemm_seg operand");
+    TORCH_CHECK(t->scalar_type() == at::kBFloat16 && t->dim() == 2 && t->is_contiguous(),
+                "conv1x1_gemm_seg: operands must be 2-D contiguous bf16");
+  }
+  const int64_t M = a1.size(0), k1 = a1.size(1), k2 = a2.size(1), N = b.size(0);
+  TORCH_CHECK(a2.size(0) == M && out.size(0) == M && out.size(1) == N && b.size(1) == k1 + rep2 * k2 + 32 && rep2 >= 1,
+              "conv1x1_gemm_seg: shape mismatch");
+  TORCH_CHECK(k1 % 32 == 0 && k2 % 32 == 0 && N % 64 == 0, "conv1x1_gemm_seg: k1, k2 % 32 and N % 64 required");
+  c10::optional<Tensor> part;
+  const uint16_t* bx = nullptr;
+  const uint8_t* bm = nullptr;
+  const float* bmean = nullptr;
+  if (bn_x.has_value() && bn_x->defined()) {
+    check_cuda(*bn_x, "bn_x");
+    TORCH_CHECK(bn_x->scalar_type() == at::kBFloat16 && bn_x->numel() == M * N && bn_x->is_contiguous(
+                    bn_x->dim() == 4 ? at::MemoryFormat::ChannelsLast : at::MemoryFormat::Contiguous),
+                "conv1x1_gemm_seg: bn_x must be [M, N] bf16 (channels_last when 4-D)");
+    TORCH_CHECK(bn_mean.has_value() && bn_mean->defined() && bn_mean->scalar_type() == at::kFloat &&
+                bn_mean->numel() == N && bn_mean->is_contiguous() && bn_mean->is_cuda(),
+                "conv1x1_gemm_seg: bn_mean must be fp32 [N]");
+    if (bn_mask.has_value() && bn_mask->defined()) {
+      TORCH_CHECK(bn_mask->scalar_type() == at::kByte && bn_mask->numel() == M * N / 8 && bn_mask->is_cuda(),
+                  "conv1x1_gemm_seg: bn_mask must be uint8 [M * N / 8]");
+      bm = bn_mask->data_ptr<uint8_t>();
+    }
+    bx = reinterpret_cast<const uint16_t*>(bn_x->data_ptr());
+    bmean = bn_mean->data_ptr<float>();
+    const int64_t T = (M + pdt_conv1x1_tile_rows() - 1) / pdt_conv1x1_tile_rows();
+    part = at::empty({2, T, N}, a1.options().dtype(at::kFloat));
+  }
+  const int rc = pdt_conv1x1_gemm_seg(reinterpret_cast<const uint16_t*>(a1.data_ptr()), (int)k1,
+                                      reinterpret_cast<const uint16_t*>(a2.data_ptr()), (int)k2, (int)rep2,
+                                      reinterpret_cast<const uint16_t*>(b.data_ptr()),
+                                      reinterpret_cast<uint16_t*>(out.data_ptr()), (int)M, (int)N, bx, bm, bmean,
+                                      part.has_value() ? part->data_ptr<float>() : nullptr, stream());
+  TORCH_CHECK(rc == 0, "pdt_conv1x1_gemm_seg failed: ", rc);
+  return part;
+}
+
+// (bcat [CW, C4 + 2 CW + 32] bf16, dW [C4, CW] bf16) of the ALG backward (csrc/kernels/bn_alg.hip).
+std::vector<Tensor> bn_alg_assemble(Tensor w, Tensor coef, Tensor mean, Tensor G, Tensor wg, Tensor BWG) {
+  for (const Tensor* t : {&w, &coef, &mean, &G, &wg, &BWG}) {
+    check_cuda(*t, "bn_alg_assemble operand");
+    TORCH_CHECK(t->is_contiguous(), "bn_alg_assemble: contiguous operands");
+  }
+  TORCH_CHECK(w.dim() == 2 && w.scalar_type() == at::kBFloat16, "bn_alg_assemble: w [C4, CW] bf16");
+  const int64_t C4 = w.size(0), CW = w.size(1);
+  TORCH_CHECK(coef.scalar_type() == at::kFloat && coef.numel() == 3 * C4 && mean.scalar_type() == at::kFloat &&
+                  mean.numel() == C4 && G.scalar_type() == at::kFloat && G.numel() == CW * CW &&
+                  BWG.scalar_type() == at::kFloat && BWG.numel() == C4 * CW && wg.scalar_type() == at::kFloat &&
+                  wg.dim() == 2 && wg.size(1) == CW && wg.size(0) > C4 + CW,
+              "bn_alg_assemble: operand shapes");
+  auto bcat = at::empty({CW, C4 + 2 * CW + 32}, w.options());
+  auto dW = at::empty({C4, CW}, w.options());
+  const int rc = pdt_bn_alg_assemble(reinterpret_cast<const uint16_t*>(w.data_ptr()), coef.data_ptr<float>(),
+                                     mean.data_ptr<float>(), G.data_ptr<float>(), wg.data_ptr<float>(),
+                                     BWG.data_ptr<float>(), reinterpret_cast<uint16_t*>(bcat.data_ptr()),
+                                     reinterpret_cast<uint16_t*>(dW.data_ptr()), (int)C4, (int)CW, stream());
+  TORCH_CHECK(rc == 0, "pdt_bn_alg_assemble failed: ", rc);
+  return {bcat, dW};
 }
 
 // BN training forward with the statistics taken from conv1x1_gemm's per-tile partials.
@@ -2209,6 +2310,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("stem_conv_wgrad_bn_pool", &stem_conv_wgrad_bn_pool);
   m.def("conv3x3s1_wgrad", &conv3x3s1_wgrad);
   m.def("conv1x1_wgrad", &conv1x1_wgrad);
+  m.def("conv1x1_wgrad_seg", &conv1x1_wgrad_seg);
+  m.def("conv1x1_gemm_seg", &conv1x1_gemm_seg, py::arg("a1"), py::arg("a2"), py::arg("rep2"), py::arg("b"),
+        py::arg("out"), py::arg("bn_x") = py::none(), py::arg("bn_mask") = py::none(), py::arg("bn_mean") = py::none());
+  m.def("bn_alg_assemble", &bn_alg_assemble);
   m.def("conv1x1_wgrad_tune", [](int target_wgs, int variant, int interleave) { pdt_conv1x1_wgrad_tune(target_wgs, variant, interleave); },
         py::arg("target_wgs"), py::arg("variant") = -2, py::arg("interleave") = -2);
   m.def("embedding_fwd", &embedding_fwd);

@@ -975,12 +975,13 @@ __global__ __launch_bounds__(256) void gap_bwd_kernel(const uint16_t* __restrict
     st.y = (uint32_t)f2bf(v[2] * scale) | ((uint32_t)f2bf(v[3] * scale) << 16);
     st.z = (uint32_t)f2bf(v[4] * scale) | ((uint32_t)f2bf(v[5] * scale) << 16);
     st.w = (uint32_t)f2bf(v[6] * scale) | ((uint32_t)f2bf(v[7] * scale) << 16);
-    *reinterpret_cast<uint4*>(dy + e * 8) = st;
     if constexpr (BNRED) {
       const uint4 xv = *reinterpret_cast<const uint4*>(xb + e * 8);
       const unsigned mk = mask ? mask[e] : 0xffu;
       bn_bwd_accum8(st, xv, mk, mu, s1, s2);
+      st = mask8(st, mk);  // stored masked, as the 1x1 GEMM's BSTATS epilogue (tile_stats.h mask8)
     }
+    *reinterpret_cast<uint4*>(dy + e * 8) = st;
   }
   if constexpr (BNRED) {
     __shared__ float red[256 * 16];

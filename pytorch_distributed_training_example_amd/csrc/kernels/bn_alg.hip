@@ -1,0 +1,83 @@
+// Small-matrix assembly of the ALGEBRAIC backward of a ResNet bottleneck's conv3 + bn3 (gfx950).
+//
+// conv3: z = a W^T (a [M, CW] = bn2's output, W [C4, CW]); bn3's backward gives its input gradient as
+//   dz = A g + B (z - mu) + D          (per channel c of C4; g = dy * relu mask, A B D = bn_bwd_coef)
+// Substituting z = a W^T (the conv's own forward) removes z and dz from the backward entirely:
+//   da = dz W     = g (diag(A) W) + a G + c,      G = W^T diag(B) W [CW, CW],  c = E W,  E = D - B mu
+//   dW = dz^T a   = diag(A) P + diag(B) W Gram + E (x) S
+// with P = g^T a [C4, CW], Gram = a^T a [CW, CW] and S = column sums of a — all three from ONE pass of
+// the 1x1 weight-gradient kernel over (g, a) (conv1x1_wgrad.hip SEG), and da from ONE GEMM over the
+// K-concatenation [g | a | a | 1] against b = [diag(A) W | G_hi | G_lo | c_hi, c_lo, 0...]^T rows
+// (conv1x1.hip SEG; G and c split into bf16 hi + lo parts: the a G term can cancel part of g diag(A) W).
+// The BatchNorm's backward apply pass (read dy, z, mask; write dz) and both re-reads of dz are gone:
+// per bottleneck of ResNet-50 layers 2-4 one 4C-channel tensor is read twice instead of five times.
+//
+// This file: one launch that writes b (bf16 [CW, Kt], Kt = C4 + 2 CW + 32) and dW (bf16 [C4, CW]) from
+// W, the coefficients and the fp32 products G (= W^T diag(B) W) and BWG (= diag(B) W Gram).
+// Not in the reference (LeNet has no BatchNorm, /root/reference/cnn.py:9-23).
+#include "../common.h"
+
+using namespace pdt;
+
+namespace {
+
+__device__ __forceinline__ float bfv(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
+
+// blocks [0, CW): row k of b; blocks [CW, ...): 256-element slices of dW
+__global__ __launch_bounds__(256) void bn_alg_assemble_kernel(const uint16_t* __restrict__ W, const float* __restrict__ coef,
+                                                              const float* __restrict__ mean, const float* __restrict__ G,
+                                                              const float* __restrict__ wg, const float* __restrict__ BWG,
+                                                              uint16_t* __restrict__ bcat, uint16_t* __restrict__ dW,
+                                                              int C4, int CW) {
+  __shared__ float red[4];
+  const int tid = threadIdx.x;
+  const int Kt = C4 + 2 * CW + 32;
+  const float* A = coef;
+  const float* Bc = coef + C4;
+  const float* D = coef + 2 * C4;
+  if ((int)blockIdx.x < CW) {
+    const int k = blockIdx.x;
+    uint16_t* row = bcat + (int64_t)k * Kt;
+    float cs = 0.f;
+    for (int c = tid; c < C4; c += 256) {
+      const float w = bfv(W[(int64_t)c * CW + k]);
+      row[c] = f2bf(w * A[c]);
+      cs += (D[c] - Bc[c] * mean[c]) * w;
+    }
+    for (int j = tid; j < CW; j += 256) {
+      const float gv = G[(int64_t)k * CW + j];
+      const uint16_t hi = f2bf(gv);
+      row[C4 + j] = hi;
+      row[C4 + CW + j] = f2bf(gv - bfv(hi));
+    }
+    cs = block_sum(cs, red);
+    if (tid < 32) {
+      const uint16_t hi = f2bf(cs);
+      row[C4 + 2 * CW + tid] = tid == 0 ? hi : (tid == 1 ? f2bf(cs - bfv(hi)) : (uint16_t)0);
+    }
+    return;
+  }
+  const int64_t e = (int64_t)(blockIdx.x - CW) * 256 + tid;
+  if (e >= (int64_t)C4 * CW) return;
+  const int c = (int)(e / CW), k = (int)(e % CW);
+  const float S = wg[(int64_t)(C4 + CW) * CW + k];  // first row of the ones block: column sums of a
+  const float E = D[c] - Bc[c] * mean[c];
+  dW[e] = f2bf(A[c] * wg[e] + BWG[e] + E * S);
+}
+
+}  // namespace
+
+extern "C" {
+
+// bcat [CW, C4 + 2 CW + 32] bf16, dW [C4, CW] bf16; W [C4, CW] bf16 row-major; coef [3, C4] (A, B, D), mean [C4],
+// G [CW, CW], BWG [C4, CW] fp32; wg: pdt_conv1x1_wgrad_seg's output (rows 0..C4-1 = P, row C4 + CW = S).
+int pdt_bn_alg_assemble(const uint16_t* W, const float* coef, const float* mean, const float* G, const float* wg,
+                        const float* BWG, uint16_t* bcat, uint16_t* dW, int C4, int CW, hipStream_t s) {
+  if (C4 < 1 || CW < 1) return -1;
+  const int64_t nd = ((int64_t)C4 * CW + 255) / 256;
+  hipLaunchKernelGGL(bn_alg_assemble_kernel, dim3((unsigned)(CW + nd)), dim3(256), 0, s, W, coef, mean, G, wg, BWG,
+                     bcat, dW, C4, CW);
+  return 0;
+}
+
+}  // extern "C"

@@ -60,6 +60,15 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 #define PDT_LDS __attribute__((address_space(3)))
 
 __device__ __attribute__((aligned(256))) uint4 g_gemm_zero[16];  // zero page for rows past M (never written)
+__device__ __attribute__((aligned(256))) uint4 g_gemm_ones[16] = {  // bf16 1.0 page (SEG's bias segment)
+    {0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u}, {0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u},
+    {0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u}, {0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u},
+    {0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u}, {0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u},
+    {0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u}, {0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u},
+    {0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u}, {0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u},
+    {0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u}, {0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u},
+    {0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u}, {0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u},
+    {0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u}, {0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u}};
 __device__ uint8_t g_mask_ones[16] = {  // (non-const: global, not constant, address space)
    0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff,
                                             0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff};  // "no mask"
@@ -122,6 +131,11 @@ struct ApArgs {
   uint8_t* mask;
   int probe;  // diagnosis only (pdt_conv1x1_probe): 1 = no output stores, 2 = no MFMA, 4 = no operand DMA,
              // 8 = 64-channel tiles (4 waves) for every N, 64 = no 256-channel tiles
+  // SEG (a2 != null; one-tile kernel only): A is the K-concatenation [A (k1 columns) | a2 (k2) repeated rep2
+  // times | 32 columns of 1.0] — B holds the matching [N, k1 + rep2 k2 + 32] rows. The ones segment adds a
+  // per-column bias (B's columns there); a repeated a2 segment meets a hi / lo split of its B block.
+  const uint16_t* a2;
+  int k1, k2, rep2;
 };
 
 int g_probe = 0;
@@ -145,11 +159,16 @@ __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv1x1_kernel(
   const int m0 = mt * BM, n0 = (tile % ntiles) * BN;
 
   const int sub = lane >> 2, p = lane & 3;
+  // SEG: A rows are k1 long (the first segment); a2 rows k2 long (workgroup-uniform)
+  const bool seg = ap.a2 != nullptr;
+  const int lda = seg ? ap.k1 : K;
   int aoff[Cf::kALd];  // element offset of this lane's A piece, -1 = zero page
+  int a2off[Cf::kALd];
 #pragma unroll
   for (int i = 0; i < Cf::kALd; ++i) {
     const int r = (wid * Cf::kALd + i) * 16 + sub;
-    aoff[i] = m0 + r < M ? (m0 + r) * K + chk64(r, p) * 8 : -1;
+    aoff[i] = m0 + r < M ? (m0 + r) * lda + chk64(r, p) * 8 : -1;
+    a2off[i] = (m0 + r) * ap.k2 + chk64(r, p) * 8;
   }
   int boff[Cf::kBLd];
 #pragma unroll
@@ -162,9 +181,15 @@ __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv1x1_kernel(
   auto issue = [&](int s) {
     char* slot = lds + (s % Cf::kSlots) * Cf::kSlot;
     const int ko = s * Cf::BK;
+    // SEG: which segment this k-step reads (uniform), and the column inside it
+    const int ks2 = ko - ap.k1, seg2 = seg && ks2 >= 0 && ks2 < ap.rep2 * ap.k2 ? 1 : (seg && ks2 >= 0 ? 2 : 0);
+    const int ko2 = seg2 == 1 ? ks2 % ap.k2 : 0;
 #pragma unroll
     for (int i = 0; i < Cf::kALd; ++i) {
-      const uint16_t* src = aoff[i] >= 0 ? A + (aoff[i] + ko) : reinterpret_cast<const uint16_t*>(g_gemm_zero);
+      const uint16_t* src = aoff[i] < 0 ? reinterpret_cast<const uint16_t*>(g_gemm_zero)
+                            : seg2 == 0 ? A + (aoff[i] + ko)
+                            : seg2 == 1 ? ap.a2 + (a2off[i] + ko2)
+                                        : reinterpret_cast<const uint16_t*>(g_gemm_ones);
       dma16(src, slot + (wid * Cf::kALd + i) * 1024);
     }
 #pragma unroll
@@ -382,7 +407,10 @@ __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv1x1_kernel(
       v.z = (uint32_t)f2bf(z[4]) | ((uint32_t)f2bf(z[5]) << 16);
       v.w = (uint32_t)f2bf(z[6]) | ((uint32_t)f2bf(z[7]) << 16);
     }
-    if constexpr (BSTATS) bn_bwd_accum8(v, xbv[it], bmkv[it], bmu, bs1, bs2);
+    if constexpr (BSTATS) {
+      bn_bwd_accum8(v, xbv[it], bmkv[it], bmu, bs1, bs2);
+      v = mask8(v, bmkv[it]);  // stored masked (tile_stats.h mask8)
+    }
     if (!ok) continue;
     if constexpr (STATS) rs8_add(rst, v);
     if constexpr (APPLY) {
@@ -718,7 +746,10 @@ __global__ __launch_bounds__(Cf::kThreads, PL<Cf>::kMinWaves) void conv1x1p_kern
             v.z = (uint32_t)f2bf(z[4]) | ((uint32_t)f2bf(z[5]) << 16);
             v.w = (uint32_t)f2bf(z[6]) | ((uint32_t)f2bf(z[7]) << 16);
           }
-          if constexpr (BSTATS) bn_bwd_accum8(v, xbv[it], bmkv[it], bmu, bs1, bs2);
+          if constexpr (BSTATS) {
+            bn_bwd_accum8(v, xbv[it], bmkv[it], bmu, bs1, bs2);
+            v = mask8(v, bmkv[it]);  // stored masked (tile_stats.h mask8)
+          }
           if constexpr (STATS) {
             if (ok) rs8_add(rst, v);
           }
@@ -814,7 +845,8 @@ int launch_nt(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t*
   if constexpr (!NT) {
     constexpr bool kMeasured = Cf::kWaves >= 16 && !ACC && !ATR && !APPLY;  // see g_persist
     const int pm = persist_mode();
-    if ((pm == 2 || (pm == 1 && kMeasured)) && g_probe == 0 && grid >= 2 * 256 * (int64_t)((160 * 1024) / PL<Cf>::kLds))
+    if ((pm == 2 || (pm == 1 && kMeasured)) && g_probe == 0 && !ap.a2 &&
+        grid >= 2 * 256 * (int64_t)((160 * 1024) / PL<Cf>::kLds))
       return launch_p<Cf, ACC, STATS, BSTATS, ATR, APPLY, STR>(a, b, y, c, cm, part, M, K, N, bs, cg, s, acoef, apx);
   }
   hipLaunchKernelGGL((conv1x1_kernel<Cf, ACC, STATS, NT, BSTATS, ATR, APPLY, STR>), dim3((unsigned)grid),
@@ -916,6 +948,28 @@ int pdt_conv1x1_gemm(const uint16_t* a, const uint16_t* b, uint16_t* y, const ui
   if (N % 128 == 0 && !(g_probe & 8) && !small_grid_narrow((int64_t)((M + 255) / 256) * (N / 128)))
     return dispatch<GWide>(a, b, y, c, cm, part, M, K, N, bs, cg, s, acoef);
   return dispatch<GNarrow>(a, b, y, c, cm, part, M, K, N, bs, cg, s, acoef);
+}
+
+// SEG: y[M,N] = [a1 | a2 (x rep2) | 1] [M, k1 + rep2 k2 + 32] * b[N, k1 + rep2 k2 + 32]^T, with the BSTATS
+// epilogue when bn_x is given (as pdt_conv1x1_gemm). a1 [M, k1], a2 [M, k2] row-major bf16, k1 % 32 == 0,
+// k2 % 32 == 0 (ops/conv.py _bwd_alg: the data gradient of conv3 with bn3's backward folded into b).
+int pdt_conv1x1_gemm_seg(const uint16_t* a1, int k1, const uint16_t* a2, int k2, int rep2, const uint16_t* b,
+                         uint16_t* y, int M, int N, const uint16_t* bn_x, const uint8_t* bn_mask, const float* bn_mean,
+                         float* bn_part, hipStream_t s) {
+  const int K = k1 + rep2 * k2 + 32;
+  if (M < 1 || k1 < 32 || k1 % 32 || k2 < 32 || k2 % 32 || rep2 < 1 || N < 64 || N % 64 != 0 || !a2) return -1;
+  if ((int64_t)M * (K > N ? K : N) >= ((int64_t)1 << 31) || (int64_t)N * K >= ((int64_t)1 << 31)) return -2;
+  const BnSrc bs{bn_x, bn_mask, bn_mean, bn_part};
+  const CGeom cg{0, 1, 1, 1, 1};
+  ApArgs ap{};
+  ap.a2 = a2; ap.k1 = k1; ap.k2 = k2; ap.rep2 = rep2;
+  if (bn_part) {
+    if (!bn_x || !bn_mean) return -1;
+    if (N % 128 == 0) return launch_nt<GWide, false, false, false, true>(a1, b, y, nullptr, nullptr, nullptr, M, K, N, bs, cg, s, nullptr, ap);
+    return launch_nt<GNarrow, false, false, false, true>(a1, b, y, nullptr, nullptr, nullptr, M, K, N, bs, cg, s, nullptr, ap);
+  }
+  if (N % 128 == 0) return launch_nt<GWide, false, false, false, false>(a1, b, y, nullptr, nullptr, nullptr, M, K, N, bs, cg, s, nullptr, ap);
+  return launch_nt<GNarrow, false, false, false, false>(a1, b, y, nullptr, nullptr, nullptr, M, K, N, bs, cg, s, nullptr, ap);
 }
 
 // APPLY: y[M,N] = relu(ab[0] * (a b^T) + ab[1] + r) with r = res (rab null) or rab[0] res + rab[1], and its

@@ -111,7 +111,21 @@ __device__ __forceinline__ void wait_stages(int later) {
 struct W1Geo {
   int M, Ci, Co, ntiles, tiles_per_split, nsplit, nblk;
   int ilv;  // 1: split k takes stages k, k + nsplit, ... (all workgroups stream neighbouring pixels)
+  // SEG (dy2 != null): the dY operand is the channel concatenation [dY (co1) | dy2 (co2) | CO_B columns of
+  // 1.0]; Co = co1 + co2 + CO_B. The ones block's rows are the column sums of X (ops/conv.py _bwd_alg).
+  const uint16_t* dy2;
+  int co1, co2;
 };
+
+__device__ __attribute__((aligned(256))) uint4 g_wg1_ones[16] = {  // bf16 1.0 page (SEG)
+    {0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u}, {0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u},
+    {0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u}, {0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u},
+    {0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u}, {0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u},
+    {0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u}, {0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u},
+    {0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u}, {0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u},
+    {0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u}, {0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u},
+    {0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u}, {0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u},
+    {0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u}, {0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u}};
 
 template <class Cf>
 __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv1x1_wgrad_kernel(const uint16_t* __restrict__ X,
@@ -130,13 +144,22 @@ __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv1x1_wgrad_ker
                       : min(g.ntiles, t_begin + g.tiles_per_split) - t_begin;
   constexpr int kKP = Cf::kKP, kSlots = Cf::kSlots, kAhead = Cf::kAhead;
 
+  // SEG: this workgroup's dY source (uniform): dY, dy2, or the ones page, with its row stride
+  const uint16_t* ysrc = dY;
+  int ldy = g.Co, ycol = co0;
+  bool yones = false;
+  if (g.dy2) {
+    if (co0 < g.co1) { ldy = g.co1; }
+    else if (co0 < g.co1 + g.co2) { ysrc = g.dy2; ldy = g.co2; ycol = co0 - g.co1; }
+    else { yones = true; ldy = 0; ycol = 0; }
+  }
   // per-lane DMA pieces (stage independent): row in the tile and element offset from its first pixel
   int yrow[Cf::kYLd], yoff[Cf::kYLd], xrow[Cf::kXLd], xoff[Cf::kXLd];
 #pragma unroll
   for (int i = 0; i < Cf::kYLd; ++i) {
     const int o = (wid * Cf::kYLd + i) * 1024 + lane * 16, row = o / RY, slot = (o % RY) >> 4;
     yrow[i] = row;
-    yoff[i] = row * g.Co + co0 + swz<RY>(row, slot) * 8;
+    yoff[i] = row * ldy + ycol + swz<RY>(row, slot) * 8;
   }
 #pragma unroll
   for (int i = 0; i < Cf::kXLd; ++i) {
@@ -147,11 +170,12 @@ __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv1x1_wgrad_ker
   auto issue = [&](int s) {
     char* slot = lds + (s % kSlots) * Cf::kSlot;
     const int p0 = (t_begin + s * t_step) * kKP;
-    const uint16_t* yb = dY + (int64_t)p0 * g.Co;
+    const uint16_t* yb = ysrc + (int64_t)p0 * ldy;
     const uint16_t* xb = X + (int64_t)p0 * g.Ci;
 #pragma unroll
     for (int i = 0; i < Cf::kYLd; ++i) {
-      const void* src = p0 + yrow[i] < g.M ? (const void*)(yb + yoff[i]) : (const void*)g_wg1_zero;
+      const void* src = p0 + yrow[i] < g.M ? (yones ? (const void*)g_wg1_ones : (const void*)(yb + yoff[i]))
+                                           : (const void*)g_wg1_zero;
       dma16(src, slot + (wid * Cf::kYLd + i) * 1024);
     }
 #pragma unroll
@@ -237,8 +261,9 @@ __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv1x1_wgrad_ker
 // fixed-order pass over the 16 group sums: deterministic, and 16x the parallelism of one thread per
 // column (whose serial 192-deep loads ran 49 us for a 64 KB result).
 constexpr int kRedCols = 16, kRedGroups = 16;
+template <bool F32>
 __global__ __launch_bounds__(256) void conv1x1_wgrad_reduce_kernel(const float* __restrict__ ws,
-                                                                   uint16_t* __restrict__ dw, int nsplit, int64_t n4) {
+                                                                   void* __restrict__ dw, int nsplit, int64_t n4) {
   __shared__ float4 part[kRedGroups][kRedCols];
   const int col = threadIdx.x % kRedCols, grp = threadIdx.x / kRedCols;
   const int64_t i = (int64_t)blockIdx.x * kRedCols + col;
@@ -257,15 +282,19 @@ __global__ __launch_bounds__(256) void conv1x1_wgrad_reduce_kernel(const float* 
       const float4 v = part[k][col];
       t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
     }
-    const uint32_t lo = (uint32_t)f2bf(t.x) | ((uint32_t)f2bf(t.y) << 16);
-    const uint32_t hi = (uint32_t)f2bf(t.z) | ((uint32_t)f2bf(t.w) << 16);
-    reinterpret_cast<uint2*>(dw)[i] = make_uint2(lo, hi);
+    if constexpr (F32) {
+      reinterpret_cast<float4*>(dw)[i] = t;
+    } else {
+      const uint32_t lo = (uint32_t)f2bf(t.x) | ((uint32_t)f2bf(t.y) << 16);
+      const uint32_t hi = (uint32_t)f2bf(t.z) | ((uint32_t)f2bf(t.w) << 16);
+      reinterpret_cast<uint2*>(dw)[i] = make_uint2(lo, hi);
+    }
   }
 }
 
 // Channel-block configurations (the block covers all of dW for ResNet-50's layer-1 shapes) x
 // pipeline variants (pixels per stage, ring depth; the ring is clamped to the 160 KB of LDS)
-enum class Blk { k64x64, k256x64, k64x256, k128x256 };
+enum class Blk { k64x64, k256x64, k64x256, k128x256, k128x128 };
 constexpr int kVariants = 4;
 constexpr int kVarKP[kVariants] = {32, 32, 64, 64};
 constexpr int kVarSlots[kVariants] = {4, 8, 4, 3};
@@ -280,6 +309,8 @@ template <int V>
 struct CfgOf<Blk::k64x256, V> { using T = W1Cfg<64, 256, 64, 64, kVarKP[V], kVarSlots[V]>; };   // 4 waves
 template <int V>
 struct CfgOf<Blk::k128x256, V> { using T = W1Cfg<128, 256, 64, 64, kVarKP[V], kVarSlots[V]>; }; // 8 waves
+template <int V>
+struct CfgOf<Blk::k128x128, V> { using T = W1Cfg<128, 128, 64, 64, kVarKP[V], kVarSlots[V]>; }; // 4 waves (SEG)
 
 inline Blk pick_block(int Co, int Ci) {
   if (Co % 128 == 0 && Ci % 256 == 0) return Blk::k128x256;
@@ -304,6 +335,7 @@ CfgInfo info_var(int v) {
 }
 inline CfgInfo info(Blk b, int v) {
   switch (b) {
+    case Blk::k128x128: return info_var<Blk::k128x128>(v);
     case Blk::k128x256: return info_var<Blk::k128x256>(v);
     case Blk::k256x64: return info_var<Blk::k256x64>(v);
     case Blk::k64x256: return info_var<Blk::k64x256>(v);
@@ -328,9 +360,22 @@ int g_ilv = -1;        // -1: by shape; 0 / 1 forced
 inline int variant_default(Blk b) { return b == Blk::k64x64 ? 2 : 0; }
 inline int wgs_default(const CfgInfo&, int nblk) { return nblk == 1 ? 192 : 256; }
 
-inline bool geo_of(int M, int Ci, int Co, W1Geo& g) {
+// SEG: a block whose CO_B divides both concatenated segments
+inline Blk pick_block_seg(int co1, int co2, int Ci) {
+  if (Ci % 256 == 0 && co1 % 128 == 0 && co2 % 128 == 0) return Blk::k128x256;
+  if (Ci % 128 == 0 && co1 % 128 == 0 && co2 % 128 == 0) return Blk::k128x128;
+  if (Ci % 256 == 0) return Blk::k64x256;
+  return Blk::k64x64;
+}
+
+inline bool geo_of(int M, int Ci, int Co, W1Geo& g, int seg_co1 = 0, int seg_co2 = 0) {
   if (M < 1 || Ci % 64 != 0 || Co % 64 != 0) return false;
-  const Blk b = pick_block(Co, Ci);
+  const Blk b = seg_co1 ? pick_block_seg(seg_co1, seg_co2, Ci) : pick_block(Co, Ci);
+  if (seg_co1) {  // Co = co1 + co2 + CO_B (the ones block)
+    const CfgInfo i0 = info(b, 0);
+    Co = seg_co1 + seg_co2 + i0.cob;
+  }
+  g.dy2 = nullptr; g.co1 = seg_co1; g.co2 = seg_co2;
   const CfgInfo ci = info(b, g_variant >= 0 ? g_variant : variant_default(b));
   g.M = M; g.Ci = Ci; g.Co = Co;
   g.ntiles = (M + ci.kp - 1) / ci.kp;
@@ -345,8 +390,8 @@ inline bool geo_of(int M, int Ci, int Co, W1Geo& g) {
   return true;
 }
 
-template <class Cf>
-int launch(const uint16_t* x, const uint16_t* dy, uint16_t* dw, float* ws, const W1Geo& g, hipStream_t s) {
+template <class Cf, bool F32 = false>
+int launch(const uint16_t* x, const uint16_t* dy, void* dw, float* ws, const W1Geo& g, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(&conv1x1_wgrad_kernel<Cf>),
@@ -356,18 +401,18 @@ int launch(const uint16_t* x, const uint16_t* dy, uint16_t* dw, float* ws, const
   }
   hipLaunchKernelGGL(conv1x1_wgrad_kernel<Cf>, dim3(g.nsplit * g.nblk), dim3(Cf::kThreads), Cf::kLds, s, x, dy, ws, g);
   const int64_t n4 = (int64_t)g.Co * g.Ci / 4;
-  hipLaunchKernelGGL(conv1x1_wgrad_reduce_kernel, dim3((unsigned)((n4 + kRedCols - 1) / kRedCols)),
+  hipLaunchKernelGGL(conv1x1_wgrad_reduce_kernel<F32>, dim3((unsigned)((n4 + kRedCols - 1) / kRedCols)),
                      dim3(kRedCols * kRedGroups), 0, s, ws, dw, g.nsplit, n4);
   return 0;
 }
 
-template <Blk B>
-int launch_var(int v, const uint16_t* x, const uint16_t* dy, uint16_t* dw, float* ws, const W1Geo& g, hipStream_t s) {
+template <Blk B, bool F32 = false>
+int launch_var(int v, const uint16_t* x, const uint16_t* dy, void* dw, float* ws, const W1Geo& g, hipStream_t s) {
   switch (v) {
-    case 1: return launch<typename CfgOf<B, 1>::T>(x, dy, dw, ws, g, s);
-    case 2: return launch<typename CfgOf<B, 2>::T>(x, dy, dw, ws, g, s);
-    case 3: return launch<typename CfgOf<B, 3>::T>(x, dy, dw, ws, g, s);
-    default: return launch<typename CfgOf<B, 0>::T>(x, dy, dw, ws, g, s);
+    case 1: return launch<typename CfgOf<B, 1>::T, F32>(x, dy, dw, ws, g, s);
+    case 2: return launch<typename CfgOf<B, 2>::T, F32>(x, dy, dw, ws, g, s);
+    case 3: return launch<typename CfgOf<B, 3>::T, F32>(x, dy, dw, ws, g, s);
+    default: return launch<typename CfgOf<B, 0>::T, F32>(x, dy, dw, ws, g, s);
   }
 }
 
@@ -403,6 +448,32 @@ int pdt_conv1x1_wgrad(const uint16_t* x, const uint16_t* dy, uint16_t* dw, float
 
 // Tuning hook (tools/conv1x1_wgrad_bench.py): target workgroups (0 = by shape) and pipeline
 // variant (-1 = by shape; 0..3 = kVarKP / kVarSlots), each left alone when < -1.
+// SEG: out[co1 + co2 + cob, Ci] fp32 = [dy1 | dy2 | 1]^T x over M pixels (dy1 [M, co1], dy2 [M, co2], x [M, Ci]
+// row-major bf16); rows co1 + co2 .. are the column sums of x. ws: pdt_conv1x1_wgrad_seg_ws_floats() floats;
+// *rows_out = co1 + co2 + cob. Fixed-order split reduction (deterministic).
+int64_t pdt_conv1x1_wgrad_seg_ws_floats(int M, int Ci, int co1, int co2, int* rows_out) {
+  W1Geo g;
+  if (co1 < 64 || co2 < 64 || !geo_of(M, Ci, co1 + co2 + 64, g, co1, co2)) return 0;
+  if (rows_out) *rows_out = g.Co;
+  return (int64_t)g.nsplit * g.Co * Ci;
+}
+
+int pdt_conv1x1_wgrad_seg(const uint16_t* x, const uint16_t* dy1, int co1, const uint16_t* dy2, int co2, float* out,
+                          float* ws, int M, int Ci, hipStream_t s) {
+  if ((int64_t)M * (Ci > co1 ? (Ci > co2 ? Ci : co2) : (co1 > co2 ? co1 : co2)) >= ((int64_t)1 << 31)) return -2;
+  W1Geo g;
+  if (co1 < 64 || co2 < 64 || !dy2 || !geo_of(M, Ci, co1 + co2 + 64, g, co1, co2)) return -1;
+  g.dy2 = dy2;
+  const Blk b = pick_block_seg(co1, co2, Ci);
+  const int v = g_variant >= 0 ? g_variant : variant_default(b);
+  switch (b) {
+    case Blk::k128x256: return launch_var<Blk::k128x256, true>(v, x, dy1, out, ws, g, s);
+    case Blk::k128x128: return launch_var<Blk::k128x128, true>(v, x, dy1, out, ws, g, s);
+    case Blk::k64x256: return launch_var<Blk::k64x256, true>(v, x, dy1, out, ws, g, s);
+    default: return launch_var<Blk::k64x64, true>(v, x, dy1, out, ws, g, s);
+  }
+}
+
 void pdt_conv1x1_wgrad_tune(int target_wgs, int variant, int interleave) {
   if (target_wgs >= 0) g_target_wgs = target_wgs;
   if (variant >= -1 && variant < kVariants) g_variant = variant;

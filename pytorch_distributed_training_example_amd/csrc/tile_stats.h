@@ -167,6 +167,20 @@ __device__ __forceinline__ void bn_bwd_accum8(uint4 v, uint4 xb, unsigned mk, co
   }
 }
 
+// The 8 bf16 values of v with the lanes whose ReLU bit is clear set to +0: a BSTATS epilogue stores the
+// gradient at a BatchNorm + ReLU output already masked (every consumer multiplies by that mask anyway,
+// so the stored values are bit-identical in effect, and the ALG backward of conv3 + bn3 needs g = dy m
+// as a plain GEMM operand: ops/conv.py _bwd_alg).
+__device__ __forceinline__ uint4 mask8(uint4 v, unsigned mk) {
+  uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t lo = (mk >> (2 * k)) & 1u ? 0x0000ffffu : 0u, hi = (mk >> (2 * k + 1)) & 1u ? 0xffff0000u : 0u;
+    w[k] &= lo | hi;
+  }
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
 // Block-wide sum of every thread's (s1, s2) for its chunk (tid % CHUNKS; CHUNKS = BN/8 divides 64)
 // and the tile's partials store. `red`: WAVES * 2 * BN floats of LDS no one reads any more
 // (contains __syncthreads: every thread of the block must call it).

@@ -134,10 +134,13 @@ class Bottleneck(nn.Module):
             z2 = self.conv2(out)  # same shape / layout as bn2's output: decides conv3's paths
             ds_bn = self.downsample[1] if self.downsample is not None else None
             # conv3 + bn3 backward as one kernel: bn3 hands its input gradient to conv3 in deferred form
-            blink = BNGradLink() if (self.conv3.fused_bwd_ok(z2) and not self.bn3.has_hooks()
+            # (or the ALG backward for the shapes the fused kernel does not take: ops/conv.py _bwd_alg)
+            fused3 = self.conv3.fused_bwd_ok(z2)
+            blink = BNGradLink(needs_masked=not fused3) if ((fused3 or self.conv3.alg_bwd_ok(z2)) and not self.bn3.has_hooks()
                                      and (link.lazy or (isinstance(ds_bn, BatchNorm2d) and DS_MASKED_GRAD[0]))) \
                 else None
-            if blink is not None and SW.bn2_defer and isinstance(self.bn2, BatchNorm2d) and not self.bn2.has_hooks():
+            if (blink is not None and fused3 and SW.bn2_defer and isinstance(self.bn2, BatchNorm2d)
+                    and not self.bn2.has_hooks()):
                 # bn2 -> conv3: statistics only here; conv3's GEMM reads relu(a z2 + b) on load and its fused
                 # backward recomputes that operand (ops/batchnorm.py DeferredReLUBN): bn2's output never exists
                 out = self.bn2._forward_deferred_relu(z2)
@@ -274,7 +277,7 @@ class _GlobalAvgPoolFn(torch.autograd.Function):
             r = native().gap_bwd(gy.contiguous(), h, w, gs.x if gs else None, gs.mask if gs else None,
                                  gs.mean if gs else None)
             if gs is not None and len(r) == 2:
-                gs.deposit(r[1], r[0])  # the last bn3's backward skips its reduce pass
+                gs.deposit(r[1], r[0], masked=gs.mask is not None)  # the last bn3's backward skips its reduce pass
             return r[0], None
         g = (gy * (1.0 / (h * w))).view(n, c, 1, 1).expand(n, c, h, w)
         return g.contiguous(memory_format=torch.channels_last), None

@@ -69,17 +69,20 @@ class GradStatsSource:
     another branch's gradient into it — and otherwise falls back to its own reduce pass.
     ``PDT_BN_BWD_STATS=0`` turns the hand-off off."""
 
-    __slots__ = ("x", "mask", "mean", "out_version", "part", "grad_ptr", "grad_version")
+    __slots__ = ("x", "mask", "mean", "out_version", "part", "grad_ptr", "grad_version", "masked")
 
     def __init__(self):
         self.x = self.mask = self.mean = self.part = None
         self.out_version = self.grad_ptr = self.grad_version = None
+        self.masked = False  # the depositing kernel stored the gradient already multiplied by the ReLU mask
 
     def ready(self) -> bool:
         return self.x is not None and self.part is None
 
-    def deposit(self, part: torch.Tensor, grad: torch.Tensor) -> None:
+    def deposit(self, part: torch.Tensor, grad: torch.Tensor, masked: bool = False) -> None:
+        """``masked``: ``grad`` was stored as dy * relu mask (our 1x1 GEMM's BSTATS epilogue does)."""
         self.part, self.grad_ptr, self.grad_version = part, grad.data_ptr(), grad._version
+        self.masked = bool(masked)
 
     def take(self, dy: torch.Tensor):
         part, self.part = self.part, None
@@ -122,10 +125,13 @@ class DeferredBNGrad:
     backward (csrc/kernels/conv1x1_bwd_fused.hip) forms dx while loading it, so the BatchNorm's apply
     pass — a read of (dy, x, mask) and a write of dx, then two re-reads of dx — never runs."""
 
-    __slots__ = ("dy", "x", "mask", "mean", "coef")
+    __slots__ = ("dy", "x", "mask", "mean", "coef", "dy_masked")
 
-    def __init__(self, dy, x, mask, mean, coef):
+    def __init__(self, dy, x, mask, mean, coef, dy_masked: bool = False):
         self.dy, self.x, self.mask, self.mean, self.coef = dy, x, mask, mean, coef
+        # dy_masked: dy already equals dy * m (no mask, or the producing kernel stored it masked): the ALG
+        # backward (ops/conv.py _bwd_alg) then uses dy directly as the GEMM operand g
+        self.dy_masked = dy_masked
 
     def materialize(self) -> torch.Tensor:
         """dx as a tensor (fallback when the consumer cannot take the deferred form)."""
@@ -144,10 +150,13 @@ class BNGradLink:
     as its input gradient) to the backward of the conv that produced the BatchNorm's input (which
     runs next, with its output gradient None: ``set_materialize_grads(False)``)."""
 
-    __slots__ = ("grad",)
+    __slots__ = ("grad", "needs_masked")
 
-    def __init__(self):
+    def __init__(self, needs_masked: bool = False):
         self.grad = None
+        # needs_masked: the receiving conv takes the deferred form only with dy already masked (the ALG backward,
+        # ops/conv.py _bwd_alg); otherwise the BatchNorm's backward runs its own apply and returns dx to autograd
+        self.needs_masked = needs_masked
 
     def take(self):
         g, self.grad = self.grad, None
@@ -248,11 +257,13 @@ class _BNTrainFn(torch.autograd.Function):
                 return native().bn_bwd_train_tiles(dy, x, part, mask, weight, mean, invstd, relu, has_res, need_w)
             return native().bn_bwd_train(dy, x, mask, weight, mean, invstd, relu, has_res, need_w)
 
-        if ctx.out_link is not None and (not ctx.relu or mask is not None):
+        dy_masked = not ctx.relu or (part is not None and ctx.gsrc.masked)
+        if (ctx.out_link is not None and (not ctx.relu or mask is not None)
+                and (dy_masked or not ctx.out_link.needs_masked)):
             # coefficients only: the producing conv's fused backward forms dx = A dy m + B (x - mean) + D
             coef, dg, db = native().bn_bwd_coef(dy, x, part, mask if ctx.relu else None, weight, mean, invstd,
                                                 ctx.relu, need_w)
-            ctx.out_link.grad = DeferredBNGrad(dy, x, mask if ctx.relu else None, mean, coef)
+            ctx.out_link.grad = DeferredBNGrad(dy, x, mask if ctx.relu else None, mean, coef, dy_masked)
             if ctx.has_res:  # lazy link (checked in forward): the shortcut gets (dy, mask) as before
                 ctx.link.grad = MaskedGrad(dy, mask) if ctx.relu else dy
             return (None, None, dg if need_w else None, db if need_w else None) + tail

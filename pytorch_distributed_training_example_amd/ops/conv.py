@@ -369,6 +369,8 @@ class _Conv1x1Fn(torch.autograd.Function):
             if d is None:
                 return (None, None) + none7
             r = _bwd_fused(ctx, d, x, weight)
+            if r is None:
+                r = _bwd_alg(ctx, d, x, weight)
             if r is not None:
                 return (r[0], r[1]) + none7
             gy = d.materialize()
@@ -414,7 +416,7 @@ class _Conv1x1Fn(torch.autograd.Function):
             gpart = native().conv1x1_gemm(g2, _wt_of(weight, w2), _nhwc2d(dx), True, False, strided.t,
                                           bn_x=gs.x, bn_mask=gs.mask, bn_mean=gs.mean, c_stride=strided.s, c_H=H,
                                           c_W=W)
-            gs.deposit(gpart, dx)
+            gs.deposit(gpart, dx, masked=gs.mask is not None)
             strided = None
             return dx, _Conv1x1Fn._wgrad(ctx, g2, x2, x, gy, weight, M, Ci, Co, fork)
         # dx is final (nothing is added to it after the GEMM) unless this is the first of two linked
@@ -469,7 +471,7 @@ class _Conv1x1Fn(torch.autograd.Function):
         if strided is not None and dx is not None:
             strided.add_into(dx)
         if gpart is not None and dx is not None:
-            gs.deposit(gpart, dx)
+            gs.deposit(gpart, dx, masked=gs.mask is not None)  # conv1x1.hip stores BSTATS outputs masked
         if first and dx is not None:  # first of the two branches: leave dx for the partner to add to
             ctx.link.grad, dx = dx, None
         return dx, _Conv1x1Fn._wgrad(ctx, g2, x2, x, gy, weight, M, Ci, Co, fork)
@@ -536,6 +538,51 @@ def _bwd_fused(ctx, d, x, weight):
     if linked:
         ctx.link.grad, dx = dx, None
     return dx, dw
+
+
+def alg_bwd_shape_ok(weight: torch.Tensor) -> bool:
+    """(Co, Ci) of a bottleneck conv3 whose backward ``_bwd_alg`` takes: Co (bn3's channels) and Ci multiples of
+    128 (the segment blocks of conv1x1_wgrad.hip / the GEMM's 128-wide tiles), bf16 1x1 weights."""
+    return (weight.dim() == 4 and tuple(weight.shape[2:]) == (1, 1) and weight.dtype == torch.bfloat16
+            and weight.shape[0] % 128 == 0 and weight.shape[1] % 128 == 0 and weight.shape[0] > weight.shape[1])
+
+
+def _bwd_alg(ctx, d, x, weight):
+    """conv3 + bn3 backward of a bottleneck WITHOUT bn3's apply pass (csrc/kernels/bn_alg.hip header): with
+    z = a W^T (this conv's forward) substituted into bn3's backward dz = A g + B (z - mean) + D,
+
+        dW = diag(A) P + diag(B) W Gram + E (x) S,    da = [g | a | a | 1] [diag(A) W | G_hi | G_lo | c]^T
+
+    where P = g^T a, Gram = a^T a, S = sum(a) come from ONE weight-gradient pass over (g, a)
+    (conv1x1_wgrad_seg), G = W^T diag(B) W, c = E W, E = D - B mean. The data-gradient GEMM
+    (conv1x1_gemm_seg) also takes bn2's backward reduction in its epilogue. Neither dz nor z is read: per
+    block the 4C-channel tensor is read twice (g) instead of five times (dy, z, dz x 2 + the apply's write).
+    Needs g = dy * mask as a plain tensor (``d.dy_masked``: the producer stored it masked). None when the
+    path does not apply (the caller materialises dz)."""
+    if not (SW.bwd_alg and ctx.link is None and ctx.dre is None and ctx.needs_input_grad[0]
+            and ctx.needs_input_grad[1] and d.dy_masked and alg_bwd_shape_ok(weight)
+            and x.dtype == torch.bfloat16 and x.is_contiguous(memory_format=torch.channels_last)):
+        return None
+    from ._native import native
+    C4, CW = weight.shape[0], weight.shape[1]
+    g2 = _nhwc2d(d.dy.contiguous(memory_format=torch.channels_last))  # [M, C4] gradient at bn3's output, masked
+    a2 = _nhwc2d(x)  # [M, CW] this conv's input (bn2's output)
+    wg = native().conv1x1_wgrad_seg(a2, g2, a2)  # [C4 + CW + ones, CW] fp32: P, Gram, column sums of a
+    if wg is None:
+        return None
+    w2 = weight.reshape(C4, CW).contiguous()
+    w2f = w2.float()
+    bw = w2f * d.coef[1].unsqueeze(1)       # diag(B) W
+    G = (w2f.t() @ bw).contiguous()         # W^T diag(B) W   [CW, CW]
+    bwg = (bw @ wg[C4:C4 + CW]).contiguous()  # diag(B) W Gram  [C4, CW]
+    bcat, dw2 = native().bn_alg_assemble(w2, d.coef.contiguous(), d.mean.contiguous(), G, wg, bwg)
+    gs = ctx.gsrc if (ctx.gsrc is not None and ctx.gsrc.ready()) else None
+    dx = torch.empty_like(x, memory_format=torch.channels_last)
+    part = native().conv1x1_gemm_seg(g2, a2, 2, bcat, _nhwc2d(dx), bn_x=gs.x if gs else None,
+                                     bn_mask=gs.mask if gs else None, bn_mean=gs.mean if gs else None)
+    if gs is not None and part is not None:
+        gs.deposit(part, dx, masked=gs.mask is not None)
+    return dx, dw2.as_strided(weight.shape, weight.stride())
 
 
 def fused_bwd_shape_ok(weight: torch.Tensor) -> bool:
@@ -1014,6 +1061,13 @@ class Conv1x1(nn.Conv2d):
             return y
         assert res_link is None and bwd_link is None, "res_link / bwd_link need a GEMM path"
         return super().forward(x)
+
+    def alg_bwd_ok(self, x: torch.Tensor) -> bool:
+        """This conv's backward can take its consuming BatchNorm's input gradient in deferred form and run the
+        ALG backward (``_bwd_alg``; ``PDT_BWD_ALG=0`` turns it off)."""
+        return (SW.bwd_alg and self.training and torch.is_grad_enabled() and x.dtype == torch.bfloat16
+                and self.gemm_eligible(x) and alg_bwd_shape_ok(self.weight) and not _has_hooks(self)
+                and not self._backward_hooks and not self._backward_pre_hooks)
 
     def fused_bwd_ok(self, x: torch.Tensor) -> bool:
         """This conv's backward can take its consuming BatchNorm's input gradient in deferred form

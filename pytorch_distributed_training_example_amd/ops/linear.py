@@ -86,6 +86,13 @@ class _LinearFn(torch.autograd.Function):
 
 
 def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    if x.is_cuda and torch.is_autocast_enabled("cuda"):
+        # autocast does not reach into an autograd.Function: cast the operands the way autocast casts
+        # F.linear's, then run (and later backpropagate) the Function with autocast off, so its saved
+        # tensors and the incoming gradient share one dtype (amp_bf16: our bf16 path; amp_fp16: aten)
+        dt = torch.get_autocast_dtype("cuda")
+        with torch.autocast("cuda", enabled=False):
+            return linear(x.to(dt), weight.to(dt), bias.to(dt) if bias is not None else None)
     if (use_native(x) and x.dtype in (torch.float32, torch.bfloat16) and weight.dtype == x.dtype
             and (bias is None or bias.dtype == x.dtype) and weight.shape[0] % 8 == 0):
         return _LinearFn.apply(x, weight, bias)

@@ -60,6 +60,7 @@ def test_grad_scaler_matches_torch_over_scripted_sequence():
             p.grad = g * s
         for p, g in zip(ref_p, gs):
             p.grad = g * s
+        ref.scale(torch.ones((), device="cuda"))  # torch's scaler creates its scale tensor lazily in scale()
         ours.step(opt_o)
         ours.update()
         ref.step(opt_r)

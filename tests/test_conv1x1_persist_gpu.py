@@ -113,7 +113,9 @@ def test_dgrad_masked_acc_bstats_persistent_equals_per_tile(M, K, N):
     rows = _rows(M)
     bits = torch.arange(8, device="cuda")
     mexp = ((cmask.view(M, N // 8)[rows].long()[..., None] >> bits) & 1).view(len(rows), N).float()
-    ref = _oracle_rows(a, b, rows) + dres[rows].float() * mexp
+    bexp = ((bmask.view(M, N // 8)[rows].long()[..., None] >> bits) & 1).view(len(rows), N).float()
+    # stored masked by the BatchNorm's ReLU bits (BSTATS, tile_stats.h mask8)
+    ref = (_oracle_rows(a, b, rows) + dres[rows].float() * mexp) * bexp
     torch.testing.assert_close(r[1][0][rows].float(), ref, rtol=2e-2, atol=3e-2)
 
 
