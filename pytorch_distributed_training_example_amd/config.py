@@ -44,7 +44,8 @@ PDT_BWD_FUSED_SHAPES        256x64       (Co x Ci) of the conv3s that take the f
                                          profiles/r5/ab_layer2_unfused.txt)
 PDT_BWD_ALG                 1            bottleneck conv3 + bn3 backward (the shapes PDT_BWD_FUSED does not take) without
                                          bn3's apply pass: z = a W^T substituted into bn3's backward (ops/conv.py
-                                         _bwd_alg, csrc/kernels/bn_alg.hip): one wgrad pass + one data-gradient GEMM
+                                         _bwd_alg, csrc/kernels/bn_alg.hip): one wgrad pass + one data-gradient GEMM;
+                                         2: also bn3's backward reduction without reading z (sum-only producer)
 PDT_BN2_DEFER               0            1: with PDT_BWD_FUSED, bn2's apply + ReLU deferred into conv3 (read on load
                                          in the forward GEMM, recomputed in the fused backward, which writes bn2's
                                          mask). Measured -0.2 %, and -2 % with PDT_BN_APPLY_GEMM_K (the relu(a x + b)
@@ -55,8 +56,9 @@ PDT_BN_APPLY_GEMM_K         64           a BatchNorm(+residual)+ReLU apply after
                                          256-channel GEMM tiles: 128 (layers 1-2) +0.7 % over off; 64 (layer 1
                                          only) +0.2 % over 128 in two same-box A/Bs; 256 (adds layer 3) -0.6 %
                                          (profiles/r4/ab_bn_apply_gemm.md)
-PDT_LINEAR_EPILOGUE         0            1: Linear forward GEMMs (+bias, MLP fc1+bias+GELU) on our MFMA kernel
-                                         (gemm.hip; 0.61-0.94x of tuned hipBLASLt, so off)
+PDT_LINEAR_EPILOGUE         auto         Linear forward GEMMs (+bias, MLP fc1+bias+GELU) on our MFMA kernel (gemm.hip)
+                                         per shape by measurement (tuning/linear_gfx950.json, else timed once);
+                                         1 / 0: forced on / off
 PDT_FP8_FUSED_GELU          1            fp8 MLPs: bias+GELU (and its backward) emit e4m3 + transpose directly
                                          (fp8.hip fp8_gelu_cast_kernel): no bf16 activation, no cast pass
 PDT_FP8_WEIGHT_MULTI        1            fp8: every Linear weight cast in one launch per forward (fp8_cast_multi)
@@ -118,11 +120,14 @@ class _Switches:
         self.linear_splitk = on("PDT_LINEAR_SPLITK")
         self.fused_addln = on("PDT_FUSED_ADDLN")
         self.embedding_native = on("PDT_EMBEDDING_NATIVE")
-        self.linear_epilogue = e("PDT_LINEAR_EPILOGUE", "0") == "1"
+        # "auto": per-shape measured choice between our GEMM and hipBLASLt (ops/linear.py _ours); "1" / "0": forced
+        self.linear_epilogue = e("PDT_LINEAR_EPILOGUE", "auto")
         self.bwd_fused = on("PDT_BWD_FUSED")
         self.bwd_fused_shapes = tuple(tuple(int(v) for v in t.split("x")) for t in
                                       e("PDT_BWD_FUSED_SHAPES", "256x64").split(",") if "x" in t)
-        self.bwd_alg = on("PDT_BWD_ALG")
+        # 0 off; 1: ALG backward; 2: also the producer of bn3's gradient skips reading bn3's input for the backward
+        # reduction (sum-only epilogue) and the ALG pass completes it (ops/batchnorm.py _BNTrainFn.backward)
+        self.bwd_alg = int(e("PDT_BWD_ALG", "1"))
         self.bn2_defer = on("PDT_BN2_DEFER", "0")
         self.bn_apply_gemm_k = int(e("PDT_BN_APPLY_GEMM_K", "64"))
         self.strided_bstats = on("PDT_STRIDED_BSTATS")

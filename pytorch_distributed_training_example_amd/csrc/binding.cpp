@@ -145,6 +145,7 @@ int pdt_conv1x1_wgrad_seg(const uint16_t* x, const uint16_t* dy1, int co1, const
 int pdt_conv1x1_gemm_seg(const uint16_t* a1, int k1, const uint16_t* a2, int k2, int rep2, const uint16_t* b,
                          uint16_t* y, int M, int N, const uint16_t* bn_x, const uint8_t* bn_mask, const float* bn_mean,
                          float* bn_part, hipStream_t s);
+int pdt_bn_alg_fix_s2(float* part, int T, const float* wg, const uint16_t* W, int C4, int CW, hipStream_t s);
 int pdt_bn_alg_assemble(const uint16_t* W, const float* coef, const float* mean, const float* G, const float* wg,
                         const float* BWG, uint16_t* bcat, uint16_t* dW, int C4, int CW, hipStream_t s);
 int pdt_conv1x1_wgrad(const uint16_t* x, const uint16_t* dy, uint16_t* dw, float* ws, int M, int Ci, int Co,
@@ -545,27 +546,29 @@ std::vector<Tensor> bn_relu_maxpool_fwd_parts(Tensor x, Tensor part, c10::option
 // bn_mean (the pooled tensor is a BatchNorm(+ReLU) output): also that BatchNorm's backward partials [2, T, C]
 // (the input of bn_bwd_train_tiles); {dy} alone when the reduction does not apply to C.
 std::vector<Tensor> gap_bwd(Tensor g, int64_t H, int64_t W, c10::optional<Tensor> bn_x, c10::optional<Tensor> bn_mask,
-                            c10::optional<Tensor> bn_mean) {
+                            c10::optional<Tensor> bn_mean, bool bn_sum_only) {
   check_cuda(g, "g");
   TORCH_CHECK(g.dim() == 2 && g.scalar_type() == at::kBFloat16 && g.is_contiguous() && g.size(1) % 8 == 0,
               "gap_bwd: g [N, C] contiguous bf16, C % 8 == 0");
   const int64_t N = g.size(0), C = g.size(1), M = N * H * W;
   auto dy = at::empty({N, C, H, W}, g.options().memory_format(at::MemoryFormat::ChannelsLast));
-  const bool red = bn_x.has_value() && bn_x->defined() && pdt_gap_bwd_parts(M, (int)C) > 0;
+  const bool red = ((bn_x.has_value() && bn_x->defined()) || bn_sum_only) && pdt_gap_bwd_parts(M, (int)C) > 0;
   Tensor part;
   const uint16_t* xp = nullptr;
   const uint8_t* mp = nullptr;
   const float* mu = nullptr;
   if (red) {
-    check_nhwc_bf16(*bn_x, "bn_x");
-    TORCH_CHECK(bn_x->sizes() == dy.sizes(), "gap_bwd: bn_x must be [N, C, H, W]");
+    if (!bn_sum_only) {
+      check_nhwc_bf16(*bn_x, "bn_x");
+      TORCH_CHECK(bn_x->sizes() == dy.sizes(), "gap_bwd: bn_x must be [N, C, H, W]");
+      xp = reinterpret_cast<const uint16_t*>(bn_x->data_ptr());
+    }
     TORCH_CHECK(bn_mean.has_value() && bn_mean->defined() && bn_mean->scalar_type() == at::kFloat &&
                     bn_mean->numel() == C && bn_mean->is_cuda(), "gap_bwd: bn_mean fp32 [C]");
     if (bn_mask.has_value() && bn_mask->defined()) {
       TORCH_CHECK(bn_mask->scalar_type() == at::kByte && bn_mask->numel() == M * C / 8, "gap_bwd: bn_mask uint8 [M C / 8]");
       mp = bn_mask->data_ptr<uint8_t>();
     }
-    xp = reinterpret_cast<const uint16_t*>(bn_x->data_ptr());
     mu = bn_mean->data_ptr<float>();
     part = at::empty({2, pdt_gap_bwd_parts(M, (int)C), C}, g.options().dtype(at::kFloat));
   }
@@ -943,7 +946,7 @@ c10::optional<Tensor> conv1x1_gemm(Tensor a, Tensor b, Tensor out, bool acc, boo
                                    c10::optional<Tensor> c_in, c10::optional<Tensor> c_mask,
                                    c10::optional<Tensor> bn_x, c10::optional<Tensor> bn_mask,
                                    c10::optional<Tensor> bn_mean, int64_t c_stride, int64_t c_H, int64_t c_W,
-                                   c10::optional<Tensor> a_coef) {
+                                   c10::optional<Tensor> a_coef, bool bn_sum_only) {
   for (const Tensor* t : {&a, &b, &out}) {
     check_cuda(*t, "conv1x1_gemm operand");
     TORCH_CHECK(t->scalar_type() == at::kBFloat16 && t->dim() == 2 && t->is_contiguous(),
@@ -977,16 +980,20 @@ c10::optional<Tensor> conv1x1_gemm(Tensor a, Tensor b, Tensor out, bool acc, boo
   c10::optional<Tensor> part;
   const int64_t T = (M + pdt_conv1x1_tile_rows() - 1) / pdt_conv1x1_tile_rows();
   if (stats) part = at::empty({2, T, N}, a.options().dtype(at::kFloat));
-  const bool bstats = bn_x.has_value() && bn_x->defined();
+  // bn_sum_only: the BatchNorm input is not read; only the partials' sum(dz) row is meaningful (ALG backward)
+  const bool bstats = (bn_x.has_value() && bn_x->defined()) || bn_sum_only;
   const uint16_t* bx = nullptr;
   const uint8_t* bm = nullptr;
   const float* bmean = nullptr;
   if (bstats) {
     TORCH_CHECK(!stats, "conv1x1_gemm: stats and bn_x are exclusive");
-    check_cuda(*bn_x, "bn_x");
-    TORCH_CHECK(bn_x->scalar_type() == at::kBFloat16 && bn_x->numel() == M * N && bn_x->is_contiguous(
-                    bn_x->dim() == 4 ? at::MemoryFormat::ChannelsLast : at::MemoryFormat::Contiguous),
-                "conv1x1_gemm: bn_x must be [M, N] bf16 (channels_last when 4-D)");
+    if (!bn_sum_only) {
+      check_cuda(*bn_x, "bn_x");
+      TORCH_CHECK(bn_x->scalar_type() == at::kBFloat16 && bn_x->numel() == M * N && bn_x->is_contiguous(
+                      bn_x->dim() == 4 ? at::MemoryFormat::ChannelsLast : at::MemoryFormat::Contiguous),
+                  "conv1x1_gemm: bn_x must be [M, N] bf16 (channels_last when 4-D)");
+      bx = reinterpret_cast<const uint16_t*>(bn_x->data_ptr());
+    }
     TORCH_CHECK(bn_mean.has_value() && bn_mean->defined() && bn_mean->scalar_type() == at::kFloat &&
                 bn_mean->numel() == N && bn_mean->is_contiguous() && bn_mean->is_cuda(),
                 "conv1x1_gemm: bn_mean must be fp32 [N]");
@@ -995,7 +1002,6 @@ c10::optional<Tensor> conv1x1_gemm(Tensor a, Tensor b, Tensor out, bool acc, boo
                   "conv1x1_gemm: bn_mask must be uint8 [M * N / 8]");
       bm = bn_mask->data_ptr<uint8_t>();
     }
-    bx = reinterpret_cast<const uint16_t*>(bn_x->data_ptr());
     bmean = bn_mean->data_ptr<float>();
     part = at::empty({2, T, N}, a.options().dtype(at::kFloat));
   }
@@ -1214,6 +1220,22 @@ std::vector<Tensor> bn_alg_assemble(Tensor w, Tensor coef, Tensor mean, Tensor G
                                      reinterpret_cast<uint16_t*>(dW.data_ptr()), (int)C4, (int)CW, stream());
   TORCH_CHECK(rc == 0, "pdt_bn_alg_assemble failed: ", rc);
   return {bcat, dW};
+}
+
+// Completes a sum-only producer's BatchNorm backward partials in place (csrc/kernels/bn_alg.hip).
+void bn_alg_fix_s2(Tensor part, Tensor wg, Tensor w) {
+  check_cuda(part, "part");
+  check_cuda(wg, "wg");
+  check_cuda(w, "w");
+  TORCH_CHECK(w.dim() == 2 && w.scalar_type() == at::kBFloat16 && w.is_contiguous(), "bn_alg_fix_s2: w [C4, CW] bf16");
+  const int64_t C4 = w.size(0), CW = w.size(1);
+  TORCH_CHECK(part.scalar_type() == at::kFloat && part.is_contiguous() && part.dim() == 3 && part.size(0) == 2 &&
+                  part.size(2) == C4 && wg.scalar_type() == at::kFloat && wg.is_contiguous() && wg.dim() == 2 &&
+                  wg.size(1) == CW && wg.size(0) >= C4,
+              "bn_alg_fix_s2: part [2, T, C4], wg [>= C4, CW] fp32");
+  TORCH_CHECK(pdt_bn_alg_fix_s2(part.data_ptr<float>(), (int)part.size(1), wg.data_ptr<float>(),
+                                reinterpret_cast<const uint16_t*>(w.data_ptr()), (int)C4, (int)CW, stream()) == 0,
+              "pdt_bn_alg_fix_s2 failed");
 }
 
 // BN training forward with the statistics taken from conv1x1_gemm's per-tile partials.
@@ -2269,7 +2291,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv1x1_gemm", &conv1x1_gemm, py::arg("a"), py::arg("b"), py::arg("out"), py::arg("acc"), py::arg("stats"),
         py::arg("c_in") = py::none(), py::arg("c_mask") = py::none(), py::arg("bn_x") = py::none(),
         py::arg("bn_mask") = py::none(), py::arg("bn_mean") = py::none(), py::arg("c_stride") = 0,
-        py::arg("c_H") = 0, py::arg("c_W") = 0, py::arg("a_coef") = py::none());
+        py::arg("c_H") = 0, py::arg("c_W") = 0, py::arg("a_coef") = py::none(), py::arg("bn_sum_only") = false);
   m.def("conv1x1_probe", [](int probe) { pdt_conv1x1_probe(probe); });
   m.def("conv1x1_persist", [](int mode) { return pdt_conv1x1_persist(mode); },
         "1x1 GEMM persistence mode (0 off, 1 measured kinds, 2 all, -1 env default); returns the previous mode");
@@ -2282,7 +2304,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_apply_wgs", [](int n) { pdt_bn_apply_wgs(n); });
   m.def("bn_row_wgs", [](int n) { pdt_bn_row_wgs(n); });
   m.def("gap_bwd", &gap_bwd, py::arg("g"), py::arg("H"), py::arg("W"), py::arg("bn_x") = py::none(),
-        py::arg("bn_mask") = py::none(), py::arg("bn_mean") = py::none());
+        py::arg("bn_mask") = py::none(), py::arg("bn_mean") = py::none(), py::arg("bn_sum_only") = false);
   m.def("conv1x1_gemm_apply", &conv1x1_gemm_apply, py::arg("a"), py::arg("b"), py::arg("res"), py::arg("ab"),
         py::arg("rab") = py::none(), py::arg("a_coef") = py::none());
   m.def("bn_bwd_train_tiles", &bn_bwd_train_tiles);
@@ -2314,6 +2336,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv1x1_gemm_seg", &conv1x1_gemm_seg, py::arg("a1"), py::arg("a2"), py::arg("rep2"), py::arg("b"),
         py::arg("out"), py::arg("bn_x") = py::none(), py::arg("bn_mask") = py::none(), py::arg("bn_mean") = py::none());
   m.def("bn_alg_assemble", &bn_alg_assemble);
+  m.def("bn_alg_fix_s2", &bn_alg_fix_s2);
   m.def("conv1x1_wgrad_tune", [](int target_wgs, int variant, int interleave) { pdt_conv1x1_wgrad_tune(target_wgs, variant, interleave); },
         py::arg("target_wgs"), py::arg("variant") = -2, py::arg("interleave") = -2);
   m.def("embedding_fwd", &embedding_fwd);

@@ -976,7 +976,8 @@ __global__ __launch_bounds__(256) void gap_bwd_kernel(const uint16_t* __restrict
     st.z = (uint32_t)f2bf(v[4] * scale) | ((uint32_t)f2bf(v[5] * scale) << 16);
     st.w = (uint32_t)f2bf(v[6] * scale) | ((uint32_t)f2bf(v[7] * scale) << 16);
     if constexpr (BNRED) {
-      const uint4 xv = *reinterpret_cast<const uint4*>(xb + e * 8);
+      // (xb null: sum-only, the ALG backward derives the centred sum itself; see conv1x1.hip)
+      const uint4 xv = xb ? *reinterpret_cast<const uint4*>(xb + e * 8) : make_uint4(0u, 0u, 0u, 0u);
       const unsigned mk = mask ? mask[e] : 0xffu;
       bn_bwd_accum8(st, xv, mk, mu, s1, s2);
       st = mask8(st, mk);  // stored masked, as the 1x1 GEMM's BSTATS epilogue (tile_stats.h mask8)
@@ -1402,9 +1403,9 @@ int pdt_gap_bwd(const uint16_t* g, int N, int HW, int C, uint16_t* dy, const uin
   const int64_t M = (int64_t)N * HW;
   if (C % 8 != 0 || M < 1) return -1;
   const float scale = (float)(1.0 / (double)HW);
-  if (xb) {
+  if (part) {  // the pooled BatchNorm's backward partials (xb null: sum-only)
     const int T = pdt_gap_bwd_parts(M, C);
-    if (T == 0 || !mean || !part) return -2;
+    if (T == 0 || !mean) return -2;
     hipLaunchKernelGGL(gap_bwd_kernel<true>, dim3(T), dim3(256), 0, s, g, scale, HW, C, M, dy, xb, mask, mean, part);
   } else {
     const int grid = (int)std::min<int64_t>((M * (C / 8) + 255) / 256, 4096);

@@ -65,9 +65,29 @@ __global__ __launch_bounds__(256) void bn_alg_assemble_kernel(const uint16_t* __
   dW[e] = f2bf(A[c] * wg[e] + BWG[e] + E * S);
 }
 
+// Sum-only producer (conv1x1.hip / gap_bwd with the BatchNorm input not read): each tile's centred-sum entry
+// is sum(g (0 - mean)) = -mean sum(g). The true one is sum(g (z - mean)) = sum_k P[c, k] W[c, k] - mean sum(g)
+// (z = a W^T): adding rowsum(P * W) to one tile's entry completes the reduction the finalize sums.
+__global__ __launch_bounds__(256) void bn_alg_fix_s2_kernel(float* __restrict__ part, int T, const float* __restrict__ wg,
+                                                            const uint16_t* __restrict__ W, int C4, int CW) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C4) return;
+  float s = 0.f;
+  for (int k = 0; k < CW; ++k) s += wg[(int64_t)c * CW + k] * bfv(W[(int64_t)c * CW + k]);
+  part[(int64_t)T * C4 + c] += s;  // part[1][0][c]
+}
+
 }  // namespace
 
 extern "C" {
+
+// part [2, T, C4] fp32 (a sum-only producer's BatchNorm backward partials), wg: pdt_conv1x1_wgrad_seg's output
+// (rows 0..C4-1 = P), W [C4, CW] bf16: completes part's centred sums in place (see bn_alg_fix_s2_kernel).
+int pdt_bn_alg_fix_s2(float* part, int T, const float* wg, const uint16_t* W, int C4, int CW, hipStream_t s) {
+  if (T < 1 || C4 < 1 || CW < 1) return -1;
+  hipLaunchKernelGGL(bn_alg_fix_s2_kernel, dim3((C4 + 255) / 256), dim3(256), 0, s, part, T, wg, W, C4, CW);
+  return 0;
+}
 
 // bcat [CW, C4 + 2 CW + 32] bf16, dW [C4, CW] bf16; W [C4, CW] bf16 row-major; coef [3, C4] (A, B, D), mean [C4],
 // G [CW, CW], BWG [C4, CW] fp32; wg: pdt_conv1x1_wgrad_seg's output (rows 0..C4-1 = P, row C4 + CW = S).

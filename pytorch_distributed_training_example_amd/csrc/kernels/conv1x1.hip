@@ -331,6 +331,10 @@ __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv1x1_kernel(
   const int64_t cm_scale = Cmask ? 1 : 0;
   const uint8_t* const bm_base = bs.mask ? bs.mask : g_mask_ones;
   const int64_t bm_scale = bs.mask ? 1 : 0;
+  // BSTATS sum-only (bs.x null): the BatchNorm input is not read (a zero page, stride 0) — only sum(dz) is
+  // meaningful then; the ALG backward derives sum(dz (x - mean)) from its weight-gradient pass (bn_alg.hip)
+  const uint16_t* const bx_base = bs.x ? bs.x : reinterpret_cast<const uint16_t*>(g_gemm_zero);
+  const int64_t bx_scale = bs.x ? 1 : 0;
 #pragma unroll 1
   for (int h = 0; h < kIt; h += kB) {
   uint4 cv[kB], xbv[kB];
@@ -344,7 +348,7 @@ __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv1x1_kernel(
     const int mc = ok ? m : M - 1;
     const int64_t off = (int64_t)mc * N + n0 + c * 8;
     if constexpr (BSTATS) {
-      xbv[it] = *reinterpret_cast<const uint4*>(bs.x + off);
+      xbv[it] = *reinterpret_cast<const uint4*>(bx_base + off * bx_scale);
       const unsigned b = bm_base[(off >> 3) * bm_scale];
       bmkv[it] = ok ? b : 0u;  // a dropped row adds nothing to the reduction
     }
@@ -540,6 +544,10 @@ __global__ __launch_bounds__(Cf::kThreads, PL<Cf>::kMinWaves) void conv1x1p_kern
   const int64_t cm_scale = Cmask ? 1 : 0;
   const uint8_t* const bm_base = bs.mask ? bs.mask : g_mask_ones;
   const int64_t bm_scale = bs.mask ? 1 : 0;
+  // BSTATS sum-only (bs.x null): the BatchNorm input is not read (a zero page, stride 0) — only sum(dz) is
+  // meaningful then; the ALG backward derives sum(dz (x - mean)) from its weight-gradient pass (bn_alg.hip)
+  const uint16_t* const bx_base = bs.x ? bs.x : reinterpret_cast<const uint16_t*>(g_gemm_zero);
+  const int64_t bx_scale = bs.x ? 1 : 0;
 
   int mt = tile / ntn, n0 = (tile % ntn) * BN, m0 = mt * BM;
 #pragma unroll
@@ -684,7 +692,7 @@ __global__ __launch_bounds__(Cf::kThreads, PL<Cf>::kMinWaves) void conv1x1p_kern
           const int mc = ok ? m : M - 1;
           const int64_t off = (int64_t)mc * N + cur_n0 + c * 8;
           if constexpr (BSTATS) {
-            xbv[it] = *reinterpret_cast<const uint4*>(bs.x + off);
+            xbv[it] = *reinterpret_cast<const uint4*>(bx_base + off * bx_scale);
             const unsigned b8 = bm_base[(off >> 3) * bm_scale];
             bmkv[it] = ok ? b8 : 0u;
           }
@@ -888,7 +896,7 @@ int dispatch(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t* 
     return launch_nt<Cf, false, false, false, false, true>(a, b, y, c, cm, part, M, K, N, bs, cg, s, acoef);
   }
   if (bs.part) {
-    if (!bs.x || !bs.mean) return -1;
+    if (!bs.mean) return -1;
     if (c) return launch<Cf, true, false, true>(a, b, y, c, cm, part, M, K, N, bs, cg, s);
     return launch<Cf, false, false, true>(a, b, y, c, cm, part, M, K, N, bs, cg, s);
   }
@@ -964,7 +972,7 @@ int pdt_conv1x1_gemm_seg(const uint16_t* a1, int k1, const uint16_t* a2, int k2,
   ApArgs ap{};
   ap.a2 = a2; ap.k1 = k1; ap.k2 = k2; ap.rep2 = rep2;
   if (bn_part) {
-    if (!bn_x || !bn_mean) return -1;
+    if (!bn_mean) return -1;
     if (N % 128 == 0) return launch_nt<GWide, false, false, false, true>(a1, b, y, nullptr, nullptr, nullptr, M, K, N, bs, cg, s, nullptr, ap);
     return launch_nt<GNarrow, false, false, false, true>(a1, b, y, nullptr, nullptr, nullptr, M, K, N, bs, cg, s, nullptr, ap);
   }

@@ -274,10 +274,9 @@ class _GlobalAvgPoolFn(torch.autograd.Function):
                 and not native_disabled()):
             from ..ops._native import native
             gs = ctx.gsrc if (ctx.gsrc is not None and ctx.gsrc.ready()) else None
-            r = native().gap_bwd(gy.contiguous(), h, w, gs.x if gs else None, gs.mask if gs else None,
-                                 gs.mean if gs else None)
-            if gs is not None and len(r) == 2:
-                gs.deposit(r[1], r[0], masked=gs.mask is not None)  # the last bn3's backward skips its reduce pass
+            r = native().gap_bwd(gy.contiguous(), h, w, **(gs.bn_kwargs() if gs else {}))
+            if gs is not None and len(r) == 2:  # the last bn3's backward skips its reduce pass
+                gs.deposit(r[1], r[0], masked=gs.mask is not None, sum_only=gs.sum_only)
             return r[0], None
         g = (gy * (1.0 / (h * w))).view(n, c, 1, 1).expand(n, c, h, w)
         return g.contiguous(memory_format=torch.channels_last), None

@@ -69,20 +69,32 @@ class GradStatsSource:
     another branch's gradient into it — and otherwise falls back to its own reduce pass.
     ``PDT_BN_BWD_STATS=0`` turns the hand-off off."""
 
-    __slots__ = ("x", "mask", "mean", "out_version", "part", "grad_ptr", "grad_version", "masked")
+    __slots__ = ("x", "mask", "mean", "out_version", "part", "grad_ptr", "grad_version", "masked", "sum_only",
+                 "part_sum_only")
 
     def __init__(self):
         self.x = self.mask = self.mean = self.part = None
         self.out_version = self.grad_ptr = self.grad_version = None
         self.masked = False  # the depositing kernel stored the gradient already multiplied by the ReLU mask
+        # sum_only (set by the BatchNorm's forward, PDT_BWD_ALG=2): the consumer computes sum(dz) only and never
+        # reads x; the BatchNorm's backward completes sum(dz (x - mean)) through the ALG pass (part_sum_only)
+        self.sum_only = self.part_sum_only = False
 
     def ready(self) -> bool:
         return self.x is not None and self.part is None
 
-    def deposit(self, part: torch.Tensor, grad: torch.Tensor, masked: bool = False) -> None:
-        """``masked``: ``grad`` was stored as dy * relu mask (our 1x1 GEMM's BSTATS epilogue does)."""
+    def deposit(self, part: torch.Tensor, grad: torch.Tensor, masked: bool = False, sum_only: bool = False) -> None:
+        """``masked``: ``grad`` was stored as dy * relu mask (our 1x1 GEMM's BSTATS epilogue does);
+        ``sum_only``: ``part``'s centred sums are NOT valid (the producer did not read x)."""
         self.part, self.grad_ptr, self.grad_version = part, grad.data_ptr(), grad._version
         self.masked = bool(masked)
+        self.part_sum_only = bool(sum_only)
+
+    def bn_kwargs(self) -> dict:
+        """conv1x1_gemm / gap_bwd keyword arguments of this BatchNorm's backward reduction."""
+        if self.sum_only:
+            return dict(bn_x=None, bn_mask=self.mask, bn_mean=self.mean, bn_sum_only=True)
+        return dict(bn_x=self.x, bn_mask=self.mask, bn_mean=self.mean)
 
     def take(self, dy: torch.Tensor):
         part, self.part = self.part, None
@@ -125,13 +137,14 @@ class DeferredBNGrad:
     backward (csrc/kernels/conv1x1_bwd_fused.hip) forms dx while loading it, so the BatchNorm's apply
     pass — a read of (dy, x, mask) and a write of dx, then two re-reads of dx — never runs."""
 
-    __slots__ = ("dy", "x", "mask", "mean", "coef", "dy_masked")
+    __slots__ = ("dy", "x", "mask", "mean", "coef", "dy_masked", "wg")
 
-    def __init__(self, dy, x, mask, mean, coef, dy_masked: bool = False):
+    def __init__(self, dy, x, mask, mean, coef, dy_masked: bool = False, wg=None):
         self.dy, self.x, self.mask, self.mean, self.coef = dy, x, mask, mean, coef
         # dy_masked: dy already equals dy * m (no mask, or the producing kernel stored it masked): the ALG
         # backward (ops/conv.py _bwd_alg) then uses dy directly as the GEMM operand g
         self.dy_masked = dy_masked
+        self.wg = wg  # the ALG weight-gradient pass, when the BatchNorm's backward already ran it
 
     def materialize(self) -> torch.Tensor:
         """dx as a tensor (fallback when the consumer cannot take the deferred form)."""
@@ -150,13 +163,14 @@ class BNGradLink:
     as its input gradient) to the backward of the conv that produced the BatchNorm's input (which
     runs next, with its output gradient None: ``set_materialize_grads(False)``)."""
 
-    __slots__ = ("grad", "needs_masked")
+    __slots__ = ("grad", "needs_masked", "alg_src")
 
     def __init__(self, needs_masked: bool = False):
         self.grad = None
         # needs_masked: the receiving conv takes the deferred form only with dy already masked (the ALG backward,
         # ops/conv.py _bwd_alg); otherwise the BatchNorm's backward runs its own apply and returns dx to autograd
         self.needs_masked = needs_masked
+        self.alg_src = None  # (a, W): the receiving conv's input and weight (set by its forward)
 
     def take(self):
         g, self.grad = self.grad, None
@@ -222,6 +236,9 @@ class _BNTrainFn(torch.autograd.Function):
             ctx.set_materialize_grads(False)
         if gsrc is not None:  # what the consumer's dgrad GEMM needs for this BN's backward reduction
             gsrc.x, gsrc.mask, gsrc.mean = x, (mask if relu else None), mean
+            # PDT_BWD_ALG=2: the consumer takes sum(dz) only; this backward completes the reduction (ALG prelude)
+            gsrc.sum_only = bool(SW.bwd_alg >= 2 and ctx.out_link is not None and ctx.out_link.needs_masked
+                                 and relu)
         # backward needs the BN input and a 1-bit ReLU mask, never the output y
         ctx.save_for_backward(x, mask if (relu and defer_relu is None) else None, weight, mean, invstd)
         return y
@@ -251,6 +268,13 @@ class _BNTrainFn(torch.autograd.Function):
         dy = dy.contiguous(memory_format=fmt)
         # the reduction over (dy, x), if the kernel that wrote dy already took it (GradStatsSource)
         part = ctx.gsrc.take(dy) if ctx.gsrc is not None else None
+        alg_wg = None
+        if part is not None and ctx.gsrc.part_sum_only:
+            # the producer summed dz only: complete sum(dz (x - mean)) from the ALG weight-gradient pass of the
+            # conv that produced x (z = a W^T: sum_m dz (z - mean) = rowsum(P * W) - mean sum(dz), bn_alg.hip)
+            alg_wg = _alg_prelude(ctx, dy, part)
+            if alg_wg is None:
+                part = None  # not completable: the finalize below reduces over (dy, x) itself
 
         def bwd(relu, has_res):
             if part is not None:
@@ -263,7 +287,7 @@ class _BNTrainFn(torch.autograd.Function):
             # coefficients only: the producing conv's fused backward forms dx = A dy m + B (x - mean) + D
             coef, dg, db = native().bn_bwd_coef(dy, x, part, mask if ctx.relu else None, weight, mean, invstd,
                                                 ctx.relu, need_w)
-            ctx.out_link.grad = DeferredBNGrad(dy, x, mask if ctx.relu else None, mean, coef, dy_masked)
+            ctx.out_link.grad = DeferredBNGrad(dy, x, mask if ctx.relu else None, mean, coef, dy_masked, alg_wg)
             if ctx.has_res:  # lazy link (checked in forward): the shortcut gets (dy, mask) as before
                 ctx.link.grad = MaskedGrad(dy, mask) if ctx.relu else dy
             return (None, None, dg if need_w else None, db if need_w else None) + tail
@@ -277,6 +301,24 @@ class _BNTrainFn(torch.autograd.Function):
             ctx.link.grad = dres  # the main-branch consumer adds its gradient into this buffer
             dres = None
         return (dx, dres if ctx.has_res else None, dg if need_w else None, db if need_w else None) + tail
+
+
+def _alg_prelude(ctx, dy, part):
+    """The ALG weight-gradient pass [g | a | 1]^T a (ops/conv.py _bwd_alg) run from the BatchNorm's backward, and
+    ``part``'s centred sums completed from it in place; returns that pass's fp32 output (handed to the conv's
+    backward in the DeferredBNGrad), or None when it cannot run (no conv source, unmasked dy)."""
+    link = ctx.out_link
+    src = link.alg_src if link is not None else None
+    if src is None or not ctx.gsrc.masked:
+        return None
+    a, w = src
+    from .conv import _nhwc2d
+    C4, CW = w.shape[0], w.shape[1]
+    wg = native().conv1x1_wgrad_seg(_nhwc2d(a), _nhwc2d(dy), _nhwc2d(a))
+    if wg is None:
+        return None
+    native().bn_alg_fix_s2(part, wg, w.reshape(C4, CW).contiguous())
+    return wg
 
 
 class _BNEvalFn(torch.autograd.Function):

@@ -325,6 +325,8 @@ class _Conv1x1Fn(torch.autograd.Function):
         ctx.bwd_link = bwd_link
         if bwd_link is not None:
             ctx.set_materialize_grads(False)
+            if bwd_link.needs_masked:  # the consuming BatchNorm's backward may run the ALG pass (batchnorm.py)
+                bwd_link.alg_src = (x, weight)
         ctx.save_for_backward(x, weight)
         ctx.dre = dre
         if dre is not None:  # always our GEMM: no library takes the deferred operand
@@ -414,16 +416,15 @@ class _Conv1x1Fn(torch.autograd.Function):
             gs = ctx.gsrc
             dx = torch.empty_like(x)
             gpart = native().conv1x1_gemm(g2, _wt_of(weight, w2), _nhwc2d(dx), True, False, strided.t,
-                                          bn_x=gs.x, bn_mask=gs.mask, bn_mean=gs.mean, c_stride=strided.s, c_H=H,
-                                          c_W=W)
-            gs.deposit(gpart, dx, masked=gs.mask is not None)
+                                          c_stride=strided.s, c_H=H, c_W=W, **gs.bn_kwargs())
+            gs.deposit(gpart, dx, masked=gs.mask is not None, sum_only=gs.sum_only)
             strided = None
             return dx, _Conv1x1Fn._wgrad(ctx, g2, x2, x, gy, weight, M, Ci, Co, fork)
         # dx is final (nothing is added to it after the GEMM) unless this is the first of two linked
         # branches or a strided shortcut's gradient is added below: only then can the GEMM's epilogue
         # take the producing BatchNorm's backward reduction (GradStatsSource)
         gs = ctx.gsrc if (ctx.gsrc is not None and ctx.gsrc.ready() and not first and strided is None) else None
-        bn_kw = dict(bn_x=gs.x, bn_mask=gs.mask, bn_mean=gs.mean) if gs is not None else {}
+        bn_kw = gs.bn_kwargs() if gs is not None else {}
         gpart = None
         if isinstance(acc, MaskedGrad) and ctx.needs_input_grad[0] and _ours_ok("dgrad", M, Co, Ci):
             # dx = dy*mask + dY W: the shortcut's ReLU-masked gradient applied in the GEMM epilogue
@@ -471,7 +472,7 @@ class _Conv1x1Fn(torch.autograd.Function):
         if strided is not None and dx is not None:
             strided.add_into(dx)
         if gpart is not None and dx is not None:
-            gs.deposit(gpart, dx, masked=gs.mask is not None)  # conv1x1.hip stores BSTATS outputs masked
+            gs.deposit(gpart, dx, masked=gs.mask is not None, sum_only=gs.sum_only)  # stored masked (conv1x1.hip)
         if first and dx is not None:  # first of the two branches: leave dx for the partner to add to
             ctx.link.grad, dx = dx, None
         return dx, _Conv1x1Fn._wgrad(ctx, g2, x2, x, gy, weight, M, Ci, Co, fork)
@@ -567,7 +568,9 @@ def _bwd_alg(ctx, d, x, weight):
     C4, CW = weight.shape[0], weight.shape[1]
     g2 = _nhwc2d(d.dy.contiguous(memory_format=torch.channels_last))  # [M, C4] gradient at bn3's output, masked
     a2 = _nhwc2d(x)  # [M, CW] this conv's input (bn2's output)
-    wg = native().conv1x1_wgrad_seg(a2, g2, a2)  # [C4 + CW + ones, CW] fp32: P, Gram, column sums of a
+    wg = d.wg  # run by bn3's backward already (PDT_BWD_ALG=2, batchnorm.py _alg_prelude)
+    if wg is None:
+        wg = native().conv1x1_wgrad_seg(a2, g2, a2)  # [C4 + CW + ones, CW] fp32: P, Gram, column sums of a
     if wg is None:
         return None
     w2 = weight.reshape(C4, CW).contiguous()

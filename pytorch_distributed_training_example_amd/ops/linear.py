@@ -5,13 +5,20 @@ two library GEMMs (dX = dY·W, dW = dYᵀ·X) plus ``colsum`` for dbias — aten
 generic ``sum(0)`` reduction kernel, which streams a [tokens, D] bf16 gradient at a fraction of
 HBM rate (profiles/r1_steady_gpt2_medium_ours.md: 73 ``reduce_kernel`` calls, 1.6 ms/step).
 
-``PDT_LINEAR_EPILOGUE=1`` runs the forward GEMMs on our MFMA kernel instead (csrc/kernels/gemm.hip:
-bias epilogue, and the MLP's fc1 + bias + GELU in one pass, ``linear_gelu``). Default OFF: measured
-at 0.61-0.94x of the tuned hipBLASLt GEMM (+ standalone GELU kernel) on every ViT-B/16 and
-GPT-2-medium shape (profiles/r3/gemm_vs_hipblaslt.md).
+Forward GEMMs on our MFMA kernel (csrc/kernels/gemm.hip: bias epilogue, and the MLP's fc1 + bias + GELU in
+one pass, ``linear_gelu``) are chosen PER SHAPE by measurement, as the 1x1 convs are (ops/conv.py _pick):
+``PDT_LINEAR_EPILOGUE=auto`` (default) looks the (kind, M, N, K) up in ``tuning/linear_gfx950.json``, and a
+shape not in the table is timed once (eager steps only; under hipGraph capture the library runs) against
+hipBLASLt (+ our standalone bias+GELU kernel for the fused kind) and the winner cached. Our kernel wins on
+some shapes only (vit_qkv 1.08x, vit_fc2 1.03x, gpt2_proj + bias 1.05x; 0.61-0.94x on the others:
+profiles/r5/gemm_bn128.txt, profiles/r3/gemm_vs_hipblaslt.md), so all-or-nothing would lose. ``=1``: ours
+on every shape it serves, ``=0``: never. ``PDT_LINEAR_DUMP=path`` writes the decisions at exit.
 """
 from __future__ import annotations
 
+import atexit
+import json
+import os
 from typing import Dict, Optional, Tuple
 
 import torch
@@ -54,8 +61,73 @@ def gemm_nt_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
             and w.shape[0] % 128 == 0 and w.shape[1] % 64 == 0 and x.shape[-1] == w.shape[1] and x.numel() > 0)
 
 
-def _ours(x: torch.Tensor, w: torch.Tensor) -> bool:
-    return SW.linear_epilogue and gemm_nt_ok(x, w)
+_LIN_CHOICE: Dict[str, str] = {}
+_LIN_TABLE = [False]
+TABLE = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), "tuning",
+                     "linear_gfx950.json")
+
+
+def _lin_table() -> None:
+    if _LIN_TABLE[0]:
+        return
+    _LIN_TABLE[0] = True
+    try:
+        with open(TABLE) as f:
+            d = json.load(f)
+        if d.get("arch") in (None, _arch()):
+            _LIN_CHOICE.update({k: v for k, v in d.get("choices", {}).items() if v in ("ours", "lib")})
+    except (OSError, ValueError):
+        pass
+    out = os.environ.get("PDT_LINEAR_DUMP")
+    if out:
+        atexit.register(lambda: json.dump({"arch": _arch(), "choices": dict(sorted(_LIN_CHOICE.items()))},
+                                          open(out, "w"), indent=1))
+
+
+def _arch() -> str:
+    try:
+        return torch.cuda.get_device_properties(0).gcnArchName.split(":")[0]
+    except Exception:  # pragma: no cover - no GPU
+        return "cpu"
+
+
+def _ours(x: torch.Tensor, w: torch.Tensor, kind: str = "bias", b: Optional[torch.Tensor] = None,
+          tanh_form: bool = False) -> bool:
+    """Run this forward GEMM (``kind``: "bias" | "nobias" | "gelu") on our kernel? See the module docstring."""
+    mode = SW.linear_epilogue
+    if mode == "0" or not gemm_nt_ok(x, w):
+        return False
+    if mode == "1":
+        return True
+    M, K, N = x.numel() // x.shape[-1], x.shape[-1], w.shape[0]
+    key = f"{kind},{M},{N},{K}"
+    c = _LIN_CHOICE.get(key)
+    if c is None:
+        _lin_table()
+        c = _LIN_CHOICE.get(key)
+    if c is None:
+        if torch.cuda.is_current_stream_capturing():
+            return False
+        from .conv import _time
+        x2, wc = x.reshape(-1, K).contiguous(), w.contiguous()
+        if kind == "gelu":
+            bf = b.float() if b is not None else None
+            ours = lambda: native().gemm_nt(x2, wc, bf, 2, tanh_form)  # noqa: E731
+            from .gelu import bias_gelu
+            lib = lambda: bias_gelu(F.linear(x2, wc), bf, "tanh" if tanh_form else "none")  # noqa: E731
+        else:
+            bb = b if kind == "bias" else None
+            ours = lambda: native().gemm_nt(x2, wc, bb, 1 if bb is not None else 0, False)  # noqa: E731
+            lib = lambda: F.linear(x2, wc, bb)  # noqa: E731
+        with torch.no_grad():
+            c = "ours" if _time(ours) < _time(lib) else "lib"
+        _LIN_CHOICE[key] = c
+    return c == "ours"
+
+
+def linear_choices() -> Dict[str, str]:
+    """Decisions taken so far: {"kind,M,N,K": "ours" | "lib"}."""
+    return dict(_LIN_CHOICE)
 
 
 class _LinearFn(torch.autograd.Function):
@@ -63,7 +135,7 @@ class _LinearFn(torch.autograd.Function):
     def forward(ctx, x, w, b):
         ctx.save_for_backward(x, w)
         ctx.has_b = b is not None
-        if _ours(x, w):
+        if _ours(x, w, "bias" if b is not None else "nobias", b):
             x2 = x.reshape(-1, x.shape[-1]).contiguous()
             y = native().gemm_nt(x2, w.contiguous(), b, 1 if b is not None else 0, False)[0]
             return y.view(*x.shape[:-1], w.shape[0])
@@ -129,6 +201,7 @@ class _LinearGeluFn(torch.autograd.Function):
 def linear_gelu(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor], approximate: str) -> Optional[torch.Tensor]:
     """gelu(linear(x, weight, bias)) on the fused-epilogue kernel, or None when it does not apply
     (switch off, unsupported shape/dtype): the caller then runs linear + bias_gelu."""
-    if not (use_native(x) and _ours(x, weight)) or (bias is not None and bias.dtype not in (torch.bfloat16, torch.float32)):
+    if (bias is not None and bias.dtype not in (torch.bfloat16, torch.float32)) or not use_native(x) \
+            or not _ours(x, weight, "gelu", bias, approximate == "tanh"):
         return None
     return _LinearGeluFn.apply(x, weight, bias, approximate == "tanh")

@@ -151,10 +151,12 @@ def _rel(ga, gref):
     return torch.tensor([float((ga[n] - gref[n]).norm() / gref[n].norm().clamp_min(1e-12)) for n in gref])
 
 
-def test_resnet50_grads_alg_vs_unfused(switch):
+@pytest.mark.parametrize("mode", ["1", "2"])
+def test_resnet50_grads_alg_vs_unfused(switch, mode):
     """Whole ResNet-50: with the ALG backward every layer-2/3/4 conv3 takes it (13 blocks, the last one fed by
     the global-average-pool gradient kernel), and the gradients are as accurate against the fp32 oracle as
-    the unfused chain's, tensor by tensor."""
+    the unfused chain's, tensor by tensor. mode 2: bn3's backward reduction completed from the ALG pass (the
+    producing epilogue never reads bn3's input)."""
     from pytorch_distributed_training_example_amd.ops import conv as conv_ops
     calls = []
     orig = conv_ops._bwd_alg
@@ -165,7 +167,7 @@ def test_resnet50_grads_alg_vs_unfused(switch):
         return r
     conv_ops._bwd_alg = spy
     try:
-        switch("PDT_BWD_ALG", "1")
+        switch("PDT_BWD_ALG", mode)
         ga = _grads()
     finally:
         conv_ops._bwd_alg = orig

@@ -65,3 +65,30 @@ def test_mlp_on_fused_epilogue_matches_default_path(switch, approximate):
     for a, b in zip(outs[0], outs[1]):
         assert _rel(b, a) < 1e-2, _rel(b, a)
 
+
+
+def test_linear_per_shape_dispatch(switch):
+    """PDT_LINEAR_EPILOGUE=auto (ops/linear.py _ours): every forward Linear GEMM shape is decided once — table
+    or timing — between our MFMA kernel and hipBLASLt; both give the same result to bf16 accuracy, and the
+    fused fc1 + bias + GELU kind is decided separately."""
+    import torch.nn.functional as F
+    from pytorch_distributed_training_example_amd.ops import linear as L
+    switch("PDT_LINEAR_EPILOGUE", "auto")
+    g = torch.Generator(device="cuda").manual_seed(0)
+    x = torch.randn(4, 197, 768, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(2304, 768, device="cuda", generator=g) * 0.03).bfloat16()
+    b = torch.randn(2304, device="cuda", generator=g).bfloat16()
+    y = L.linear(x, w, b)
+    torch.testing.assert_close(y.float(), F.linear(x.float(), w.float(), b.float()), rtol=2e-2, atol=2e-2)
+    key = f"bias,{4 * 197},2304,768"
+    assert L.linear_choices().get(key) in ("ours", "lib"), L.linear_choices()
+    for forced in ("ours", "lib"):
+        L._LIN_CHOICE[key] = forced
+        torch.testing.assert_close(L.linear(x, w, b).float(), y.float(), rtol=2e-2, atol=2e-2)
+    w1 = (torch.randn(3072, 768, device="cuda", generator=g) * 0.03).bfloat16()
+    b1 = torch.randn(3072, device="cuda", generator=g)
+    gl = L.linear_gelu(x, w1, b1, "tanh")
+    ref = F.gelu(F.linear(x.float(), w1.float(), b1), approximate="tanh")
+    if gl is not None:
+        torch.testing.assert_close(gl.float(), ref, rtol=3e-2, atol=3e-2)
+    assert L.linear_choices().get(f"gelu,{4 * 197},3072,768") in ("ours", "lib")
