@@ -382,6 +382,10 @@ inline bool geo_of(int M, int Ci, int Co, W1Geo& g, int seg_co1 = 0, int seg_co2
   g.nblk = (Co / ci.cob) * (Ci / ci.cib);
   const int target = g_target_wgs > 0 ? g_target_wgs : wgs_default(ci, g.nblk);
   int ns = (target + g.nblk - 1) / g.nblk;
+  // SEG (many channel blocks): ONE wave of workgroups — as many splits as fit the CUs' resident slots
+  // (256 x LDS occupancy) rather than rounding up past them: 11 blocks x 24 splits = 264 workgroups at one
+  // per CU would run 8 of them as a second, full-length wave
+  if (seg_co1 && g_target_wgs <= 0) ns = (256 * (ci.occ > 0 ? ci.occ : 1)) / g.nblk;
   if (ns > g.ntiles) ns = g.ntiles;
   if (ns < 1) ns = 1;
   g.tiles_per_split = (g.ntiles + ns - 1) / ns;

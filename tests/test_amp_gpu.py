@@ -172,25 +172,48 @@ def _amp_ddp_worker(rank, world, model_name):
     loss = float(step(x, y))
     torch.cuda.synchronize()
     got = [p.grad.detach().float().cpu() for p in model.parameters()]
+    stock = copy.deepcopy(oracle)
     oracle.zero_grad(set_to_none=True)
     ref_loss = loss_fn(oracle(x), y)
     ref_loss.backward()
     want = [p.grad.detach().float().cpu() for p in oracle.parameters()]
-    return loss, float(ref_loss), got, want, scaler.get_scale(), int(scaler._growth_tracker.item())
+    # torch's own recipe on stock ops (PDT_DISABLE_NATIVE): autocast fp16 + torch.amp.GradScaler — the accuracy
+    # fp16 autocast itself reaches on this model (random-init ResNets amplify fp16 rounding: ~13 % per tensor)
+    import os
+    from pytorch_distributed_training_example_amd.config import SW
+    os.environ["PDT_DISABLE_NATIVE"] = "1"
+    SW.reload()
+    try:
+        ts = torch.amp.GradScaler("cuda", init_scale=2.0 ** 12)
+        with torch.autocast("cuda", dtype=torch.float16):
+            sl = torch.nn.functional.cross_entropy(stock(x), y)
+        ts.scale(sl).backward()
+        ts.unscale_(torch.optim.SGD(stock.parameters(), lr=0.0))
+        ref16 = [p.grad.detach().float().cpu() for p in stock.parameters()]
+    finally:
+        os.environ.pop("PDT_DISABLE_NATIVE", None)
+        SW.reload()
+    return loss, float(ref_loss), got, want, scaler.get_scale(), int(scaler._growth_tracker.item()), ref16
 
 
 @pytest.mark.parametrize("model_name", ["vit_tiny", "resnet18"])
 def test_amp_fp16_ddp_step_matches_fp32_oracle(model_name):
-    (loss, ref_loss, got, want, scale, tracker), = run_ranks(_amp_ddp_worker, 1, (model_name,), use_gpu=True,
-                                                             backend="nccl")
+    (loss, ref_loss, got, want, scale, tracker, ref16), = run_ranks(_amp_ddp_worker, 1, (model_name,),
+                                                                    use_gpu=True, backend="nccl")
     # a clean step: no overflow at 2^12, the tracker counted it, the unscaled gradients are the fp32 ones
     assert scale == 2.0 ** 12 and tracker == 1
     assert abs(loss - ref_loss) < 1e-2 * max(1.0, abs(ref_loss)), (loss, ref_loss)
-    rel = torch.tensor([((a - b).norm() / (b.norm() + 1e-12)).item() for a, b in zip(got, want)
-                        if b.norm() > 1e-6 * max(w.norm() for w in want)])
-    # fp16 autocast: 11-bit significands through the forward and backward GEMMs. Per-tensor errors are
-    # ~1e-3; a missing unscale would be 4096x off, a skipped update of the scale would show above
-    assert rel.median() < 1e-2 and rel.max() < 6e-2, (float(rel.median()), float(rel.max()), int(rel.argmax()))
+    big = max(w.norm() for w in want)
+    keep = [i for i, w in enumerate(want) if w.norm() > 1e-6 * big]
+    rel = torch.tensor([((got[i] - want[i]).norm() / want[i].norm()).item() for i in keep])
+    rel16 = torch.tensor([((ref16[i] - want[i]).norm() / want[i].norm()).item() for i in keep])
+    # our AMP step (device-side scaler, fused optimizer, DDP buckets) is as accurate as torch's own fp16 recipe
+    # on the same model; a missing unscale would be 4096x off, a dropped gradient 100 %
+    print(f"amp16 ours vs fp32: median {float(rel.median()):.3e} max {float(rel.max()):.3e}; "
+          f"torch amp16: median {float(rel16.median()):.3e} max {float(rel16.max()):.3e}")
+    assert rel.median() <= 1.25 * rel16.median() + 5e-3, (float(rel.median()), float(rel16.median()))
+    assert rel.max() <= 1.25 * rel16.max() + 2e-2, (float(rel.max()), float(rel16.max()))
+    assert rel.max() < 0.5
 
 
 def test_amp_fp16_graph_captured_step():

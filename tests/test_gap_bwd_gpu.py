@@ -46,9 +46,9 @@ def test_resnet50_grads_with_native_gap(switch):
     deposits = []
     orig = B.GradStatsSource.deposit
 
-    def spy(self, part, grad):
+    def spy(self, part, grad, **kw):
         deposits.append(tuple(grad.shape))
-        return orig(self, part, grad)
+        return orig(self, part, grad, **kw)
     out = {}
     for on in ("1", "0"):
         switch("PDT_GAP_NATIVE", on)
