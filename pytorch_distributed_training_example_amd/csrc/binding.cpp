@@ -146,6 +146,8 @@ int pdt_conv1x1_gemm_seg(const uint16_t* a1, int k1, const uint16_t* a2, int k2,
                          uint16_t* y, int M, int N, const uint16_t* bn_x, const uint8_t* bn_mask, const float* bn_mean,
                          float* bn_part, hipStream_t s);
 int pdt_bn_alg_fix_s2(float* part, int T, const float* wg, const uint16_t* W, int C4, int CW, hipStream_t s);
+int pdt_bn_alg_small_gemm(const uint16_t* W, const float* coef, const float* wg, float* G, float* BWG, int C4, int CW,
+                          hipStream_t s);
 int pdt_bn_alg_assemble(const uint16_t* W, const float* coef, const float* mean, const float* G, const float* wg,
                         const float* BWG, uint16_t* bcat, uint16_t* dW, int C4, int CW, hipStream_t s);
 int pdt_conv1x1_wgrad(const uint16_t* x, const uint16_t* dy, uint16_t* dw, float* ws, int M, int Ci, int Co,
@@ -1220,6 +1222,26 @@ std::vector<Tensor> bn_alg_assemble(Tensor w, Tensor coef, Tensor mean, Tensor G
                                      reinterpret_cast<uint16_t*>(dW.data_ptr()), (int)C4, (int)CW, stream());
   TORCH_CHECK(rc == 0, "pdt_bn_alg_assemble failed: ", rc);
   return {bcat, dW};
+}
+
+// (G [CW, CW], BWG [C4, CW]) fp32 of the ALG backward: W^T diag(B) W and diag(B) W Gram (csrc/kernels/bn_alg.hip).
+std::vector<Tensor> bn_alg_small_gemm(Tensor w, Tensor coef, Tensor wg) {
+  check_cuda(w, "w");
+  check_cuda(coef, "coef");
+  check_cuda(wg, "wg");
+  TORCH_CHECK(w.dim() == 2 && w.scalar_type() == at::kBFloat16 && w.is_contiguous(), "bn_alg_small_gemm: w [C4, CW] bf16");
+  const int64_t C4 = w.size(0), CW = w.size(1);
+  TORCH_CHECK(coef.scalar_type() == at::kFloat && coef.is_contiguous() && coef.numel() == 3 * C4 &&
+                  wg.scalar_type() == at::kFloat && wg.is_contiguous() && wg.dim() == 2 && wg.size(1) == CW &&
+                  wg.size(0) >= C4 + CW && C4 % 64 == 0 && CW % 64 == 0,
+              "bn_alg_small_gemm: coef [3, C4], wg [>= C4 + CW, CW] fp32, C4 / CW % 64");
+  auto G = at::empty({CW, CW}, wg.options());
+  auto BWG = at::empty({C4, CW}, wg.options());
+  TORCH_CHECK(pdt_bn_alg_small_gemm(reinterpret_cast<const uint16_t*>(w.data_ptr()), coef.data_ptr<float>(),
+                                    wg.data_ptr<float>(), G.data_ptr<float>(), BWG.data_ptr<float>(), (int)C4, (int)CW,
+                                    stream()) == 0,
+              "pdt_bn_alg_small_gemm failed");
+  return {G, BWG};
 }
 
 // Completes a sum-only producer's BatchNorm backward partials in place (csrc/kernels/bn_alg.hip).
@@ -2337,6 +2359,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("out"), py::arg("bn_x") = py::none(), py::arg("bn_mask") = py::none(), py::arg("bn_mean") = py::none());
   m.def("bn_alg_assemble", &bn_alg_assemble);
   m.def("bn_alg_fix_s2", &bn_alg_fix_s2);
+  m.def("bn_alg_small_gemm", &bn_alg_small_gemm);
   m.def("conv1x1_wgrad_tune", [](int target_wgs, int variant, int interleave) { pdt_conv1x1_wgrad_tune(target_wgs, variant, interleave); },
         py::arg("target_wgs"), py::arg("variant") = -2, py::arg("interleave") = -2);
   m.def("embedding_fwd", &embedding_fwd);

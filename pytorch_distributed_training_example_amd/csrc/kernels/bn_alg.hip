@@ -68,13 +68,80 @@ __global__ __launch_bounds__(256) void bn_alg_assemble_kernel(const uint16_t* __
 // Sum-only producer (conv1x1.hip / gap_bwd with the BatchNorm input not read): each tile's centred-sum entry
 // is sum(g (0 - mean)) = -mean sum(g). The true one is sum(g (z - mean)) = sum_k P[c, k] W[c, k] - mean sum(g)
 // (z = a W^T): adding rowsum(P * W) to one tile's entry completes the reduction the finalize sums.
+// One wave per channel: lanes stride the (contiguous) row, then a fixed-order wave sum.
 __global__ __launch_bounds__(256) void bn_alg_fix_s2_kernel(float* __restrict__ part, int T, const float* __restrict__ wg,
                                                             const uint16_t* __restrict__ W, int C4, int CW) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (c >= C4) return;
   float s = 0.f;
-  for (int k = 0; k < CW; ++k) s += wg[(int64_t)c * CW + k] * bfv(W[(int64_t)c * CW + k]);
-  part[(int64_t)T * C4 + c] += s;  // part[1][0][c]
+  for (int k = lane; k < CW; k += 64) s += wg[(int64_t)c * CW + k] * bfv(W[(int64_t)c * CW + k]);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
+  if (lane == 0) part[(int64_t)T * C4 + c] += s;  // part[1][0][c]
+}
+
+// The two small fp32 products of the ALG backward in one launch (64 x 64 output tiles, 256 threads x 4 x 4):
+//   G   [CW, CW] = W^T diag(Bc) W          (tiles [0, nG): sum over the C4 rows of W)
+//   BWG [C4, CW] = diag(Bc) W Gram         (tiles [nG, ...): sum over CW; Gram = wg rows C4 .. C4 + CW - 1)
+__global__ __launch_bounds__(256) void bn_alg_small_gemm_kernel(const uint16_t* __restrict__ W, const float* __restrict__ coef,
+                                                                const float* __restrict__ wg, float* __restrict__ G,
+                                                                float* __restrict__ BWG, int C4, int CW) {
+  __shared__ float sa[16][65], sb[16][65];
+  const float* Bc = coef + C4;
+  const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+  const int tcw = CW / 64, nG = tcw * tcw;
+  int t = blockIdx.x;
+  float acc[4][4] = {};
+  if (t < nG) {  // G tile (i0, j0): sum_c W[c, i] Bc[c] W[c, j]
+    const int i0 = (t / tcw) * 64, j0 = (t % tcw) * 64;
+    for (int c0 = 0; c0 < C4; c0 += 16) {
+      for (int e = tid; e < 16 * 64; e += 256) {
+        const int r = e >> 6, q = e & 63, c = c0 + r;
+        const float bcv = Bc[c];
+        sa[r][q] = bfv(W[(int64_t)c * CW + i0 + q]) * bcv;
+        sb[r][q] = bfv(W[(int64_t)c * CW + j0 + q]);
+      }
+      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int v = 0; v < 4; ++v) acc[u][v] += sa[r][ty * 4 + u] * sb[r][tx * 4 + v];
+      __syncthreads();
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) G[(int64_t)(i0 + ty * 4 + u) * CW + j0 + tx * 4 + v] = acc[u][v];
+    return;
+  }
+  t -= nG;  // BWG tile (c0, k0): Bc[c] sum_j W[c, j] Gram[j, k]
+  const int cr0 = (t / tcw) * 64, k0 = (t % tcw) * 64;
+  const float* Gram = wg + (int64_t)C4 * CW;
+  for (int j0 = 0; j0 < CW; j0 += 16) {
+    for (int e = tid; e < 16 * 64; e += 256) {
+      const int r = e >> 6, q = e & 63;
+      sa[r][q] = bfv(W[(int64_t)(cr0 + q) * CW + j0 + r]);
+      sb[r][q] = Gram[(int64_t)(j0 + r) * CW + k0 + q];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) acc[u][v] += sa[r][ty * 4 + u] * sb[r][tx * 4 + v];
+    __syncthreads();
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int c = cr0 + ty * 4 + u;
+    const float bcv = Bc[c];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) BWG[(int64_t)c * CW + k0 + tx * 4 + v] = bcv * acc[u][v];
+  }
 }
 
 }  // namespace
@@ -85,7 +152,17 @@ extern "C" {
 // (rows 0..C4-1 = P), W [C4, CW] bf16: completes part's centred sums in place (see bn_alg_fix_s2_kernel).
 int pdt_bn_alg_fix_s2(float* part, int T, const float* wg, const uint16_t* W, int C4, int CW, hipStream_t s) {
   if (T < 1 || C4 < 1 || CW < 1) return -1;
-  hipLaunchKernelGGL(bn_alg_fix_s2_kernel, dim3((C4 + 255) / 256), dim3(256), 0, s, part, T, wg, W, C4, CW);
+  hipLaunchKernelGGL(bn_alg_fix_s2_kernel, dim3((C4 + 3) / 4), dim3(256), 0, s, part, T, wg, W, C4, CW);
+  return 0;
+}
+
+// G [CW, CW] and BWG [C4, CW] fp32 (see bn_alg_small_gemm_kernel); C4, CW % 64 == 0.
+int pdt_bn_alg_small_gemm(const uint16_t* W, const float* coef, const float* wg, float* G, float* BWG, int C4, int CW,
+                          hipStream_t s) {
+  if (C4 % 64 || CW % 64 || C4 < 64 || CW < 64) return -1;
+  const int tcw = CW / 64;
+  hipLaunchKernelGGL(bn_alg_small_gemm_kernel, dim3(tcw * tcw + (C4 / 64) * tcw), dim3(256), 0, s, W, coef, wg, G, BWG,
+                     C4, CW);
   return 0;
 }
 

@@ -574,11 +574,9 @@ def _bwd_alg(ctx, d, x, weight):
     if wg is None:
         return None
     w2 = weight.reshape(C4, CW).contiguous()
-    w2f = w2.float()
-    bw = w2f * d.coef[1].unsqueeze(1)       # diag(B) W
-    G = (w2f.t() @ bw).contiguous()         # W^T diag(B) W   [CW, CW]
-    bwg = (bw @ wg[C4:C4 + CW]).contiguous()  # diag(B) W Gram  [C4, CW]
-    bcat, dw2 = native().bn_alg_assemble(w2, d.coef.contiguous(), d.mean.contiguous(), G, wg, bwg)
+    coef = d.coef.contiguous()
+    G, bwg = native().bn_alg_small_gemm(w2, coef, wg)  # W^T diag(B) W [CW, CW], diag(B) W Gram [C4, CW] (fp32)
+    bcat, dw2 = native().bn_alg_assemble(w2, coef, d.mean.contiguous(), G, wg, bwg)
     gs = ctx.gsrc if (ctx.gsrc is not None and ctx.gsrc.ready()) else None
     dx = torch.empty_like(x, memory_format=torch.channels_last)
     part = native().conv1x1_gemm_seg(g2, a2, 2, bcat, _nhwc2d(dx), bn_x=gs.x if gs else None,

@@ -188,3 +188,25 @@ def test_alg_path_is_deterministic():
     assert SW.bwd_alg
     ga, gb = _grads(seed=3), _grads(seed=3)
     assert all(torch.equal(ga[k], gb[k]) for k in ga)
+
+
+@pytest.mark.parametrize("C4,CW", [(512, 128), (1024, 256), (2048, 512)])
+def test_small_gemm_and_fix_s2(C4, CW):
+    """bn_alg_small_gemm (G = W^T diag(B) W, BWG = diag(B) W Gram) and bn_alg_fix_s2 (a sum-only producer's
+    centred sums completed from P) against fp64 math."""
+    M = 1500
+    a, w, z, dy, bits, mean, coef = _deferred(M, C4, CW, 3 * C4)
+    wg = _n().conv1x1_wgrad_seg(a, dy, a)
+    G, bwg = _n().bn_alg_small_gemm(w, coef, wg)
+    wd, B = w.double(), coef[1].double()
+    torch.testing.assert_close(G.double(), wd.t() @ (B.unsqueeze(1) * wd), rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(bwg.double(), B.unsqueeze(1) * (wd @ wg[C4:C4 + CW].double()), rtol=1e-4, atol=1e-4)
+    # a sum-only producer's partials: sums of g, centred sums of g (0 - mean) per 256-row tile
+    T = (M + 255) // 256
+    g = dy.float()
+    pad = torch.cat([g, g.new_zeros(T * 256 - M, C4)]).view(T, 256, C4)
+    part = torch.stack([pad.sum(1), -mean * pad.sum(1)]).contiguous()
+    _n().bn_alg_fix_s2(part, wg, w)
+    zf = a.double() @ w.double().t()  # the conv's unrounded output: what z = a W^T gives the identity
+    want = (g.double() * (zf - mean.double())).sum(0)
+    torch.testing.assert_close(part[1].double().sum(0), want, rtol=1e-3, atol=1e-2)
