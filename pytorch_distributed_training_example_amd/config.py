@@ -42,7 +42,7 @@ PDT_BWD_FUSED               1            bottleneck conv3 + bn3 backward as one 
 PDT_BWD_FUSED_SHAPES        256x64       (Co x Ci) of the conv3s that take the fused backward ("256x64,512x128" adds
                                          layer 2: 0.9 % slower in-step since the branch-free conv1x1 epilogue,
                                          profiles/r5/ab_layer2_unfused.txt)
-PDT_BWD_ALG                 1            bottleneck conv3 + bn3 backward (the shapes PDT_BWD_FUSED does not take) without
+PDT_BWD_ALG                 2            bottleneck conv3 + bn3 backward (the shapes PDT_BWD_FUSED does not take) without
                                          bn3's apply pass: z = a W^T substituted into bn3's backward (ops/conv.py
                                          _bwd_alg, csrc/kernels/bn_alg.hip): one wgrad pass + one data-gradient GEMM;
                                          2: also bn3's backward reduction without reading z (sum-only producer)
@@ -127,7 +127,7 @@ class _Switches:
                                       e("PDT_BWD_FUSED_SHAPES", "256x64").split(",") if "x" in t)
         # 0 off; 1: ALG backward; 2: also the producer of bn3's gradient skips reading bn3's input for the backward
         # reduction (sum-only epilogue) and the ALG pass completes it (ops/batchnorm.py _BNTrainFn.backward)
-        self.bwd_alg = int(e("PDT_BWD_ALG", "1"))
+        self.bwd_alg = int(e("PDT_BWD_ALG", "2"))
         self.bn2_defer = on("PDT_BN2_DEFER", "0")
         self.bn_apply_gemm_k = int(e("PDT_BN_APPLY_GEMM_K", "64"))
         self.strided_bstats = on("PDT_STRIDED_BSTATS")

@@ -23,6 +23,8 @@ namespace {
 
 __device__ __forceinline__ float bfv(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
 
+constexpr int kSK = 128;  // K rows per split-K slice of the small products (bn_alg_small_gemm_kernel)
+
 // blocks [0, CW): row k of b; blocks [CW, ...): 256-element slices of dW
 __global__ __launch_bounds__(256) void bn_alg_assemble_kernel(const uint16_t* __restrict__ W, const float* __restrict__ coef,
                                                               const float* __restrict__ mean, const float* __restrict__ G,
@@ -45,7 +47,8 @@ __global__ __launch_bounds__(256) void bn_alg_assemble_kernel(const uint16_t* __
       cs += (D[c] - Bc[c] * mean[c]) * w;
     }
     for (int j = tid; j < CW; j += 256) {
-      const float gv = G[(int64_t)k * CW + j];
+      float gv = 0.f;  // the split-K slices of G in order (bn_alg_small_gemm_kernel)
+      for (int sl = 0; sl < C4 / kSK; ++sl) gv += G[((int64_t)sl * CW + k) * CW + j];
       const uint16_t hi = f2bf(gv);
       row[C4 + j] = hi;
       row[C4 + CW + j] = f2bf(gv - bfv(hi));
@@ -62,7 +65,9 @@ __global__ __launch_bounds__(256) void bn_alg_assemble_kernel(const uint16_t* __
   const int c = (int)(e / CW), k = (int)(e % CW);
   const float S = wg[(int64_t)(C4 + CW) * CW + k];  // first row of the ones block: column sums of a
   const float E = D[c] - Bc[c] * mean[c];
-  dW[e] = f2bf(A[c] * wg[e] + BWG[e] + E * S);
+  float bwg = 0.f;
+  for (int sl = 0; sl < CW / kSK; ++sl) bwg += BWG[(int64_t)sl * C4 * CW + e];
+  dW[e] = f2bf(A[c] * wg[e] + bwg + E * S);
 }
 
 // Sum-only producer (conv1x1.hip / gap_bwd with the BatchNorm input not read): each tile's centred-sum entry
@@ -81,66 +86,84 @@ __global__ __launch_bounds__(256) void bn_alg_fix_s2_kernel(float* __restrict__ 
   if (lane == 0) part[(int64_t)T * C4 + c] += s;  // part[1][0][c]
 }
 
-// The two small fp32 products of the ALG backward in one launch (64 x 64 output tiles, 256 threads x 4 x 4):
-//   G   [CW, CW] = W^T diag(Bc) W          (tiles [0, nG): sum over the C4 rows of W)
-//   BWG [C4, CW] = diag(Bc) W Gram         (tiles [nG, ...): sum over CW; Gram = wg rows C4 .. C4 + CW - 1)
+// The two small fp32 products of the ALG backward in one launch, as split-K partials (64 x 64 output tiles,
+// 256 threads x 4 x 4, K slices of 128 rows: 8 steps of 16 with the next step's operands loaded into registers
+// before the current step's FMAs — a serial K loop of C4 / 16 latency-bound steps ran 110-200 us):
+//   Gp[s]  [CW, CW] = sum over rows c of slice s: W[c, i] Bc[c] W[c, j]        (s < C4 / 128)
+//   Bp[s]  [C4, CW] = Bc[c] sum over rows j of slice s: W[c, j] Gram[j, k]       (s < CW / 128)
+// bn_alg_assemble_kernel sums the slices in a fixed order (deterministic).
 __global__ __launch_bounds__(256) void bn_alg_small_gemm_kernel(const uint16_t* __restrict__ W, const float* __restrict__ coef,
-                                                                const float* __restrict__ wg, float* __restrict__ G,
-                                                                float* __restrict__ BWG, int C4, int CW) {
-  __shared__ float sa[16][65], sb[16][65];
+                                                                const float* __restrict__ wg, float* __restrict__ Gp,
+                                                                float* __restrict__ Bp, int C4, int CW) {
+  __shared__ float sa[16][68], sb[16][68];
   const float* Bc = coef + C4;
   const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
   const int tcw = CW / 64, nG = tcw * tcw;
-  int t = blockIdx.x;
-  float acc[4][4] = {};
-  if (t < nG) {  // G tile (i0, j0): sum_c W[c, i] Bc[c] W[c, j]
-    const int i0 = (t / tcw) * 64, j0 = (t % tcw) * 64;
-    for (int c0 = 0; c0 < C4; c0 += 16) {
-      for (int e = tid; e < 16 * 64; e += 256) {
-        const int r = e >> 6, q = e & 63, c = c0 + r;
-        const float bcv = Bc[c];
-        sa[r][q] = bfv(W[(int64_t)c * CW + i0 + q]) * bcv;
-        sb[r][q] = bfv(W[(int64_t)c * CW + j0 + q]);
-      }
-      __syncthreads();
-#pragma unroll
-      for (int r = 0; r < 16; ++r)
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-#pragma unroll
-          for (int v = 0; v < 4; ++v) acc[u][v] += sa[r][ty * 4 + u] * sb[r][tx * 4 + v];
-      __syncthreads();
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-      for (int v = 0; v < 4; ++v) G[(int64_t)(i0 + ty * 4 + u) * CW + j0 + tx * 4 + v] = acc[u][v];
-    return;
-  }
-  t -= nG;  // BWG tile (c0, k0): Bc[c] sum_j W[c, j] Gram[j, k]
-  const int cr0 = (t / tcw) * 64, k0 = (t % tcw) * 64;
+  const int t = blockIdx.x, sl = blockIdx.y;
+  const bool isG = t < nG;
+  if (isG ? sl >= C4 / kSK : sl >= CW / kSK) return;
+  const int k0 = sl * kSK;
   const float* Gram = wg + (int64_t)C4 * CW;
-  for (int j0 = 0; j0 < CW; j0 += 16) {
-    for (int e = tid; e < 16 * 64; e += 256) {
-      const int r = e >> 6, q = e & 63;
-      sa[r][q] = bfv(W[(int64_t)(cr0 + q) * CW + j0 + r]);
-      sb[r][q] = Gram[(int64_t)(j0 + r) * CW + k0 + q];
+  int i0, j0;
+  if (isG) { i0 = (t / tcw) * 64; j0 = (t % tcw) * 64; }
+  else { i0 = ((t - nG) / tcw) * 64; j0 = ((t - nG) % tcw) * 64; }  // (c rows, k cols)
+  // this thread's 4 (a, b) operand elements of one 16-row step: e = tid + 256 u
+  float ra[4], rb[4];
+  auto load = [&](int kk) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = tid + 256 * u;
+      if (isG) {
+        const int r = e >> 6, q = e & 63, c = kk + r;
+        ra[u] = bfv(W[(int64_t)c * CW + i0 + q]) * Bc[c];
+        rb[u] = bfv(W[(int64_t)c * CW + j0 + q]);
+      } else {
+        const int r = e & 15, q = e >> 4;  // a: W[c = i0 + q, j = kk + r] (16 consecutive j per row)
+        ra[u] = bfv(W[(int64_t)(i0 + q) * CW + kk + r]);
+        const int r2 = e >> 6, q2 = e & 63;
+        rb[u] = Gram[(int64_t)(kk + r2) * CW + j0 + q2];
+      }
     }
+  };
+  float acc[4][4] = {};
+  load(k0);
+  for (int kk = k0; kk < k0 + kSK; kk += 16) {
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < 16; ++r)
+    for (int u = 0; u < 4; ++u) {
+      const int e = tid + 256 * u;
+      if (isG) { sa[e >> 6][e & 63] = ra[u]; }
+      else { sa[e & 15][e >> 4] = ra[u]; }
+      sb[e >> 6][e & 63] = rb[u];
+    }
+    __syncthreads();
+    if (kk + 16 < k0 + kSK) load(kk + 16);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float4 av = *reinterpret_cast<const float4*>(&sa[r][ty * 4]);
+      const float4 bv = *reinterpret_cast<const float4*>(&sb[r][tx * 4]);
+      const float a4[4] = {av.x, av.y, av.z, av.w}, b4[4] = {bv.x, bv.y, bv.z, bv.w};
 #pragma unroll
       for (int u = 0; u < 4; ++u)
 #pragma unroll
-        for (int v = 0; v < 4; ++v) acc[u][v] += sa[r][ty * 4 + u] * sb[r][tx * 4 + v];
-    __syncthreads();
+        for (int v = 0; v < 4; ++v) acc[u][v] += a4[u] * b4[v];
+    }
   }
+  if (isG) {
+    float* o = Gp + (int64_t)sl * CW * CW;
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int c = cr0 + ty * 4 + u;
-    const float bcv = Bc[c];
+    for (int u = 0; u < 4; ++u)
+      *reinterpret_cast<float4*>(o + (int64_t)(i0 + ty * 4 + u) * CW + j0 + tx * 4) =
+          make_float4(acc[u][0], acc[u][1], acc[u][2], acc[u][3]);
+  } else {
+    float* o = Bp + (int64_t)sl * C4 * CW;
 #pragma unroll
-    for (int v = 0; v < 4; ++v) BWG[(int64_t)c * CW + k0 + tx * 4 + v] = bcv * acc[u][v];
+    for (int u = 0; u < 4; ++u) {
+      const int c = i0 + ty * 4 + u;
+      const float bcv = Bc[c];
+      *reinterpret_cast<float4*>(o + (int64_t)c * CW + j0 + tx * 4) =
+          make_float4(bcv * acc[u][0], bcv * acc[u][1], bcv * acc[u][2], bcv * acc[u][3]);
+    }
   }
 }
 
@@ -156,13 +179,15 @@ int pdt_bn_alg_fix_s2(float* part, int T, const float* wg, const uint16_t* W, in
   return 0;
 }
 
-// G [CW, CW] and BWG [C4, CW] fp32 (see bn_alg_small_gemm_kernel); C4, CW % 64 == 0.
+// Gp [C4 / 128, CW, CW] and Bp [CW / 128, C4, CW] fp32 split-K slices (see bn_alg_small_gemm_kernel);
+// C4, CW % 128 == 0.
 int pdt_bn_alg_small_gemm(const uint16_t* W, const float* coef, const float* wg, float* G, float* BWG, int C4, int CW,
                           hipStream_t s) {
-  if (C4 % 64 || CW % 64 || C4 < 64 || CW < 64) return -1;
+  if (C4 % kSK || CW % kSK) return -1;
   const int tcw = CW / 64;
-  hipLaunchKernelGGL(bn_alg_small_gemm_kernel, dim3(tcw * tcw + (C4 / 64) * tcw), dim3(256), 0, s, W, coef, wg, G, BWG,
-                     C4, CW);
+  const int sy = C4 / kSK > CW / kSK ? C4 / kSK : CW / kSK;
+  hipLaunchKernelGGL(bn_alg_small_gemm_kernel, dim3(tcw * tcw + (C4 / 64) * tcw, sy), dim3(256), 0, s, W, coef, wg, G,
+                     BWG, C4, CW);
   return 0;
 }
 

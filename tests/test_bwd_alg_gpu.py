@@ -100,7 +100,12 @@ def test_assemble_matches_torch(C4, CW):
     bw = wf * coef[1].unsqueeze(1)
     G = (wf.t() @ bw).contiguous()
     bwg = (bw @ wg[C4:C4 + CW]).contiguous()
-    bcat, dw = _n().bn_alg_assemble(w, coef, mean, G, wg, bwg)
+    # the assemble kernel takes split-K slices (bn_alg_small_gemm's layout): whole products in slice 0
+    Gs = torch.zeros(C4 // 128, CW, CW, device="cuda")
+    Gs[0] = G
+    Bs = torch.zeros(CW // 128, C4, CW, device="cuda")
+    Bs[0] = bwg
+    bcat, dw = _n().bn_alg_assemble(w, coef, mean, Gs, wg, Bs)
     assert bcat.shape == (CW, C4 + 2 * CW + 32) and dw.shape == (C4, CW)
     E = coef[2] - coef[1] * mean
     c = E @ wf
@@ -198,6 +203,7 @@ def test_small_gemm_and_fix_s2(C4, CW):
     a, w, z, dy, bits, mean, coef = _deferred(M, C4, CW, 3 * C4)
     wg = _n().conv1x1_wgrad_seg(a, dy, a)
     G, bwg = _n().bn_alg_small_gemm(w, coef, wg)
+    G, bwg = G.sum(0), bwg.sum(0)  # split-K slices
     wd, B = w.double(), coef[1].double()
     torch.testing.assert_close(G.double(), wd.t() @ (B.unsqueeze(1) * wd), rtol=1e-4, atol=1e-5)
     torch.testing.assert_close(bwg.double(), B.unsqueeze(1) * (wd @ wg[C4:C4 + CW].double()), rtol=1e-4, atol=1e-4)
