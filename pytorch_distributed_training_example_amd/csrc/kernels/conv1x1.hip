@@ -971,8 +971,23 @@ int pdt_conv1x1_gemm_seg(const uint16_t* a1, int k1, const uint16_t* a2, int k2,
   const CGeom cg{0, 1, 1, 1, 1};
   ApArgs ap{};
   ap.a2 = a2; ap.k1 = k1; ap.k2 = k2; ap.rep2 = rep2;
-  if (bn_part) {
-    if (!bn_mean) return -1;
+  // tile for N % 256 (PDT_SEG_TILE, A/B): 0 = 8 waves of 64 x 64 (256 x 128), 1 = 8 waves of 128 x 64 (256 x 256:
+  // half the LDS bytes per MFMA for these deep-K shapes), 2 = 16 waves of 64 x 64 (256 x 256)
+  static const int seg_tile = [] {
+    const char* e = getenv("PDT_SEG_TILE");
+    return (e && e[0]) ? (int)strtol(e, nullptr, 10) : 0;
+  }();
+  const bool bst = bn_part != nullptr;
+  if (bst && !bn_mean) return -1;
+  if (N % 256 == 0 && seg_tile == 1) {
+    if (bst) return launch_nt<GXWide2, false, false, false, true>(a1, b, y, nullptr, nullptr, nullptr, M, K, N, bs, cg, s, nullptr, ap);
+    return launch_nt<GXWide2, false, false, false, false>(a1, b, y, nullptr, nullptr, nullptr, M, K, N, bs, cg, s, nullptr, ap);
+  }
+  if (N % 256 == 0 && seg_tile == 2) {
+    if (bst) return launch_nt<GXWide, false, false, false, true>(a1, b, y, nullptr, nullptr, nullptr, M, K, N, bs, cg, s, nullptr, ap);
+    return launch_nt<GXWide, false, false, false, false>(a1, b, y, nullptr, nullptr, nullptr, M, K, N, bs, cg, s, nullptr, ap);
+  }
+  if (bst) {
     if (N % 128 == 0) return launch_nt<GWide, false, false, false, true>(a1, b, y, nullptr, nullptr, nullptr, M, K, N, bs, cg, s, nullptr, ap);
     return launch_nt<GNarrow, false, false, false, true>(a1, b, y, nullptr, nullptr, nullptr, M, K, N, bs, cg, s, nullptr, ap);
   }

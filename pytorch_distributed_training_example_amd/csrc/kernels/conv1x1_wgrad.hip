@@ -295,9 +295,9 @@ __global__ __launch_bounds__(256) void conv1x1_wgrad_reduce_kernel(const float* 
 // Channel-block configurations (the block covers all of dW for ResNet-50's layer-1 shapes) x
 // pipeline variants (pixels per stage, ring depth; the ring is clamped to the 160 KB of LDS)
 enum class Blk { k64x64, k256x64, k64x256, k128x256, k128x128 };
-constexpr int kVariants = 4;
-constexpr int kVarKP[kVariants] = {32, 32, 64, 64};
-constexpr int kVarSlots[kVariants] = {4, 8, 4, 3};
+constexpr int kVariants = 5;
+constexpr int kVarKP[kVariants] = {32, 32, 64, 64, 32};
+constexpr int kVarSlots[kVariants] = {4, 8, 4, 3, 3};  // 4: a 3-slot ring, two 128x256 workgroups per CU (SEG A/B)
 
 template <Blk B, int V>
 struct CfgOf;
@@ -327,6 +327,7 @@ CfgInfo info_of() { return CfgInfo{Cf::CO_B, Cf::CI_B, Cf::kOcc, Cf::kKP}; }
 template <Blk B>
 CfgInfo info_var(int v) {
   switch (v) {
+    case 4: return info_of<typename CfgOf<B, 4>::T>();
     case 1: return info_of<typename CfgOf<B, 1>::T>();
     case 2: return info_of<typename CfgOf<B, 2>::T>();
     case 3: return info_of<typename CfgOf<B, 3>::T>();
@@ -368,6 +369,16 @@ inline Blk pick_block_seg(int co1, int co2, int Ci) {
   return Blk::k64x64;
 }
 
+// SEG pipeline variant (PDT_WGRAD_SEG_VARIANT, A/B; -1 = the shape default)
+inline int seg_variant() {
+  static const int v = [] {
+    const char* e = getenv("PDT_WGRAD_SEG_VARIANT");
+    const int x = (e && e[0]) ? (int)strtol(e, nullptr, 10) : -1;
+    return x >= -1 && x < kVariants ? x : -1;
+  }();
+  return v;
+}
+
 inline bool geo_of(int M, int Ci, int Co, W1Geo& g, int seg_co1 = 0, int seg_co2 = 0) {
   if (M < 1 || Ci % 64 != 0 || Co % 64 != 0) return false;
   const Blk b = seg_co1 ? pick_block_seg(seg_co1, seg_co2, Ci) : pick_block(Co, Ci);
@@ -376,7 +387,8 @@ inline bool geo_of(int M, int Ci, int Co, W1Geo& g, int seg_co1 = 0, int seg_co2
     Co = seg_co1 + seg_co2 + i0.cob;
   }
   g.dy2 = nullptr; g.co1 = seg_co1; g.co2 = seg_co2;
-  const CfgInfo ci = info(b, g_variant >= 0 ? g_variant : variant_default(b));
+  const int var = seg_co1 && seg_variant() >= 0 ? seg_variant() : (g_variant >= 0 ? g_variant : variant_default(b));
+  const CfgInfo ci = info(b, var);
   g.M = M; g.Ci = Ci; g.Co = Co;
   g.ntiles = (M + ci.kp - 1) / ci.kp;
   g.nblk = (Co / ci.cob) * (Ci / ci.cib);
@@ -413,6 +425,7 @@ int launch(const uint16_t* x, const uint16_t* dy, void* dw, float* ws, const W1G
 template <Blk B, bool F32 = false>
 int launch_var(int v, const uint16_t* x, const uint16_t* dy, void* dw, float* ws, const W1Geo& g, hipStream_t s) {
   switch (v) {
+    case 4: return launch<typename CfgOf<B, 4>::T, F32>(x, dy, dw, ws, g, s);
     case 1: return launch<typename CfgOf<B, 1>::T, F32>(x, dy, dw, ws, g, s);
     case 2: return launch<typename CfgOf<B, 2>::T, F32>(x, dy, dw, ws, g, s);
     case 3: return launch<typename CfgOf<B, 3>::T, F32>(x, dy, dw, ws, g, s);
@@ -469,7 +482,7 @@ int pdt_conv1x1_wgrad_seg(const uint16_t* x, const uint16_t* dy1, int co1, const
   if (co1 < 64 || co2 < 64 || !dy2 || !geo_of(M, Ci, co1 + co2 + 64, g, co1, co2)) return -1;
   g.dy2 = dy2;
   const Blk b = pick_block_seg(co1, co2, Ci);
-  const int v = g_variant >= 0 ? g_variant : variant_default(b);
+  const int v = seg_variant() >= 0 ? seg_variant() : (g_variant >= 0 ? g_variant : variant_default(b));
   switch (b) {
     case Blk::k128x256: return launch_var<Blk::k128x256, true>(v, x, dy1, out, ws, g, s);
     case Blk::k128x128: return launch_var<Blk::k128x128, true>(v, x, dy1, out, ws, g, s);
