@@ -373,8 +373,10 @@ inline Blk pick_block_seg(int co1, int co2, int Ci) {
 inline int seg_variant() {
   static const int v = [] {
     const char* e = getenv("PDT_WGRAD_SEG_VARIANT");
-    const int x = (e && e[0]) ? (int)strtol(e, nullptr, 10) : -1;
-    return x >= -1 && x < kVariants ? x : -1;
+    // default 4 (a 3-slot ring: two 128 x 256 workgroups per CU): 1.08-1.13x variant 0 at ResNet-50's layer 2-4
+    // shapes (tools/alg_bench.py, profiles/r6/alg_kernels_bench.txt)
+    const int x = (e && e[0]) ? (int)strtol(e, nullptr, 10) : 4;
+    return x >= -1 && x < kVariants ? x : 4;
   }();
   return v;
 }

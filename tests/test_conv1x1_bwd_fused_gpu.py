@@ -179,6 +179,7 @@ def test_resnet50_grads_fused_vs_unfused(switch, defer):
         calls.append(r is not None)
         return r
     conv_ops._bwd_fused = spy
+    switch("PDT_BWD_ALG", "0")  # layers 3-4 on the unfused chain both ways (the ALG path: test_bwd_alg_gpu.py)
     try:
         switch("PDT_BWD_FUSED", "1")
         switch("PDT_BWD_FUSED_SHAPES", "256x64,512x128")  # layer 2 too (off by default since round 5)
