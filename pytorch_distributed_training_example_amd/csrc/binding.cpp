@@ -156,7 +156,7 @@ void pdt_conv1x1_wgrad_tune(int target_wgs, int variant, int interleave);
 int pdt_conv1x1_gemm(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t* c, const uint8_t* cm,
                      float* part, int M, int K, int N, const uint16_t* bn_x, const uint8_t* bn_mask,
                      const float* bn_mean, float* bn_part, int c_s, int c_H, int c_W, const float* acoef,
-                     hipStream_t s);
+                     hipStream_t s, int nostore);
 void pdt_conv1x1_probe(int probe);
 int pdt_conv1x1_persist(int mode);
 int pdt_conv3x3_opt(int v);
@@ -948,7 +948,7 @@ c10::optional<Tensor> conv1x1_gemm(Tensor a, Tensor b, Tensor out, bool acc, boo
                                    c10::optional<Tensor> c_in, c10::optional<Tensor> c_mask,
                                    c10::optional<Tensor> bn_x, c10::optional<Tensor> bn_mask,
                                    c10::optional<Tensor> bn_mean, int64_t c_stride, int64_t c_H, int64_t c_W,
-                                   c10::optional<Tensor> a_coef, bool bn_sum_only) {
+                                   c10::optional<Tensor> a_coef, bool bn_sum_only, bool no_store) {
   for (const Tensor* t : {&a, &b, &out}) {
     check_cuda(*t, "conv1x1_gemm operand");
     TORCH_CHECK(t->scalar_type() == at::kBFloat16 && t->dim() == 2 && t->is_contiguous(),
@@ -1019,7 +1019,7 @@ c10::optional<Tensor> conv1x1_gemm(Tensor a, Tensor b, Tensor out, bool acc, boo
                                   reinterpret_cast<uint16_t*>(out.data_ptr()), cp, mp,
                                   stats ? part->data_ptr<float>() : nullptr, (int)M, (int)K, (int)N, bx, bm, bmean,
                                   bstats ? part->data_ptr<float>() : nullptr, (int)c_stride, (int)c_H, (int)c_W, acp,
-                                  stream());
+                                  stream(), no_store ? 1 : 0);
   TORCH_CHECK(rc == 0, "pdt_conv1x1_gemm failed: ", rc);
   return part;
 }
@@ -2315,7 +2315,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv1x1_gemm", &conv1x1_gemm, py::arg("a"), py::arg("b"), py::arg("out"), py::arg("acc"), py::arg("stats"),
         py::arg("c_in") = py::none(), py::arg("c_mask") = py::none(), py::arg("bn_x") = py::none(),
         py::arg("bn_mask") = py::none(), py::arg("bn_mean") = py::none(), py::arg("c_stride") = 0,
-        py::arg("c_H") = 0, py::arg("c_W") = 0, py::arg("a_coef") = py::none(), py::arg("bn_sum_only") = false);
+        py::arg("c_H") = 0, py::arg("c_W") = 0, py::arg("a_coef") = py::none(), py::arg("bn_sum_only") = false,
+        py::arg("no_store") = false);
   m.def("conv1x1_probe", [](int probe) { pdt_conv1x1_probe(probe); });
   m.def("conv1x1_persist", [](int mode) { return pdt_conv1x1_persist(mode); },
         "1x1 GEMM persistence mode (0 off, 1 measured kinds, 2 all, -1 env default); returns the previous mode");

@@ -136,6 +136,9 @@ struct ApArgs {
   // per-column bias (B's columns there); a repeated a2 segment meets a hi / lo split of its B block.
   const uint16_t* a2;
   int k1, k2, rep2;
+  // nostore (STATS forward): the statistics only, Y is not written (ops/conv.py: a bottleneck conv3 whose output
+  // is consumed only by its BatchNorm's statistics and its recomputed APPLY GEMM, and never by the backward)
+  int nostore;
 };
 
 int g_probe = 0;
@@ -420,7 +423,7 @@ __global__ __launch_bounds__(Cf::kThreads, Cf::kMinWaves) void conv1x1_kernel(
     if constexpr (APPLY) {
       if (!(probe & 32)) ap.mask[off >> 3] = (uint8_t)amb;
     }
-    if (probe & 1) continue;
+    if ((probe & 1) || ap.nostore) continue;
     if constexpr (NT) {
       const u32x4 t = {v.x, v.y, v.z, v.w};
       __builtin_nontemporal_store(t, reinterpret_cast<u32x4*>(Y + off));
@@ -762,7 +765,7 @@ __global__ __launch_bounds__(Cf::kThreads, PL<Cf>::kMinWaves) void conv1x1p_kern
             if (ok) rs8_add(rst, v);
           }
           // every thread stores every row (past M: the sink) so the vmcnt counts above are exact
-          uint4* yp = ok ? reinterpret_cast<uint4*>(Y + off) : g_gemm_sink + tid;
+          uint4* yp = ok && !ap.nostore ? reinterpret_cast<uint4*>(Y + off) : g_gemm_sink + tid;
           *yp = v;
           if constexpr (APPLY) {
             uint8_t* mp = ok ? ap.mask + (off >> 3) : g_mask_sink + tid;
@@ -864,12 +867,13 @@ int launch_nt(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t*
 
 template <class Cf, bool ACC, bool STATS, bool BSTATS = false>
 int launch(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t* c, const uint8_t* cm, float* part, int M,
-           int K, int N, const BnSrc& bs, const CGeom& cg, hipStream_t s) {
+           int K, int N, const BnSrc& bs, const CGeom& cg, hipStream_t s, const ApArgs& ap = ApArgs{}) {
   if constexpr (ACC)
-    if (cg.s) return launch_nt<Cf, ACC, STATS, false, BSTATS, false, false, true>(a, b, y, c, cm, part, M, K, N, bs, cg, s);
+    if (cg.s) return launch_nt<Cf, ACC, STATS, false, BSTATS, false, false, true>(a, b, y, c, cm, part, M, K, N, bs, cg, s,
+                                                                                  nullptr, ap);
   // (non-temporal output stores, NT = true, measured no gain: default-policy stores keep the
   // output in L2 for the consuming BatchNorm)
-  return launch_nt<Cf, ACC, STATS, false, BSTATS>(a, b, y, c, cm, part, M, K, N, bs, cg, s);
+  return launch_nt<Cf, ACC, STATS, false, BSTATS>(a, b, y, c, cm, part, M, K, N, bs, cg, s, nullptr, ap);
 }
 
 using GXWide = G1<256, 4, 4>;  // N % 256 == 0 (large M): 16 waves of 64x64, a block writes whole 512-B rows
@@ -888,7 +892,8 @@ inline bool w2_on() {
 
 template <class Cf>
 int dispatch(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t* c, const uint8_t* cm, float* part,
-             int M, int K, int N, const BnSrc& bs, const CGeom& cg, hipStream_t s, const float* acoef = nullptr) {
+             int M, int K, int N, const BnSrc& bs, const CGeom& cg, hipStream_t s, const float* acoef = nullptr,
+             const ApArgs& ap = ApArgs{}) {
   if ((c && part) || (cm && !c) || (part && bs.part) || (cg.s && (!c || cm))) return -1;  // not instantiated
   if (acoef) {  // forward with the producing BatchNorm's apply deferred here (+ statistics epilogue)
     if (c || bs.part) return -1;
@@ -901,7 +906,7 @@ int dispatch(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t* 
     return launch<Cf, false, false, true>(a, b, y, c, cm, part, M, K, N, bs, cg, s);
   }
   if (c) return launch<Cf, true, false>(a, b, y, c, cm, part, M, K, N, bs, cg, s);
-  if (part) return launch<Cf, false, true>(a, b, y, c, cm, part, M, K, N, bs, cg, s);
+  if (part) return launch<Cf, false, true>(a, b, y, c, cm, part, M, K, N, bs, cg, s, ap);
   return launch<Cf, false, false>(a, b, y, c, cm, part, M, K, N, bs, cg, s);
 }
 
@@ -934,7 +939,10 @@ int pdt_conv1x1_persist(int mode) {
 int pdt_conv1x1_gemm(const uint16_t* a, const uint16_t* b, uint16_t* y, const uint16_t* c, const uint8_t* cm,
                      float* part, int M, int K, int N, const uint16_t* bn_x, const uint8_t* bn_mask,
                      const float* bn_mean, float* bn_part, int c_s, int c_H, int c_W, const float* acoef,
-                     hipStream_t s) {
+                     hipStream_t s, int nostore) {
+  ApArgs ap{};
+  ap.nostore = nostore && part && !c && !acoef && !bn_part ? 1 : 0;  // statistics-only forward (see ApArgs)
+  if (nostore && !ap.nostore) return -1;
   if (M < 1 || K < 32 || K % 32 != 0 || N < 64 || N % 64 != 0) return -1;
   if ((int64_t)M * (K > N ? K : N) >= ((int64_t)1 << 31) || (int64_t)N * K >= ((int64_t)1 << 31)) return -2;
   const BnSrc bs{bn_x, bn_mask, bn_mean, bn_part};
@@ -950,12 +958,12 @@ int pdt_conv1x1_gemm(const uint16_t* a, const uint16_t* b, uint16_t* y, const ui
   // source — with the ATR operand transform or an accumulate source the 8-wave tile, two workgroups per
   // CU, ran 5-10 % faster at every ResNet-50 depth: profiles/r5/conv1x1_tiles_bench_b1024.txt)
   if (w2_on() && N % 256 == 0 && K >= 256 && !c && !acoef && !bs.part && !(g_probe & 64))
-    return dispatch<GXWide2>(a, b, y, c, cm, part, M, K, N, bs, cg, s, acoef);
+    return dispatch<GXWide2>(a, b, y, c, cm, part, M, K, N, bs, cg, s, acoef, ap);
   if (N % 256 == 0 && (int64_t)((M + 255) / 256) * (N / 256) >= 2048 && !(g_probe & 64) && !c && !acoef)
-    return dispatch<GXWide>(a, b, y, c, cm, part, M, K, N, bs, cg, s, acoef);
+    return dispatch<GXWide>(a, b, y, c, cm, part, M, K, N, bs, cg, s, acoef, ap);
   if (N % 128 == 0 && !(g_probe & 8) && !small_grid_narrow((int64_t)((M + 255) / 256) * (N / 128)))
-    return dispatch<GWide>(a, b, y, c, cm, part, M, K, N, bs, cg, s, acoef);
-  return dispatch<GNarrow>(a, b, y, c, cm, part, M, K, N, bs, cg, s, acoef);
+    return dispatch<GWide>(a, b, y, c, cm, part, M, K, N, bs, cg, s, acoef, ap);
+  return dispatch<GNarrow>(a, b, y, c, cm, part, M, K, N, bs, cg, s, acoef, ap);
 }
 
 // SEG: y[M,N] = [a1 | a2 (x rep2) | 1] [M, k1 + rep2 k2 + 32] * b[N, k1 + rep2 k2 + 32]^T, with the BSTATS

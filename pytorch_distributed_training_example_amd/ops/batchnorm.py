@@ -137,10 +137,11 @@ class DeferredBNGrad:
     backward (csrc/kernels/conv1x1_bwd_fused.hip) forms dx while loading it, so the BatchNorm's apply
     pass — a read of (dy, x, mask) and a write of dx, then two re-reads of dx — never runs."""
 
-    __slots__ = ("dy", "x", "mask", "mean", "coef", "dy_masked", "wg")
+    __slots__ = ("dy", "x", "mask", "mean", "coef", "dy_masked", "wg", "virt")
 
-    def __init__(self, dy, x, mask, mean, coef, dy_masked: bool = False, wg=None):
+    def __init__(self, dy, x, mask, mean, coef, dy_masked: bool = False, wg=None, virt=None):
         self.dy, self.x, self.mask, self.mean, self.coef = dy, x, mask, mean, coef
+        self.virt = virt  # (conv input, weight) when x was never written (PDT_Z3_VIRTUAL, ops/conv.py)
         # dy_masked: dy already equals dy * m (no mask, or the producing kernel stored it masked): the ALG
         # backward (ops/conv.py _bwd_alg) then uses dy directly as the GEMM operand g
         self.dy_masked = dy_masked
@@ -184,6 +185,14 @@ class _BNTrainFn(torch.autograd.Function):
                 gemm=None):
         C = native()
         ctx.defer_relu = defer_relu
+        # x may be a statistics-only conv output (never written, PDT_Z3_VIRTUAL): only the APPLY GEMM path below and
+        # the ALG backward may leave it unwritten; any other use recomputes it first (ops/conv.py materialize_virtual)
+        virt = getattr(x, "_pdt_virtual", None)
+        if virt is not None and not (defer_relu is None and defer is None and gemm is not None and part is not None
+                                     and residual is not None and relu):
+            from .conv import materialize_virtual
+            materialize_virtual(x, virt)
+            x._pdt_virtual = virt = None
         if defer_relu is not None:  # stats only; the consumer conv applies relu(a x + b) (DeferredReLUBN)
             if part is not None:
                 _, _, mean, invstd, ab = C.bn_fwd_train_tiles(x, part, None, weight, bias, running_mean,
@@ -239,6 +248,12 @@ class _BNTrainFn(torch.autograd.Function):
             # PDT_BWD_ALG=2: the consumer takes sum(dz) only; this backward completes the reduction (ALG prelude)
             gsrc.sum_only = bool(SW.bwd_alg >= 2 and ctx.out_link is not None and ctx.out_link.needs_masked
                                  and relu)
+        if virt is not None and not (gsrc is not None and gsrc.sum_only):
+            # the consumer's backward epilogue would read x for this BN's reduction: write it after all
+            from .conv import materialize_virtual
+            materialize_virtual(x, virt)
+            x._pdt_virtual = virt = None
+        ctx.virt = virt
         # backward needs the BN input and a 1-bit ReLU mask, never the output y
         ctx.save_for_backward(x, mask if (relu and defer_relu is None) else None, weight, mean, invstd)
         return y
@@ -282,12 +297,19 @@ class _BNTrainFn(torch.autograd.Function):
             return native().bn_bwd_train(dy, x, mask, weight, mean, invstd, relu, has_res, need_w)
 
         dy_masked = not ctx.relu or (part is not None and ctx.gsrc.masked)
-        if (ctx.out_link is not None and (not ctx.relu or mask is not None)
-                and (dy_masked or not ctx.out_link.needs_masked)):
+        defer_out = (ctx.out_link is not None and (not ctx.relu or mask is not None)
+                     and (dy_masked or not ctx.out_link.needs_masked))
+        if ctx.virt is not None and not (defer_out and part is not None):
+            # every remaining path reads x (its reduce pass or apply): recompute the unwritten conv output
+            from .conv import materialize_virtual
+            materialize_virtual(x, ctx.virt)
+            ctx.virt = None
+        if defer_out:
             # coefficients only: the producing conv's fused backward forms dx = A dy m + B (x - mean) + D
             coef, dg, db = native().bn_bwd_coef(dy, x, part, mask if ctx.relu else None, weight, mean, invstd,
                                                 ctx.relu, need_w)
-            ctx.out_link.grad = DeferredBNGrad(dy, x, mask if ctx.relu else None, mean, coef, dy_masked, alg_wg)
+            ctx.out_link.grad = DeferredBNGrad(dy, x, mask if ctx.relu else None, mean, coef, dy_masked, alg_wg,
+                                               ctx.virt)
             if ctx.has_res:  # lazy link (checked in forward): the shortcut gets (dy, mask) as before
                 ctx.link.grad = MaskedGrad(dy, mask) if ctx.relu else dy
             return (None, None, dg if need_w else None, db if need_w else None) + tail

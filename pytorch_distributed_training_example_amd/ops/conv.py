@@ -218,6 +218,16 @@ def gemm_source_of(z: torch.Tensor):
     return g if (g is not None and g.version == z._version) else None
 
 
+def materialize_virtual(z: torch.Tensor, src) -> torch.Tensor:
+    """Write a statistics-only conv output z (PDT_Z3_VIRTUAL: never stored) by running its GEMM; ``src`` =
+    (input, weight). Every consumer that reads z's values outside the APPLY GEMM calls this first."""
+    from ._native import native
+    a, w = src
+    Co, Ci = w.shape[:2]
+    native().conv1x1_gemm(_nhwc2d(a), w.reshape(Co, Ci).contiguous(), _nhwc2d(z), False, False)
+    return z
+
+
 def _attach_gemm_source(y, x, weight, acoef):
     if 0 < weight.shape[1] <= SW.bn_apply_gemm_k:
         y._pdt_gemm_src = GemmSource(x, weight, acoef, y._version)
@@ -310,9 +320,11 @@ def _nhwc2d(t: torch.Tensor) -> torch.Tensor:
 
 class _Conv1x1Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, link=None, stats_out=None, gsrc=None, bwd_link=None, dre=None):
+    def forward(ctx, x, weight, link=None, stats_out=None, gsrc=None, bwd_link=None, dre=None, nostore=False):
         """``dre``: x is the INPUT of a BatchNorm + ReLU whose apply is deferred to here
-        (ops/batchnorm.py DeferredReLUBN): the GEMM reads relu(a x + b) (our kernel, ATR)."""
+        (ops/batchnorm.py DeferredReLUBN): the GEMM reads relu(a x + b) (our kernel, ATR). ``nostore``: with
+        ``stats_out``, our GEMM takes the statistics only and y stays unwritten ("virtual": ``stats_out``
+        then gets a second entry, True)."""
         N, Ci, H, W = x.shape
         Co = weight.shape[0]
         x2 = _nhwc2d(x)
@@ -341,15 +353,18 @@ class _Conv1x1Fn(torch.autograd.Function):
         if x.dtype == torch.bfloat16 and _ours_ok("fwd", M, Ci, Co):
             from ._native import native
 
-            def ours(stats=False):
+            def ours(stats=False, no_store=False):
                 y = torch.empty((N, Co, H, W), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
-                return y, native().conv1x1_gemm(x2, w2.contiguous(), _nhwc2d(y), False, stats)
+                return y, native().conv1x1_gemm(x2, w2.contiguous(), _nhwc2d(y), False, stats, no_store=no_store)
             cands["ours"] = ours
         algo = _pick(("fwd", _dtype_name(x), M, Ci, Co), cands, fused=stats_out is not None)
         if algo == "ours":  # with the consuming BatchNorm's statistics in the epilogue
-            y, part = cands["ours"](stats_out is not None)
+            nostore = bool(nostore and stats_out is not None)
+            y, part = cands["ours"](stats_out is not None, nostore)
             if stats_out is not None:
                 stats_out.append(part)
+                if nostore:
+                    stats_out.append(True)
             return y
         if algo == "gemm":
             y = torch.mm(x2, w2.t()).view(N, H, W, Co).permute(0, 3, 1, 2)
@@ -362,12 +377,12 @@ class _Conv1x1Fn(torch.autograd.Function):
         x, weight = ctx.saved_tensors
         N, Ci, H, W = x.shape
         Co = weight.shape[0]
-        none7 = (None,) * 5
+        none7 = (None,) * 6
         if gy is None:  # the consuming BatchNorm handed its input gradient over (or there is none)
             d = ctx.bwd_link.take() if ctx.bwd_link is not None else None
             if d is None and ctx.link is not None:  # the partner branch still expects this one's gradient
                 gy = torch.zeros((N, Co, H, W), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
-                return _Conv1x1Fn._backward_dense(ctx, gy, x, weight) + (None,) * 5
+                return _Conv1x1Fn._backward_dense(ctx, gy, x, weight) + (None,) * 6
             if d is None:
                 return (None, None) + none7
             r = _bwd_fused(ctx, d, x, weight)
@@ -375,13 +390,15 @@ class _Conv1x1Fn(torch.autograd.Function):
                 r = _bwd_alg(ctx, d, x, weight)
             if r is not None:
                 return (r[0], r[1]) + none7
+            if d.virt is not None:  # the BatchNorm input was never written (PDT_Z3_VIRTUAL): recompute it
+                materialize_virtual(d.x, d.virt)
             gy = d.materialize()
         if ctx.dre is not None:  # fallback: materialise the deferred operand and its ReLU bits
             xa, bits = ctx.dre.materialize_parts()
             ctx.dre.mask.copy_(bits)
             r = _Conv1x1Fn._backward_dense(ctx, gy, xa, weight)
-            return r + (None,) * 5
-        return _Conv1x1Fn._backward_dense(ctx, gy, x, weight) + (None,) * 5
+            return r + (None,) * 6
+        return _Conv1x1Fn._backward_dense(ctx, gy, x, weight) + (None,) * 6
 
     @staticmethod
     def _backward_dense(ctx, gy, x, weight):
@@ -1046,12 +1063,21 @@ class Conv1x1(nn.Conv2d):
             holder = [] if (self.emit_bn_stats and self.training and torch.is_grad_enabled()
                             and SW.conv_bn_stats) else None
             from .batchnorm import grad_stats_source_of
+            # a bottleneck conv3 on the ALG backward (PDT_BWD_ALG=2): its output z is needed only for the consuming
+            # BatchNorm's statistics (this GEMM's epilogue) and its apply, which runs as this GEMM again (APPLY
+            # epilogue) — so z is never written (PDT_Z3_VIRTUAL; materialize_virtual recomputes it on a fallback)
+            virt = (holder is not None and bwd_link is not None and bwd_link.needs_masked and SW.bwd_alg >= 2
+                    and SW.z3_virtual and x.dtype == torch.bfloat16)
             y = _Conv1x1Fn.apply(x, self.weight, res_link, holder,
                                  grad_stats_source_of(x) if self.training and torch.is_grad_enabled() else None,
-                                 bwd_link)
+                                 bwd_link, None, virt)
             if holder:  # (our GEMM ran: the statistics came from its epilogue)
                 y._pdt_bn_stats = BNStats(holder[0], y._version)
-                _attach_gemm_source(y, x, self.weight, None)
+                if virt and len(holder) > 1:  # the store was skipped: only the APPLY GEMM may consume z
+                    y._pdt_virtual = (x, self.weight)
+                    y._pdt_gemm_src = GemmSource(x, self.weight, None, y._version)
+                else:
+                    _attach_gemm_source(y, x, self.weight, None)
             return y
         if self.strided_gemm_eligible(x):
             holder = [] if (self.emit_bn_stats and self.training and torch.is_grad_enabled()

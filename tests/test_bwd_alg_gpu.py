@@ -216,3 +216,18 @@ def test_small_gemm_and_fix_s2(C4, CW):
     zf = a.double() @ w.double().t()  # the conv's unrounded output: what z = a W^T gives the identity
     want = (g.double() * (zf - mean.double())).sum(0)
     torch.testing.assert_close(part[1].double().sum(0), want, rtol=1e-3, atol=1e-2)
+
+
+@pytest.mark.parametrize("gap_native", ["1", "0"])
+def test_unwritten_conv3_output_matches_written(switch, gap_native):
+    """PDT_Z3_VIRTUAL: layer 2-4 conv3 outputs are never written (statistics-only GEMM, bn3 applied by the GEMM
+    again). The step's gradients equal the run that writes them bit for bit — including, with the global-average-
+    pool kernel off (its gradient arrives unmasked, so the last block leaves the ALG path), the fallback that
+    recomputes the unwritten output (ops/conv.py materialize_virtual)."""
+    switch("PDT_GAP_NATIVE", gap_native)
+    switch("PDT_Z3_VIRTUAL", "1")
+    ga = _grads(seed=5)
+    switch("PDT_Z3_VIRTUAL", "0")
+    gb = _grads(seed=5)
+    bad = [k for k in gb if not torch.equal(ga[k], gb[k])]
+    assert not bad, bad[:8]
