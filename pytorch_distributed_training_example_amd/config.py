@@ -46,7 +46,7 @@ PDT_BWD_ALG                 2            bottleneck conv3 + bn3 backward (the sh
                                          bn3's apply pass: z = a W^T substituted into bn3's backward (ops/conv.py
                                          _bwd_alg, csrc/kernels/bn_alg.hip): one wgrad pass + one data-gradient GEMM;
                                          2: also bn3's backward reduction without reading z (sum-only producer)
-PDT_Z3_VIRTUAL              1            with PDT_BWD_ALG=2: a bottleneck conv3's output (bn3's input) is never written —
+PDT_Z3_VIRTUAL              0            1 (with PDT_BWD_ALG=2): a bottleneck conv3 output (bn3 input) is never written —
                                          statistics-only GEMM, bn3's apply as the GEMM again (APPLY epilogue)
 PDT_BN2_DEFER               0            1: with PDT_BWD_FUSED, bn2's apply + ReLU deferred into conv3 (read on load
                                          in the forward GEMM, recomputed in the fused backward, which writes bn2's
@@ -132,7 +132,7 @@ class _Switches:
         self.bwd_alg = int(e("PDT_BWD_ALG", "2"))
         # bottleneck conv3 on the ALG backward: z (bn3's input) never written — statistics-only GEMM, bn3 applied by
         # the GEMM again (APPLY epilogue); recomputed only on a fallback (ops/conv.py materialize_virtual)
-        self.z3_virtual = on("PDT_Z3_VIRTUAL")
+        self.z3_virtual = on("PDT_Z3_VIRTUAL", "0")
         self.bn2_defer = on("PDT_BN2_DEFER", "0")
         self.bn_apply_gemm_k = int(e("PDT_BN_APPLY_GEMM_K", "64"))
         self.strided_bstats = on("PDT_STRIDED_BSTATS")
