@@ -105,6 +105,10 @@ def _ours(x: torch.Tensor, w: torch.Tensor, kind: str = "bias", b: Optional[torc
     if c is None:
         _lin_table()
         c = _LIN_CHOICE.get(key)
+    if c is None and kind == "gelu":
+        # the fused fc1 + bias + GELU kind changes the backward too (bias_gelu_bwd from h): a forward-only timing
+        # picked it on GPT-2-medium and the step lost 3.7 % — only a table entry selects it
+        c = _LIN_CHOICE[key] = "lib"
     if c is None:
         if torch.cuda.is_current_stream_capturing():
             return False
