@@ -1211,7 +1211,8 @@ std::vector<Tensor> bn_alg_assemble(Tensor w, Tensor coef, Tensor mean, Tensor G
   const int64_t C4 = w.size(0), CW = w.size(1);
   TORCH_CHECK(coef.scalar_type() == at::kFloat && coef.numel() == 3 * C4 && mean.scalar_type() == at::kFloat &&
                   mean.numel() == C4 && G.scalar_type() == at::kFloat && G.numel() == (C4 / 128) * CW * CW &&
-                  BWG.scalar_type() == at::kFloat && BWG.numel() == (CW / 128) * C4 * CW && wg.scalar_type() == at::kFloat &&
+                  BWG.scalar_type() == at::kFloat && BWG.numel() == std::max<int64_t>(1, CW / 128) * C4 * CW &&
+                  wg.scalar_type() == at::kFloat &&
                   wg.dim() == 2 && wg.size(1) == CW && wg.size(0) > C4 + CW,
               "bn_alg_assemble: operand shapes");
   auto bcat = at::empty({CW, C4 + 2 * CW + 32}, w.options());
@@ -1235,10 +1236,10 @@ std::vector<Tensor> bn_alg_small_gemm(Tensor w, Tensor coef, Tensor wg) {
                   wg.scalar_type() == at::kFloat && wg.is_contiguous() && wg.dim() == 2 && wg.size(1) == CW &&
                   wg.size(0) >= C4 + CW && C4 % 64 == 0 && CW % 64 == 0,
               "bn_alg_small_gemm: coef [3, C4], wg [>= C4 + CW, CW] fp32, C4 / CW % 64");
-  TORCH_CHECK(C4 % 128 == 0 && CW % 128 == 0, "bn_alg_small_gemm: C4, CW % 128");
-  // split-K slices (summed by bn_alg_assemble): G [C4 / 128, CW, CW], BWG [CW / 128, C4, CW]
+  TORCH_CHECK(C4 % 128 == 0 && (CW == 64 || CW % 128 == 0), "bn_alg_small_gemm: C4 % 128, CW 64 or % 128");
+  // split-K slices (summed by bn_alg_assemble): G [C4 / 128, CW, CW], BWG [max(1, CW / 128), C4, CW]
   auto G = at::empty({C4 / 128, CW, CW}, wg.options());
-  auto BWG = at::empty({CW / 128, C4, CW}, wg.options());
+  auto BWG = at::empty({std::max<int64_t>(1, CW / 128), C4, CW}, wg.options());
   TORCH_CHECK(pdt_bn_alg_small_gemm(reinterpret_cast<const uint16_t*>(w.data_ptr()), coef.data_ptr<float>(),
                                     wg.data_ptr<float>(), G.data_ptr<float>(), BWG.data_ptr<float>(), (int)C4, (int)CW,
                                     stream()) == 0,

@@ -24,6 +24,9 @@ namespace {
 __device__ __forceinline__ float bfv(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
 
 constexpr int kSK = 128;  // K rows per split-K slice of the small products (bn_alg_small_gemm_kernel)
+// BWG's K is CW: one 64-row slice when CW == 64 (ResNet layer 1), 128-row slices otherwise
+__host__ __device__ __forceinline__ int bwg_len(int CW) { return CW < kSK ? CW : kSK; }
+__host__ __device__ __forceinline__ int bwg_slices(int CW) { return CW / bwg_len(CW); }
 
 // blocks [0, CW): row k of b; blocks [CW, ...): 256-element slices of dW
 __global__ __launch_bounds__(256) void bn_alg_assemble_kernel(const uint16_t* __restrict__ W, const float* __restrict__ coef,
@@ -66,7 +69,7 @@ __global__ __launch_bounds__(256) void bn_alg_assemble_kernel(const uint16_t* __
   const float S = wg[(int64_t)(C4 + CW) * CW + k];  // first row of the ones block: column sums of a
   const float E = D[c] - Bc[c] * mean[c];
   float bwg = 0.f;
-  for (int sl = 0; sl < CW / kSK; ++sl) bwg += BWG[(int64_t)sl * C4 * CW + e];
+  for (int sl = 0; sl < bwg_slices(CW); ++sl) bwg += BWG[(int64_t)sl * C4 * CW + e];
   dW[e] = f2bf(A[c] * wg[e] + bwg + E * S);
 }
 
@@ -101,8 +104,9 @@ __global__ __launch_bounds__(256) void bn_alg_small_gemm_kernel(const uint16_t* 
   const int tcw = CW / 64, nG = tcw * tcw;
   const int t = blockIdx.x, sl = blockIdx.y;
   const bool isG = t < nG;
-  if (isG ? sl >= C4 / kSK : sl >= CW / kSK) return;
-  const int k0 = sl * kSK;
+  if (isG ? sl >= C4 / kSK : sl >= bwg_slices(CW)) return;
+  const int klen = isG ? kSK : bwg_len(CW);
+  const int k0 = sl * klen;
   const float* Gram = wg + (int64_t)C4 * CW;
   int i0, j0;
   if (isG) { i0 = (t / tcw) * 64; j0 = (t % tcw) * 64; }
@@ -127,7 +131,7 @@ __global__ __launch_bounds__(256) void bn_alg_small_gemm_kernel(const uint16_t* 
   };
   float acc[4][4] = {};
   load(k0);
-  for (int kk = k0; kk < k0 + kSK; kk += 16) {
+  for (int kk = k0; kk < k0 + klen; kk += 16) {
     __syncthreads();
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -137,7 +141,7 @@ __global__ __launch_bounds__(256) void bn_alg_small_gemm_kernel(const uint16_t* 
       sb[e >> 6][e & 63] = rb[u];
     }
     __syncthreads();
-    if (kk + 16 < k0 + kSK) load(kk + 16);
+    if (kk + 16 < k0 + klen) load(kk + 16);
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const float4 av = *reinterpret_cast<const float4*>(&sa[r][ty * 4]);
@@ -179,13 +183,13 @@ int pdt_bn_alg_fix_s2(float* part, int T, const float* wg, const uint16_t* W, in
   return 0;
 }
 
-// Gp [C4 / 128, CW, CW] and Bp [CW / 128, C4, CW] fp32 split-K slices (see bn_alg_small_gemm_kernel);
-// C4, CW % 128 == 0.
+// Gp [C4 / 128, CW, CW] and Bp [max(1, CW / 128), C4, CW] fp32 split-K slices (see bn_alg_small_gemm_kernel);
+// C4 % 128 == 0, CW == 64 or CW % 128 == 0.
 int pdt_bn_alg_small_gemm(const uint16_t* W, const float* coef, const float* wg, float* G, float* BWG, int C4, int CW,
                           hipStream_t s) {
-  if (C4 % kSK || CW % kSK) return -1;
+  if (C4 % kSK || CW % 64 || (CW > 64 && CW % kSK)) return -1;
   const int tcw = CW / 64;
-  const int sy = C4 / kSK > CW / kSK ? C4 / kSK : CW / kSK;
+  const int sy = C4 / kSK > bwg_slices(CW) ? C4 / kSK : bwg_slices(CW);
   hipLaunchKernelGGL(bn_alg_small_gemm_kernel, dim3(tcw * tcw + (C4 / 64) * tcw, sy), dim3(256), 0, s, W, coef, wg, G,
                      BWG, C4, CW);
   return 0;

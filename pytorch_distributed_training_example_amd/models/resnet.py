@@ -135,8 +135,9 @@ class Bottleneck(nn.Module):
             ds_bn = self.downsample[1] if self.downsample is not None else None
             # conv3 + bn3 backward as one kernel: bn3 hands its input gradient to conv3 in deferred form
             # (or the ALG backward for the shapes the fused kernel does not take: ops/conv.py _bwd_alg)
-            fused3 = self.conv3.fused_bwd_ok(z2)
-            blink = BNGradLink(needs_masked=not fused3) if ((fused3 or self.conv3.alg_bwd_ok(z2)) and not self.bn3.has_hooks()
+            alg3 = self.conv3.alg_bwd_ok(z2)
+            fused3 = self.conv3.fused_bwd_ok(z2) and not (SW.bwd_alg_first and SW.bwd_alg >= 2 and alg3)
+            blink = BNGradLink(needs_masked=not fused3) if ((fused3 or alg3) and not self.bn3.has_hooks()
                                      and (link.lazy or (isinstance(ds_bn, BatchNorm2d) and DS_MASKED_GRAD[0]))) \
                 else None
             if (blink is not None and fused3 and SW.bn2_defer and isinstance(self.bn2, BatchNorm2d)

@@ -537,6 +537,8 @@ def _bwd_fused(ctx, d, x, weight):
     # linked (a downsample shortcut conv): only as the FIRST of the two branches — dx is deposited for
     # conv1's dgrad GEMM to accumulate into, so it is not final and takes no BatchNorm reduction
     linked = ctx.link is not None
+    if ctx.bwd_link is not None and ctx.bwd_link.needs_masked:
+        return None  # planned for the ALG backward (models/resnet.py)
     if not (SW.bwd_fused and (not linked or ctx.link.grad is None) and ctx.needs_input_grad[0]
             and ctx.needs_input_grad[1] and d.mask is not None and fused_bwd_shape_ok(weight)):
         return None
@@ -559,10 +561,12 @@ def _bwd_fused(ctx, d, x, weight):
 
 
 def alg_bwd_shape_ok(weight: torch.Tensor) -> bool:
-    """(Co, Ci) of a bottleneck conv3 whose backward ``_bwd_alg`` takes: Co (bn3's channels) and Ci multiples of
-    128 (the segment blocks of conv1x1_wgrad.hip / the GEMM's 128-wide tiles), bf16 1x1 weights."""
+    """(Co, Ci) of a bottleneck conv3 whose backward ``_bwd_alg`` takes: Co (bn3's channels) a multiple of 128, Ci 64
+    or a multiple of 128 (the segment blocks of conv1x1_wgrad.hip / the GEMM tiles), bf16 1x1 weights. (Layer 1's
+    256x64 conv3 takes the fused kernel first where PDT_BWD_FUSED_SHAPES lists it.)"""
     return (weight.dim() == 4 and tuple(weight.shape[2:]) == (1, 1) and weight.dtype == torch.bfloat16
-            and weight.shape[0] % 128 == 0 and weight.shape[1] % 128 == 0 and weight.shape[0] > weight.shape[1])
+            and weight.shape[0] % 128 == 0 and (weight.shape[1] == 64 or weight.shape[1] % 128 == 0)
+            and weight.shape[0] > weight.shape[1])
 
 
 def _bwd_alg(ctx, d, x, weight):

@@ -7,9 +7,10 @@ HBM rate (profiles/r1_steady_gpt2_medium_ours.md: 73 ``reduce_kernel`` calls, 1.
 
 Forward GEMMs on our MFMA kernel (csrc/kernels/gemm.hip: bias epilogue, and the MLP's fc1 + bias + GELU in
 one pass, ``linear_gelu``) are chosen PER SHAPE by measurement, as the 1x1 convs are (ops/conv.py _pick):
-``PDT_LINEAR_EPILOGUE=auto`` (default) looks the (kind, M, N, K) up in ``tuning/linear_gfx950.json``, and a
-shape not in the table is timed once (eager steps only; under hipGraph capture the library runs) against
-hipBLASLt (+ our standalone bias+GELU kernel for the fused kind) and the winner cached. Our kernel wins on
+``PDT_LINEAR_EPILOGUE=auto`` (default) looks the (kind, M, N, K) up in ``tuning/linear_gfx950.json`` (decided by
+whole-step A/B); a shape not in the table runs the library. ``=time`` times an unlisted shape once (eager steps
+only) against hipBLASLt (+ our bias+GELU kernel for the fused kind) and caches the winner — isolated timings
+mispredict the step (GPT-2-medium lost 3 % on them), hence not the default. Our kernel wins on
 some shapes only (vit_qkv 1.08x, vit_fc2 1.03x, gpt2_proj + bias 1.05x; 0.61-0.94x on the others:
 profiles/r5/gemm_bn128.txt, profiles/r3/gemm_vs_hipblaslt.md), so all-or-nothing would lose. ``=1``: ours
 on every shape it serves, ``=0``: never. ``PDT_LINEAR_DUMP=path`` writes the decisions at exit.
@@ -105,9 +106,9 @@ def _ours(x: torch.Tensor, w: torch.Tensor, kind: str = "bias", b: Optional[torc
     if c is None:
         _lin_table()
         c = _LIN_CHOICE.get(key)
-    if c is None and kind == "gelu":
-        # the fused fc1 + bias + GELU kind changes the backward too (bias_gelu_bwd from h): a forward-only timing
-        # picked it on GPT-2-medium and the step lost 3.7 % — only a table entry selects it
+    if c is None and mode != "time":
+        # a shape the table does not list runs the library: isolated forward timings picked ours for GPT-2-medium's
+        # qkv / fc1 / fused GELU and the whole step lost 3 % (tuning/linear_gfx950.json _note); "time" re-enables it
         c = _LIN_CHOICE[key] = "lib"
     if c is None:
         if torch.cuda.is_current_stream_capturing():
