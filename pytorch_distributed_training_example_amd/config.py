@@ -48,7 +48,7 @@ PDT_BWD_ALG                 2            bottleneck conv3 + bn3 backward (the sh
                                          2: also bn3's backward reduction without reading z (sum-only producer)
 PDT_Z3_VIRTUAL              0            1 (with PDT_BWD_ALG=2): a bottleneck conv3 output (bn3 input) is never written —
                                          statistics-only GEMM, bn3's apply as the GEMM again (APPLY epilogue)
-PDT_BWD_ALG_FIRST           0            1: the ALG backward also where PDT_BWD_FUSED would run (layer 1's conv3)
+PDT_BWD_ALG_FIRST           1            the ALG backward also where PDT_BWD_FUSED would run (layer 1's conv3)
 PDT_BN2_DEFER               0            1: with PDT_BWD_FUSED, bn2's apply + ReLU deferred into conv3 (read on load
                                          in the forward GEMM, recomputed in the fused backward, which writes bn2's
                                          mask). Measured -0.2 %, and -2 % with PDT_BN_APPLY_GEMM_K (the relu(a x + b)
@@ -135,7 +135,7 @@ class _Switches:
         # the GEMM again (APPLY epilogue); recomputed only on a fallback (ops/conv.py materialize_virtual)
         self.z3_virtual = on("PDT_Z3_VIRTUAL", "0")
         # the ALG backward also for the conv3 shapes the fused kernel takes (ResNet-50 layer 1: 256x64)
-        self.bwd_alg_first = on("PDT_BWD_ALG_FIRST", "0")
+        self.bwd_alg_first = on("PDT_BWD_ALG_FIRST", "1")
         self.bn2_defer = on("PDT_BN2_DEFER", "0")
         self.bn_apply_gemm_k = int(e("PDT_BN_APPLY_GEMM_K", "64"))
         self.strided_bstats = on("PDT_STRIDED_BSTATS")
