@@ -120,34 +120,62 @@ def test_global_avgpool_channels_last_grad():
     assert x.grad.is_contiguous(memory_format=torch.channels_last)
 
 
-def test_resnet50_fp32_native_matches_stock():
-    """fp32 ResNet-50 with native ops enabled against stock PyTorch (PDT_DISABLE_NATIVE): the same model.
-    Round 5 found the bottleneck's residual-gradient link taken in fp32, where only the bf16 BatchNorm
-    kernel deposits the shortcut gradient: conv1's branch gradient was dropped in every block and the
-    stem gradient came out 360x too small (tools/diag_oracle.py)."""
+def _r50_grads(dtype, native: bool, corrupt=None):
+    """ResNet-50 parameter gradients at 96 x 96, batch 8, in ``dtype`` with our native ops on or off. Each residual
+    branch's last BatchNorm starts at gamma = 0.2: a well-conditioned net (the default random init amplifies fp32
+    rounding to a 2 % gradient spread even between stock fp32 and fp64: profiles/r6/diag_oracle_fp64.txt)."""
     from pytorch_distributed_training_example_amd.config import SW
     from pytorch_distributed_training_example_amd.models import get_model
-
-    def grads(disable):
-        if disable:
-            os.environ["PDT_DISABLE_NATIVE"] = "1"
+    from pytorch_distributed_training_example_amd.models.resnet import Bottleneck
+    if not native:
+        os.environ["PDT_DISABLE_NATIVE"] = "1"
+    SW.reload()
+    try:
+        torch.manual_seed(0)
+        m = get_model("resnet50").cuda().to(memory_format=torch.channels_last).to(dtype)
+        for b in m.modules():
+            if isinstance(b, Bottleneck):
+                torch.nn.init.constant_(b.bn3.weight, 0.2)
+        g = torch.Generator(device="cuda").manual_seed(1)
+        x = torch.randn(8, 3, 96, 96, device="cuda", generator=g).to(dtype).contiguous(memory_format=torch.channels_last)
+        y = torch.randint(0, 1000, (8,), device="cuda", generator=g)
+        if corrupt is not None:
+            corrupt(m)
+        torch.nn.functional.cross_entropy(m(x), y).backward()
+        return {k: p.grad.double().clone() for k, p in m.named_parameters()}
+    finally:
+        os.environ.pop("PDT_DISABLE_NATIVE", None)
         SW.reload()
-        try:
-            torch.manual_seed(0)
-            m = get_model("resnet50").cuda().to(memory_format=torch.channels_last)
-            x = torch.randn(8, 3, 96, 96, device="cuda").contiguous(memory_format=torch.channels_last)
-            y = torch.randint(0, 1000, (8,), device="cuda")
-            torch.nn.functional.cross_entropy(m(x), y).backward()
-            return {k: p.grad.clone() for k, p in m.named_parameters()}
-        finally:
-            os.environ.pop("PDT_DISABLE_NATIVE", None)
-            SW.reload()
 
-    ga, gb = grads(False), grads(True)
-    e = torch.tensor([float((ga[k] - gb[k]).norm() / gb[k].norm().clamp_min(1e-12)) for k in gb])
-    ratio = float(ga["conv1.weight"].norm() / gb["conv1.weight"].norm())
-    assert 0.8 < ratio < 1.25, ratio
-    assert float(e.median()) < 0.05 and float(e.max()) < 0.5, (float(e.median()), float(e.max()))
+
+def _oracle_errors(g, g64):
+    big = max(float(v.norm()) for v in g64.values())
+    return {k: float((g[k] - v).norm() / v.norm()) for k, v in g64.items() if float(v.norm()) > 1e-6 * big}
+
+
+def check_fp32_native_against_fp64(corrupt=None):
+    """(passed, message): fp32 ResNet-50 with native ops on, against the fp64 gradient of the same model and batch
+    (stock PyTorch ops in float64 — no reduced-precision solver anywhere), next to stock fp32's own distance."""
+    g64 = _r50_grads(torch.float64, native=False)
+    en = _oracle_errors(_r50_grads(torch.float32, native=True, corrupt=corrupt), g64)
+    es = _oracle_errors(_r50_grads(torch.float32, native=False), g64)
+    worst = sorted(en, key=lambda k: -en[k])[:3]
+    msg = "worst native: " + ", ".join(f"{k} {en[k]:.2e} (stock {es[k]:.2e})" for k in worst)
+    med = sorted(en.values())[len(en) // 2]
+    # fp32 rounding (MIOpen's fp32 convolution solvers included: 1e-6 .. 6e-3 from fp64 on this stack, solver
+    # dependent) stays under 1e-2 per tensor; a wrong channel in one BatchNorm's backward or a dropped branch does
+    # not. Each tensor also within 2x (+ 2e-3) of stock fp32's distance on the same box.
+    ok = max(en.values()) < 1e-2 and med < 5e-3 and all(en[k] <= 2 * es[k] + 2e-3 for k in en)
+    return ok, f"median {med:.2e} max {max(en.values()):.2e}; {msg}"
+
+
+def test_resnet50_fp32_native_matches_fp64_oracle():
+    """fp32 ResNet-50 with native ops enabled, against fp64. Round 5 found the bottleneck's residual-gradient link
+    taken in fp32 (conv1's branch gradient dropped, the stem gradient 360x too small); the round-5 bound
+    (median 5 % / max 50 % against stock fp32) was mostly oracle noise of an ill-conditioned random init."""
+    ok, msg = check_fp32_native_against_fp64()
+    print(msg)
+    assert ok, msg
 
 
 def test_resnet50_frozen_bn3_keeps_conv1_branch_gradient():
