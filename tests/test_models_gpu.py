@@ -164,8 +164,10 @@ def check_fp32_native_against_fp64(corrupt=None):
     med = sorted(en.values())[len(en) // 2]
     # fp32 rounding (MIOpen's fp32 convolution solvers included: 1e-6 .. 6e-3 from fp64 on this stack, solver
     # dependent) stays under 1e-2 per tensor; a wrong channel in one BatchNorm's backward or a dropped branch does
-    # not. Each tensor also within 2x (+ 2e-3) of stock fp32's distance on the same box.
-    ok = max(en.values()) < 1e-2 and med < 5e-3 and all(en[k] <= 2 * es[k] + 2e-3 for k in en)
+    # not (measured: median 2.2e-2, max 5.7e-2 with one of 256 channels dropped — tools/oracle_negative_check.py,
+    # profiles/r6/oracle_negative_check.txt). Stock fp32's distance is reported, not bounded against: MIOpen picks
+    # its fp32 solver per process, so stock and native land at 5e-6 or at 5e-3 independently of each other.
+    ok = max(en.values()) < 1e-2 and med < 5e-3
     return ok, f"median {med:.2e} max {max(en.values()):.2e}; {msg}"
 
 
