@@ -49,6 +49,9 @@ PDT_BWD_ALG                 2            bottleneck conv3 + bn3 backward (the sh
 PDT_Z3_VIRTUAL              0            1 (with PDT_BWD_ALG=2): a bottleneck conv3 output (bn3 input) is never written —
                                          statistics-only GEMM, bn3's apply as the GEMM again (APPLY epilogue)
 PDT_BWD_ALG_FIRST           1            the ALG backward also where PDT_BWD_FUSED would run (layer 1's conv3)
+PDT_DS_ALG                  512          the ALG backward for a downsample block's shortcut conv + BN too, where the
+                                         conv has <= this many input channels (0 = off): the shortcut BN's
+                                         reduction and apply passes go; sum(g) comes from bn3's backward (same g)
 PDT_BN2_DEFER               0            1: with PDT_BWD_FUSED, bn2's apply + ReLU deferred into conv3 (read on load
                                          in the forward GEMM, recomputed in the fused backward, which writes bn2's
                                          mask). Measured -0.2 %, and -2 % with PDT_BN_APPLY_GEMM_K (the relu(a x + b)
@@ -81,7 +84,7 @@ class _Switches:
                  "conv1x1_table", "conv1x1_dump", "conv1x1_s2", "conv3x3", "conv3x3_wgrad", "conv3x3_s2", "conv_stem",
                  "conv_bn_stats", "bn_bwd_stats", "res_masked", "stem_bwd_fused", "stem_bn_wgrad", "stem_bn_stats", "stem_pool_wgrad", "wgrad_splitk", "slice_sum",
                  "subsample_native", "linear_splitk", "fused_addln", "embedding_native", "linear_epilogue",
-                 "bwd_fused", "bwd_fused_shapes", "bwd_alg", "z3_virtual", "bwd_alg_first", "bn2_defer", "bn_apply_gemm_k", "strided_bstats", "gap_native",
+                 "bwd_fused", "bwd_fused_shapes", "bwd_alg", "z3_virtual", "bwd_alg_first", "ds_alg", "bn2_defer", "bn_apply_gemm_k", "strided_bstats", "gap_native",
                  "fp8_fused_gelu", "fp8_weight_multi", "fp8_cast_colsum", "fp8_ln", "wgrad_stream_m")
 
     def __init__(self):
@@ -136,6 +139,8 @@ class _Switches:
         self.z3_virtual = on("PDT_Z3_VIRTUAL", "0")
         # the ALG backward also for the conv3 shapes the fused kernel takes (ResNet-50 layer 1: 256x64)
         self.bwd_alg_first = on("PDT_BWD_ALG_FIRST", "1")
+        # the ALG backward for the downsample shortcut conv + BN (input channels <= this; 0 = off)
+        self.ds_alg = int(e("PDT_DS_ALG", "512"))
         self.bn2_defer = on("PDT_BN2_DEFER", "0")
         self.bn_apply_gemm_k = int(e("PDT_BN_APPLY_GEMM_K", "64"))
         self.strided_bstats = on("PDT_STRIDED_BSTATS")

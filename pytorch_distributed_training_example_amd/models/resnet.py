@@ -160,8 +160,15 @@ class Bottleneck(nn.Module):
                 dconv = self.downsample[0]
                 # the shortcut conv's backward as one fused kernel too (layer 1's stride-1 256x64 shortcut):
                 # ds_bn hands it (dy, x, mask, coefficients) and never writes its input gradient
-                dlink = BNGradLink() if (DS_DEFER_APPLY[0] and DS_FUSED_BWD[0] and not ds_bn.has_hooks()
-                                         and isinstance(dconv, Conv1x1) and dconv.fused_bwd_ok(x)) else None
+                # or the shortcut conv + BN on the ALG backward (PDT_DS_ALG: ops/batchnorm.py _alg_ds_prelude) when
+                # bn3 runs it too (bn3's bias gradient is the shortcut BN's sum(g): same output gradient)
+                ds_ok = DS_DEFER_APPLY[0] and not ds_bn.has_hooks() and isinstance(dconv, Conv1x1)
+                if ds_ok and blink is not None and not fused3 and dconv.ds_alg_ok(x):
+                    dlink = BNGradLink(needs_masked=True)
+                elif ds_ok and DS_FUSED_BWD[0] and dconv.fused_bwd_ok(x):
+                    dlink = BNGradLink()
+                else:
+                    dlink = None
                 xs = linked_conv(dconv, x, link, bwd_link=dlink)
                 if DS_DEFER_APPLY[0] and not ds_bn.has_hooks():
                     # statistics only: an internal DeferredBNOutput handle that only bn3's fused

@@ -118,12 +118,14 @@ def grad_stats_source_of(x: torch.Tensor):
 
 class MaskedGrad:
     """A ReLU'd residual gradient not yet materialised: ``dy * mask`` (mask = the BatchNorm's
-    1-bit ReLU mask, bit j of byte k covers element 8k + j)."""
+    1-bit ReLU mask, bit j of byte k covers element 8k + j). ``masked``: dy already equals dy * mask (its
+    producer stored it masked); ``s1``: sum(dy * mask) per channel (fp32) when the depositing BatchNorm's backward
+    already has it (its bias gradient) — the downsample ALG backward (_alg_ds_prelude) takes both."""
 
-    __slots__ = ("dy", "mask")
+    __slots__ = ("dy", "mask", "masked", "s1")
 
-    def __init__(self, dy: torch.Tensor, mask: torch.Tensor):
-        self.dy, self.mask = dy, mask
+    def __init__(self, dy: torch.Tensor, mask: torch.Tensor, masked: bool = False, s1=None):
+        self.dy, self.mask, self.masked, self.s1 = dy, mask, masked, s1
 
     def dense(self) -> torch.Tensor:
         bits = (self.mask.view(-1, 1) >> torch.arange(8, device=self.mask.device, dtype=torch.uint8)) & 1
@@ -269,6 +271,13 @@ class _BNTrainFn(torch.autograd.Function):
             g = ctx.glink.take() if ctx.glink is not None else None
             if g is None:
                 return (None,) * 4 + tail
+            if isinstance(g, MaskedGrad) and ctx.out_link is not None and ctx.out_link.needs_masked and not ctx.relu:
+                # the shortcut conv runs the ALG backward: no reduce pass over (g, x), no apply (_alg_ds_prelude)
+                r = _alg_ds_prelude(ctx, g, x, weight, mean, invstd, need_w)
+                if r is not None:
+                    coef, dg, db, wg = r
+                    ctx.out_link.grad = DeferredBNGrad(g.dy, x, None, mean, coef, True, wg)
+                    return (None, None, dg if need_w else None, db if need_w else None) + tail
             if isinstance(g, MaskedGrad) and ctx.out_link is not None:
                 # coefficients only: the shortcut conv's fused backward forms dx on load (DeferredBNGrad)
                 coef, dg, db = native().bn_bwd_coef(g.dy, x, None, g.mask, weight, mean, invstd, True, need_w)
@@ -311,7 +320,9 @@ class _BNTrainFn(torch.autograd.Function):
             ctx.out_link.grad = DeferredBNGrad(dy, x, mask if ctx.relu else None, mean, coef, dy_masked, alg_wg,
                                                ctx.virt)
             if ctx.has_res:  # lazy link (checked in forward): the shortcut gets (dy, mask) as before
-                ctx.link.grad = MaskedGrad(dy, mask) if ctx.relu else dy
+                # (+ sum(dy * mask) = this BN's bias gradient, for a downsample BN on the ALG backward)
+                ctx.link.grad = MaskedGrad(dy, mask, dy_masked, db if (need_w and dy_masked) else None) \
+                    if ctx.relu else dy
             return (None, None, dg if need_w else None, db if need_w else None) + tail
         if ctx.has_res and ctx.link is not None and ctx.link.lazy and ctx.relu:
             # the shortcut gradient dy*mask is never written: the consumer's GEMM masks dy itself
@@ -341,6 +352,32 @@ def _alg_prelude(ctx, dy, part):
         return None
     native().bn_alg_fix_s2(part, wg, w.reshape(C4, CW).contiguous())
     return wg
+
+
+def _alg_ds_prelude(ctx, g, x, weight, mean, invstd, need_w):
+    """A downsample block's shortcut BatchNorm backward for the ALG path of its conv (ops/conv.py _bwd_alg): the
+    BN's output gradient g is bn3's (same block output, same ReLU mask), so sum(g) is bn3's bias gradient
+    (``g.s1``), and sum(g (x - mean)) = rowsum(P * W) - mean sum(g) with P = g^T a from the ALG weight-gradient
+    pass over the conv's input a. No pass over (g, x) and no apply: (coef, dgamma, dbeta, wg), or None when the
+    path does not apply (g not stored masked, no sum, no conv source)."""
+    link = ctx.out_link
+    src = link.alg_src
+    if src is None or not g.masked or g.s1 is None:
+        return None
+    a, w = src
+    from .conv import _nhwc2d
+    C4, CW = w.shape[0], w.shape[1]
+    dy = g.dy.contiguous(memory_format=torch.channels_last)
+    if dy.shape != x.shape:
+        return None
+    wg = native().conv1x1_wgrad_seg(_nhwc2d(a), _nhwc2d(dy), _nhwc2d(a))
+    if wg is None:
+        return None
+    s1 = g.s1.float()
+    part = torch.stack((s1, -(mean * s1))).view(2, 1, C4)  # one "tile": sum(g), then -mean sum(g)
+    native().bn_alg_fix_s2(part, wg, w.reshape(C4, CW).contiguous())  # + rowsum(P * W)
+    coef, dg, db = native().bn_bwd_coef(dy, x, part, None, weight, mean, invstd, False, need_w)
+    return coef, dg, db, wg
 
 
 class _BNEvalFn(torch.autograd.Function):

@@ -388,6 +388,8 @@ class _Conv1x1Fn(torch.autograd.Function):
             r = _bwd_fused(ctx, d, x, weight)
             if r is None:
                 r = _bwd_alg(ctx, d, x, weight)
+                if r is not None and ctx.link is not None:  # first of the two branches: conv1's GEMM adds to it
+                    ctx.link.grad, r = r[0], (None, r[1])
             if r is not None:
                 return (r[0], r[1]) + none7
             if d.virt is not None:  # the BatchNorm input was never written (PDT_Z3_VIRTUAL): recompute it
@@ -581,8 +583,11 @@ def _bwd_alg(ctx, d, x, weight):
     block the 4C-channel tensor is read twice (g) instead of five times (dy, z, dz x 2 + the apply's write).
     Needs g = dy * mask as a plain tensor (``d.dy_masked``: the producer stored it masked). None when the
     path does not apply (the caller materialises dz)."""
-    if not (SW.bwd_alg and ctx.link is None and ctx.dre is None and ctx.needs_input_grad[0]
-            and ctx.needs_input_grad[1] and d.dy_masked and alg_bwd_shape_ok(weight)
+    # linked (a downsample block's shortcut conv, PDT_DS_ALG): only as the FIRST of the two branches — dx is handed
+    # to conv1's dgrad GEMM to accumulate into (or, strided, added at the sampled pixels), so it takes no reduction
+    linked = ctx.link is not None
+    if not (SW.bwd_alg and (not linked or ctx.link.grad is None) and getattr(ctx, "dre", None) is None
+            and ctx.needs_input_grad[0] and ctx.needs_input_grad[1] and d.dy_masked and alg_bwd_shape_ok(weight)
             and x.dtype == torch.bfloat16 and x.is_contiguous(memory_format=torch.channels_last)):
         return None
     from ._native import native
@@ -598,7 +603,8 @@ def _bwd_alg(ctx, d, x, weight):
     coef = d.coef.contiguous()
     G, bwg = native().bn_alg_small_gemm(w2, coef, wg)  # W^T diag(B) W [CW, CW], diag(B) W Gram [C4, CW] (fp32)
     bcat, dw2 = native().bn_alg_assemble(w2, coef, d.mean.contiguous(), G, wg, bwg)
-    gs = ctx.gsrc if (ctx.gsrc is not None and ctx.gsrc.ready()) else None
+    gsrc = getattr(ctx, "gsrc", None)
+    gs = gsrc if (gsrc is not None and gsrc.ready() and not linked) else None
     dx = torch.empty_like(x, memory_format=torch.channels_last)
     part = native().conv1x1_gemm_seg(g2, a2, 2, bcat, _nhwc2d(dx), bn_x=gs.x if gs else None,
                                      bn_mask=gs.mask if gs else None, bn_mean=gs.mean if gs else None)
@@ -649,7 +655,9 @@ class _Conv1x1StridedFn(torch.autograd.Function):
     positions, so no full-size zero tensor is ever written."""
 
     @staticmethod
-    def forward(ctx, x, weight, s, link, stats_out=None):
+    def forward(ctx, x, weight, s, link, stats_out=None, bwd_link=None):
+        """``bwd_link``: the shortcut BatchNorm may hand its input gradient over in deferred form for the ALG
+        backward (``_bwd_alg`` on the gathered input; PDT_DS_ALG)."""
         N, Ci, H, W = x.shape
         Co = weight.shape[0]
         if _subsample_native(x):
@@ -661,6 +669,10 @@ class _Conv1x1StridedFn(torch.autograd.Function):
         M = N * Hs * Ws
         ctx.save_for_backward(xs, weight)
         ctx.s, ctx.link, ctx.xshape = s, link, x.shape
+        ctx.bwd_link = bwd_link
+        if bwd_link is not None:
+            ctx.set_materialize_grads(False)
+            bwd_link.alg_src = (xs, weight)
         if x.dtype == torch.bfloat16 and _ours_ok("fwd", M, Ci, Co):
             # our GEMM, with the consuming (downsample) BatchNorm's statistics in the epilogue
             from ._native import native
@@ -677,6 +689,15 @@ class _Conv1x1StridedFn(torch.autograd.Function):
         xs, weight = ctx.saved_tensors
         N, Ci, Hs, Ws = xs.shape
         Co = weight.shape[0]
+        if gy is None:  # the shortcut BatchNorm handed its input gradient over (or there is none)
+            d = ctx.bwd_link.take() if ctx.bwd_link is not None else None
+            r = _bwd_alg(ctx, d, xs, weight) if d is not None else None
+            if r is not None:
+                return _Conv1x1StridedFn._deliver(ctx, r[0]), r[1], None, None, None, None
+            if d is None and ctx.link is None:
+                return (None,) * 6
+            gy = d.materialize() if d is not None else torch.zeros(
+                (N, Co, Hs, Ws), dtype=xs.dtype, device=xs.device, memory_format=torch.channels_last)
         gy = gy.contiguous(memory_format=torch.channels_last)
         g2, w2 = _nhwc2d(gy), weight.reshape(Co, Ci)
         M = g2.shape[0]
@@ -688,21 +709,27 @@ class _Conv1x1StridedFn(torch.autograd.Function):
                 native().conv1x1_gemm(g2, _wt_of(weight, w2), _nhwc2d(d), False, False)
             else:
                 d = torch.mm(g2, w2).view(N, Hs, Ws, Ci).permute(0, 3, 1, 2)
-            compact = StridedGrad(d, ctx.s)
-            acc = ctx.link.take() if ctx.link is not None else None
-            if ctx.link is not None and acc is None:
-                ctx.link.grad = compact  # first: conv1's backward adds it into its full gradient
-            elif acc is not None:
-                dx = compact.add_into(acc)
-            else:
-                dx = compact.dense(ctx.xshape)
+            dx = _Conv1x1StridedFn._deliver(ctx, d)
         if ctx.needs_input_grad[1]:
             sk = max(8, min(64, 1 << max(0, (M // 3136).bit_length() - 1)))  # ~3-6K pixels per slice
             if M % sk == 0 and M // sk >= 256:
                 dw = _wgrad_splitk(g2, _nhwc2d(xs), sk).as_strided(weight.shape, weight.stride())
             else:
                 dw = torch.mm(g2.t(), _nhwc2d(xs)).as_strided(weight.shape, weight.stride())
-        return dx, dw, None, None, None
+        return dx, dw, None, None, None, None
+
+    @staticmethod
+    def _deliver(ctx, d):
+        """The compact data gradient ``d`` (sampled pixels only) to the input: handed to conv1's backward through
+        the link when this branch is first, else added into the partner's gradient / a zero tensor (returned)."""
+        compact = StridedGrad(d, ctx.s)
+        acc = ctx.link.take() if ctx.link is not None else None
+        if ctx.link is not None and acc is None:
+            ctx.link.grad = compact  # first: conv1's backward adds it into its full gradient
+            return None
+        if acc is not None:
+            return compact.add_into(acc)
+        return compact.dense(ctx.xshape)
 
 
 class _LinkedConvFn(torch.autograd.Function):
@@ -1086,7 +1113,7 @@ class Conv1x1(nn.Conv2d):
         if self.strided_gemm_eligible(x):
             holder = [] if (self.emit_bn_stats and self.training and torch.is_grad_enabled()
                             and SW.conv_bn_stats) else None
-            y = _Conv1x1StridedFn.apply(x, self.weight, self.stride[0], res_link, holder)
+            y = _Conv1x1StridedFn.apply(x, self.weight, self.stride[0], res_link, holder, bwd_link)
             if holder:
                 y._pdt_bn_stats = BNStats(holder[0], y._version)
             return y
@@ -1098,6 +1125,15 @@ class Conv1x1(nn.Conv2d):
         ALG backward (``_bwd_alg``; ``PDT_BWD_ALG=0`` turns it off)."""
         return (SW.bwd_alg and self.training and torch.is_grad_enabled() and x.dtype == torch.bfloat16
                 and self.gemm_eligible(x) and alg_bwd_shape_ok(self.weight) and not _has_hooks(self)
+                and not self._backward_hooks and not self._backward_pre_hooks)
+
+    def ds_alg_ok(self, x: torch.Tensor) -> bool:
+        """As a downsample block's shortcut conv (stride 1 or strided GEMM path): its backward can run the ALG
+        backward with the shortcut BatchNorm's input gradient in deferred form (``PDT_DS_ALG``: input channels up
+        to that many; ResNet-50 layer 4's 1024 -> 2048 shortcut would double its GEMM for a 180 us pass)."""
+        return (SW.bwd_alg >= 2 and 0 < self.in_channels <= SW.ds_alg and self.training and torch.is_grad_enabled()
+                and x.dtype == torch.bfloat16 and (self.gemm_eligible(x) or self.strided_gemm_eligible(x))
+                and alg_bwd_shape_ok(self.weight) and not _has_hooks(self)
                 and not self._backward_hooks and not self._backward_pre_hooks)
 
     def fused_bwd_ok(self, x: torch.Tensor) -> bool:

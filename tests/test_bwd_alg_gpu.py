@@ -24,7 +24,7 @@ def _bits(b: torch.Tensor) -> torch.Tensor:
 
 @pytest.mark.parametrize("bstats", [False, True])
 @pytest.mark.parametrize("M,C4,CW", [(1000, 512, 128), (777, 1024, 256), (300, 2048, 512), (2048, 256, 128),
-                                    (1500, 256, 64)])
+                                    (1500, 256, 64), (900, 512, 256), (640, 1024, 512), (300, 2048, 1024)])
 def test_gemm_seg_matches_fp32(M, C4, CW, bstats):
     """y = [g | a | a | 1] b^T (K = C4 + 2 CW + 32), rows past a 256-row tile boundary included; BSTATS: the
     epilogue's BatchNorm partials and the masked store."""
@@ -54,7 +54,8 @@ def test_gemm_seg_matches_fp32(M, C4, CW, bstats):
     torch.testing.assert_close(out.float(), ref, rtol=2e-2, atol=2e-2)
 
 
-@pytest.mark.parametrize("M,C4,CW", [(1000, 512, 128), (3000, 1024, 256), (517, 2048, 512), (2000, 256, 64)])
+@pytest.mark.parametrize("M,C4,CW", [(1000, 512, 128), (3000, 1024, 256), (517, 2048, 512), (2000, 256, 64),
+                                    (1200, 512, 256), (700, 1024, 512), (400, 2048, 1024)])
 def test_wgrad_seg_matches_fp32(M, C4, CW):
     """[g | a | 1]^T a in fp32: P = g^T a, Gram = a^T a, and the ones block's rows = column sums of a."""
     gen = torch.Generator(device="cuda").manual_seed(M)
@@ -92,7 +93,8 @@ def _deferred(M, C4, CW, seed):
     return a, w, z, dy, bits, mean, torch.stack([A, B, D]).contiguous()
 
 
-@pytest.mark.parametrize("C4,CW", [(256, 64), (512, 128), (1024, 256), (2048, 512)])
+@pytest.mark.parametrize("C4,CW", [(256, 64), (512, 128), (1024, 256), (2048, 512), (512, 256), (1024, 512),
+                                   (2048, 1024)])
 def test_assemble_matches_torch(C4, CW):
     M = 2000
     a, w, z, dy, bits, mean, coef = _deferred(M, C4, CW, C4)
@@ -120,7 +122,8 @@ def test_assemble_matches_torch(C4, CW):
     torch.testing.assert_close(dw.float(), want, rtol=1e-2, atol=1e-3)
 
 
-@pytest.mark.parametrize("N,H,C4,CW", [(8, 14, 1024, 256), (16, 7, 2048, 512), (4, 28, 512, 128), (2, 56, 256, 64)])
+@pytest.mark.parametrize("N,H,C4,CW", [(8, 14, 1024, 256), (16, 7, 2048, 512), (4, 28, 512, 128), (2, 56, 256, 64),
+                                        (4, 28, 512, 256), (8, 14, 1024, 512), (16, 7, 2048, 1024)])
 def test_alg_backward_matches_materialised_bn_backward(N, H, C4, CW):
     """_bwd_alg's (da, dW) against the fp32 math of the materialised path: dz = A g + B (z - mean) + D, then
     da = dz W and dW = dz^T a. The ALG path never forms dz; its error is bf16-level against fp32."""
@@ -174,6 +177,7 @@ def test_resnet50_grads_alg_vs_unfused(switch, mode, first):
     conv_ops._bwd_alg = spy
     try:
         switch("PDT_BWD_ALG", mode)
+        switch("PDT_DS_ALG", "0")  # the shortcut convs: test_resnet50_grads_ds_alg
         switch("PDT_BWD_ALG_FIRST", first)  # 1: layer 1's conv3 on the ALG path too (instead of the fused kernel)
         ga = _grads()
     finally:
@@ -190,6 +194,46 @@ def test_resnet50_grads_alg_vs_unfused(switch, mode, first):
     assert not worse, worse[:8]
 
 
+@pytest.mark.parametrize("ds", ["512", "2048"])
+def test_resnet50_grads_ds_alg(switch, ds):
+    """PDT_DS_ALG: each downsample block's shortcut conv + BN on the ALG backward too (layer 1's stride-1 shortcut,
+    layers 2-3's strided ones; "2048": layer 4's 1024 -> 2048 as well): the shortcut BN takes sum(g) from bn3's
+    bias gradient and sum(g (x - mean)) from the ALG pass — no reduce or apply pass. Gradients as accurate against
+    the fp32 oracle as with the shortcut on its old path, tensor by tensor."""
+    from pytorch_distributed_training_example_amd.ops import conv as conv_ops
+    from pytorch_distributed_training_example_amd.ops import batchnorm as bn_ops
+    calls, pre = [], []
+    orig, orig_pre = conv_ops._bwd_alg, bn_ops._alg_ds_prelude
+
+    def spy(*a):
+        r = orig(*a)
+        calls.append(r is not None)
+        return r
+
+    def spy_pre(*a):
+        r = orig_pre(*a)
+        pre.append(r is not None)
+        return r
+    conv_ops._bwd_alg, bn_ops._alg_ds_prelude = spy, spy_pre
+    try:
+        switch("PDT_DS_ALG", ds)
+        ga = _grads()
+    finally:
+        conv_ops._bwd_alg, bn_ops._alg_ds_prelude = orig, orig_pre
+    n_ds = 3 if ds == "512" else 4
+    assert pre == [True] * n_ds, pre
+    assert calls == [True] * (16 + n_ds), calls
+    switch("PDT_DS_ALG", "0")
+    gb = _grads()
+    g32 = _grads(fp32=True)
+    ea, eb = _rel(ga, g32), _rel(gb, g32)
+    print(f"ds alg vs fp32: median {float(ea.median()):.4f} max {float(ea.max()):.4f}; "
+          f"ds old path vs fp32: median {float(eb.median()):.4f} max {float(eb.max()):.4f}")
+    assert float(ea.median()) <= 1.1 * float(eb.median()) + 1e-3, (float(ea.median()), float(eb.median()))
+    worse = [(n, float(a), float(b)) for n, a, b in zip(g32, ea, eb) if a > 1.5 * b + 5e-3]
+    assert not worse, worse[:8]
+
+
 def test_alg_path_is_deterministic():
     from pytorch_distributed_training_example_amd.config import SW
     assert SW.bwd_alg
@@ -197,7 +241,8 @@ def test_alg_path_is_deterministic():
     assert all(torch.equal(ga[k], gb[k]) for k in ga)
 
 
-@pytest.mark.parametrize("C4,CW", [(256, 64), (512, 128), (1024, 256), (2048, 512)])
+@pytest.mark.parametrize("C4,CW", [(256, 64), (512, 128), (1024, 256), (2048, 512), (512, 256), (1024, 512),
+                                   (2048, 1024)])
 def test_small_gemm_and_fix_s2(C4, CW):
     """bn_alg_small_gemm (G = W^T diag(B) W, BWG = diag(B) W Gram) and bn_alg_fix_s2 (a sum-only producer's
     centred sums completed from P) against fp64 math."""
