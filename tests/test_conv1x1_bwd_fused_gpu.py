@@ -134,7 +134,9 @@ def test_bn_bwd_coef_matches_full_backward(relu, with_part):
 def _grads(seed=0, fp32=False):
     """ResNet-50 parameter gradients of one step at batch 8 (96 x 96): bf16-mixed on our kernels, or
     (fp32=True) the same weights, input and labels in fp32 on stock PyTorch ops (PDT_DISABLE_NATIVE) —
-    the oracle, as in tests/test_models_gpu.py."""
+    the oracle, as in tests/test_models_gpu.py. Each residual branch's last BatchNorm starts at gamma 0.2: the
+    default random init is so ill-conditioned that bf16 and fp32 gradients differ by > 100 % (median) whatever the
+    kernels, which left these comparisons without power; at 0.2 they agree to bf16 rounding."""
     from pytorch_distributed_training_example_amd.config import SW
     from pytorch_distributed_training_example_amd.models import get_model
     from pytorch_distributed_training_example_amd.models.precision import to_bf16_mixed
@@ -144,6 +146,9 @@ def _grads(seed=0, fp32=False):
     try:
         torch.manual_seed(seed)
         m = get_model("resnet50").cuda().to(memory_format=torch.channels_last)
+        for name, mod in m.named_modules():
+            if name.endswith(".bn3"):
+                torch.nn.init.constant_(mod.weight, 0.2)
         if not fp32:
             m = to_bf16_mixed(m)
         x = torch.randn(8, 3, 96, 96, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
@@ -230,6 +235,7 @@ def test_bottleneck_block_grads_fused_vs_unfused(switch, layer, block, defer):
 
     def run(flag):
         switch("PDT_BWD_FUSED", flag)
+        switch("PDT_BWD_ALG_FIRST", "0")  # layer 1's conv3 on the fused kernel, not the ALG path
         switch("PDT_BWD_FUSED_SHAPES", "256x64,512x128")
         switch("PDT_BN2_DEFER", defer)
         blk.zero_grad(set_to_none=True)
