@@ -46,8 +46,13 @@ PDT_BWD_ALG                 2            bottleneck conv3 + bn3 backward (the sh
                                          bn3's apply pass: z = a W^T substituted into bn3's backward (ops/conv.py
                                          _bwd_alg, csrc/kernels/bn_alg.hip): one wgrad pass + one data-gradient GEMM;
                                          2: also bn3's backward reduction without reading z (sum-only producer)
-PDT_Z3_VIRTUAL              0            1 (with PDT_BWD_ALG=2): a bottleneck conv3 output (bn3 input) is never written —
-                                         statistics-only GEMM, bn3's apply as the GEMM again (APPLY epilogue)
+PDT_Z3_VIRTUAL              0            (with PDT_BWD_ALG=2) a bottleneck conv3 output (bn3 input) is never written —
+                                         statistics-only GEMM, bn3's apply as the GEMM again (APPLY epilogue): 1 every
+                                         block; 2 only where that APPLY GEMM runs anyway (conv3 input channels <=
+                                         PDT_BN_APPLY_GEMM_K: the skipped store is then pure gain)
+PDT_BWD_ALG_MIN_M           50176        the ALG paths (conv3 and shortcut) only for convs with at least this many output
+                                         pixels: their small per-block GEMMs cost ~30-60 us whatever the batch, more
+                                         than the apply pass they remove on ResNet-50 layers 3-4 at 128 images/GPU
 PDT_BWD_ALG_FIRST           1            the ALG backward also where PDT_BWD_FUSED would run (layer 1's conv3)
 PDT_DS_ALG                  512          the ALG backward for a downsample block's shortcut conv + BN too, where the
                                          conv has <= this many input channels (0 = off): the shortcut BN's
@@ -84,7 +89,7 @@ class _Switches:
                  "conv1x1_table", "conv1x1_dump", "conv1x1_s2", "conv3x3", "conv3x3_wgrad", "conv3x3_s2", "conv_stem",
                  "conv_bn_stats", "bn_bwd_stats", "res_masked", "stem_bwd_fused", "stem_bn_wgrad", "stem_bn_stats", "stem_pool_wgrad", "wgrad_splitk", "slice_sum",
                  "subsample_native", "linear_splitk", "fused_addln", "embedding_native", "linear_epilogue",
-                 "bwd_fused", "bwd_fused_shapes", "bwd_alg", "z3_virtual", "bwd_alg_first", "ds_alg", "bn2_defer", "bn_apply_gemm_k", "strided_bstats", "gap_native",
+                 "bwd_fused", "bwd_fused_shapes", "bwd_alg", "bwd_alg_min_m", "z3_virtual", "bwd_alg_first", "ds_alg", "bn2_defer", "bn_apply_gemm_k", "strided_bstats", "gap_native",
                  "fp8_fused_gelu", "fp8_weight_multi", "fp8_cast_colsum", "fp8_ln", "wgrad_stream_m")
 
     def __init__(self):
@@ -134,9 +139,10 @@ class _Switches:
         # 0 off; 1: ALG backward; 2: also the producer of bn3's gradient skips reading bn3's input for the backward
         # reduction (sum-only epilogue) and the ALG pass completes it (ops/batchnorm.py _BNTrainFn.backward)
         self.bwd_alg = int(e("PDT_BWD_ALG", "2"))
+        self.bwd_alg_min_m = int(e("PDT_BWD_ALG_MIN_M", "50176"))
         # bottleneck conv3 on the ALG backward: z (bn3's input) never written — statistics-only GEMM, bn3 applied by
         # the GEMM again (APPLY epilogue); recomputed only on a fallback (ops/conv.py materialize_virtual)
-        self.z3_virtual = on("PDT_Z3_VIRTUAL", "0")
+        self.z3_virtual = int(e("PDT_Z3_VIRTUAL", "0"))
         # the ALG backward also for the conv3 shapes the fused kernel takes (ResNet-50 layer 1: 256x64)
         self.bwd_alg_first = on("PDT_BWD_ALG_FIRST", "1")
         # the ALG backward for the downsample shortcut conv + BN (input channels <= this; 0 = off)

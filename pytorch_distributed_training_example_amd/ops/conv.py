@@ -1098,7 +1098,8 @@ class Conv1x1(nn.Conv2d):
             # BatchNorm's statistics (this GEMM's epilogue) and its apply, which runs as this GEMM again (APPLY
             # epilogue) — so z is never written (PDT_Z3_VIRTUAL; materialize_virtual recomputes it on a fallback)
             virt = (holder is not None and bwd_link is not None and bwd_link.needs_masked and SW.bwd_alg >= 2
-                    and SW.z3_virtual and x.dtype == torch.bfloat16)
+                    and x.dtype == torch.bfloat16
+                    and (SW.z3_virtual == 1 or (SW.z3_virtual == 2 and 0 < self.in_channels <= SW.bn_apply_gemm_k)))
             y = _Conv1x1Fn.apply(x, self.weight, res_link, holder,
                                  grad_stats_source_of(x) if self.training and torch.is_grad_enabled() else None,
                                  bwd_link, None, virt)
@@ -1124,6 +1125,7 @@ class Conv1x1(nn.Conv2d):
         """This conv's backward can take its consuming BatchNorm's input gradient in deferred form and run the
         ALG backward (``_bwd_alg``; ``PDT_BWD_ALG=0`` turns it off)."""
         return (SW.bwd_alg and self.training and torch.is_grad_enabled() and x.dtype == torch.bfloat16
+                and x.numel() // max(1, x.shape[1]) >= SW.bwd_alg_min_m
                 and self.gemm_eligible(x) and alg_bwd_shape_ok(self.weight) and not _has_hooks(self)
                 and not self._backward_hooks and not self._backward_pre_hooks)
 
@@ -1131,8 +1133,11 @@ class Conv1x1(nn.Conv2d):
         """As a downsample block's shortcut conv (stride 1 or strided GEMM path): its backward can run the ALG
         backward with the shortcut BatchNorm's input gradient in deferred form (``PDT_DS_ALG``: input channels up
         to that many; ResNet-50 layer 4's 1024 -> 2048 shortcut would double its GEMM for a 180 us pass)."""
+        s = self.stride[0]
+        m_out = x.shape[0] * (-(-x.shape[2] // s)) * (-(-x.shape[3] // s)) if x.dim() == 4 else 0
         return (SW.bwd_alg >= 2 and 0 < self.in_channels <= SW.ds_alg and self.training and torch.is_grad_enabled()
-                and x.dtype == torch.bfloat16 and (self.gemm_eligible(x) or self.strided_gemm_eligible(x))
+                and x.dtype == torch.bfloat16 and m_out >= SW.bwd_alg_min_m
+                and (self.gemm_eligible(x) or self.strided_gemm_eligible(x))
                 and alg_bwd_shape_ok(self.weight) and not _has_hooks(self)
                 and not self._backward_hooks and not self._backward_pre_hooks)
 

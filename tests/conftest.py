@@ -7,6 +7,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+# the ALG backward paths at the tests' small batches too (by default they need >= 50176 output pixels per conv)
+os.environ.setdefault("PDT_BWD_ALG_MIN_M", "0")
 # MIOpen reads its solver switches once per process: exclude the capture-unsafe solvers before
 # any test runs a convolution so the hipGraph tests see the same solver set as bench --graph 1
 from pytorch_distributed_training_example_amd.engine.graph import make_miopen_capture_safe  # noqa: E402

@@ -234,6 +234,29 @@ def test_resnet50_grads_ds_alg(switch, ds):
     assert not worse, worse[:8]
 
 
+def test_alg_min_pixels_threshold(switch):
+    """PDT_BWD_ALG_MIN_M: below the threshold no conv takes the ALG paths (their per-block small GEMMs cost more
+    than the apply pass they save on small feature maps); at batch 8 / 96 x 96 every conv is below 50176."""
+    from pytorch_distributed_training_example_amd.ops import conv as conv_ops
+    calls = []
+    orig = conv_ops._bwd_alg
+
+    def spy(*a):
+        r = orig(*a)
+        calls.append(r is not None)
+        return r
+    conv_ops._bwd_alg = spy
+    try:
+        switch("PDT_BWD_ALG_MIN_M", "50176")
+        _grads()
+        assert calls == [], calls
+        switch("PDT_BWD_ALG_MIN_M", "1152")  # layers 1-2 only (8 x 24 x 24 = 4608 and 8 x 12 x 12 = 1152 pixels)
+        _grads()
+    finally:
+        conv_ops._bwd_alg = orig
+    assert calls == [True] * (3 + 4 + 2), calls  # layer-1 and layer-2 conv3s and their shortcuts
+
+
 def test_alg_path_is_deterministic():
     from pytorch_distributed_training_example_amd.config import SW
     assert SW.bwd_alg
@@ -265,14 +288,14 @@ def test_small_gemm_and_fix_s2(C4, CW):
     torch.testing.assert_close(part[1].double().sum(0), want, rtol=1e-3, atol=1e-2)
 
 
-@pytest.mark.parametrize("gap_native", ["1", "0"])
-def test_unwritten_conv3_output_matches_written(switch, gap_native):
+@pytest.mark.parametrize("gap_native,mode", [("1", "1"), ("0", "1"), ("1", "2")])
+def test_unwritten_conv3_output_matches_written(switch, gap_native, mode):
     """PDT_Z3_VIRTUAL: layer 2-4 conv3 outputs are never written (statistics-only GEMM, bn3 applied by the GEMM
     again). The step's gradients equal the run that writes them bit for bit — including, with the global-average-
     pool kernel off (its gradient arrives unmasked, so the last block leaves the ALG path), the fallback that
     recomputes the unwritten output (ops/conv.py materialize_virtual)."""
     switch("PDT_GAP_NATIVE", gap_native)
-    switch("PDT_Z3_VIRTUAL", "1")
+    switch("PDT_Z3_VIRTUAL", mode)  # 2: only layer 1 (where bn3's apply runs as the APPLY GEMM anyway)
     ga = _grads(seed=5)
     switch("PDT_Z3_VIRTUAL", "0")
     gb = _grads(seed=5)
