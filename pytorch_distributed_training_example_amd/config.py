@@ -61,12 +61,14 @@ PDT_BN2_DEFER               0            1: with PDT_BWD_FUSED, bn2's apply + Re
                                          in the forward GEMM, recomputed in the fused backward, which writes bn2's
                                          mask). Measured -0.2 %, and -2 % with PDT_BN_APPLY_GEMM_K (the relu(a x + b)
                                          operand transform then runs in both GEMM passes): off
-PDT_BN_APPLY_GEMM_K         64           a BatchNorm(+residual)+ReLU apply after a 1x1 conv with <= this many input
+PDT_BN_APPLY_GEMM_K         0            a BatchNorm(+residual)+ReLU apply after a 1x1 conv with <= this many input
                                          channels runs as that conv's GEMM again with the apply epilogue (reads
-                                         the conv input, C/4 channels, instead of its output; 0 = off). With the
-                                         256-channel GEMM tiles: 128 (layers 1-2) +0.7 % over off; 64 (layer 1
-                                         only) +0.2 % over 128 in two same-box A/Bs; 256 (adds layer 3) -0.6 %
-                                         (profiles/r4/ab_bn_apply_gemm.md)
+                                         the conv input, C/4 channels, instead of its output; 0 = off). Round 4
+                                         (256-channel GEMM tiles): 128 (layers 1-2) +0.7 % over off, 64 +0.2 % over
+                                         128 (profiles/r4/ab_bn_apply_gemm.md). Round 6, with the ALG backward: 64
+                                         is 0.4 % SLOWER than off (16,202-16,226 vs 16,265-16,287 img/s, same box,
+                                         profiles/r6/ab_apply_gemm_r6.txt): the layer-1 APPLY GEMM runs at ~4 TB/s
+                                         (906-1217 us) against the 5.4 TB/s apply pass
 PDT_LINEAR_EPILOGUE         auto         Linear forward GEMMs (+bias, MLP fc1+bias+GELU) on our MFMA kernel (gemm.hip)
                                          per shape by measurement (tuning/linear_gfx950.json, else timed once);
                                          1 / 0: forced on / off
@@ -148,7 +150,7 @@ class _Switches:
         # the ALG backward for the downsample shortcut conv + BN (input channels <= this; 0 = off)
         self.ds_alg = int(e("PDT_DS_ALG", "512"))
         self.bn2_defer = on("PDT_BN2_DEFER", "0")
-        self.bn_apply_gemm_k = int(e("PDT_BN_APPLY_GEMM_K", "64"))
+        self.bn_apply_gemm_k = int(e("PDT_BN_APPLY_GEMM_K", "0"))
         self.strided_bstats = on("PDT_STRIDED_BSTATS")
         self.gap_native = on("PDT_GAP_NATIVE")
         self.fp8_fused_gelu = on("PDT_FP8_FUSED_GELU")
