@@ -112,6 +112,10 @@ class _WgradFork:
             self.ev.record(self.cur)
 
     def run(self, fn):
+        # Allocator safety of the operands fn reads on the side stream (gy, x and their 2-D views, allocated on the
+        # current stream, NOT record_stream'ed): the join below (current stream waits for the side stream) is
+        # enqueued before this returns, and the caller holds the operands until after — so any free of them, and
+        # any reuse of that memory by a later kernel on the current stream, is stream-ordered after fn's kernels.
         if self.cur is None:
             return fn()
         dev = self.cur.device

@@ -68,14 +68,20 @@ class Fp8State(nn.Module):
         rows = [self.state[m._fp8[1] + 1] for m in lins if fp8_ok_weight(m.weight)]
         out = native().fp8_cast_multi(ws, rows)
         for i, w in enumerate(ws):
-            self.wcache[id(w)] = (w, out[2 * i], out[2 * i + 1])
+            self.wcache[id(w)] = (w, out[2 * i], out[2 * i + 1], w._version)
 
     def weight_fp8(self, w: torch.Tensor, slot: int):
-        """(wq, wqt) of ``w``: this forward's cached cast, or a cast now (eval / untagged calls)."""
+        """(wq, wqt) of ``w``: this forward's cached cast, or a cast now (eval / untagged calls, or a weight
+        modified in place since the cast — e.g. a submodule called right after optimizer.step: the version
+        counter tells, so a GEMM never reads a stale fp8 copy)."""
         e = self.wcache.get(id(w)) if getattr(self, "wcache", None) else None
-        if e is not None and e[0] is w:
+        if e is not None and e[0] is w and e[3] == w._version:
             return e[1], e[2]
         return native().fp8_cast_transpose(w, self.state[slot + 1], True)
+
+    def clear_weight_cache(self) -> None:
+        """Drop this forward's fp8 weight copies (they are otherwise kept until the next forward recasts)."""
+        self.wcache = {}
 
 
 class _Fp8LinearFn(torch.autograd.Function):

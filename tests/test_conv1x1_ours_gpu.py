@@ -298,14 +298,19 @@ def test_bn_backward_from_tiles_matches_reduce(relu, res):
 def test_bottleneck_chain_takes_bn_backward_stats(monkeypatch, switch):
     """Two Bottlenecks (downsample + identity): with the BN-backward hand-off on, bn2 (conv3's
     dgrad) and the first block's bn3 (the second block's conv1 dgrad, shortcut accumulated) take
-    their reduction from the GEMM epilogue — and every gradient matches the hand-off-off run."""
+    their reduction from the GEMM epilogue (and block 0's conv3 + shortcut run the ALG backward) — and every
+    gradient is as close to an fp32 oracle of the same weights and input as the hand-off-off run's, tensor by
+    tensor. (The two bf16 runs differ from the oracle by 1-10 % on this random init — forward bf16 rounding, the
+    same for both — so a direct on-vs-off bound measures that noise, not the hand-off.)"""
+    import copy
     from pytorch_distributed_training_example_amd.models import resnet as R
     from pytorch_distributed_training_example_amd.models.precision import to_bf16_mixed
     from pytorch_distributed_training_example_amd.ops import batchnorm as B
     torch.manual_seed(0)
     ds = R._Downsample(R.conv1x1(64, 256, 1), R._bn(256))
-    net = to_bf16_mixed(torch.nn.Sequential(R.Bottleneck(64, 64, 1, ds), R.Bottleneck(256, 64, 1, None))
-                        .cuda().to(memory_format=torch.channels_last))
+    base = torch.nn.Sequential(R.Bottleneck(64, 64, 1, ds), R.Bottleneck(256, 64, 1, None)).cuda()
+    net = to_bf16_mixed(copy.deepcopy(base).to(memory_format=torch.channels_last))
+    ref = copy.deepcopy(base).to(memory_format=torch.channels_last)
     x0 = torch.randn(8, 64, 28, 28, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
     switch("PDT_CONV1X1", "ours")
     used = []
@@ -316,20 +321,26 @@ def test_bottleneck_chain_takes_bn_backward_stats(monkeypatch, switch):
         used.append(p is not None)
         return p
     monkeypatch.setattr(B.GradStatsSource, "take", spy)
+
+    def grads(m, x_in):
+        m.zero_grad(set_to_none=True)
+        x = x_in.clone().requires_grad_(True)
+        y = m(x)
+        y.backward(torch.ones_like(y) * 0.01 + y.detach() * 0.1)
+        return [x.grad.double()] + [p.grad.double().clone() for p in m.parameters()]
     out = {}
     for on in ("1", "0"):
         switch("PDT_BN_BWD_STATS", on)
         used.clear()
-        net.zero_grad(set_to_none=True)
-        x = x0.clone().requires_grad_(True)
-        y = net(x)
-        y.backward(torch.ones_like(y) * 0.01 + y.detach() * 0.1)
-        out[on] = [x.grad.float()] + [p.grad.float().clone() for p in net.parameters()]
+        out[on] = grads(net, x0)
         if on == "1":
             assert sum(used) >= 3, used  # bn2 of both blocks + block 0's bn3
-    for a, b in zip(out["1"], out["0"]):
-        err = ((a - b).norm() / (b.norm() + 1e-12)).item()
-        assert err < 2e-2, err
+    switch("PDT_DISABLE_NATIVE", "1")
+    want = grads(ref, x0.float())
+    rel = lambda a, b: float((a - b).norm() / b.norm().clamp_min(1e-30))  # noqa: E731
+    for i, (a, b, w) in enumerate(zip(out["1"], out["0"], want)):
+        ea, eb = rel(a, w), rel(b, w)
+        assert ea <= 1.25 * eb + 5e-3, (i, ea, eb)
 
 
 @pytest.mark.parametrize("shape", [(4, 64, 56, 56), (3, 64, 17, 23)])

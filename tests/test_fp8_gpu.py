@@ -303,3 +303,26 @@ def test_striped_amax_rows(kind):
     st.update()
     assert st.state[0, Fp8State.STRIPED].item() == ref[0].item() > 0
     assert (st.state[0, 4:Fp8State.STRIPED] == 0).all()
+
+
+def test_weight_cache_recasts_after_inplace_update():
+    """Fp8State.cast_weights caches each weight's fp8 copies for one forward; a weight modified in place after the
+    cast (optimizer.step, then a submodule called directly) must not be served from the stale copy."""
+    from pytorch_distributed_training_example_amd.ops.fp8 import Fp8State
+    torch.manual_seed(5)
+    lin = torch.nn.Linear(256, 128, bias=False).cuda().bfloat16()
+    st = Fp8State(3).cuda()
+    lin._fp8 = (st, st.alloc(3))
+    st.cast_weights([lin])
+    q0, _ = st.weight_fp8(lin.weight, 0)
+    assert st.weight_fp8(lin.weight, 0)[0] is q0  # served from the cache while unchanged
+    with torch.no_grad():
+        lin.weight.mul_(-1.0)
+    q1, _ = st.weight_fp8(lin.weight, 0)
+    assert q1 is not q0
+    from pytorch_distributed_training_example_amd.ops._native import native
+    want, _ = native().fp8_cast_transpose(lin.weight, st.state[1].clone(), True)  # same scale row, fresh cast
+    assert torch.equal(q1.view(torch.uint8), want.view(torch.uint8)), "recast of the updated weight"
+    assert not torch.equal(q1.view(torch.uint8), q0.view(torch.uint8))
+    st.clear_weight_cache()
+    assert st.wcache == {}
