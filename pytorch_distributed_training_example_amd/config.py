@@ -61,6 +61,8 @@ PDT_BN2_DEFER               0            1: with PDT_BWD_FUSED, bn2's apply + Re
                                          in the forward GEMM, recomputed in the fused backward, which writes bn2's
                                          mask). Measured -0.2 %, and -2 % with PDT_BN_APPLY_GEMM_K (the relu(a x + b)
                                          operand transform then runs in both GEMM passes): off
+PDT_SUB_OUT                 1            a ResNet stage's last BatchNorm apply also writes the stride-2 subsample the next
+                                         stage's strided 1x1 shortcut reads (its gather pass does not run)
 PDT_BN_APPLY_GEMM_K         0            a BatchNorm(+residual)+ReLU apply after a 1x1 conv with <= this many input
                                          channels runs as that conv's GEMM again with the apply epilogue (reads
                                          the conv input, C/4 channels, instead of its output; 0 = off). Round 4
@@ -91,7 +93,7 @@ class _Switches:
                  "conv1x1_table", "conv1x1_dump", "conv1x1_s2", "conv3x3", "conv3x3_wgrad", "conv3x3_s2", "conv_stem",
                  "conv_bn_stats", "bn_bwd_stats", "res_masked", "stem_bwd_fused", "stem_bn_wgrad", "stem_bn_stats", "stem_pool_wgrad", "wgrad_splitk", "slice_sum",
                  "subsample_native", "linear_splitk", "fused_addln", "embedding_native", "linear_epilogue",
-                 "bwd_fused", "bwd_fused_shapes", "bwd_alg", "bwd_alg_min_m", "z3_virtual", "bwd_alg_first", "ds_alg", "bn2_defer", "bn_apply_gemm_k", "strided_bstats", "gap_native",
+                 "bwd_fused", "bwd_fused_shapes", "bwd_alg", "bwd_alg_min_m", "z3_virtual", "bwd_alg_first", "ds_alg", "bn2_defer", "bn_apply_gemm_k", "strided_bstats", "gap_native", "sub_out",
                  "fp8_fused_gelu", "fp8_weight_multi", "fp8_cast_colsum", "fp8_ln", "wgrad_stream_m")
 
     def __init__(self):
@@ -153,6 +155,7 @@ class _Switches:
         self.bn_apply_gemm_k = int(e("PDT_BN_APPLY_GEMM_K", "0"))
         self.strided_bstats = on("PDT_STRIDED_BSTATS")
         self.gap_native = on("PDT_GAP_NATIVE")
+        self.sub_out = on("PDT_SUB_OUT")
         self.fp8_fused_gelu = on("PDT_FP8_FUSED_GELU")
         self.fp8_weight_multi = on("PDT_FP8_WEIGHT_MULTI")
         self.fp8_cast_colsum = on("PDT_FP8_CAST_COLSUM")

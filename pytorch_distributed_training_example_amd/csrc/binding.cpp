@@ -191,7 +191,8 @@ int pdt_bn_fwd_train_tiles(const float* part, int T, int BMt, const uint16_t* x,
                            const float* res_a, const float* res_b,
                            const float* gamma, const float* beta, float* running_mean, float* running_var,
                            float momentum, float eps, int64_t M, int C, int relu, uint16_t* y, uint8_t* mask,
-                           float* mean, float* invstd, float* ws, hipStream_t s);
+                           float* mean, float* invstd, float* ws, hipStream_t s, uint16_t* sub_y, int sub_H,
+                           int sub_W, int sub_s);
 int pdt_fp8_cast_transpose(const uint16_t* x, int64_t M, int64_t K, const float* scale, uint8_t* out,
                            uint8_t* out_t, float* amax, int striped, hipStream_t s);
 int pdt_fp8_update_scales(float* state, int n, int L, float margin_scale, int striped, hipStream_t s);
@@ -1267,7 +1268,7 @@ void bn_alg_fix_s2(Tensor part, Tensor wg, Tensor w) {
 std::vector<Tensor> bn_fwd_train_tiles(Tensor x, Tensor part, c10::optional<Tensor> res, c10::optional<Tensor> weight,
                                        c10::optional<Tensor> bias, c10::optional<Tensor> running_mean,
                                        c10::optional<Tensor> running_var, double momentum, double eps, bool relu,
-                                       c10::optional<Tensor> res_ab, bool apply) {
+                                       c10::optional<Tensor> res_ab, bool apply, int64_t sub) {
   check_nhwc_bf16(x, "x");
   const int64_t C = x.size(1);
   const int64_t M = x.numel() / C;
@@ -1295,15 +1296,26 @@ std::vector<Tensor> bn_fwd_train_tiles(Tensor x, Tensor part, c10::optional<Tens
   }
   float* rm = running_mean.has_value() && running_mean->defined() ? running_mean->data_ptr<float>() : nullptr;
   float* rv = running_var.has_value() && running_var->defined() ? running_var->data_ptr<float>() : nullptr;
+  // sub >= 2: also the stride-sub subsample of y (x must be 4-D [N, C, H, W])
+  Tensor ys;
+  if (sub >= 2) {
+    TORCH_CHECK(apply && x.dim() == 4, "bn_fwd_train_tiles: the subsample output needs the apply and a 4-D x");
+    ys = at::empty({x.size(0), C, (x.size(2) - 1) / sub + 1, (x.size(3) - 1) / sub + 1},
+                   x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  }
   const int rc = pdt_bn_fwd_train_tiles(part.data_ptr<float>(), (int)T, BMt, reinterpret_cast<const uint16_t*>(x.data_ptr()),
                                         rp, rab.first, rab.second, opt_fptr(weight), opt_fptr(bias), rm, rv,
                                         (float)momentum, (float)eps, M, (int)C, relu,
                                         apply ? reinterpret_cast<uint16_t*>(y.data_ptr()) : nullptr,
                                         (relu && apply) ? mask.data_ptr<uint8_t>() : nullptr, mean.data_ptr<float>(),
-                                        invstd.data_ptr<float>(), ws.data_ptr<float>(), stream());
+                                        invstd.data_ptr<float>(), ws.data_ptr<float>(), stream(),
+                                        sub >= 2 ? reinterpret_cast<uint16_t*>(ys.data_ptr()) : nullptr,
+                                        sub >= 2 ? (int)x.size(2) : 0, sub >= 2 ? (int)x.size(3) : 0, (int)sub);
+  if (rc == -4) return {};  // (subsample not taken: the caller gathers)
   TORCH_CHECK(rc == 0, "pdt_bn_fwd_train_tiles failed: ", rc);
   if (!apply)  // the apply coefficients (a, b) are the workspace's last 2C floats (past the level-1 sums)
     return {Tensor(), Tensor(), mean, invstd, ws.narrow(0, ws.numel() - 2 * C, 2 * C).view({2, C})};
+  if (sub >= 2) return {y, mask, mean, invstd, ys};
   return {y, mask, mean, invstd};
 }
 
@@ -2342,7 +2354,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("subsample_scatter_add", &subsample_scatter_add);
   m.def("bn_fwd_train_tiles", &bn_fwd_train_tiles, py::arg("x"), py::arg("part"), py::arg("res"), py::arg("weight"),
         py::arg("bias"), py::arg("running_mean"), py::arg("running_var"), py::arg("momentum"), py::arg("eps"),
-        py::arg("relu"), py::arg("res_ab") = py::none(), py::arg("apply") = true);
+        py::arg("relu"), py::arg("res_ab") = py::none(), py::arg("apply") = true, py::arg("sub") = 0);
   m.def("conv3x3s1_fwd", &conv3x3s1_fwd);
   m.def("conv3x3s1_fwd_stats", &conv3x3s1_fwd_stats);
   m.def("conv3x3s1_fwd_bnbwd", &conv3x3s1_fwd_bnbwd);

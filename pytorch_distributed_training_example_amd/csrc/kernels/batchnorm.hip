@@ -608,11 +608,26 @@ __global__ void bn_eval_coef_kernel(int C, const float* __restrict__ gamma, cons
 // 5-10 % SLOWER on the ResNet-50 shapes (tools/bn_trace.py, 822 MB: 350 vs 318 us, 520 vs 469 us).
 // RA: the residual is a BatchNorm's INPUT whose apply was deferred to here (ResNet downsample
 // shortcut): the added term is ra*res + rb per channel, so that BN's output is never written.
+// SubOut (y != null): the output's stride-s subsample [N, Hs, Ws, C] is written as well (the input of the next
+// ResNet stage's strided 1x1 shortcut, whose gather pass over y then never runs: ops/conv.py _Conv1x1StridedFn).
+struct SubOut {
+  uint16_t* y;
+  int H, W, Hs, Ws, s;
+  float inv_w, inv_h;  // 1 / W, 1 / H (pixel index decomposition in fp32, corrected: exact below 2^24 pixels)
+};
+
+__device__ __forceinline__ int div_fix(int v, int d, float inv) {
+  int q = (int)((float)v * inv);
+  q -= q * d > v ? 1 : 0;
+  q += (q + 1) * d <= v ? 1 : 0;
+  return q;
+}
+
 template <bool RELU, bool RES, bool MASK, int U, bool RA = false>
 __global__ __launch_bounds__(256) void bn_apply_kernel(
     const uint16_t* __restrict__ x, const uint16_t* __restrict__ res, const float* __restrict__ a,
     const float* __restrict__ b, uint16_t* __restrict__ y, uint8_t* __restrict__ mask, int64_t nvec, int C,
-    int fixed, const float* __restrict__ ra = nullptr, const float* __restrict__ rb = nullptr) {
+    int fixed, const float* __restrict__ ra = nullptr, const float* __restrict__ rb = nullptr, SubOut so = SubOut{}) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   float av[8], bv[8], rav[8], rbv[8];
@@ -658,6 +673,14 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(
       }
       st8_bf16(y + k * 8, v);
       if (MASK) mask[k] = (uint8_t)mb;
+      if (so.y) {  // (uniform) the stride-s subsample too
+        const int e = (int)(k * 8);  // (M C < 2^31: checked by the host)
+        const int row = e / C, cc = e - row * C;
+        const int t = div_fix(row, so.W, so.inv_w), w = row - t * so.W;
+        const int n = div_fix(t, so.H, so.inv_h), h = t - n * so.H;
+        if (h % so.s == 0 && w % so.s == 0)
+          st8_bf16(so.y + (((int64_t)n * so.Hs + h / so.s) * so.Ws + w / so.s) * C + cc, v);
+      }
     }
   }
 }
@@ -1177,12 +1200,13 @@ int pdt_bn_fwd_train(const uint16_t* x, const uint16_t* res, const float* res_a,
   const int64_t nvec = M * C / 8;
   const int fixed = (2048 % C) == 0;
   const int grid = apply_grid(nvec, res ? kApplyRes : kApplyPlain);
+  const SubOut so{};
 #define PDT_APPLY(RL, RS, MK)                                                                                 \
   hipLaunchKernelGGL((bn_apply_kernel<RL, RS, MK, 1>), dim3(grid), dim3(256), 0, s, x, res, a, b, y, mask, \
-                     nvec, C, fixed, nullptr, nullptr)
+                     nvec, C, fixed, nullptr, nullptr, so)
 #define PDT_APPLY_RA()                                                                                         \
   hipLaunchKernelGGL((bn_apply_kernel<true, true, true, 1, true>), dim3(grid), dim3(256), 0, s, x, res, a, b, y, \
-                     mask, nvec, C, fixed, res_a, res_b)
+                     mask, nvec, C, fixed, res_a, res_b, so)
   const bool mk = mask != nullptr;
   if (res_a && !(relu && res && mk)) return -3;  // the deferred-residual form exists for relu+res+mask only
   if (res_a) PDT_APPLY_RA();
@@ -1205,8 +1229,12 @@ int pdt_bn_fwd_train_tiles(const float* part, int T, int BMt, const uint16_t* x,
                            const float* res_a, const float* res_b,
                            const float* gamma, const float* beta, float* running_mean, float* running_var,
                            float momentum, float eps, int64_t M, int C, int relu, uint16_t* y, uint8_t* mask,
-                           float* mean, float* invstd, float* ws, hipStream_t s) {
+                           float* mean, float* invstd, float* ws, hipStream_t s, uint16_t* sub_y, int sub_H,
+                           int sub_W, int sub_s) {
   if (C % kCC != 0 || M < 1 || T != (int)((M + BMt - 1) / BMt)) return -1;
+  if (sub_y && (sub_s < 2 || sub_H < 1 || sub_W < 1 || M % ((int64_t)sub_H * sub_W) != 0 || M >= (1 << 24) ||
+                M * C >= ((int64_t)1 << 31)))
+    return -4;  // (the fp32 index decomposition is exact below 2^24 pixels)
   const int P = (T + tiles_per_block() - 1) / tiles_per_block();
   double* lv = reinterpret_cast<double*>(ws);
   float* a = ws + 4 * (int64_t)P * C;
@@ -1227,6 +1255,9 @@ int pdt_bn_fwd_train_tiles(const float* part, int T, int BMt, const uint16_t* x,
   const int grid = apply_grid(nvec, res ? kApplyRes : kApplyPlain);
   const bool mk = mask != nullptr;
   if (res_a && !(relu && res && mk)) return -3;
+  const SubOut so = sub_y ? SubOut{sub_y, sub_H, sub_W, (sub_H - 1) / sub_s + 1, (sub_W - 1) / sub_s + 1, sub_s,
+                                   1.f / (float)sub_W, 1.f / (float)sub_H}
+                          : SubOut{};
   if (res_a) PDT_APPLY_RA();
   else if (relu && res) { if (mk) PDT_APPLY(true, true, true); else PDT_APPLY(true, true, false); }
   else if (relu) { if (mk) PDT_APPLY(true, false, true); else PDT_APPLY(true, false, false); }
@@ -1310,6 +1341,7 @@ int pdt_bn_fwd_eval(const uint16_t* x, const uint16_t* res, const float* gamma, 
   const int64_t nvec = M * C / 8;
   const int fixed = (2048 % C) == 0;
   const int grid = apply_grid(nvec, res ? kApplyRes : kApplyPlain);
+  const SubOut so{};
   if (relu && res) PDT_APPLY(true, true, false);
   else if (relu) PDT_APPLY(true, false, false);
   else if (res) PDT_APPLY(false, true, false);

@@ -88,6 +88,9 @@ class BasicBlock(nn.Module):
         self.bn2 = _bn(planes)
         self.downsample = downsample
         self.stride = stride
+        # >= 2: this block's output also feeds the next stage's strided 1x1 shortcut — its bn3 apply writes that
+        # subsample too (set by ResNet; the shortcut's gather pass never runs)
+        self.emit_sub = 0
 
     def forward(self, x):
         identity = x if self.downsample is None else self.downsample(x)
@@ -110,6 +113,9 @@ class Bottleneck(nn.Module):
         self.relu = nn.ReLU(inplace=True)
         self.downsample = downsample
         self.stride = stride
+        # >= 2: this block's output also feeds the next stage's strided 1x1 shortcut — its bn3 apply writes that
+        # subsample too (set by ResNet; the shortcut's gather pass never runs)
+        self.emit_sub = 0
 
     def forward(self, x):
         # The linked path needs bn3 on its native kernel (bf16): only that path deposits the shortcut
@@ -149,7 +155,7 @@ class Bottleneck(nn.Module):
                 out = bn_act(self.bn2, z2, relu=True)
             out = self.conv3(out, bwd_link=blink)
             if self.downsample is None:  # identity: bn3's backward deposits the shortcut gradient
-                return self.bn3(out, residual=x, relu=True, res_link=link, out_link=blink)
+                return self.bn3(out, residual=x, relu=True, res_link=link, out_link=blink, sub_stride=self.emit_sub)
             # shortcut built AFTER the main branch so its backward nodes run first (higher
             # autograd sequence numbers): the shortcut conv deposits, conv1 accumulates. Either
             # order is correct (whichever branch finishes second adds), this one saves a pass.
@@ -176,7 +182,8 @@ class Bottleneck(nn.Module):
                     identity = ds_bn._forward_stats_only(xs, grad_link=glink, out_link=dlink)
                 else:
                     identity = ds_bn(xs, grad_link=glink)
-                return self.bn3(out, residual=identity, relu=True, res_link=glink, out_link=blink)
+                return self.bn3(out, residual=identity, relu=True, res_link=glink, out_link=blink,
+                                sub_stride=self.emit_sub)
             identity = bn_act(ds_bn, linked_conv(self.downsample[0], x, link))
             return bn_act(self.bn3, out, residual=identity, relu=True)  # (blink unused: conv3 gets a dense gy)
         identity = x if self.downsample is None else self.downsample(x)
@@ -213,6 +220,13 @@ class ResNet(nn.Module):
                 nn.init.constant_(m.weight, 1)
                 nn.init.constant_(m.bias, 0)
         _norm_kind[0] = "pdt"
+        # a stage's last block writes the stride-2 subsample the next stage's strided 1x1 shortcut reads
+        stages = [self.layer1, self.layer2, self.layer3, self.layer4]
+        for prev, nxt in zip(stages[:-1], stages[1:]):
+            ds = getattr(nxt[0], "downsample", None)
+            if (isinstance(prev[-1], Bottleneck) and ds is not None and isinstance(ds[0], Conv1x1)
+                    and ds[0].stride[0] > 1 and ds[0].stride[0] == ds[0].stride[1]):
+                prev[-1].emit_sub = ds[0].stride[0]
         if zero_init_residual:
             for m in self.modules():
                 if isinstance(m, Bottleneck):

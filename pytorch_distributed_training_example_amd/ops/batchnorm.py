@@ -184,7 +184,7 @@ class _BNTrainFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, residual, weight, bias, running_mean, running_var, momentum, eps, relu, link=None,
                 part=None, gsrc=None, glink=None, res_ab=None, defer=None, out_link=None, defer_relu=None,
-                gemm=None):
+                gemm=None, sub=None):
         C = native()
         ctx.defer_relu = defer_relu
         # x may be a statistics-only conv output (never written, PDT_Z3_VIRTUAL): only the APPLY GEMM path below and
@@ -223,8 +223,14 @@ class _BNTrainFn(torch.autograd.Function):
             a2, w2 = gemm.operands()
             y, mask = C.conv1x1_gemm_apply(a2, w2, residual, ab, res_ab, gemm.acoef)
         elif part is not None:  # statistics from the producing conv's epilogue: no reduce pass over x
-            y, mask, mean, invstd = C.bn_fwd_train_tiles(x, part, residual, weight, bias, running_mean,
-                                                         running_var, momentum, eps, relu, res_ab=res_ab)
+            r = C.bn_fwd_train_tiles(x, part, residual, weight, bias, running_mean, running_var, momentum, eps, relu,
+                                     res_ab=res_ab, sub=sub[0] if sub else 0) if sub else ()
+            if len(r) == 5:  # + the stride-s subsample of y (the next stage's strided shortcut input)
+                y, mask, mean, invstd, ys = r
+                sub.append(ys)
+            else:
+                y, mask, mean, invstd = C.bn_fwd_train_tiles(x, part, residual, weight, bias, running_mean,
+                                                             running_var, momentum, eps, relu, res_ab=res_ab)
         else:
             y, mask, mean, invstd = C.bn_fwd_train(x, residual, weight, bias, running_mean, running_var,
                                                    momentum, eps, relu, res_ab=res_ab)
@@ -265,7 +271,7 @@ class _BNTrainFn(torch.autograd.Function):
         x, mask, weight, mean, invstd = ctx.saved_tensors
         if ctx.defer_relu is not None:  # the mask was written by the consumer's backward
             mask = ctx.dmask
-        tail = (None,) * 14
+        tail = (None,) * 15
         need_w = ctx.has_weight and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3])
         if dy is None:  # gradient handed over through glink as (dy, mask): a ReLU'd dy of the consumer
             g = ctx.glink.take() if ctx.glink is not None else None
@@ -475,7 +481,7 @@ def materialize(t):
 def batch_norm_act(x, residual, weight, bias, running_mean, running_var, training, momentum, eps, relu,
                    res_link: Optional[ResidualGradLink] = None, grad_link: Optional[ResidualGradLink] = None,
                    defer_apply: bool = False, out_link: Optional[BNGradLink] = None,
-                   defer_relu_apply: bool = False):
+                   defer_relu_apply: bool = False, sub_stride: int = 0):
     """Functional fused BN(+add)(+ReLU). Native when x is a channels_last bf16 GPU tensor.
     ``res_link``: route the residual gradient through it instead of returning it (see
     ``ResidualGradLink``); only honoured on the native training path — callers check
@@ -484,7 +490,9 @@ def batch_norm_act(x, residual, weight, bias, running_mean, running_var, trainin
     the same link as ``res_link``: a ResNet downsample shortcut's BN). ``defer_apply`` (internal):
     compute the statistics only and return a ``DeferredBNOutput`` handle (when the native path
     applies; a plain tensor otherwise); the consumer BN (the handle as its ``residual``) adds
-    a*x + b in its own apply pass, so this output is never written."""
+    a*x + b in its own apply pass, so this output is never written. ``sub_stride`` (internal, >= 2): the apply also
+    writes the output's stride-s subsample, attached to the output as ``_pdt_sub`` for the next stage's strided
+    1x1 shortcut (ops/conv.py ``subsample_of``), whose gather pass then never runs."""
     ab = None
     if isinstance(residual, DeferredBNOutput):
         residual, ab = residual.raw, residual.ab
@@ -510,9 +518,13 @@ def batch_norm_act(x, residual, weight, bias, running_mean, running_var, trainin
             dre = [] if (defer_relu_apply and residual is None and relu and x.dim() == 4 and gsrc is not None) else None
             from .conv import gemm_source_of
             gemm = gemm_source_of(x) if (relu and residual is not None and part is not None) else None
+            sub = [int(sub_stride)] if (sub_stride >= 2 and x.dim() == 4 and defer is None and dre is None
+                                         and SW.subsample_native and SW.sub_out) else None
             y = _BNTrainFn.apply(x, residual, weight, bias, running_mean, running_var,
                                  float(momentum), float(eps), bool(relu), res_link, part, gsrc, grad_link, ab, defer,
-                                 out_link, dre, gemm)
+                                 out_link, dre, gemm, sub)
+            if sub is not None and len(sub) > 1:
+                y._pdt_sub = (sub[0], sub[1], y._version)
             if defer:
                 return DeferredBNOutput(y, defer[0])
             if dre:
@@ -575,7 +587,8 @@ class BatchNorm2d(nn.BatchNorm2d):
 
     def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
                 relu: Optional[bool] = None, res_link: Optional[ResidualGradLink] = None,
-                grad_link: Optional[ResidualGradLink] = None, out_link: Optional[BNGradLink] = None) -> torch.Tensor:
+                grad_link: Optional[ResidualGradLink] = None, out_link: Optional[BNGradLink] = None,
+                sub_stride: int = 0) -> torch.Tensor:
         relu = self.fused_relu if relu is None else relu
         training = self.training or not self.track_running_stats
         momentum = self.momentum
@@ -588,7 +601,7 @@ class BatchNorm2d(nn.BatchNorm2d):
         w = self.weight if self.affine else None
         b = self.bias if self.affine else None
         return batch_norm_act(x, residual, w, b, rm, rv, training, momentum if momentum is not None else 0.0,
-                              self.eps, relu, res_link, grad_link, out_link=out_link)
+                              self.eps, relu, res_link, grad_link, out_link=out_link, sub_stride=sub_stride)
 
     def has_hooks(self) -> bool:
         """Forward (pre-)hooks registered on this module or globally: they must see real outputs."""

@@ -628,6 +628,15 @@ def _subsample_native(t: torch.Tensor) -> bool:
             and t.is_contiguous(memory_format=torch.channels_last) and not disabled() and SW.subsample_native)
 
 
+def subsample_of(x: torch.Tensor, s: int):
+    """``x[:, :, ::s, ::s]`` as a compact channels_last tensor when the kernel that wrote x also wrote it (a ResNet
+    stage's last BatchNorm apply, ops/batchnorm.py ``sub_stride``) and x is unmodified since; else None."""
+    t = getattr(x, "_pdt_sub", None)
+    if t is not None and t[0] == s and t[2] == x._version:
+        return t[1]
+    return None
+
+
 class StridedGrad:
     """Gradient of a strided subsampling ``x[:, :, ::s, ::s]`` kept compact (only the sampled
     positions are non-zero) until it is added into a full-size gradient of ``x``."""
@@ -664,7 +673,10 @@ class _Conv1x1StridedFn(torch.autograd.Function):
         backward (``_bwd_alg`` on the gathered input; PDT_DS_ALG)."""
         N, Ci, H, W = x.shape
         Co = weight.shape[0]
-        if _subsample_native(x):
+        xs = subsample_of(x, s)  # written by the producing BatchNorm apply (its _pdt_sub), or None
+        if xs is not None:
+            pass
+        elif _subsample_native(x):
             from ._native import native
             xs = native().subsample_gather(x, s)  # csrc/kernels/subsample.hip
         else:
