@@ -41,8 +41,10 @@ def test_resnet50_gather_replaced_and_unchanged():
     torch.manual_seed(0)
     m = to_bf16_mixed(get_model("resnet50", num_classes=10).cuda().to(memory_format=torch.channels_last))
     assert [m.layer1[-1].emit_sub, m.layer2[-1].emit_sub, m.layer3[-1].emit_sub, m.layer4[-1].emit_sub] == [2, 2, 2, 0]
-    x = torch.randn(4, 3, 112, 112, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
-    y = torch.randint(0, 10, (4,), device="cuda")
+    # (the shape of tests/test_determinism_gpu.py, whose step is bit-reproducible: at 4 x 112 x 112 the stem weight
+    # gradient is not, tools/diag_sub_out.py)
+    x = torch.randn(8, 3, 96, 96, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (8,), device="cuda")
     taken = []
     orig = conv_ops.subsample_of
 
