@@ -3,7 +3,7 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export HSA_ENABLE_IPC_MODE_LEGACY=0 TMPDIR=/tmp
 mkdir -p gpurun_out
-for cfg in "gpt2_medium" "vit_b16" "vit_b16 --precision fp8"; do
+for cfg in ${TX_CFGS:-"gpt2_medium" "gpt2_medium --precision fp8" "vit_b16" "vit_b16 --precision fp8"}; do
   tag=$(echo $cfg | tr ' -' '__')
   timeout -k 10 400 python3 bench.py --model $cfg --gpus 1 --steps 20 --warmup 5 > gpurun_out/tx_$tag.log 2>&1
   rc=$?; echo "$cfg rc=$rc $(grep -o '"value": [0-9.]*' gpurun_out/tx_$tag.log) $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/tx_$tag.log)"
