@@ -146,8 +146,8 @@ int pdt_conv1x1_gemm_seg(const uint16_t* a1, int k1, const uint16_t* a2, int k2,
                          uint16_t* y, int M, int N, const uint16_t* bn_x, const uint8_t* bn_mask, const float* bn_mean,
                          float* bn_part, hipStream_t s);
 int pdt_bn_alg_fix_s2(float* part, int T, const float* wg, const uint16_t* W, int C4, int CW, hipStream_t s);
-int pdt_bn_alg_small_gemm(const uint16_t* W, const float* coef, const float* wg, float* G, float* BWG, int C4, int CW,
-                          hipStream_t s);
+int pdt_bn_alg_small_gemm(const uint16_t* W, const uint16_t* Wt, const float* coef, const float* wg, float* G,
+                          float* BWG, int C4, int CW, hipStream_t s);
 int pdt_bn_alg_assemble(const uint16_t* W, const float* coef, const float* mean, const float* G, const float* wg,
                         const float* BWG, uint16_t* bcat, uint16_t* dW, int C4, int CW, hipStream_t s);
 int pdt_conv1x1_wgrad(const uint16_t* x, const uint16_t* dy, uint16_t* dw, float* ws, int M, int Ci, int Co,
@@ -1227,7 +1227,7 @@ std::vector<Tensor> bn_alg_assemble(Tensor w, Tensor coef, Tensor mean, Tensor G
 }
 
 // (G [CW, CW], BWG [C4, CW]) fp32 of the ALG backward: W^T diag(B) W and diag(B) W Gram (csrc/kernels/bn_alg.hip).
-std::vector<Tensor> bn_alg_small_gemm(Tensor w, Tensor coef, Tensor wg) {
+std::vector<Tensor> bn_alg_small_gemm(Tensor w, Tensor coef, Tensor wg, c10::optional<Tensor> wt) {
   check_cuda(w, "w");
   check_cuda(coef, "coef");
   check_cuda(wg, "wg");
@@ -1241,7 +1241,14 @@ std::vector<Tensor> bn_alg_small_gemm(Tensor w, Tensor coef, Tensor wg) {
   // split-K slices (summed by bn_alg_assemble): G [C4 / 128, CW, CW], BWG [max(1, CW / 128), C4, CW]
   auto G = at::empty({C4 / 128, CW, CW}, wg.options());
   auto BWG = at::empty({std::max<int64_t>(1, CW / 128), C4, CW}, wg.options());
-  TORCH_CHECK(pdt_bn_alg_small_gemm(reinterpret_cast<const uint16_t*>(w.data_ptr()), coef.data_ptr<float>(),
+  const uint16_t* wtp = nullptr;
+  if (wt.has_value() && wt->defined()) {  // W^T [CW, C4]: the matrix-core form
+    check_cuda(*wt, "wt");
+    TORCH_CHECK(wt->scalar_type() == at::kBFloat16 && wt->is_contiguous() && wt->dim() == 2 && wt->size(0) == CW &&
+                    wt->size(1) == C4, "bn_alg_small_gemm: wt [CW, C4] bf16 contiguous");
+    wtp = reinterpret_cast<const uint16_t*>(wt->data_ptr());
+  }
+  TORCH_CHECK(pdt_bn_alg_small_gemm(reinterpret_cast<const uint16_t*>(w.data_ptr()), wtp, coef.data_ptr<float>(),
                                     wg.data_ptr<float>(), G.data_ptr<float>(), BWG.data_ptr<float>(), (int)C4, (int)CW,
                                     stream()) == 0,
               "pdt_bn_alg_small_gemm failed");
@@ -2375,7 +2382,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("out"), py::arg("bn_x") = py::none(), py::arg("bn_mask") = py::none(), py::arg("bn_mean") = py::none());
   m.def("bn_alg_assemble", &bn_alg_assemble);
   m.def("bn_alg_fix_s2", &bn_alg_fix_s2);
-  m.def("bn_alg_small_gemm", &bn_alg_small_gemm);
+  m.def("bn_alg_small_gemm", &bn_alg_small_gemm, py::arg("w"), py::arg("coef"), py::arg("wg"), py::arg("wt") = py::none());
   m.def("conv1x1_wgrad_tune", [](int target_wgs, int variant, int interleave) { pdt_conv1x1_wgrad_tune(target_wgs, variant, interleave); },
         py::arg("target_wgs"), py::arg("variant") = -2, py::arg("interleave") = -2);
   m.def("embedding_fwd", &embedding_fwd);

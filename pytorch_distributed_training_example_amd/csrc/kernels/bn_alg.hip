@@ -17,6 +17,8 @@
 // Not in the reference (LeNet has no BatchNorm, /root/reference/cnn.py:9-23).
 #include "../common.h"
 
+#include <stdlib.h>
+
 using namespace pdt;
 
 namespace {
@@ -171,6 +173,119 @@ __global__ __launch_bounds__(256) void bn_alg_small_gemm_kernel(const uint16_t* 
   }
 }
 
+// The same split-K partials on the matrix cores (v_mfma_f32_16x16x32_bf16) with every non-bf16 operand carried as
+// a bf16 hi + lo pair (two MFMAs; products exact, sums fp32: ~1e-5 relative, the VALU kernel above is the oracle in
+// tests/test_bwd_alg_gpu.py). No LDS: every fragment is 8 K-contiguous elements of one row —
+//   Gp: X = W^T rows i (the dgrad GEMM's prepared transpose), Y = (Bc W^T) rows j, K = c (slice of 128);
+//   Bp: X = W rows c, Y = Gram rows k (Gram is symmetric: its row k is its column k), K = j.
+// 256 threads = 4 waves, each a 32 x 32 quarter of the 64 x 64 tile (2 x 2 16 x 16 blocks). The VALU kernel ran
+// 17-44 us per launch at ResNet-50's shapes, latency-bound.
+typedef __bf16 bf16x8a __attribute__((ext_vector_type(8)));
+typedef float f4a __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void split8(const float (&v)[8], bf16x8a& hi, bf16x8a& lo) {
+  typedef unsigned u4 __attribute__((ext_vector_type(4)));
+  u4 h, l;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint16_t h0 = f2bf(v[2 * k]), h1 = f2bf(v[2 * k + 1]);
+    const uint16_t l0 = f2bf(v[2 * k] - bfv(h0)), l1 = f2bf(v[2 * k + 1] - bfv(h1));
+    h[k] = (uint32_t)h0 | ((uint32_t)h1 << 16);
+    l[k] = (uint32_t)l0 | ((uint32_t)l1 << 16);
+  }
+  hi = __builtin_bit_cast(bf16x8a, h);
+  lo = __builtin_bit_cast(bf16x8a, l);
+}
+
+__global__ __launch_bounds__(256) void bn_alg_small_mfma_kernel(const uint16_t* __restrict__ W,
+                                                                const uint16_t* __restrict__ Wt,
+                                                                const float* __restrict__ coef,
+                                                                const float* __restrict__ wg, float* __restrict__ Gp,
+                                                                float* __restrict__ Bp, int C4, int CW) {
+  const float* Bc = coef + C4;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int lr = lane & 15, lq = lane >> 4;
+  const int tcw = CW / 64, nG = tcw * tcw;
+  const int t = blockIdx.x, sl = blockIdx.y;
+  const bool isG = t < nG;
+  if (isG ? sl >= C4 / kSK : sl >= bwg_slices(CW)) return;
+  const int klen = isG ? kSK : bwg_len(CW);
+  const int k0 = sl * klen;
+  const float* Gram = wg + (int64_t)C4 * CW;
+  int i0, j0;
+  if (isG) { i0 = (t / tcw) * 64; j0 = (t % tcw) * 64; }
+  else { i0 = ((t - nG) / tcw) * 64; j0 = ((t - nG) % tcw) * 64; }  // (c rows, k cols)
+  i0 += 32 * (w >> 1);
+  j0 += 32 * (w & 1);
+  f4a acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = f4a{0.f, 0.f, 0.f, 0.f};
+  for (int kk = k0; kk < k0 + klen; kk += 32) {
+    const int kc = kk + 8 * lq;  // this lane's 8 K elements
+    bf16x8a x[2], yh[2], yl[2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      const int r = i0 + 16 * a + lr;
+      x[a] = *reinterpret_cast<const bf16x8a*>(isG ? Wt + (int64_t)r * C4 + kc : W + (int64_t)r * CW + kc);
+    }
+    float bsc[8];
+    if (isG) {
+      *reinterpret_cast<float4*>(bsc) = *reinterpret_cast<const float4*>(Bc + kc);
+      *reinterpret_cast<float4*>(bsc + 4) = *reinterpret_cast<const float4*>(Bc + kc + 4);
+    }
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int r = j0 + 16 * b + lr;
+      float v[8];
+      if (isG) {
+        typedef unsigned u4 __attribute__((ext_vector_type(4)));
+        const u4 q = *reinterpret_cast<const u4*>(Wt + (int64_t)r * C4 + kc);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          v[2 * k] = __uint_as_float(q[k] << 16) * bsc[2 * k];
+          v[2 * k + 1] = __uint_as_float(q[k] & 0xffff0000u) * bsc[2 * k + 1];
+        }
+      } else {
+        *reinterpret_cast<float4*>(v) = *reinterpret_cast<const float4*>(Gram + (int64_t)r * CW + kc);
+        *reinterpret_cast<float4*>(v + 4) = *reinterpret_cast<const float4*>(Gram + (int64_t)r * CW + kc + 4);
+      }
+      split8(v, yh[b], yl[b]);
+    }
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[a], yh[b], acc[a][b], 0, 0, 0);
+        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x[a], yl[b], acc[a][b], 0, 0, 0);
+      }
+  }
+  // lane's acc[r] = D[row = block row 4 lq + r][col = lr]
+  if (isG) {
+    float* o = Gp + (int64_t)sl * CW * CW;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[(int64_t)(i0 + 16 * a + 4 * lq + r) * CW + j0 + 16 * b + lr] = acc[a][b][r];
+  } else {
+    float* o = Bp + (int64_t)sl * C4 * CW;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = i0 + 16 * a + 4 * lq + r;
+        const float bcv = Bc[c];
+#pragma unroll
+        for (int b = 0; b < 2; ++b) o[(int64_t)c * CW + j0 + 16 * b + lr] = bcv * acc[a][b][r];
+      }
+  }
+}
+
+int g_small_mfma = -1;  // PDT_ALG_SMALL_MFMA (default 1), read once
+
 }  // namespace
 
 extern "C" {
@@ -185,13 +300,23 @@ int pdt_bn_alg_fix_s2(float* part, int T, const float* wg, const uint16_t* W, in
 
 // Gp [C4 / 128, CW, CW] and Bp [max(1, CW / 128), C4, CW] fp32 split-K slices (see bn_alg_small_gemm_kernel);
 // C4 % 128 == 0, CW == 64 or CW % 128 == 0.
-int pdt_bn_alg_small_gemm(const uint16_t* W, const float* coef, const float* wg, float* G, float* BWG, int C4, int CW,
-                          hipStream_t s) {
+// Wt (nullable): W^T [CW, C4] bf16 — with it the products run on the matrix cores (bn_alg_small_mfma_kernel,
+// PDT_ALG_SMALL_MFMA=0 keeps the fp32 VALU kernel).
+int pdt_bn_alg_small_gemm(const uint16_t* W, const uint16_t* Wt, const float* coef, const float* wg, float* G,
+                          float* BWG, int C4, int CW, hipStream_t s) {
   if (C4 % kSK || CW % 64 || (CW > 64 && CW % kSK)) return -1;
+  if (g_small_mfma < 0) {
+    const char* e = getenv("PDT_ALG_SMALL_MFMA");
+    g_small_mfma = (e && e[0] == '0') ? 0 : 1;
+  }
   const int tcw = CW / 64;
   const int sy = C4 / kSK > bwg_slices(CW) ? C4 / kSK : bwg_slices(CW);
-  hipLaunchKernelGGL(bn_alg_small_gemm_kernel, dim3(tcw * tcw + (C4 / 64) * tcw, sy), dim3(256), 0, s, W, coef, wg, G,
-                     BWG, C4, CW);
+  if (Wt && g_small_mfma)
+    hipLaunchKernelGGL(bn_alg_small_mfma_kernel, dim3(tcw * tcw + (C4 / 64) * tcw, sy), dim3(256), 0, s, W, Wt, coef,
+                       wg, G, BWG, C4, CW);
+  else
+    hipLaunchKernelGGL(bn_alg_small_gemm_kernel, dim3(tcw * tcw + (C4 / 64) * tcw, sy), dim3(256), 0, s, W, coef, wg,
+                       G, BWG, C4, CW);
   return 0;
 }
 

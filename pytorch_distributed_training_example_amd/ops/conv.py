@@ -605,7 +605,8 @@ def _bwd_alg(ctx, d, x, weight):
         return None
     w2 = weight.reshape(C4, CW).contiguous()
     coef = d.coef.contiguous()
-    G, bwg = native().bn_alg_small_gemm(w2, coef, wg)  # W^T diag(B) W [CW, CW], diag(B) W Gram [C4, CW] (fp32)
+    # W^T diag(B) W [CW, CW], diag(B) W Gram [C4, CW] (fp32), on the matrix cores from W^T (the dgrad's prepared copy)
+    G, bwg = native().bn_alg_small_gemm(w2, coef, wg, _wt_of(weight, w2))
     bcat, dw2 = native().bn_alg_assemble(w2, coef, d.mean.contiguous(), G, wg, bwg)
     gsrc = getattr(ctx, "gsrc", None)
     gs = gsrc if (gsrc is not None and gsrc.ready() and not linked) else None

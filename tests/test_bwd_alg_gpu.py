@@ -272,11 +272,14 @@ def test_small_gemm_and_fix_s2(C4, CW):
     M = 1500
     a, w, z, dy, bits, mean, coef = _deferred(M, C4, CW, 3 * C4)
     wg = _n().conv1x1_wgrad_seg(a, dy, a)
-    G, bwg = _n().bn_alg_small_gemm(w, coef, wg)
-    G, bwg = G.sum(0), bwg.sum(0)  # split-K slices
     wd, B = w.double(), coef[1].double()
-    torch.testing.assert_close(G.double(), wd.t() @ (B.unsqueeze(1) * wd), rtol=1e-4, atol=1e-5)
-    torch.testing.assert_close(bwg.double(), B.unsqueeze(1) * (wd @ wg[C4:C4 + CW].double()), rtol=1e-4, atol=1e-4)
+    # the fp32 VALU kernel and the matrix-core one (W^T given: bf16 hi + lo operand pairs)
+    for wt in (None, w.t().contiguous()):
+        G, bwg = _n().bn_alg_small_gemm(w, coef, wg, wt)
+        G, bwg = G.sum(0), bwg.sum(0)  # split-K slices
+        torch.testing.assert_close(G.double(), wd.t() @ (B.unsqueeze(1) * wd), rtol=1e-4, atol=1e-5)
+        torch.testing.assert_close(bwg.double(), B.unsqueeze(1) * (wd @ wg[C4:C4 + CW].double()), rtol=1e-4,
+                                   atol=1e-4)
     # a sum-only producer's partials: sums of g, centred sums of g (0 - mean) per 256-row tile
     T = (M + 255) // 256
     g = dy.float()

@@ -46,9 +46,11 @@ def main():
         bmean = torch.randn(CW, device="cuda")
         wg = C.conv1x1_wgrad_seg(x, g, x)
         t_wg = timeit(lambda: C.conv1x1_wgrad_seg(x, g, x))
-        t_sm = timeit(lambda: C.bn_alg_assemble(w, coef, mean, *C.bn_alg_small_gemm(w, coef, wg)[:1],
-                                                 wg, C.bn_alg_small_gemm(w, coef, wg)[1]))
-        G, B = C.bn_alg_small_gemm(w, coef, wg)
+        wt = w.t().contiguous()
+        t_sv = timeit(lambda: C.bn_alg_small_gemm(w, coef, wg))  # fp32 VALU
+        t_sm = timeit(lambda: C.bn_alg_small_gemm(w, coef, wg, wt))  # matrix cores (hi / lo bf16 pairs)
+        G, B = C.bn_alg_small_gemm(w, coef, wg, wt)
+        t_as = timeit(lambda: C.bn_alg_assemble(w, coef, mean, G, wg, B))
         bcat, _ = C.bn_alg_assemble(w, coef, mean, G, wg, B)
         out = torch.empty(M, CW, device="cuda", dtype=torch.bfloat16)
         t_gm = timeit(lambda: C.conv1x1_gemm_seg(g, x, 2, bcat, out, bn_x=xb, bn_mask=bmask, bn_mean=bmean))
@@ -57,7 +59,7 @@ def main():
         tf_wg = 2 * M * (C4 + CW + 128) * CW / (t_wg * 1e-6) / 1e12
         tf_gm = 2 * M * (C4 + 2 * CW + 32) * CW / (t_gm * 1e-6) / 1e12
         print(f"[{tag}] M={M:7d} {C4:4d}/{CW:3d}: wgrad_seg {t_wg:6.1f} us ({tf_wg:4.0f} TF, floor {f_wg:5.1f}) | "
-              f"small+assemble x2 {t_sm:5.1f} | gemm_seg {t_gm:6.1f} us ({tf_gm:4.0f} TF, floor {f_gm:5.1f})", flush=True)
+              f"small VALU {t_sv:5.1f} MFMA {t_sm:5.1f} assemble {t_as:5.1f} | gemm_seg {t_gm:6.1f} us ({tf_gm:4.0f} TF, floor {f_gm:5.1f})", flush=True)
 
 
 if __name__ == "__main__":
