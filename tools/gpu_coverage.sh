@@ -1,6 +1,6 @@
 #!/bin/bash
 # Kernel-name coverage gate: the GPU test tier under rocprofv3 --kernel-trace, then which kernels of the
-# committed steady-state ResNet-50 step window (profiles/r5/steady_resnet50_b1024_kernels.csv) no test
+# committed steady-state ResNet-50 step window (profiles/r6/steady_resnet50_b1024_final_kernels.csv) no test
 # launched (tools/kernel_coverage.py). Report -> gpurun_out/kernel_coverage_resnet50.md.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export HSA_ENABLE_IPC_MODE_LEGACY=0 TMPDIR=/tmp
@@ -21,9 +21,9 @@ with open("gpurun_out/cov_kernel_names.csv", "w", newline="") as f:
 print(len(rows), "distinct kernels launched by the GPU tests")
 PY
 # profiles/ is gpurun-ignored (does not travel to the box): the gate runs where the step window is
-if [ -f profiles/r5/steady_resnet50_b1024_kernels.csv ]; then
-  python3 tools/kernel_coverage.py gpurun_out/cov_kernel_names.csv profiles/r5/steady_resnet50_b1024_kernels.csv \
+if [ -f profiles/r6/steady_resnet50_b1024_final_kernels.csv ]; then
+  python3 tools/kernel_coverage.py gpurun_out/cov_kernel_names.csv profiles/r6/steady_resnet50_b1024_final_kernels.csv \
     --out gpurun_out/kernel_coverage_resnet50.md
 else
-  echo "step window not here: run  python3 tools/kernel_coverage.py gpurun_out/cov_kernel_names.csv profiles/r5/steady_resnet50_b1024_kernels.csv  locally"
+  echo "step window not here: run  python3 tools/kernel_coverage.py gpurun_out/cov_kernel_names.csv profiles/r6/steady_resnet50_b1024_final_kernels.csv  locally"
 fi
