@@ -50,6 +50,8 @@ PDT_Z3_VIRTUAL              0            (with PDT_BWD_ALG=2) a bottleneck conv3
                                          statistics-only GEMM, bn3's apply as the GEMM again (APPLY epilogue): 1 every
                                          block; 2 only where that APPLY GEMM runs anyway (conv3 input channels <=
                                          PDT_BN_APPLY_GEMM_K: the skipped store is then pure gain)
+PDT_ALG_GLO                 1            the ALG data gradient carries G = W^T diag(B) W as a bf16 hi + lo pair (a twice
+                                         in K); 0: hi only (K = C4 + CW + 32 instead of C4 + 2 CW + 32)
 PDT_BWD_ALG_MIN_M           50176        the ALG paths (conv3 and shortcut) only for convs with at least this many output
                                          pixels: their small per-block GEMMs cost ~30-60 us whatever the batch, more
                                          than the apply pass they remove on ResNet-50 layers 3-4 at 128 images/GPU
@@ -93,7 +95,7 @@ class _Switches:
                  "conv1x1_table", "conv1x1_dump", "conv1x1_s2", "conv3x3", "conv3x3_wgrad", "conv3x3_s2", "conv_stem",
                  "conv_bn_stats", "bn_bwd_stats", "res_masked", "stem_bwd_fused", "stem_bn_wgrad", "stem_bn_stats", "stem_pool_wgrad", "wgrad_splitk", "slice_sum",
                  "subsample_native", "linear_splitk", "fused_addln", "embedding_native", "linear_epilogue",
-                 "bwd_fused", "bwd_fused_shapes", "bwd_alg", "bwd_alg_min_m", "z3_virtual", "bwd_alg_first", "ds_alg", "bn2_defer", "bn_apply_gemm_k", "strided_bstats", "gap_native", "sub_out",
+                 "bwd_fused", "bwd_fused_shapes", "bwd_alg", "alg_glo", "bwd_alg_min_m", "z3_virtual", "bwd_alg_first", "ds_alg", "bn2_defer", "bn_apply_gemm_k", "strided_bstats", "gap_native", "sub_out",
                  "fp8_fused_gelu", "fp8_weight_multi", "fp8_cast_colsum", "fp8_ln", "wgrad_stream_m")
 
     def __init__(self):
@@ -144,6 +146,7 @@ class _Switches:
         # reduction (sum-only epilogue) and the ALG pass completes it (ops/batchnorm.py _BNTrainFn.backward)
         self.bwd_alg = int(e("PDT_BWD_ALG", "2"))
         self.bwd_alg_min_m = int(e("PDT_BWD_ALG_MIN_M", "50176"))
+        self.alg_glo = on("PDT_ALG_GLO")
         # bottleneck conv3 on the ALG backward: z (bn3's input) never written — statistics-only GEMM, bn3 applied by
         # the GEMM again (APPLY epilogue); recomputed only on a fallback (ops/conv.py materialize_virtual)
         self.z3_virtual = int(e("PDT_Z3_VIRTUAL", "0"))

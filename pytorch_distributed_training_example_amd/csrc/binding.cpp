@@ -149,7 +149,7 @@ int pdt_bn_alg_fix_s2(float* part, int T, const float* wg, const uint16_t* W, in
 int pdt_bn_alg_small_gemm(const uint16_t* W, const uint16_t* Wt, const float* coef, const float* wg, float* G,
                           float* BWG, int C4, int CW, hipStream_t s);
 int pdt_bn_alg_assemble(const uint16_t* W, const float* coef, const float* mean, const float* G, const float* wg,
-                        const float* BWG, uint16_t* bcat, uint16_t* dW, int C4, int CW, hipStream_t s);
+                        const float* BWG, uint16_t* bcat, uint16_t* dW, int C4, int CW, int rep, hipStream_t s);
 int pdt_conv1x1_wgrad(const uint16_t* x, const uint16_t* dy, uint16_t* dw, float* ws, int M, int Ci, int Co,
                       hipStream_t s);
 void pdt_conv1x1_wgrad_tune(int target_wgs, int variant, int interleave);
@@ -1203,7 +1203,7 @@ c10::optional<Tensor> conv1x1_gemm_seg(Tensor a1, Tensor a2, int64_t rep2, Tenso
 }
 
 // (bcat [CW, C4 + 2 CW + 32] bf16, dW [C4, CW] bf16) of the ALG backward (csrc/kernels/bn_alg.hip).
-std::vector<Tensor> bn_alg_assemble(Tensor w, Tensor coef, Tensor mean, Tensor G, Tensor wg, Tensor BWG) {
+std::vector<Tensor> bn_alg_assemble(Tensor w, Tensor coef, Tensor mean, Tensor G, Tensor wg, Tensor BWG, int64_t rep) {
   for (const Tensor* t : {&w, &coef, &mean, &G, &wg, &BWG}) {
     check_cuda(*t, "bn_alg_assemble operand");
     TORCH_CHECK(t->is_contiguous(), "bn_alg_assemble: contiguous operands");
@@ -1216,12 +1216,13 @@ std::vector<Tensor> bn_alg_assemble(Tensor w, Tensor coef, Tensor mean, Tensor G
                   wg.scalar_type() == at::kFloat &&
                   wg.dim() == 2 && wg.size(1) == CW && wg.size(0) > C4 + CW,
               "bn_alg_assemble: operand shapes");
-  auto bcat = at::empty({CW, C4 + 2 * CW + 32}, w.options());
+  TORCH_CHECK(rep == 1 || rep == 2, "bn_alg_assemble: rep 1 or 2");
+  auto bcat = at::empty({CW, C4 + rep * CW + 32}, w.options());
   auto dW = at::empty({C4, CW}, w.options());
   const int rc = pdt_bn_alg_assemble(reinterpret_cast<const uint16_t*>(w.data_ptr()), coef.data_ptr<float>(),
                                      mean.data_ptr<float>(), G.data_ptr<float>(), wg.data_ptr<float>(),
                                      BWG.data_ptr<float>(), reinterpret_cast<uint16_t*>(bcat.data_ptr()),
-                                     reinterpret_cast<uint16_t*>(dW.data_ptr()), (int)C4, (int)CW, stream());
+                                     reinterpret_cast<uint16_t*>(dW.data_ptr()), (int)C4, (int)CW, (int)rep, stream());
   TORCH_CHECK(rc == 0, "pdt_bn_alg_assemble failed: ", rc);
   return {bcat, dW};
 }
@@ -2380,7 +2381,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv1x1_wgrad_seg", &conv1x1_wgrad_seg);
   m.def("conv1x1_gemm_seg", &conv1x1_gemm_seg, py::arg("a1"), py::arg("a2"), py::arg("rep2"), py::arg("b"),
         py::arg("out"), py::arg("bn_x") = py::none(), py::arg("bn_mask") = py::none(), py::arg("bn_mean") = py::none());
-  m.def("bn_alg_assemble", &bn_alg_assemble);
+  m.def("bn_alg_assemble", &bn_alg_assemble, py::arg("w"), py::arg("coef"), py::arg("mean"), py::arg("G"), py::arg("wg"),
+        py::arg("BWG"), py::arg("rep") = 2);
   m.def("bn_alg_fix_s2", &bn_alg_fix_s2);
   m.def("bn_alg_small_gemm", &bn_alg_small_gemm, py::arg("w"), py::arg("coef"), py::arg("wg"), py::arg("wt") = py::none());
   m.def("conv1x1_wgrad_tune", [](int target_wgs, int variant, int interleave) { pdt_conv1x1_wgrad_tune(target_wgs, variant, interleave); },

@@ -35,10 +35,10 @@ __global__ __launch_bounds__(256) void bn_alg_assemble_kernel(const uint16_t* __
                                                               const float* __restrict__ mean, const float* __restrict__ G,
                                                               const float* __restrict__ wg, const float* __restrict__ BWG,
                                                               uint16_t* __restrict__ bcat, uint16_t* __restrict__ dW,
-                                                              int C4, int CW) {
+                                                              int C4, int CW, int rep) {
   __shared__ float red[4];
   const int tid = threadIdx.x;
-  const int Kt = C4 + 2 * CW + 32;
+  const int Kt = C4 + rep * CW + 32;
   const float* A = coef;
   const float* Bc = coef + C4;
   const float* D = coef + 2 * C4;
@@ -56,12 +56,12 @@ __global__ __launch_bounds__(256) void bn_alg_assemble_kernel(const uint16_t* __
       for (int sl = 0; sl < C4 / kSK; ++sl) gv += G[((int64_t)sl * CW + k) * CW + j];
       const uint16_t hi = f2bf(gv);
       row[C4 + j] = hi;
-      row[C4 + CW + j] = f2bf(gv - bfv(hi));
+      if (rep == 2) row[C4 + CW + j] = f2bf(gv - bfv(hi));
     }
     cs = block_sum(cs, red);
     if (tid < 32) {
       const uint16_t hi = f2bf(cs);
-      row[C4 + 2 * CW + tid] = tid == 0 ? hi : (tid == 1 ? f2bf(cs - bfv(hi)) : (uint16_t)0);
+      row[C4 + rep * CW + tid] = tid == 0 ? hi : (tid == 1 ? f2bf(cs - bfv(hi)) : (uint16_t)0);
     }
     return;
   }
@@ -322,12 +322,14 @@ int pdt_bn_alg_small_gemm(const uint16_t* W, const uint16_t* Wt, const float* co
 
 // bcat [CW, C4 + 2 CW + 32] bf16, dW [C4, CW] bf16; W [C4, CW] bf16 row-major; coef [3, C4] (A, B, D), mean [C4],
 // G [CW, CW], BWG [C4, CW] fp32; wg: pdt_conv1x1_wgrad_seg's output (rows 0..C4-1 = P, row C4 + CW = S).
+// rep = 2: G as a bf16 hi + lo pair (bcat [CW, C4 + 2 CW + 32], the data-gradient GEMM repeats a twice);
+// rep = 1: G's hi half only (bcat [CW, C4 + CW + 32]: PDT_ALG_GLO=0).
 int pdt_bn_alg_assemble(const uint16_t* W, const float* coef, const float* mean, const float* G, const float* wg,
-                        const float* BWG, uint16_t* bcat, uint16_t* dW, int C4, int CW, hipStream_t s) {
-  if (C4 < 1 || CW < 1) return -1;
+                        const float* BWG, uint16_t* bcat, uint16_t* dW, int C4, int CW, int rep, hipStream_t s) {
+  if (C4 < 1 || CW < 1 || rep < 1 || rep > 2) return -1;
   const int64_t nd = ((int64_t)C4 * CW + 255) / 256;
   hipLaunchKernelGGL(bn_alg_assemble_kernel, dim3((unsigned)(CW + nd)), dim3(256), 0, s, W, coef, mean, G, wg, BWG,
-                     bcat, dW, C4, CW);
+                     bcat, dW, C4, CW, rep);
   return 0;
 }
 

@@ -607,11 +607,12 @@ def _bwd_alg(ctx, d, x, weight):
     coef = d.coef.contiguous()
     # W^T diag(B) W [CW, CW], diag(B) W Gram [C4, CW] (fp32), on the matrix cores from W^T (the dgrad's prepared copy)
     G, bwg = native().bn_alg_small_gemm(w2, coef, wg, _wt_of(weight, w2))
-    bcat, dw2 = native().bn_alg_assemble(w2, coef, d.mean.contiguous(), G, wg, bwg)
+    rep = 2 if SW.alg_glo else 1  # G as a bf16 hi + lo pair (a repeated in K), or its hi half only
+    bcat, dw2 = native().bn_alg_assemble(w2, coef, d.mean.contiguous(), G, wg, bwg, rep)
     gsrc = getattr(ctx, "gsrc", None)
     gs = gsrc if (gsrc is not None and gsrc.ready() and not linked) else None
     dx = torch.empty_like(x, memory_format=torch.channels_last)
-    part = native().conv1x1_gemm_seg(g2, a2, 2, bcat, _nhwc2d(dx), bn_x=gs.x if gs else None,
+    part = native().conv1x1_gemm_seg(g2, a2, rep, bcat, _nhwc2d(dx), bn_x=gs.x if gs else None,
                                      bn_mask=gs.mask if gs else None, bn_mean=gs.mean if gs else None)
     if gs is not None and part is not None:
         gs.deposit(part, dx, masked=gs.mask is not None)
