@@ -122,10 +122,11 @@ def test_assemble_matches_torch(C4, CW):
     torch.testing.assert_close(dw.float(), want, rtol=1e-2, atol=1e-3)
 
 
+@pytest.mark.parametrize("bheavy", [False, True])
 @pytest.mark.parametrize("glo", ["1", "0"])
 @pytest.mark.parametrize("N,H,C4,CW", [(8, 14, 1024, 256), (16, 7, 2048, 512), (4, 28, 512, 128), (2, 56, 256, 64),
                                         (4, 28, 512, 256), (8, 14, 1024, 512), (16, 7, 2048, 1024)])
-def test_alg_backward_matches_materialised_bn_backward(switch, N, H, C4, CW, glo):
+def test_alg_backward_matches_materialised_bn_backward(switch, N, H, C4, CW, glo, bheavy):
     """_bwd_alg's (da, dW) against the fp32 math of the materialised path: dz = A g + B (z - mean) + D, then
     da = dz W and dW = dz^T a. The ALG path never forms dz; its error is bf16-level against fp32."""
     from pytorch_distributed_training_example_amd.ops import conv as C
@@ -133,6 +134,9 @@ def test_alg_backward_matches_materialised_bn_backward(switch, N, H, C4, CW, glo
     switch("PDT_ALG_GLO", glo)  # 0: G's bf16 hi half only in the data-gradient GEMM
     M = N * H * H
     a, w, z, dy, bits, mean, coef = _deferred(M, C4, CW, M + C4)
+    if bheavy:  # B (z - mean) as large as A g: the G term (hi half only at glo 0) carries half of dz
+        coef = coef.clone()
+        coef[1] = -coef[0] / z.float().std(0).clamp_min(1e-3)
 
     class Ctx:
         link = dre = gsrc = None
@@ -151,6 +155,14 @@ def test_alg_backward_matches_materialised_bn_backward(switch, N, H, C4, CW, glo
     e_da = float((got_da - ref_da).norm() / ref_da.norm())
     e_dw = float((dw.view(C4, CW).float() - ref_dw).norm() / ref_dw.norm())
     assert e_da < 1e-2 and e_dw < 1e-2, (e_da, e_dw)
+    # as accurate as the unfused chain, which rounds dz to bf16 before its GEMMs (the data gradient also rounded to
+    # bf16 at the end, as both paths store it). With G's hi half only (glo 0) and B (z - mean) as large as A g
+    # (bheavy), 1.36x the unfused chain's error was measured (2.7e-3 vs 2.0e-3, still the output's bf16 rounding
+    # level); in the ordinary case the two are equal to 3 digits
+    dzb = dz.bfloat16().float()
+    e_un = float(((dzb @ w.float()).bfloat16().float() - ref_da).norm() / ref_da.norm())
+    print(f"glo={glo} bheavy={bheavy} {C4}x{CW}: e_da {e_da:.2e} (unfused bf16 chain {e_un:.2e}) e_dw {e_dw:.2e}")
+    assert e_da <= (1.5 if (glo == "0" and bheavy) else 1.1) * e_un + 1e-4, (e_da, e_un)
 
 
 def _grads(seed=0, fp32=False):
