@@ -50,11 +50,12 @@ PDT_Z3_VIRTUAL              0            (with PDT_BWD_ALG=2) a bottleneck conv3
                                          statistics-only GEMM, bn3's apply as the GEMM again (APPLY epilogue): 1 every
                                          block; 2 only where that APPLY GEMM runs anyway (conv3 input channels <=
                                          PDT_BN_APPLY_GEMM_K: the skipped store is then pure gain)
-PDT_ALG_GLO                 0            1: the ALG data gradient carries G = W^T diag(B) W as a bf16 hi + lo pair (a
-                                         twice in K); 0: hi only (K = C4 + CW + 32 instead of C4 + 2 CW + 32): +1.0 %
-                                         (profiles/r6/ab_alg_glo.txt), as accurate as the unfused chain (which rounds
-                                         all of dz to bf16) except where B (z - mean) is as large as A g: 1.36x its
-                                         error there, still the bf16 output rounding level (tests/test_bwd_alg_gpu.py)
+PDT_ALG_GLO                 1            the ALG data gradient carries G = W^T diag(B) W as a bf16 hi + lo pair (a twice
+                                         in K). 0 (hi only, K = C4 + CW + 32) ran +1.0 % but is NOT kept: the dropped
+                                         lo half is a fixed matrix, so its error a (G - G_hi) is correlated with bn2's
+                                         input and biases bn2's gamma gradient (10.5 % vs 4.6 % from fp32 in
+                                         tests/test_conv1x1_ours_gpu.py::test_bottleneck_chain_takes_bn_backward_stats;
+                                         profiles/r6/ab_alg_glo.txt)
 PDT_BWD_ALG_MIN_M           50176        the ALG paths (conv3 and shortcut) only for convs with at least this many output
                                          pixels: their small per-block GEMMs cost ~30-60 us whatever the batch, more
                                          than the apply pass they remove on ResNet-50 layers 3-4 at 128 images/GPU
@@ -149,7 +150,7 @@ class _Switches:
         # reduction (sum-only epilogue) and the ALG pass completes it (ops/batchnorm.py _BNTrainFn.backward)
         self.bwd_alg = int(e("PDT_BWD_ALG", "2"))
         self.bwd_alg_min_m = int(e("PDT_BWD_ALG_MIN_M", "50176"))
-        self.alg_glo = on("PDT_ALG_GLO", "0")
+        self.alg_glo = on("PDT_ALG_GLO", "1")
         # bottleneck conv3 on the ALG backward: z (bn3's input) never written — statistics-only GEMM, bn3 applied by
         # the GEMM again (APPLY epilogue); recomputed only on a fallback (ops/conv.py materialize_virtual)
         self.z3_virtual = int(e("PDT_Z3_VIRTUAL", "0"))
