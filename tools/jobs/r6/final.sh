@@ -7,4 +7,4 @@ mkdir -p gpurun_out/r6
 bash tools/gpu_prof_calls.sh || exit 1
 bash tools/gpu_step_roofline.sh > gpurun_out/r6/final_roof.log 2>&1 || { echo roofline failed; exit 1; }
 tail -14 gpurun_out/r6/final_roof.log | head -3
-bash tools/jobs/r6/s.sh
+bash tools/gpu_strong128.sh && bash tools/jobs/r6/s.sh
