@@ -87,10 +87,10 @@ int pdt_attn_bwd(const uint16_t* dout, const int64_t* dos, const uint16_t* q, co
                  const float* lse, float* delta, uint16_t* dq, uint16_t* dk, uint16_t* dv, const int64_t* gs, int B,
                  int H, int T, int Dh, int causal, float scale, hipStream_t s);
 int64_t pdt_gelu_workspace_floats(int64_t N, int D);
-int pdt_bias_gelu_fwd(const void* x, int dtype, const float* bias, void* y, int64_t N, int D, int tanh_form,
-                      hipStream_t s);
-int pdt_bias_gelu_bwd(const void* dy, const void* x, int dtype, const float* bias, void* dx, float* dbias,
-                      int64_t N, int D, int tanh_form, float* ws, hipStream_t s);
+int pdt_bias_gelu_fwd(const void* x, int dtype, const void* bias, void* y, int64_t N, int D, int tanh_form,
+                      hipStream_t s, int bias_bf16);
+int pdt_bias_gelu_bwd(const void* dy, const void* x, int dtype, const void* bias, void* dx, void* dbias,
+                      int64_t N, int D, int tanh_form, float* ws, hipStream_t s, int bias_bf16);
 int pdt_bn_relu_maxpool_fwd_train(const uint16_t* x, const float* gamma, const float* beta, float* running_mean,
                                   float* running_var, float momentum, float eps, int N, int H, int W, int C,
                                   uint16_t* y, uint8_t* code, float* mean, float* invstd, float* ws,
@@ -1753,7 +1753,15 @@ Tensor bias_gelu_fwd(Tensor x, c10::optional<Tensor> bias, bool tanh_form) {
   TORCH_CHECK(x.is_contiguous(), "gelu: x must be contiguous");
   const int64_t D = x.size(-1), N = x.numel() / D;
   auto y = at::empty_like(x);
-  int rc = pdt_bias_gelu_fwd(x.data_ptr(), dcode(x), opt_fptr(bias), y.data_ptr(), N, (int)D, tanh_form, stream());
+  const bool hb = bias.has_value() && bias->defined();
+  const bool bb = hb && bias->scalar_type() == at::kBFloat16;  // a bf16 model's bias, read as is
+  if (hb) {
+    check_cuda(*bias, "bias");
+    TORCH_CHECK(bias->is_contiguous() && bias->numel() == D && (bb || bias->scalar_type() == at::kFloat),
+                "bias_gelu: bias [D] fp32 or bf16");
+  }
+  int rc = pdt_bias_gelu_fwd(x.data_ptr(), dcode(x), hb ? bias->data_ptr() : nullptr, y.data_ptr(), N, (int)D,
+                             tanh_form, stream(), bb ? 1 : 0);
   TORCH_CHECK(rc == 0, "pdt_bias_gelu_fwd failed");
   return y;
 }
@@ -1764,14 +1772,15 @@ std::vector<Tensor> bias_gelu_bwd(Tensor dy, Tensor x, c10::optional<Tensor> bia
   auto dx = at::empty_like(x);
   auto fopt = x.options().dtype(at::kFloat);
   const bool hb = bias.has_value() && bias->defined();
+  const bool bb = hb && bias->scalar_type() == at::kBFloat16;
   Tensor db, ws;
   if (hb) {
-    db = at::empty({D}, fopt);
+    db = at::empty({D}, bb ? x.options().dtype(at::kBFloat16) : fopt);  // the bias's own dtype
     ws = at::empty({pdt_gelu_workspace_floats(N, (int)D)}, fopt);
   }
-  int rc = pdt_bias_gelu_bwd(dy.data_ptr(), x.data_ptr(), dcode(x), opt_fptr(bias), dx.data_ptr(),
-                             hb ? db.data_ptr<float>() : nullptr, N, (int)D, tanh_form,
-                             hb ? ws.data_ptr<float>() : nullptr, stream());
+  int rc = pdt_bias_gelu_bwd(dy.data_ptr(), x.data_ptr(), dcode(x), hb ? bias->data_ptr() : nullptr, dx.data_ptr(),
+                             hb ? db.data_ptr() : nullptr, N, (int)D, tanh_form,
+                             hb ? ws.data_ptr<float>() : nullptr, stream(), bb ? 1 : 0);
   TORCH_CHECK(rc == 0, "pdt_bias_gelu_bwd failed");
   return {dx, db};
 }

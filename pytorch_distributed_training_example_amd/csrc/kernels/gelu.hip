@@ -58,11 +58,28 @@ template <> struct Vec8<float> {
 // ~2048 workgroups (8 waves/CU) keep enough loads in flight to stream at HBM rate; the
 // per-chunk partials (nchunk x D fp32) are reduced in a fixed order by colsum_finalize.
 constexpr int kStrip = 512;
+// 8 bias values at column c: fp32, or the bf16 parameter itself (bb: a bf16 model's bias needs no fp32 copy — the
+// cast and its backward were two aten kernels per MLP per step)
+__device__ __forceinline__ void ld_bias8(const void* bias, int bb, int c, float (&b)[8]) {
+  if (bb) {
+    const uint4 q = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(bias) + c);
+    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      b[2 * k] = __uint_as_float(w[k] << 16);
+      b[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+    }
+  } else {
+    Vec4<float>::ld(reinterpret_cast<const float*>(bias), c, *reinterpret_cast<float(*)[4]>(b));
+    Vec4<float>::ld(reinterpret_cast<const float*>(bias), c + 4, *reinterpret_cast<float(*)[4]>(b + 4));
+  }
+}
+
 template <typename T, bool GELU>
 __global__ __launch_bounds__(256) void strip_kernel(const T* __restrict__ dy, const T* __restrict__ x,
-                                                    const float* __restrict__ bias, T* __restrict__ dx,
+                                                    const void* __restrict__ bias, T* __restrict__ dx,
                                                     float* __restrict__ part, int64_t N, int D, int rows_per_chunk,
-                                                    int tanh_form) {
+                                                    int tanh_form, int bb) {
   __shared__ float red[4][kStrip + 4];
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int c = blockIdx.x * kStrip + lane * 8;
@@ -72,10 +89,7 @@ __global__ __launch_bounds__(256) void strip_kernel(const T* __restrict__ dy, co
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   float b[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (valid) {
-    if (GELU && bias) {
-      Vec4<float>::ld(bias, c, *reinterpret_cast<float(*)[4]>(b));
-      Vec4<float>::ld(bias, c + 4, *reinterpret_cast<float(*)[4]>(b + 4));
-    }
+    if (GELU && bias) ld_bias8(bias, bb, c, b);
     int64_t r = r0 + wv;
     for (; r + 4 < r1; r += 8) {  // two rows in flight
       float g0[8], g1[8];
@@ -128,19 +142,16 @@ __global__ __launch_bounds__(256) void strip_kernel(const T* __restrict__ dy, co
 // Forward over the same strip mapping (no per-element div/mod for the bias column, 16-byte
 // accesses, two rows in flight per wave).
 template <typename T>
-__global__ __launch_bounds__(256) void gelu_fwd_strip_kernel(const T* __restrict__ x, const float* __restrict__ bias,
+__global__ __launch_bounds__(256) void gelu_fwd_strip_kernel(const T* __restrict__ x, const void* __restrict__ bias,
                                                              T* __restrict__ y, int64_t N, int D, int rows_per_chunk,
-                                                             int tanh_form) {
+                                                             int tanh_form, int bb) {
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int c = blockIdx.x * kStrip + lane * 8;
   if (c >= D) return;
   const int64_t r0 = (int64_t)blockIdx.y * rows_per_chunk;
   const int64_t r1 = min(N, r0 + rows_per_chunk);
   float b[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  if (bias) {
-    Vec4<float>::ld(bias, c, *reinterpret_cast<float(*)[4]>(b));
-    Vec4<float>::ld(bias, c + 4, *reinterpret_cast<float(*)[4]>(b + 4));
-  }
+  if (bias) ld_bias8(bias, bb, c, b);
   int64_t r = r0 + wv;
   for (; r + 4 < r1; r += 8) {
     float v0[8], v1[8];
@@ -206,12 +217,12 @@ inline int strip_chunks(int64_t N, int D, int& rpc) {
 }
 
 template <typename T, bool GELU>
-void launch_strip(const T* dy, const T* x, const float* bias, T* dx, float* part, int64_t N, int D, int tanh_form,
-                  int& nchunk, hipStream_t s) {
+void launch_strip(const T* dy, const T* x, const void* bias, T* dx, float* part, int64_t N, int D, int tanh_form,
+                  int& nchunk, hipStream_t s, int bb = 0) {
   int rpc;
   nchunk = strip_chunks(N, D, rpc);
   const dim3 grid((D + kStrip - 1) / kStrip, nchunk);
-  hipLaunchKernelGGL((strip_kernel<T, GELU>), grid, dim3(256), 0, s, dy, x, bias, dx, part, N, D, rpc, tanh_form);
+  hipLaunchKernelGGL((strip_kernel<T, GELU>), grid, dim3(256), 0, s, dy, x, bias, dx, part, N, D, rpc, tanh_form, bb);
 }
 
 }  // namespace
@@ -223,8 +234,9 @@ int64_t pdt_gelu_workspace_floats(int64_t N, int D) {
   return (int64_t)strip_chunks(N, D, rpc) * D;
 }
 
-int pdt_bias_gelu_fwd(const void* x, int dtype, const float* bias, void* y, int64_t N, int D, int tanh_form,
-                      hipStream_t s) {
+// bias_bf16: bias is bf16 (the strip path, D % 8 == 0, only)
+int pdt_bias_gelu_fwd(const void* x, int dtype, const void* bias, void* y, int64_t N, int D, int tanh_form,
+                      hipStream_t s, int bias_bf16) {
   if (D % 8 == 0) {
     if (N == 0) return 0;
     int rpc;
@@ -232,39 +244,45 @@ int pdt_bias_gelu_fwd(const void* x, int dtype, const float* bias, void* y, int6
     const dim3 grid((D + kStrip - 1) / kStrip, nchunk);
     if (dtype == 0)
       hipLaunchKernelGGL(gelu_fwd_strip_kernel<float>, grid, dim3(256), 0, s, (const float*)x, bias, (float*)y, N, D,
-                         rpc, tanh_form);
+                         rpc, tanh_form, bias_bf16);
     else
       hipLaunchKernelGGL(gelu_fwd_strip_kernel<uint16_t>, grid, dim3(256), 0, s, (const uint16_t*)x, bias,
-                         (uint16_t*)y, N, D, rpc, tanh_form);
+                         (uint16_t*)y, N, D, rpc, tanh_form, bias_bf16);
     return 0;
   }
-  if (D % 4 != 0) return -1;
+  if (D % 4 != 0 || bias_bf16) return -1;
   const int64_t nvec = N * D / 4;
   if (nvec == 0) return 0;
   int64_t grid = (nvec + 255) / 256;
   if (grid > 2048) grid = 2048;
   if (dtype == 0)
-    hipLaunchKernelGGL(bias_gelu_fwd_kernel<float>, dim3(grid), dim3(256), 0, s, (const float*)x, bias, (float*)y,
-                       nvec, D, tanh_form);
+    hipLaunchKernelGGL(bias_gelu_fwd_kernel<float>, dim3(grid), dim3(256), 0, s, (const float*)x, (const float*)bias,
+                       (float*)y, nvec, D, tanh_form);
   else
-    hipLaunchKernelGGL(bias_gelu_fwd_kernel<uint16_t>, dim3(grid), dim3(256), 0, s, (const uint16_t*)x, bias,
-                       (uint16_t*)y, nvec, D, tanh_form);
+    hipLaunchKernelGGL(bias_gelu_fwd_kernel<uint16_t>, dim3(grid), dim3(256), 0, s, (const uint16_t*)x,
+                       (const float*)bias, (uint16_t*)y, nvec, D, tanh_form);
   return 0;
 }
 
-int pdt_bias_gelu_bwd(const void* dy, const void* x, int dtype, const float* bias, void* dx, float* dbias,
-                      int64_t N, int D, int tanh_form, float* ws, hipStream_t s) {
+// bias_bf16: bias is bf16 and dbias is written as bf16 too
+int pdt_bias_gelu_bwd(const void* dy, const void* x, int dtype, const void* bias, void* dx, void* dbias,
+                      int64_t N, int D, int tanh_form, float* ws, hipStream_t s, int bias_bf16) {
   if (D % 8 != 0) return -1;
   if (N == 0) return 0;
   float* part = dbias ? ws : nullptr;
   int nchunk;
   if (dtype == 0)
-    launch_strip<float, true>((const float*)dy, (const float*)x, bias, (float*)dx, part, N, D, tanh_form, nchunk, s);
+    launch_strip<float, true>((const float*)dy, (const float*)x, bias, (float*)dx, part, N, D, tanh_form, nchunk, s,
+                              bias_bf16);
   else
     launch_strip<uint16_t, true>((const uint16_t*)dy, (const uint16_t*)x, bias, (uint16_t*)dx, part, N, D,
-                                 tanh_form, nchunk, s);
-  if (dbias)
-    hipLaunchKernelGGL(colsum_finalize_kernel<float>, dim3((D + 15) / 16), dim3(256), 0, s, ws, nchunk, D, dbias);
+                                 tanh_form, nchunk, s, bias_bf16);
+  if (dbias && bias_bf16)
+    hipLaunchKernelGGL(colsum_finalize_kernel<uint16_t>, dim3((D + 15) / 16), dim3(256), 0, s, ws, nchunk, D,
+                       (uint16_t*)dbias);
+  else if (dbias)
+    hipLaunchKernelGGL(colsum_finalize_kernel<float>, dim3((D + 15) / 16), dim3(256), 0, s, ws, nchunk, D,
+                       (float*)dbias);
   return 0;
 }
 

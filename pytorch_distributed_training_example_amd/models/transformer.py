@@ -71,7 +71,7 @@ class MLP(nn.Module):
                 return linear(g, self.c_proj)
         h = linear(x, self.c_fc, bias=False)  # bias is fused into the GELU kernel
         b = self.c_fc.bias
-        h = bias_gelu(h, b.float() if b is not None and b.dtype != torch.float32 else b, self.approximate)
+        h = bias_gelu(h, b if b is None or b.dtype in (torch.float32, torch.bfloat16) else b.float(), self.approximate)
         return linear(h, self.c_proj)
 
 

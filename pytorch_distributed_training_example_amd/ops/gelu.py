@@ -26,8 +26,11 @@ class _BiasGeluFn(torch.autograd.Function):
 
 def bias_gelu(x: torch.Tensor, bias: Optional[torch.Tensor] = None, approximate: str = "none") -> torch.Tensor:
     tanh_form = approximate == "tanh"
+    if bias is not None and bias.dtype == torch.bfloat16 and (not bias.is_contiguous() or bias.data_ptr() % 16):
+        bias = bias.float()  # the kernel reads 8 bf16 bias values per 16-B load
     if (use_native(x) and x.dtype in (torch.float32, torch.bfloat16) and x.shape[-1] % 8 == 0
-            and (bias is None or bias.dtype == torch.float32)):
+            and (bias is None or bias.dtype == torch.float32 or (bias.dtype == torch.bfloat16 and bias.is_contiguous()))):
+        # (a bf16 bias is read as is and gets a bf16 gradient: no fp32 copy and no cast back)
         return _BiasGeluFn.apply(x.contiguous(), bias, tanh_form)
     if bias is not None:
         x = x + bias.to(x.dtype)

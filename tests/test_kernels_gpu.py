@@ -421,3 +421,26 @@ def test_subsample_gather_and_scatter_add(shape, s):
     exp[:, :, ::s, ::s] += t.float()
     native().subsample_scatter_add(t, full, s)
     torch.testing.assert_close(full.float(), exp, rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("approx", ["none", "tanh"])
+@pytest.mark.parametrize("n,d", [(67, 3072), (4099, 776), (3, 1024)])
+def test_bias_gelu_bf16_bias_matches_fp32_bias(approx, n, d):
+    """A bf16 bias (a bf16 model's parameter) is read as is: the same y and dx bit for bit as its fp32 copy, and its
+    gradient is the fp32 path's bias gradient rounded to bf16 (no aten cast kernels around the MLP)."""
+    from pytorch_distributed_training_example_amd.ops.gelu import bias_gelu
+    torch.manual_seed(1)
+    x = torch.randn(n, d, device=DEV).bfloat16()
+    b16 = torch.randn(d, device=DEV).bfloat16()
+    g = torch.randn(n, d, device=DEV).bfloat16()
+    xa = x.clone().requires_grad_(True)
+    ba = b16.clone().requires_grad_(True)
+    ya = bias_gelu(xa, ba, approx)
+    ya.backward(g)
+    xb = x.clone().requires_grad_(True)
+    bb = b16.float().requires_grad_(True)
+    yb = bias_gelu(xb, bb, approx)
+    yb.backward(g)
+    assert ba.grad.dtype == torch.bfloat16
+    assert torch.equal(ya, yb) and torch.equal(xa.grad, xb.grad)
+    assert torch.equal(ba.grad, bb.grad.bfloat16())
