@@ -6,8 +6,6 @@
 // fixed order) and reduced by a small finalize kernel. The same column-strip kernel without the
 // GELU part is the bias gradient of every Linear layer (pdt_colsum, ops/linear.py).
 #include "../common.h"
-
-#include <stdlib.h>
 #include "../gelu_math.h"
 
 using namespace pdt;
@@ -77,18 +75,11 @@ __device__ __forceinline__ void ld_bias8(const void* bias, int bb, int c, float 
   }
 }
 
-// One-launch column sums (out != null): the LAST block of each column strip to finish (release fences, a ticket on a
-// self-resetting per-strip counter, acquire fence — batchnorm.hip bn_tiles_fin_kernel's pattern) sums the strip's
-// nchunk partial rows in colsum_finalize_kernel's exact order (16 strided groups, then the groups in order), so the
-// result is bit-identical to the two-launch form; the ~5 us finalize launch per Linear backward is gone.
-__device__ unsigned g_strip_ctr[256];  // one per 512-column strip (D <= 131072), zero at load, self-resetting
-
 template <typename T, bool GELU>
 __global__ __launch_bounds__(256) void strip_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                     const void* __restrict__ bias, T* __restrict__ dx,
                                                     float* __restrict__ part, int64_t N, int D, int rows_per_chunk,
-                                                    int tanh_form, int bb, void* __restrict__ out = nullptr,
-                                                    int out_bf16 = 0) {
+                                                    int tanh_form, int bb) {
   __shared__ float red[4][kStrip + 4];
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int c = blockIdx.x * kStrip + lane * 8;
@@ -145,32 +136,6 @@ __global__ __launch_bounds__(256) void strip_kernel(const T* __restrict__ dy, co
   for (int q = threadIdx.x; q < kStrip; q += 256) {
     const int cc = blockIdx.x * kStrip + q;
     if (cc < D) part[(int64_t)blockIdx.y * D + cc] = (red[0][q] + red[1][q]) + (red[2][q] + red[3][q]);
-  }
-  if (!out) return;
-  __shared__ int last;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // this thread's partial stores, before the ticket
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned tk = __hip_atomic_fetch_add(&g_strip_ctr[blockIdx.x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = tk == gridDim.y - 1;
-  }
-  __syncthreads();
-  if (!last) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  if (threadIdx.x == 0) g_strip_ctr[blockIdx.x] = 0u;
-  const int nblk = (int)gridDim.y;
-  for (int q = threadIdx.x; q < kStrip; q += 256) {
-    const int cc = blockIdx.x * kStrip + q;
-    if (cc >= D) continue;
-    float s = 0.f;
-    for (int grp = 0; grp < 16; ++grp) {  // colsum_finalize_kernel's order
-      float a = 0.f;
-      for (int blk = grp; blk < nblk; blk += 16) a += __builtin_nontemporal_load(&part[(int64_t)blk * D + cc]);
-      s += a;
-    }
-    if (out_bf16) reinterpret_cast<uint16_t*>(out)[cc] = f2bf(s);
-    else reinterpret_cast<float*>(out)[cc] = s;
   }
 }
 
@@ -251,23 +216,13 @@ inline int strip_chunks(int64_t N, int D, int& rpc) {
   return (int)((N + rpc - 1) / rpc);
 }
 
-int g_colsum_one = -1;  // PDT_COLSUM_ONE_LAUNCH (default 1), read once
-inline bool colsum_one_launch() {
-  if (g_colsum_one < 0) {
-    const char* e = getenv("PDT_COLSUM_ONE_LAUNCH");
-    g_colsum_one = (e && e[0] == '0') ? 0 : 1;
-  }
-  return g_colsum_one == 1;
-}
-
 template <typename T, bool GELU>
 void launch_strip(const T* dy, const T* x, const void* bias, T* dx, float* part, int64_t N, int D, int tanh_form,
-                  int& nchunk, hipStream_t s, int bb = 0, void* out = nullptr, int out_bf16 = 0) {
+                  int& nchunk, hipStream_t s, int bb = 0) {
   int rpc;
   nchunk = strip_chunks(N, D, rpc);
   const dim3 grid((D + kStrip - 1) / kStrip, nchunk);
-  hipLaunchKernelGGL((strip_kernel<T, GELU>), grid, dim3(256), 0, s, dy, x, bias, dx, part, N, D, rpc, tanh_form, bb,
-                     out, out_bf16);
+  hipLaunchKernelGGL((strip_kernel<T, GELU>), grid, dim3(256), 0, s, dy, x, bias, dx, part, N, D, rpc, tanh_form, bb);
 }
 
 }  // namespace
@@ -316,18 +271,16 @@ int pdt_bias_gelu_bwd(const void* dy, const void* x, int dtype, const void* bias
   if (N == 0) return 0;
   float* part = dbias ? ws : nullptr;
   int nchunk;
-  const bool one = colsum_one_launch() && (D + kStrip - 1) / kStrip <= 256;
-  void* fin = one ? dbias : nullptr;  // (dbias null: no partials, nothing to finalize)
   if (dtype == 0)
     launch_strip<float, true>((const float*)dy, (const float*)x, bias, (float*)dx, part, N, D, tanh_form, nchunk, s,
-                              bias_bf16, fin, bias_bf16);
+                              bias_bf16);
   else
     launch_strip<uint16_t, true>((const uint16_t*)dy, (const uint16_t*)x, bias, (uint16_t*)dx, part, N, D,
-                                 tanh_form, nchunk, s, bias_bf16, fin, bias_bf16);
-  if (dbias && !one && bias_bf16)
+                                 tanh_form, nchunk, s, bias_bf16);
+  if (dbias && bias_bf16)
     hipLaunchKernelGGL(colsum_finalize_kernel<uint16_t>, dim3((D + 15) / 16), dim3(256), 0, s, ws, nchunk, D,
                        (uint16_t*)dbias);
-  else if (dbias && !one)
+  else if (dbias)
     hipLaunchKernelGGL(colsum_finalize_kernel<float>, dim3((D + 15) / 16), dim3(256), 0, s, ws, nchunk, D,
                        (float*)dbias);
   return 0;
@@ -349,14 +302,10 @@ int pdt_colsum(const void* x, int dtype, int64_t N, int D, void* out, int odtype
   if (D % 8 != 0) return -1;
   int nchunk = 1;
   if (N > 0) {
-    const bool one = colsum_one_launch() && (D + kStrip - 1) / kStrip <= 256;
-    void* fin = one ? out : nullptr;
     if (dtype == 0)
-      launch_strip<float, false>((const float*)x, nullptr, nullptr, nullptr, ws, N, D, 0, nchunk, s, 0, fin, odtype);
+      launch_strip<float, false>((const float*)x, nullptr, nullptr, nullptr, ws, N, D, 0, nchunk, s);
     else
-      launch_strip<uint16_t, false>((const uint16_t*)x, nullptr, nullptr, nullptr, ws, N, D, 0, nchunk, s, 0, fin,
-                                    odtype);
-    if (one) return 0;
+      launch_strip<uint16_t, false>((const uint16_t*)x, nullptr, nullptr, nullptr, ws, N, D, 0, nchunk, s);
   } else {
     nchunk = 0;
   }
