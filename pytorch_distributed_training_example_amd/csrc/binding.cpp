@@ -146,6 +146,8 @@ int pdt_conv1x1_gemm_seg(const uint16_t* a1, int k1, const uint16_t* a2, int k2,
                          uint16_t* y, int M, int N, const uint16_t* bn_x, const uint8_t* bn_mask, const float* bn_mean,
                          float* bn_part, hipStream_t s);
 int pdt_bn_alg_fix_s2(float* part, int T, const float* wg, const uint16_t* W, int C4, int CW, hipStream_t s);
+int pdt_bn_alg_ds_part(float* part, const float* s1, const float* mean, const float* wg, const uint16_t* W, int C4,
+                       int CW, hipStream_t s);
 int pdt_bn_alg_small_gemm(const uint16_t* W, const uint16_t* Wt, const float* coef, const float* wg, float* G,
                           float* BWG, int C4, int CW, hipStream_t s);
 int pdt_bn_alg_assemble(const uint16_t* W, const float* coef, const float* mean, const float* G, const float* wg,
@@ -1272,6 +1274,23 @@ void bn_alg_fix_s2(Tensor part, Tensor wg, Tensor w) {
               "pdt_bn_alg_fix_s2 failed");
 }
 
+// A downsample BatchNorm's backward partials [2, 1, C4] from s1 = sum(g), its mean and the ALG pass (bn_alg.hip).
+Tensor bn_alg_ds_part(Tensor s1, Tensor mean, Tensor wg, Tensor w) {
+  for (const Tensor* t : {&s1, &mean, &wg, &w}) check_cuda(*t, "bn_alg_ds_part operand");
+  TORCH_CHECK(w.dim() == 2 && w.scalar_type() == at::kBFloat16 && w.is_contiguous(), "bn_alg_ds_part: w [C4, CW] bf16");
+  const int64_t C4 = w.size(0), CW = w.size(1);
+  TORCH_CHECK(s1.scalar_type() == at::kFloat && s1.is_contiguous() && s1.numel() == C4 && mean.scalar_type() == at::kFloat &&
+                  mean.is_contiguous() && mean.numel() == C4 && wg.scalar_type() == at::kFloat && wg.is_contiguous() &&
+                  wg.dim() == 2 && wg.size(1) == CW && wg.size(0) >= C4,
+              "bn_alg_ds_part: s1 / mean [C4] fp32, wg [>= C4, CW] fp32");
+  auto part = at::empty({2, 1, C4}, s1.options());
+  TORCH_CHECK(pdt_bn_alg_ds_part(part.data_ptr<float>(), s1.data_ptr<float>(), mean.data_ptr<float>(),
+                                 wg.data_ptr<float>(), reinterpret_cast<const uint16_t*>(w.data_ptr()), (int)C4, (int)CW,
+                                 stream()) == 0,
+              "pdt_bn_alg_ds_part failed");
+  return part;
+}
+
 // BN training forward with the statistics taken from conv1x1_gemm's per-tile partials.
 std::vector<Tensor> bn_fwd_train_tiles(Tensor x, Tensor part, c10::optional<Tensor> res, c10::optional<Tensor> weight,
                                        c10::optional<Tensor> bias, c10::optional<Tensor> running_mean,
@@ -2393,6 +2412,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_alg_assemble", &bn_alg_assemble, py::arg("w"), py::arg("coef"), py::arg("mean"), py::arg("G"), py::arg("wg"),
         py::arg("BWG"), py::arg("rep") = 2);
   m.def("bn_alg_fix_s2", &bn_alg_fix_s2);
+  m.def("bn_alg_ds_part", &bn_alg_ds_part);
   m.def("bn_alg_small_gemm", &bn_alg_small_gemm, py::arg("w"), py::arg("coef"), py::arg("wg"), py::arg("wt") = py::none());
   m.def("conv1x1_wgrad_tune", [](int target_wgs, int variant, int interleave) { pdt_conv1x1_wgrad_tune(target_wgs, variant, interleave); },
         py::arg("target_wgs"), py::arg("variant") = -2, py::arg("interleave") = -2);

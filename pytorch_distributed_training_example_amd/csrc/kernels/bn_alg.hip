@@ -91,6 +91,26 @@ __global__ __launch_bounds__(256) void bn_alg_fix_s2_kernel(float* __restrict__ 
   if (lane == 0) part[(int64_t)T * C4 + c] += s;  // part[1][0][c]
 }
 
+// A downsample shortcut BatchNorm's backward partials in one "tile" (ops/batchnorm.py _alg_ds_prelude): part[0][0] =
+// s1 = sum(g) (bn3's bias gradient: the same g), part[1][0] = -mean s1 + rowsum(P * W) — the same fp32 operations as
+// building -(mean * s1) and then bn_alg_fix_s2_kernel's add (one launch instead of four).
+__global__ __launch_bounds__(256) void bn_alg_ds_part_kernel(float* __restrict__ part, const float* __restrict__ s1,
+                                                             const float* __restrict__ mean, const float* __restrict__ wg,
+                                                             const uint16_t* __restrict__ W, int C4, int CW) {
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (c >= C4) return;
+  float s = 0.f;
+  for (int k = lane; k < CW; k += 64) s += wg[(int64_t)c * CW + k] * bfv(W[(int64_t)c * CW + k]);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
+  if (lane == 0) {
+    const float v = s1[c];
+    part[c] = v;
+    part[C4 + c] = -(mean[c] * v) + s;
+  }
+}
+
 // The two small fp32 products of the ALG backward in one launch, as split-K partials (64 x 64 output tiles,
 // 256 threads x 4 x 4, K slices of 128 rows: 8 steps of 16 with the next step's operands loaded into registers
 // before the current step's FMAs — a serial K loop of C4 / 16 latency-bound steps ran 110-200 us):
@@ -295,6 +315,14 @@ extern "C" {
 int pdt_bn_alg_fix_s2(float* part, int T, const float* wg, const uint16_t* W, int C4, int CW, hipStream_t s) {
   if (T < 1 || C4 < 1 || CW < 1) return -1;
   hipLaunchKernelGGL(bn_alg_fix_s2_kernel, dim3((C4 + 3) / 4), dim3(256), 0, s, part, T, wg, W, C4, CW);
+  return 0;
+}
+
+// part [2, 1, C4] fp32 of a downsample BatchNorm on the ALG backward (see bn_alg_ds_part_kernel).
+int pdt_bn_alg_ds_part(float* part, const float* s1, const float* mean, const float* wg, const uint16_t* W, int C4,
+                       int CW, hipStream_t s) {
+  if (C4 < 1 || CW < 1) return -1;
+  hipLaunchKernelGGL(bn_alg_ds_part_kernel, dim3((C4 + 3) / 4), dim3(256), 0, s, part, s1, mean, wg, W, C4, CW);
   return 0;
 }
 

@@ -379,9 +379,8 @@ def _alg_ds_prelude(ctx, g, x, weight, mean, invstd, need_w):
     wg = native().conv1x1_wgrad_seg(_nhwc2d(a), _nhwc2d(dy), _nhwc2d(a))
     if wg is None:
         return None
-    s1 = g.s1.float()
-    part = torch.stack((s1, -(mean * s1))).view(2, 1, C4)  # one "tile": sum(g), then -mean sum(g)
-    native().bn_alg_fix_s2(part, wg, w.reshape(C4, CW).contiguous())  # + rowsum(P * W)
+    # one "tile": sum(g), then -mean sum(g) + rowsum(P * W)
+    part = native().bn_alg_ds_part(g.s1.float().contiguous(), mean.contiguous(), wg, w.reshape(C4, CW).contiguous())
     coef, dg, db = native().bn_bwd_coef(dy, x, part, None, weight, mean, invstd, False, need_w)
     return coef, dg, db, wg
 

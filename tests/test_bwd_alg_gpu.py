@@ -341,3 +341,17 @@ def test_unwritten_conv3_output_matches_written(switch, gap_native, mode):
     gb = _grads(seed=5)
     bad = [k for k in gb if not torch.equal(ga[k], gb[k])]
     assert not bad, bad[:8]
+
+
+@pytest.mark.parametrize("C4,CW", [(256, 64), (512, 256), (1024, 512)])
+def test_ds_part_matches_stack_and_fix_s2(C4, CW):
+    """bn_alg_ds_part (the shortcut BN's one-tile partials in one launch) equals building [s1, -mean s1] and adding
+    rowsum(P * W) with bn_alg_fix_s2, bit for bit."""
+    M = 900
+    a, w, z, dy, bits, mean, coef = _deferred(M, C4, CW, C4 + 7)
+    wg = _n().conv1x1_wgrad_seg(a, dy, a)
+    s1 = dy.float().sum(0)
+    want = torch.stack((s1, -(mean * s1))).view(2, 1, C4).contiguous()
+    _n().bn_alg_fix_s2(want, wg, w)
+    got = _n().bn_alg_ds_part(s1, mean.contiguous(), wg, w)
+    assert got.shape == (2, 1, C4) and torch.equal(got, want)
