@@ -107,7 +107,7 @@ __global__ __launch_bounds__(256) void bn_alg_ds_part_kernel(float* __restrict__
   if (lane == 0) {
     const float v = s1[c];
     part[c] = v;
-    part[C4 + c] = -(mean[c] * v) + s;
+    part[C4 + c] = -__fmul_rn(mean[c], v) + s;  // (no fma contraction: the two-step form rounds the product)
   }
 }
 
