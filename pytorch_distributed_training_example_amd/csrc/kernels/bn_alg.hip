@@ -105,9 +105,11 @@ __global__ __launch_bounds__(256) void bn_alg_ds_part_kernel(float* __restrict__
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
   if (lane == 0) {
+#pragma clang fp contract(off)
     const float v = s1[c];
     part[c] = v;
-    part[C4 + c] = -__fmul_rn(mean[c], v) + s;  // (no fma contraction: the two-step form rounds the product)
+    const float mv = mean[c] * v;  // rounded on its own (no fma): the two-step form's product
+    part[C4 + c] = -mv + s;
   }
 }
 
