@@ -31,10 +31,12 @@ def timeit(fn, it=10):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=1024)
+    ap.add_argument("--ds", action="store_true", help="the downsample shortcuts' shapes (Co = 2 Ci) instead of conv3's")
     a = ap.parse_args()
     C = native()
     tag = f"tile={os.environ.get('PDT_SEG_TILE', '0')} wvar={os.environ.get('PDT_WGRAD_SEG_VARIANT', '-1')}"
-    for H, C4, CW in ((28, 512, 128), (14, 1024, 256), (7, 2048, 512)):
+    shapes = ((56, 256, 64), (28, 512, 256), (14, 1024, 512)) if a.ds else ((28, 512, 128), (14, 1024, 256), (7, 2048, 512))
+    for H, C4, CW in shapes:
         M = a.batch * H * H
         g = torch.randn(M, C4, device="cuda").bfloat16()
         x = torch.randn(M, CW, device="cuda").relu().bfloat16()
