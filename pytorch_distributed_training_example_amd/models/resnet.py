@@ -23,6 +23,7 @@ from ..ops.batchnorm import BatchNorm2d, BNGradLink, ResidualGradLink
 from ..config import SW
 from ..ops._native import disabled as native_disabled
 from ..ops.conv import Conv1x1, SplitConv2d, linked_conv, prepare_weights, stem_block
+from ..ops.linear import Linear
 
 
 def conv3x3(inp: int, out: int, stride: int = 1, groups: int = 1, dilation: int = 1) -> nn.Conv2d:
@@ -212,7 +213,9 @@ class ResNet(nn.Module):
         self.layer3 = self._make_layer(block, 256, layers[2], stride=2)
         self.layer4 = self._make_layer(block, 512, layers[3], stride=2)
         self.avgpool = nn.AdaptiveAvgPool2d((1, 1))
-        self.fc = nn.Linear(512 * block.expansion, num_classes)
+        # ours: the head's bias gradient on the colsum kernel (ops/linear.py Linear: aten's reduction
+        # there replays wrong under hipGraph capture at 1024/GPU)
+        self.fc = (Linear if norm == "pdt" else nn.Linear)(512 * block.expansion, num_classes)
         for m in self.modules():
             if isinstance(m, nn.Conv2d):
                 nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")

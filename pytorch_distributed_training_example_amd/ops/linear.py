@@ -176,6 +176,17 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] =
     return F.linear(x, weight, bias)
 
 
+class Linear(torch.nn.Linear):
+    """``nn.Linear`` (same parameters and state-dict keys) on :func:`linear`: dbias on the ``colsum``
+    kernel. Besides speed this keeps the step hipGraph-safe: aten's ``sum(0)`` over a [1024, 1000]
+    gradient takes its multi-block path, whose staging workspace does not survive a captured
+    backward — a replay after any later allocation returns a wrong bias gradient (the ResNet head at
+    1024/GPU trained to NaN; tools/diag_graph_colsum_bwd.py, profiles/r6/graph_colsum_bwd.txt)."""
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return linear(x, self.weight, self.bias)
+
+
 class _LinearGeluFn(torch.autograd.Function):
     """g = gelu(x·Wᵀ + b) with the GEMM, bias and GELU in one kernel (EPI_GELU); h = x·Wᵀ is kept for
     the backward, which is the column-strip GELU-backward + bias-gradient kernel and two GEMMs."""

@@ -136,3 +136,40 @@ def test_side_stream_wgrad_matches_in_stream(arch):
         assert torch.equal(l2, le), (tag, l2, le)
         bad = [i for i, (a, b) in enumerate(zip(g2, ge)) if not torch.equal(a, b)]
         assert not bad, f"{tag}: {len(bad)} of {len(ge)} gradients differ (first: {bad[:5]})"
+
+
+def test_linear_bias_grad_replays_after_allocations():
+    """The ResNet head (ops/linear.py Linear) at 1024 rows: a captured backward replayed after later
+    allocations gives the eager bias gradient. aten's sum(0) there does not (profiles/r6/graph_colsum_bwd.txt),
+    which trained the graphed 1024/GPU bench to NaN."""
+    from pytorch_distributed_training_example_amd.ops.linear import Linear
+    torch.manual_seed(0)
+    lin = Linear(2048, 1000).cuda().bfloat16()
+    x = torch.randn(1024, 2048, device="cuda").bfloat16()
+    t = torch.randn(1024, 1000, device="cuda").bfloat16()
+
+    def fb():
+        for p in lin.parameters():
+            if p.grad is not None:
+                p.grad.zero_()
+        (lin(x).float() * t).sum().backward()
+
+    for _ in range(3):
+        fb()
+    torch.cuda.synchronize()
+    ref = lin.bias.grad.float().clone()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            fb()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, capture_error_mode="thread_local"):
+        fb()
+    for _ in range(3):
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(lin.bias.grad.float(), ref)
+        junk = [torch.randn(1024, 1000, device="cuda") for _ in range(8)]  # reuse of freed non-graph memory
+        del junk
