@@ -70,11 +70,11 @@ def parse(argv=None):
     ap.add_argument("--image-size", type=int, default=224)
     ap.add_argument("--seq-len", type=int, default=1024)
     ap.add_argument("--impl", default="ours", choices=["ours", "torch_ddp", "reference"])
-    ap.add_argument("--graph", type=int, default=-1,
-                    help="hipGraph-capture the step (ours; excludes the capture-unsafe MIOpen solvers). -1 (default): "
-                         "on for the ResNet models at world size 1 (the whole step — forward, backward, the bucket "
-                         "all-reduce, the optimizer — replayed: +1.9 %% at 1024/GPU, profiles/r6/ab_graph_b1024.txt), "
-                         "off at N > 1, where the eager step is the path multi-rank runs have exercised")
+    ap.add_argument("--graph", type=int, default=0,
+                    help="1: hipGraph-capture the step (ours: forward, backward, the bucket all-reduce and the optimizer "
+                         "replayed; excludes the capture-unsafe MIOpen solvers). Default 0: at 1024/GPU the captured "
+                         "step measures the same as eager (15,455-15,468 vs 15,467-15,487 img/s on one box, "
+                         "profiles/r6/ab_graph_b1024.txt); it pays at small per-GPU batches (launch-bound)")
     ap.add_argument("--bucket-cap-mb", default="auto",
                     help="MiB cap per gradient bucket, or 'auto' (ours): the comm-model plan whose last-filling "
                          "bucket is <= 2 MiB (parallel/buckets.py plan_auto); torch_ddp uses 25 for 'auto'")
@@ -365,10 +365,6 @@ def main(argv=None):
     rc = self_launch(args, argv)
     if rc is not None:
         return rc
-    if args.graph < 0:  # auto (see --graph): the captured step for the ResNet models on one rank
-        world = int(os.environ.get("WORLD_SIZE", "1"))
-        args.graph = int(world == 1 and args.impl == "ours" and args.model.startswith("resnet")
-                         and torch.cuda.device_count() > 0)
     if os.environ.get("PDT_STACK_DUMP"):  # periodic Python stacks: where a slow warm-up spends time
         import faulthandler
         faulthandler.dump_traceback_later(float(os.environ["PDT_STACK_DUMP"]), repeat=True)

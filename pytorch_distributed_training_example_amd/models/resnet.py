@@ -215,7 +215,9 @@ class ResNet(nn.Module):
         self.avgpool = nn.AdaptiveAvgPool2d((1, 1))
         # ours: the head's bias gradient on the colsum kernel (ops/linear.py Linear: aten's reduction
         # there replays wrong under hipGraph capture at 1024/GPU)
-        self.fc = (Linear if norm == "pdt" else nn.Linear)(512 * block.expansion, num_classes)
+        # (PDT_HEAD_COLSUM=0: aten's nn.Linear, for A/B)
+        head = Linear if norm == "pdt" and os.environ.get("PDT_HEAD_COLSUM", "1") != "0" else nn.Linear
+        self.fc = head(512 * block.expansion, num_classes)
         for m in self.modules():
             if isinstance(m, nn.Conv2d):
                 nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
