@@ -173,3 +173,46 @@ def test_linear_bias_grad_replays_after_allocations():
         assert torch.equal(lin.bias.grad.float(), ref)
         junk = [torch.randn(1024, 1000, device="cuda") for _ in range(8)]  # reuse of freed non-graph memory
         del junk
+
+
+def test_resnet50_b1024_captured_backward_replays_bitwise():
+    """The bench's shape (ResNet-50, 1024/GPU): a captured forward+backward replayed after unrelated
+    allocations gives every gradient bit-identical to eager (tools/diag_graph_model.py, whole model)."""
+    from pytorch_distributed_training_example_amd.engine.graph import make_miopen_capture_safe
+    from pytorch_distributed_training_example_amd.ops.cross_entropy import cross_entropy
+    make_miopen_capture_safe()
+    torch.manual_seed(0)
+    from pytorch_distributed_training_example_amd.models import get_model
+    from pytorch_distributed_training_example_amd.models.precision import to_bf16_mixed
+    m = to_bf16_mixed(get_model("resnet50").cuda().to(memory_format=torch.channels_last))
+    x = torch.randn(1024, 3, 224, 224, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 1000, (1024,), device="cuda")
+    params = [p for p in m.parameters() if p.requires_grad]
+
+    def fb():
+        for p in params:
+            if p.grad is not None:
+                p.grad.zero_()
+        cross_entropy(m(x), y, label_smoothing=0.1).backward()
+
+    for _ in range(2):
+        fb()
+    torch.cuda.synchronize()
+    ref = [p.grad.clone() for p in params]
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            fb()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, capture_error_mode="thread_local"):
+        fb()
+    for _ in range(2):
+        g.replay()
+        torch.cuda.synchronize()
+        bad = [i for i, (p, r) in enumerate(zip(params, ref)) if not torch.equal(p.grad, r)]
+        assert not bad, f"{len(bad)} gradients differ after replay, first: param {bad[0]}"
+        junk = [torch.randn(1 << 20, device="cuda") for _ in range(64)]
+        del junk
+    del g
