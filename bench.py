@@ -28,6 +28,7 @@ from __future__ import annotations
 import argparse
 import contextlib
 import json
+import math
 import os
 import sys
 import time
@@ -376,6 +377,12 @@ def main(argv=None):
             with open(args.json_out, "w") as f:
                 json.dump(result, f)
     launcher.destroy()
+    if not math.isfinite(result["config"]["final_loss"]):
+        # a step that trains to NaN/inf measures nothing (round 6: a graphed run looked faster while
+        # its loss was NaN, profiles/r6/graph_colsum_bwd.txt) — fail the run instead of reporting it
+        print(f"[bench] final loss is {result['config']['final_loss']}: the timed steps are not valid",
+              file=sys.stderr, flush=True)
+        return 3
     return 0
 
 
