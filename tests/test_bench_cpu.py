@@ -67,3 +67,15 @@ def test_bench_global_batch_strong_scaling():
     r = _run(2, 0, extra=("--global-batch", "5"), self_launch=True)
     assert r["scaling"] == "strong" and r["config"]["per_gpu_batch"] == 3
     assert r["config"]["global_batch"] == 6 and r["n_gpus"] == 2
+
+
+def test_bench_fails_on_non_finite_loss():
+    """A run whose loss ends NaN is not a measurement: bench.py exits 3 (round 6: a graphed run looked
+    faster while training to NaN, profiles/r6/graph_colsum_bwd.txt)."""
+    env = dict(os.environ, OMP_NUM_THREADS="2", MASTER_ADDR="127.0.0.1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_PORT"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, "bench.py", "--model", "lenet", "--steps", "3", "--warmup", "2",
+                        "--lr", "1e30"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=400)
+    assert p.returncode == 3, (p.returncode, p.stderr[-2000:])
+    assert "not valid" in p.stderr
